@@ -1,0 +1,291 @@
+"""crane_dyn — Python binding of the MI355X Dynamic-plugin engine (libcrane_dyn.so).
+
+A thin ctypes layer over include/crane_dyn.h.  There is no CPU fallback: if the
+HIP library is missing, importing this module raises.  Build it with
+``make -C crane-scheduler_amd/csrc`` (or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libcrane_dyn.so")
+
+CRANE_TS_INVALID = -(2**63)
+CRANE_POD_DAEMONSET = 1
+_ERRS = {-1: "invalid argument", -2: "HIP error", -3: "bad state", -4: "policy parse error", -5: "I/O error"}
+
+
+class CraneError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{_ERRS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class _CPolicy(C.Structure):
+    _fields_ = [
+        ("n_sync", C.c_int32), ("sync_name", C.POINTER(C.c_char_p)), ("sync_period_ns", C.POINTER(C.c_int64)),
+        ("n_pred", C.c_int32), ("pred_name", C.POINTER(C.c_char_p)), ("pred_limit", C.POINTER(C.c_double)),
+        ("n_prio", C.c_int32), ("prio_name", C.POINTER(C.c_char_p)), ("prio_weight", C.POINTER(C.c_double)),
+        ("n_hot", C.c_int32), ("hot_tr_ns", C.POINTER(C.c_int64)), ("hot_count", C.POINTER(C.c_int64)),
+    ]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"crane_dyn: HIP library not built ({LIB_PATH}); run make -C crane-scheduler_amd/csrc")
+    L = C.CDLL(LIB_PATH)
+    P, vp = C.POINTER, C.c_void_p
+    sig = {
+        "crane_policy_load_file": (C.c_int, [C.c_char_p, P(vp), C.c_char_p, C.c_size_t]),
+        "crane_policy_load_bytes": (C.c_int, [C.c_char_p, C.c_size_t, P(vp), C.c_char_p, C.c_size_t]),
+        "crane_policy_view": (P(_CPolicy), [vp]),
+        "crane_policy_free": (None, [vp]),
+        "crane_tz_offset": (C.c_int, [C.c_char_p, P(C.c_int64)]),
+        "crane_parse_annotation": (None, [C.c_char_p, C.c_size_t, C.c_int64, P(C.c_double), P(C.c_int64)]),
+        "crane_dyn_create": (C.c_int, [P(_CPolicy), C.c_int32, P(vp)]),
+        "crane_dyn_destroy": (C.c_int, [vp]),
+        "crane_dyn_last_error": (C.c_char_p, [vp]),
+        "crane_dyn_num_metrics": (C.c_int32, [vp]),
+        "crane_dyn_metric_name": (C.c_char_p, [vp, C.c_int32]),
+        "crane_dyn_upload_nodes": (C.c_int, [vp, C.c_int64, C.c_int64, vp, vp, vp, vp]),
+        "crane_dyn_upload_bindings": (C.c_int, [vp, C.c_int64, vp, vp]),
+        "crane_dyn_refresh_hot_values": (C.c_int, [vp, C.c_int64, C.c_int64]),
+        "crane_dyn_eval": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, vp]),
+        "crane_dyn_eval_keys_async": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp]),
+        "crane_dyn_refresh_hot_values_async": (C.c_int, [vp, C.c_int64, C.c_int64, vp]),
+        "crane_dyn_node_pass_async": (C.c_int, [vp, vp]),
+        "crane_dyn_greedy": (C.c_int, [vp, C.c_int64, C.c_int64, vp, vp]),
+        "crane_dyn_key_node": (C.c_int64, [C.c_int64, P(C.c_int64)]),
+        "crane_dyn_version": (C.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+lib = _load()
+
+# The symbols include/crane_dyn.h declares (checked by tests/test_abi.py).
+ABI_SYMBOLS = (
+    "crane_policy_load_file", "crane_policy_load_bytes", "crane_policy_view", "crane_policy_free",
+    "crane_tz_offset", "crane_parse_annotation", "crane_dyn_create", "crane_dyn_destroy", "crane_dyn_last_error",
+    "crane_dyn_num_metrics", "crane_dyn_metric_name", "crane_dyn_upload_nodes", "crane_dyn_upload_bindings",
+    "crane_dyn_refresh_hot_values", "crane_dyn_eval", "crane_dyn_eval_keys_async",
+    "crane_dyn_refresh_hot_values_async", "crane_dyn_node_pass_async", "crane_dyn_greedy", "crane_dyn_key_node",
+    "crane_dyn_version",
+)
+
+
+def _ptr(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+# ------------------------------------------------------------------ policy
+class Policy:
+    """A DynamicSchedulerPolicy spec (pkg/plugins/apis/policy/types.go:14-39).
+
+    Build from a dict {"syncPolicy": [(name, period_ns)], "predicate": [(name, maxLimitPecent)],
+    "priority": [(name, weight)], "hotValue": [(timeRange_ns, count)]}, or decode a policy
+    file with :meth:`load_file` / :meth:`load_bytes` (strict, like LoadPolicyFromFile).
+    """
+
+    def __init__(self, spec):
+        self.spec = {k: [tuple(x) for x in spec.get(k, [])] for k in ("syncPolicy", "predicate", "priority", "hotValue")}
+        sp, pr, pi, hv = (self.spec[k] for k in ("syncPolicy", "predicate", "priority", "hotValue"))
+        n = lambda xs: max(1, len(xs))  # noqa: E731
+        self._keep = [
+            (C.c_char_p * n(sp))(*[a.encode() for a, _ in sp]), (C.c_int64 * n(sp))(*[int(b) for _, b in sp]),
+            (C.c_char_p * n(pr))(*[a.encode() for a, _ in pr]), (C.c_double * n(pr))(*[float(b) for _, b in pr]),
+            (C.c_char_p * n(pi))(*[a.encode() for a, _ in pi]), (C.c_double * n(pi))(*[float(b) for _, b in pi]),
+            (C.c_int64 * n(hv))(*[int(a) for a, _ in hv]), (C.c_int64 * n(hv))(*[int(b) for _, b in hv]),
+        ]
+        k = self._keep
+        cp = C.POINTER
+        self.c = _CPolicy(len(sp), C.cast(k[0], cp(C.c_char_p)), C.cast(k[1], cp(C.c_int64)),
+                          len(pr), C.cast(k[2], cp(C.c_char_p)), C.cast(k[3], cp(C.c_double)),
+                          len(pi), C.cast(k[4], cp(C.c_char_p)), C.cast(k[5], cp(C.c_double)),
+                          len(hv), C.cast(k[6], cp(C.c_int64)), C.cast(k[7], cp(C.c_int64)))
+
+    @staticmethod
+    def _from_doc(doc):
+        v = lib.crane_policy_view(doc).contents
+        spec = {
+            "syncPolicy": [(v.sync_name[i].decode(), v.sync_period_ns[i]) for i in range(v.n_sync)],
+            "predicate": [(v.pred_name[i].decode(), v.pred_limit[i]) for i in range(v.n_pred)],
+            "priority": [(v.prio_name[i].decode(), v.prio_weight[i]) for i in range(v.n_prio)],
+            "hotValue": [(v.hot_tr_ns[i], v.hot_count[i]) for i in range(v.n_hot)],
+        }
+        lib.crane_policy_free(doc)
+        return Policy(spec)
+
+    @staticmethod
+    def load_bytes(data: bytes | str) -> "Policy":
+        if isinstance(data, str):
+            data = data.encode()
+        doc, err = C.c_void_p(), C.create_string_buffer(512)
+        rc = lib.crane_policy_load_bytes(data, len(data), C.byref(doc), err, len(err))
+        if rc:
+            raise CraneError(rc, err.value.decode())
+        return Policy._from_doc(doc)
+
+    @staticmethod
+    def load_file(path: str) -> "Policy":
+        doc, err = C.c_void_p(), C.create_string_buffer(512)
+        rc = lib.crane_policy_load_file(path.encode(), C.byref(doc), err, len(err))
+        if rc:
+            raise CraneError(rc, err.value.decode())
+        return Policy._from_doc(doc)
+
+
+def default_policy_spec():
+    """deploy/manifests/dynamic/policy.yaml:1-52 (the README default policy)."""
+    m = 60 * 10**9
+    return {
+        "syncPolicy": [("cpu_usage_avg_5m", 3 * m), ("cpu_usage_max_avg_1h", 15 * m), ("cpu_usage_max_avg_1d", 180 * m),
+                       ("mem_usage_avg_5m", 3 * m), ("mem_usage_max_avg_1h", 15 * m), ("mem_usage_max_avg_1d", 180 * m)],
+        "predicate": [("cpu_usage_avg_5m", 0.65), ("cpu_usage_max_avg_1h", 0.75), ("mem_usage_avg_5m", 0.65),
+                      ("mem_usage_max_avg_1h", 0.75)],
+        "priority": [("cpu_usage_avg_5m", 0.2), ("cpu_usage_max_avg_1h", 0.3), ("cpu_usage_max_avg_1d", 0.5),
+                     ("mem_usage_avg_5m", 0.2), ("mem_usage_max_avg_1h", 0.3), ("mem_usage_max_avg_1d", 0.5)],
+        "hotValue": [(5 * m, 5), (1 * m, 2)],
+    }
+
+
+# ------------------------------------------------------------- annotations
+def tz_offset(name: str | None = None) -> int:
+    off = C.c_int64()
+    rc = lib.crane_tz_offset(None if name is None else name.encode(), C.byref(off))
+    if rc:
+        raise CraneError(rc, f"unsupported time zone {name!r}")
+    return off.value
+
+
+def parse_annotation(s: str, tz_offset_s: int):
+    """(value, ts_ns) of one annotation value; ts_ns == CRANE_TS_INVALID when unusable."""
+    b = s.encode()
+    v, t = C.c_double(), C.c_int64()
+    lib.crane_parse_annotation(b, len(b), tz_offset_s, C.byref(v), C.byref(t))
+    return v.value, t.value
+
+
+def parse_nodes(metric_names, nodes, tz_offset_s):
+    """Node annotation dicts -> SoA (val[M][N], ts[M][N], hv[N], hv_ts[N])."""
+    M, N = len(metric_names), len(nodes)
+    val = np.zeros((M, N))
+    ts = np.full((M, N), CRANE_TS_INVALID, np.int64)
+    hv = np.zeros(N)
+    hv_ts = np.full(N, CRANE_TS_INVALID, np.int64)
+    for n, a in enumerate(nodes):
+        for m, name in enumerate(metric_names):
+            s = a.get(name)
+            if s is not None:
+                val[m, n], ts[m, n] = parse_annotation(s, tz_offset_s)
+        s = a.get("node_hot_value")
+        if s is not None:
+            hv[n], hv_ts[n] = parse_annotation(s, tz_offset_s)
+    return val, ts, hv, hv_ts
+
+
+def key_node(key: int):
+    s = C.c_int64()
+    n = lib.crane_dyn_key_node(int(key), C.byref(s))
+    return n, s.value
+
+
+# ------------------------------------------------------------------ engine
+class Engine:
+    """One engine = one node shard on one HIP device (crane_dyn_create)."""
+
+    def __init__(self, policy: Policy, device: int = 0):
+        self.policy = policy
+        h = C.c_void_p()
+        rc = lib.crane_dyn_create(C.byref(policy.c), device, C.byref(h))
+        self.h = h
+        if rc:
+            msg = lib.crane_dyn_last_error(h).decode() if h.value else ""
+            self.close()
+            raise CraneError(rc, msg)
+        self.metric_names = [lib.crane_dyn_metric_name(h, i).decode() for i in range(lib.crane_dyn_num_metrics(h))]
+        self.n_nodes = 0
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib.crane_dyn_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc):
+        if rc:
+            raise CraneError(rc, lib.crane_dyn_last_error(self.h).decode())
+
+    def upload_nodes(self, val, ts, hv=None, hv_ts=None, node_offset=0):
+        val = np.ascontiguousarray(val, np.float64)
+        ts = np.ascontiguousarray(ts, np.int64)
+        M = len(self.metric_names)
+        N = val.shape[1] if val.ndim == 2 else (len(hv) if hv is not None else 0)
+        if val.shape != (M, N) or ts.shape != (M, N):
+            raise ValueError(f"val/ts must be [{M}][N] in engine metric order {self.metric_names}")
+        if hv is not None:
+            hv = np.ascontiguousarray(hv, np.float64)
+            hv_ts = np.ascontiguousarray(hv_ts, np.int64)
+            if hv.shape != (N,) or hv_ts.shape != (N,):
+                raise ValueError("hv/hv_ts must have one entry per node")
+        self._check(lib.crane_dyn_upload_nodes(self.h, N, node_offset, _ptr(val), _ptr(ts), _ptr(hv), _ptr(hv_ts)))
+        self.n_nodes = N
+
+    def upload_bindings(self, node, ts_s):
+        node = np.ascontiguousarray(node, np.int32)
+        ts_s = np.ascontiguousarray(ts_s, np.int64)
+        if node.shape != ts_s.shape:
+            raise ValueError("node/ts_s length mismatch")
+        self._check(lib.crane_dyn_upload_bindings(self.h, len(node), _ptr(node), _ptr(ts_s)))
+
+    def refresh_hot_values(self, now_ns, hv_ts_ns=None):
+        self._check(lib.crane_dyn_refresh_hot_values(self.h, int(now_ns), int(now_ns if hv_ts_ns is None else hv_ts_ns)))
+
+    def eval(self, now_ns, pod_flags=None, matrix=False):
+        """Returns (first_fail[P,N] or None, score[P,N] or None, chosen[P], chosen_score[P])."""
+        now = np.ascontiguousarray(now_ns, np.int64).reshape(-1)
+        P, N = len(now), self.n_nodes
+        fl = None if pod_flags is None else np.ascontiguousarray(pod_flags, np.uint8).reshape(-1)
+        if fl is not None and len(fl) != P:
+            raise ValueError("pod_flags length mismatch")
+        ff = np.empty((P, N), np.int8) if matrix else None
+        sc = np.empty((P, N), np.int64) if matrix else None
+        ch = np.empty(P, np.int64)
+        cs = np.empty(P, np.int64)
+        self._check(lib.crane_dyn_eval(self.h, P, _ptr(now), _ptr(fl), _ptr(ff), _ptr(sc), _ptr(ch), _ptr(cs)))
+        return ff, sc, ch, cs
+
+    # device-resident pipeline (torch tensors on the engine's device)
+    def refresh_hot_values_async(self, now_ns, hv_ts_ns, stream=None):
+        self._check(lib.crane_dyn_refresh_hot_values_async(self.h, int(now_ns), int(hv_ts_ns), stream))
+
+    def node_pass_async(self, stream=None):
+        self._check(lib.crane_dyn_node_pass_async(self.h, stream))
+
+    def eval_keys_async(self, d_now, d_flags, d_keys, stream=None):
+        """d_now int64[P], d_flags uint8[P] or None, d_keys int64[P]: torch CUDA tensors."""
+        P = d_now.numel()
+        assert d_keys.numel() == P and d_now.dtype.itemsize == 8 and d_keys.dtype.itemsize == 8
+        self._check(lib.crane_dyn_eval_keys_async(self.h, P, C.c_void_p(d_now.data_ptr()),
+                                                  None if d_flags is None else C.c_void_p(d_flags.data_ptr()),
+                                                  C.c_void_p(d_keys.data_ptr()), stream))
+
+    def greedy(self, n_pods, now_ns, pod_flags=None):
+        fl = None if pod_flags is None else np.ascontiguousarray(pod_flags, np.uint8)
+        ch = np.empty(n_pods, np.int64)
+        self._check(lib.crane_dyn_greedy(self.h, n_pods, int(now_ns), _ptr(fl), _ptr(ch)))
+        return ch
+
+
+def version() -> str:
+    return lib.crane_dyn_version().decode()

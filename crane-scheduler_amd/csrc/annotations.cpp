@@ -1,0 +1,263 @@
+// annotations.cpp — host parser for Dynamic-plugin node annotations.
+//
+// Value format written by the controller: "<float>,<local time>" —
+// strconv.FormatFloat(v,'f',5,64) / strconv.Itoa for the value
+// (pkg/controller/prometheus/prometheus.go:124, pkg/controller/annotator/node.go:120)
+// and utils.GetLocalTime() = time.Now().In($TZ).Format("2006-01-02T15:04:05Z")
+// (pkg/utils/utils.go:11,26-45) for the stamp, joined in node.go:142.
+//
+// The plugin re-reads it with strings.Split(v, ",") (exactly 2 parts),
+// time.ParseInLocation(TimeFormat, parts[1], GetLocation()) and
+// strconv.ParseFloat(parts[0], 64) (pkg/plugins/dynamic/stats.go:51-76).  This
+// file restates those Go stdlib (go1.17) semantics so that parsing once per
+// sync gives exactly the value/timestamp the reference would see per call.
+#include <cerrno>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../../include/crane_dyn.h"
+
+namespace {
+
+inline int lower(int c) { return c | 0x20; }
+inline bool digit(char c) { return c >= '0' && c <= '9'; }
+
+int prefix_fold(const char* s, size_t n, const char* w) {
+    size_t i = 0;
+    while (i < n && w[i] && lower((unsigned char)s[i]) == w[i]) ++i;
+    return (int)i;
+}
+
+// strconv.underscoreOK
+bool underscores_ok(const char* s, size_t n) {
+    char saw = '^';
+    size_t i = 0;
+    if (n >= 1 && (s[0] == '+' || s[0] == '-')) { ++s; --n; }
+    bool hex = false;
+    if (n >= 2 && s[0] == '0' && (lower(s[1]) == 'b' || lower(s[1]) == 'o' || lower(s[1]) == 'x')) {
+        i = 2;
+        saw = '0';
+        hex = lower(s[1]) == 'x';
+    }
+    for (; i < n; ++i) {
+        const char c = s[i];
+        if (digit(c) || (hex && lower(c) >= 'a' && lower(c) <= 'f')) { saw = '0'; continue; }
+        if (c == '_') {
+            if (saw != '0') return false;
+            saw = '_';
+            continue;
+        }
+        if (saw == '_') return false;
+        saw = '!';
+    }
+    return saw != '_';
+}
+
+}  // namespace
+
+// strconv.ParseFloat(s, 64): true + value on success; false on ErrSyntax or
+// ErrRange (the plugin treats both as an error, stats.go:66-69).
+bool crane_go_parse_float(const char* s, size_t n, double* out) {
+    *out = 0;
+    if (n == 0) return false;
+    // special(): [+-]inf|infinity (case-folded), unsigned nan
+    {
+        size_t off = 0;
+        double sign = 1;
+        if (s[0] == '+' || s[0] == '-') { sign = s[0] == '-' ? -1 : 1; off = 1; }
+        if (off < n && lower((unsigned char)s[off]) == 'i') {
+            int k = prefix_fold(s + off, n - off, "infinity");
+            if (k > 3 && k < 8) k = 3;
+            if (k == 3 || k == 8) {
+                if (off + (size_t)k != n) return false;
+                *out = sign * INFINITY;
+                return true;
+            }
+        } else if (off == 0 && lower((unsigned char)s[0]) == 'n') {
+            if (prefix_fold(s, n, "nan") == 3) {
+                if (n != 3) return false;
+                *out = NAN;
+                return true;
+            }
+        }
+    }
+    // readFloat() grammar
+    size_t i = 0;
+    bool unders = false, dot = false, digits = false;
+    if (s[i] == '+' || s[i] == '-') ++i;
+    bool hex = false;
+    if (i + 2 < n && s[i] == '0' && lower(s[i + 1]) == 'x') { hex = true; i += 2; }
+    for (; i < n; ++i) {
+        const char c = s[i];
+        if (c == '_') { unders = true; continue; }
+        if (c == '.') {
+            if (dot) break;
+            dot = true;
+            continue;
+        }
+        if (digit(c) || (hex && lower(c) >= 'a' && lower(c) <= 'f')) { digits = true; continue; }
+        break;
+    }
+    if (!digits) return false;
+    const char expc = hex ? 'p' : 'e';
+    if (i < n && lower(s[i]) == expc) {
+        ++i;
+        if (i >= n) return false;
+        if (s[i] == '+' || s[i] == '-') ++i;
+        if (i >= n || !digit(s[i])) return false;
+        for (; i < n && (digit(s[i]) || s[i] == '_'); ++i)
+            if (s[i] == '_') unders = true;
+    } else if (hex) {
+        return false;  // a hex mantissa needs a 'p' exponent
+    }
+    if (unders && !underscores_ok(s, i)) return false;
+    if (i != n) return false;  // trailing bytes
+    std::string buf;
+    buf.reserve(n);
+    for (size_t j = 0; j < n; ++j)
+        if (s[j] != '_') buf.push_back(s[j]);
+    char* end = nullptr;
+    errno = 0;
+    const double v = std::strtod(buf.c_str(), &end);  // correctly rounded, like Go
+    if (end != buf.c_str() + buf.size()) return false;
+    if (std::isinf(v)) return false;  // ErrRange on overflow; underflow is not an error in Go
+    *out = v;
+    return true;
+}
+
+namespace {
+
+bool getnum(const char* s, size_t n, size_t* p, bool fixed, int* out) {
+    const size_t i = *p;
+    if (i >= n || !digit(s[i])) return false;
+    if (i + 1 >= n || !digit(s[i + 1])) {
+        if (fixed) return false;
+        *out = s[i] - '0';
+        *p = i + 1;
+        return true;
+    }
+    *out = (s[i] - '0') * 10 + (s[i + 1] - '0');
+    *p = i + 2;
+    return true;
+}
+
+bool lit(const char* s, size_t n, size_t* p, char c) {
+    if (*p >= n || s[*p] != c) return false;
+    ++*p;
+    return true;
+}
+
+int month_days(int m, int64_t y) {
+    static const int d[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    const bool leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+    return (m == 2 && leap) ? 29 : d[m - 1];
+}
+
+// days since 1970-01-01 in the proleptic Gregorian calendar (Go's time.Date)
+int64_t civil_days(int64_t y, int m, int d) {
+    y -= m <= 2;
+    const int64_t era = (y >= 0 ? y : y - 399) / 400;
+    const int64_t yoe = y - era * 400;
+    const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+    const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+    return era * 146097 + doe - 719468;
+}
+
+}  // namespace
+
+// time.ParseInLocation("2006-01-02T15:04:05Z", s, loc) with loc a fixed
+// offset.  Layout chunks (go1.17 time/format.go): stdLongYear '-' stdZeroMonth
+// '-' stdZeroDay 'T' stdHour ':' stdZeroMinute ':' stdZeroSecond [.frac] 'Z'.
+bool crane_go_parse_time(const char* s, size_t n, int64_t tz_offset_s, int64_t* out_ns) {
+    if (n < 4 || !digit(s[0])) return false;
+    int year = 0;
+    for (int k = 0; k < 4; ++k) {
+        if (!digit(s[k])) return false;
+        year = year * 10 + (s[k] - '0');
+    }
+    size_t p = 4;
+    int mon, day, hour, min, sec;
+    if (!lit(s, n, &p, '-') || !getnum(s, n, &p, true, &mon) || mon < 1 || mon > 12) return false;
+    if (!lit(s, n, &p, '-') || !getnum(s, n, &p, true, &day)) return false;
+    if (!lit(s, n, &p, 'T') || !getnum(s, n, &p, false, &hour) || hour > 23) return false;
+    if (!lit(s, n, &p, ':') || !getnum(s, n, &p, true, &min) || min > 59) return false;
+    if (!lit(s, n, &p, ':') || !getnum(s, n, &p, true, &sec) || sec > 59) return false;
+    int64_t nsec = 0;
+    if (n - p >= 2 && s[p] == '.' && digit(s[p + 1])) {  // fraction not in the layout: accepted
+        size_t q = p + 2;
+        while (q < n && digit(s[q])) ++q;
+        const size_t nb = q - p, lim = nb > 10 ? 10 : nb;
+        int64_t v = 0;
+        for (size_t k = p + 1; k < p + lim; ++k) v = v * 10 + (s[k] - '0');
+        for (size_t k = lim; k < 10; ++k) v *= 10;
+        nsec = v;
+        p = q;
+    }
+    if (!lit(s, n, &p, 'Z') || p != n) return false;
+    if (day < 1 || day > month_days(mon, year)) return false;
+    const __int128 t =
+        ((__int128)civil_days(year, mon, day) * 86400 + hour * 3600 + min * 60 + sec - tz_offset_s) * 1000000000 + nsec;
+    // int64 ns spans 1678..2262; saturate so "long ago" stays stale and "far
+    // future" stays fresh, as with Go's wider Time.
+    const __int128 lo = (__int128)INT64_MIN / 2, hi = (__int128)INT64_MAX / 2;
+    *out_ns = (int64_t)(t < lo ? lo : (t > hi ? hi : t));
+    return true;
+}
+
+extern "C" {
+
+// utils.GetLocation (utils.go:35-45): $TZ, default Asia/Shanghai.  No tzdata
+// is read: supported zones are those with a fixed offset for every
+// timestamp a live controller can write (Asia/Shanghai = UTC+8 since 1991).
+int crane_tz_offset(const char* tz_name, int64_t* offset_s) {
+    std::string z = tz_name && *tz_name ? tz_name : "";
+    if (z.empty()) {
+        const char* env = std::getenv("TZ");
+        z = env && *env ? env : "Asia/Shanghai";
+    }
+    static const struct { const char* name; int64_t off; } zones[] = {
+        {"UTC", 0}, {"Etc/UTC", 0}, {"GMT", 0}, {"Etc/GMT", 0}, {"Universal", 0}, {"Zulu", 0},
+        {"Asia/Shanghai", 8 * 3600}, {"Asia/Chongqing", 8 * 3600}, {"Asia/Harbin", 8 * 3600}, {"PRC", 8 * 3600},
+        {"Asia/Singapore", 8 * 3600}, {"Asia/Taipei", 8 * 3600}, {"Asia/Tokyo", 9 * 3600}, {"Asia/Seoul", 9 * 3600},
+        {"Asia/Kolkata", 19800},
+    };
+    for (const auto& e : zones)
+        if (z == e.name) {
+            *offset_s = e.off;
+            return CRANE_OK;
+        }
+    if (z.rfind("Etc/GMT", 0) == 0 && z.size() > 7) {  // POSIX-inverted sign: Etc/GMT-8 = UTC+8
+        char* end = nullptr;
+        const long h = std::strtol(z.c_str() + 7, &end, 10);
+        if (end && *end == 0 && h >= -14 && h <= 12) {
+            *offset_s = -h * 3600;
+            return CRANE_OK;
+        }
+    }
+    return CRANE_E_INVALID;
+}
+
+void crane_parse_annotation(const char* s, size_t n, int64_t tz_offset_s, double* value, int64_t* ts_ns) {
+    *value = 0;
+    *ts_ns = CRANE_TS_INVALID;
+    size_t comma = (size_t)-1, ncomma = 0;
+    for (size_t i = 0; i < n; ++i)
+        if (s[i] == ',') {
+            if (!ncomma) comma = i;
+            ++ncomma;
+        }
+    if (ncomma != 1) return;  // strings.Split must give exactly two parts
+    const char* t = s + comma + 1;
+    const size_t tn = n - comma - 1;
+    int64_t ts;
+    if (tn < 5 || !crane_go_parse_time(t, tn, tz_offset_s, &ts)) return;  // stats.go:31-40
+    double v;
+    if (!crane_go_parse_float(s, comma, &v)) return;
+    *value = v;
+    *ts_ns = ts;
+}
+
+}  // extern "C"

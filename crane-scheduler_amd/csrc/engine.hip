@@ -1,0 +1,431 @@
+// engine.hip — the C ABI of include/crane_dyn.h: engine lifecycle, device
+// buffers, policy flattening and the pipeline K2 -> K1 -> K3 on a HIP stream.
+//
+// Reference mapping (/root/reference):
+//   crane_dyn_create      NewDynamicScheduler      pkg/plugins/dynamic/plugins.go:105-120
+//   policy flattening     getActiveDuration        pkg/plugins/dynamic/stats.go:140-150
+//   crane_dyn_eval        Filter + Score + select  plugins.go:39-98 (+ upstream selectHost)
+//   refresh_hot_values    GetLastNodeBindingCount  pkg/controller/annotator/binding.go:81-97
+//                         annotateNodeHotValue     pkg/controller/annotator/node.go:113-121
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/crane_dyn.h"
+#include "dyn_types.hpp"
+#include "kernels.hpp"
+
+using namespace crane;
+
+namespace {
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;  // elements
+    hipError_t reserve(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            p = nullptr;
+            n = 0;
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T));
+        if (e == hipSuccess) n = std::max<size_t>(want, 1);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+// Go: int64(d.Seconds()) (binding.go:85)
+int64_t go_seconds_trunc(int64_t d) {
+    const int64_t sec = d / 1000000000LL, nsec = d % 1000000000LL;
+    const double s = (double)sec + (double)nsec / 1e9;
+    if (!(s >= -9223372036854775808.0 && s < 9223372036854775808.0)) return INT64_MIN;
+    return (int64_t)s;
+}
+
+int64_t floor_div(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+    return q;
+}
+
+}  // namespace
+
+struct crane_dyn {
+    std::mutex mu;
+    std::string err;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // policy
+    DevPolicy dp{};
+    int shape = kShape16x16;
+    size_t rec_bytes = 0;
+    std::vector<std::string> slot_names;
+    int8_t pred_orig[kMaxPred] = {};
+    std::vector<int64_t> hot_tr;  // hotValue.timeRange in policy order
+    int n_pred_policy = 0;
+    // shard state
+    int64_t N = -1, node_offset = 0;
+    bool have_hv = false;
+    bool hv_from_counts = false;
+    int64_t hv_ts_counts = 0;
+    bool rec_dirty = true;
+    int64_t B = 0;
+    DevBuf<double> val, hv;
+    DevBuf<int64_t> ts, hv_ts;
+    DevBuf<unsigned char> rec;
+    DevBuf<uint32_t> buckets;
+    DevBuf<int32_t> bnode;
+    DevBuf<int64_t> bts;
+    // scratch for the host-pointer API
+    DevBuf<int64_t> now;
+    DevBuf<uint8_t> flags;
+    DevBuf<long long> keys;
+    DevBuf<int8_t> ff;
+    DevBuf<int64_t> score;
+
+    int fail(int code, const std::string& m) {
+        err = m;
+        return code;
+    }
+    int hipfail(hipError_t e, const char* what) {
+        err = std::string(what) + ": " + hipGetErrorString(e);
+        return CRANE_E_HIP;
+    }
+};
+
+#define HIPTRY(h, expr)                                        \
+    do {                                                       \
+        hipError_t _e = (expr);                                \
+        if (_e != hipSuccess) return (h)->hipfail(_e, #expr);  \
+    } while (0)
+
+static int flatten_policy(crane_dyn* h, const crane_policy* pol) {
+    if (!pol) return h->fail(CRANE_E_INVALID, "policy is NULL");
+    if (pol->n_sync < 0 || pol->n_pred < 0 || pol->n_prio < 0 || pol->n_hot < 0)
+        return h->fail(CRANE_E_INVALID, "negative policy list length");
+    DevPolicy& dp = h->dp;
+    std::memset(&dp, 0, sizeof dp);
+    auto active = [&](const char* name, int64_t* dur) -> bool {  // getActiveDuration
+        for (int32_t i = 0; i < pol->n_sync; ++i)
+            if (std::strcmp(pol->sync_name[i], name) == 0 && pol->sync_period_ns[i] != 0) {
+                *dur = pol->sync_period_ns[i] + kExtraActiveNs;
+                return true;
+            }
+        return false;
+    };
+    auto slot_of = [&](const char* name) -> int {
+        for (size_t i = 0; i < h->slot_names.size(); ++i)
+            if (h->slot_names[i] == name) return (int)i;
+        h->slot_names.emplace_back(name);
+        return (int)h->slot_names.size() - 1;
+    };
+    h->slot_names.clear();
+    h->n_pred_policy = pol->n_pred;
+    for (int32_t k = 0; k < pol->n_pred; ++k) {
+        int64_t dur;
+        // Filter skips predicates with no/zero active duration (plugins.go:56-61)
+        if (!active(pol->pred_name[k], &dur) || dur == 0) continue;
+        if (dp.npd >= kMaxPred) return h->fail(CRANE_E_INVALID, "more than 16 active predicates");
+        if (k > 127) return h->fail(CRANE_E_INVALID, "predicate index > 127");
+        dp.pred_slot[dp.npd] = slot_of(pol->pred_name[k]);
+        dp.pred_limit[dp.npd] = pol->pred_limit[k];
+        dp.pred_dur[dp.npd] = dur;
+        h->pred_orig[dp.npd] = (int8_t)k;
+        dp.npd++;
+    }
+    double wsum = 0.0;
+    for (int32_t k = 0; k < pol->n_prio; ++k) {
+        wsum += pol->prio_weight[k];  // accumulates even for failed terms (stats.go:131)
+        int64_t dur;
+        if (!active(pol->prio_name[k], &dur) || dur == 0) continue;  // term is 0 (stats.go:79-82)
+        if (dp.npr >= kMaxPrio) return h->fail(CRANE_E_INVALID, "more than 16 active priorities");
+        dp.prio_slot[dp.npr] = slot_of(pol->prio_name[k]);
+        dp.prio_w[dp.npr] = pol->prio_weight[k];
+        dp.prio_dur[dp.npr] = dur;
+        dp.npr++;
+    }
+    if ((int)h->slot_names.size() > kMaxSlots) return h->fail(CRANE_E_INVALID, "more than 32 metric keys");
+    dp.n_slots = (int32_t)h->slot_names.size();
+    dp.wsum = wsum;
+    dp.noprio = pol->n_prio == 0;
+    if (pol->n_hot > kMaxWin) return h->fail(CRANE_E_INVALID, "more than 8 hotValue windows");
+    dp.n_win = pol->n_hot;
+    for (int32_t w = 0; w < pol->n_hot; ++w) {
+        // Go integer division by zero panics in annotateNodeHotValue (node.go:117)
+        if (pol->hot_count[w] == 0) return h->fail(CRANE_E_INVALID, "hotValue count must not be 0");
+        dp.win_count[w] = pol->hot_count[w];
+    }
+    h->hot_tr.assign(pol->hot_tr_ns, pol->hot_tr_ns + pol->n_hot);
+    if (dp.npd <= 4 && dp.npr <= 6) h->shape = kShape4x6;
+    else if (dp.npd <= 8 && dp.npr <= 8) h->shape = kShape8x8;
+    else h->shape = kShape16x16;
+    h->rec_bytes = node_rec_bytes(h->shape);
+    return CRANE_OK;
+}
+
+extern "C" {
+
+const char* crane_dyn_version(void) { return "crane_dyn 0.1 gfx950"; }
+
+int64_t crane_dyn_key_node(int64_t key, int64_t* score) {
+    if (key < 0) {
+        if (score) *score = -1;
+        return -1;
+    }
+    if (score) *score = key >> 32;
+    return (int64_t)(0xFFFFFFFFull - ((uint64_t)key & 0xFFFFFFFFull));
+}
+
+int crane_dyn_create(const crane_policy* pol, int32_t device, crane_dyn** out) {
+    if (!out) return CRANE_E_INVALID;
+    *out = nullptr;
+    crane_dyn* h = new crane_dyn();
+    int rc = flatten_policy(h, pol);
+    if (rc) {
+        // keep the handle so the caller can read the error, but flag it unusable
+        h->N = -2;
+        *out = h;
+        return rc;
+    }
+    h->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        h->hipfail(e, "hipSetDevice/hipStreamCreate");
+        h->N = -2;
+        *out = h;
+        return CRANE_E_HIP;
+    }
+    *out = h;
+    return CRANE_OK;
+}
+
+int crane_dyn_destroy(crane_dyn* h) {
+    if (!h) return CRANE_OK;
+    if (h->stream) {
+        (void)hipSetDevice(h->device);
+        (void)hipStreamSynchronize(h->stream);
+    }
+    h->val.release(); h->hv.release(); h->ts.release(); h->hv_ts.release(); h->rec.release();
+    h->buckets.release(); h->bnode.release(); h->bts.release(); h->now.release(); h->flags.release();
+    h->keys.release(); h->ff.release(); h->score.release();
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return CRANE_OK;
+}
+
+const char* crane_dyn_last_error(const crane_dyn* h) { return h ? h->err.c_str() : "null engine"; }
+
+int32_t crane_dyn_num_metrics(const crane_dyn* h) { return h ? (int32_t)h->slot_names.size() : 0; }
+
+const char* crane_dyn_metric_name(const crane_dyn* h, int32_t slot) {
+    if (!h || slot < 0 || slot >= (int32_t)h->slot_names.size()) return nullptr;
+    return h->slot_names[slot].c_str();
+}
+
+int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const double* val, const int64_t* ts,
+                           const double* hv, const int64_t* hv_ts) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->N == -2) return h->fail(CRANE_E_STATE, "engine was not created successfully");
+    if (n < 0 || n > 0xFFFFFFFFLL || node_offset < 0 || node_offset + n > 0xFFFFFFFFLL)
+        return h->fail(CRANE_E_INVALID, "node count/offset out of range (global indices must fit 32 bits)");
+    const int64_t M = h->dp.n_slots;
+    if (n > 0 && M > 0 && (!val || !ts)) return h->fail(CRANE_E_INVALID, "val/ts must not be NULL");
+    if ((hv == nullptr) != (hv_ts == nullptr)) return h->fail(CRANE_E_INVALID, "hv and hv_ts must both be set or NULL");
+    HIPTRY(h, hipSetDevice(h->device));
+    HIPTRY(h, h->val.reserve((size_t)(M * n)));
+    HIPTRY(h, h->ts.reserve((size_t)(M * n)));
+    HIPTRY(h, h->hv.reserve((size_t)n));
+    HIPTRY(h, h->hv_ts.reserve((size_t)n));
+    HIPTRY(h, h->rec.reserve((size_t)n * h->rec_bytes));
+    if (M * n > 0) {
+        HIPTRY(h, hipMemcpyAsync(h->val.p, val, sizeof(double) * M * n, hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipMemcpyAsync(h->ts.p, ts, sizeof(int64_t) * M * n, hipMemcpyHostToDevice, h->stream));
+    }
+    if (hv && n > 0) {
+        HIPTRY(h, hipMemcpyAsync(h->hv.p, hv, sizeof(double) * n, hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipMemcpyAsync(h->hv_ts.p, hv_ts, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
+    }
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    h->N = n;
+    h->node_offset = node_offset;
+    h->have_hv = hv != nullptr;
+    h->hv_from_counts = false;
+    h->rec_dirty = true;
+    return CRANE_OK;
+}
+
+int crane_dyn_upload_bindings(crane_dyn* h, int64_t n, const int32_t* node, const int64_t* ts_s) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->N == -2) return h->fail(CRANE_E_STATE, "engine was not created successfully");
+    if (n < 0 || (n > 0 && (!node || !ts_s))) return h->fail(CRANE_E_INVALID, "bad binding arrays");
+    HIPTRY(h, hipSetDevice(h->device));
+    HIPTRY(h, h->bnode.reserve((size_t)n));
+    HIPTRY(h, h->bts.reserve((size_t)n));
+    if (n > 0) {
+        HIPTRY(h, hipMemcpyAsync(h->bnode.p, node, sizeof(int32_t) * n, hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipMemcpyAsync(h->bts.p, ts_s, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
+    }
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    h->B = n;
+    return CRANE_OK;
+}
+
+static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hipStream_t st) {
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before refreshing hot values");
+    DevPolicy& dp = h->dp;
+    HotCutoffs cut{};
+    cut.n_win = dp.n_win;
+    // time.Now().UTC().Unix() - int64(timeRange.Seconds())   (binding.go:85)
+    const int64_t now_unix = floor_div(now_ns, 1000000000LL);
+    int64_t c[kMaxWin];
+    int order[kMaxWin];
+    for (int w = 0; w < dp.n_win; ++w) {
+        const int64_t trs = go_seconds_trunc(h->hot_tr[w]);
+        c[w] = now_unix - trs;
+        order[w] = w;
+    }
+    std::stable_sort(order, order + dp.n_win, [&](int a, int b) { return c[a] < c[b]; });
+    for (int r = 0; r < dp.n_win; ++r) {
+        cut.sorted[r] = c[order[r]];
+        dp.win_pos[order[r]] = r;
+        dp.win_cut_sorted[r] = c[order[r]];
+    }
+    const size_t nb = (size_t)std::max(1, dp.n_win) * (size_t)std::max<int64_t>(h->N, 1);
+    HIPTRY(h, h->buckets.reserve(nb));
+    HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
+    HIPTRY(h, launch_hot_count(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, st));
+    h->hv_from_counts = true;
+    h->hv_ts_counts = hv_ts_ns;
+    h->rec_dirty = true;
+    return CRANE_OK;
+}
+
+static int node_pass_locked(crane_dyn* h, hipStream_t st) {
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before the node pass");
+    HIPTRY(h, launch_node_pass(h->shape, h->dp, h->N, h->val.p, h->ts.p, h->have_hv ? h->hv.p : nullptr,
+                               h->hv_ts.p, h->hv_from_counts ? h->buckets.p : nullptr, h->hv_ts_counts, h->rec.p,
+                               st));
+    h->rec_dirty = false;
+    return CRANE_OK;
+}
+
+static int eval_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags, long long* d_keys,
+                       int8_t* d_ff, int64_t* d_score, hipStream_t st) {
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
+    if (h->rec_dirty) {
+        int rc = node_pass_locked(h, st);
+        if (rc) return rc;
+    }
+    HIPTRY(h, hipMemsetAsync(d_keys, 0xFF, sizeof(long long) * (size_t)P, st));
+    MatrixOut mo{};
+    mo.first_fail = d_ff;
+    mo.score = d_score;
+    std::memcpy(mo.pred_orig, h->pred_orig, sizeof mo.pred_orig);
+    HIPTRY(h, launch_eval(h->shape, h->rec.p, h->N, h->node_offset, d_now, d_flags, P, h->dp.wsum, h->dp.noprio,
+                          d_keys, mo, st));
+    return CRANE_OK;
+}
+
+int crane_dyn_refresh_hot_values(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    HIPTRY(h, hipSetDevice(h->device));
+    int rc = hot_values_locked(h, now_ns, hv_ts_ns, h->stream);
+    if (rc) return rc;
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    return CRANE_OK;
+}
+
+int crane_dyn_refresh_hot_values_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, void* stream) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    HIPTRY(h, hipSetDevice(h->device));
+    return hot_values_locked(h, now_ns, hv_ts_ns, stream ? (hipStream_t)stream : h->stream);
+}
+
+int crane_dyn_node_pass_async(crane_dyn* h, void* stream) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    HIPTRY(h, hipSetDevice(h->device));
+    return node_pass_locked(h, stream ? (hipStream_t)stream : h->stream);
+}
+
+int crane_dyn_eval_keys_async(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags,
+                              int64_t* d_keys, void* stream) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (P < 0 || (P > 0 && (!d_now || !d_keys))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
+    if (P > (int64_t)0x7FFFFFFF * 256) return h->fail(CRANE_E_INVALID, "too many pods");
+    HIPTRY(h, hipSetDevice(h->device));
+    return eval_locked(h, P, d_now, d_flags, reinterpret_cast<long long*>(d_keys), nullptr, nullptr,
+                       stream ? (hipStream_t)stream : h->stream);
+}
+
+int crane_dyn_eval(crane_dyn* h, int64_t P, const int64_t* now_ns, const uint8_t* pod_flags, int8_t* first_fail,
+                   int64_t* score, int64_t* chosen, int64_t* chosen_score) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (P < 0 || (P > 0 && !now_ns)) return h->fail(CRANE_E_INVALID, "bad pod arrays");
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
+    HIPTRY(h, hipSetDevice(h->device));
+    const int64_t N = h->N;
+    const bool matrix = first_fail || score;
+    // bound the matrix scratch to ~64M entries per pass
+    int64_t pc = P;
+    if (matrix && N > 0) pc = std::max<int64_t>(1, std::min<int64_t>(P, (int64_t)(64LL << 20) / N));
+    if (pc <= 0) pc = 1;
+    HIPTRY(h, h->now.reserve((size_t)pc));
+    HIPTRY(h, h->flags.reserve((size_t)pc));
+    HIPTRY(h, h->keys.reserve((size_t)pc));
+    if (first_fail) HIPTRY(h, h->ff.reserve((size_t)(pc * std::max<int64_t>(N, 1))));
+    if (score) HIPTRY(h, h->score.reserve((size_t)(pc * std::max<int64_t>(N, 1))));
+    std::vector<long long> hk((size_t)pc);
+    for (int64_t p0 = 0; p0 < P; p0 += pc) {
+        const int64_t np = std::min(pc, P - p0);
+        HIPTRY(h, hipMemcpyAsync(h->now.p, now_ns + p0, sizeof(int64_t) * np, hipMemcpyHostToDevice, h->stream));
+        if (pod_flags)
+            HIPTRY(h, hipMemcpyAsync(h->flags.p, pod_flags + p0, np, hipMemcpyHostToDevice, h->stream));
+        int rc = eval_locked(h, np, h->now.p, pod_flags ? h->flags.p : nullptr, h->keys.p,
+                             first_fail ? h->ff.p : nullptr, score ? h->score.p : nullptr, h->stream);
+        if (rc) return rc;
+        HIPTRY(h, hipMemcpyAsync(hk.data(), h->keys.p, sizeof(long long) * np, hipMemcpyDeviceToHost, h->stream));
+        if (first_fail && N > 0)
+            HIPTRY(h, hipMemcpyAsync(first_fail + p0 * N, h->ff.p, (size_t)(np * N), hipMemcpyDeviceToHost, h->stream));
+        if (score && N > 0)
+            HIPTRY(h, hipMemcpyAsync(score + p0 * N, h->score.p, sizeof(int64_t) * np * N, hipMemcpyDeviceToHost,
+                                     h->stream));
+        HIPTRY(h, hipStreamSynchronize(h->stream));
+        for (int64_t i = 0; i < np; ++i) {
+            int64_t s;
+            const int64_t nd = crane_dyn_key_node(hk[i], &s);
+            if (chosen) chosen[p0 + i] = nd;
+            if (chosen_score) chosen_score[p0 + i] = s;
+        }
+    }
+    return CRANE_OK;
+}
+
+int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod_flags, int64_t* chosen) {
+    if (!h) return CRANE_E_INVALID;
+    (void)P; (void)now_ns; (void)pod_flags; (void)chosen;
+    return h->fail(CRANE_E_STATE, "greedy mode not built yet");
+}
+
+}  // extern "C"

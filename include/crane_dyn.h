@@ -1,0 +1,162 @@
+/*
+ * crane_dyn.h — C ABI of the MI355X engine for crane-scheduler's Dynamic
+ * plugin hot path (Filter + Score batched over pods x nodes, hot values,
+ * selection).  Plain C types only: this is what a cgo shim in the scheduler
+ * binds.  Citations are into /root/reference.
+ *
+ * Reference interfaces this ABI replaces:
+ *   - DynamicScheduler.Filter        pkg/plugins/dynamic/plugins.go:39-69
+ *   - DynamicScheduler.Score         pkg/plugins/dynamic/plugins.go:73-98
+ *   - getNodeScore/isOverLoad/...    pkg/plugins/dynamic/stats.go:30-166
+ *   - NewDynamicScheduler            pkg/plugins/dynamic/plugins.go:105-120
+ *   - LoadPolicyFromFile/loadPolicy  pkg/plugins/dynamic/policyfile.go:11-33
+ *   - BindingRecords.GetLastNodeBindingCount  pkg/controller/annotator/binding.go:81-97
+ *   - annotateNodeHotValue           pkg/controller/annotator/node.go:113-121
+ *   - upstream selectHost (argmax; lowest node index wins ties — declared
+ *     deviation from upstream's random tie-break)
+ *
+ * Conventions: every function returns 0 on success and a negative CRANE_E_*
+ * code on failure; crane_dyn_last_error() then describes it.  Callers own all
+ * host arrays; the engine copies them during the call and keeps no pointer.
+ * Calls on one engine are serialised by an internal mutex.
+ */
+#ifndef CRANE_DYN_H
+#define CRANE_DYN_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRANE_OK 0
+#define CRANE_E_INVALID -1  /* bad argument / policy */
+#define CRANE_E_HIP -2      /* HIP runtime failure */
+#define CRANE_E_STATE -3    /* call out of order (e.g. eval before upload) */
+#define CRANE_E_PARSE -4    /* policy file could not be decoded */
+#define CRANE_E_IO -5       /* policy file could not be read */
+
+/* Sentinel timestamp for an annotation that is missing or malformed
+ * (getResourceUsage errors that do not depend on the current time). */
+#define CRANE_TS_INVALID INT64_MIN
+
+/* Pod flag bits (crane_dyn_eval*). */
+#define CRANE_POD_DAEMONSET 1u /* utils.IsDaemonsetPod (utils.go:17-24): Filter bypass */
+
+/* DynamicSchedulerPolicy.Spec (pkg/plugins/apis/policy/types.go:14-39),
+ * flattened in policy order.  Durations in nanoseconds. */
+typedef struct crane_policy {
+    int32_t n_sync;
+    const char *const *sync_name;
+    const int64_t *sync_period_ns;
+    int32_t n_pred;
+    const char *const *pred_name;
+    const double *pred_limit; /* maxLimitPecent */
+    int32_t n_prio;
+    const char *const *prio_name;
+    const double *prio_weight;
+    int32_t n_hot;
+    const int64_t *hot_tr_ns;  /* hotValue.timeRange */
+    const int64_t *hot_count;  /* hotValue.count (must be != 0) */
+} crane_policy;
+
+/* ---------------------------------------------------------------- policy
+ * Strict decoder for the DynamicSchedulerPolicy file (YAML block subset or
+ * JSON), apiVersion scheduler.policy.crane.io/v1alpha1 — replaces
+ * LoadPolicyFromFile/loadPolicy (policyfile.go:11-33).  Unknown or duplicate
+ * fields are errors, as with the reference's strict codec
+ * (policy/scheme/scheme.go:17). */
+typedef struct crane_policy_doc crane_policy_doc;
+int crane_policy_load_file(const char *path, crane_policy_doc **out, char *err, size_t errcap);
+int crane_policy_load_bytes(const char *data, size_t n, crane_policy_doc **out, char *err, size_t errcap);
+const crane_policy *crane_policy_view(const crane_policy_doc *doc);
+void crane_policy_free(crane_policy_doc *doc);
+
+/* ------------------------------------------------------------ annotations
+ * Host parser for one node annotation value "<float>,<YYYY-MM-DDTHH:MM:SSZ>"
+ * (written by node.go:123-146 with prometheus.go:124 / strconv.Itoa values,
+ * local time per utils.go:26-45).  Follows strings.Split + time.ParseInLocation
+ * + strconv.ParseFloat of getResourceUsage (stats.go:51-76).  *ts_ns is the
+ * Unix time in ns or CRANE_TS_INVALID when the value is unusable at any time
+ * (missing parts, bad timestamp, bad float); negative values are returned as
+ * parsed — the engine rejects them like stats.go:71-73. */
+int crane_tz_offset(const char *tz_name, int64_t *offset_s); /* "" or NULL = $TZ, default Asia/Shanghai */
+void crane_parse_annotation(const char *s, size_t n, int64_t tz_offset_s, double *value, int64_t *ts_ns);
+
+/* ------------------------------------------------------------------ engine */
+typedef struct crane_dyn crane_dyn;
+
+/* NewDynamicScheduler (plugins.go:105-120) minus the policy file read: build
+ * an engine for `pol` on HIP device `device`.  The policy is validated and
+ * flattened into the device policy table here. */
+int crane_dyn_create(const crane_policy *pol, int32_t device, crane_dyn **out);
+int crane_dyn_destroy(crane_dyn *h);
+const char *crane_dyn_last_error(const crane_dyn *h);
+
+/* Metric slots: the distinct annotation keys the policy reads, in the order
+ * the SoA rows of crane_dyn_upload_nodes must follow. */
+int32_t crane_dyn_num_metrics(const crane_dyn *h);
+const char *crane_dyn_metric_name(const crane_dyn *h, int32_t slot);
+
+/* Upload one node shard's parsed annotations (host SoA):
+ *   val[m*n_nodes + i], ts_ns[m*n_nodes + i] for metric slot m;
+ *   hv[i], hv_ts_ns[i] = node_hot_value annotation (hv may be NULL: all
+ *   nodes have no hot value).
+ * node_offset = global index of local node 0 (node sharding across GPUs);
+ * chosen-node results and packed keys use global indices. */
+int crane_dyn_upload_nodes(crane_dyn *h, int64_t n_nodes, int64_t node_offset,
+                           const double *val, const int64_t *ts_ns,
+                           const double *hv, const int64_t *hv_ts_ns);
+
+/* Upload the binding records (BindingRecords heap content, binding.go:14-19):
+ * node = LOCAL node index of the shard (<0 or >= n_nodes: matches no node),
+ * ts_s = Binding.Timestamp (Unix seconds). */
+int crane_dyn_upload_bindings(crane_dyn *h, int64_t n, const int32_t *node, const int64_t *ts_s);
+
+/* Recompute every node's hot value from the uploaded bindings as the
+ * controller does at `now_ns` (binding.go:81-97, node.go:113-121) and use it
+ * as the node_hot_value annotation, stamped hv_ts_ns, from now on. */
+int crane_dyn_refresh_hot_values(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns);
+
+/* Evaluate a pod batch against the current shard.  now_ns[p] is pod p's
+ * time.Now(); pod_flags[p] carries CRANE_POD_* bits (NULL = 0).
+ * Outputs (any may be NULL):
+ *   first_fail[p*n + i]: -1 = Filter Success, else index (policy order) of the
+ *                        first overloaded predicate (Unschedulable);
+ *   score[p*n + i]     : Score() result in [0,100] for every node;
+ *   chosen[p]          : global index of the feasible node with the highest
+ *                        score, lowest index on ties; -1 = none feasible;
+ *   chosen_score[p]    : that node's score (-1 when none). */
+int crane_dyn_eval(crane_dyn *h, int64_t n_pods, const int64_t *now_ns, const uint8_t *pod_flags,
+                   int8_t *first_fail, int64_t *score, int64_t *chosen, int64_t *chosen_score);
+
+/* Device-resident variant for batched pipelines: all pointers are device
+ * pointers, work is enqueued on `stream` (hipStream_t; NULL = engine stream)
+ * and the call returns without synchronising.  keys[p] = (score << 32) |
+ * (0xFFFFFFFF - global_node_index) of the shard's best feasible node, or -1.
+ * A max-reduction of keys across node shards (e.g. RCCL allreduce, int64,
+ * max) gives the global choice. */
+int crane_dyn_eval_keys_async(crane_dyn *h, int64_t n_pods, const int64_t *d_now_ns,
+                              const uint8_t *d_pod_flags, int64_t *d_keys, void *stream);
+/* Asynchronous pieces of one scheduling step on `stream`:
+ * hot values from bindings (K2) and the node pass (K1). */
+int crane_dyn_refresh_hot_values_async(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns, void *stream);
+int crane_dyn_node_pass_async(crane_dyn *h, void *stream);
+
+/* Sequential-greedy batch: one `now_ns` for the whole batch; pods are placed
+ * in order and each placement appends a binding (Timestamp = now) to the
+ * chosen node, refreshing its hot value before the next pod is scored.  The
+ * hot values start from the uploaded bindings.  chosen[p] as above. */
+int crane_dyn_greedy(crane_dyn *h, int64_t n_pods, int64_t now_ns, const uint8_t *pod_flags, int64_t *chosen);
+
+/* Decode a packed key: returns the global node index (-1 for key < 0) and
+ * stores the score in *score (-1 for key < 0) when score != NULL. */
+int64_t crane_dyn_key_node(int64_t key, int64_t *score);
+
+/* Build/version info string (static storage). */
+const char *crane_dyn_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,168 @@
+"""Parity of the HIP engine (through the C ABI) with the oracle and the golden vectors.
+
+Bit-exact on filter results (first failing predicate), int64 scores and chosen
+nodes, per /root/reference/pkg/plugins/dynamic/{plugins,stats}.go.
+"""
+import numpy as np
+import pytest
+
+from conftest import policy_from_json
+from helpers import SH, engine_for, oracle_soa
+
+pytestmark = pytest.mark.gpu
+
+cd = pytest.importorskip("crane_dyn")
+from crane_dyn import synth  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+
+def _eval_annotations(spec, nodes, now, ds):
+    eng = engine_for(spec)
+    val, ts, hv, hv_ts = cd.parse_nodes(eng.metric_names, nodes, SH)
+    eng.upload_nodes(val, ts, hv, hv_ts)
+    return eng.eval(np.asarray(now, np.int64), np.asarray(ds, np.uint8), matrix=True)
+
+
+def test_kats(kats):
+    for k in kats["kats"]:
+        spec = policy_from_json(k["policy"])
+        ff, sc, ch, cs = _eval_annotations(spec, [k["annotations"]], [k["now_ns"]], [k["daemonset"]])
+        assert ff[0, 0] == k["expect_filter"], k["name"]
+        assert sc[0, 0] == k["expect_score"], k["name"]
+        assert ch[0] == (0 if k["expect_filter"] < 0 else -1), k["name"]
+        assert cs[0] == (k["expect_score"] if k["expect_filter"] < 0 else -1), k["name"]
+
+
+def test_golden_cluster(cluster_small):
+    c = cluster_small
+    spec = policy_from_json(c["policy"])
+    now = [p["now_ns"] for p in c["pods"]]
+    ds = [p["daemonset"] for p in c["pods"]]
+    ff, sc, ch, _ = _eval_annotations(spec, c["nodes"], now, ds)
+    assert ff.tolist() == c["expect_filter"]
+    assert sc.tolist() == c["expect_score"]
+    assert ch.tolist() == c["expect_chosen"]
+
+
+@pytest.mark.parametrize("n_nodes,n_pods,seed", [(1, 1, 1), (100, 1, 2), (257, 33, 3), (5000, 64, 4), (3000, 700, 5)])
+def test_random_vs_oracle(n_nodes, n_pods, seed):
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, n_nodes, n_pods, seed=seed, pod_step_ns=1_700_000_000)
+    eng = engine_for(spec, c)
+    ff, sc, ch, cs = eng.eval(c.now, c.ds, matrix=True)
+    off, osc, och = oracle_soa(spec, c)
+    assert np.array_equal(ff, off)
+    assert np.array_equal(sc, osc)
+    assert np.array_equal(ch, och)
+    # chosen score equals the max feasible score
+    for p in range(n_pods):
+        feas = (off[p] < 0)
+        assert cs[p] == (osc[p][feas].max() if feas.any() else -1)
+
+
+def test_keys_only_matches_matrix():
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 20000, 300, seed=11, pod_step_ns=3_000_000_000)
+    eng = engine_for(spec, c)
+    _, _, ch_m, cs_m = eng.eval(c.now, c.ds, matrix=True)
+    _, _, ch, cs = eng.eval(c.now, c.ds, matrix=False)
+    assert np.array_equal(ch, ch_m) and np.array_equal(cs, cs_m)
+    _, _, och = oracle_soa(spec, c, want_matrix=False)
+    assert np.array_equal(ch, och)
+
+
+def test_no_hot_value_and_empty_shard():
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 50, 4, seed=7)
+    eng = cd.Engine(cd.Policy(spec))
+    val, ts, _ = c.rows(eng.metric_names)
+    eng.upload_nodes(val, ts)  # no node_hot_value annotations at all
+    ff, sc, ch, _ = eng.eval(c.now, c.ds, matrix=True)
+    off, osc, och = O.eval_soa(spec, c.metric_names, c.ok, c.val, np.where(c.ok == 1, c.ts, 0),
+                               np.zeros(50, np.uint8), np.zeros(50), np.zeros(50, np.int64), c.now, c.ds)
+    assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch, och)
+    M = len(eng.metric_names)
+    eng.upload_nodes(np.zeros((M, 0)), np.zeros((M, 0), np.int64))
+    _, _, ch, cs = eng.eval(c.now, c.ds)
+    assert (ch == -1).all() and (cs == -1).all()
+
+
+def test_policy_variants():
+    """Non-default policy shapes exercise the 8x8 and 16x16 NodeRec kernels and skipped entries."""
+    m = 60 * 10**9
+    base = cd.default_policy_spec()
+    specs = []
+    s = dict(base)
+    s["predicate"] = base["predicate"] + [("cpu_usage_max_avg_1d", 0.5), ("mem_usage_max_avg_1d", 0.0),
+                                          ("not_synced", 0.1), ("mem_usage_avg_5m", 0.3)]
+    specs.append(s)
+    s = dict(base)
+    s["syncPolicy"] = base["syncPolicy"] + [("m%d" % i, (i + 1) * m) for i in range(10)] + [("zero", 0), ("neg5", -5 * m)]
+    s["priority"] = base["priority"] + [("m%d" % i, 0.1 * (i + 1)) for i in range(10)] + [("zero", 1.0), ("neg5", 2.0)]
+    s["predicate"] = [("m%d" % i, 0.4 + 0.05 * i) for i in range(10)] + [("neg5", 0.5)]
+    specs.append(s)
+    s = dict(base)
+    s["priority"] = []
+    specs.append(s)
+    s = dict(base)
+    s["priority"] = [("cpu_usage_avg_5m", 1.0), ("mem_usage_avg_5m", -1.0)]  # weight sum 0 -> NaN/Inf scores
+    specs.append(s)
+    for i, spec in enumerate(specs):
+        c = synth.make_cluster(spec, 777, 40, seed=100 + i, pod_step_ns=20_000_000_000)
+        eng = engine_for(spec, c)
+        ff, sc, ch, _ = eng.eval(c.now, c.ds, matrix=True)
+        off, osc, och = oracle_soa(spec, c)
+        assert np.array_equal(ff, off), i
+        assert np.array_equal(sc, osc), i
+        assert np.array_equal(ch, och), i
+
+
+def test_hot_values_vs_oracle(kats):
+    """KAT-11 through the engine: every metric fresh at 0.0 (base score 100), so score = 100 - 10*hv."""
+    h = kats["hot"]["KAT-11"]
+    spec = policy_from_json(h["policy"])
+    b = np.array(h["bindings"], np.int64)
+    eng = cd.Engine(cd.Policy(spec))
+    M, N = len(eng.metric_names), h["n_nodes"]
+    now_ns = h["now_unix"] * 10**9
+    eng.upload_nodes(np.zeros((M, N)), np.full((M, N), now_ns, np.int64))
+    eng.upload_bindings(b[:, 0], b[:, 1])
+    eng.refresh_hot_values(now_ns, now_ns)
+    _, sc, _, _ = eng.eval(np.array([now_ns]), matrix=True)
+    assert sc[0].tolist() == [max(0, 100 - 10 * v) for v in h["expect_hv"]]
+    assert sc[0, 0] == 50  # hv = 5 (SURVEY KAT-11)
+
+
+@pytest.mark.parametrize("n_nodes,n_bind,seed", [(1000, 50_000, 1), (20_000, 300_000, 2), (100, 10, 3)])
+def test_hot_values_random(n_nodes, n_bind, seed):
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, n_nodes, 16, n_bindings=n_bind, seed=seed, pod_step_ns=10_000_000_000)
+    # include bindings for nodes outside the shard
+    bn = c.b_node.copy()
+    bn[::97] = -1
+    bn[1::101] = n_nodes + 5
+    eng = engine_for(spec, c)
+    eng.upload_bindings(bn, c.b_ts)
+    now = int(c.now[0])
+    eng.refresh_hot_values(now, now)
+    _, cnt_hv = O.hot_values(spec, bn, c.b_ts, n_nodes, now // 10**9)
+    ff, sc, ch, _ = eng.eval(c.now, c.ds, matrix=True)
+    off, osc, och = oracle_soa(spec, c, hv_override=(cnt_hv.astype(np.float64), np.full(n_nodes, now, np.int64)))
+    assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch, och)
+
+
+def test_division_exactness_sweep():
+    """Dense random usages: int(score/weight) must match the CPU bit for bit (KAT-3/4 FMA traps)."""
+    spec = cd.default_policy_spec()
+    rng = np.random.default_rng(5)
+    N = 200_000
+    c = synth.make_cluster(spec, N, 1, seed=9, invalid=False)
+    r = rng.random(c.val.shape)
+    dec = rng.integers(1, 4, c.val.shape)
+    c.val = np.select([dec == 1, dec == 2], [np.round(r, 1), np.round(r, 2)], np.round(r, 3))  # 1-3 decimals
+    c.ts[:] = synth.NOW0_NS
+    c.hv_ts[:] = synth.TS_INVALID
+    eng = engine_for(spec, c)
+    _, sc, _, _ = eng.eval(c.now, c.ds, matrix=True)
+    _, osc, _ = oracle_soa(spec, c)
+    assert np.array_equal(sc, osc)
