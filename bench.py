@@ -127,13 +127,14 @@ def main():
     # (pod, node) come from the shipped code object's loop body.
     info_path = os.path.join(ROOT, "crane-scheduler_amd", "lib", "k3_isa.json")
     isa = json.load(open(info_path)) if os.path.exists(info_path) else {}
-    valu_per_eval = isa.get("valu_per_node_iter")
+    variant = os.environ.get("CRANE_K3_VARIANT", str(isa.get("default_variant", 4)))
+    valu_per_eval = isa.get("variants", {}).get(variant, {}).get("valu_per_node")
     roof = None
     if valu_per_eval:
         achieved = valu_per_eval * P * N / (k3_ms * 1e-3) / 1e12  # Tops/s (lane-ops)
         peak = VALU_PEAK_GOPS / 1e3
         roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "Tlane-op/s",
-                "frac": round(achieved / peak, 4), "traffic": None, "kernel": "k3_eval<4,6>",
+                "frac": round(achieved / peak, 4), "traffic": None, "kernel": f"k3_eval<4,6,false,{variant}>",
                 "valu_per_eval": valu_per_eval}
     # node pass + hot values: HBM-bound streaming kernels (algorithmic bytes)
     rec_bytes = 144

@@ -215,7 +215,7 @@ class Engine:
         self.n_nodes = 0
 
     def close(self):
-        if getattr(self, "h", None) and self.h.value:
+        if getattr(self, "h", None) and self.h.value and lib is not None:
             lib.crane_dyn_destroy(self.h)
             self.h = C.c_void_p()
 

@@ -83,6 +83,7 @@ struct crane_dyn {
     bool hv_from_counts = false;
     int64_t hv_ts_counts = 0;
     bool rec_dirty = true;
+    bool buckets_zero = false;  // K1 consumes (zeroes) the buckets K2 filled
     int64_t B = 0;
     DevBuf<double> val, hv;
     DevBuf<int64_t> ts, hv_ts;
@@ -96,6 +97,11 @@ struct crane_dyn {
     DevBuf<long long> keys;
     DevBuf<int8_t> ff;
     DevBuf<int64_t> score;
+    DevBuf<uint32_t> gcnt;  // greedy: per-window counts [W][N]
+    DevBuf<int64_t> gbase, gchosen;
+    DevBuf<uint8_t> gleaf, gflags;
+    DevBuf<double> thr;  // quotient thresholds (K3 division-free path), empty if unusable
+    double inv_w = 0.0;
 
     int fail(int code, const std::string& m) {
         err = m;
@@ -210,6 +216,32 @@ int crane_dyn_create(const crane_policy* pol, int32_t device, crane_dyn** out) {
         *out = h;
         return CRANE_E_HIP;
     }
+    // quotient thresholds T[k] = min{s : RN(s/W) >= k} for the division-free K3 path
+    const double W = h->dp.wsum;
+    if (!h->dp.noprio && W > 0 && std::isfinite(W)) {
+        std::vector<double> T(kQMax + 1);
+        T[0] = -INFINITY;
+        const uint64_t inf_bits = 0x7FF0000000000000ull;
+        for (int k = 1; k <= kQMax; ++k) {
+            uint64_t lo = 0, hi = inf_bits;  // predicate false at lo=+0, true at +inf
+            while (hi - lo > 1) {
+                const uint64_t mid = lo + (hi - lo) / 2;
+                double sm;
+                std::memcpy(&sm, &mid, 8);
+                if (sm / W >= (double)k) hi = mid;
+                else lo = mid;
+            }
+            std::memcpy(&T[k], &hi, 8);
+        }
+        e = h->thr.reserve(T.size());
+        if (e == hipSuccess) e = hipMemcpy(h->thr.p, T.data(), sizeof(double) * T.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            h->hipfail(e, "threshold table");
+            h->N = -2;
+            return CRANE_E_HIP;
+        }
+        h->inv_w = 1.0 / W;
+    }
     *out = h;
     return CRANE_OK;
 }
@@ -222,7 +254,8 @@ int crane_dyn_destroy(crane_dyn* h) {
     }
     h->val.release(); h->hv.release(); h->ts.release(); h->hv_ts.release(); h->rec.release();
     h->buckets.release(); h->bnode.release(); h->bts.release(); h->now.release(); h->flags.release();
-    h->keys.release(); h->ff.release(); h->score.release();
+    h->keys.release(); h->ff.release(); h->score.release(); h->thr.release();
+    h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -262,6 +295,7 @@ int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const d
         HIPTRY(h, hipMemcpyAsync(h->hv_ts.p, hv_ts, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
     }
     HIPTRY(h, hipStreamSynchronize(h->stream));
+    if (n != h->N) h->buckets_zero = false;
     h->N = n;
     h->node_offset = node_offset;
     h->have_hv = hv != nullptr;
@@ -308,20 +342,23 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         dp.win_cut_sorted[r] = c[order[r]];
     }
     const size_t nb = (size_t)std::max(1, dp.n_win) * (size_t)std::max<int64_t>(h->N, 1);
+    if (nb > h->buckets.n) h->buckets_zero = false;
     HIPTRY(h, h->buckets.reserve(nb));
-    HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
+    if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
     HIPTRY(h, launch_hot_count(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, st));
+    h->buckets_zero = false;
     h->hv_from_counts = true;
     h->hv_ts_counts = hv_ts_ns;
     h->rec_dirty = true;
     return CRANE_OK;
 }
 
-static int node_pass_locked(crane_dyn* h, hipStream_t st) {
+static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nullptr) {
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before the node pass");
     HIPTRY(h, launch_node_pass(h->shape, h->dp, h->N, h->val.p, h->ts.p, h->have_hv ? h->hv.p : nullptr,
                                h->hv_ts.p, h->hv_from_counts ? h->buckets.p : nullptr, h->hv_ts_counts, h->rec.p,
-                               st));
+                               st, cnt_out));
+    if (h->hv_from_counts) h->buckets_zero = true;  // K1 zeroed what it read
     h->rec_dirty = false;
     return CRANE_OK;
 }
@@ -339,7 +376,7 @@ static int eval_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint
     mo.score = d_score;
     std::memcpy(mo.pred_orig, h->pred_orig, sizeof mo.pred_orig);
     HIPTRY(h, launch_eval(h->shape, h->rec.p, h->N, h->node_offset, d_now, d_flags, P, h->dp.wsum, h->dp.noprio,
-                          d_keys, mo, st));
+                          d_keys, mo, h->inv_w, h->thr.n ? h->thr.p : nullptr, st));
     return CRANE_OK;
 }
 
@@ -424,8 +461,44 @@ int crane_dyn_eval(crane_dyn* h, int64_t P, const int64_t* now_ns, const uint8_t
 
 int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod_flags, int64_t* chosen) {
     if (!h) return CRANE_E_INVALID;
-    (void)P; (void)now_ns; (void)pod_flags; (void)chosen;
-    return h->fail(CRANE_E_STATE, "greedy mode not built yet");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (P < 0 || (P > 0 && !chosen)) return h->fail(CRANE_E_INVALID, "bad pod arrays");
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before greedy placement");
+    if (h->N > kGreedyMaxNodes) return h->fail(CRANE_E_INVALID, "greedy mode supports up to 64^4 nodes");
+    HIPTRY(h, hipSetDevice(h->device));
+    hipStream_t st = h->stream;
+    const int64_t N = h->N;
+    // hot values from the binding log at `now`, annotation stamped `now` (fresh)
+    int rc = hot_values_locked(h, now_ns, now_ns, st);
+    if (rc) return rc;
+    const int W = h->dp.n_win;
+    HIPTRY(h, h->gcnt.reserve((size_t)std::max(1, W) * (size_t)std::max<int64_t>(N, 1)));
+    rc = node_pass_locked(h, st, h->gcnt.p);
+    if (rc) return rc;
+    h->rec_dirty = true;  // records now carry the greedy batch's hot values; recompute for eval
+    GreedyArgs a{};
+    a.now = now_ns;
+    a.wsum = h->dp.wsum;
+    a.noprio = h->dp.noprio;
+    a.n_win = W;
+    const int64_t now_unix = floor_div(now_ns, 1000000000LL);
+    for (int w = 0; w < W; ++w) {
+        a.win_count[w] = h->dp.win_count[w];
+        // binding.go:85-91 for Binding{Timestamp: now_unix}
+        a.win_inc[w] = now_unix > now_unix - go_seconds_trunc(h->hot_tr[w]);
+    }
+    HIPTRY(h, h->gbase.reserve((size_t)std::max<int64_t>(N, 1)));
+    HIPTRY(h, h->gleaf.reserve((size_t)std::max<int64_t>(N, 1)));
+    HIPTRY(h, h->gchosen.reserve((size_t)std::max<int64_t>(P, 1)));
+    HIPTRY(h, h->gflags.reserve((size_t)std::max<int64_t>(P, 1)));
+    if (pod_flags && P > 0) HIPTRY(h, hipMemcpyAsync(h->gflags.p, pod_flags, P, hipMemcpyHostToDevice, st));
+    HIPTRY(h, launch_greedy(h->shape, h->rec.p, N, h->gcnt.p, a, h->gbase.p, h->gleaf.p, P,
+                            pod_flags ? h->gflags.p : nullptr, h->gchosen.p, st));
+    if (P > 0) HIPTRY(h, hipMemcpyAsync(chosen, h->gchosen.p, sizeof(int64_t) * P, hipMemcpyDeviceToHost, st));
+    HIPTRY(h, hipStreamSynchronize(st));
+    for (int64_t p = 0; p < P; ++p)
+        if (chosen[p] >= 0) chosen[p] += h->node_offset;
+    return CRANE_OK;
 }
 
 }  // extern "C"

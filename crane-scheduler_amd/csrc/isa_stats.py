@@ -16,6 +16,16 @@ def loop_valu(asm: str, func_pat: str):
         raise SystemExit(f"function {func_pat} not found")
     body = asm[m.end(): asm.index("s_endpgm", m.end())]
     counts, in_loop = {"valu": 0, "salu": 0, "smem": 0, "vmem": 0}, False
+    # drop loop blocks that call the exact (rare) path: count the fast path
+    blocks, cur = [], []
+    for line in body.splitlines():
+        t = line.strip()
+        if (t.startswith(".LBB") or t.startswith("; %bb.")) and cur:
+            blocks.append(cur)
+            cur = []
+        cur.append(line)
+    blocks.append(cur)
+    body = "\n".join(l for b in blocks if not any("s_swappc" in x for x in b) for l in b)
     for line in body.splitlines():
         t = line.strip()
         if t.startswith(".LBB") or t.startswith("; %bb."):
@@ -40,8 +50,12 @@ def loop_valu(asm: str, func_pat: str):
 
 if __name__ == "__main__":
     asm = open(sys.argv[1]).read()
-    c = loop_valu(asm, r"_ZN5crane7k3_evalILi4ELi6ELb0EEEv\S*")
-    out = {"kernel": "k3_eval<4,6,false>", "valu_per_node_iter": c["valu"], "salu_per_node_iter": c["salu"],
-           "smem_per_node_iter": c["smem"], "vmem_per_node_iter": c["vmem"]}
+    out = {"kernel": "k3_eval<4,6,false,V>", "variants": {}}
+    for v, nodes in ((0, 1), (1, 1), (2, 2), (3, 1), (4, 1)):
+        c = loop_valu(asm, r"_ZN5crane7k3_evalILi4ELi6ELb0ELi%dEEEv\S*" % v)
+        out["variants"][str(v)] = {"valu_per_node": c["valu"] / nodes, "salu_per_node": c["salu"] / nodes,
+                                   "smem_per_node": c["smem"] / nodes, "vmem_per_node": c["vmem"] / nodes}
+    out["default_variant"] = 4  # kernels.hip k3_variant() default
+    out["valu_per_node_iter"] = out["variants"]["4"]["valu_per_node"]
     json.dump(out, open(sys.argv[2], "w"), indent=1)
     print(out)

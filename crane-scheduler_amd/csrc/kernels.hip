@@ -11,6 +11,8 @@
 // record is wave-uniform and arrives through scalar loads.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "dyn_types.hpp"
 #include "kernels.hpp"
 
@@ -38,24 +40,28 @@ __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {
 // table keyed by node (open addressing, CAS insert) before touching global
 // memory, so Zipf-hot nodes cost one global atomic per workgroup instead of
 // one per binding.
-constexpr int kHashSlots = 4096;  // per workgroup
-constexpr int kMaxProbe = 16;
-constexpr int kK2Threads = 1024;
+constexpr int kHashSlots = 8192;  // per workgroup: load factor <= 1/2 for its 4096 bindings
+constexpr int kMaxProbe = 32;
+constexpr int kK2Threads = 256;
 constexpr int kK2PerThread = 16;
 
 __global__ __launch_bounds__(kK2Threads) void k2_hot_count(const int32_t* __restrict__ bnode,
                                                             const int64_t* __restrict__ bts, int64_t B,
                                                             int64_t N, HotCutoffs cut, uint32_t* __restrict__ buckets) {
-    __shared__ int32_t hkey[kHashSlots];
-    __shared__ uint32_t hcnt[kHashSlots * kLdsWin];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = cut.n_win;
-    for (int i = threadIdx.x; i < kHashSlots; i += blockDim.x) hkey[i] = -1;
-    for (int i = threadIdx.x; i < kHashSlots * kLdsWin; i += blockDim.x) hcnt[i] = 0;
-    __syncthreads();
+    const bool lds = W <= kLdsWin;
+    int32_t* hkey = reinterpret_cast<int32_t*>(smem);
+    uint32_t* hcnt = reinterpret_cast<uint32_t*>(smem + sizeof(int32_t) * kHashSlots);  // [slot][W]
+    if (lds) {
+        for (int i = threadIdx.x; i < kHashSlots; i += kK2Threads) hkey[i] = -1;
+        for (int i = threadIdx.x; i < kHashSlots * W; i += kK2Threads) hcnt[i] = 0;
+        __syncthreads();
+    }
     const int64_t per_block = (int64_t)kK2Threads * kK2PerThread;
     const int64_t b0 = (int64_t)blockIdx.x * per_block;
     const int64_t b1 = min(B, b0 + per_block);
-    for (int64_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
+    for (int64_t b = b0 + threadIdx.x; b < b1; b += kK2Threads) {
         const int32_t nd = bnode[b];
         const int64_t ts = bts[b];
         if (nd < 0 || (int64_t)nd >= N) continue;  // binding.go:88 — matches no node of this shard
@@ -65,35 +71,33 @@ __global__ __launch_bounds__(kK2Threads) void k2_hot_count(const int32_t* __rest
             if (w < W) j += ts > cut.sorted[w] ? 1 : 0;
         if (j == 0) continue;
         const int bucket = j - 1;
-        if (W > kLdsWin) {  // wide policies: straight to global
-            atomicAdd(&buckets[(int64_t)bucket * N + nd], 1u);
-            continue;
-        }
-        uint32_t h = ((uint32_t)nd * 2654435761u) >> (32 - 12);
         bool done = false;
-        for (int p = 0; p < kMaxProbe && !done; ++p) {
-            const int32_t k = __hip_atomic_load(&hkey[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (k == nd) {
-                atomicAdd(&hcnt[h * kLdsWin + bucket], 1u);
-                done = true;
-            } else if (k == -1) {
-                const int32_t old = atomicCAS(&hkey[h], -1, nd);
-                if (old == -1 || old == nd) {
-                    atomicAdd(&hcnt[h * kLdsWin + bucket], 1u);
+        if (lds) {
+            uint32_t h = ((uint32_t)nd * 2654435761u) >> (32 - 13);
+            for (int p = 0; p < kMaxProbe && !done; ++p) {
+                const int32_t k = __hip_atomic_load(&hkey[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (k == nd) {
+                    atomicAdd(&hcnt[h * W + bucket], 1u);
                     done = true;
+                } else if (k == -1) {
+                    const int32_t old = atomicCAS(&hkey[h], -1, nd);
+                    if (old == -1 || old == nd) {
+                        atomicAdd(&hcnt[h * W + bucket], 1u);
+                        done = true;
+                    }
                 }
+                h = (h + 1) & (kHashSlots - 1);
             }
-            h = (h + 1) & (kHashSlots - 1);
         }
         if (!done) atomicAdd(&buckets[(int64_t)bucket * N + nd], 1u);
     }
+    if (!lds) return;
     __syncthreads();
-    if (W > kLdsWin) return;
-    for (int s = threadIdx.x; s < kHashSlots; s += blockDim.x) {
-        const int32_t nd = hkey[s];
+    for (int sl = threadIdx.x; sl < kHashSlots; sl += kK2Threads) {
+        const int32_t nd = hkey[sl];
         if (nd < 0) continue;
         for (int w = 0; w < W; ++w) {
-            const uint32_t c = hcnt[s * kLdsWin + w];
+            const uint32_t c = hcnt[sl * W + w];
             if (c) atomicAdd(&buckets[(int64_t)w * N + nd], c);
         }
     }
@@ -110,8 +114,9 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(DevPolicy pol, int64_
                                                            const int64_t* __restrict__ ts,
                                                            const double* __restrict__ hv,
                                                            const int64_t* __restrict__ hv_ts,
-                                                           const uint32_t* __restrict__ buckets, int64_t hv_ts_counts,
-                                                           NodeRec<PD, PR>* __restrict__ out) {
+                                                           uint32_t* __restrict__ buckets, int64_t hv_ts_counts,
+                                                           NodeRec<PD, PR>* __restrict__ out,
+                                                           uint32_t* __restrict__ cnt_out) {
     using Rec = NodeRec<PD, PR>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Rec* lrec = reinterpret_cast<Rec*>(smem);
@@ -153,10 +158,17 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(DevPolicy pol, int64_
         }
         if (buckets) {
             // annotateNodeHotValue (node.go:113-121): value += count / p.Count (Go int division)
+            // window w counts the bindings of buckets >= its cutoff rank (K2)
+            uint32_t bc[kMaxWin];
+            for (int b = 0; b < pol.n_win; ++b) {
+                bc[b] = buckets[(int64_t)b * N + n];
+                buckets[(int64_t)b * N + n] = 0;  // consumed: leaves the buckets zeroed for the next K2
+            }
             int64_t v = 0;
             for (int w = 0; w < pol.n_win; ++w) {
                 int64_t c = 0;
-                for (int b = pol.win_pos[w]; b < pol.n_win; ++b) c += buckets[(int64_t)b * N + n];
+                for (int b = pol.win_pos[w]; b < pol.n_win; ++b) c += bc[b];
+                if (cnt_out) cnt_out[(int64_t)w * N + n] = (uint32_t)c;
                 v += c / pol.win_count[w];
             }
             // the plugin re-reads it via ParseFloat (exact) and rejects negatives (stats.go:71-73)
@@ -172,6 +184,17 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(DevPolicy pol, int64_
             r.pen = 0;
             r.e_hv = kTsInvalid;
         }
+        int64_t e_fail = kTsInvalid;
+#pragma unroll
+        for (int k = 0; k < PD; ++k) e_fail = max(e_fail, r.e_pred[k]);
+        r.e_fail = e_fail;
+        bool slow = pol.noprio != 0;
+#pragma unroll
+        for (int k = 0; k < PR; ++k) slow |= !(__builtin_fabs(r.t[k]) < kTermMax);  // NaN/Inf/huge
+        const bool pen_fast = r.pen >= 0 && r.pen < (1LL << 30);
+        slow |= r.e_hv != kTsInvalid && !pen_fast;
+        r.pen32 = pen_fast ? (int32_t)r.pen : 0;
+        r.flags = slow ? kRecSlow : 0;
         lrec[threadIdx.x] = r;
     }
     __syncthreads();
@@ -184,64 +207,178 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(DevPolicy pol, int64_
 
 // ---------------------------------------------------------------- K3
 // blockIdx.x -> 256 pods (4 waves x 64), blockIdx.y -> a chunk of nodes.
-// Every lane walks the chunk's nodes in ascending order keeping the first
-// node with the highest score (lowest-index tie-break), then one 64-bit
-// atomicMax per pod merges chunks.  The NodeRec address depends only on the
-// loop counter, so it is wave-uniform and loaded with s_load into SGPRs.
+// Every lane walks the chunk's nodes in ascending order keeping a packed
+// 32-bit running key (score << 24 | ~local index) — max keeps the first node
+// with the highest score (lowest-index tie-break) — and one 64-bit atomicMax
+// per pod merges chunks.  The NodeRec address depends only on the loop
+// counter, so it is wave-uniform and arrives through s_load into SGPRs.
 constexpr int kK3Threads = 256;
 
-template <int PD, int PR, bool MATRIX>
-__global__ __launch_bounds__(kK3Threads) void k3_eval(const NodeRec<PD, PR>* __restrict__ rec, int64_t N,
-                                                      int64_t chunk, int64_t node_offset,
+// Exact reference semantics in 64-bit, for the rare lanes/nodes the fast
+// path cannot take (non-finite usage, |score| >= 2^30, huge or NaN hot value).
+template <int PD, int PR>
+__device__ __attribute__((noinline)) int32_t score_exact(int64_t tnow, const NodeRec<PD, PR>& r, double wsum,
+                                                         int32_t noprio) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < PR; ++k)
+        if (tnow < r.e_prio[k]) s += r.t[k];  // stats.go:124-133, policy order
+    const int64_t base = noprio ? 0 : go_int(s / wsum);  // stats.go:135
+    const int64_t pen = tnow < r.e_hv ? r.pen : 0;
+    int64_t f = (int64_t)((uint64_t)base - (uint64_t)pen);  // plugins.go:91, Go int64 wraps
+    return (int32_t)(f < 0 ? 0 : (f > 100 ? 100 : f));     // NormalizeScore (utils.go:58-68)
+}
+
+// A node record's fields as the loop consumes them (wave-uniform -> SGPRs).
+template <int PD, int PR>
+struct RecRegs {
+    int64_t e_fail, e_hv;
+    int32_t pen32, flags;
+    int64_t e_prio[PR];
+    double t[PR];
+};
+
+template <int PD, int PR>
+__device__ __forceinline__ RecRegs<PD, PR> load_rec(const NodeRec<PD, PR>& r) {
+    RecRegs<PD, PR> x;
+    x.e_fail = r.e_fail;
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+        x.e_prio[k] = r.e_prio[k];
+        x.t[k] = r.t[k];
+    }
+    x.e_hv = r.e_hv;
+    x.pen32 = r.pen32;
+    x.flags = r.flags;
+    return x;
+}
+
+// Filter + Score of one (pod, node) pair; returns the packed running key
+// (score << 24 | 0xFFFFFF - i), or -1 when the pod may not go to the node.
+template <int PD, int PR, bool DIVT = false>
+__device__ __forceinline__ int32_t eval_pair(int64_t tnow, bool ds, const RecRegs<PD, PR>& x,
+                                             const NodeRec<PD, PR>& r, int32_t i, double wsum, int32_t noprio,
+                                             int32_t* score_out, double inv_w = 0.0, const double* thr = nullptr) {
+    // Filter (plugins.go:55-66): some predicate fresh and over its limit
+    const bool fail = tnow < x.e_fail;
+    // getNodeScore (stats.go:124-135): fresh terms summed in policy order.
+    // fma(1.0, t, s) == s + t exactly; fma(0.0, t, s) == s for finite t
+    // (s is never -0.0), so a 0/1 mask replaces the select of the sum.
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+        const double m = tnow < x.e_prio[k] ? 1.0 : 0.0;
+        s = __builtin_fma(m, x.t[k], s);
+    }
+    int32_t base;
+    bool in_range;
+    if constexpr (DIVT) {
+        // trunc(RN(s/W)) from q0 = RN(s * RN(1/W)): within 1, fixed by the thresholds.
+        // For RN(s/W) < 1 this yields 0, which clamps to the same final score
+        // as the reference's (<= 0) base since the penalty is >= 0 here.
+        const double q0 = s * inv_w;
+        in_range = q0 < kQFast;  // false for NaN; negative q0 clamps to k0 = 0
+        int32_t k0;
+        asm("v_cvt_i32_f64 %0, %1" : "=v"(k0) : "v"(q0));
+        k0 = min(max(k0, 0), kQMax - 1);
+        base = k0 + (s >= thr[k0 + 1] ? 1 : 0) - (s < thr[k0] ? 1 : 0);
+    } else {
+        const double q = s / wsum;
+        in_range = __builtin_fabs(q) < kFastLim;  // false for NaN
+        // v_cvt_i32_f64 truncates (saturating; lanes out of range take the exact path below)
+        asm("v_cvt_i32_f64 %0, %1" : "=v"(base) : "v"(q));
+    }
+    // score - int(hotValue*10), NormalizeScore to [0,100] (plugins.go:91-93)
+    const int32_t pen = tnow < x.e_hv ? x.pen32 : 0;
+    int32_t f = min(max(base - pen, 0), 100);
+    if ((x.flags & kRecSlow) || !in_range) f = score_exact<PD, PR>(tnow, r, wsum, noprio);
+    if (score_out) *score_out = f;
+    const bool feasible = ds || !fail;
+    return feasible ? ((f << 24) | (0xFFFFFF - i)) : -1;
+}
+
+// V: 0 = plain loop, 1 = next record prefetched into SGPRs during the current
+// one, 2 = two nodes per iteration.
+template <int PD, int PR, bool MATRIX, int V>
+__global__ __launch_bounds__(kK3Threads) void k3_eval(const NodeRec<PD, PR>* __restrict__ rec, int32_t N,
+                                                      int32_t chunk, int64_t node_offset,
                                                       const int64_t* __restrict__ now, const uint8_t* __restrict__ flags,
                                                       int64_t P, double wsum, int32_t noprio,
-                                                      long long* __restrict__ keys, MatrixOut mo) {
-    const int64_t pod = (int64_t)blockIdx.x * kK3Threads + threadIdx.x;
+                                                      long long* __restrict__ keys, MatrixOut mo, double inv_w,
+                                                      const double* __restrict__ thr_g) {
+    // V4: V3 + division-free threshold quotient (thr_g has kQMax + 1 entries)
+    constexpr bool DIVT = V == 4;
+    __shared__ double thr[DIVT ? kQMax + 1 : 1];
+    if constexpr (DIVT) {
+        for (int k = threadIdx.x; k <= kQMax; k += kK3Threads) thr[k] = thr_g[k];
+        __syncthreads();
+    }
+    // V3: 1-D grid, XCD-aware.  Workgroups are dealt round-robin over the 8
+    // XCDs (b % 8 shares an XCD), so give every XCD its own 1/8 of the node
+    // chunks: each XCD's L2 then holds 1/8 of the record table.
+    int64_t pg, ch;
+    if constexpr (V == 3 || V == 4) {
+        const int64_t b = blockIdx.x, slot = b >> 3, pgs = (P + kK3Threads - 1) / kK3Threads;
+        pg = slot % pgs;
+        ch = (b & 7) + 8 * (slot / pgs);
+    } else {
+        pg = blockIdx.x;
+        ch = blockIdx.y;
+    }
+    const int64_t pod = pg * kK3Threads + threadIdx.x;
     const bool live = pod < P;
     const int64_t tnow = live ? now[pod] : INT64_MIN;
     const bool ds = live && flags && (flags[pod] & 1u);
-    const int64_t n0 = (int64_t)blockIdx.y * chunk;
-    const int64_t n1 = min(N, n0 + chunk);
-    int32_t best_s = -1;
-    int64_t best_n = 0;
-    for (int64_t n = n0; n < n1; ++n) {
-        const NodeRec<PD, PR>& r = rec[n];
-        // Filter (plugins.go:55-66): some predicate fresh and over its limit
-        bool fail = false;
-#pragma unroll
-        for (int k = 0; k < PD; ++k) fail |= tnow < r.e_pred[k];
-        // getNodeScore (stats.go:124-135): fresh terms summed in policy order
-        double s = 0.0;
-#pragma unroll
-        for (int k = 0; k < PR; ++k) {
-            const double a = s + r.t[k];
-            s = tnow < r.e_prio[k] ? a : s;
-        }
-        const int64_t base = noprio ? 0 : go_int(s / wsum);
-        // score - int(hotValue*10), NormalizeScore to [0,100] (plugins.go:91-93)
-        const int64_t pen = tnow < r.e_hv ? r.pen : 0;
-        int64_t f = (int64_t)((uint64_t)base - (uint64_t)pen);
-        f = f < 0 ? 0 : (f > 100 ? 100 : f);
-        const bool feasible = ds || !fail;
-        if (feasible && (int32_t)f > best_s) {
-            best_s = (int32_t)f;
-            best_n = n;
-        }
-        if constexpr (MATRIX) {
+    const int32_t n0 = (int32_t)min((int64_t)N, ch * chunk);
+    const int32_t cnt = min(N - n0, chunk);
+    const NodeRec<PD, PR>* __restrict__ r0 = rec + n0;
+    int32_t best = -1;
+    if constexpr (MATRIX) {
+        for (int32_t i = 0; i < cnt; ++i) {
+            const RecRegs<PD, PR> x = load_rec(r0[i]);
+            int32_t f;
+            best = max(best, eval_pair<PD, PR, DIVT>(tnow, ds, x, r0[i], i, wsum, noprio, &f, inv_w, thr));
             if (live) {
                 int8_t ff = -1;
                 if (!ds) {
 #pragma unroll
                     for (int k = PD - 1; k >= 0; --k)
-                        if (tnow < r.e_pred[k]) ff = mo.pred_orig[k];
+                        if (tnow < r0[i].e_pred[k]) ff = mo.pred_orig[k];
                 }
+                const int64_t n = n0 + i;
                 if (mo.first_fail) mo.first_fail[pod * N + n] = ff;
                 if (mo.score) mo.score[pod * N + n] = f;
             }
         }
+    } else if constexpr (V == 1) {
+        if (cnt > 0) {
+            RecRegs<PD, PR> cur = load_rec(r0[0]);
+            for (int32_t i = 0; i < cnt; ++i) {
+                const int32_t j = i + 1 < cnt ? i + 1 : i;
+                const RecRegs<PD, PR> nxt = load_rec(r0[j]);
+                best = max(best, eval_pair<PD, PR>(tnow, ds, cur, r0[i], i, wsum, noprio, nullptr));
+                cur = nxt;
+            }
+        }
+    } else if constexpr (V == 2) {
+        int32_t i = 0;
+        for (; i + 1 < cnt; i += 2) {
+            const RecRegs<PD, PR> a = load_rec(r0[i]);
+            const RecRegs<PD, PR> b = load_rec(r0[i + 1]);
+            const int32_t ka = eval_pair<PD, PR>(tnow, ds, a, r0[i], i, wsum, noprio, nullptr);
+            const int32_t kb = eval_pair<PD, PR>(tnow, ds, b, r0[i + 1], i + 1, wsum, noprio, nullptr);
+            best = max(best, max(ka, kb));
+        }
+        if (i < cnt) best = max(best, eval_pair<PD, PR>(tnow, ds, load_rec(r0[i]), r0[i], i, wsum, noprio, nullptr));
+    } else {
+        for (int32_t i = 0; i < cnt; ++i)
+            best = max(best, eval_pair<PD, PR, DIVT>(tnow, ds, load_rec(r0[i]), r0[i], i, wsum, noprio, nullptr,
+                                                     inv_w, thr));
     }
-    if (live && best_s >= 0) {
-        const long long key = ((long long)best_s << 32) | (long long)(0xFFFFFFFFull - (uint64_t)(node_offset + best_n));
+    if (live && best >= 0) {
+        const int64_t sc = best >> 24;
+        const int64_t n = n0 + (0xFFFFFF - (best & 0xFFFFFF));
+        const long long key = (long long)((sc << 32) | (int64_t)(0xFFFFFFFFull - (uint64_t)(node_offset + n)));
         atomicMax(&keys[pod], key);
     }
 }
@@ -249,23 +386,23 @@ __global__ __launch_bounds__(kK3Threads) void k3_eval(const NodeRec<PD, PR>* __r
 // ---------------------------------------------------------------- launchers
 template <int PD, int PR>
 static hipError_t launch_k1_t(const DevPolicy& pol, int64_t N, const double* val, const int64_t* ts, const double* hv,
-                              const int64_t* hv_ts, const uint32_t* buckets, int64_t hv_ts_counts, void* out,
-                              hipStream_t st) {
+                              const int64_t* hv_ts, uint32_t* buckets, int64_t hv_ts_counts, void* out,
+                              hipStream_t st, uint32_t* cnt_out) {
     if (N <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((N + kK1Threads - 1) / kK1Threads);
     const size_t lds = sizeof(NodeRec<PD, PR>) * kK1Threads;
     hipLaunchKernelGGL((k1_node_pass<PD, PR>), dim3(grid), dim3(kK1Threads), lds, st, pol, N, val, ts, hv, hv_ts,
-                       buckets, hv_ts_counts, static_cast<NodeRec<PD, PR>*>(out));
+                       buckets, hv_ts_counts, static_cast<NodeRec<PD, PR>*>(out), cnt_out);
     return hipGetLastError();
 }
 
 hipError_t launch_node_pass(int shape, const DevPolicy& pol, int64_t N, const double* val, const int64_t* ts,
-                            const double* hv, const int64_t* hv_ts, const uint32_t* buckets, int64_t hv_ts_counts,
-                            void* out, hipStream_t st) {
+                            const double* hv, const int64_t* hv_ts, uint32_t* buckets, int64_t hv_ts_counts,
+                            void* out, hipStream_t st, uint32_t* cnt_out) {
     switch (shape) {
-        case kShape4x6: return launch_k1_t<4, 6>(pol, N, val, ts, hv, hv_ts, buckets, hv_ts_counts, out, st);
-        case kShape8x8: return launch_k1_t<8, 8>(pol, N, val, ts, hv, hv_ts, buckets, hv_ts_counts, out, st);
-        default: return launch_k1_t<16, 16>(pol, N, val, ts, hv, hv_ts, buckets, hv_ts_counts, out, st);
+        case kShape4x6: return launch_k1_t<4, 6>(pol, N, val, ts, hv, hv_ts, buckets, hv_ts_counts, out, st, cnt_out);
+        case kShape8x8: return launch_k1_t<8, 8>(pol, N, val, ts, hv, hv_ts, buckets, hv_ts_counts, out, st, cnt_out);
+        default: return launch_k1_t<16, 16>(pol, N, val, ts, hv, hv_ts, buckets, hv_ts_counts, out, st, cnt_out);
     }
 }
 
@@ -282,43 +419,82 @@ hipError_t launch_hot_count(const int32_t* bnode, const int64_t* bts, int64_t B,
     if (B <= 0 || cut.n_win <= 0) return hipSuccess;
     const int64_t per_block = (int64_t)kK2Threads * kK2PerThread;
     const unsigned grid = (unsigned)((B + per_block - 1) / per_block);
-    hipLaunchKernelGGL(k2_hot_count, dim3(grid), dim3(kK2Threads), 0, st, bnode, bts, B, N, cut, buckets);
+    const size_t lds = cut.n_win <= kLdsWin ? (size_t)kHashSlots * (4 + 4 * cut.n_win) : 0;
+    static const hipError_t attr =
+        hipFuncSetAttribute((const void*)k2_hot_count, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(k2_hot_count, dim3(grid), dim3(kK2Threads), lds, st, bnode, bts, B, N, cut, buckets);
     return hipGetLastError();
 }
 
+// Tuning knobs read per launch (for A/B runs): CRANE_K3_VARIANT, CRANE_K3_ROUNDS.
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+int k3_variant() { return env_int("CRANE_K3_VARIANT", 4); }
+
 int64_t eval_chunk_nodes(int64_t P, int64_t N) {
-    // Enough workgroups to fill 256 CUs several times over, chunks of >= 64 nodes.
+    // Size the grid to whole residency rounds: 256 CUs x 8 blocks of 4 waves
+    // (8 waves/SIMD at <= 64 VGPRs) = 2048 resident blocks per round.
+    int rounds = env_int("CRANE_K3_ROUNDS", 16);
+    if (rounds < 1) rounds = 16;
     const int64_t pod_blocks = (P + kK3Threads - 1) / kK3Threads;
-    int64_t want_chunks = (4096 + pod_blocks - 1) / pod_blocks;
-    int64_t chunk = (N + want_chunks - 1) / want_chunks;
+    int64_t chunks = (2048LL * rounds) / pod_blocks;
+    if (chunks < 1) chunks = 1;
+    int64_t chunk = (N + chunks - 1) / chunks;
     if (chunk < 64) chunk = 64;
+    if (chunk > (1 << 24)) chunk = 1 << 24;  // the running key keeps 24 bits of local index
     return chunk;
 }
 
 template <int PD, int PR>
 static hipError_t launch_k3_t(const void* rec, int64_t N, int64_t node_offset, const int64_t* now,
                               const uint8_t* flags, int64_t P, double wsum, int32_t noprio, long long* keys,
-                              const MatrixOut& mo, hipStream_t st) {
+                              const MatrixOut& mo, double inv_w, const double* thr, hipStream_t st) {
     if (P <= 0 || N <= 0) return hipSuccess;
+    if (N > 0x7FFFFFFF) return hipErrorInvalidValue;
     const int64_t chunk = eval_chunk_nodes(P, N);
     const dim3 grid((unsigned)((P + kK3Threads - 1) / kK3Threads), (unsigned)((N + chunk - 1) / chunk));
     const auto* r = static_cast<const NodeRec<PD, PR>*>(rec);
-    if (mo.first_fail || mo.score)
-        hipLaunchKernelGGL((k3_eval<PD, PR, true>), grid, dim3(kK3Threads), 0, st, r, N, chunk, node_offset, now,
-                           flags, P, wsum, noprio, keys, mo);
-    else
-        hipLaunchKernelGGL((k3_eval<PD, PR, false>), grid, dim3(kK3Threads), 0, st, r, N, chunk, node_offset, now,
-                           flags, P, wsum, noprio, keys, mo);
+    const int32_t n32 = (int32_t)N, c32 = (int32_t)chunk;
+    const bool matrix = mo.first_fail || mo.score;
+    int v = k3_variant();
+    if (v == 4 && !thr) v = 3;  // no threshold table for this policy (weight sum <= 0 or no priorities)
+    if (matrix && (v == 1 || v == 2)) v = 0;
+    // V3/V4 use a 1-D XCD-swizzled grid with the chunk count padded to a multiple of 8
+    const unsigned chunks8 = (grid.y + 7) / 8 * 8;
+    const dim3 g1(grid.x * chunks8), blk(kK3Threads);
+#define K3_LAUNCH(M, V, G)                                                                                     \
+    hipLaunchKernelGGL((k3_eval<PD, PR, M, V>), G, blk, 0, st, r, n32, c32, node_offset, now, flags, P, wsum, \
+                       noprio, keys, mo, inv_w, thr)
+    if (matrix) {
+        if (v == 4) K3_LAUNCH(true, 4, g1);
+        else if (v == 3) K3_LAUNCH(true, 3, g1);
+        else K3_LAUNCH(true, 0, grid);
+    } else {
+        switch (v) {
+            case 1: K3_LAUNCH(false, 1, grid); break;
+            case 2: K3_LAUNCH(false, 2, grid); break;
+            case 3: K3_LAUNCH(false, 3, g1); break;
+            case 4: K3_LAUNCH(false, 4, g1); break;
+            default: K3_LAUNCH(false, 0, grid); break;
+        }
+    }
+#undef K3_LAUNCH
     return hipGetLastError();
 }
 
 hipError_t launch_eval(int shape, const void* rec, int64_t N, int64_t node_offset, const int64_t* now,
                        const uint8_t* flags, int64_t P, double wsum, int32_t noprio, long long* keys,
-                       const MatrixOut& mo, hipStream_t st) {
+                       const MatrixOut& mo, double inv_w, const double* thr, hipStream_t st) {
     switch (shape) {
-        case kShape4x6: return launch_k3_t<4, 6>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, mo, st);
-        case kShape8x8: return launch_k3_t<8, 8>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, mo, st);
-        default: return launch_k3_t<16, 16>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, mo, st);
+        case kShape4x6:
+            return launch_k3_t<4, 6>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, mo, inv_w, thr, st);
+        case kShape8x8:
+            return launch_k3_t<8, 8>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, mo, inv_w, thr, st);
+        default:
+            return launch_k3_t<16, 16>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, mo, inv_w, thr, st);
     }
 }
 

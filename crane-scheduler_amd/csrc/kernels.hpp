@@ -22,16 +22,33 @@ struct MatrixOut {
     int8_t pred_orig[kMaxPred];  // device predicate -> policy predicate index
 };
 
+// Sequential greedy (greedy.hip)
+constexpr int64_t kGreedyMaxNodes = 64LL * 64 * 64 * 64;
+constexpr size_t kGreedyLdsBytes = 160 * 1024;
+struct GreedyArgs {
+    int64_t now;       // batch time, ns
+    double wsum;
+    int32_t noprio;
+    int32_t n_win;
+    int64_t win_count[kMaxWin];
+    int32_t win_inc[kMaxWin];  // a binding stamped now_unix falls in window w
+};
+hipError_t launch_greedy(int shape, const void* rec, int64_t N, uint32_t* cnt, const GreedyArgs& a, int64_t* base,
+                         uint8_t* leaf, int64_t P, const uint8_t* flags, int64_t* chosen, hipStream_t st);
+
 size_t node_rec_bytes(int shape);
 int64_t eval_chunk_nodes(int64_t P, int64_t N);
 
 hipError_t launch_hot_count(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N, const HotCutoffs& cut,
                             uint32_t* buckets, hipStream_t st);
+// K1 zeroes the buckets it consumes (so the next K2 needs no memset); with
+// cnt_out it also stores the per-window counts [W][N].
 hipError_t launch_node_pass(int shape, const DevPolicy& pol, int64_t N, const double* val, const int64_t* ts,
-                            const double* hv, const int64_t* hv_ts, const uint32_t* buckets, int64_t hv_ts_counts,
-                            void* out, hipStream_t st);
+                            const double* hv, const int64_t* hv_ts, uint32_t* buckets, int64_t hv_ts_counts,
+                            void* out, hipStream_t st, uint32_t* cnt_out = nullptr);
+// thr: device table of kQMax + 1 quotient thresholds (null = divide); inv_w = RN(1/wsum)
 hipError_t launch_eval(int shape, const void* rec, int64_t N, int64_t node_offset, const int64_t* now,
                        const uint8_t* flags, int64_t P, double wsum, int32_t noprio, long long* keys,
-                       const MatrixOut& mo, hipStream_t st);
+                       const MatrixOut& mo, double inv_w, const double* thr, hipStream_t st);
 
 }  // namespace crane

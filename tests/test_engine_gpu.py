@@ -11,6 +11,15 @@ from helpers import SH, engine_for, oracle_soa
 
 pytestmark = pytest.mark.gpu
 
+# K3 variants (kernels.hip): 0 plain, 1 prefetch, 2 unroll-2, 3 XCD swizzle, 4 swizzle + division-free quotient
+VARIANTS = ["0", "1", "2", "3", "4"]
+
+
+@pytest.fixture(params=VARIANTS)
+def k3_variant(request, monkeypatch):
+    monkeypatch.setenv("CRANE_K3_VARIANT", request.param)
+    return request.param
+
 cd = pytest.importorskip("crane_dyn")
 from crane_dyn import synth  # noqa: E402
 from oracle import oracle as O  # noqa: E402
@@ -45,7 +54,7 @@ def test_golden_cluster(cluster_small):
 
 
 @pytest.mark.parametrize("n_nodes,n_pods,seed", [(1, 1, 1), (100, 1, 2), (257, 33, 3), (5000, 64, 4), (3000, 700, 5)])
-def test_random_vs_oracle(n_nodes, n_pods, seed):
+def test_random_vs_oracle(n_nodes, n_pods, seed, k3_variant):
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, n_nodes, n_pods, seed=seed, pod_step_ns=1_700_000_000)
     eng = engine_for(spec, c)
@@ -60,7 +69,7 @@ def test_random_vs_oracle(n_nodes, n_pods, seed):
         assert cs[p] == (osc[p][feas].max() if feas.any() else -1)
 
 
-def test_keys_only_matches_matrix():
+def test_keys_only_matches_matrix(k3_variant):
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 20000, 300, seed=11, pod_step_ns=3_000_000_000)
     eng = engine_for(spec, c)
@@ -87,7 +96,7 @@ def test_no_hot_value_and_empty_shard():
     assert (ch == -1).all() and (cs == -1).all()
 
 
-def test_policy_variants():
+def test_policy_variants(k3_variant):
     """Non-default policy shapes exercise the 8x8 and 16x16 NodeRec kernels and skipped entries."""
     m = 60 * 10**9
     base = cd.default_policy_spec()
@@ -151,7 +160,7 @@ def test_hot_values_random(n_nodes, n_bind, seed):
     assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch, och)
 
 
-def test_division_exactness_sweep():
+def test_division_exactness_sweep(k3_variant):
     """Dense random usages: int(score/weight) must match the CPU bit for bit (KAT-3/4 FMA traps)."""
     spec = cd.default_policy_spec()
     rng = np.random.default_rng(5)
@@ -164,5 +173,33 @@ def test_division_exactness_sweep():
     c.hv_ts[:] = synth.TS_INVALID
     eng = engine_for(spec, c)
     _, sc, _, _ = eng.eval(c.now, c.ds, matrix=True)
-    _, osc, _ = oracle_soa(spec, c)
+    off, osc, och = oracle_soa(spec, c)
     assert np.array_equal(sc, osc)
+    _, _, ch, cs = eng.eval(c.now, c.ds)
+    assert ch[0] == och[0] and cs[0] == osc[0][(off[0] < 0) | bool(c.ds[0])].max()
+
+
+def test_quotient_threshold_adversarial(k3_variant):
+    """Single-priority policies whose score/weight lands exactly on, and one ulp around, integers."""
+    m = 60 * 10**9
+    rng = np.random.default_rng(17)
+    for w in (0.3, 1.7, 2.0, 0.1, 3.0):
+        spec = {"syncPolicy": [("a", 3 * m), ("b", 3 * m)], "predicate": [],
+                "priority": [("a", w), ("b", w / 3.0)], "hotValue": [(5 * m, 5)]}
+        N = 4096
+        c = synth.make_cluster(spec, N, 1, seed=int(w * 100), invalid=False)
+        # usages u with (1-u)*w*100 near integer multiples of the weight sum
+        k = rng.integers(0, 140, N)
+        base = 1.0 - k / 100.0
+        ulps = rng.integers(-3, 4, N)
+        u = np.array([np.nextafter(b, np.inf if d > 0 else -np.inf) if d else b for b, d in zip(base, ulps)])
+        for _ in range(2):
+            u = np.where(ulps > 1, np.nextafter(u, np.inf), np.where(ulps < -1, np.nextafter(u, -np.inf), u))
+        c.val[0] = np.abs(u)
+        c.val[1] = np.abs(rng.choice([0.0, 0.5, 1.0, 1.5], N))
+        c.ts[:] = synth.NOW0_NS
+        c.hv_ts[:] = synth.TS_INVALID
+        eng = engine_for(spec, c)
+        _, sc, _, _ = eng.eval(c.now, c.ds, matrix=True)
+        _, osc, _ = oracle_soa(spec, c)
+        assert np.array_equal(sc, osc), w
