@@ -1,0 +1,67 @@
+"""Node sharding across GPUs: one engine per rank, one int64 MAX all-reduce per pod batch.
+
+Each rank owns a contiguous node range [lo, hi) (uploaded with node_offset=lo,
+so keys carry GLOBAL node indices).  A per-pod key packs (score, node):
+    key = (score << 32) | (0xFFFFFFFF - global_node),   -1 = no feasible node
+so max(key) is the highest score with the lowest global node index — the
+same tie-break on every shard layout.  torch.distributed with the "nccl"
+backend is RCCL on ROCm (xGMI); "gloo" runs the same protocol on CPU.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+NO_NODE = -1
+
+
+def shard_range(n_nodes: int, world: int, rank: int):
+    """Contiguous, balanced node range of `rank` (first n % world ranks get one extra)."""
+    q, r = divmod(n_nodes, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def pack_keys(chosen_global, chosen_score):
+    """Host-side packing identical to the device's (engine crane_dyn_eval_keys_async)."""
+    ch = np.asarray(chosen_global, np.int64)
+    sc = np.asarray(chosen_score, np.int64)
+    keys = (sc << 32) | (np.int64(0xFFFFFFFF) - ch)
+    return np.where(ch < 0, np.int64(NO_NODE), keys)
+
+
+def unpack_keys(keys):
+    k = np.asarray(keys, np.int64)
+    node = np.where(k < 0, -1, np.int64(0xFFFFFFFF) - (k & 0xFFFFFFFF))
+    score = np.where(k < 0, -1, k >> 32)
+    return node, score
+
+
+def allreduce_keys(keys, group=None):
+    """MAX all-reduce of a torch int64 tensor of per-pod keys, in place (RCCL / gloo)."""
+    import torch.distributed as dist
+
+    dist.all_reduce(keys, op=dist.ReduceOp.MAX, group=group)
+    return keys
+
+
+class ShardedEngine:
+    """One rank's shard: an Engine holding nodes [lo, hi) of a cluster, plus the combine step."""
+
+    def __init__(self, policy, n_nodes_total, world, rank, device=0):
+        from crane_dyn import Engine
+
+        self.lo, self.hi = shard_range(n_nodes_total, world, rank)
+        self.engine = Engine(policy, device)
+
+    def upload(self, val, ts, hv=None, hv_ts=None, b_node=None, b_ts=None):
+        """Full-cluster SoA in; this rank keeps its slice (bindings re-indexed locally)."""
+        lo, hi = self.lo, self.hi
+        self.engine.upload_nodes(val[:, lo:hi], ts[:, lo:hi], None if hv is None else hv[lo:hi],
+                                 None if hv_ts is None else hv_ts[lo:hi], node_offset=lo)
+        if b_node is not None:
+            m = (b_node >= lo) & (b_node < hi)
+            self.engine.upload_bindings((b_node[m] - lo).astype(np.int32), b_ts[m])
+
+    def schedule(self, d_now, d_flags, d_keys, stream=None, group=None):
+        self.engine.eval_keys_async(d_now, d_flags, d_keys, stream)
+        return allreduce_keys(d_keys, group)
