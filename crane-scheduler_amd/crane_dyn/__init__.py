@@ -35,6 +35,14 @@ class _CPolicy(C.Structure):
 
 
 def _load():
+    # PyTorch-ROCm bundles its own libamdhip64.so with the same SONAME
+    # (libamdhip64.so.7).  Loading torch first makes this library bind to that
+    # same HIP runtime, so device pointers and streams are shared; loading it
+    # first would put two HIP runtimes in the process.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"crane_dyn: HIP library not built ({LIB_PATH}); run make -C crane-scheduler_amd/csrc")
     L = C.CDLL(LIB_PATH)

@@ -36,7 +36,12 @@ __device__ __forceinline__ int32_t final_score(int64_t base, int64_t pen) {
 // hot value of a node from its per-window counts (node.go:113-121)
 __device__ __forceinline__ int64_t pen_of(const uint32_t* cnt, int64_t N, int64_t n, const GreedyArgs& a) {
     int64_t v = 0;
-    for (int w = 0; w < a.n_win; ++w) v += (int64_t)cnt[(int64_t)w * N + n] / a.win_count[w];
+    for (int w = 0; w < a.n_win; ++w) {
+        const uint32_t c = cnt[(int64_t)w * N + n];
+        const int64_t k = a.win_count[w];
+        // Go int division truncates toward zero; 32-bit unsigned division when it is the same thing
+        v += (k > 0 && k <= 0xFFFFFFFFll) ? (int64_t)(c / (uint32_t)k) : (int64_t)c / k;
+    }
     if (v < 0) return 0;  // a negative annotation is rejected (stats.go:71-73) -> hot value 0
     return go_int_g((double)v * 10.0);
 }
@@ -81,9 +86,16 @@ __device__ __forceinline__ int wave_argmax7(int v, int* lane_out) {
     return m;
 }
 
-__device__ __forceinline__ int wave_max7(int v) {
-    int l;
-    return wave_argmax7(v, &l);
+// wave max via DPP: row_shr 1,2,4,8 then row_bcast15/31 (GFX9 family) -> lane 63.
+// Out-of-range source lanes return `old` = v itself, the identity of max.
+__device__ __forceinline__ int wave_max_dpp(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xF, 0xF, false));  // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x112, 0xF, 0xF, false));  // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x114, 0xF, 0xF, false));  // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x118, 0xF, 0xF, false));  // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
 constexpr int kGreedyLevels = 4;  // 64^4 = 16.7M nodes
@@ -148,45 +160,52 @@ __global__ __launch_bounds__(256) void greedy_run(int64_t N, uint8_t* __restrict
         __syncthreads();
     }
     if (wave != 0) return;
-    const int64_t now_unix_ok = 1;
-    (void)now_unix_ok;
+    const int top = t.nlev;
     for (int64_t p0 = 0; p0 < P; p0 += 64) {
         const int64_t pl = p0 + lane;
-        const bool dsl = pl < P && flags && (flags[pl] & 1u);
+        // DaemonSet pods bypass Filter (plugins.go:41-43): one bit per pod of this chunk
+        const uint64_t dsmask = ballot64(pl < P && flags && (flags[pl] & 1u));
         int64_t out = -1;
         const int np = (int)min((int64_t)64, P - p0);
         for (int q = 0; q < np; ++q) {
-            const bool any = __shfl(dsl ? 1 : 0, q) != 0;  // DaemonSet: Filter bypass (plugins.go:41-43)
+            const bool any = (dsmask >> q) & 1;
             // ---- descent: root level (<= 64 entries), then one ballot per level
-            const int top = t.nlev;
-            int v = lane < t.size[top] ? ent_val(t.lvl[top][lane], any) : -1;
-            int ln;
-            const int M = wave_argmax7(v, &ln);
+            const int v = lane < t.size[top] ? ent_val(t.lvl[top][lane], any) : -1;
+            const int M = wave_max_dpp(v);
             int64_t idx = -1;
             if (M >= 0) {
-                idx = ln;
+                idx = __builtin_ctzll(ballot64(v == M));
                 for (int l = top - 1; l >= 0; --l) {
                     const int64_t c = idx * 64 + lane;
                     int w = -1;
                     if (c < t.size[l]) w = l == 0 ? leaf_val(leaf[c], any) : ent_val(t.lvl[l][c], any);
-                    const uint64_t hit = ballot64(w == M);
-                    idx = idx * 64 + __builtin_ctzll(hit);
+                    idx = idx * 64 + __builtin_ctzll(ballot64(w == M));
                 }
             }
             if (lane == q) out = idx;
             if (idx < 0) continue;
             // ---- commit: Binding{Node: idx, Timestamp: now_unix}
             if (lane == 0) {
-                for (int w = 0; w < a.n_win; ++w)
-                    if (a.win_inc[w]) cnt[(int64_t)w * N + idx] += 1;
-                const int64_t pen = pen_of(cnt, N, idx, a);
+                // one round trip: counts and base load together, counts stored back
+                uint32_t c[kMaxWin];
+                for (int w = 0; w < a.n_win; ++w) c[w] = cnt[(int64_t)w * N + idx];
+                const int64_t b = base[idx];
+                int64_t v = 0;
+                for (int w = 0; w < a.n_win; ++w) {
+                    c[w] += a.win_inc[w] ? 1u : 0u;
+                    cnt[(int64_t)w * N + idx] = c[w];
+                    const int64_t k = a.win_count[w];
+                    v += (k > 0 && k <= 0xFFFFFFFFll) ? (int64_t)(c[w] / (uint32_t)k) : (int64_t)c[w] / k;
+                }
+                const int64_t pen = v < 0 ? 0 : go_int_g((double)v * 10.0);  // node.go:117, plugins.go:91
                 const uint8_t old = leaf[idx];
-                leaf[idx] = (uint8_t)(final_score(base[idx], pen) | (old & 0x80));
+                leaf[idx] = (uint8_t)(final_score(b, pen) | (old & 0x80));
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            // LDS instructions of one wave execute in order, so lane 0's leaf store
+            // is seen by the reads below; a global leaf store is waited for.
+            if (!leaves_in_lds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            // ---- re-reduce the ancestors of idx
+            // ---- re-reduce the ancestors of idx; stop once an entry is unchanged
             int64_t child = idx;
             for (int l = 1; l <= t.nlev; ++l) {
                 const int64_t e = child / 64, c = e * 64 + lane;
@@ -200,11 +219,13 @@ __global__ __launch_bounds__(256) void greedy_run(int64_t N, uint8_t* __restrict
                         vf = ent_val(t.lvl[l - 1][c], false);
                     }
                 }
-                const int ma = wave_max7(va), mf = wave_max7(vf);
-                if (lane == 0) t.lvl[l][e] = (uint16_t)(max(ma, 0) | ((mf + 1) << 8));
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                const int ma = wave_max_dpp(va), mf = wave_max_dpp(vf);
+                const uint16_t ne = (uint16_t)(max(ma, 0) | ((mf + 1) << 8));
+                const uint16_t oe = t.lvl[l][e];
+                if (ne == oe) break;
                 __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                if (lane == 0) t.lvl[l][e] = ne;
+                __builtin_amdgcn_wave_barrier();
                 child = e;
             }
         }

@@ -15,7 +15,7 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
-    config.addinivalue_line("markers", "slow: full-size parity runs")
+    config.addinivalue_line("markers", "slow: full-size parity runs (GPU)")
 
 
 def load_golden(name):
