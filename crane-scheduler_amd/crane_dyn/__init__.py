@@ -54,6 +54,7 @@ def _load():
         "crane_policy_free": (None, [vp]),
         "crane_tz_offset": (C.c_int, [C.c_char_p, P(C.c_int64)]),
         "crane_parse_annotation": (None, [C.c_char_p, C.c_size_t, C.c_int64, P(C.c_double), P(C.c_int64)]),
+        "crane_parse_annotations": (C.c_int, [C.c_int64, vp, vp, C.c_int64, vp, vp, C.c_int32]),
         "crane_dyn_create": (C.c_int, [P(_CPolicy), C.c_int32, P(vp)]),
         "crane_dyn_destroy": (C.c_int, [vp]),
         "crane_dyn_last_error": (C.c_char_p, [vp]),
@@ -82,7 +83,7 @@ lib = _load()
 # The symbols include/crane_dyn.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
     "crane_policy_load_file", "crane_policy_load_bytes", "crane_policy_view", "crane_policy_free",
-    "crane_tz_offset", "crane_parse_annotation", "crane_dyn_create", "crane_dyn_destroy", "crane_dyn_last_error",
+    "crane_tz_offset", "crane_parse_annotation", "crane_parse_annotations", "crane_dyn_create", "crane_dyn_destroy", "crane_dyn_last_error",
     "crane_dyn_num_metrics", "crane_dyn_metric_name", "crane_dyn_upload_nodes", "crane_dyn_upload_bindings",
     "crane_dyn_refresh_hot_values", "crane_dyn_eval", "crane_dyn_eval_keys_async",
     "crane_dyn_refresh_hot_values_async", "crane_dyn_node_pass_async", "crane_dyn_greedy", "crane_dyn_key_node",
@@ -182,22 +183,23 @@ def parse_annotation(s: str, tz_offset_s: int):
     return v.value, t.value
 
 
-def parse_nodes(metric_names, nodes, tz_offset_s):
-    """Node annotation dicts -> SoA (val[M][N], ts[M][N], hv[N], hv_ts[N])."""
+def parse_nodes(metric_names, nodes, tz_offset_s, threads=0):
+    """Node annotation dicts -> SoA (val[M][N], ts[M][N], hv[N], hv_ts[N]) in one bulk parse."""
     M, N = len(metric_names), len(nodes)
-    val = np.zeros((M, N))
-    ts = np.full((M, N), CRANE_TS_INVALID, np.int64)
-    hv = np.zeros(N)
-    hv_ts = np.full(N, CRANE_TS_INVALID, np.int64)
-    for n, a in enumerate(nodes):
-        for m, name in enumerate(metric_names):
-            s = a.get(name)
-            if s is not None:
-                val[m, n], ts[m, n] = parse_annotation(s, tz_offset_s)
-        s = a.get("node_hot_value")
-        if s is not None:
-            hv[n], hv_ts[n] = parse_annotation(s, tz_offset_s)
-    return val, ts, hv, hv_ts
+    keys = list(metric_names) + ["node_hot_value"]
+    raw = [a.get(k) for k in keys for a in nodes]  # row-major [M+1][N]
+    enc = [None if x is None else x.encode() for x in raw]
+    strs = (C.c_char_p * max(1, len(enc)))(*enc)
+    lens = np.array([0 if x is None else len(x) for x in enc], dtype=np.uint64)
+    val = np.zeros(len(enc))
+    ts = np.empty(len(enc), np.int64)
+    rc = lib.crane_parse_annotations(len(enc), C.cast(strs, C.c_void_p), _ptr(lens), tz_offset_s, _ptr(val), _ptr(ts),
+                                     threads)
+    if rc:
+        raise CraneError(rc, "bulk annotation parse")
+    val = val.reshape(M + 1, N)
+    ts = ts.reshape(M + 1, N)
+    return val[:M].copy(), ts[:M].copy(), val[M].copy(), ts[M].copy()
 
 
 def key_node(key: int):

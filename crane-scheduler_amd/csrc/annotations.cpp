@@ -15,8 +15,11 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/crane_dyn.h"
 
@@ -115,14 +118,20 @@ bool crane_go_parse_float(const char* s, size_t n, double* out) {
     }
     if (unders && !underscores_ok(s, i)) return false;
     if (i != n) return false;  // trailing bytes
-    std::string buf;
-    buf.reserve(n);
+    char small[64];
+    std::string big;
+    char* buf = small;
+    if (n >= sizeof small) {
+        big.resize(n + 1);
+        buf = &big[0];
+    }
+    size_t m = 0;
     for (size_t j = 0; j < n; ++j)
-        if (s[j] != '_') buf.push_back(s[j]);
+        if (s[j] != '_') buf[m++] = s[j];
+    buf[m] = 0;
     char* end = nullptr;
-    errno = 0;
-    const double v = std::strtod(buf.c_str(), &end);  // correctly rounded, like Go
-    if (end != buf.c_str() + buf.size()) return false;
+    const double v = std::strtod(buf, &end);  // correctly rounded, like Go
+    if (end != buf + m) return false;
     if (std::isinf(v)) return false;  // ErrRange on overflow; underflow is not an error in Go
     *out = v;
     return true;
@@ -258,6 +267,32 @@ void crane_parse_annotation(const char* s, size_t n, int64_t tz_offset_s, double
     if (!crane_go_parse_float(s, comma, &v)) return;
     *value = v;
     *ts_ns = ts;
+}
+
+int crane_parse_annotations(int64_t n, const char* const* strs, const size_t* lens, int64_t tz_offset_s,
+                            double* value, int64_t* ts_ns, int32_t n_threads) {
+    if (n < 0 || (n > 0 && (!strs || !lens || !value || !ts_ns))) return CRANE_E_INVALID;
+    int64_t nt = n_threads > 0 ? n_threads : (int64_t)std::thread::hardware_concurrency();
+    if (nt < 1) nt = 1;
+    nt = std::min<int64_t>(nt, std::max<int64_t>(1, n / 4096));  // >= 4096 strings per thread
+    auto work = [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i) {
+            if (!strs[i]) {
+                value[i] = 0;
+                ts_ns[i] = CRANE_TS_INVALID;  // key not found (stats.go:52-55)
+            } else {
+                crane_parse_annotation(strs[i], lens[i], tz_offset_s, &value[i], &ts_ns[i]);
+            }
+        }
+    };
+    if (nt == 1) {
+        work(0, n);
+        return CRANE_OK;
+    }
+    std::vector<std::thread> th;
+    for (int64_t t = 0; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+    for (auto& x : th) x.join();
+    return CRANE_OK;
 }
 
 }  // extern "C"

@@ -112,6 +112,7 @@ __device__ __forceinline__ int leaf_val(uint8_t b, bool any) {
 }
 __device__ __forceinline__ int ent_val(uint16_t e, bool any) { return any ? (int)(e & 0xFF) : (int)(e >> 8) - 1; }
 
+template <int NLEV>
 __global__ __launch_bounds__(256) void greedy_run(int64_t N, uint8_t* __restrict__ leaf_g, const int64_t* __restrict__ base,
                                                   uint32_t* __restrict__ cnt, GreedyArgs a, int64_t P,
                                                   const uint8_t* __restrict__ flags, int64_t* __restrict__ chosen,
@@ -119,26 +120,39 @@ __global__ __launch_bounds__(256) void greedy_run(int64_t N, uint8_t* __restrict
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // layout: [leaves (if in LDS)] [level 1] [level 2] ...
+    // Every index into t.size / t.lvl below is a compile-time constant (loops
+    // over levels are fully unrolled), so the metadata stays in registers.
     Tree t;
     t.size[0] = N;
-    t.nlev = 0;
-    int64_t off = leaves_in_lds ? (N + 15) / 16 * 16 : 0;
+    t.nlev = NLEV;
     {
-        int64_t sz = N;
-        do {
+        int64_t off = leaves_in_lds ? (N + 15) / 16 * 16 : 0, sz = N;
+#pragma unroll
+        for (int l = 1; l <= NLEV; ++l) {
             sz = (sz + 63) / 64;
-            t.nlev++;
-            t.size[t.nlev] = sz;
-            t.lvl[t.nlev] = reinterpret_cast<uint16_t*>(smem + off);
+            t.size[l] = sz;
+            t.lvl[l] = reinterpret_cast<uint16_t*>(smem + off);
             off += (sz * 2 + 15) / 16 * 16;
-        } while (sz > 64 && t.nlev < kGreedyLevels);
+        }
     }
     uint8_t* leaf = leaves_in_lds ? smem : leaf_g;
     if (leaves_in_lds)
         for (int64_t i = threadIdx.x; i < N; i += blockDim.x) leaf[i] = leaf_g[i];
+    // Warm this XCD's L2 with the per-node state the commits touch (base, counts):
+    // most placements hit a node for the first time, which would otherwise be an
+    // HBM-latency miss on the serial path.  The xor keeps the loads live.
+    {
+        uint64_t x = 0;
+        for (int64_t i = threadIdx.x; i < N; i += blockDim.x) {
+            x ^= (uint64_t)base[i];
+            for (int w = 0; w < a.n_win; ++w) x ^= cnt[(int64_t)w * N + i];
+        }
+        if (x == 0x9E3779B97F4A7C15ull && P < 0) chosen[0] = (int64_t)x;  // never true: keeps the loads
+    }
     __syncthreads();
     // build level 1 from leaves, then each level from the one below
-    for (int l = 1; l <= t.nlev; ++l) {
+#pragma unroll
+    for (int l = 1; l <= NLEV; ++l) {
         for (int64_t e = threadIdx.x; e < t.size[l]; e += blockDim.x) {
             int ma = 0, mf = -1;
             for (int j = 0; j < 64; ++j) {
@@ -160,7 +174,7 @@ __global__ __launch_bounds__(256) void greedy_run(int64_t N, uint8_t* __restrict
         __syncthreads();
     }
     if (wave != 0) return;
-    const int top = t.nlev;
+    constexpr int top = NLEV;
     for (int64_t p0 = 0; p0 < P; p0 += 64) {
         const int64_t pl = p0 + lane;
         // DaemonSet pods bypass Filter (plugins.go:41-43): one bit per pod of this chunk
@@ -175,6 +189,7 @@ __global__ __launch_bounds__(256) void greedy_run(int64_t N, uint8_t* __restrict
             int64_t idx = -1;
             if (M >= 0) {
                 idx = __builtin_ctzll(ballot64(v == M));
+#pragma unroll
                 for (int l = top - 1; l >= 0; --l) {
                     const int64_t c = idx * 64 + lane;
                     int w = -1;
@@ -188,10 +203,14 @@ __global__ __launch_bounds__(256) void greedy_run(int64_t N, uint8_t* __restrict
             if (lane == 0) {
                 // one round trip: counts and base load together, counts stored back
                 uint32_t c[kMaxWin];
-                for (int w = 0; w < a.n_win; ++w) c[w] = cnt[(int64_t)w * N + idx];
+#pragma unroll
+                for (int w = 0; w < kMaxWin; ++w)
+                    if (w < a.n_win) c[w] = cnt[(int64_t)w * N + idx];
                 const int64_t b = base[idx];
                 int64_t v = 0;
-                for (int w = 0; w < a.n_win; ++w) {
+#pragma unroll
+                for (int w = 0; w < kMaxWin; ++w) {
+                    if (w >= a.n_win) break;
                     c[w] += a.win_inc[w] ? 1u : 0u;
                     cnt[(int64_t)w * N + idx] = c[w];
                     const int64_t k = a.win_count[w];
@@ -207,7 +226,8 @@ __global__ __launch_bounds__(256) void greedy_run(int64_t N, uint8_t* __restrict
             __builtin_amdgcn_wave_barrier();
             // ---- re-reduce the ancestors of idx; stop once an entry is unchanged
             int64_t child = idx;
-            for (int l = 1; l <= t.nlev; ++l) {
+#pragma unroll
+            for (int l = 1; l <= NLEV; ++l) {
                 const int64_t e = child / 64, c = e * 64 + lane;
                 int va = -1, vf = -1;
                 if (c < t.size[l - 1]) {
@@ -259,11 +279,26 @@ static hipError_t launch_greedy_t(const void* rec, int64_t N, uint32_t* cnt, con
     }
     const bool in_lds = greedy_lds_bytes(N, true) <= kGreedyLdsBytes;
     const size_t lds = greedy_lds_bytes(N, in_lds);
-    static const hipError_t attr =
-        hipFuncSetAttribute((const void*)greedy_run, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(greedy_run, dim3(1), dim3(256), lds, st, N, leaf, base, cnt, a, P, flags, chosen,
-                       (int32_t)in_lds);
+    int nlev = 0;
+    for (int64_t sz = N; nlev == 0 || sz > 64;) {
+        sz = (sz + 63) / 64;
+        ++nlev;
+    }
+#define GREEDY_LAUNCH(L)                                                                                        \
+    do {                                                                                                        \
+        static const hipError_t attr = hipFuncSetAttribute((const void*)greedy_run<L>,                          \
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+        if (attr != hipSuccess) return attr;                                                                    \
+        hipLaunchKernelGGL(greedy_run<L>, dim3(1), dim3(256), lds, st, N, leaf, base, cnt, a, P, flags, chosen, \
+                           (int32_t)in_lds);                                                                    \
+    } while (0)
+    switch (nlev) {
+        case 1: GREEDY_LAUNCH(1); break;
+        case 2: GREEDY_LAUNCH(2); break;
+        case 3: GREEDY_LAUNCH(3); break;
+        default: GREEDY_LAUNCH(4); break;
+    }
+#undef GREEDY_LAUNCH
     return hipGetLastError();
 }
 

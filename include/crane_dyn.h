@@ -82,6 +82,12 @@ void crane_policy_free(crane_policy_doc *doc);
  * parsed — the engine rejects them like stats.go:71-73. */
 int crane_tz_offset(const char *tz_name, int64_t *offset_s); /* "" or NULL = $TZ, default Asia/Shanghai */
 void crane_parse_annotation(const char *s, size_t n, int64_t tz_offset_s, double *value, int64_t *ts_ns);
+/* Bulk form for a whole snapshot: strs[i] (NULL = key missing) of length
+ * lens[i] -> value[i], ts_ns[i]; n_threads host threads (<= 0: hardware
+ * concurrency).  This is the once-per-sync parse that replaces the
+ * reference's per-call parsing (stats.go:51-76). */
+int crane_parse_annotations(int64_t n, const char *const *strs, const size_t *lens, int64_t tz_offset_s,
+                            double *value, int64_t *ts_ns, int32_t n_threads);
 
 /* ------------------------------------------------------------------ engine */
 typedef struct crane_dyn crane_dyn;

@@ -69,3 +69,19 @@ def test_engine_rejects_bad_policy():
     spec["hotValue"] = [(60 * 10**9, 0)]
     with pytest.raises(cd.CraneError, match="count"):
         cd.Engine(cd.Policy(spec))
+
+
+def test_bulk_parse_matches_single(cluster_small):
+    nodes = cluster_small["nodes"] * 50  # > 4096 strings: threaded path
+    names = ["cpu_usage_avg_5m", "cpu_usage_max_avg_1h", "cpu_usage_max_avg_1d", "mem_usage_avg_5m",
+             "mem_usage_max_avg_1h", "mem_usage_max_avg_1d"]
+    val, ts, hv, hv_ts = cd.parse_nodes(names, nodes, 8 * 3600)
+    for n in range(0, len(nodes), 37):
+        for m, k in enumerate(names):
+            if k in nodes[n]:
+                v1, t1 = cd.parse_annotation(nodes[n][k], 8 * 3600)
+                assert t1 == ts[m, n] and (v1 == val[m, n] or (v1 != v1 and val[m, n] != val[m, n]))
+            else:
+                assert ts[m, n] == cd.CRANE_TS_INVALID
+        if "node_hot_value" in nodes[n]:
+            assert (hv[n], hv_ts[n]) == cd.parse_annotation(nodes[n]["node_hot_value"], 8 * 3600)
