@@ -66,6 +66,8 @@ def main():
         N = N // 8
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, N, P, n_bindings=B, seed=20250215 + args.config * 1000 + rank)
+    # the pod batch is the same on every shard (only nodes and bindings are per rank)
+    c.now, c.ds = synth.make_pods(P, seed=20250215 + args.config)
     eng = cd.Engine(cd.Policy(spec), local)
     val, ts, _ = c.rows(eng.metric_names)
     eng.upload_nodes(val, ts, c.hv, c.hv_ts, node_offset=rank * N)

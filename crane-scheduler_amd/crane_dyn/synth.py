@@ -63,6 +63,7 @@ class Cluster:
         c.hv, c.hv_ts = self.hv[lo:hi], self.hv_ts[lo:hi]
         m = (self.b_node >= lo) & (self.b_node < hi)
         c.b_node, c.b_ts = (self.b_node[m] - lo).astype(np.int32), self.b_ts[m]
+        c._raw_ts_s = self._raw_ts_s[:, lo:hi]
         return c
 
     def annotations(self, lo=0, hi=None, tz_offset_s=SHANGHAI):
@@ -91,6 +92,13 @@ class Cluster:
 
 def _fmt(unix_s, off):
     return (_dt.datetime(1970, 1, 1) + _dt.timedelta(seconds=int(unix_s) + off)).strftime("%Y-%m-%dT%H:%M:%SZ")
+
+
+def make_pods(n_pods, seed, now0=NOW0, ds_frac=0.01, pod_step_ns=1_000_000):
+    """A pod batch independent of the node shard: now_p = now0 + p*step, DaemonSet flags."""
+    rng = np.random.default_rng(seed)
+    now = now0 * 10**9 + np.arange(n_pods, dtype=np.int64) * pod_step_ns
+    return now, (rng.random(n_pods) < ds_frac).astype(np.uint8)
 
 
 def make_cluster(policy_spec, n_nodes, n_pods, n_bindings=0, seed=20250215, now0=NOW0, invalid=True, ds_frac=0.01,

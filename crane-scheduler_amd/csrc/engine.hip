@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -97,6 +98,7 @@ struct crane_dyn {
     DevBuf<long long> keys;
     DevBuf<int8_t> ff;
     DevBuf<int64_t> score;
+    DevBuf<uint32_t> k2_cnt, k2_tot, k2_sorted;  // bin-partitioned K2 scratch
     DevBuf<uint32_t> gcnt;  // greedy: per-window counts [W][N]
     DevBuf<int64_t> gbase, gchosen;
     DevBuf<uint8_t> gleaf, gflags;
@@ -255,6 +257,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->val.release(); h->hv.release(); h->ts.release(); h->hv_ts.release(); h->rec.release();
     h->buckets.release(); h->bnode.release(); h->bts.release(); h->now.release(); h->flags.release();
     h->keys.release(); h->ff.release(); h->score.release(); h->thr.release();
+    h->k2_cnt.release(); h->k2_tot.release(); h->k2_sorted.release();
     h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -345,7 +348,17 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     if (nb > h->buckets.n) h->buckets_zero = false;
     HIPTRY(h, h->buckets.reserve(nb));
     if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
-    HIPTRY(h, launch_hot_count(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, st));
+    const HotBins g = hot_bins_geometry(h->B, h->N, dp.n_win);
+    const char* k2e = getenv("CRANE_K2");
+    if (g.ok && !(k2e && std::strcmp(k2e, "hash") == 0)) {
+        HIPTRY(h, h->k2_cnt.reserve((size_t)g.nbins * (size_t)g.nchunks));
+        HIPTRY(h, h->k2_tot.reserve((size_t)g.nbins));
+        HIPTRY(h, h->k2_sorted.reserve((size_t)h->B));
+        HIPTRY(h, launch_hot_count_binned(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, g, h->k2_cnt.p,
+                                          h->k2_tot.p, h->k2_sorted.p, st));
+    } else {
+        HIPTRY(h, launch_hot_count(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, st));
+    }
     h->buckets_zero = false;
     h->hv_from_counts = true;
     h->hv_ts_counts = hv_ts_ns;

@@ -107,9 +107,8 @@ __global__ __launch_bounds__(kK2Threads) void k2_hot_count(const int32_t* __rest
 // One thread per node.  Reads the parsed SoA (and K2 buckets), writes the
 // node's NodeRec into LDS, then the workgroup streams its records out with
 // 16-byte coalesced stores.
-constexpr int kK1Threads = 128;
-
-template <int PD, int PR>
+// block size: 128 by default, CRANE_K1_THREADS=256 selects the wide variant
+template <int PD, int PR, int kK1Threads>
 __global__ __launch_bounds__(kK1Threads) void k1_node_pass(DevPolicy pol, int64_t N, const double* __restrict__ val,
                                                            const int64_t* __restrict__ ts,
                                                            const double* __restrict__ hv,
@@ -389,10 +388,16 @@ static hipError_t launch_k1_t(const DevPolicy& pol, int64_t N, const double* val
                               const int64_t* hv_ts, uint32_t* buckets, int64_t hv_ts_counts, void* out,
                               hipStream_t st, uint32_t* cnt_out) {
     if (N <= 0) return hipSuccess;
-    const unsigned grid = (unsigned)((N + kK1Threads - 1) / kK1Threads);
-    const size_t lds = sizeof(NodeRec<PD, PR>) * kK1Threads;
-    hipLaunchKernelGGL((k1_node_pass<PD, PR>), dim3(grid), dim3(kK1Threads), lds, st, pol, N, val, ts, hv, hv_ts,
-                       buckets, hv_ts_counts, static_cast<NodeRec<PD, PR>*>(out), cnt_out);
+    const char* e = getenv("CRANE_K1_THREADS");
+    const int T = e && atoi(e) == 256 ? 256 : 128;
+    const unsigned grid = (unsigned)((N + T - 1) / T);
+    const size_t lds = sizeof(NodeRec<PD, PR>) * T;
+    if (T == 256)
+        hipLaunchKernelGGL((k1_node_pass<PD, PR, 256>), dim3(grid), dim3(256), lds, st, pol, N, val, ts, hv, hv_ts,
+                           buckets, hv_ts_counts, static_cast<NodeRec<PD, PR>*>(out), cnt_out);
+    else
+        hipLaunchKernelGGL((k1_node_pass<PD, PR, 128>), dim3(grid), dim3(128), lds, st, pol, N, val, ts, hv, hv_ts,
+                           buckets, hv_ts_counts, static_cast<NodeRec<PD, PR>*>(out), cnt_out);
     return hipGetLastError();
 }
 

@@ -36,6 +36,20 @@ struct GreedyArgs {
 hipError_t launch_greedy(int shape, const void* rec, int64_t N, uint32_t* cnt, const GreedyArgs& a, int64_t* base,
                          uint8_t* leaf, int64_t P, const uint8_t* flags, int64_t* chosen, hipStream_t st);
 
+// Bin-partitioned K2 (hotcount.hip)
+constexpr int kMaxBins = 4096;
+struct HotBins {
+    int32_t bb;       // log2(nodes per bin)
+    int32_t nbins, nchunks, splits;
+    int64_t chunk;    // bindings per chunk workgroup
+    bool ok;          // per-bin histogram fits LDS
+};
+HotBins hot_bins_geometry(int64_t B, int64_t N, int32_t W);
+// scratch: chunk_cnt [nbins * nchunks], bin_tot [nbins], sorted [B]
+hipError_t launch_hot_count_binned(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
+                                   const HotCutoffs& cut, uint32_t* buckets, const HotBins& g, uint32_t* chunk_cnt,
+                                   uint32_t* bin_tot, uint32_t* sorted, hipStream_t st);
+
 size_t node_rec_bytes(int shape);
 int64_t eval_chunk_nodes(int64_t P, int64_t N);
 

@@ -142,8 +142,11 @@ def test_hot_values_vs_oracle(kats):
     assert sc[0, 0] == 50  # hv = 5 (SURVEY KAT-11)
 
 
-@pytest.mark.parametrize("n_nodes,n_bind,seed", [(1000, 50_000, 1), (20_000, 300_000, 2), (100, 10, 3)])
-def test_hot_values_random(n_nodes, n_bind, seed):
+@pytest.mark.parametrize("k2", ["binned", "hash"])
+@pytest.mark.parametrize("n_nodes,n_bind,seed", [(1000, 50_000, 1), (20_000, 300_000, 2), (100, 10, 3),
+                                                 (70_000, 2_000_000, 4)])
+def test_hot_values_random(n_nodes, n_bind, seed, k2, monkeypatch):
+    monkeypatch.setenv("CRANE_K2", k2)
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, n_nodes, 16, n_bindings=n_bind, seed=seed, pod_step_ns=10_000_000_000)
     # include bindings for nodes outside the shard
