@@ -102,6 +102,9 @@ struct crane_dyn {
     DevBuf<uint32_t> gcnt;  // greedy: per-window counts [W][N]
     DevBuf<int64_t> gbase, gchosen;
     DevBuf<uint8_t> gleaf, gflags;
+    DevBuf<int32_t> sperm, sflat, svcnt;  // K3 step path scratch (step.hip)
+    DevBuf<int64_t> stile;
+    DevBuf<unsigned char> svrec;
     DevBuf<double> thr;  // quotient thresholds (K3 division-free path), empty if unusable
     double inv_w = 0.0;
 
@@ -259,6 +262,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->keys.release(); h->ff.release(); h->score.release(); h->thr.release();
     h->k2_cnt.release(); h->k2_tot.release(); h->k2_sorted.release();
     h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
+    h->sperm.release(); h->sflat.release(); h->svcnt.release(); h->stile.release(); h->svrec.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -382,6 +386,20 @@ static int eval_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint
     if (h->rec_dirty) {
         int rc = node_pass_locked(h, st);
         if (rc) return rc;
+    }
+    const bool matrix = d_ff || d_score;
+    if (!matrix && k3_variant() == 5 && h->N < kStepMaxNodes && P < (1LL << 31)) {
+        // step path: K3p (pod partition + key init) -> K3a (node step tables) -> K3s (pairs)
+        const StepGeometry g = step_geometry(P, h->N);
+        HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
+        HIPTRY(h, h->stile.reserve((size_t)(2 * g.ntiles)));
+        HIPTRY(h, h->sflat.reserve((size_t)(2 * g.npad)));
+        HIPTRY(h, h->svcnt.reserve((size_t)(2 * g.nseg)));
+        HIPTRY(h, h->svrec.reserve((size_t)(2 * g.npad) * step_vrec_bytes(h->shape)));
+        StepTables stt{h->sflat.p, h->svcnt.p, h->svrec.p, g.npad, g.nseg};
+        HIPTRY(h, launch_eval_step(h->shape, h->rec.p, h->N, h->node_offset, d_now, d_flags, P, h->dp.wsum,
+                                   h->dp.noprio, d_keys, stt, g, h->sperm.p, h->stile.p, st));
+        return CRANE_OK;
     }
     HIPTRY(h, hipMemsetAsync(d_keys, 0xFF, sizeof(long long) * (size_t)P, st));
     MatrixOut mo{};

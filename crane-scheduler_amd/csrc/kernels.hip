@@ -437,7 +437,7 @@ static int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
     return e && *e ? atoi(e) : dflt;
 }
-int k3_variant() { return env_int("CRANE_K3_VARIANT", 4); }
+int k3_variant() { return env_int("CRANE_K3_VARIANT", 5); }
 
 int64_t eval_chunk_nodes(int64_t P, int64_t N) {
     // Size the grid to whole residency rounds: 256 CUs x 8 blocks of 4 waves
@@ -465,6 +465,7 @@ static hipError_t launch_k3_t(const void* rec, int64_t N, int64_t node_offset, c
     const int32_t n32 = (int32_t)N, c32 = (int32_t)chunk;
     const bool matrix = mo.first_fail || mo.score;
     int v = k3_variant();
+    if (v == 5) v = 4;  // the step path (step.hip) serves keys-only launches; matrix output uses V4
     if (v == 4 && !thr) v = 3;  // no threshold table for this policy (weight sum <= 0 or no priorities)
     if (matrix && (v == 1 || v == 2)) v = 0;
     // V3/V4 use a 1-D XCD-swizzled grid with the chunk count padded to a multiple of 8

@@ -50,6 +50,36 @@ hipError_t launch_hot_count_binned(const int32_t* bnode, const int64_t* bts, int
                                    const HotCutoffs& cut, uint32_t* buckets, const HotBins& g, uint32_t* chunk_cnt,
                                    uint32_t* bin_tot, uint32_t* sorted, hipStream_t st);
 
+// K3 step path (step.hip): per-batch node step tables + pair eval.
+constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
+constexpr int64_t kStepMaxNodes = 1LL << 24;  // packed key keeps 24 bits of node index
+// A node whose key changes inside the batch: cnt ascending expiries in
+// (tmin, tmax]; key[j] holds for bp[j-1] <= now < bp[j] (bp[-1] = -inf).
+template <int NB>
+struct VRec {
+    int64_t bp[NB];
+    int32_t key[NB + 1];
+    int32_t cnt;
+};
+struct StepTables {
+    int32_t* flat;  // [2][npad] key of a node constant over the batch, -1 if stepped/infeasible
+    int32_t* vcnt;  // [2][nseg] stepped nodes per segment
+    void* vrec;     // [2][npad] VRec<NB>, segment s's list at s * kStepSeg
+    int64_t npad, nseg;
+};
+struct StepGeometry {
+    int64_t nseg, npad, ntiles, ptiles;
+    int32_t segs_per_chunk, nchunks;
+};
+size_t step_vrec_bytes(int shape);
+StepGeometry step_geometry(int64_t P, int64_t N);
+// perm [ntiles * 1024], tile_mm [2 * ntiles]; also initialises keys[0..P) to -1
+hipError_t launch_eval_step(int shape, const void* rec, int64_t N, int64_t node_offset, const int64_t* now,
+                            const uint8_t* flags, int64_t P, double wsum, int32_t noprio, long long* keys,
+                            const StepTables& st, const StepGeometry& g, int32_t* perm, int64_t* tile_mm,
+                            hipStream_t s);
+int k3_variant();
+
 size_t node_rec_bytes(int shape);
 int64_t eval_chunk_nodes(int64_t P, int64_t N);
 

@@ -11,8 +11,9 @@ from helpers import SH, engine_for, oracle_soa
 
 pytestmark = pytest.mark.gpu
 
-# K3 variants (kernels.hip): 0 plain, 1 prefetch, 2 unroll-2, 3 XCD swizzle, 4 swizzle + division-free quotient
-VARIANTS = ["0", "1", "2", "3", "4"]
+# K3 variants (kernels.hip): 0 plain, 1 prefetch, 2 unroll-2, 3 XCD swizzle, 4 swizzle + division-free quotient,
+# 5 step path (step.hip) for keys-only launches (matrix launches use 4)
+VARIANTS = ["0", "1", "2", "3", "4", "5"]
 
 
 @pytest.fixture(params=VARIANTS)

@@ -1,0 +1,119 @@
+"""Parity of the K3 step path (crane-scheduler_amd/csrc/step.hip) with the oracle.
+
+The step path serves keys-only evaluation (chosen node + chosen score per pod):
+K3p partitions pods by DaemonSet flag, K3a folds every node into a step function
+of `now` over the batch's time range, K3s evaluates every (pod, node) pair.
+These cases aim at its seams: pod times exactly on node expiries (stats.go:42-48
+now.Before(ts + dur) is strict), unsorted and duplicated pod times, DaemonSet
+mixes that make waves uniform, mixed and all-DaemonSet, segment / tile / chunk
+edges (N and P not multiples of 256 / 64 / 1024), and the 8x8 / 16x16 record
+shapes.  Reference: plugins.go:39-98 (Filter, Score), utils.go:17-24.
+"""
+import numpy as np
+import pytest
+
+from helpers import engine_for, oracle_soa
+
+pytestmark = pytest.mark.gpu
+
+cd = pytest.importorskip("crane_dyn")
+from crane_dyn import synth  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def _step_variant(monkeypatch):
+    monkeypatch.setenv("CRANE_K3_VARIANT", "5")
+
+
+def _check(spec, c, now, ds):
+    eng = engine_for(spec, c)
+    _, _, ch, cs = eng.eval(now, ds)
+    off, osc, och = oracle_soa(spec, c, now=now, ds=ds)
+    assert np.array_equal(ch, och)
+    for p in range(len(now)):
+        ok = (off[p] < 0) | bool(ds[p])
+        assert cs[p] == (osc[p][ok].max() if ok.any() else -1), p
+    eng.close()
+
+
+@pytest.mark.parametrize("n_nodes,n_pods,step_ns,ds_frac,seed", [
+    (1, 1, 0, 0.0, 1),
+    (255, 63, 1_000_000, 0.01, 2),
+    (257, 65, 1_000_000_000, 0.5, 3),
+    (4099, 1025, 1_000_000, 0.01, 4),
+    (3000, 700, 1_700_000_000, 0.05, 5),   # 20-minute batch: almost every node steps
+    (20000, 2100, 0, 0.01, 6),             # one `now` for the whole batch: every node flat
+    (1000, 300, 60_000_000_000, 1.0, 7),   # all DaemonSet pods
+])
+def test_step_random_vs_oracle(n_nodes, n_pods, step_ns, ds_frac, seed):
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, n_nodes, n_pods, seed=seed, pod_step_ns=step_ns, ds_frac=ds_frac)
+    _check(spec, c, c.now, c.ds)
+
+
+def test_step_pod_times_on_expiries():
+    """Pods placed exactly on, and 1 ns either side of, node expiries (ts + period + 5m)."""
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 2000, 1, seed=21)
+    rng = np.random.default_rng(3)
+    dur = {n: p + 300 * 10**9 for n, p in spec["syncPolicy"]}
+    exp = []
+    for m, name in enumerate(c.metric_names):
+        ok = c.ok[m] == 1
+        exp.append(c.ts[m][ok] + dur[name])
+    exp.append(c.hv_ts[c.hv_ts != synth.TS_INVALID] + 300 * 10**9)  # hot value: no extra 5m (stats.go:152-166)
+    exp = np.concatenate(exp)
+    pick = rng.choice(exp, 1500)
+    now = np.concatenate([pick, pick - 1, pick + 1]).astype(np.int64)
+    rng.shuffle(now)
+    ds = (rng.random(len(now)) < 0.02).astype(np.uint8)
+    _check(spec, c, now, ds)
+
+
+def test_step_unsorted_duplicate_times():
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 5000, 1, seed=22)
+    rng = np.random.default_rng(4)
+    base = synth.NOW0_NS + rng.integers(-600, 600, 300) * 10**9
+    now = np.repeat(base, 4).astype(np.int64)
+    rng.shuffle(now)
+    ds = (rng.random(len(now)) < 0.3).astype(np.uint8)
+    _check(spec, c, now, ds)
+
+
+def test_step_policy_shapes():
+    """8x8 and 16x16 records, skipped entries, no priorities, weight sum 0 (NaN/Inf scores)."""
+    m = 60 * 10**9
+    base = cd.default_policy_spec()
+    specs = []
+    s = dict(base)
+    s["predicate"] = base["predicate"] + [("cpu_usage_max_avg_1d", 0.5), ("mem_usage_max_avg_1d", 0.0),
+                                          ("not_synced", 0.1), ("mem_usage_avg_5m", 0.3)]
+    specs.append(s)
+    s = dict(base)
+    s["syncPolicy"] = base["syncPolicy"] + [("m%d" % i, (i + 1) * m) for i in range(10)] + [("zero", 0), ("neg5", -5 * m)]
+    s["priority"] = base["priority"] + [("m%d" % i, 0.1 * (i + 1)) for i in range(10)] + [("zero", 1.0), ("neg5", 2.0)]
+    s["predicate"] = [("m%d" % i, 0.4 + 0.05 * i) for i in range(10)] + [("neg5", 0.5)]
+    specs.append(s)
+    s = dict(base)
+    s["priority"] = []
+    specs.append(s)
+    s = dict(base)
+    s["priority"] = [("cpu_usage_avg_5m", 1.0), ("mem_usage_avg_5m", -1.0)]
+    specs.append(s)
+    for i, spec in enumerate(specs):
+        c = synth.make_cluster(spec, 777, 90, seed=200 + i, pod_step_ns=20_000_000_000, ds_frac=0.1)
+        _check(spec, c, c.now, c.ds)
+
+
+def test_step_matches_v4_keys():
+    """Same device-resident keys from the step path and the V4 pair kernel."""
+    import os
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 30000, 3000, seed=23, pod_step_ns=5_000_000)
+    eng = engine_for(spec, c)
+    _, _, ch5, cs5 = eng.eval(c.now, c.ds)
+    os.environ["CRANE_K3_VARIANT"] = "4"
+    _, _, ch4, cs4 = eng.eval(c.now, c.ds)
+    os.environ["CRANE_K3_VARIANT"] = "5"
+    assert np.array_equal(ch5, ch4) and np.array_equal(cs5, cs4)
