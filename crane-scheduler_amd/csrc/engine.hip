@@ -102,9 +102,11 @@ struct crane_dyn {
     DevBuf<uint32_t> gcnt;  // greedy: per-window counts [W][N]
     DevBuf<int64_t> gbase, gchosen;
     DevBuf<uint8_t> gleaf, gflags;
-    DevBuf<int32_t> sperm, sflat, svcnt;  // K3 step path scratch (step.hip)
+    DevBuf<int32_t> sperm, svcnt;
+    DevBuf<int16_t> sflat;  // K3 step path scratch (step.hip)
     DevBuf<int64_t> stile;
     DevBuf<unsigned char> svrec;
+    DevBuf<Step1> sstep1;
     DevBuf<double> thr;  // quotient thresholds (K3 division-free path), empty if unusable
     double inv_w = 0.0;
 
@@ -262,7 +264,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->keys.release(); h->ff.release(); h->score.release(); h->thr.release();
     h->k2_cnt.release(); h->k2_tot.release(); h->k2_sorted.release();
     h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
-    h->sperm.release(); h->sflat.release(); h->svcnt.release(); h->stile.release(); h->svrec.release();
+    h->sperm.release(); h->sflat.release(); h->svcnt.release(); h->stile.release(); h->svrec.release(); h->sstep1.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -394,9 +396,10 @@ static int eval_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint
         HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
         HIPTRY(h, h->stile.reserve((size_t)(2 * g.ntiles)));
         HIPTRY(h, h->sflat.reserve((size_t)(2 * g.npad)));
-        HIPTRY(h, h->svcnt.reserve((size_t)(2 * g.nseg)));
+        HIPTRY(h, h->svcnt.reserve((size_t)(4 * g.nseg)));
+        HIPTRY(h, h->sstep1.reserve((size_t)(2 * g.npad)));
         HIPTRY(h, h->svrec.reserve((size_t)(2 * g.npad) * step_vrec_bytes(h->shape)));
-        StepTables stt{h->sflat.p, h->svcnt.p, h->svrec.p, g.npad, g.nseg};
+        StepTables stt{h->sflat.p, h->svcnt.p, h->sstep1.p, h->svrec.p, g.npad, g.nseg};
         HIPTRY(h, launch_eval_step(h->shape, h->rec.p, h->N, h->node_offset, d_now, d_flags, P, h->dp.wsum,
                                    h->dp.noprio, d_keys, stt, g, h->sperm.p, h->stile.p, st));
         return CRANE_OK;

@@ -53,8 +53,13 @@ hipError_t launch_hot_count_binned(const int32_t* bnode, const int64_t* bts, int
 // K3 step path (step.hip): per-batch node step tables + pair eval.
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
 constexpr int64_t kStepMaxNodes = 1LL << 24;  // packed key keeps 24 bits of node index
-// A node whose key changes inside the batch: cnt ascending expiries in
-// (tmin, tmax]; key[j] holds for bp[j-1] <= now < bp[j] (bp[-1] = -inf).
+// A node whose key changes once inside the batch: key k0 for now < bp, k1 after.
+struct alignas(16) Step1 {
+    int64_t bp;
+    int32_t k0, k1;
+};
+// A node whose key changes more than once: cnt ascending expiries in
+// (tmin, tmax], padded with INT64_MAX; key[j] holds for bp[j-1] <= now < bp[j].
 template <int NB>
 struct VRec {
     int64_t bp[NB];
@@ -62,9 +67,10 @@ struct VRec {
     int32_t cnt;
 };
 struct StepTables {
-    int32_t* flat;  // [2][npad] key of a node constant over the batch, -1 if stepped/infeasible
-    int32_t* vcnt;  // [2][nseg] stepped nodes per segment
-    void* vrec;     // [2][npad] VRec<NB>, segment s's list at s * kStepSeg
+    int16_t* flat;   // [2][npad] (score << 8 | 255 - local) of a node constant over the batch, -1 if stepped/infeasible
+    int32_t* cnt;    // [2][nseg][2] per segment: Step1 count (padded to x8), VRec count
+    Step1* single;   // [2][npad]  segment s's Step1 list at s * kStepSeg
+    void* multi;     // [2][npad]  VRec<NB>, segment s's list at s * kStepSeg
     int64_t npad, nseg;
 };
 struct StepGeometry {

@@ -8,10 +8,10 @@
 // times lie in [tmin, tmax], only expiries b with tmin < b <= tmax can split
 // the batch, so the node's packed (feasible, score, index) key is a step
 // function of `now` with at most PR + 2 steps.  K3a evaluates that function
-// once per step with the literal int64 restatement (score_exact), at a
-// representative time inside the step; K3s then evaluates every (pod, node)
-// pair by selecting its step: one int32 max for a node with no step inside the
-// batch (most nodes), a 64-bit compare + select per step otherwise.
+// once per step with the literal int64 restatement (score_at), at the first
+// instant of the step; K3s then evaluates every (pod, node) pair by selecting
+// its step: one int32 max for a node with no step inside the batch (most
+// nodes), a 64-bit compare + select per step otherwise.
 //
 //   K3p  pods  : DaemonSet partition per 1024-pod tile (so waves are uniform),
 //                key init, per-tile min/max of now
@@ -33,11 +33,11 @@ namespace crane {
 // same packing as K3: (score << 24) | (0xFFFFFF - node), -1 = pod may not go there
 __device__ __forceinline__ int32_t pack_key(int32_t f, int64_t n) { return (f << 24) | (int32_t)(0xFFFFFF - n); }
 
-// Exact Filter + Score key of (pod at time t, node n) — the same semantics as
-// K3's eval_pair (kernels.hip), through the literal int64 path.
+// Exact clamped Score of (pod at time t, node) — the literal int64 restatement
+// of stats.go:114-138 + plugins.go:91-93, the semantics of K3's eval_pair and
+// score_exact (kernels.hip).
 template <int PD, int PR>
-__device__ __attribute__((noinline)) int32_t key_at(int64_t t, bool ds, const NodeRec<PD, PR>& r, int64_t n,
-                                                    double wsum, int32_t noprio) {
+__device__ __forceinline__ int32_t score_at(int64_t t, const NodeRec<PD, PR>& r, double wsum, int32_t noprio) {
     double s = 0.0;
 #pragma unroll
     for (int k = 0; k < PR; ++k)
@@ -49,9 +49,13 @@ __device__ __attribute__((noinline)) int32_t key_at(int64_t t, bool ds, const No
     }
     const int64_t pen = t < r.e_hv ? r.pen : 0;
     const int64_t f = (int64_t)((uint64_t)base - (uint64_t)pen);  // plugins.go:91, wraps like Go
-    const int32_t fc = (int32_t)(f < 0 ? 0 : (f > 100 ? 100 : f));  // NormalizeScore (utils.go:58-68)
-    const bool feasible = ds || !(t < r.e_fail);                     // plugins.go:41-43, 55-66
-    return feasible ? pack_key(fc, n) : -1;
+    return (int32_t)(f < 0 ? 0 : (f > 100 ? 100 : f));            // NormalizeScore (utils.go:58-68)
+}
+
+// Filter (plugins.go:41-43, 55-66) + packed key for pod kind T (0: Filter applies, 1: DaemonSet)
+template <int PD, int PR>
+__device__ __forceinline__ int32_t key_of(int T, int64_t t, int32_t score, const NodeRec<PD, PR>& r, int64_t n) {
+    return (T == 1 || !(t < r.e_fail)) ? pack_key(score, n) : -1;
 }
 
 // ---------------------------------------------------------------- K3p
@@ -109,6 +113,11 @@ __global__ __launch_bounds__(kPodTile) void k3p_pods(const int64_t* __restrict__
 }
 
 // ---------------------------------------------------------------- K3a
+// One workgroup per 256-node segment, one thread per node.  Most nodes have no
+// expiry inside the batch and only store their flat key; the rest append a
+// Step1 (one step) or VRec (more) record to the segment's list for each pod
+// kind, and the Step1 lists are padded to a multiple of 8 with records that
+// never win, so K3s reads them eight at a time.
 template <int PD, int PR>
 __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __restrict__ rec, int64_t N,
                                                       const int64_t* __restrict__ tile_mm, int32_t ntiles,
@@ -116,7 +125,7 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
     constexpr int NB = PR + 2;
     using VR = VRec<NB>;
     __shared__ int64_t smn[kStepSeg / 64], smx[kStepSeg / 64];
-    __shared__ int32_t vc[2];
+    __shared__ int32_t lc[2][2];
     // batch time range [tmin, tmax] from K3p's tile partials
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     for (int i = threadIdx.x; i < ntiles; i += kStepSeg) {
@@ -132,95 +141,169 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
         smn[threadIdx.x >> 6] = mn;
         smx[threadIdx.x >> 6] = mx;
     }
-    if (threadIdx.x < 2) vc[threadIdx.x] = 0;
+    if (threadIdx.x < 4) lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
     __syncthreads();
     int64_t tmin = smn[0], tmax = smx[0];
+#pragma unroll
     for (int i = 1; i < kStepSeg / 64; ++i) {
         tmin = min(tmin, smn[i]);
         tmax = max(tmax, smx[i]);
     }
     const int64_t seg = blockIdx.x;
     const int64_t n = seg * kStepSeg + threadIdx.x;
-    int32_t key0[2] = {-1, -1}, cnt[2] = {0, 0};
-    int64_t bp[2][NB];
-    int32_t kk[2][NB];
+    auto in_range = [&](int64_t e) { return e > tmin && e <= tmax; };
+    int32_t flat[2] = {-1, -1};
     if (n < N) {
         const NodeRec<PD, PR> r = rec[n];
+        const int32_t s0 = score_at<PD, PR>(tmin, r, wsum, noprio);
+        int m = in_range(r.e_hv);
 #pragma unroll
-        for (int T = 0; T < 2; ++T) {
-            // expiries inside (tmin, tmax], ascending (out-of-range -> INT64_MAX, sorted
-            // last).  Equal expiries stay: the chain then selects equal keys twice.
-            int64_t* c = bp[T];
+        for (int k = 0; k < PR; ++k) m += in_range(r.e_prio[k]);
+        const bool fail_in = in_range(r.e_fail);
+        if (m == 0 && !fail_in) {
+            flat[0] = key_of<PD, PR>(0, tmin, s0, r, n);
+            flat[1] = key_of<PD, PR>(1, tmin, s0, r, n);
+        } else {
+            // stepped node (a few % of nodes): sort the in-range expiries (static indices)
 #pragma unroll
-            for (int k = 0; k < PR; ++k) c[k] = r.e_prio[k];
-            c[PR] = r.e_hv;
-            c[PR + 1] = T == 0 ? r.e_fail : INT64_MIN;  // DaemonSet pods bypass the Filter
-            int m = 0;
+            for (int T = 0; T < 2; ++T) {
+                int64_t c[NB];
 #pragma unroll
-            for (int j = 0; j < NB; ++j) {
-                const bool in = c[j] > tmin && c[j] <= tmax;
-                c[j] = in ? c[j] : INT64_MAX;
-                m += in;
-            }
+                for (int k = 0; k < PR; ++k) c[k] = r.e_prio[k];
+                c[PR] = r.e_hv;
+                c[PR + 1] = T == 0 ? r.e_fail : INT64_MIN;  // DaemonSet pods bypass the Filter
+                int cnt = 0;
 #pragma unroll
-            for (int i = 0; i < NB; ++i)  // odd-even transposition sort, static indices
-#pragma unroll
-                for (int j = i & 1; j + 1 < NB; j += 2) {
-                    const int64_t a = c[j], b2 = c[j + 1];
-                    c[j] = min(a, b2);
-                    c[j + 1] = max(a, b2);
+                for (int j = 0; j < NB; ++j) {
+                    const bool in = in_range(c[j]);
+                    c[j] = in ? c[j] : INT64_MAX;
+                    cnt += in;
                 }
-            cnt[T] = m;
-            key0[T] = key_at<PD, PR>(tmin, T == 1, r, n, wsum, noprio);
+                if (cnt == 0) {
+                    flat[T] = key_of<PD, PR>(T, tmin, s0, r, n);
+                    continue;
+                }
 #pragma unroll
-            for (int j = 0; j < NB; ++j)
-                kk[T][j] = j < m ? key_at<PD, PR>(c[j], T == 1, r, n, wsum, noprio) : -1;
+                for (int i = 0; i < NB; ++i)  // odd-even transposition sort
+#pragma unroll
+                    for (int j = i & 1; j + 1 < NB; j += 2) {
+                        const int64_t x = c[j], y = c[j + 1];
+                        c[j] = min(x, y);
+                        c[j + 1] = max(x, y);
+                    }
+                // key of step j+1 at its first instant c[j] (equal expiries give equal keys)
+                const int32_t k0 = key_of<PD, PR>(T, tmin, s0, r, n);
+                if (cnt == 1) {
+                    const int32_t slot = atomicAdd(&lc[T][0], 1);
+                    Step1 v;
+                    v.bp = c[0];
+                    v.k0 = k0;
+                    v.k1 = key_of<PD, PR>(T, c[0], score_at<PD, PR>(c[0], r, wsum, noprio), r, n);
+                    st.single[(int64_t)T * st.npad + seg * kStepSeg + slot] = v;
+                } else {
+                    const int32_t slot = atomicAdd(&lc[T][1], 1);
+                    VR v;
+                    v.cnt = cnt;
+                    v.key[0] = k0;
+#pragma unroll
+                    for (int j = 0; j < NB; ++j) {
+                        v.bp[j] = c[j];  // INT64_MAX past cnt: never selected
+                        v.key[j + 1] =
+                            j < cnt ? key_of<PD, PR>(T, c[j], score_at<PD, PR>(c[j], r, wsum, noprio), r, n) : -1;
+                    }
+                    reinterpret_cast<VR*>(st.multi)[(int64_t)T * st.npad + seg * kStepSeg + slot] = v;
+                }
+            }
         }
     }
-    if (n < st.npad) {
+    if (n < st.npad) {  // 16-bit segment-local form of the flat key
 #pragma unroll
-        for (int T = 0; T < 2; ++T) st.flat[T * st.npad + n] = cnt[T] ? -1 : key0[T];
-    }
-    int32_t slot[2] = {0, 0};
-#pragma unroll
-    for (int T = 0; T < 2; ++T)
-        if (cnt[T]) slot[T] = atomicAdd(&vc[T], 1);
-#pragma unroll
-    for (int T = 0; T < 2; ++T) {
-        if (!cnt[T]) continue;
-        VR v;
-        v.cnt = cnt[T];
-        v.key[0] = key0[T];
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            v.bp[j] = j < cnt[T] ? bp[T][j] : INT64_MAX;
-            v.key[j + 1] = j < cnt[T] ? kk[T][j] : -1;
-        }
-        VR* dst = reinterpret_cast<VR*>(st.vrec) + (int64_t)T * st.npad + seg * kStepSeg + slot[T];
-        *dst = v;
+        for (int T = 0; T < 2; ++T)
+            st.flat[T * st.npad + n] = flat[T] < 0 ? (int16_t)-1 : (int16_t)(((flat[T] >> 24) << 8) | (255 - threadIdx.x));
     }
     __syncthreads();
-    if (threadIdx.x < 2) st.vcnt[threadIdx.x * st.nseg + seg] = vc[threadIdx.x];
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+        const int32_t c = lc[T][0], c4 = (c + 7) & ~7;
+        if ((int32_t)threadIdx.x >= c && (int32_t)threadIdx.x < c4) {
+            Step1 v;
+            v.bp = INT64_MAX;
+            v.k0 = -1;
+            v.k1 = -1;
+            st.single[(int64_t)T * st.npad + seg * kStepSeg + threadIdx.x] = v;
+        }
+        if (threadIdx.x == 0) {
+            st.cnt[((int64_t)T * st.nseg + seg) * 2] = c4;
+            st.cnt[((int64_t)T * st.nseg + seg) * 2 + 1] = lc[T][1];
+        }
+    }
 }
 
 // ---------------------------------------------------------------- K3s
 constexpr int kK3sWaves = 4;
 
 // Max over one 256-node segment for the 64 pods of a wave: flat keys (one
-// int32 max per pair), then the segment's stepped nodes (select per step).
+// packed 16-bit max per two pairs), then the segment's one-step nodes eight
+// records per scalar-load batch (64-bit compare + select), then the rare
+// multi-step nodes.
+// Pin a wave-uniform loaded value in an SGPR: keeps the compiler from turning
+// "select between two loaded keys" into a per-lane gather of the selected one.
+__device__ __forceinline__ int32_t sreg(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+typedef short v2i16 __attribute__((ext_vector_type(2)));
+
 template <int NB>
-__device__ __forceinline__ int32_t seg_max(int64_t tnow, int32_t best, const int32_t* __restrict__ flat,
-                                           const int32_t* __restrict__ vcnt, const VRec<NB>* __restrict__ vrec,
-                                           int64_t seg) {
-    const int32_t* __restrict__ f = flat + seg * kStepSeg;
-#pragma unroll 64
-    for (int i = 0; i < kStepSeg; ++i) best = max(best, f[i]);
-    const int32_t nv = vcnt[seg];
-    const VRec<NB>* __restrict__ v = vrec + seg * kStepSeg;
-    for (int32_t j = 0; j < nv; ++j) {
-        const int32_t c = v[j].cnt;
-        int32_t k = v[j].key[0];
-        for (int32_t s = 0; s < c; ++s) k = tnow >= v[j].bp[s] ? v[j].key[s + 1] : k;
+__device__ __forceinline__ int32_t seg_max(int64_t tnow, int32_t best, const int16_t* __restrict__ flat,
+                                           const int32_t* __restrict__ cnt, const Step1* __restrict__ single,
+                                           const VRec<NB>* __restrict__ multi, int32_t seg) {
+    const int2 nc = *reinterpret_cast<const int2*>(cnt + 2 * seg);  // issued ahead of the flat loop
+    // flat keys: 16-bit segment-local (score << 8 | 255 - local), two per dword,
+    // one packed v_pk_max_i16 per pair of (pod, node) evaluations
+    const int4* __restrict__ f = reinterpret_cast<const int4*>(flat + (int64_t)seg * kStepSeg);
+    v2i16 b2 = {-1, -1};
+#pragma unroll
+    for (int i = 0; i < kStepSeg / 8; i += 16) {  // 128 keys per batch of scalar loads
+        int4 k[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) k[j] = f[i + j];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            b2 = __builtin_elementwise_max(b2, __builtin_bit_cast(v2i16, k[j].x));
+            b2 = __builtin_elementwise_max(b2, __builtin_bit_cast(v2i16, k[j].y));
+            b2 = __builtin_elementwise_max(b2, __builtin_bit_cast(v2i16, k[j].z));
+            b2 = __builtin_elementwise_max(b2, __builtin_bit_cast(v2i16, k[j].w));
+        }
+    }
+    const int32_t m16 = max((int32_t)b2.x, (int32_t)b2.y);
+    if (m16 >= 0)  // back to the global 32-bit key: (score << 24) | (0xFFFFFF - node)
+        best = max(best, ((m16 >> 8) << 24) | (0xFFFFFF - (seg * kStepSeg + 255 - (m16 & 255))));
+    const int4* __restrict__ s1 = reinterpret_cast<const int4*>(single + (int64_t)seg * kStepSeg);
+    for (int32_t j = 0; j < nc.x; j += 8) {
+        int4 q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] = s1[j + u];
+        int32_t k0[8], k1[8];
+        int64_t bp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            bp[u] = (int64_t)(((uint64_t)(uint32_t)sreg(q[u].y) << 32) | (uint32_t)sreg(q[u].x));
+            k0[u] = sreg(q[u].z);
+            k1[u] = sreg(q[u].w);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) best = max(best, tnow >= bp[u] ? k1[u] : k0[u]);
+    }
+    const VRec<NB>* __restrict__ vm = multi + (int64_t)seg * kStepSeg;
+    for (int32_t j = 0; j < nc.y; ++j) {
+        int32_t key[NB + 1];
+        int64_t bp[NB];
+#pragma unroll
+        for (int s = 0; s <= NB; ++s) key[s] = sreg(vm[j].key[s]);
+#pragma unroll
+        for (int s = 0; s < NB; ++s) bp[s] = vm[j].bp[s];
+        int32_t k = key[0];
+#pragma unroll
+        for (int s = 0; s < NB; ++s) k = tnow >= bp[s] ? key[s + 1] : k;
         best = max(best, k);
     }
     return best;
@@ -232,41 +315,32 @@ __global__ __launch_bounds__(kK3sWaves * 64) void k3s_eval(StepTables st, const 
                                                            const uint8_t* __restrict__ flags, int64_t P,
                                                            int64_t node_offset, int32_t segs_per_chunk,
                                                            int32_t nchunks, long long* __restrict__ keys) {
-    __shared__ int32_t red[kK3sWaves][64];
     const int64_t b = blockIdx.x;
     const int64_t chunk = b % nchunks;  // nchunks % 8 == 0 when >= 8: an XCD keeps its chunks
     const int64_t ptile = b / nchunks;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int64_t slot = ptile * 64 + lane;
+    // the 4 waves take 4 different 64-pod tiles over the SAME node segments, so a
+    // segment's keys are fetched into the scalar cache once per workgroup
+    const int64_t slot = ptile * (kK3sWaves * 64) + threadIdx.x;
     const bool live = slot < P;
     const int32_t pod = live ? perm[slot] : 0;
     const int64_t tnow = live ? now[pod] : 0;
     const bool ds = live && flags && (flags[pod] & 1u);
     const bool any_n = __ballot(live && !ds) != 0, any_d = __ballot(ds) != 0;
-    // this wave's segments of the workgroup's chunk
-    const int64_t cs = chunk * segs_per_chunk;
-    const int64_t ce = min((int64_t)st.nseg, cs + segs_per_chunk);
-    const int64_t q = (segs_per_chunk + kK3sWaves - 1) / kK3sWaves;
-    const int64_t s0 = min(ce, cs + wave * q), s1 = min(ce, s0 + q);
-    const VRec<NB>* __restrict__ vr = reinterpret_cast<const VRec<NB>*>(st.vrec);
+    const int32_t s0 = __builtin_amdgcn_readfirstlane((int32_t)chunk * segs_per_chunk);
+    const int32_t s1 = __builtin_amdgcn_readfirstlane(min((int32_t)st.nseg, s0 + segs_per_chunk));
+    const VRec<NB>* __restrict__ vm = reinterpret_cast<const VRec<NB>*>(st.multi);
     int32_t bn = -1, bd = -1;
     if (any_n)
-        for (int64_t s = s0; s < s1; ++s) bn = seg_max<NB>(tnow, bn, st.flat, st.vcnt, vr, s);
+        for (int32_t s = s0; s < s1; ++s) bn = seg_max<NB>(tnow, bn, st.flat, st.cnt, st.single, vm, s);
     if (any_d)
-        for (int64_t s = s0; s < s1; ++s)
-            bd = seg_max<NB>(tnow, bd, st.flat + st.npad, st.vcnt + st.nseg, vr + st.npad, s);
-    red[wave][lane] = ds ? bd : bn;
-    __syncthreads();
-    if (wave == 0) {
-        int32_t best = red[0][lane];
-#pragma unroll
-        for (int i = 1; i < kK3sWaves; ++i) best = max(best, red[i][lane]);
-        if (live && best >= 0) {
-            const int64_t sc = best >> 24;
-            const int64_t n = 0xFFFFFF - (best & 0xFFFFFF);
-            atomicMax(&keys[pod], (long long)((sc << 32) | (int64_t)(0xFFFFFFFFull - (uint64_t)(node_offset + n))));
-        }
+        for (int32_t s = s0; s < s1; ++s)
+            bd = seg_max<NB>(tnow, bd, st.flat + st.npad, st.cnt + 2 * st.nseg, st.single + st.npad, vm + st.npad,
+                             s);
+    const int32_t best = ds ? bd : bn;
+    if (live && best >= 0) {
+        const int64_t sc = best >> 24;
+        const int64_t n = 0xFFFFFF - (best & 0xFFFFFF);
+        atomicMax(&keys[pod], (long long)((sc << 32) | (int64_t)(0xFFFFFFFFull - (uint64_t)(node_offset + n))));
     }
 }
 
@@ -284,7 +358,7 @@ StepGeometry step_geometry(int64_t P, int64_t N) {
     g.nseg = (N + kStepSeg - 1) / kStepSeg;
     g.npad = g.nseg * kStepSeg;
     g.ntiles = (P + kPodTile - 1) / kPodTile;
-    const int64_t ptiles = (P + 63) / 64;
+    const int64_t ptiles = (P + kK3sWaves * 64 - 1) / (kK3sWaves * 64);
     // ~4 waves per SIMD: 256 CUs x 4 SIMDs x 4 waves / 4 waves per workgroup
     const char* e = getenv("CRANE_K3S_BLOCKS");
     const int64_t target = e && atoi(e) > 0 ? atoi(e) : 4096;
