@@ -99,12 +99,14 @@ struct crane_dyn {
     DevBuf<int8_t> ff;
     DevBuf<int64_t> score;
     DevBuf<uint32_t> k2_cnt, k2_tot, k2_sorted;  // bin-partitioned K2 scratch
+    DevBuf<uint32_t> k2_cur;                      // two-kernel K2: [2][nbins] bin cursors
+    int32_t k2p_nbins = -1, k2p_parity = 0;
     DevBuf<uint32_t> gcnt;  // greedy: per-window counts [W][N]
     DevBuf<int64_t> gbase, gchosen;
     DevBuf<uint8_t> gleaf, gflags;
     DevBuf<int32_t> sperm, svcnt;
     DevBuf<int16_t> sflat;  // K3 step path scratch (step.hip)
-    DevBuf<int64_t> stile;
+    DevBuf<int64_t> stile, spnow;
     DevBuf<unsigned char> svrec;
     DevBuf<Step1> sstep1;
     DevBuf<double> thr;  // quotient thresholds (K3 division-free path), empty if unusable
@@ -262,9 +264,9 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->val.release(); h->hv.release(); h->ts.release(); h->hv_ts.release(); h->rec.release();
     h->buckets.release(); h->bnode.release(); h->bts.release(); h->now.release(); h->flags.release();
     h->keys.release(); h->ff.release(); h->score.release(); h->thr.release();
-    h->k2_cnt.release(); h->k2_tot.release(); h->k2_sorted.release();
+    h->k2_cnt.release(); h->k2_tot.release(); h->k2_sorted.release(); h->k2_cur.release();
     h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
-    h->sperm.release(); h->sflat.release(); h->svcnt.release(); h->stile.release(); h->svrec.release(); h->sstep1.release();
+    h->sperm.release(); h->sflat.release(); h->svcnt.release(); h->stile.release(); h->spnow.release(); h->svrec.release(); h->sstep1.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -353,10 +355,33 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     const size_t nb = (size_t)std::max(1, dp.n_win) * (size_t)std::max<int64_t>(h->N, 1);
     if (nb > h->buckets.n) h->buckets_zero = false;
     HIPTRY(h, h->buckets.reserve(nb));
+    const char* k2e = getenv("CRANE_K2");
+    const std::string mode = k2e ? k2e : "part";
+    const HotPart gp = hot_part_geometry(h->B, h->N, dp.n_win);
+    if (mode == "part" && gp.ok) {
+        // two kernels adding into zeroed buckets (K1 zeroes what it consumed)
+        if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
+        if (gp.nbins != h->k2p_nbins || !h->k2_cur.p) {
+            HIPTRY(h, h->k2_cur.reserve((size_t)2 * gp.nbins));
+            HIPTRY(h, hipMemsetAsync(h->k2_cur.p, 0, sizeof(uint32_t) * 2 * gp.nbins, st));
+            h->k2p_nbins = gp.nbins;
+            h->k2p_parity = 0;
+        }
+        HIPTRY(h, h->k2_sorted.reserve((size_t)gp.nbins * (size_t)gp.cap));
+        uint32_t* cur = h->k2_cur.p + (size_t)h->k2p_parity * gp.nbins;
+        uint32_t* nxt = h->k2_cur.p + (size_t)(h->k2p_parity ^ 1) * gp.nbins;
+        HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, cur, nxt,
+                                        h->k2_sorted.p, st));
+        h->k2p_parity ^= 1;
+        h->buckets_zero = false;
+        h->hv_from_counts = true;
+        h->hv_ts_counts = hv_ts_ns;
+        h->rec_dirty = true;
+        return CRANE_OK;
+    }
     if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
     const HotBins g = hot_bins_geometry(h->B, h->N, dp.n_win);
-    const char* k2e = getenv("CRANE_K2");
-    if (g.ok && !(k2e && std::strcmp(k2e, "hash") == 0)) {
+    if (g.ok && mode != "hash") {
         HIPTRY(h, h->k2_cnt.reserve((size_t)g.nbins * (size_t)g.nchunks));
         HIPTRY(h, h->k2_tot.reserve((size_t)g.nbins));
         HIPTRY(h, h->k2_sorted.reserve((size_t)h->B));
@@ -395,13 +420,14 @@ static int eval_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint
         const StepGeometry g = step_geometry(P, h->N);
         HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
         HIPTRY(h, h->stile.reserve((size_t)(2 * g.ntiles)));
+        HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
         HIPTRY(h, h->sflat.reserve((size_t)(2 * g.npad)));
         HIPTRY(h, h->svcnt.reserve((size_t)(4 * g.nseg)));
         HIPTRY(h, h->sstep1.reserve((size_t)(2 * g.npad)));
         HIPTRY(h, h->svrec.reserve((size_t)(2 * g.npad) * step_vrec_bytes(h->shape)));
         StepTables stt{h->sflat.p, h->svcnt.p, h->sstep1.p, h->svrec.p, g.npad, g.nseg};
         HIPTRY(h, launch_eval_step(h->shape, h->rec.p, h->N, h->node_offset, d_now, d_flags, P, h->dp.wsum,
-                                   h->dp.noprio, d_keys, stt, g, h->sperm.p, h->stile.p, st));
+                                   h->dp.noprio, d_keys, stt, g, h->sperm.p, h->spnow.p, h->stile.p, st));
         return CRANE_OK;
     }
     HIPTRY(h, hipMemsetAsync(d_keys, 0xFF, sizeof(long long) * (size_t)P, st));

@@ -154,6 +154,125 @@ __global__ __launch_bounds__(kHT) void k2d_bin_hist(const uint32_t* __restrict__
         }
 }
 
+// ---------------------------------------------------------------- two-kernel form
+// X  partition : each workgroup takes 2048 bindings (8 per thread, loads issued
+//                together), counts them per node bin in LDS, reserves its run of
+//                every bin region with ONE global atomic per bin, and writes
+//                (local node | bucket << 24) entries into the bin regions.
+//                Bin regions have capacity B, so no pre-count pass is needed.
+// Y  bin_hist  : kYSplits workgroups per bin, each an LDS histogram [W][2^bb]
+//                of a contiguous slice of the bin's entries, flushed with
+//                contiguous atomics into the (zeroed) buckets.
+// The per-bin cursors alternate between two arrays; X zeroes the idle one for
+// the next refresh.
+constexpr int kXPer = 8;     // bindings per thread in X
+constexpr int kYSplits = 8;  // workgroups per bin in Y
+
+__global__ __launch_bounds__(kHT) void k2x_partition(const int32_t* __restrict__ bnode,
+                                                     const int64_t* __restrict__ bts, int64_t B, int64_t N,
+                                                     HotCutoffs cut, HotPart g, uint32_t* __restrict__ cur,
+                                                     uint32_t* __restrict__ cur_next, uint32_t* __restrict__ region) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];  // hist [nbins], base [nbins]
+    uint32_t* hist = sh;
+    uint32_t* base = sh + g.nbins;
+    for (int i = threadIdx.x; i < g.nbins; i += kHT) hist[i] = 0;
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < g.nbins; i += kHT) cur_next[i] = 0;
+    __syncthreads();
+    const int64_t b0 = (int64_t)blockIdx.x * (kHT * kXPer) + threadIdx.x;
+    int32_t nd[kXPer];
+    int64_t ts[kXPer];
+#pragma unroll
+    for (int u = 0; u < kXPer; ++u) {
+        const int64_t b = b0 + u * kHT;
+        nd[u] = b < B ? bnode[b] : -1;
+        ts[u] = b < B ? bts[b] : INT64_MIN;
+    }
+    uint32_t ent[kXPer], pos[kXPer];
+    int32_t bin[kXPer];
+    const uint32_t mask = (1u << g.bb) - 1;
+#pragma unroll
+    for (int u = 0; u < kXPer; ++u) {
+        const int j = window_rank(ts[u], cut);
+        const bool ok = nd[u] >= 0 && (int64_t)nd[u] < N && j > 0;  // binding.go:85-91
+        bin[u] = ok ? nd[u] >> g.bb : -1;
+        ent[u] = ((uint32_t)nd[u] & mask) | ((uint32_t)(j - 1) << 24);
+        pos[u] = ok ? atomicAdd(&hist[bin[u]], 1u) : 0u;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < g.nbins; i += kHT) {
+        const uint32_t c = hist[i];
+        base[i] = c ? atomicAdd(&cur[i], c) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kXPer; ++u)
+        if (bin[u] >= 0) region[(int64_t)bin[u] * g.cap + base[bin[u]] + pos[u]] = ent[u];
+}
+
+__global__ __launch_bounds__(kHT) void k2y_bin_hist(const uint32_t* __restrict__ region,
+                                                    const uint32_t* __restrict__ cur, HotPart g, int32_t W,
+                                                    int64_t N, uint32_t* __restrict__ buckets) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // [W][2^bb]
+    const int bin = blockIdx.x, split = blockIdx.y;
+    const int binw = 1 << g.bb;
+    for (int i = threadIdx.x; i < W * binw; i += kHT) hist[i] = 0;
+    const uint32_t len = cur[bin];
+    // contiguous 1/splits of the bin's entries: Zipf-hot bins spread over the splits
+    const uint32_t lo = (uint32_t)((uint64_t)len * split / gridDim.y);
+    const uint32_t hi = (uint32_t)((uint64_t)len * (split + 1) / gridDim.y);
+    const uint32_t* __restrict__ r = region + (int64_t)bin * g.cap + lo;
+    const uint32_t n_e = hi - lo;
+    __syncthreads();
+    for (uint32_t e0 = threadIdx.x; e0 < n_e; e0 += kHT * kXPer) {
+        uint32_t v[kXPer];
+#pragma unroll
+        for (int u = 0; u < kXPer; ++u) {
+            const uint32_t e = e0 + u * kHT;
+            v[u] = e < n_e ? r[e] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < kXPer; ++u)
+            if (v[u] != 0xFFFFFFFFu) atomicAdd(&hist[(v[u] >> 24) * binw + (v[u] & 0xFFFFFF)], 1u);
+    }
+    __syncthreads();
+    // buckets are zero on entry (K1 zeroes what it consumes): add the non-zero
+    // counts, lane i -> node i (contiguous atomics)
+    const int64_t n0 = (int64_t)bin << g.bb;
+    for (int w = 0; w < W; ++w)
+        for (int i = threadIdx.x; i < binw; i += kHT) {
+            const uint32_t c = hist[w * binw + i];
+            if (c && n0 + i < N) atomicAdd(&buckets[(int64_t)w * N + n0 + i], c);
+        }
+}
+
+HotPart hot_part_geometry(int64_t B, int64_t N, int32_t W) {
+    HotPart g{};
+    int bb = 10;
+    while (((N + (1LL << bb) - 1) >> bb) > 4096) ++bb;
+    g.bb = bb;
+    g.nbins = (int32_t)((N + (1LL << bb) - 1) >> bb);
+    g.cap = B;
+    g.nblk = (int32_t)((B + kHT * kXPer - 1) / (kHT * kXPer));
+    g.ok = N > 0 && B > 0 && bb <= 24 && W >= 1 && (size_t)W * ((size_t)1 << bb) * 4 <= 128 * 1024 &&
+           (double)g.nbins * (double)B <= (double)(1LL << 28);
+    return g;
+}
+
+hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
+                                 const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* cur,
+                                 uint32_t* cur_next, uint32_t* region, hipStream_t st) {
+    static const hipError_t attr =
+        hipFuncSetAttribute((const void*)k2y_bin_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(k2x_partition, dim3(g.nblk), dim3(kHT), sizeof(uint32_t) * 2 * g.nbins, st, bnode, bts, B, N,
+                       cut, g, cur, cur_next, region);
+    const size_t lds = sizeof(uint32_t) * (size_t)cut.n_win * ((size_t)1 << g.bb);
+    hipLaunchKernelGGL(k2y_bin_hist, dim3(g.nbins, kYSplits), dim3(kHT), lds, st, region, cur, g, cut.n_win, N,
+                       buckets);
+    return hipGetLastError();
+}
+
 HotBins hot_bins_geometry(int64_t B, int64_t N, int32_t W) {
     HotBins g{};
     int bb = 12;

@@ -50,6 +50,20 @@ hipError_t launch_hot_count_binned(const int32_t* bnode, const int64_t* bts, int
                                    const HotCutoffs& cut, uint32_t* buckets, const HotBins& g, uint32_t* chunk_cnt,
                                    uint32_t* bin_tot, uint32_t* sorted, hipStream_t st);
 
+// Two-kernel partitioned K2 (hotcount.hip): per-bin regions of capacity B
+struct HotPart {
+    int32_t bb, nbins;  // 2^bb nodes per bin
+    int64_t cap;        // entries per bin region
+    int32_t nblk;       // partition workgroups
+    bool ok;
+};
+HotPart hot_part_geometry(int64_t B, int64_t N, int32_t W);
+// cur/cur_next: [nbins] cursors (cur zero on entry; cur_next zeroed here), region [nbins * cap].
+// Adds into buckets[W][N], which must be zero on entry.
+hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
+                                 const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* cur,
+                                 uint32_t* cur_next, uint32_t* region, hipStream_t st);
+
 // K3 step path (step.hip): per-batch node step tables + pair eval.
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
 constexpr int64_t kStepMaxNodes = 1LL << 24;  // packed key keeps 24 bits of node index
@@ -79,11 +93,11 @@ struct StepGeometry {
 };
 size_t step_vrec_bytes(int shape);
 StepGeometry step_geometry(int64_t P, int64_t N);
-// perm [ntiles * 1024], tile_mm [2 * ntiles]; also initialises keys[0..P) to -1
+// perm, pnow [ntiles * 1024], tile_mm [2 * ntiles]; also initialises keys[0..P) to -1
 hipError_t launch_eval_step(int shape, const void* rec, int64_t N, int64_t node_offset, const int64_t* now,
                             const uint8_t* flags, int64_t P, double wsum, int32_t noprio, long long* keys,
-                            const StepTables& st, const StepGeometry& g, int32_t* perm, int64_t* tile_mm,
-                            hipStream_t s);
+                            const StepTables& st, const StepGeometry& g, int32_t* perm, int64_t* pnow,
+                            int64_t* tile_mm, hipStream_t s);
 int k3_variant();
 
 size_t node_rec_bytes(int shape);

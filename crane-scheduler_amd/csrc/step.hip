@@ -63,8 +63,8 @@ constexpr int kPodTile = 1024;
 
 __global__ __launch_bounds__(kPodTile) void k3p_pods(const int64_t* __restrict__ now,
                                                      const uint8_t* __restrict__ flags, int64_t P,
-                                                     int32_t* __restrict__ perm, int64_t* __restrict__ tile_mm,
-                                                     long long* __restrict__ keys) {
+                                                     int32_t* __restrict__ perm, int64_t* __restrict__ pnow,
+                                                     int64_t* __restrict__ tile_mm, long long* __restrict__ keys) {
     __shared__ int32_t cn[kPodTile / 64], cd[kPodTile / 64];
     __shared__ int64_t wmn[kPodTile / 64], wmx[kPodTile / 64];
     const int64_t t = blockIdx.x;
@@ -99,7 +99,8 @@ __global__ __launch_bounds__(kPodTile) void k3p_pods(const int64_t* __restrict__
     }
     if (live) {
         const int32_t pos = ds ? tot_n + pre_d + __popcll(md_mask & lt) : pre_n + __popcll(mn_mask & lt);
-        perm[t * kPodTile + pos] = (int32_t)p;
+        perm[t * kPodTile + pos] = (int32_t)p | (ds ? (int32_t)0x80000000 : 0);  // bit 31: DaemonSet
+        pnow[t * kPodTile + pos] = tn;
     }
     if (threadIdx.x == 0) {
         int64_t a = INT64_MAX, b = INT64_MIN;
@@ -241,6 +242,7 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
 
 // ---------------------------------------------------------------- K3s
 constexpr int kK3sWaves = 4;
+constexpr int kK3sMaxSegs = 16;  // segments per workgroup chunk: 16 KB of LDS flat keys
 
 // Max over one 256-node segment for the 64 pods of a wave: flat keys (one
 // packed 16-bit max per two pairs), then the segment's one-step nodes eight
@@ -253,16 +255,17 @@ __device__ __forceinline__ int32_t sreg(int32_t x) { return __builtin_amdgcn_rea
 typedef short v2i16 __attribute__((ext_vector_type(2)));
 
 template <int NB>
-__device__ __forceinline__ int32_t seg_max(int64_t tnow, int32_t best, const int16_t* __restrict__ flat,
+__device__ __forceinline__ int32_t seg_max(int64_t tnow, int32_t best, const int4* lflat,
                                            const int32_t* __restrict__ cnt, const Step1* __restrict__ single,
                                            const VRec<NB>* __restrict__ multi, int32_t seg) {
     const int2 nc = *reinterpret_cast<const int2*>(cnt + 2 * seg);  // issued ahead of the flat loop
     // flat keys: 16-bit segment-local (score << 8 | 255 - local), two per dword,
-    // one packed v_pk_max_i16 per pair of (pod, node) evaluations
-    const int4* __restrict__ f = reinterpret_cast<const int4*>(flat + (int64_t)seg * kStepSeg);
+    // one packed v_pk_max_i16 per pair of (pod, node) evaluations; read from
+    // the workgroup's LDS copy with broadcast ds_read_b128 (8 keys per read)
+    const int4* f = lflat;
     v2i16 b2 = {-1, -1};
 #pragma unroll
-    for (int i = 0; i < kStepSeg / 8; i += 16) {  // 128 keys per batch of scalar loads
+    for (int i = 0; i < kStepSeg / 8; i += 16) {
         int4 k[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) k[j] = f[i + j];
@@ -311,8 +314,7 @@ __device__ __forceinline__ int32_t seg_max(int64_t tnow, int32_t best, const int
 
 template <int NB>
 __global__ __launch_bounds__(kK3sWaves * 64) void k3s_eval(StepTables st, const int32_t* __restrict__ perm,
-                                                           const int64_t* __restrict__ now,
-                                                           const uint8_t* __restrict__ flags, int64_t P,
+                                                           const int64_t* __restrict__ pnow, int64_t P,
                                                            int64_t node_offset, int32_t segs_per_chunk,
                                                            int32_t nchunks, long long* __restrict__ keys) {
     const int64_t b = blockIdx.x;
@@ -322,20 +324,33 @@ __global__ __launch_bounds__(kK3sWaves * 64) void k3s_eval(StepTables st, const 
     // segment's keys are fetched into the scalar cache once per workgroup
     const int64_t slot = ptile * (kK3sWaves * 64) + threadIdx.x;
     const bool live = slot < P;
-    const int32_t pod = live ? perm[slot] : 0;
-    const int64_t tnow = live ? now[pod] : 0;
-    const bool ds = live && flags && (flags[pod] & 1u);
+    // K3p wrote the pods in partitioned order: two independent coalesced loads
+    const int32_t praw = live ? perm[slot] : 0;
+    const int64_t tnow = live ? pnow[slot] : 0;
+    const bool ds = praw < 0;
+    const int32_t pod = praw & 0x7FFFFFFF;
     const bool any_n = __ballot(live && !ds) != 0, any_d = __ballot(ds) != 0;
     const int32_t s0 = __builtin_amdgcn_readfirstlane((int32_t)chunk * segs_per_chunk);
     const int32_t s1 = __builtin_amdgcn_readfirstlane(min((int32_t)st.nseg, s0 + segs_per_chunk));
+    // stage the chunk's flat keys of both pod kinds in LDS: [kind][segment][32 x int4]
+    extern __shared__ int4 lds_flat[];
+    constexpr int kSegI4 = kStepSeg * 2 / 16;  // int4 per segment of 16-bit keys
+    const int32_t nsi4 = (s1 - s0) * kSegI4;
+    for (int32_t i = threadIdx.x; i < 2 * nsi4; i += kK3sWaves * 64) {
+        const int32_t T = i >= nsi4, j = i - T * nsi4;
+        lds_flat[T * segs_per_chunk * kSegI4 + j] =
+            reinterpret_cast<const int4*>(st.flat + T * st.npad + (int64_t)s0 * kStepSeg)[j];
+    }
+    __syncthreads();
     const VRec<NB>* __restrict__ vm = reinterpret_cast<const VRec<NB>*>(st.multi);
     int32_t bn = -1, bd = -1;
     if (any_n)
-        for (int32_t s = s0; s < s1; ++s) bn = seg_max<NB>(tnow, bn, st.flat, st.cnt, st.single, vm, s);
+        for (int32_t s = s0; s < s1; ++s)
+            bn = seg_max<NB>(tnow, bn, lds_flat + (s - s0) * kSegI4, st.cnt, st.single, vm, s);
     if (any_d)
         for (int32_t s = s0; s < s1; ++s)
-            bd = seg_max<NB>(tnow, bd, st.flat + st.npad, st.cnt + 2 * st.nseg, st.single + st.npad, vm + st.npad,
-                             s);
+            bd = seg_max<NB>(tnow, bd, lds_flat + (segs_per_chunk + s - s0) * kSegI4, st.cnt + 2 * st.nseg,
+                             st.single + st.npad, vm + st.npad, s);
     const int32_t best = ds ? bd : bn;
     if (live && best >= 0) {
         const int64_t sc = best >> 24;
@@ -367,6 +382,7 @@ StepGeometry step_geometry(int64_t P, int64_t N) {
     nch = std::min<int64_t>(nch, std::max<int64_t>(g.nseg, 1));
     g.segs_per_chunk = (int32_t)((g.nseg + nch - 1) / std::max<int64_t>(nch, 1));
     if (g.segs_per_chunk < 1) g.segs_per_chunk = 1;
+    if (g.segs_per_chunk > kK3sMaxSegs) g.segs_per_chunk = kK3sMaxSegs;  // LDS copy of the flat keys
     g.nchunks = (int32_t)((g.nseg + g.segs_per_chunk - 1) / g.segs_per_chunk);
     if (g.nchunks < 1) g.nchunks = 1;
     g.ptiles = ptiles;
@@ -376,32 +392,33 @@ StepGeometry step_geometry(int64_t P, int64_t N) {
 template <int PD, int PR>
 static hipError_t launch_step_t(const void* rec, int64_t N, int64_t node_offset, const int64_t* now,
                                 const uint8_t* flags, int64_t P, double wsum, int32_t noprio, long long* keys,
-                                const StepTables& st, const StepGeometry& g, int32_t* perm, int64_t* tile_mm,
-                                hipStream_t s) {
+                                const StepTables& st, const StepGeometry& g, int32_t* perm, int64_t* pnow,
+                                int64_t* tile_mm, hipStream_t s) {
     if (P <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k3p_pods, dim3((unsigned)g.ntiles), dim3(kPodTile), 0, s, now, flags, P, perm, tile_mm,
+    hipLaunchKernelGGL(k3p_pods, dim3((unsigned)g.ntiles), dim3(kPodTile), 0, s, now, flags, P, perm, pnow, tile_mm,
                        keys);
     if (N <= 0) return hipGetLastError();
     hipLaunchKernelGGL((k3a_steps<PD, PR>), dim3((unsigned)g.nseg), dim3(kStepSeg), 0, s,
                        static_cast<const NodeRec<PD, PR>*>(rec), N, tile_mm, (int32_t)g.ntiles, wsum, noprio, st);
     const unsigned blocks = (unsigned)(g.ptiles * g.nchunks);
-    hipLaunchKernelGGL((k3s_eval<PR + 2>), dim3(blocks), dim3(kK3sWaves * 64), 0, s, st, perm, now, flags, P,
+    const size_t lds = (size_t)g.segs_per_chunk * kStepSeg * 2 * sizeof(int16_t);  // both pod kinds
+    hipLaunchKernelGGL((k3s_eval<PR + 2>), dim3(blocks), dim3(kK3sWaves * 64), lds, s, st, perm, pnow, P,
                        node_offset, g.segs_per_chunk, g.nchunks, keys);
     return hipGetLastError();
 }
 
 hipError_t launch_eval_step(int shape, const void* rec, int64_t N, int64_t node_offset, const int64_t* now,
                             const uint8_t* flags, int64_t P, double wsum, int32_t noprio, long long* keys,
-                            const StepTables& st, const StepGeometry& g, int32_t* perm, int64_t* tile_mm,
-                            hipStream_t s) {
+                            const StepTables& st, const StepGeometry& g, int32_t* perm, int64_t* pnow,
+                            int64_t* tile_mm, hipStream_t s) {
     if (N >= kStepMaxNodes) return hipErrorInvalidValue;
     switch (shape) {
         case kShape4x6:
-            return launch_step_t<4, 6>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, st, g, perm, tile_mm, s);
+            return launch_step_t<4, 6>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, st, g, perm, pnow, tile_mm, s);
         case kShape8x8:
-            return launch_step_t<8, 8>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, st, g, perm, tile_mm, s);
+            return launch_step_t<8, 8>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, st, g, perm, pnow, tile_mm, s);
         default:
-            return launch_step_t<16, 16>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, st, g, perm, tile_mm,
+            return launch_step_t<16, 16>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, st, g, perm, pnow, tile_mm,
                                          s);
     }
 }

@@ -143,7 +143,7 @@ def test_hot_values_vs_oracle(kats):
     assert sc[0, 0] == 50  # hv = 5 (SURVEY KAT-11)
 
 
-@pytest.mark.parametrize("k2", ["binned", "hash"])
+@pytest.mark.parametrize("k2", ["part", "binned", "hash"])
 @pytest.mark.parametrize("n_nodes,n_bind,seed", [(1000, 50_000, 1), (20_000, 300_000, 2), (100, 10, 3),
                                                  (70_000, 2_000_000, 4)])
 def test_hot_values_random(n_nodes, n_bind, seed, k2, monkeypatch):
