@@ -104,6 +104,9 @@ struct crane_dyn {
     DevBuf<uint32_t> gcnt;  // greedy: per-window counts [W][N]
     DevBuf<int64_t> gbase, gchosen;
     DevBuf<uint8_t> gleaf, gflags;
+    DevBuf<unsigned long long> mH, mbs;  // merge-form greedy (merge.hip)
+    DevBuf<int32_t> mflag, mapos, mtk;
+    DevBuf<int64_t> mFs, mIs, mgi;
     DevBuf<int32_t> sperm, svcnt;
     DevBuf<int16_t> sflat;  // K3 step path scratch (step.hip)
     DevBuf<int64_t> stile, spnow;
@@ -266,6 +269,8 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->keys.release(); h->ff.release(); h->score.release(); h->thr.release();
     h->k2_cnt.release(); h->k2_tot.release(); h->k2_sorted.release(); h->k2_cur.release();
     h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
+    h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
+    h->mFs.release(); h->mIs.release(); h->mgi.release();
     h->sperm.release(); h->sflat.release(); h->svcnt.release(); h->stile.release(); h->spnow.release(); h->svrec.release(); h->sstep1.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -552,8 +557,66 @@ int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod
     HIPTRY(h, h->gchosen.reserve((size_t)std::max<int64_t>(P, 1)));
     HIPTRY(h, h->gflags.reserve((size_t)std::max<int64_t>(P, 1)));
     if (pod_flags && P > 0) HIPTRY(h, hipMemcpyAsync(h->gflags.p, pod_flags, P, hipMemcpyHostToDevice, st));
-    HIPTRY(h, launch_greedy(h->shape, h->rec.p, N, h->gcnt.p, a, h->gbase.p, h->gleaf.p, P,
-                            pod_flags ? h->gflags.p : nullptr, h->gchosen.p, st));
+    // Merge form (merge.hip) when every hotValue count is positive; else the sequential kernel
+    const char* ge = getenv("CRANE_GREEDY");
+    bool merge = !(ge && std::strcmp(ge, "seq") == 0) && N > 0 && P > 0;
+    for (int w = 0; w < W; ++w) merge = merge && a.win_count[w] > 0;
+    bool done = false;
+    if (merge) {
+        int64_t Pd = 0;
+        if (pod_flags)
+            for (int64_t p = 0; p < P; ++p) Pd += pod_flags[p] & 1;
+        HIPTRY(h, launch_greedy(h->shape, h->rec.p, N, h->gcnt.p, a, h->gbase.p, h->gleaf.p, P, nullptr, nullptr, st,
+                                kGreedyPrep));
+        MergeArgs ma{};
+        ma.n_win = W;
+        for (int w = 0; w < W; ++w) {
+            ma.win_count[w] = a.win_count[w];
+            ma.win_inc[w] = a.win_inc[w];
+        }
+        HIPTRY(h, h->mH.reserve(2 * 101));
+        HIPTRY(h, h->mflag.reserve(1));
+        HIPTRY(h, launch_merge_hist(h->gbase.p, h->gleaf.p, h->gcnt.p, N, ma, P, Pd, h->mH.p, h->mflag.p, st));
+        unsigned long long Hh[2 * 101];
+        int32_t flag = 1;
+        HIPTRY(h, hipMemcpyAsync(Hh, h->mH.p, sizeof Hh, hipMemcpyDeviceToHost, st));
+        HIPTRY(h, hipMemcpyAsync(&flag, h->mflag.p, sizeof flag, hipMemcpyDeviceToHost, st));
+        HIPTRY(h, hipStreamSynchronize(st));
+        if (flag == 0) {
+            // cut level: the stream's first `cap` elements all have score >= vlo
+            auto cut = [&](int T, int64_t cap, int* vlo) -> int64_t {
+                unsigned long long cum = 0;
+                *vlo = 0;
+                for (int u = 100; u >= 0; --u) {
+                    cum += Hh[T * 101 + u];
+                    if (cum >= (unsigned long long)cap) {
+                        *vlo = u;
+                        return cap;
+                    }
+                }
+                return (int64_t)cum;
+            };
+            int vF = 0, vI = 0;
+            const int64_t nF = cut(0, P, &vF);
+            const int64_t nI = Pd ? cut(1, Pd, &vI) : 0;
+            HIPTRY(h, h->mbs.reserve((size_t)merge_bsum_len(N, std::min(vF, vI))));
+            HIPTRY(h, h->mFs.reserve((size_t)std::max<int64_t>(nF, 1)));
+            HIPTRY(h, h->mIs.reserve((size_t)std::max<int64_t>(nI, 1)));
+            HIPTRY(h, h->mapos.reserve((size_t)std::max<int64_t>(Pd, 1)));
+            HIPTRY(h, h->mtk.reserve((size_t)P));
+            HIPTRY(h, h->mgi.reserve((size_t)std::max<int64_t>(nI, 1)));
+            if (nF) HIPTRY(h, launch_merge_stream(h->gbase.p, h->gleaf.p, h->gcnt.p, N, ma, 0, vF, nF, h->mbs.p,
+                                                  h->mFs.p, st));
+            if (nI) HIPTRY(h, launch_merge_stream(h->gbase.p, h->gleaf.p, h->gcnt.p, N, ma, 1, vI, nI, h->mbs.p,
+                                                  h->mIs.p, st));
+            HIPTRY(h, launch_merge_assign(h->mFs.p, nF, h->mIs.p, nI, h->gflags.p, P, Pd, h->mapos.p, h->mtk.p,
+                                          h->mgi.p, h->gchosen.p, st));
+            done = true;
+        }
+    }
+    if (!done)
+        HIPTRY(h, launch_greedy(h->shape, h->rec.p, N, h->gcnt.p, a, h->gbase.p, h->gleaf.p, P,
+                                pod_flags ? h->gflags.p : nullptr, h->gchosen.p, st, merge ? kGreedyRun : kGreedyBoth));
     if (P > 0) HIPTRY(h, hipMemcpyAsync(chosen, h->gchosen.p, sizeof(int64_t) * P, hipMemcpyDeviceToHost, st));
     HIPTRY(h, hipStreamSynchronize(st));
     for (int64_t p = 0; p < P; ++p)

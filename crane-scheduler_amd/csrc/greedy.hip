@@ -269,14 +269,16 @@ size_t greedy_lds_bytes(int64_t N, bool leaves_in_lds) {
 
 template <int PD, int PR>
 static hipError_t launch_greedy_t(const void* rec, int64_t N, uint32_t* cnt, const GreedyArgs& a, int64_t* base,
-                                  uint8_t* leaf, int64_t P, const uint8_t* flags, int64_t* chosen, hipStream_t st) {
+                                  uint8_t* leaf, int64_t P, const uint8_t* flags, int64_t* chosen, hipStream_t st,
+                                  int what) {
     if (N > kGreedyMaxNodes) return hipErrorInvalidValue;
-    if (N > 0) {
+    if (N > 0 && (what & kGreedyPrep)) {
         hipLaunchKernelGGL((greedy_prep<PD, PR>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st,
                            static_cast<const NodeRec<PD, PR>*>(rec), N, cnt, a, base, leaf);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
+    if (!(what & kGreedyRun)) return hipSuccess;
     const bool in_lds = greedy_lds_bytes(N, true) <= kGreedyLdsBytes;
     const size_t lds = greedy_lds_bytes(N, in_lds);
     int nlev = 0;
@@ -303,11 +305,11 @@ static hipError_t launch_greedy_t(const void* rec, int64_t N, uint32_t* cnt, con
 }
 
 hipError_t launch_greedy(int shape, const void* rec, int64_t N, uint32_t* cnt, const GreedyArgs& a, int64_t* base,
-                         uint8_t* leaf, int64_t P, const uint8_t* flags, int64_t* chosen, hipStream_t st) {
+                         uint8_t* leaf, int64_t P, const uint8_t* flags, int64_t* chosen, hipStream_t st, int what) {
     switch (shape) {
-        case kShape4x6: return launch_greedy_t<4, 6>(rec, N, cnt, a, base, leaf, P, flags, chosen, st);
-        case kShape8x8: return launch_greedy_t<8, 8>(rec, N, cnt, a, base, leaf, P, flags, chosen, st);
-        default: return launch_greedy_t<16, 16>(rec, N, cnt, a, base, leaf, P, flags, chosen, st);
+        case kShape4x6: return launch_greedy_t<4, 6>(rec, N, cnt, a, base, leaf, P, flags, chosen, st, what);
+        case kShape8x8: return launch_greedy_t<8, 8>(rec, N, cnt, a, base, leaf, P, flags, chosen, st, what);
+        default: return launch_greedy_t<16, 16>(rec, N, cnt, a, base, leaf, P, flags, chosen, st, what);
     }
 }
 

@@ -33,8 +33,32 @@ struct GreedyArgs {
     int64_t win_count[kMaxWin];
     int32_t win_inc[kMaxWin];  // a binding stamped now_unix falls in window w
 };
+// prep = G1 only (base, leaf); run = G2 only (expects G1's outputs); both = G1 + G2
+enum { kGreedyPrep = 1, kGreedyRun = 2, kGreedyBoth = 3 };
 hipError_t launch_greedy(int shape, const void* rec, int64_t N, uint32_t* cnt, const GreedyArgs& a, int64_t* base,
-                         uint8_t* leaf, int64_t P, const uint8_t* flags, int64_t* chosen, hipStream_t st);
+                         uint8_t* leaf, int64_t P, const uint8_t* flags, int64_t* chosen, hipStream_t st,
+                         int what = kGreedyBoth);
+
+// Merge form of the sequential greedy (merge.hip)
+struct MergeArgs {
+    int32_t n_win;
+    int32_t pad;
+    int64_t win_count[kMaxWin];  // all > 0 (else the sequential kernel runs)
+    int32_t win_inc[kMaxWin];    // a binding stamped now_unix falls in window w
+};
+// H [2][101] per-level element counts of the F (feasible) and I streams; flag != 0: use the sequential kernel
+hipError_t launch_merge_hist(const int64_t* base, const uint8_t* leaf, const uint32_t* cnt, int64_t N,
+                             const MergeArgs& a, int64_t capF, int64_t capI, unsigned long long* H, int32_t* flag,
+                             hipStream_t st);
+int64_t merge_bsum_len(int64_t N, int vlo);
+// stream [cap] packed (level << 32 | ~node) keys of stream T (0 = F, 1 = I), levels >= vlo; bs scratch [merge_bsum_len]
+hipError_t launch_merge_stream(const int64_t* base, const uint8_t* leaf, const uint32_t* cnt, int64_t N,
+                               const MergeArgs& a, int T, int vlo, int64_t cap, unsigned long long* bs,
+                               int64_t* stream, hipStream_t st);
+// scratch: apos [Pd], tk [P], gi [nI]
+hipError_t launch_merge_assign(const int64_t* Fs, int64_t nF, const int64_t* Is, int64_t nI, const uint8_t* flags,
+                               int64_t P, int64_t Pd, int32_t* apos, int32_t* tk, int64_t* gi, int64_t* chosen,
+                               hipStream_t st);
 
 // Bin-partitioned K2 (hotcount.hip)
 constexpr int kMaxBins = 4096;

@@ -1,0 +1,356 @@
+// merge.hip — config-5 sequential greedy as a merge of per-node score staircases.
+//
+// Sequential greedy (greedy.hip, oracle or_greedy): with one `now` for the
+// batch, pod p takes the node of highest (score, -index) among its candidates
+// (all nodes for a DaemonSet pod — plugins.go:41-43 — the feasible ones
+// otherwise), then a Binding{Timestamp: now} on that node raises its window
+// counts (binding.go:85-91), hot value Σ_w count_w / Count_w (node.go:113-121)
+// and penalty int(hv*10) (plugins.go:91).  Only the chosen node's score moves.
+//
+// With every Count_w > 0 the hot value, hence the penalty, is non-decreasing in
+// the number k of bindings a node has received in the batch, so each node's
+// score s_n(k) = clamp(base_n - 10 v_n(k), 0, 100) is a non-increasing
+// staircase in k.  Taking the max head of N non-increasing lists is a k-way
+// merge: the non-DaemonSet pods receive, in order, the elements of
+//   F = sort_desc{ (s_n(k), -n) : n feasible, k >= 0 },
+// and a DaemonSet pod takes the larger of the heads of F and of the analogous
+// stream I over the infeasible nodes.  Element i of I goes to the first
+// DaemonSet pod m (at pod position a_m, after the one that took i-1) with
+// a_m >= T_i = i + #{j : F[j] > I[i]}, i.e. m_i = i + prefix-max(g_i - i) with
+// g_i = first m with a_m >= T_i.  Every other pod p takes F[p - #(I-takers
+// before p)].  Results are identical to the sequential loop; the engine falls
+// back to greedy.hip when the staircase premise fails (a Count_w <= 0, or a
+// base score of int(NaN) whose int64 subtraction could wrap).
+//
+//   M1 hist   : per node, the staircase's runs (level, length) -> per-level
+//               element counts of F and I (capped at the pods that can use them)
+//   M2 bsum   : per 256-node block, per level >= the cut level, element counts
+//   M3 scan   : exclusive scan over (level desc, block asc)
+//   M4 place  : per level, block-wide scan of each node's run length -> the
+//               node's positions in F (or I); writes packed keys
+//   M5 assign : DaemonSet merge (a_m compaction, binary searches, prefix max,
+//               I-taker marks, pod-order scan) -> chosen node per pod
+#include <hip/hip_runtime.h>
+
+#include "dyn_types.hpp"
+#include "kernels.hpp"
+
+namespace crane {
+
+constexpr int kMT = 256;     // node-block size of M1, M2, M4
+constexpr int kM5T = 1024;   // single-workgroup kernels of M5
+constexpr int kLevels = 101; // scores 0..100
+
+__device__ __forceinline__ int64_t stair_v(const uint32_t* c, int64_t k, const MergeArgs& a) {
+    int64_t v = 0;
+    for (int w = 0; w < a.n_win; ++w) v += ((int64_t)c[w] + (a.win_inc[w] ? k : 0)) / a.win_count[w];
+    return v;
+}
+
+// Runs of a node's staircase s(k), k = 0 .. cap-1, in order (levels non-increasing).
+struct RunIter {
+    int64_t base, k, cap;
+    uint32_t c[kMaxWin];
+    __device__ bool next(const MergeArgs& a, int& lvl, int64_t& len) {
+        if (k >= cap) return false;
+        const int64_t f = base - 10 * stair_v(c, k, a);  // no wrap: base >= INT64_MIN + 2^40 (M1 flag)
+        lvl = (int)(f < 0 ? 0 : (f > 100 ? 100 : f));
+        int64_t d = INT64_MAX;
+        if (lvl > 0)
+            for (int w = 0; w < a.n_win; ++w)
+                if (a.win_inc[w]) {
+                    const int64_t C = a.win_count[w];
+                    d = min(d, C - ((int64_t)c[w] + k) % C);  // bindings until this window's quotient grows
+                }
+        len = min(d, cap - k);
+        k += len;
+        return true;
+    }
+};
+
+__device__ __forceinline__ RunIter make_iter(const int64_t* base, const uint32_t* cnt, int64_t N, int64_t n,
+                                             int64_t cap, const MergeArgs& a) {
+    RunIter it;
+    it.base = base[n];
+    it.k = 0;
+    it.cap = cap;
+    for (int w = 0; w < kMaxWin; ++w) it.c[w] = w < a.n_win ? cnt[(int64_t)w * N + n] : 0u;
+    return it;
+}
+
+__device__ __forceinline__ int64_t pack_level_key(int u, int64_t n) {
+    return ((int64_t)u << 32) | (int64_t)(0xFFFFFFFFull - (uint64_t)n);
+}
+
+// ---- block scans (256 threads)
+__device__ __forceinline__ unsigned long long block_excl_scan_u64(unsigned long long v, unsigned long long* lds4,
+                                                                  unsigned long long* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned long long x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds4[w] = x;
+    __syncthreads();
+    unsigned long long pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kMT / 64; ++i) {
+        if (i < w) pre += lds4[i];
+        tot += lds4[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return pre + x - v;
+}
+
+// ---------------------------------------------------------------- M1
+__global__ __launch_bounds__(kMT) void m1_hist(const int64_t* __restrict__ base, const uint8_t* __restrict__ leaf,
+                                               const uint32_t* __restrict__ cnt, int64_t N, MergeArgs a,
+                                               int64_t capF, int64_t capI, unsigned long long* __restrict__ H,
+                                               int32_t* __restrict__ flag) {
+    __shared__ unsigned long long lh[2 * kLevels];
+    for (int i = threadIdx.x; i < 2 * kLevels; i += kMT) lh[i] = 0;
+    __syncthreads();
+    const int64_t n = (int64_t)blockIdx.x * kMT + threadIdx.x;
+    if (n < N) {
+        if (base[n] < INT64_MIN + (1LL << 40)) atomicOr(flag, 1);  // int(NaN) base: s_n(k) may rise
+        const int T = (leaf[n] & 0x80) ? 0 : 1;
+        RunIter it = make_iter(base, cnt, N, n, T ? capI : capF, a);
+        int lvl;
+        int64_t len;
+        while (it.next(a, lvl, len)) atomicAdd(&lh[T * kLevels + lvl], (unsigned long long)len);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * kLevels; i += kMT)
+        if (lh[i]) atomicAdd(&H[i], lh[i]);
+}
+
+// ---------------------------------------------------------------- M2
+__global__ __launch_bounds__(kMT) void m2_bsum(const int64_t* __restrict__ base, const uint8_t* __restrict__ leaf,
+                                               const uint32_t* __restrict__ cnt, int64_t N, MergeArgs a, int T,
+                                               int vlo, int64_t cap, unsigned long long* __restrict__ bs) {
+    __shared__ unsigned long long ls[kLevels];
+    for (int i = threadIdx.x; i < kLevels; i += kMT) ls[i] = 0;
+    __syncthreads();
+    const int64_t n = (int64_t)blockIdx.x * kMT + threadIdx.x;
+    if (n < N && ((leaf[n] & 0x80) ? 0 : 1) == T) {
+        RunIter it = make_iter(base, cnt, N, n, cap, a);
+        int lvl;
+        int64_t len;
+        while (it.next(a, lvl, len) && lvl >= vlo) atomicAdd(&ls[100 - lvl], (unsigned long long)len);
+    }
+    __syncthreads();
+    const int L = 101 - vlo;
+    for (int r = threadIdx.x; r < L; r += kMT) bs[(int64_t)r * gridDim.x + blockIdx.x] = ls[r];
+}
+
+// ---------------------------------------------------------------- M3 (one workgroup)
+__global__ __launch_bounds__(kM5T) void m3_scan(unsigned long long* __restrict__ v, int64_t len) {
+    __shared__ unsigned long long part[kM5T];
+    const int64_t per = (len + kM5T - 1) / kM5T;
+    const int64_t lo = threadIdx.x * per, hi = min(len, lo + per);
+    unsigned long long s = 0;
+    for (int64_t i = lo; i < hi; ++i) s += v[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < kM5T; off <<= 1) {
+        const unsigned long long y = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += y;
+        __syncthreads();
+    }
+    unsigned long long run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+    for (int64_t i = lo; i < hi; ++i) {
+        const unsigned long long x = v[i];
+        v[i] = run;
+        run += x;
+    }
+}
+
+// ---------------------------------------------------------------- M4
+__global__ __launch_bounds__(kMT) void m4_place(const int64_t* __restrict__ base, const uint8_t* __restrict__ leaf,
+                                                const uint32_t* __restrict__ cnt, int64_t N, MergeArgs a, int T,
+                                                int vlo, int64_t cap, const unsigned long long* __restrict__ off,
+                                                int64_t* __restrict__ stream) {
+    __shared__ unsigned long long lds4[kMT / 64];
+    const int64_t n = (int64_t)blockIdx.x * kMT + threadIdx.x;
+    const bool mine = n < N && ((leaf[n] & 0x80) ? 0 : 1) == T;
+    RunIter it = make_iter(base, cnt, N, mine ? n : 0, mine ? cap : 0, a);
+    int lvl = -1;
+    int64_t len = 0;
+    bool have = mine && it.next(a, lvl, len);
+    for (int u = 100; u >= vlo; --u) {
+        unsigned long long c = 0;
+        while (have && lvl == u) {
+            c += (unsigned long long)len;
+            have = it.next(a, lvl, len);
+        }
+        unsigned long long tot;
+        const unsigned long long ex = block_excl_scan_u64(c, lds4, &tot);
+        if (c) {
+            const unsigned long long p0 = off[(int64_t)(100 - u) * gridDim.x + blockIdx.x] + ex;
+            const unsigned long long p1 = min(p0 + c, (unsigned long long)cap);
+            for (unsigned long long p = p0; p < p1; ++p) stream[p] = pack_level_key(u, n);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- M5
+// M5a: positions a[m] of the DaemonSet pods (pod order); zero the I-taker marks
+__global__ __launch_bounds__(kM5T) void m5a_compact(const uint8_t* __restrict__ flags, int64_t P,
+                                                    int32_t* __restrict__ apos, int32_t* __restrict__ tk) {
+    __shared__ int32_t wc[kM5T / 64];
+    int32_t run = 0;
+    for (int64_t t0 = 0; t0 < P; t0 += kM5T) {
+        const int64_t p = t0 + threadIdx.x;
+        const bool d = p < P && (flags[p] & 1u);
+        if (p < P) tk[p] = 0;
+        const uint64_t m = __ballot(d);
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        if (lane == 0) wc[w] = __popcll(m);
+        __syncthreads();
+        int32_t pre = 0, tot = 0;
+        for (int i = 0; i < kM5T / 64; ++i) {
+            if (i < w) pre += wc[i];
+            tot += wc[i];
+        }
+        if (d) apos[run + pre + __popcll(m & ((1ull << lane) - 1))] = (int32_t)p;
+        run += tot;
+        __syncthreads();
+    }
+}
+
+// M5b: per I element i, g_i - i where g_i = first DaemonSet pod m with a_m >= T_i
+__global__ __launch_bounds__(kMT) void m5b_thresholds(const int64_t* __restrict__ Fs, int64_t nF,
+                                                      const int64_t* __restrict__ Is, int64_t nI,
+                                                      const int32_t* __restrict__ apos, int64_t Pd,
+                                                      int64_t* __restrict__ gi) {
+    const int64_t i = (int64_t)blockIdx.x * kMT + threadIdx.x;
+    if (i >= nI) return;
+    const int64_t key = Is[i];
+    int64_t lo = 0, hi = nF;  // first j with Fs[j] < key (Fs descending)
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (Fs[mid] < key) hi = mid;
+        else lo = mid + 1;
+    }
+    const int64_t T = i + lo;
+    int64_t l2 = 0, h2 = Pd;  // first m with apos[m] >= T
+    while (l2 < h2) {
+        const int64_t mid = (l2 + h2) >> 1;
+        if ((int64_t)apos[mid] >= T) h2 = mid;
+        else l2 = mid + 1;
+    }
+    gi[i] = l2 - i;
+}
+
+// M5c: m_i = i + prefix-max(g_i - i); mark tk[a_{m_i}] = i + 1 for m_i < Pd (one workgroup)
+__global__ __launch_bounds__(kM5T) void m5c_takers(const int64_t* __restrict__ gi, int64_t nI,
+                                                   const int32_t* __restrict__ apos, int64_t Pd,
+                                                   int32_t* __restrict__ tk) {
+    __shared__ int64_t part[kM5T];
+    const int64_t per = (nI + kM5T - 1) / kM5T;
+    const int64_t lo = threadIdx.x * per, hi = min(nI, lo + per);
+    int64_t s = INT64_MIN;
+    for (int64_t i = lo; i < hi; ++i) s = max(s, gi[i]);
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < kM5T; off <<= 1) {
+        const int64_t y = threadIdx.x >= off ? part[threadIdx.x - off] : INT64_MIN;
+        __syncthreads();
+        part[threadIdx.x] = max(part[threadIdx.x], y);
+        __syncthreads();
+    }
+    int64_t run = threadIdx.x ? part[threadIdx.x - 1] : INT64_MIN;
+    for (int64_t i = lo; i < hi; ++i) {
+        run = max(run, gi[i]);
+        const int64_t m = i + run;
+        if (m < Pd) tk[apos[m]] = (int32_t)(i + 1);
+    }
+}
+
+// M5d: pod order scan of the I-taker marks -> chosen node per pod (one workgroup)
+__global__ __launch_bounds__(kM5T) void m5d_assign(const int64_t* __restrict__ Fs, int64_t nF,
+                                                   const int64_t* __restrict__ Is, const int32_t* __restrict__ tk,
+                                                   int64_t P, int64_t* __restrict__ chosen) {
+    __shared__ int32_t wc[kM5T / 64];
+    int64_t run = 0;
+    for (int64_t t0 = 0; t0 < P; t0 += kM5T) {
+        const int64_t p = t0 + threadIdx.x;
+        const int32_t t = p < P ? tk[p] : 0;
+        const uint64_t m = __ballot(t > 0);
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        if (lane == 0) wc[w] = __popcll(m);
+        __syncthreads();
+        int32_t pre = 0, tot = 0;
+        for (int i = 0; i < kM5T / 64; ++i) {
+            if (i < w) pre += wc[i];
+            tot += wc[i];
+        }
+        if (p < P) {
+            int64_t key = -1;
+            if (t > 0) key = Is[t - 1];
+            else {
+                const int64_t j = p - (run + pre + __popcll(m & ((1ull << lane) - 1)));
+                if (j < nF) key = Fs[j];
+            }
+            chosen[p] = key < 0 ? -1 : (int64_t)(0xFFFFFFFFull - ((uint64_t)key & 0xFFFFFFFFull));
+        }
+        run += tot;
+        __syncthreads();
+    }
+}
+
+// no DaemonSet pods: pod p takes F[p]
+__global__ __launch_bounds__(kMT) void m5z_direct(const int64_t* __restrict__ Fs, int64_t nF, int64_t P,
+                                                  int64_t* __restrict__ chosen) {
+    const int64_t p = (int64_t)blockIdx.x * kMT + threadIdx.x;
+    if (p >= P) return;
+    chosen[p] = p < nF ? (int64_t)(0xFFFFFFFFull - ((uint64_t)Fs[p] & 0xFFFFFFFFull)) : -1;
+}
+
+// ---------------------------------------------------------------- launchers
+hipError_t launch_merge_hist(const int64_t* base, const uint8_t* leaf, const uint32_t* cnt, int64_t N,
+                             const MergeArgs& a, int64_t capF, int64_t capI, unsigned long long* H, int32_t* flag,
+                             hipStream_t st) {
+    hipError_t e = hipMemsetAsync(H, 0, sizeof(unsigned long long) * 2 * kLevels, st);
+    if (e == hipSuccess) e = hipMemsetAsync(flag, 0, sizeof(int32_t), st);
+    if (e != hipSuccess) return e;
+    if (N > 0)
+        hipLaunchKernelGGL(m1_hist, dim3((unsigned)((N + kMT - 1) / kMT)), dim3(kMT), 0, st, base, leaf, cnt, N, a,
+                           capF, capI, H, flag);
+    return hipGetLastError();
+}
+
+int64_t merge_bsum_len(int64_t N, int vlo) { return (int64_t)(101 - vlo) * ((N + kMT - 1) / kMT); }
+
+hipError_t launch_merge_stream(const int64_t* base, const uint8_t* leaf, const uint32_t* cnt, int64_t N,
+                               const MergeArgs& a, int T, int vlo, int64_t cap, unsigned long long* bs,
+                               int64_t* stream, hipStream_t st) {
+    if (N <= 0 || cap <= 0) return hipSuccess;
+    const unsigned nb = (unsigned)((N + kMT - 1) / kMT);
+    hipLaunchKernelGGL(m2_bsum, dim3(nb), dim3(kMT), 0, st, base, leaf, cnt, N, a, T, vlo, cap, bs);
+    hipLaunchKernelGGL(m3_scan, dim3(1), dim3(kM5T), 0, st, bs, merge_bsum_len(N, vlo));
+    hipLaunchKernelGGL(m4_place, dim3(nb), dim3(kMT), 0, st, base, leaf, cnt, N, a, T, vlo, cap, bs, stream);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_assign(const int64_t* Fs, int64_t nF, const int64_t* Is, int64_t nI, const uint8_t* flags,
+                               int64_t P, int64_t Pd, int32_t* apos, int32_t* tk, int64_t* gi, int64_t* chosen,
+                               hipStream_t st) {
+    if (P <= 0) return hipSuccess;
+    if (Pd == 0 || nI == 0) {  // no DaemonSet pod can take an infeasible node: pod p takes F[p]
+        hipLaunchKernelGGL(m5z_direct, dim3((unsigned)((P + kMT - 1) / kMT)), dim3(kMT), 0, st, Fs, nF, P, chosen);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(m5a_compact, dim3(1), dim3(kM5T), 0, st, flags, P, apos, tk);
+    hipLaunchKernelGGL(m5b_thresholds, dim3((unsigned)((nI + kMT - 1) / kMT)), dim3(kMT), 0, st, Fs, nF, Is, nI,
+                       apos, Pd, gi);
+    hipLaunchKernelGGL(m5c_takers, dim3(1), dim3(kM5T), 0, st, gi, nI, apos, Pd, tk);
+    hipLaunchKernelGGL(m5d_assign, dim3(1), dim3(kM5T), 0, st, Fs, nF, Is, tk, P, chosen);
+    return hipGetLastError();
+}
+
+}  // namespace crane

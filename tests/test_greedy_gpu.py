@@ -15,6 +15,13 @@ from helpers import engine_for  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 
+@pytest.fixture(autouse=True, params=["merge", "seq"])
+def greedy_mode(request, monkeypatch):
+    """merge: merge.hip (default); seq: the one-workgroup sequential kernel (greedy.hip)."""
+    monkeypatch.setenv("CRANE_GREEDY", request.param)
+    return request.param
+
+
 def _oracle(spec, c, P, now):
     return O.greedy(spec, c.metric_names, c.ok, c.val, np.where(c.ok == 1, c.ts, 0), c.b_node, c.b_ts, now, P,
                     c.ds[:P])
@@ -69,3 +76,72 @@ def test_greedy_then_eval_consistent():
     _, _, ch, _ = eng.eval(c.now, c.ds)
     from helpers import oracle_soa
     assert np.array_equal(ch, oracle_soa(spec, c, want_matrix=False)[2])
+
+
+@pytest.mark.parametrize("ds_frac,feas_all", [(0.0, False), (1.0, False), (0.3, False), (0.02, True)])
+def test_greedy_daemonset_mixes(ds_frac, feas_all):
+    """DaemonSet pods take the best of the feasible (F) and infeasible (I) streams."""
+    spec = cd.default_policy_spec()
+    if feas_all:
+        spec = dict(spec, predicate=[])
+    N, P = 3000, 4000
+    c = synth.make_cluster(spec, N, P, n_bindings=30000, seed=61, ds_frac=ds_frac)
+    now = int(synth.NOW0_NS)
+    eng = engine_for(spec, c)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    assert np.array_equal(eng.greedy(P, now, c.ds), _oracle(spec, c, P, now))
+
+
+def test_greedy_no_feasible_node():
+    """Every node overloaded: non-DaemonSet pods get -1, DaemonSet pods still place."""
+    spec = dict(cd.default_policy_spec(), predicate=[("cpu_usage_avg_5m", 1e-9)])
+    N, P = 200, 500
+    c = synth.make_cluster(spec, N, P, n_bindings=2000, seed=62, ds_frac=0.2, invalid=False)
+    c.ts[:] = synth.NOW0_NS  # all fresh, so every node is over the tiny limit
+    now = int(synth.NOW0_NS)
+    eng = engine_for(spec, c)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    ch = eng.greedy(P, now, c.ds)
+    assert np.array_equal(ch, _oracle(spec, c, P, now))
+    assert (ch[c.ds[:P] == 0] == -1).all()
+
+
+def test_greedy_many_pods_per_node():
+    """P >> N: every node runs down its staircase to score 0."""
+    spec = cd.default_policy_spec()
+    N, P = 37, 3000
+    c = synth.make_cluster(spec, N, P, n_bindings=500, seed=63, ds_frac=0.05)
+    now = int(synth.NOW0_NS)
+    eng = engine_for(spec, c)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    assert np.array_equal(eng.greedy(P, now, c.ds), _oracle(spec, c, P, now))
+
+
+def test_greedy_windows_shapes():
+    """Zero-length window (bindings stamped now never count), several counts, one window."""
+    m = 60 * 10**9
+    base = cd.default_policy_spec()
+    for i, hot in enumerate([[(0, 2), (5 * m, 5)], [(5 * m, 3), (1 * m, 7), (10 * m, 1)], [(2 * m, 1)]]):
+        spec = dict(base, hotValue=hot)
+        c = synth.make_cluster(spec, 800, 1500, n_bindings=20000, seed=70 + i, ds_frac=0.05)
+        now = int(synth.NOW0_NS)
+        eng = engine_for(spec, c)
+        eng.upload_bindings(c.b_node, c.b_ts)
+        assert np.array_equal(eng.greedy(1500, now, c.ds), _oracle(spec, c, 1500, now)), i
+
+
+@pytest.mark.slow
+def test_greedy_config5_merge_equals_sequential(greedy_mode, monkeypatch):
+    """BASELINE config 5 size (100k nodes x 50k pods): merge form == sequential kernel, bit for bit."""
+    if greedy_mode != "merge":
+        pytest.skip("compares both modes itself")
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 100_000, 50_000, n_bindings=1_000_000, seed=20255215)
+    now = int(synth.NOW0_NS)
+    eng = engine_for(spec, c)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    a = eng.greedy(50_000, now, c.ds)
+    monkeypatch.setenv("CRANE_GREEDY", "seq")
+    b = eng.greedy(50_000, now, c.ds)
+    assert np.array_equal(a, b)
+    assert (a >= 0).all()
