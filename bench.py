@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16, help="upstream kube-scheduler parallelism")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-greedy", action="store_true", help="skip the config-5 sequential-greedy measurement")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as a captured graph (measured slower than eager launches on ROCm 7.2)")
     return ap.parse_args()
 
 
@@ -84,7 +86,7 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
-    def step(e=None):
+    def step(e=None, collective=True):
         if e:
             e[0].record(stream)
         eng.refresh_hot_values_async(now_sync, now_sync, sh)   # K2
@@ -94,7 +96,7 @@ def main():
         eng.eval_keys_async(d_now, d_flags, d_keys, sh)         # K3 (+ key init)
         if e:
             e[2].record(stream)
-        if world > 1:
+        if world > 1 and collective:
             dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)       # RCCL over xGMI
         if e:
             e[3].record(stream)
@@ -102,12 +104,34 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    # per-stage times from an eager pass with HIP events on the engine's stream
+    for k in range(args.steps):
+        step(ev[k])
+    torch.cuda.synchronize(dev)
+    graph = None
+    if args.graph:
+        # one scheduling batch = one graph replay: K2 + K1 + K3 launches captured once,
+        # inputs (pods, binding log, node SoA) stay in device buffers updated in place
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            step(collective=False)
+        graph.replay()
+        torch.cuda.synchronize(dev)
+
+    def timed_step():
+        if graph is None:
+            step()
+        else:
+            graph.replay()
+            if world > 1:
+                dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)  # RCCL over xGMI
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(ev[k])
+        timed_step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -198,7 +222,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"config{args.config}: {N} nodes/GPU x {P} pods, 6 metrics, hot values from "
                                    f"{B}-entry binding log per GPU, README default policy",
-                       "nodes_per_gpu": N, "pods": P, "bindings_per_gpu": B, "parallelism": f"node-shard x{world}"},
+                       "nodes_per_gpu": N, "pods": P, "bindings_per_gpu": B, "parallelism": f"node-shard x{world}",
+                       "launch": "eager" if graph is None else "hipGraph replay per batch"},
             "placements_per_s": round(placements, 1),
             "kernel_ms": {"k2_k1": round(k12_ms, 4), "k3": round(k3_ms, 4), "allreduce": round(ar_ms, 4)},
             "roofline": roof,

@@ -99,8 +99,7 @@ struct crane_dyn {
     DevBuf<int8_t> ff;
     DevBuf<int64_t> score;
     DevBuf<uint32_t> k2_cnt, k2_tot, k2_sorted;  // bin-partitioned K2 scratch
-    DevBuf<uint32_t> k2_cur;                      // two-kernel K2: [2][nbins] bin cursors
-    int32_t k2p_nbins = -1, k2p_parity = 0;
+    DevBuf<uint32_t> k2_cur;                      // two-kernel K2: [nbins] bin cursors
     DevBuf<uint32_t> gcnt;  // greedy: per-window counts [W][N]
     DevBuf<int64_t> gbase, gchosen;
     DevBuf<uint8_t> gleaf, gflags;
@@ -366,18 +365,12 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     if (mode == "part" && gp.ok) {
         // two kernels adding into zeroed buckets (K1 zeroes what it consumed)
         if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
-        if (gp.nbins != h->k2p_nbins || !h->k2_cur.p) {
-            HIPTRY(h, h->k2_cur.reserve((size_t)2 * gp.nbins));
-            HIPTRY(h, hipMemsetAsync(h->k2_cur.p, 0, sizeof(uint32_t) * 2 * gp.nbins, st));
-            h->k2p_nbins = gp.nbins;
-            h->k2p_parity = 0;
-        }
+        // bin cursors reset in-stream, so the launch sequence can be captured in a graph and replayed
+        HIPTRY(h, h->k2_cur.reserve((size_t)gp.nbins));
+        HIPTRY(h, hipMemsetAsync(h->k2_cur.p, 0, sizeof(uint32_t) * gp.nbins, st));
         HIPTRY(h, h->k2_sorted.reserve((size_t)gp.nbins * (size_t)gp.cap));
-        uint32_t* cur = h->k2_cur.p + (size_t)h->k2p_parity * gp.nbins;
-        uint32_t* nxt = h->k2_cur.p + (size_t)(h->k2p_parity ^ 1) * gp.nbins;
-        HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, cur, nxt,
+        HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, h->k2_cur.p,
                                         h->k2_sorted.p, st));
-        h->k2p_parity ^= 1;
         h->buckets_zero = false;
         h->hv_from_counts = true;
         h->hv_ts_counts = hv_ts_ns;

@@ -163,21 +163,18 @@ __global__ __launch_bounds__(kHT) void k2d_bin_hist(const uint32_t* __restrict__
 // Y  bin_hist  : kYSplits workgroups per bin, each an LDS histogram [W][2^bb]
 //                of a contiguous slice of the bin's entries, flushed with
 //                contiguous atomics into the (zeroed) buckets.
-// The per-bin cursors alternate between two arrays; X zeroes the idle one for
-// the next refresh.
+// The per-bin cursors are zeroed by a memset in the same stream before X.
 constexpr int kXPer = 8;     // bindings per thread in X
 constexpr int kYSplits = 8;  // workgroups per bin in Y
 
 __global__ __launch_bounds__(kHT) void k2x_partition(const int32_t* __restrict__ bnode,
                                                      const int64_t* __restrict__ bts, int64_t B, int64_t N,
                                                      HotCutoffs cut, HotPart g, uint32_t* __restrict__ cur,
-                                                     uint32_t* __restrict__ cur_next, uint32_t* __restrict__ region) {
+                                                     uint32_t* __restrict__ region) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];  // hist [nbins], base [nbins]
     uint32_t* hist = sh;
     uint32_t* base = sh + g.nbins;
     for (int i = threadIdx.x; i < g.nbins; i += kHT) hist[i] = 0;
-    if (blockIdx.x == 0)
-        for (int i = threadIdx.x; i < g.nbins; i += kHT) cur_next[i] = 0;
     __syncthreads();
     const int64_t b0 = (int64_t)blockIdx.x * (kHT * kXPer) + threadIdx.x;
     int32_t nd[kXPer];
@@ -261,12 +258,12 @@ HotPart hot_part_geometry(int64_t B, int64_t N, int32_t W) {
 
 hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                  const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* cur,
-                                 uint32_t* cur_next, uint32_t* region, hipStream_t st) {
+                                 uint32_t* region, hipStream_t st) {
     static const hipError_t attr =
         hipFuncSetAttribute((const void*)k2y_bin_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
     if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(k2x_partition, dim3(g.nblk), dim3(kHT), sizeof(uint32_t) * 2 * g.nbins, st, bnode, bts, B, N,
-                       cut, g, cur, cur_next, region);
+                       cut, g, cur, region);
     const size_t lds = sizeof(uint32_t) * (size_t)cut.n_win * ((size_t)1 << g.bb);
     hipLaunchKernelGGL(k2y_bin_hist, dim3(g.nbins, kYSplits), dim3(kHT), lds, st, region, cur, g, cut.n_win, N,
                        buckets);

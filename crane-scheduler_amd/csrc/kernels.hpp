@@ -82,11 +82,11 @@ struct HotPart {
     bool ok;
 };
 HotPart hot_part_geometry(int64_t B, int64_t N, int32_t W);
-// cur/cur_next: [nbins] cursors (cur zero on entry; cur_next zeroed here), region [nbins * cap].
+// cur: [nbins] cursors, zero on entry; region [nbins * cap].
 // Adds into buckets[W][N], which must be zero on entry.
 hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                  const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* cur,
-                                 uint32_t* cur_next, uint32_t* region, hipStream_t st);
+                                 uint32_t* region, hipStream_t st);
 
 // K3 step path (step.hip): per-batch node step tables + pair eval.
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
