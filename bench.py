@@ -30,7 +30,6 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VALU_PEAK_GOPS = 256 * 4 * 32 * 2.4  # lane-ops/ns: 256 CUs x 4 SIMD32 x 2.4 GHz (fp64 add/mul full rate)
 
 
 def parse():
@@ -89,11 +88,10 @@ def main():
     def step(e=None, collective=True):
         if e:
             e[0].record(stream)
-        eng.refresh_hot_values_async(now_sync, now_sync, sh)   # K2
-        eng.node_pass_async(sh)                                 # K1
+        eng.refresh_hot_values_async(now_sync, now_sync, sh)   # K2 (k2x, k2y)
         if e:
             e[1].record(stream)
-        eng.eval_keys_async(d_now, d_flags, d_keys, sh)         # K3 (+ key init)
+        eng.eval_keys_async(d_now, d_flags, d_keys, sh)         # K3p, K1+K3a (fused node pass), K3s
         if e:
             e[2].record(stream)
         if world > 1 and collective:
@@ -104,9 +102,15 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    # per-stage times from an eager pass with HIP events on the engine's stream
+    # per-stage times from eager passes: HIP events around the engine calls, and the
+    # engine's own per-kernel events (crane_dyn_set_profiling) on the same stream
+    eng.set_profiling(True)
+    stages = {}
     for k in range(args.steps):
         step(ev[k])
+        for name, t in eng.stage_times():
+            stages.setdefault(name, []).append(t)
+    eng.set_profiling(False)
     torch.cuda.synchronize(dev)
     graph = None
     if args.graph:
@@ -141,34 +145,46 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_step = elapsed * 1e3 / args.steps
-    k12_ms = float(np.mean([a.elapsed_time(b) for a, b, _, _ in ev]))
+    k2_ms = float(np.mean([a.elapsed_time(b) for a, b, _, _ in ev]))
     k3_ms = float(np.mean([b.elapsed_time(c_) for _, b, c_, _ in ev]))
     ar_ms = float(np.mean([c_.elapsed_time(d) for _, _, c_, d in ev]))
+    stage_ms = {k: float(np.mean(v)) for k, v in stages.items()}
 
     keys = d_keys.cpu().numpy()
     evals = P * N * world
     value = evals / (ms_step / 1e3)
     placements = P / (ms_step / 1e3)
 
-    # roofline of the dominant kernel (K3): VALU issue bound.  Instructions per
-    # (pod, node) come from the shipped code object's loop body.
-    info_path = os.path.join(ROOT, "crane-scheduler_amd", "lib", "k3_isa.json")
-    isa = json.load(open(info_path)) if os.path.exists(info_path) else {}
-    variant = os.environ.get("CRANE_K3_VARIANT", str(isa.get("default_variant", 4)))
-    valu_per_eval = isa.get("variants", {}).get(variant, {}).get("valu_per_node")
+    # Rooflines per kernel stage: ALGORITHMIC bytes per launch / the
+    # stage's mean duration from the engine's HIP events above.  The dominant stage is `roofline`.
+    M = len(eng.metric_names)
+    W = len(spec["hotValue"])
+    PD, PR = len(spec["predicate"]), len(spec["priority"])
+    pd_, pr_ = (4, 6) if PD <= 4 and PR <= 6 else ((8, 8) if PD <= 8 and PR <= 8 else (16, 16))
+    rec_bytes = -(-(24 + 16 * pr_ + 8 + 8 * pd_) // 16) * 16  # sizeof(NodeRec<PD,PR>)
+    max_tr_s = max(tr for tr, _ in spec["hotValue"]) // 10**9
+    b_in = int((c.b_ts > now_sync // 10**9 - max_tr_s).sum())  # bindings inside the widest window
+    alg = {
+        "k2x_partition": (B * 12 + b_in * 4, "bindings read (int32 node + int64 ts) + kept entries written"),
+        "k2y_bin_hist": (b_in * 4 + 4 * W * N, "kept entries read + window counts added"),
+        "k1_node_pass+k3a_steps": (N * (16 * M + 8 * W + rec_bytes + 8),
+                                   "SoA (value, ts) read + buckets read and zeroed + NodeRec + hot value written"),
+        "k1_node_pass": (N * (16 * M + 8 * W + rec_bytes + 8), "as above"),
+        "k3p_pods": (P * (8 + 1 + 4 + 8 + 8), "pod now + flag read, partition + keys written"),
+    }
+    roofs = {}
+    for name, t in stage_ms.items():
+        if name in alg and t > 0:
+            gbs = alg[name][0] / (t * 1e-3) / 1e9
+            roofs[name] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(gbs / HBM_PEAK_GBS, 4), "ms": round(t, 4),
+                           "alg_bytes": int(alg[name][0]), "bytes": alg[name][1]}
+    dom = max(stage_ms, key=stage_ms.get) if stage_ms else None
     roof = None
-    if valu_per_eval:
-        achieved = valu_per_eval * P * N / (k3_ms * 1e-3) / 1e12  # Tops/s (lane-ops)
-        peak = VALU_PEAK_GOPS / 1e3
-        roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "Tlane-op/s",
-                "frac": round(achieved / peak, 4), "traffic": None, "kernel": f"k3_eval<4,6,false,{variant}>",
-                "valu_per_eval": valu_per_eval}
-    # node pass + hot values: HBM-bound streaming kernels (algorithmic bytes)
-    rec_bytes = 144
-    k1_bytes = N * (len(eng.metric_names) * 16 + 2 * 4 + rec_bytes)
-    k2_bytes = B * 12 + 2 * 4 * N
-    stream_gbs = (k1_bytes + k2_bytes) / (k12_ms * 1e-3) / 1e9
-
+    if dom in roofs:
+        roof = dict(roofs[dom], kernel=dom, traffic=None)
+    elif dom:
+        roof = {"bound": None, "kernel": dom, "ms": round(stage_ms[dom], 4), "note": "no HBM roofline for this stage"}
     greedy = None
     if world == 1 and not args.no_greedy:
         # BASELINE config 5: 100k nodes x 50k pods placed sequentially, each binding
@@ -225,10 +241,11 @@ def main():
                        "nodes_per_gpu": N, "pods": P, "bindings_per_gpu": B, "parallelism": f"node-shard x{world}",
                        "launch": "eager" if graph is None else "hipGraph replay per batch"},
             "placements_per_s": round(placements, 1),
-            "kernel_ms": {"k2_k1": round(k12_ms, 4), "k3": round(k3_ms, 4), "allreduce": round(ar_ms, 4)},
+            "kernel_ms": {"refresh_k2": round(k2_ms, 4), "eval_k3p_k1_k3s": round(k3_ms, 4),
+                          "allreduce": round(ar_ms, 4)},
+            "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
             "roofline": roof,
-            "roofline_stream": {"bound": "hbm", "kernels": "k2_hot_count+k1_node_pass", "achieved": round(stream_gbs, 1),
-                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(stream_gbs / HBM_PEAK_GBS, 4)},
+            "roofline_stages": roofs,
             "cpu_baseline": cpu,
             "greedy": greedy,
             "chosen_sample": [int(x) for x in keys[:4]],

@@ -68,6 +68,8 @@ def _load():
         "crane_dyn_refresh_hot_values_async": (C.c_int, [vp, C.c_int64, C.c_int64, vp]),
         "crane_dyn_node_pass_async": (C.c_int, [vp, vp]),
         "crane_dyn_greedy": (C.c_int, [vp, C.c_int64, C.c_int64, vp, vp]),
+        "crane_dyn_set_profiling": (C.c_int, [vp, C.c_int]),
+        "crane_dyn_stage_times": (C.c_int, [vp, C.c_int32, P(C.c_char_p), P(C.c_double)]),
         "crane_dyn_key_node": (C.c_int64, [C.c_int64, P(C.c_int64)]),
         "crane_dyn_version": (C.c_char_p, []),
     }
@@ -87,6 +89,7 @@ ABI_SYMBOLS = (
     "crane_dyn_num_metrics", "crane_dyn_metric_name", "crane_dyn_upload_nodes", "crane_dyn_upload_bindings",
     "crane_dyn_refresh_hot_values", "crane_dyn_eval", "crane_dyn_eval_keys_async",
     "crane_dyn_refresh_hot_values_async", "crane_dyn_node_pass_async", "crane_dyn_greedy", "crane_dyn_key_node",
+    "crane_dyn_set_profiling", "crane_dyn_stage_times",
     "crane_dyn_version",
 )
 
@@ -289,6 +292,19 @@ class Engine:
         self._check(lib.crane_dyn_eval_keys_async(self.h, P, C.c_void_p(d_now.data_ptr()),
                                                   None if d_flags is None else C.c_void_p(d_flags.data_ptr()),
                                                   C.c_void_p(d_keys.data_ptr()), stream))
+
+    # stage timing: HIP events the engine records after each kernel stage
+    def set_profiling(self, on=True):
+        self._check(lib.crane_dyn_set_profiling(self.h, 1 if on else 0))
+
+    def stage_times(self, max_stages=64):
+        """[(stage name, ms)] of the stages enqueued since the last call (waits for them)."""
+        names = (C.c_char_p * max_stages)()
+        ms = (C.c_double * max_stages)()
+        n = lib.crane_dyn_stage_times(self.h, max_stages, names, ms)
+        if n < 0:
+            self._check(n)
+        return [(names[i].decode(), ms[i]) for i in range(n)]
 
     def greedy(self, n_pods, now_ns, pod_flags=None):
         fl = None if pod_flags is None else np.ascontiguousarray(pod_flags, np.uint8)

@@ -85,6 +85,9 @@ struct crane_dyn {
     int64_t hv_ts_counts = 0;
     bool rec_dirty = true;
     bool buckets_zero = false;  // K1 consumes (zeroes) the buckets K2 filled
+    bool counts_pending = false;  // buckets hold K2 counts no node pass has consumed yet
+    bool cur_zero = false;        // K2 bin cursors are zero
+    int32_t cur_n = 0;            // K2 bin cursors the next consuming node pass zeroes
     int64_t B = 0;
     DevBuf<double> val, hv;
     DevBuf<int64_t> ts, hv_ts;
@@ -100,19 +103,24 @@ struct crane_dyn {
     DevBuf<int64_t> score;
     DevBuf<uint32_t> k2_cnt, k2_tot, k2_sorted;  // bin-partitioned K2 scratch
     DevBuf<uint32_t> k2_cur;                      // two-kernel K2: [nbins] bin cursors
+    DevBuf<double> hvc;                           // [N] binding-log hot values of the last consuming K1
     DevBuf<uint32_t> gcnt;  // greedy: per-window counts [W][N]
     DevBuf<int64_t> gbase, gchosen;
     DevBuf<uint8_t> gleaf, gflags;
     DevBuf<unsigned long long> mH, mbs;  // merge-form greedy (merge.hip)
     DevBuf<int32_t> mflag, mapos, mtk;
     DevBuf<int64_t> mFs, mIs, mgi;
-    DevBuf<int32_t> sperm, svcnt;
-    DevBuf<int16_t> sflat;  // K3 step path scratch (step.hip)
+    DevBuf<int32_t> sperm, shdr;  // K3 step path scratch (step.hip)
     DevBuf<int64_t> stile, spnow;
     DevBuf<unsigned char> svrec;
     DevBuf<Step1> sstep1;
     DevBuf<double> thr;  // quotient thresholds (K3 division-free path), empty if unusable
     double inv_w = 0.0;
+    // stage timing (crane_dyn_set_profiling)
+    bool prof = false;
+    std::vector<hipEvent_t> ev;    // pool
+    std::vector<const char*> ev_name;  // ev_name[i]: stage ending at event i (ev_name[0] unused)
+    int nev = 0;
 
     int fail(int code, const std::string& m) {
         err = m;
@@ -263,14 +271,16 @@ int crane_dyn_destroy(crane_dyn* h) {
         (void)hipSetDevice(h->device);
         (void)hipStreamSynchronize(h->stream);
     }
+    for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+    h->ev.clear();
     h->val.release(); h->hv.release(); h->ts.release(); h->hv_ts.release(); h->rec.release();
     h->buckets.release(); h->bnode.release(); h->bts.release(); h->now.release(); h->flags.release();
     h->keys.release(); h->ff.release(); h->score.release(); h->thr.release();
-    h->k2_cnt.release(); h->k2_tot.release(); h->k2_sorted.release(); h->k2_cur.release();
+    h->k2_cnt.release(); h->k2_tot.release(); h->k2_sorted.release(); h->k2_cur.release(); h->hvc.release();
     h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
     h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
     h->mFs.release(); h->mIs.release(); h->mgi.release();
-    h->sperm.release(); h->sflat.release(); h->svcnt.release(); h->stile.release(); h->spnow.release(); h->svrec.release(); h->sstep1.release();
+    h->sperm.release(); h->shdr.release(); h->stile.release(); h->spnow.release(); h->svrec.release(); h->sstep1.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -336,6 +346,23 @@ int crane_dyn_upload_bindings(crane_dyn* h, int64_t n, const int32_t* node, cons
     return CRANE_OK;
 }
 
+// Stage-timing marks: an event before the first stage, then one after each.
+static hipError_t prof_mark(crane_dyn* h, hipStream_t st, const char* name) {
+    if (!h->prof) return hipSuccess;
+    if ((int)h->ev.size() <= h->nev) {
+        hipEvent_t e;
+        hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) return r;
+        h->ev.push_back(e);
+        h->ev_name.push_back(nullptr);
+    }
+    h->ev_name[h->nev] = name;
+    return hipEventRecord(h->ev[h->nev++], st);
+}
+static hipError_t prof_begin(crane_dyn* h, hipStream_t st) {
+    return h->prof && h->nev == 0 ? prof_mark(h, st, "begin") : hipSuccess;
+}
+
 static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hipStream_t st) {
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before refreshing hot values");
     DevPolicy& dp = h->dp;
@@ -365,12 +392,22 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     if (mode == "part" && gp.ok) {
         // two kernels adding into zeroed buckets (K1 zeroes what it consumed)
         if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
-        // bin cursors reset in-stream, so the launch sequence can be captured in a graph and replayed
+        // bin cursors: the node pass that consumes the buckets zeroes them in-stream, so
+        // a refresh + eval sequence needs no memset (and can be captured and replayed)
+        if ((size_t)gp.nbins > h->k2_cur.n) h->cur_zero = false;
         HIPTRY(h, h->k2_cur.reserve((size_t)gp.nbins));
-        HIPTRY(h, hipMemsetAsync(h->k2_cur.p, 0, sizeof(uint32_t) * gp.nbins, st));
+        if (!h->cur_zero) HIPTRY(h, hipMemsetAsync(h->k2_cur.p, 0, sizeof(uint32_t) * h->k2_cur.n, st));
         HIPTRY(h, h->k2_sorted.reserve((size_t)gp.nbins * (size_t)gp.cap));
+        HIPTRY(h, prof_begin(h, st));
         HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, h->k2_cur.p,
-                                        h->k2_sorted.p, st));
+                                        h->k2_sorted.p, st, 1));
+        HIPTRY(h, prof_mark(h, st, "k2x_partition"));
+        HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, h->k2_cur.p,
+                                        h->k2_sorted.p, st, 2));
+        HIPTRY(h, prof_mark(h, st, "k2y_bin_hist"));
+        h->cur_zero = false;
+        h->cur_n = gp.nbins;
+        h->counts_pending = true;
         h->buckets_zero = false;
         h->hv_from_counts = true;
         h->hv_ts_counts = hv_ts_ns;
@@ -389,18 +426,51 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         HIPTRY(h, launch_hot_count(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, st));
     }
     h->buckets_zero = false;
+    h->counts_pending = true;
     h->hv_from_counts = true;
     h->hv_ts_counts = hv_ts_ns;
     h->rec_dirty = true;
     return CRANE_OK;
 }
 
-static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nullptr) {
+// K1 (optionally with the K3 step tables fused in).  Hot values: pending K2
+// counts (consumed), else the values the last consuming pass kept, else the
+// uploaded annotation.
+static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nullptr, const K1Step* step = nullptr) {
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before the node pass");
-    HIPTRY(h, launch_node_pass(h->shape, h->dp, h->N, h->val.p, h->ts.p, h->have_hv ? h->hv.p : nullptr,
-                               h->hv_ts.p, h->hv_from_counts ? h->buckets.p : nullptr, h->hv_ts_counts, h->rec.p,
-                               st, cnt_out));
-    if (h->hv_from_counts) h->buckets_zero = true;  // K1 zeroed what it read
+    K1Args a{};
+    a.pol = h->dp;
+    a.N = h->N;
+    a.val = h->val.p;
+    a.ts = h->ts.p;
+    a.out = h->rec.p;
+    a.hv_ts_counts = h->hv_ts_counts;
+    const bool consume = h->hv_from_counts && h->counts_pending;
+    if (cnt_out && !consume) return h->fail(CRANE_E_STATE, "per-window counts need a hot-value refresh first");
+    if (consume) {
+        HIPTRY(h, h->hvc.reserve((size_t)std::max<int64_t>(h->N, 1)));
+        a.buckets = h->buckets.p;
+        a.cnt_out = cnt_out;
+        a.hvc_out = h->hvc.p;
+        if (h->cur_n > 0) {
+            a.zero_cur = h->k2_cur.p;
+            a.n_cur = h->cur_n;
+        }
+    } else if (h->hv_from_counts) {
+        a.hv = h->hvc.p;  // hv_ts null: stamped hv_ts_counts
+    } else if (h->have_hv) {
+        a.hv = h->hv.p;
+        a.hv_ts = h->hv_ts.p;
+    }
+    HIPTRY(h, prof_begin(h, st));
+    HIPTRY(h, launch_node_pass(h->shape, a, st, step));
+    HIPTRY(h, prof_mark(h, st, step ? "k1_node_pass+k3a_steps" : "k1_node_pass"));
+    if (consume) {
+        h->buckets_zero = true;  // K1 zeroed what it read
+        h->counts_pending = false;
+        if (h->cur_n > 0) h->cur_zero = true;
+        h->cur_n = 0;
+    }
     h->rec_dirty = false;
     return CRANE_OK;
 }
@@ -408,33 +478,53 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
 static int eval_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags, long long* d_keys,
                        int8_t* d_ff, int64_t* d_score, hipStream_t st) {
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
-    if (h->rec_dirty) {
-        int rc = node_pass_locked(h, st);
-        if (rc) return rc;
-    }
     const bool matrix = d_ff || d_score;
     if (!matrix && k3_variant() == 5 && h->N < kStepMaxNodes && P < (1LL << 31)) {
-        // step path: K3p (pod partition + key init) -> K3a (node step tables) -> K3s (pairs)
+        // step path: K3p (pod partition, key init, header reset) -> [K1 +] K3a (step
+        // tables; fused into the node pass when the records are stale) -> K3s (pairs)
         const StepGeometry g = step_geometry(P, h->N);
         HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
         HIPTRY(h, h->stile.reserve((size_t)(2 * g.ntiles)));
         HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
-        HIPTRY(h, h->sflat.reserve((size_t)(2 * g.npad)));
-        HIPTRY(h, h->svcnt.reserve((size_t)(4 * g.nseg)));
+        HIPTRY(h, h->shdr.reserve((size_t)kHdrLen));
         HIPTRY(h, h->sstep1.reserve((size_t)(2 * g.npad)));
         HIPTRY(h, h->svrec.reserve((size_t)(2 * g.npad) * step_vrec_bytes(h->shape)));
-        StepTables stt{h->sflat.p, h->svcnt.p, h->sstep1.p, h->svrec.p, g.npad, g.nseg};
-        HIPTRY(h, launch_eval_step(h->shape, h->rec.p, h->N, h->node_offset, d_now, d_flags, P, h->dp.wsum,
-                                   h->dp.noprio, d_keys, stt, g, h->sperm.p, h->spnow.p, h->stile.p, st));
+        StepTables stt{h->shdr.p, h->sstep1.p, h->svrec.p, g.cap, g.npad};
+        HIPTRY(h, prof_begin(h, st));
+        HIPTRY(h, launch_step_pods(d_now, d_flags, P, d_keys, stt, g, h->sperm.p, h->spnow.p, h->stile.p, st));
+        HIPTRY(h, prof_mark(h, st, "k3p_pods"));
+        if (P == 0) return CRANE_OK;
+        const char* fe = getenv("CRANE_K1_FUSE");
+        if (h->rec_dirty && !(fe && fe[0] == '0')) {
+            K1Step ks{h->stile.p, (int32_t)g.ntiles, h->dp.noprio, h->dp.wsum, stt};
+            int rc = node_pass_locked(h, st, nullptr, &ks);
+            if (rc) return rc;
+        } else {
+            if (h->rec_dirty) {
+                int rc = node_pass_locked(h, st);
+                if (rc) return rc;
+            }
+            HIPTRY(h, launch_step_nodes(h->shape, h->rec.p, h->N, h->dp.wsum, h->dp.noprio, stt, g, h->stile.p, st));
+            HIPTRY(h, prof_mark(h, st, "k3a_steps"));
+        }
+        HIPTRY(h, launch_step_pairs(h->shape, h->N, h->node_offset, P, d_keys, stt, g, h->sperm.p, h->spnow.p, st));
+        HIPTRY(h, prof_mark(h, st, "k3s_eval"));
         return CRANE_OK;
     }
+    if (h->rec_dirty) {
+        int rc = node_pass_locked(h, st);
+        if (rc) return rc;
+    }
+    HIPTRY(h, prof_begin(h, st));
     HIPTRY(h, hipMemsetAsync(d_keys, 0xFF, sizeof(long long) * (size_t)P, st));
+    HIPTRY(h, prof_mark(h, st, "keys_init"));
     MatrixOut mo{};
     mo.first_fail = d_ff;
     mo.score = d_score;
     std::memcpy(mo.pred_orig, h->pred_orig, sizeof mo.pred_orig);
     HIPTRY(h, launch_eval(h->shape, h->rec.p, h->N, h->node_offset, d_now, d_flags, P, h->dp.wsum, h->dp.noprio,
                           d_keys, mo, h->inv_w, h->thr.n ? h->thr.p : nullptr, st));
+    HIPTRY(h, prof_mark(h, st, "k3_eval"));
     return CRANE_OK;
 }
 
@@ -517,6 +607,29 @@ int crane_dyn_eval(crane_dyn* h, int64_t P, const int64_t* now_ns, const uint8_t
     return CRANE_OK;
 }
 
+int crane_dyn_set_profiling(crane_dyn* h, int on) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    h->prof = on != 0;
+    h->nev = 0;
+    return CRANE_OK;
+}
+
+int crane_dyn_stage_times(crane_dyn* h, int32_t max, const char** names, double* ms) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    int n = 0;
+    if (h->nev > 0) HIPTRY(h, hipEventSynchronize(h->ev[h->nev - 1]));
+    for (int i = 1; i < h->nev && n < max; ++i, ++n) {
+        float t = 0.f;
+        HIPTRY(h, hipEventElapsedTime(&t, h->ev[i - 1], h->ev[i]));
+        if (names) names[n] = h->ev_name[i];
+        if (ms) ms[n] = t;
+    }
+    h->nev = 0;
+    return n;
+}
+
 int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod_flags, int64_t* chosen) {
     if (!h) return CRANE_E_INVALID;
     std::lock_guard<std::mutex> g(h->mu);
@@ -561,6 +674,7 @@ int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod
             for (int64_t p = 0; p < P; ++p) Pd += pod_flags[p] & 1;
         HIPTRY(h, launch_greedy(h->shape, h->rec.p, N, h->gcnt.p, a, h->gbase.p, h->gleaf.p, P, nullptr, nullptr, st,
                                 kGreedyPrep));
+        HIPTRY(h, prof_mark(h, st, "greedy_prep"));
         MergeArgs ma{};
         ma.n_win = W;
         for (int w = 0; w < W; ++w) {
@@ -570,6 +684,7 @@ int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod
         HIPTRY(h, h->mH.reserve(2 * 101));
         HIPTRY(h, h->mflag.reserve(1));
         HIPTRY(h, launch_merge_hist(h->gbase.p, h->gleaf.p, h->gcnt.p, N, ma, P, Pd, h->mH.p, h->mflag.p, st));
+        HIPTRY(h, prof_mark(h, st, "m1_hist"));
         unsigned long long Hh[2 * 101];
         int32_t flag = 1;
         HIPTRY(h, hipMemcpyAsync(Hh, h->mH.p, sizeof Hh, hipMemcpyDeviceToHost, st));
@@ -602,14 +717,17 @@ int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod
                                                   h->mFs.p, st));
             if (nI) HIPTRY(h, launch_merge_stream(h->gbase.p, h->gleaf.p, h->gcnt.p, N, ma, 1, vI, nI, h->mbs.p,
                                                   h->mIs.p, st));
+            HIPTRY(h, prof_mark(h, st, "m2_m4_merge_stream"));
             HIPTRY(h, launch_merge_assign(h->mFs.p, nF, h->mIs.p, nI, h->gflags.p, P, Pd, h->mapos.p, h->mtk.p,
                                           h->mgi.p, h->gchosen.p, st));
+            HIPTRY(h, prof_mark(h, st, "m5_merge_assign"));
             done = true;
         }
     }
     if (!done)
         HIPTRY(h, launch_greedy(h->shape, h->rec.p, N, h->gcnt.p, a, h->gbase.p, h->gleaf.p, P,
                                 pod_flags ? h->gflags.p : nullptr, h->gchosen.p, st, merge ? kGreedyRun : kGreedyBoth));
+    if (!done) HIPTRY(h, prof_mark(h, st, "greedy_run"));
     if (P > 0) HIPTRY(h, hipMemcpyAsync(chosen, h->gchosen.p, sizeof(int64_t) * P, hipMemcpyDeviceToHost, st));
     HIPTRY(h, hipStreamSynchronize(st));
     for (int64_t p = 0; p < P; ++p)

@@ -258,15 +258,17 @@ HotPart hot_part_geometry(int64_t B, int64_t N, int32_t W) {
 
 hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                  const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* cur,
-                                 uint32_t* region, hipStream_t st) {
+                                 uint32_t* region, hipStream_t st, int which) {
     static const hipError_t attr =
         hipFuncSetAttribute((const void*)k2y_bin_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(k2x_partition, dim3(g.nblk), dim3(kHT), sizeof(uint32_t) * 2 * g.nbins, st, bnode, bts, B, N,
-                       cut, g, cur, region);
+    if (which & 1)
+        hipLaunchKernelGGL(k2x_partition, dim3(g.nblk), dim3(kHT), sizeof(uint32_t) * 2 * g.nbins, st, bnode, bts, B,
+                           N, cut, g, cur, region);
     const size_t lds = sizeof(uint32_t) * (size_t)cut.n_win * ((size_t)1 << g.bb);
-    hipLaunchKernelGGL(k2y_bin_hist, dim3(g.nbins, kYSplits), dim3(kHT), lds, st, region, cur, g, cut.n_win, N,
-                       buckets);
+    if (which & 2)
+        hipLaunchKernelGGL(k2y_bin_hist, dim3(g.nbins, kYSplits), dim3(kHT), lds, st, region, cur, g, cut.n_win, N,
+                           buckets);
     return hipGetLastError();
 }
 

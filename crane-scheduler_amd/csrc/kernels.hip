@@ -15,6 +15,7 @@
 
 #include "dyn_types.hpp"
 #include "kernels.hpp"
+#include "step_node.hpp"
 
 namespace crane {
 
@@ -108,19 +109,36 @@ __global__ __launch_bounds__(kK2Threads) void k2_hot_count(const int32_t* __rest
 // node's NodeRec into LDS, then the workgroup streams its records out with
 // 16-byte coalesced stores.
 // block size: 128 by default, CRANE_K1_THREADS=256 selects the wide variant
-template <int PD, int PR, int kK1Threads>
-__global__ __launch_bounds__(kK1Threads) void k1_node_pass(DevPolicy pol, int64_t N, const double* __restrict__ val,
-                                                           const int64_t* __restrict__ ts,
-                                                           const double* __restrict__ hv,
-                                                           const int64_t* __restrict__ hv_ts,
-                                                           uint32_t* __restrict__ buckets, int64_t hv_ts_counts,
-                                                           NodeRec<PD, PR>* __restrict__ out,
-                                                           uint32_t* __restrict__ cnt_out) {
+// STEP: also build the K3 step tables of the pod batch (K3a fused, step.hip):
+// the record is classified straight from registers.
+template <int PD, int PR, int kK1Threads, bool STEP>
+__global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step) {
+    const DevPolicy& pol = a.pol;
+    const int64_t N = a.N;
+    const double* __restrict__ val = a.val;
+    const int64_t* __restrict__ ts = a.ts;
+    const double* __restrict__ hv = a.hv;
+    const int64_t* __restrict__ hv_ts = a.hv_ts;
+    uint32_t* __restrict__ buckets = a.buckets;
+    const int64_t hv_ts_counts = a.hv_ts_counts;
+    NodeRec<PD, PR>* __restrict__ out = static_cast<NodeRec<PD, PR>*>(a.out);
+    uint32_t* __restrict__ cnt_out = a.cnt_out;
     using Rec = NodeRec<PD, PR>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Rec* lrec = reinterpret_cast<Rec*>(smem);
     const int64_t first = (int64_t)blockIdx.x * kK1Threads;
     const int64_t n = first + threadIdx.x;
+    // K2's bin cursors: consumed with the buckets (stream order: K2 has finished)
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < a.n_cur; i += kK1Threads) a.zero_cur[i] = 0;
+    __shared__ int64_t smn[kK1Threads / 64], smx[kK1Threads / 64];
+    __shared__ StepShared ssh;
+    int64_t tmin = 0, tmax = 0;
+    if (STEP) {
+        if (threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+        batch_range<kK1Threads>(step.tile_mm, step.ntiles, smn, smx, tmin, tmax);
+    }
+    StepSlots so;
     if (n < N) {
         Rec r;
 #pragma unroll
@@ -172,11 +190,12 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(DevPolicy pol, int64_
             }
             // the plugin re-reads it via ParseFloat (exact) and rejects negatives (stats.go:71-73)
             const double h = (double)v;
+            if (a.hvc_out) a.hvc_out[n] = h;  // kept for node passes after the buckets are consumed
             r.pen = go_int(h * 10.0);
             r.e_hv = v >= 0 ? sat_add(hv_ts_counts, kHotActiveNs) : kTsInvalid;
         } else if (hv) {
             const double h = hv[n];
-            const int64_t t = hv_ts[n];
+            const int64_t t = hv_ts ? hv_ts[n] : hv_ts_counts;  // null: the binding-log value of an earlier pass
             r.pen = go_int(h * 10.0);
             r.e_hv = (t != kTsInvalid && !(h < 0.0)) ? sat_add(t, kHotActiveNs) : kTsInvalid;
         } else {
@@ -195,6 +214,13 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(DevPolicy pol, int64_
         r.pen32 = pen_fast ? (int32_t)r.pen : 0;
         r.flags = slow ? kRecSlow : 0;
         lrec[threadIdx.x] = r;
+        if (STEP) step_count<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, ssh, so);
+    }
+    if (STEP) {
+        step_reserve<kK1Threads>(so, ssh, step.st);  // (its barriers also order lrec)
+        // stepped nodes (a few %) rebuild their record from the LDS copy of the NodeRec
+        if (n < N && (so.slot0 >= 0 || so.slot1 >= 0))
+            step_emit<PD, PR>(lrec[threadIdx.x], n, tmin, tmax, step.wsum, step.noprio, ssh, so, step.st);
     }
     __syncthreads();
     const int64_t nvalid = min((int64_t)kK1Threads, N - first);
@@ -384,30 +410,33 @@ __global__ __launch_bounds__(kK3Threads) void k3_eval(const NodeRec<PD, PR>* __r
 
 // ---------------------------------------------------------------- launchers
 template <int PD, int PR>
-static hipError_t launch_k1_t(const DevPolicy& pol, int64_t N, const double* val, const int64_t* ts, const double* hv,
-                              const int64_t* hv_ts, uint32_t* buckets, int64_t hv_ts_counts, void* out,
-                              hipStream_t st, uint32_t* cnt_out) {
-    if (N <= 0) return hipSuccess;
+static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t st) {
+    if (a.N <= 0) {
+        if (a.zero_cur && a.n_cur > 0) return hipMemsetAsync(a.zero_cur, 0, sizeof(uint32_t) * a.n_cur, st);
+        return hipSuccess;
+    }
     const char* e = getenv("CRANE_K1_THREADS");
     const int T = e && atoi(e) == 256 ? 256 : 128;
-    const unsigned grid = (unsigned)((N + T - 1) / T);
+    const unsigned grid = (unsigned)((a.N + T - 1) / T);
     const size_t lds = sizeof(NodeRec<PD, PR>) * T;
-    if (T == 256)
-        hipLaunchKernelGGL((k1_node_pass<PD, PR, 256>), dim3(grid), dim3(256), lds, st, pol, N, val, ts, hv, hv_ts,
-                           buckets, hv_ts_counts, static_cast<NodeRec<PD, PR>*>(out), cnt_out);
-    else
-        hipLaunchKernelGGL((k1_node_pass<PD, PR, 128>), dim3(grid), dim3(128), lds, st, pol, N, val, ts, hv, hv_ts,
-                           buckets, hv_ts_counts, static_cast<NodeRec<PD, PR>*>(out), cnt_out);
+    const K1Step sa = step ? *step : K1Step{};
+#define K1_LAUNCH(TT, S) hipLaunchKernelGGL((k1_node_pass<PD, PR, TT, S>), dim3(grid), dim3(TT), lds, st, a, sa)
+    if (T == 256) {
+        if (step) K1_LAUNCH(256, true);
+        else K1_LAUNCH(256, false);
+    } else {
+        if (step) K1_LAUNCH(128, true);
+        else K1_LAUNCH(128, false);
+    }
+#undef K1_LAUNCH
     return hipGetLastError();
 }
 
-hipError_t launch_node_pass(int shape, const DevPolicy& pol, int64_t N, const double* val, const int64_t* ts,
-                            const double* hv, const int64_t* hv_ts, uint32_t* buckets, int64_t hv_ts_counts,
-                            void* out, hipStream_t st, uint32_t* cnt_out) {
+hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step) {
     switch (shape) {
-        case kShape4x6: return launch_k1_t<4, 6>(pol, N, val, ts, hv, hv_ts, buckets, hv_ts_counts, out, st, cnt_out);
-        case kShape8x8: return launch_k1_t<8, 8>(pol, N, val, ts, hv, hv_ts, buckets, hv_ts_counts, out, st, cnt_out);
-        default: return launch_k1_t<16, 16>(pol, N, val, ts, hv, hv_ts, buckets, hv_ts_counts, out, st, cnt_out);
+        case kShape4x6: return launch_k1_t<4, 6>(a, step, st);
+        case kShape8x8: return launch_k1_t<8, 8>(a, step, st);
+        default: return launch_k1_t<16, 16>(a, step, st);
     }
 }
 

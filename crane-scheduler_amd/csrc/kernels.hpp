@@ -86,7 +86,7 @@ HotPart hot_part_geometry(int64_t B, int64_t N, int32_t W);
 // Adds into buckets[W][N], which must be zero on entry.
 hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                  const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* cur,
-                                 uint32_t* region, hipStream_t st);
+                                 uint32_t* region, hipStream_t st, int which = 3);  // 1: k2x, 2: k2y
 
 // K3 step path (step.hip): per-batch node step tables + pair eval.
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
@@ -99,29 +99,50 @@ struct alignas(16) Step1 {
 // A node whose key changes more than once: cnt ascending expiries in
 // (tmin, tmax], padded with INT64_MAX; key[j] holds for bp[j-1] <= now < bp[j].
 template <int NB>
-struct VRec {
+struct alignas(16) VRec {  // 16-byte multiple: K3s stages records with 16-byte copies
     int64_t bp[NB];
     int32_t key[NB + 1];
     int32_t cnt;
 };
+// The stepped lists are split into kStepSub sub-lists (workgroup b of the
+// producing kernel appends to sub-list b % kStepSub) so that no counter takes
+// more than a few dozen global atomics.  Header (int32) per sub-list:
+// [flat max kind 0, flat max kind 1, Step1 count kind 0, VRec count kind 0,
+//  Step1 count kind 1, VRec count kind 1, -, -].  K3p resets it.
+constexpr int kStepSub = 64;
+constexpr int kHdrFlat = 0, kHdrN1 = 2, kHdrStride = 8, kHdrLen = kStepSub * kHdrStride;
 struct StepTables {
-    int16_t* flat;   // [2][npad] (score << 8 | 255 - local) of a node constant over the batch, -1 if stepped/infeasible
-    int32_t* cnt;    // [2][nseg][2] per segment: Step1 count (padded to x8), VRec count
-    Step1* single;   // [2][npad]  segment s's Step1 list at s * kStepSeg
-    void* multi;     // [2][npad]  VRec<NB>, segment s's list at s * kStepSeg
-    int64_t npad, nseg;
+    int32_t* hdr;    // [kStepSub][kHdrStride]
+    Step1* single;   // [2][kStepSub][cap] per pod kind and sub-list (order is irrelevant: K3s takes a max)
+    void* multi;     // [2][kStepSub][cap] VRec<NB>
+    int64_t cap;     // records per sub-list: >= the nodes of the workgroups that map to it
+    int64_t npad;    // kStepSub * cap, per kind
 };
 struct StepGeometry {
-    int64_t nseg, npad, ntiles, ptiles;
-    int32_t segs_per_chunk, nchunks;
+    int64_t nseg, npad, cap, ntiles, ngroups;
+    int32_t R;  // K3s workgroups per 64-pod group
 };
 size_t step_vrec_bytes(int shape);
 StepGeometry step_geometry(int64_t P, int64_t N);
-// perm, pnow [ntiles * 1024], tile_mm [2 * ntiles]; also initialises keys[0..P) to -1
-hipError_t launch_eval_step(int shape, const void* rec, int64_t N, int64_t node_offset, const int64_t* now,
-                            const uint8_t* flags, int64_t P, double wsum, int32_t noprio, long long* keys,
+// K3p: perm, pnow [ntiles * 1024], tile_mm [2 * ntiles]; initialises keys[0..P) to -1 and the step header
+hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys,
                             const StepTables& st, const StepGeometry& g, int32_t* perm, int64_t* pnow,
                             int64_t* tile_mm, hipStream_t s);
+// K3a: step tables from NodeRecs in HBM (after K3p)
+hipError_t launch_step_nodes(int shape, const void* rec, int64_t N, double wsum, int32_t noprio,
+                             const StepTables& st, const StepGeometry& g, const int64_t* tile_mm, hipStream_t s);
+// K3s: (pod, stepped node) pairs + flat maxima -> keys (after K3a or K1's STEP form)
+hipError_t launch_step_pairs(int shape, int64_t N, int64_t node_offset, int64_t P, long long* keys,
+                             const StepTables& st, const StepGeometry& g, const int32_t* perm, const int64_t* pnow,
+                             hipStream_t s);
+// K1's fused step form: the node pass also builds the step tables of a pod batch
+struct K1Step {
+    const int64_t* tile_mm;  // K3p's per-tile time range
+    int32_t ntiles;
+    int32_t noprio;
+    double wsum;
+    StepTables st;
+};
 int k3_variant();
 
 size_t node_rec_bytes(int shape);
@@ -131,9 +152,26 @@ hipError_t launch_hot_count(const int32_t* bnode, const int64_t* bts, int64_t B,
                             uint32_t* buckets, hipStream_t st);
 // K1 zeroes the buckets it consumes (so the next K2 needs no memset); with
 // cnt_out it also stores the per-window counts [W][N].
-hipError_t launch_node_pass(int shape, const DevPolicy& pol, int64_t N, const double* val, const int64_t* ts,
-                            const double* hv, const int64_t* hv_ts, uint32_t* buckets, int64_t hv_ts_counts,
-                            void* out, hipStream_t st, uint32_t* cnt_out = nullptr);
+// K1 node pass arguments.  Hot value source: buckets (K2 counts, consumed:
+// zeroed, the value kept in hvc_out) > hv with hv_ts (annotation; hv_ts null:
+// every node stamped hv_ts_counts) > none.
+struct K1Args {
+    DevPolicy pol;
+    int64_t N;
+    const double* val;      // [M][N]
+    const int64_t* ts;      // [M][N]
+    const double* hv;       // [N] or null
+    const int64_t* hv_ts;   // [N] or null
+    uint32_t* buckets;      // [W][N] K2 window-rank buckets or null
+    int64_t hv_ts_counts;   // stamp of binding-log hot values
+    void* out;              // NodeRec [N]
+    uint32_t* cnt_out;      // [W][N] per-window counts (greedy) or null
+    double* hvc_out;        // [N] hot values from the buckets, or null
+    uint32_t* zero_cur;     // [n_cur] K2 bin cursors zeroed with the buckets (no memset before the next K2)
+    int32_t n_cur;
+};
+// step (optional): also build the K3 step tables of a pod batch (K3a fused).
+hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr);
 // thr: device table of kQMax + 1 quotient thresholds (null = divide); inv_w = RN(1/wsum)
 hipError_t launch_eval(int shape, const void* rec, int64_t N, int64_t node_offset, const int64_t* now,
                        const uint8_t* flags, int64_t P, double wsum, int32_t noprio, long long* keys,

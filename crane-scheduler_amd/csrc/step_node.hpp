@@ -1,0 +1,211 @@
+// step_node.hpp — per-node part of the K3 step path (step.hip), shared by the
+// stand-alone step-table kernel K3a and the fused node pass K1+K3a
+// (kernels.hip), which builds the step tables straight from the NodeRec it
+// has just computed in registers.
+//
+// A node's packed key (score << 24 | 0xFFFFFF - node, -1 = the pod may not go
+// there) is a step function of the pod's `now`; over a batch whose times lie
+// in [tmin, tmax] only the node's expiries inside (tmin, tmax] can change it.
+// A node with none is "flat": its key is the same for every pod of a kind and
+// only enters the workgroup's flat max.  Otherwise the node appends a Step1
+// (one step) or VRec (more) record to its kind's compact list.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "dyn_types.hpp"
+#include "kernels.hpp"
+
+namespace crane {
+
+__device__ __forceinline__ int32_t pack_key(int32_t f, int64_t n) { return (f << 24) | (int32_t)(0xFFFFFF - n); }
+
+// Exact clamped Score of (pod at time t, node) — the literal int64 restatement
+// of stats.go:114-138 + plugins.go:91-93, the semantics of K3's eval_pair and
+// score_exact (kernels.hip).
+template <int PD, int PR>
+__device__ __forceinline__ int32_t score_at(int64_t t, const NodeRec<PD, PR>& r, double wsum, int32_t noprio) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < PR; ++k)
+        if (t < r.e_prio[k]) s += r.t[k];  // stats.go:124-133, policy order
+    int64_t base = 0;
+    if (!noprio) {
+        const double q = s / wsum;  // stats.go:135 int(score / weight), Go CVTTSD2SQ
+        base = (q >= -9223372036854775808.0 && q < 9223372036854775808.0) ? (int64_t)q : INT64_MIN;
+    }
+    const int64_t pen = t < r.e_hv ? r.pen : 0;
+    const int64_t f = (int64_t)((uint64_t)base - (uint64_t)pen);  // plugins.go:91, wraps like Go
+    return (int32_t)(f < 0 ? 0 : (f > 100 ? 100 : f));            // NormalizeScore (utils.go:58-68)
+}
+
+// Filter (plugins.go:41-43, 55-66) + packed key for pod kind T (0: Filter applies, 1: DaemonSet)
+template <int PD, int PR>
+__device__ __forceinline__ int32_t key_of(int T, int64_t t, int32_t score, const NodeRec<PD, PR>& r, int64_t n) {
+    return (T == 1 || !(t < r.e_fail)) ? pack_key(score, n) : -1;
+}
+
+// Batch time range [tmin, tmax] from K3p's per-tile partials; every thread of
+// the workgroup gets it (sm: >= BS/64 entries of LDS per array).
+template <int BS>
+__device__ __forceinline__ void batch_range(const int64_t* __restrict__ tile_mm, int32_t ntiles, int64_t* smn,
+                                            int64_t* smx, int64_t& tmin, int64_t& tmax) {
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    for (int i = threadIdx.x; i < ntiles; i += BS) {
+        mn = min(mn, tile_mm[2 * i]);
+        mx = max(mx, tile_mm[2 * i + 1]);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        mn = min(mn, (int64_t)__shfl_xor((long long)mn, o));
+        mx = max(mx, (int64_t)__shfl_xor((long long)mx, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        smn[threadIdx.x >> 6] = mn;
+        smx[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    tmin = smn[0];
+    tmax = smx[0];
+#pragma unroll
+    for (int i = 1; i < BS / 64; ++i) {
+        tmin = min(tmin, smn[i]);
+        tmax = max(tmax, smx[i]);
+    }
+}
+
+// Per node and pod kind: the flat key (-1 if stepped or never feasible) and,
+// for a stepped node, its slot in the workgroup's span of the kind's list.
+// Phase 1 (step_count) only classifies — cheap and register-light, so it can
+// run inside the node pass; phase 2 (step_emit) rebuilds the record of a
+// stepped node after the workgroup has reserved its list spans.
+struct StepSlots {
+    int32_t flat0 = -1, flat1 = -1;
+    int32_t slot0 = -1, slot1 = -1;  // >= 0: stepped
+    bool multi0 = false, multi1 = false;
+};
+
+// Workgroup-shared counters of the step epilogue.
+struct StepShared {
+    int32_t lc[2][2];   // records per kind: [Step1, VRec]
+    int32_t gb[2][2];   // reserved list offsets
+    int32_t fm[2][16];  // per-wave flat maxima (<= 1024 threads)
+};
+
+// The node's in-range expiries for kind T, sorted ascending, INT64_MAX past them;
+// returns (count, distinct count).
+template <int PD, int PR, int T>
+__device__ __forceinline__ void step_points(const NodeRec<PD, PR>& r, int64_t tmin, int64_t tmax, int64_t* c,
+                                            int& cnt, int& distinct) {
+    constexpr int NB = PR + 2;
+#pragma unroll
+    for (int k = 0; k < PR; ++k) c[k] = r.e_prio[k];
+    c[PR] = r.e_hv;
+    c[PR + 1] = T == 0 ? r.e_fail : INT64_MIN;  // DaemonSet pods bypass the Filter
+    cnt = 0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const bool in = c[j] > tmin && c[j] <= tmax;
+        c[j] = in ? c[j] : INT64_MAX;
+        cnt += in;
+    }
+    distinct = 0;
+    if (cnt > 0) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i)  // odd-even transposition sort (static indices)
+#pragma unroll
+            for (int j = i & 1; j + 1 < NB; j += 2) {
+                const int64_t x = c[j], y = c[j + 1];
+                c[j] = min(x, y);
+                c[j + 1] = max(x, y);
+            }
+        // a predicate's expiry equals its metric's priority expiry when both use one metric
+#pragma unroll
+        for (int j = 0; j < NB; ++j) distinct += c[j] != INT64_MAX && (j == 0 || c[j] != c[j - 1]);
+    }
+}
+
+template <int PD, int PR>
+__device__ __forceinline__ void step_count(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
+                                           double wsum, int32_t noprio, StepShared& sh, StepSlots& o) {
+    const int32_t s0 = score_at<PD, PR>(tmin, r, wsum, noprio);
+    auto kind = [&](auto Tc, int32_t& flat, int32_t& slot, bool& multi) {
+        constexpr int T = decltype(Tc)::value;
+        int64_t c[PR + 2];
+        int cnt, distinct;
+        step_points<PD, PR, T>(r, tmin, tmax, c, cnt, distinct);
+        flat = cnt == 0 ? key_of<PD, PR>(T, tmin, s0, r, n) : -1;
+        multi = distinct > 1;
+        slot = cnt == 0 ? -1 : atomicAdd(&sh.lc[T][multi ? 1 : 0], 1);
+    };
+    kind(std::integral_constant<int, 0>{}, o.flat0, o.slot0, o.multi0);
+    kind(std::integral_constant<int, 1>{}, o.flat1, o.slot1, o.multi1);
+}
+
+// Write node n's record(s) at the reserved positions (after step_commit).
+template <int PD, int PR>
+__device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
+                                          double wsum, int32_t noprio, const StepShared& sh, const StepSlots& o,
+                                          const StepTables& st) {
+    constexpr int NB = PR + 2;
+    auto kind = [&](auto Tc, int32_t slot, bool multi) {
+        constexpr int T = decltype(Tc)::value;
+        if (slot < 0) return;
+        int64_t c[NB];
+        int cnt, distinct;
+        step_points<PD, PR, T>(r, tmin, tmax, c, cnt, distinct);
+        const int32_t k0 = key_of<PD, PR>(T, tmin, score_at<PD, PR>(tmin, r, wsum, noprio), r, n);
+        // key of the step starting at c[j], evaluated at its first instant (equal expiries give equal keys)
+        if (!multi) {
+            Step1 v;
+            v.bp = c[0];
+            v.k0 = k0;
+            v.k1 = key_of<PD, PR>(T, c[0], score_at<PD, PR>(c[0], r, wsum, noprio), r, n);
+            st.single[(int64_t)T * st.npad + sh.gb[T][0] + slot] = v;
+        } else {
+            VRec<NB> v;
+            v.cnt = cnt;
+            v.key[0] = k0;
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                v.bp[j] = c[j];  // INT64_MAX past cnt: never selected
+                v.key[j + 1] = j < cnt ? key_of<PD, PR>(T, c[j], score_at<PD, PR>(c[j], r, wsum, noprio), r, n) : -1;
+            }
+            reinterpret_cast<VRec<NB>*>(st.multi)[(int64_t)T * st.npad + sh.gb[T][1] + slot] = v;
+        }
+    };
+    kind(std::integral_constant<int, 0>{}, o.slot0, o.multi0);
+    kind(std::integral_constant<int, 1>{}, o.slot1, o.multi1);
+}
+
+// Workgroup epilogue part 1: flat max -> one atomicMax per kind, list spans
+// reserved with one atomicAdd per (kind, list).  Every thread calls it
+// (contains barriers); sh.lc must have been zeroed before step_count.
+template <int BS>
+__device__ __forceinline__ void step_reserve(const StepSlots& o, StepShared& sh, const StepTables& st) {
+    auto wmax = [&](int T, int32_t m) {
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) m = max(m, __shfl_xor(m, s));
+        if ((threadIdx.x & 63) == 0) sh.fm[T][threadIdx.x >> 6] = m;
+    };
+    wmax(0, o.flat0);
+    wmax(1, o.flat1);
+    __syncthreads();
+    int32_t* hdr = st.hdr + (blockIdx.x % kStepSub) * kHdrStride;  // this workgroup's sub-list
+    if (threadIdx.x < 2) {
+        const int T = threadIdx.x;
+        int32_t m = sh.fm[T][0];
+#pragma unroll
+        for (int i = 1; i < BS / 64; ++i) m = max(m, sh.fm[T][i]);
+        if (m >= 0) atomicMax(&hdr[kHdrFlat + T], m);
+    } else if (threadIdx.x < 6) {
+        const int T = (threadIdx.x - 2) >> 1, k = (threadIdx.x - 2) & 1;
+        // offset inside the sub-list; the sub-list starts at (blockIdx % kStepSub) * cap
+        sh.gb[T][k] = (sh.lc[T][k] ? atomicAdd(&hdr[kHdrN1 + 2 * T + k], sh.lc[T][k]) : 0) +
+                      (int32_t)((blockIdx.x % kStepSub) * st.cap);
+    }
+    __syncthreads();
+}
+
+}  // namespace crane

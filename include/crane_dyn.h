@@ -149,6 +149,14 @@ int crane_dyn_eval_keys_async(crane_dyn *h, int64_t n_pods, const int64_t *d_now
 int crane_dyn_refresh_hot_values_async(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns, void *stream);
 int crane_dyn_node_pass_async(crane_dyn *h, void *stream);
 
+/* Stage timing for benchmarks and profiling: while enabled, the engine records
+ * a HIP event on the work stream after each kernel stage it enqueues (and one
+ * before the first).  crane_dyn_stage_times() waits for the recorded events,
+ * writes up to `max` (name, milliseconds) pairs in enqueue order, returns the
+ * number of stages and clears the list.  Enabling also clears it. */
+int crane_dyn_set_profiling(crane_dyn *h, int on);
+int crane_dyn_stage_times(crane_dyn *h, int32_t max, const char **names, double *ms);
+
 /* Sequential-greedy batch: one `now_ns` for the whole batch; pods are placed
  * in order and each placement appends a binding (Timestamp = now) to the
  * chosen node, refreshing its hot value before the next pod is scored.  The

@@ -117,3 +117,63 @@ def test_step_matches_v4_keys():
     _, _, ch4, cs4 = eng.eval(c.now, c.ds)
     os.environ["CRANE_K3_VARIANT"] = "5"
     assert np.array_equal(ch5, ch4) and np.array_equal(cs5, cs4)
+
+
+def test_step_fused_and_standalone_agree():
+    """First eval after an upload fuses the node pass with the step tables (K1 STEP
+    form); a second eval rebuilds them from the stored records (K3a).  Both match."""
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 9000, 2000, seed=24, pod_step_ns=40_000_000, ds_frac=0.03)
+    eng = engine_for(spec, c)
+    _, _, ch1, cs1 = eng.eval(c.now, c.ds)      # K3p -> K1+K3a -> K3s
+    _, _, ch2, cs2 = eng.eval(c.now, c.ds)      # K3p -> K3a -> K3s
+    _, _, och = oracle_soa(spec, c, want_matrix=False)
+    assert np.array_equal(ch1, och) and np.array_equal(ch2, och) and np.array_equal(cs1, cs2)
+
+
+def _oracle_hv(spec, c, now_ns):
+    from oracle import oracle as O
+    _, hv = O.hot_values(spec, c.b_node, c.b_ts, c.n_nodes, now_ns // 10**9)
+    return hv.astype(np.float64), np.full(c.n_nodes, now_ns, np.int64)
+
+
+def test_step_replayed_batches_with_binding_log():
+    """The bench's step (K2 refresh -> keys-only eval) replayed on one stream: K1
+    consumes the K2 buckets and zeroes K2's bin cursors in-stream, so every
+    replay must give the oracle's choices with hot values from the log."""
+    import torch
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 20000, 3000, n_bindings=200_000, seed=25, pod_step_ns=3_000_000)
+    eng = engine_for(spec, c)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    now = int(synth.NOW0_NS)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
+    _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=_oracle_hv(spec, c, now))
+    with torch.cuda.stream(st):
+        for rep in range(4):
+            eng.refresh_hot_values_async(now, now, st.cuda_stream)
+            eng.eval_keys_async(d_now, d_flags, d_keys, st.cuda_stream)
+            st.synchronize()
+            ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
+            assert np.array_equal(ch, och), rep
+
+
+def test_hot_values_kept_after_consumption():
+    """After the node pass has consumed the K2 buckets, a later node pass (records
+    made stale by greedy) still sees the refreshed binding-log hot values."""
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 3000, 500, n_bindings=40_000, seed=26, pod_step_ns=0)
+    eng = engine_for(spec, c)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    now = int(c.now[0])
+    eng.refresh_hot_values(now, now)
+    _, _, ch1, _ = eng.eval(c.now, c.ds)          # consumes the counts
+    eng.greedy(50, now, c.ds[:50])                # refreshes at the same now, leaves records stale
+    ff, sc, ch2, _ = eng.eval(c.now, c.ds, matrix=True)   # K1 again from the kept hot values (V4 path)
+    off, osc, och = oracle_soa(spec, c, hv_override=_oracle_hv(spec, c, now))
+    assert np.array_equal(ch1, och) and np.array_equal(ch2, och)
+    assert np.array_equal(ff, off) and np.array_equal(sc, osc)
