@@ -86,8 +86,6 @@ struct crane_dyn {
     bool rec_dirty = true;
     bool buckets_zero = false;  // K1 consumes (zeroes) the buckets K2 filled
     bool counts_pending = false;  // buckets hold K2 counts no node pass has consumed yet
-    bool cur_zero = false;        // K2 bin cursors are zero
-    int32_t cur_n = 0;            // K2 bin cursors the next consuming node pass zeroes
     int64_t B = 0;
     DevBuf<double> val, hv;
     DevBuf<int64_t> ts, hv_ts;
@@ -102,7 +100,6 @@ struct crane_dyn {
     DevBuf<int8_t> ff;
     DevBuf<int64_t> score;
     DevBuf<uint32_t> k2_cnt, k2_tot, k2_sorted;  // bin-partitioned K2 scratch
-    DevBuf<uint32_t> k2_cur;                      // two-kernel K2: [nbins] bin cursors
     DevBuf<double> hvc;                           // [N] binding-log hot values of the last consuming K1
     DevBuf<uint32_t> gcnt;  // greedy: per-window counts [W][N]
     DevBuf<int64_t> gbase, gchosen;
@@ -276,7 +273,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->val.release(); h->hv.release(); h->ts.release(); h->hv_ts.release(); h->rec.release();
     h->buckets.release(); h->bnode.release(); h->bts.release(); h->now.release(); h->flags.release();
     h->keys.release(); h->ff.release(); h->score.release(); h->thr.release();
-    h->k2_cnt.release(); h->k2_tot.release(); h->k2_sorted.release(); h->k2_cur.release(); h->hvc.release();
+    h->k2_cnt.release(); h->k2_tot.release(); h->k2_sorted.release(); h->hvc.release();
     h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
     h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
     h->mFs.release(); h->mIs.release(); h->mgi.release();
@@ -392,21 +389,14 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     if (mode == "part" && gp.ok) {
         // two kernels adding into zeroed buckets (K1 zeroes what it consumed)
         if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
-        // bin cursors: the node pass that consumes the buckets zeroes them in-stream, so
-        // a refresh + eval sequence needs no memset (and can be captured and replayed)
-        if ((size_t)gp.nbins > h->k2_cur.n) h->cur_zero = false;
-        HIPTRY(h, h->k2_cur.reserve((size_t)gp.nbins));
-        if (!h->cur_zero) HIPTRY(h, hipMemsetAsync(h->k2_cur.p, 0, sizeof(uint32_t) * h->k2_cur.n, st));
-        HIPTRY(h, h->k2_sorted.reserve((size_t)gp.nbins * (size_t)gp.cap));
+        HIPTRY(h, h->k2_sorted.reserve(hot_part_scratch(gp)));
         HIPTRY(h, prof_begin(h, st));
-        HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, h->k2_cur.p,
-                                        h->k2_sorted.p, st, 1));
+        HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, h->k2_sorted.p, st,
+                                        1));
         HIPTRY(h, prof_mark(h, st, "k2x_partition"));
-        HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, h->k2_cur.p,
-                                        h->k2_sorted.p, st, 2));
+        HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, h->k2_sorted.p, st,
+                                        2));
         HIPTRY(h, prof_mark(h, st, "k2y_bin_hist"));
-        h->cur_zero = false;
-        h->cur_n = gp.nbins;
         h->counts_pending = true;
         h->buckets_zero = false;
         h->hv_from_counts = true;
@@ -452,10 +442,6 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
         a.buckets = h->buckets.p;
         a.cnt_out = cnt_out;
         a.hvc_out = h->hvc.p;
-        if (h->cur_n > 0) {
-            a.zero_cur = h->k2_cur.p;
-            a.n_cur = h->cur_n;
-        }
     } else if (h->hv_from_counts) {
         a.hv = h->hvc.p;  // hv_ts null: stamped hv_ts_counts
     } else if (h->have_hv) {
@@ -468,8 +454,6 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
     if (consume) {
         h->buckets_zero = true;  // K1 zeroed what it read
         h->counts_pending = false;
-        if (h->cur_n > 0) h->cur_zero = true;
-        h->cur_n = 0;
     }
     h->rec_dirty = false;
     return CRANE_OK;

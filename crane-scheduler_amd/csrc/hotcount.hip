@@ -155,28 +155,48 @@ __global__ __launch_bounds__(kHT) void k2d_bin_hist(const uint32_t* __restrict__
 }
 
 // ---------------------------------------------------------------- two-kernel form
-// X  partition : each workgroup takes 2048 bindings (8 per thread, loads issued
-//                together), counts them per node bin in LDS, reserves its run of
-//                every bin region with ONE global atomic per bin, and writes
-//                (local node | bucket << 24) entries into the bin regions.
-//                Bin regions have capacity B, so no pre-count pass is needed.
-// Y  bin_hist  : kYSplits workgroups per bin, each an LDS histogram [W][2^bb]
-//                of a contiguous slice of the bin's entries, flushed with
-//                contiguous atomics into the (zeroed) buckets.
-// The per-bin cursors are zeroed by a memset in the same stream before X.
+// X  partition : workgroup b takes 2048 bindings (8 per thread, loads issued
+//                together), counts the in-window ones per node bin in LDS,
+//                scans the bins and writes (local node | bucket << 24) entries
+//                bin-contiguously into ITS OWN 2048-entry region; per bin it
+//                publishes (count, offset) in C/O[bin][b].  No global atomics.
+// Y  bin_hist  : kYSplits workgroups per bin: scan of C[bin][*] in LDS, an
+//                even share of the bin's entries walked across the source
+//                regions, an LDS histogram [W][2^bb], flushed with contiguous
+//                atomics into the (zeroed) buckets.
+// Zipf-hot keys: both kernels aggregate equal keys within a wave before the
+// LDS atomic (one atomic per wave for the wave's most common key).
 constexpr int kXPer = 8;     // bindings per thread in X
+constexpr int kXChunk = kHT * kXPer;
 constexpr int kYSplits = 8;  // workgroups per bin in Y
+
+// LDS atomicAdd of `add` to a[key] for every active lane, the lanes sharing the
+// first active lane's key merged into one atomic; returns each lane's old value
+// (+ its rank among the merged lanes).
+__device__ __forceinline__ uint32_t wave_lds_add(uint32_t* a, uint32_t key, bool act) {
+    const uint64_t am = __ballot(act);
+    if (am == 0) return 0;
+    const int lead = __ffsll((long long)am) - 1;
+    const uint32_t kl = __shfl(key, lead);
+    const uint64_t m = __ballot(act && key == kl);
+    const int lane = threadIdx.x & 63;
+    const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
+    uint32_t old = 0;
+    if (lane == lead) old = atomicAdd(&a[kl], (uint32_t)__popcll(m));
+    const uint32_t base = __shfl(old, lead);
+    if (act && key != kl) return atomicAdd(&a[key], 1u);
+    return base + rank;
+}
 
 __global__ __launch_bounds__(kHT) void k2x_partition(const int32_t* __restrict__ bnode,
                                                      const int64_t* __restrict__ bts, int64_t B, int64_t N,
-                                                     HotCutoffs cut, HotPart g, uint32_t* __restrict__ cur,
-                                                     uint32_t* __restrict__ region) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];  // hist [nbins], base [nbins]
+                                                     HotCutoffs cut, HotPart g, uint32_t* __restrict__ C,
+                                                     uint32_t* __restrict__ O, uint32_t* __restrict__ region) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];  // hist [nbins], off [nbins]
+    __shared__ uint32_t part[kHT];
     uint32_t* hist = sh;
-    uint32_t* base = sh + g.nbins;
-    for (int i = threadIdx.x; i < g.nbins; i += kHT) hist[i] = 0;
-    __syncthreads();
-    const int64_t b0 = (int64_t)blockIdx.x * (kHT * kXPer) + threadIdx.x;
+    uint32_t* off = sh + g.nbins;
+    const int64_t b0 = (int64_t)blockIdx.x * kXChunk + threadIdx.x;
     int32_t nd[kXPer];
     int64_t ts[kXPer];
 #pragma unroll
@@ -185,6 +205,8 @@ __global__ __launch_bounds__(kHT) void k2x_partition(const int32_t* __restrict__
         nd[u] = b < B ? bnode[b] : -1;
         ts[u] = b < B ? bts[b] : INT64_MIN;
     }
+    for (int i = threadIdx.x; i < g.nbins; i += kHT) hist[i] = 0;
+    __syncthreads();
     uint32_t ent[kXPer], pos[kXPer];
     int32_t bin[kXPer];
     const uint32_t mask = (1u << g.bb) - 1;
@@ -194,43 +216,101 @@ __global__ __launch_bounds__(kHT) void k2x_partition(const int32_t* __restrict__
         const bool ok = nd[u] >= 0 && (int64_t)nd[u] < N && j > 0;  // binding.go:85-91
         bin[u] = ok ? nd[u] >> g.bb : -1;
         ent[u] = ((uint32_t)nd[u] & mask) | ((uint32_t)(j - 1) << 24);
-        pos[u] = ok ? atomicAdd(&hist[bin[u]], 1u) : 0u;
+        pos[u] = wave_lds_add(hist, ok ? (uint32_t)bin[u] : 0u, ok);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < g.nbins; i += kHT) {
+    // exclusive scan of hist over bins (each thread a contiguous run of bins)
+    const int per = (g.nbins + kHT - 1) / kHT;
+    const int lo = threadIdx.x * per, hi = min(g.nbins, lo + per);
+    uint32_t sum = 0;
+    for (int i = lo; i < hi; ++i) sum += hist[i];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int o = 1; o < kHT; o <<= 1) {  // Hillis-Steele over the 256 partials
+        const uint32_t y = (int)threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += y;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - sum;
+    for (int i = lo; i < hi; ++i) {
         const uint32_t c = hist[i];
-        base[i] = c ? atomicAdd(&cur[i], c) : 0u;
+        off[i] = run;
+        C[(int64_t)i * g.nblk + blockIdx.x] = c;
+        O[(int64_t)i * g.nblk + blockIdx.x] = run;
+        run += c;
     }
     __syncthreads();
+    uint32_t* reg = region + (int64_t)blockIdx.x * kXChunk;
 #pragma unroll
     for (int u = 0; u < kXPer; ++u)
-        if (bin[u] >= 0) region[(int64_t)bin[u] * g.cap + base[bin[u]] + pos[u]] = ent[u];
+        if (bin[u] >= 0) reg[off[bin[u]] + pos[u]] = ent[u];
 }
 
 __global__ __launch_bounds__(kHT) void k2y_bin_hist(const uint32_t* __restrict__ region,
-                                                    const uint32_t* __restrict__ cur, HotPart g, int32_t W,
-                                                    int64_t N, uint32_t* __restrict__ buckets) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // [W][2^bb]
+                                                    const uint32_t* __restrict__ C, const uint32_t* __restrict__ O,
+                                                    HotPart g, int32_t W, int64_t N,
+                                                    uint32_t* __restrict__ buckets) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];  // hist [W][2^bb], scan [nblk + 1], off [nblk]
+    __shared__ uint32_t part[kHT];
     const int bin = blockIdx.x, split = blockIdx.y;
     const int binw = 1 << g.bb;
+    uint32_t* hist = sh;
+    uint32_t* scan = sh + W * binw;
+    uint32_t* off = scan + g.nblk + 1;
     for (int i = threadIdx.x; i < W * binw; i += kHT) hist[i] = 0;
-    const uint32_t len = cur[bin];
-    // contiguous 1/splits of the bin's entries: Zipf-hot bins spread over the splits
-    const uint32_t lo = (uint32_t)((uint64_t)len * split / gridDim.y);
-    const uint32_t hi = (uint32_t)((uint64_t)len * (split + 1) / gridDim.y);
-    const uint32_t* __restrict__ r = region + (int64_t)bin * g.cap + lo;
-    const uint32_t n_e = hi - lo;
+    // scan of the bin's per-source-region counts
+    const int per = (g.nblk + kHT - 1) / kHT;
+    const int lo = threadIdx.x * per, hi = min(g.nblk, lo + per);
+    uint32_t sum = 0;
+    for (int i = lo; i < hi; ++i) {
+        const uint32_t c = C[(int64_t)bin * g.nblk + i];
+        scan[i] = c;
+        off[i] = O[(int64_t)bin * g.nblk + i];
+        sum += c;
+    }
+    part[threadIdx.x] = sum;
     __syncthreads();
-    for (uint32_t e0 = threadIdx.x; e0 < n_e; e0 += kHT * kXPer) {
-        uint32_t v[kXPer];
-#pragma unroll
-        for (int u = 0; u < kXPer; ++u) {
-            const uint32_t e = e0 + u * kHT;
-            v[u] = e < n_e ? r[e] : 0xFFFFFFFFu;
+    for (int o = 1; o < kHT; o <<= 1) {
+        const uint32_t y = (int)threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += y;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - sum;
+    for (int i = lo; i < hi; ++i) {
+        const uint32_t c = scan[i];
+        scan[i] = run;
+        run += c;
+    }
+    if (threadIdx.x == kHT - 1) scan[g.nblk] = part[kHT - 1];
+    __syncthreads();
+    const uint32_t len = scan[g.nblk];
+    // an even share of the bin's entries: Zipf-hot bins spread over the splits
+    const uint32_t e_lo = (uint32_t)((uint64_t)len * split / gridDim.y);
+    const uint32_t e_hi = (uint32_t)((uint64_t)len * (split + 1) / gridDim.y);
+    // each lane walks e = e_lo + tid, + kHT, ... advancing its source region as it goes
+    uint32_t e = e_lo + threadIdx.x;
+    int blk = 0;
+    if (e < e_hi) {  // first region: binary search, then forward steps
+        int l = 0, h = g.nblk - 1;
+        while (l < h) {
+            const int mid = (l + h + 1) >> 1;
+            if (scan[mid] <= e) l = mid;
+            else h = mid - 1;
         }
-#pragma unroll
-        for (int u = 0; u < kXPer; ++u)
-            if (v[u] != 0xFFFFFFFFu) atomicAdd(&hist[(v[u] >> 24) * binw + (v[u] & 0xFFFFFF)], 1u);
+        blk = l;
+    }
+    for (uint32_t e0 = e_lo; e0 < e_hi; e0 += kHT) {
+        const bool act = e < e_hi;
+        uint32_t v = 0;
+        if (act) {
+            while (scan[blk + 1] <= e) ++blk;
+            v = region[(int64_t)blk * kXChunk + off[blk] + (e - scan[blk])];
+        }
+        const uint32_t key = (v >> 24) * binw + (v & 0xFFFFFF);
+        (void)wave_lds_add(hist, key, act);
+        e += kHT;
     }
     __syncthreads();
     // buckets are zero on entry (K1 zeroes what it consumes): add the non-zero
@@ -249,25 +329,30 @@ HotPart hot_part_geometry(int64_t B, int64_t N, int32_t W) {
     while (((N + (1LL << bb) - 1) >> bb) > 4096) ++bb;
     g.bb = bb;
     g.nbins = (int32_t)((N + (1LL << bb) - 1) >> bb);
-    g.cap = B;
-    g.nblk = (int32_t)((B + kHT * kXPer - 1) / (kHT * kXPer));
-    g.ok = N > 0 && B > 0 && bb <= 24 && W >= 1 && (size_t)W * ((size_t)1 << bb) * 4 <= 128 * 1024 &&
-           (double)g.nbins * (double)B <= (double)(1LL << 28);
+    g.nblk = (int32_t)((B + kXChunk - 1) / kXChunk);
+    g.cap = (int64_t)g.nblk * kXChunk;  // region entries
+    const size_t ylds = 4 * ((size_t)W * ((size_t)1 << bb) + 2 * (size_t)g.nblk + 1);
+    g.ok = N > 0 && B > 0 && bb <= 24 && W >= 1 && ylds <= 150 * 1024;
     return g;
 }
 
+size_t hot_part_scratch(const HotPart& g) { return (size_t)g.cap + 2 * (size_t)g.nbins * (size_t)g.nblk; }
+
 hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
-                                 const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* cur,
-                                 uint32_t* region, hipStream_t st, int which) {
+                                 const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* scratch,
+                                 hipStream_t st, int which) {
     static const hipError_t attr =
-        hipFuncSetAttribute((const void*)k2y_bin_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+        hipFuncSetAttribute((const void*)k2y_bin_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     if (attr != hipSuccess) return attr;
+    uint32_t* region = scratch;
+    uint32_t* C = scratch + g.cap;
+    uint32_t* O = C + (size_t)g.nbins * g.nblk;
     if (which & 1)
         hipLaunchKernelGGL(k2x_partition, dim3(g.nblk), dim3(kHT), sizeof(uint32_t) * 2 * g.nbins, st, bnode, bts, B,
-                           N, cut, g, cur, region);
-    const size_t lds = sizeof(uint32_t) * (size_t)cut.n_win * ((size_t)1 << g.bb);
+                           N, cut, g, C, O, region);
+    const size_t lds = sizeof(uint32_t) * ((size_t)cut.n_win * ((size_t)1 << g.bb) + 2 * (size_t)g.nblk + 1);
     if (which & 2)
-        hipLaunchKernelGGL(k2y_bin_hist, dim3(g.nbins, kYSplits), dim3(kHT), lds, st, region, cur, g, cut.n_win, N,
+        hipLaunchKernelGGL(k2y_bin_hist, dim3(g.nbins, kYSplits), dim3(kHT), lds, st, region, C, O, g, cut.n_win, N,
                            buckets);
     return hipGetLastError();
 }

@@ -128,19 +128,16 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     Rec* lrec = reinterpret_cast<Rec*>(smem);
     const int64_t first = (int64_t)blockIdx.x * kK1Threads;
     const int64_t n = first + threadIdx.x;
-    // K2's bin cursors: consumed with the buckets (stream order: K2 has finished)
-    if (blockIdx.x == 0)
-        for (int i = threadIdx.x; i < a.n_cur; i += kK1Threads) a.zero_cur[i] = 0;
     __shared__ int64_t smn[kK1Threads / 64], smx[kK1Threads / 64];
     __shared__ StepShared ssh;
-    int64_t tmin = 0, tmax = 0;
+    int64_t tmin = 0, tmax = 0, pmn = 0, pmx = 0;
     if (STEP) {
         if (threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
-        batch_range<kK1Threads>(step.tile_mm, step.ntiles, smn, smx, tmin, tmax);
+        batch_range_load<kK1Threads>(step.tile_mm, step.ntiles, pmn, pmx);  // reduced after the SoA loads
     }
     StepSlots so;
+    Rec r;
     if (n < N) {
-        Rec r;
 #pragma unroll
         for (int k = 0; k < PD; ++k) {
             int64_t e = kTsInvalid;
@@ -214,9 +211,10 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
         r.pen32 = pen_fast ? (int32_t)r.pen : 0;
         r.flags = slow ? kRecSlow : 0;
         lrec[threadIdx.x] = r;
-        if (STEP) step_count<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, ssh, so);
     }
     if (STEP) {
+        batch_range_reduce<kK1Threads>(pmn, pmx, smn, smx, tmin, tmax);
+        if (n < N) step_count<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, ssh, so);
         step_reserve<kK1Threads>(so, ssh, step.st);  // (its barriers also order lrec)
         // stepped nodes (a few %) rebuild their record from the LDS copy of the NodeRec
         if (n < N && (so.slot0 >= 0 || so.slot1 >= 0))
@@ -411,10 +409,7 @@ __global__ __launch_bounds__(kK3Threads) void k3_eval(const NodeRec<PD, PR>* __r
 // ---------------------------------------------------------------- launchers
 template <int PD, int PR>
 static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t st) {
-    if (a.N <= 0) {
-        if (a.zero_cur && a.n_cur > 0) return hipMemsetAsync(a.zero_cur, 0, sizeof(uint32_t) * a.n_cur, st);
-        return hipSuccess;
-    }
+    if (a.N <= 0) return hipSuccess;
     const char* e = getenv("CRANE_K1_THREADS");
     const int T = e && atoi(e) == 256 ? 256 : 128;
     const unsigned grid = (unsigned)((a.N + T - 1) / T);

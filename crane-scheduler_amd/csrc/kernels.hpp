@@ -74,19 +74,21 @@ hipError_t launch_hot_count_binned(const int32_t* bnode, const int64_t* bts, int
                                    const HotCutoffs& cut, uint32_t* buckets, const HotBins& g, uint32_t* chunk_cnt,
                                    uint32_t* bin_tot, uint32_t* sorted, hipStream_t st);
 
-// Two-kernel partitioned K2 (hotcount.hip): per-bin regions of capacity B
+// Two-kernel partitioned K2 (hotcount.hip): each partition workgroup writes
+// its in-window bindings bin-contiguously into its own region and publishes
+// per-bin (count, offset); no global atomics besides the final bucket adds.
 struct HotPart {
     int32_t bb, nbins;  // 2^bb nodes per bin
-    int64_t cap;        // entries per bin region
+    int64_t cap;        // region entries (nblk * 2048)
     int32_t nblk;       // partition workgroups
     bool ok;
 };
 HotPart hot_part_geometry(int64_t B, int64_t N, int32_t W);
-// cur: [nbins] cursors, zero on entry; region [nbins * cap].
-// Adds into buckets[W][N], which must be zero on entry.
+size_t hot_part_scratch(const HotPart& g);  // uint32 entries: region + C + O
+// Adds into buckets[W][N], which must be zero on entry.  Scratch needs no initialisation.
 hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
-                                 const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* cur,
-                                 uint32_t* region, hipStream_t st, int which = 3);  // 1: k2x, 2: k2y
+                                 const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* scratch,
+                                 hipStream_t st, int which = 3);  // 1: k2x, 2: k2y
 
 // K3 step path (step.hip): per-batch node step tables + pair eval.
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
@@ -167,8 +169,6 @@ struct K1Args {
     void* out;              // NodeRec [N]
     uint32_t* cnt_out;      // [W][N] per-window counts (greedy) or null
     double* hvc_out;        // [N] hot values from the buckets, or null
-    uint32_t* zero_cur;     // [n_cur] K2 bin cursors zeroed with the buckets (no memset before the next K2)
-    int32_t n_cur;
 };
 // step (optional): also build the K3 step tables of a pod batch (K3a fused).
 hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr);

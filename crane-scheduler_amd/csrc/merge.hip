@@ -43,7 +43,9 @@ constexpr int kLevels = 101; // scores 0..100
 
 __device__ __forceinline__ int64_t stair_v(const uint32_t* c, int64_t k, const MergeArgs& a) {
     int64_t v = 0;
-    for (int w = 0; w < a.n_win; ++w) v += ((int64_t)c[w] + (a.win_inc[w] ? k : 0)) / a.win_count[w];
+#pragma unroll
+    for (int w = 0; w < kMaxWin; ++w)  // static indices: c stays in registers
+        if (w < a.n_win) v += ((int64_t)c[w] + (a.win_inc[w] ? k : 0)) / a.win_count[w];
     return v;
 }
 
@@ -57,8 +59,9 @@ struct RunIter {
         lvl = (int)(f < 0 ? 0 : (f > 100 ? 100 : f));
         int64_t d = INT64_MAX;
         if (lvl > 0)
-            for (int w = 0; w < a.n_win; ++w)
-                if (a.win_inc[w]) {
+#pragma unroll
+            for (int w = 0; w < kMaxWin; ++w)
+                if (w < a.n_win && a.win_inc[w]) {
                     const int64_t C = a.win_count[w];
                     d = min(d, C - ((int64_t)c[w] + k) % C);  // bindings until this window's quotient grows
                 }
@@ -80,29 +83,6 @@ __device__ __forceinline__ RunIter make_iter(const int64_t* base, const uint32_t
 
 __device__ __forceinline__ int64_t pack_level_key(int u, int64_t n) {
     return ((int64_t)u << 32) | (int64_t)(0xFFFFFFFFull - (uint64_t)n);
-}
-
-// ---- block scans (256 threads)
-__device__ __forceinline__ unsigned long long block_excl_scan_u64(unsigned long long v, unsigned long long* lds4,
-                                                                  unsigned long long* total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    unsigned long long x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) lds4[w] = x;
-    __syncthreads();
-    unsigned long long pre = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < kMT / 64; ++i) {
-        if (i < w) pre += lds4[i];
-        tot += lds4[i];
-    }
-    __syncthreads();
-    *total = tot;
-    return pre + x - v;
 }
 
 // ---------------------------------------------------------------- M1
@@ -147,50 +127,100 @@ __global__ __launch_bounds__(kMT) void m2_bsum(const int64_t* __restrict__ base,
 }
 
 // ---------------------------------------------------------------- M3 (one workgroup)
-__global__ __launch_bounds__(kM5T) void m3_scan(unsigned long long* __restrict__ v, int64_t len) {
-    __shared__ unsigned long long part[kM5T];
-    const int64_t per = (len + kM5T - 1) / kM5T;
-    const int64_t lo = threadIdx.x * per, hi = min(len, lo + per);
-    unsigned long long s = 0;
-    for (int64_t i = lo; i < hi; ++i) s += v[i];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int off = 1; off < kM5T; off <<= 1) {
-        const unsigned long long y = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-        __syncthreads();
-        part[threadIdx.x] += y;
-        __syncthreads();
+// Exclusive scan in place.  Each thread owns a contiguous run of the array and
+// reads it in batches of 8 independent loads; one workgroup scan of the run sums.
+__device__ __forceinline__ unsigned long long wg_excl_scan_u64(unsigned long long v, unsigned long long* part) {
+    // 1024 threads: wave scans, then a scan of the 16 wave totals
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned long long x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(x, o);
+        if (lane >= o) x += y;
     }
-    unsigned long long run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    for (int64_t i = lo; i < hi; ++i) {
-        const unsigned long long x = v[i];
-        v[i] = run;
-        run += x;
+    if (lane == 63) part[w] = x;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        unsigned long long t = threadIdx.x < kM5T / 64 ? part[threadIdx.x] : 0ull, u = t;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long y = __shfl_up(u, o);
+            if ((int)threadIdx.x >= o) u += y;
+        }
+        if (threadIdx.x < kM5T / 64) part[kM5T / 64 + threadIdx.x] = u - t;
+    }
+    __syncthreads();
+    return part[kM5T / 64 + w] + x - v;
+}
+
+__global__ __launch_bounds__(kM5T) void m3_scan(unsigned long long* __restrict__ v, int64_t len) {
+    __shared__ unsigned long long part[2 * (kM5T / 64)];
+    const int64_t per = (len + kM5T - 1) / kM5T;
+    const int64_t lo = min(len, (int64_t)threadIdx.x * per), hi = min(len, lo + per);
+    unsigned long long s = 0;
+    for (int64_t i0 = lo; i0 < hi; i0 += 8) {
+        unsigned long long x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = i0 + u < hi ? v[i0 + u] : 0ull;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += x[u];
+    }
+    unsigned long long run = wg_excl_scan_u64(s, part);
+    for (int64_t i0 = lo; i0 < hi; i0 += 8) {
+        unsigned long long x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = i0 + u < hi ? v[i0 + u] : 0ull;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u < hi) {
+                v[i0 + u] = run;
+                run += x[u];
+            }
     }
 }
 
 // ---------------------------------------------------------------- M4
+// Each node writes its runs at their positions in the stream: position of
+// (level u, node n) = off[u][block] + elements of level u from lower nodes of
+// the block.  Per-wave level counts go to LDS first (one barrier); then each
+// wave walks only the levels it has, with a wave scan per level (no barriers).
 __global__ __launch_bounds__(kMT) void m4_place(const int64_t* __restrict__ base, const uint8_t* __restrict__ leaf,
                                                 const uint32_t* __restrict__ cnt, int64_t N, MergeArgs a, int T,
                                                 int vlo, int64_t cap, const unsigned long long* __restrict__ off,
                                                 int64_t* __restrict__ stream) {
-    __shared__ unsigned long long lds4[kMT / 64];
+    __shared__ unsigned long long wc[kMT / 64][kLevels];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < (kMT / 64) * kLevels; i += kMT) (&wc[0][0])[i] = 0;
     const int64_t n = (int64_t)blockIdx.x * kMT + threadIdx.x;
     const bool mine = n < N && ((leaf[n] & 0x80) ? 0 : 1) == T;
+    __syncthreads();
+    {
+        RunIter it = make_iter(base, cnt, N, mine ? n : 0, mine ? cap : 0, a);
+        int lvl;
+        int64_t len;
+        while (it.next(a, lvl, len) && lvl >= vlo) atomicAdd(&wc[w][lvl], (unsigned long long)len);
+    }
+    __syncthreads();
     RunIter it = make_iter(base, cnt, N, mine ? n : 0, mine ? cap : 0, a);
     int lvl = -1;
     int64_t len = 0;
     bool have = mine && it.next(a, lvl, len);
     for (int u = 100; u >= vlo; --u) {
+        if (wc[w][u] == 0) continue;  // wave-uniform: this wave has no element at level u
         unsigned long long c = 0;
         while (have && lvl == u) {
             c += (unsigned long long)len;
             have = it.next(a, lvl, len);
         }
-        unsigned long long tot;
-        const unsigned long long ex = block_excl_scan_u64(c, lds4, &tot);
+        unsigned long long x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
         if (c) {
-            const unsigned long long p0 = off[(int64_t)(100 - u) * gridDim.x + blockIdx.x] + ex;
+            unsigned long long p0 = off[(int64_t)(100 - u) * gridDim.x + blockIdx.x] + x - c;
+            for (int i = 0; i < w; ++i) p0 += wc[i][u];
             const unsigned long long p1 = min(p0 + c, (unsigned long long)cap);
             for (unsigned long long p = p0; p < p1; ++p) stream[p] = pack_level_key(u, n);
         }
@@ -198,27 +228,32 @@ __global__ __launch_bounds__(kMT) void m4_place(const int64_t* __restrict__ base
 }
 
 // ---------------------------------------------------------------- M5
-// M5a: positions a[m] of the DaemonSet pods (pod order); zero the I-taker marks
+// M5a: positions a[m] of the DaemonSet pods (pod order); zero the I-taker marks.
+// One workgroup; each thread owns a contiguous run of pods (batched loads).
 __global__ __launch_bounds__(kM5T) void m5a_compact(const uint8_t* __restrict__ flags, int64_t P,
                                                     int32_t* __restrict__ apos, int32_t* __restrict__ tk) {
-    __shared__ int32_t wc[kM5T / 64];
-    int32_t run = 0;
-    for (int64_t t0 = 0; t0 < P; t0 += kM5T) {
-        const int64_t p = t0 + threadIdx.x;
-        const bool d = p < P && (flags[p] & 1u);
-        if (p < P) tk[p] = 0;
-        const uint64_t m = __ballot(d);
-        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-        if (lane == 0) wc[w] = __popcll(m);
-        __syncthreads();
-        int32_t pre = 0, tot = 0;
-        for (int i = 0; i < kM5T / 64; ++i) {
-            if (i < w) pre += wc[i];
-            tot += wc[i];
-        }
-        if (d) apos[run + pre + __popcll(m & ((1ull << lane) - 1))] = (int32_t)p;
-        run += tot;
-        __syncthreads();
+    __shared__ unsigned long long part[2 * (kM5T / 64)];
+    const int64_t per = ((P + kM5T - 1) / kM5T + 7) & ~7LL;
+    const int64_t lo = min(P, (int64_t)threadIdx.x * per), hi = min(P, lo + per);
+    unsigned long long c = 0;
+    for (int64_t i0 = lo; i0 < hi; i0 += 8) {
+        uint8_t f[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) f[u] = i0 + u < hi ? flags[i0 + u] : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c += f[u] & 1u;
+    }
+    int32_t run = (int32_t)wg_excl_scan_u64(c, part);
+    for (int64_t i0 = lo; i0 < hi; i0 += 8) {
+        uint8_t f[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) f[u] = i0 + u < hi ? flags[i0 + u] : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u < hi) {
+                tk[i0 + u] = 0;
+                if (f[u] & 1u) apos[run++] = (int32_t)(i0 + u);
+            }
     }
 }
 
@@ -271,35 +306,40 @@ __global__ __launch_bounds__(kM5T) void m5c_takers(const int64_t* __restrict__ g
     }
 }
 
-// M5d: pod order scan of the I-taker marks -> chosen node per pod (one workgroup)
+// M5d: pod order scan of the I-taker marks -> chosen node per pod (one
+// workgroup; contiguous runs of pods per thread, batched loads)
 __global__ __launch_bounds__(kM5T) void m5d_assign(const int64_t* __restrict__ Fs, int64_t nF,
                                                    const int64_t* __restrict__ Is, const int32_t* __restrict__ tk,
                                                    int64_t P, int64_t* __restrict__ chosen) {
-    __shared__ int32_t wc[kM5T / 64];
-    int64_t run = 0;
-    for (int64_t t0 = 0; t0 < P; t0 += kM5T) {
-        const int64_t p = t0 + threadIdx.x;
-        const int32_t t = p < P ? tk[p] : 0;
-        const uint64_t m = __ballot(t > 0);
-        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-        if (lane == 0) wc[w] = __popcll(m);
-        __syncthreads();
-        int32_t pre = 0, tot = 0;
-        for (int i = 0; i < kM5T / 64; ++i) {
-            if (i < w) pre += wc[i];
-            tot += wc[i];
-        }
-        if (p < P) {
+    __shared__ unsigned long long part[2 * (kM5T / 64)];
+    const int64_t per = ((P + kM5T - 1) / kM5T + 7) & ~7LL;
+    const int64_t lo = min(P, (int64_t)threadIdx.x * per), hi = min(P, lo + per);
+    unsigned long long c = 0;
+    for (int64_t i0 = lo; i0 < hi; i0 += 8) {
+        int32_t t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = i0 + u < hi ? tk[i0 + u] : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c += t[u] > 0;
+    }
+    int64_t run = (int64_t)wg_excl_scan_u64(c, part);  // I-takers before this run
+    for (int64_t i0 = lo; i0 < hi; i0 += 8) {
+        int32_t t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = i0 + u < hi ? tk[i0 + u] : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t p = i0 + u;
+            if (p >= hi) continue;
             int64_t key = -1;
-            if (t > 0) key = Is[t - 1];
-            else {
-                const int64_t j = p - (run + pre + __popcll(m & ((1ull << lane) - 1)));
-                if (j < nF) key = Fs[j];
+            if (t[u] > 0) {
+                key = Is[t[u] - 1];
+                ++run;
+            } else if (p - run < nF) {
+                key = Fs[p - run];
             }
             chosen[p] = key < 0 ? -1 : (int64_t)(0xFFFFFFFFull - ((uint64_t)key & 0xFFFFFFFFull));
         }
-        run += tot;
-        __syncthreads();
     }
 }
 

@@ -126,35 +126,8 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
 // a max.  One 64-bit atomicMax per pod per workgroup merges the slices.
 constexpr int kK3sWaves = 4;
 constexpr int kK3sThreads = kK3sWaves * 64;
-constexpr int kK3sS1 = 1024;  // Step1 records staged per round (16 KB)
-constexpr int kK3sVR = 64;    // VRec records staged per round
-
-// [lo, hi) of part u of U equal parts of n
-__device__ __forceinline__ void part_range(int32_t n, int32_t u, int32_t U, int32_t& lo, int32_t& hi) {
-    const int32_t per = (n + U - 1) / U;
-    lo = min(n, u * per);
-    hi = min(n, lo + per);
-}
-
-// Exclusive prefix of the kStepSub sub-list lengths of (kind T, list k) into
-// pre[0..kStepSub] (LDS); returns the total.  All threads call it.
-__device__ __forceinline__ int32_t sub_prefix(const int32_t* __restrict__ hdr, int T, int k, int32_t* pre) {
-    static_assert(kStepSub == 64, "one wave scans the sub-lists");
-    __syncthreads();  // earlier readers of pre are done
-    if (threadIdx.x < 64) {
-        const int32_t c = hdr[threadIdx.x * kHdrStride + kHdrN1 + 2 * T + k];
-        int32_t x = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(x, o);
-            if ((int)threadIdx.x >= o) x += y;
-        }
-        pre[threadIdx.x] = x - c;
-        if (threadIdx.x == 63) pre[64] = x;
-    }
-    __syncthreads();
-    return pre[64];
-}
+constexpr int kK3sS1 = 512;  // Step1 records staged per round and pod kind (8 KB)
+constexpr int kK3sVR = 32;   // VRec records staged per round and pod kind
 
 // global position in the [kStepSub][cap] layout of element i of the concatenated sub-lists
 __device__ __forceinline__ int64_t sub_pos(const int32_t* pre, int32_t i, int64_t cap) {
@@ -165,33 +138,156 @@ __device__ __forceinline__ int64_t sub_pos(const int32_t* pre, int32_t i, int64_
     return (int64_t)lo * cap + (i - pre[lo]);
 }
 
+// The four stepped lists: L = 2 * kind + (0: Step1, 1: VRec); header column kHdrN1 + L.
 template <int NB>
-__device__ __forceinline__ int32_t k3s_kind(int T, bool any, int64_t tnow, int32_t best, const StepTables& st,
-                                            int32_t r, int32_t R, int4* l1, VRec<NB>* lv, int32_t* pre) {
-    const int4* __restrict__ g1 = reinterpret_cast<const int4*>(st.single + (int64_t)T * st.npad);
-    const VRec<NB>* __restrict__ gv = reinterpret_cast<const VRec<NB>*>(st.multi) + (int64_t)T * st.npad;
-    int32_t a0, a1;
-    part_range(sub_prefix(st.hdr, T, 0, pre), r, R, a0, a1);
-    // one-step records, kK3sS1 per round
-    for (int32_t j0 = a0; j0 < a1; j0 += kK3sS1) {
-        const int32_t n1 = min(kK3sS1, a1 - j0);
-        __syncthreads();  // the previous round's readers are done
-        for (int32_t i = threadIdx.x; i < n1; i += 4 * kK3sThreads) {  // 4 loads in flight per thread
+__global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int32_t* __restrict__ perm,
+                                                        const int64_t* __restrict__ pnow, int64_t P,
+                                                        int64_t node_offset, int32_t R,
+                                                        long long* __restrict__ keys) {
+    static_assert(kStepSub == 64 && kK3sWaves == 4, "one wave scans each list's sub-list lengths");
+    static_assert(sizeof(VRec<NB>) % 16 == 0, "VRec must be a whole number of int4");
+    constexpr int kVRI4 = (int)(sizeof(VRec<NB>) / 16);
+    __shared__ int4 l1[2][kK3sS1];
+    __shared__ VRec<NB> lv[2][kK3sVR];
+    __shared__ int32_t pre[4][kStepSub + 1];
+    __shared__ int32_t flat[2][kK3sWaves];
+    __shared__ int64_t wr[2][2][kK3sWaves];  // per kind and wave: min, max pod time
+    __shared__ int32_t nin[2], umax[2];      // staged in-range records, uniform maximum (per kind)
+    const int64_t b = blockIdx.x;
+    const int32_t r = (int32_t)(b % R);
+    const int64_t grp = b / R;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // K3p wrote the pods in partitioned order: two independent coalesced loads
+    const int64_t slot = grp * kK3sThreads + threadIdx.x;
+    const bool live = slot < P;
+    const int32_t praw = live ? perm[slot] : 0;
+    const int64_t tnow = live ? pnow[slot] : 0;
+    // header: wave w scans list w's sub-list lengths; the flat maxima ride along
+    {
+        const int32_t* h = st.hdr + lane * kHdrStride;
+        const int32_t c = h[kHdrN1 + w];
+        int32_t f = w < 2 ? h[kHdrFlat + w] : -1;
+        int32_t x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) f = max(f, __shfl_xor(f, o));
+        pre[w][lane] = x - c;
+        if (lane == 63) pre[w][64] = x;
+        if (lane == 0) flat[0][w] = f;
+    }
+    const bool ds = praw < 0;
+    const int32_t pod = praw & 0x7FFFFFFF;
+    const bool wn = __ballot(live && !ds) != 0, wd = __ballot(ds) != 0;
+    // the workgroup's pod time range per kind: a record whose step lies outside it
+    // gives the same key to every pod of that kind here (one max, no per-lane work)
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+        const bool mine = live && (T ? ds : !ds);
+        int64_t mn = mine ? tnow : INT64_MAX, mx = mine ? tnow : INT64_MIN;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            mn = min(mn, (int64_t)__shfl_xor((long long)mn, o));
+            mx = max(mx, (int64_t)__shfl_xor((long long)mx, o));
+        }
+        if (lane == 0) {
+            wr[T][0][w] = mn;
+            wr[T][1][w] = mx;
+        }
+    }
+    if (threadIdx.x < 2) {
+        nin[threadIdx.x] = 0;
+        umax[threadIdx.x] = -1;
+    }
+    const bool bn = __syncthreads_or(live && !ds), bd = __syncthreads_or(ds);  // (also orders the LDS above)
+    int64_t tlo[2], thi[2];
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+        tlo[T] = min(min(wr[T][0][0], wr[T][0][1]), min(wr[T][0][2], wr[T][0][3]));
+        thi[T] = max(max(wr[T][1][0], wr[T][1][1]), max(wr[T][1][2], wr[T][1][3]));
+    }
+    // the flat maxima enter once per pod (slice 0)
+    int32_t best_n = r == 0 ? flat[0][0] : -1, best_d = r == 0 ? flat[0][1] : -1;
+    // this workgroup's slice [lo, hi) of each list (lists of a kind without pods here: empty)
+    int32_t lo[4], hi[4];
+#pragma unroll
+    for (int L = 0; L < 4; ++L) {
+        const int32_t n = ((L < 2) ? bn : bd) ? pre[L][64] : 0;
+        const int32_t per = (n + R - 1) / R;
+        lo[L] = min(n, r * per);
+        hi[L] = min(n, lo[L] + per);
+    }
+    int32_t um0 = -1, um1 = -1;  // this thread's share of the uniform maxima
+    for (bool first = true;; first = false) {
+        int32_t take[4];
+#pragma unroll
+        for (int L = 0; L < 4; ++L) take[L] = min((L & 1) ? kK3sVR : kK3sS1, hi[L] - lo[L]);
+        if (take[0] + take[1] + take[2] + take[3] == 0) break;
+        if (!first) {
+            __syncthreads();  // the previous round's readers are done
+            if (threadIdx.x < 2) nin[threadIdx.x] = 0;
+            __syncthreads();
+        }
+        // one pass over [S1 kind 0 | VR kind 0 (int4 words) | S1 kind 1 | VR kind 1]:
+        // one-step records outside the pod range fold into the uniform maxima, the
+        // rest (and every multi-step record) are staged in LDS
+        const int32_t e1 = take[0], e2 = e1 + take[1] * kVRI4, e3 = e2 + take[2], e4 = e3 + take[3] * kVRI4;
+        for (int32_t i0 = threadIdx.x; i0 < e4; i0 += 4 * kK3sThreads) {
+            const int4* src[4];
+            bool one[4];
+            int kind[4];
+            int4* dst[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {  // addresses first (branches only select pointers)
+                const int32_t e = min(i0 + u * kK3sThreads, e4 - 1);  // past the end: repeat the last element
+                const int T = e >= e2;
+                const int32_t f = T ? e - e2 : e;  // offset within the kind
+                const int32_t t1 = T ? take[2] : take[0], lo1 = T ? lo[2] : lo[0], lov = T ? lo[3] : lo[1];
+                const int4* g1 = reinterpret_cast<const int4*>(st.single + (int64_t)T * st.npad);
+                const VRec<NB>* gv = reinterpret_cast<const VRec<NB>*>(st.multi) + (int64_t)T * st.npad;
+                const int32_t g4 = f - t1, j = g4 / kVRI4, wd4 = g4 - j * kVRI4;
+                one[u] = f < t1;
+                kind[u] = T;
+                src[u] = one[u] ? g1 + sub_pos(pre[2 * T], lo1 + f, st.cap)
+                                : reinterpret_cast<const int4*>(gv + sub_pos(pre[2 * T + 1], lov + j, st.cap)) + wd4;
+                dst[u] = reinterpret_cast<int4*>(&lv[T][j]) + wd4;
+            }
             int4 q[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (i + u * kK3sThreads < n1) q[u] = g1[sub_pos(pre, j0 + i + u * kK3sThreads, st.cap)];
+            for (int u = 0; u < 4; ++u) q[u] = *src[u];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (i + u * kK3sThreads < n1) l1[i + u * kK3sThreads] = q[u];
+            for (int u = 0; u < 4; ++u) {
+                if (i0 + u * kK3sThreads >= e4) continue;
+                if (!one[u]) {
+                    *dst[u] = q[u];
+                    continue;
+                }
+                const int T = kind[u];
+                const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q[u].y << 32) | (uint32_t)q[u].x);
+                const int64_t lo_t = T ? tlo[1] : tlo[0], hi_t = T ? thi[1] : thi[0];
+                if (bp <= lo_t || bp > hi_t) {  // every pod of the kind here is on one side of the step
+                    const int32_t k = bp <= lo_t ? q[u].w : q[u].z;
+                    if (T) um1 = max(um1, k);
+                    else um0 = max(um0, k);
+                } else {
+                    l1[T][atomicAdd(&nin[T], 1)] = q[u];
+                }
+            }
         }
         __syncthreads();
-        if (any) {
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+            if (!(T ? wd : wn)) continue;
+            int32_t best = T ? best_d : best_n;
+            const int32_t n1 = nin[T];
             int32_t i = 0;
             for (; i + 8 <= n1; i += 8) {
                 int4 q[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) q[u] = l1[i + u];  // broadcast LDS reads
+                for (int u = 0; u < 8; ++u) q[u] = l1[T][i + u];  // broadcast LDS reads
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q[u].y << 32) | (uint32_t)q[u].x);
@@ -199,77 +295,35 @@ __device__ __forceinline__ int32_t k3s_kind(int T, bool any, int64_t tnow, int32
                 }
             }
             for (; i < n1; ++i) {
-                const int4 q = l1[i];
+                const int4 q = l1[T][i];
                 const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q.y << 32) | (uint32_t)q.x);
                 best = max(best, tnow >= bp ? q.w : q.z);
             }
-        }
-    }
-    // multi-step records, kK3sVR per round (copied as int4 words)
-    static_assert(sizeof(VRec<NB>) % 16 == 0, "VRec must be a whole number of int4");
-    constexpr int kVRI4 = (int)(sizeof(VRec<NB>) / 16);
-    int32_t m0, m1;
-    part_range(sub_prefix(st.hdr, T, 1, pre), r, R, m0, m1);
-    for (int32_t j0 = m0; j0 < m1; j0 += kK3sVR) {
-        const int32_t nv = min(kK3sVR, m1 - j0);
-        __syncthreads();
-        int4* dst = reinterpret_cast<int4*>(lv);
-        for (int32_t i = threadIdx.x; i < nv * kVRI4; i += kK3sThreads) {
-            const int32_t e = i / kVRI4, w = i - e * kVRI4;
-            dst[i] = reinterpret_cast<const int4*>(gv + sub_pos(pre, j0 + e, st.cap))[w];
-        }
-        __syncthreads();
-        if (any)
-            for (int32_t j = 0; j < nv; ++j) {
-                const VRec<NB>& v = lv[j];
+            for (int32_t j = 0; j < take[2 * T + 1]; ++j) {
+                const VRec<NB>& v = lv[T][j];
                 int32_t k = v.key[0];
 #pragma unroll
                 for (int s = 0; s < NB; ++s) k = tnow >= v.bp[s] ? v.key[s + 1] : k;
                 best = max(best, k);
             }
-    }
-    return best;
-}
-
-template <int NB>
-__global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int32_t* __restrict__ perm,
-                                                        const int64_t* __restrict__ pnow, int64_t P,
-                                                        int64_t node_offset, int32_t R,
-                                                        long long* __restrict__ keys) {
-    __shared__ int4 l1[kK3sS1];
-    __shared__ VRec<NB> lv[kK3sVR];
-    __shared__ int32_t pre[kStepSub + 1];
-    const int64_t b = blockIdx.x;
-    const int32_t r = (int32_t)(b % R);
-    const int64_t grp = b / R;
-    // K3p wrote the pods in partitioned order: two independent coalesced loads
-    const int64_t slot = grp * kK3sThreads + threadIdx.x;
-    const bool live = slot < P;
-    const int32_t praw = live ? perm[slot] : 0;
-    const int64_t tnow = live ? pnow[slot] : 0;
-    const bool ds = praw < 0;
-    const int32_t pod = praw & 0x7FFFFFFF;
-    // wave-uniform "this wave has pods of the kind"; workgroup-uniform "stage the kind"
-    const bool wn = __ballot(live && !ds) != 0, wd = __ballot(ds) != 0;
-    const bool bn = __syncthreads_or(live && !ds), bd = __syncthreads_or(ds);
-    int32_t best_n = -1, best_d = -1;
-    if (r == 0) {  // the flat maxima (max over the sub-lists) enter once per pod
-        int32_t fn = -1, fd = -1;
-        if ((threadIdx.x & 63) < kStepSub) {
-            fn = st.hdr[(threadIdx.x & 63) * kHdrStride + kHdrFlat + 0];
-            fd = st.hdr[(threadIdx.x & 63) * kHdrStride + kHdrFlat + 1];
+            if (T) best_d = best;
+            else best_n = best;
         }
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            fn = max(fn, __shfl_xor(fn, o));
-            fd = max(fd, __shfl_xor(fd, o));
-        }
-        best_n = fn;
-        best_d = fd;
+        for (int L = 0; L < 4; ++L) lo[L] += take[L];
     }
-    if (bn) best_n = k3s_kind<NB>(0, wn, tnow, best_n, st, r, R, l1, lv, pre);
-    if (bd) best_d = k3s_kind<NB>(1, wd, tnow, best_d, st, r, R, l1, lv, pre);
-    const int32_t best = ds ? best_d : best_n;
+    // uniform maxima: wave reduce, one LDS atomic per wave and kind
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        um0 = max(um0, __shfl_xor(um0, o));
+        um1 = max(um1, __shfl_xor(um1, o));
+    }
+    if (lane == 0) {
+        if (um0 >= 0) atomicMax(&umax[0], um0);
+        if (um1 >= 0) atomicMax(&umax[1], um1);
+    }
+    __syncthreads();
+    const int32_t best = ds ? max(best_d, umax[1]) : max(best_n, umax[0]);
     if (live && best >= 0) {
         const int64_t sc = best >> 24;
         const int64_t n = 0xFFFFFF - (best & 0xFFFFFF);

@@ -46,16 +46,23 @@ __device__ __forceinline__ int32_t key_of(int T, int64_t t, int32_t score, const
     return (T == 1 || !(t < r.e_fail)) ? pack_key(score, n) : -1;
 }
 
-// Batch time range [tmin, tmax] from K3p's per-tile partials; every thread of
-// the workgroup gets it (sm: >= BS/64 entries of LDS per array).
+// Batch time range [tmin, tmax] from K3p's per-tile partials, in two parts so
+// a kernel can issue the loads early and reduce after its own loads:
+// batch_range_load (per-thread partials), batch_range_reduce (every thread of
+// the workgroup gets the result; sm*: >= BS/64 LDS entries; has a barrier).
 template <int BS>
-__device__ __forceinline__ void batch_range(const int64_t* __restrict__ tile_mm, int32_t ntiles, int64_t* smn,
-                                            int64_t* smx, int64_t& tmin, int64_t& tmax) {
-    int64_t mn = INT64_MAX, mx = INT64_MIN;
+__device__ __forceinline__ void batch_range_load(const int64_t* __restrict__ tile_mm, int32_t ntiles, int64_t& mn,
+                                                 int64_t& mx) {
+    mn = INT64_MAX;
+    mx = INT64_MIN;
     for (int i = threadIdx.x; i < ntiles; i += BS) {
         mn = min(mn, tile_mm[2 * i]);
         mx = max(mx, tile_mm[2 * i + 1]);
     }
+}
+template <int BS>
+__device__ __forceinline__ void batch_range_reduce(int64_t mn, int64_t mx, int64_t* smn, int64_t* smx, int64_t& tmin,
+                                                   int64_t& tmax) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
         mn = min(mn, (int64_t)__shfl_xor((long long)mn, o));
@@ -73,6 +80,13 @@ __device__ __forceinline__ void batch_range(const int64_t* __restrict__ tile_mm,
         tmin = min(tmin, smn[i]);
         tmax = max(tmax, smx[i]);
     }
+}
+template <int BS>
+__device__ __forceinline__ void batch_range(const int64_t* __restrict__ tile_mm, int32_t ntiles, int64_t* smn,
+                                            int64_t* smx, int64_t& tmin, int64_t& tmax) {
+    int64_t mn, mx;
+    batch_range_load<BS>(tile_mm, ntiles, mn, mx);
+    batch_range_reduce<BS>(mn, mx, smn, smx, tmin, tmax);
 }
 
 // Per node and pod kind: the flat key (-1 if stepped or never feasible) and,
@@ -93,57 +107,49 @@ struct StepShared {
     int32_t fm[2][16];  // per-wave flat maxima (<= 1024 threads)
 };
 
-// The node's in-range expiries for kind T, sorted ascending, INT64_MAX past them;
-// returns (count, distinct count).
+// The node's expiries for kind T with those outside (tmin, tmax] replaced by
+// INT64_MAX; returns their count and the min / max of the in-range ones.
 template <int PD, int PR, int T>
 __device__ __forceinline__ void step_points(const NodeRec<PD, PR>& r, int64_t tmin, int64_t tmax, int64_t* c,
-                                            int& cnt, int& distinct) {
+                                            int& cnt, int64_t& mn, int64_t& mx) {
     constexpr int NB = PR + 2;
 #pragma unroll
     for (int k = 0; k < PR; ++k) c[k] = r.e_prio[k];
     c[PR] = r.e_hv;
     c[PR + 1] = T == 0 ? r.e_fail : INT64_MIN;  // DaemonSet pods bypass the Filter
     cnt = 0;
+    mn = INT64_MAX;
+    mx = INT64_MIN;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
         const bool in = c[j] > tmin && c[j] <= tmax;
         c[j] = in ? c[j] : INT64_MAX;
         cnt += in;
-    }
-    distinct = 0;
-    if (cnt > 0) {
-#pragma unroll
-        for (int i = 0; i < NB; ++i)  // odd-even transposition sort (static indices)
-#pragma unroll
-            for (int j = i & 1; j + 1 < NB; j += 2) {
-                const int64_t x = c[j], y = c[j + 1];
-                c[j] = min(x, y);
-                c[j + 1] = max(x, y);
-            }
-        // a predicate's expiry equals its metric's priority expiry when both use one metric
-#pragma unroll
-        for (int j = 0; j < NB; ++j) distinct += c[j] != INT64_MAX && (j == 0 || c[j] != c[j - 1]);
+        mn = min(mn, c[j]);
+        mx = in ? max(mx, c[j]) : mx;
     }
 }
 
+// Phase 1.  A node with one distinct in-range expiry (a predicate's expiry
+// equals its metric's priority expiry when both use one metric) is a Step1.
 template <int PD, int PR>
 __device__ __forceinline__ void step_count(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
                                            double wsum, int32_t noprio, StepShared& sh, StepSlots& o) {
     const int32_t s0 = score_at<PD, PR>(tmin, r, wsum, noprio);
     auto kind = [&](auto Tc, int32_t& flat, int32_t& slot, bool& multi) {
         constexpr int T = decltype(Tc)::value;
-        int64_t c[PR + 2];
-        int cnt, distinct;
-        step_points<PD, PR, T>(r, tmin, tmax, c, cnt, distinct);
+        int64_t c[PR + 2], mn, mx;
+        int cnt;
+        step_points<PD, PR, T>(r, tmin, tmax, c, cnt, mn, mx);
         flat = cnt == 0 ? key_of<PD, PR>(T, tmin, s0, r, n) : -1;
-        multi = distinct > 1;
+        multi = mn != mx;
         slot = cnt == 0 ? -1 : atomicAdd(&sh.lc[T][multi ? 1 : 0], 1);
     };
     kind(std::integral_constant<int, 0>{}, o.flat0, o.slot0, o.multi0);
     kind(std::integral_constant<int, 1>{}, o.flat1, o.slot1, o.multi1);
 }
 
-// Write node n's record(s) at the reserved positions (after step_commit).
+// Phase 2: write node n's record(s) at the reserved positions (after step_reserve).
 template <int PD, int PR>
 __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
                                           double wsum, int32_t noprio, const StepShared& sh, const StepSlots& o,
@@ -152,18 +158,26 @@ __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, i
     auto kind = [&](auto Tc, int32_t slot, bool multi) {
         constexpr int T = decltype(Tc)::value;
         if (slot < 0) return;
-        int64_t c[NB];
-        int cnt, distinct;
-        step_points<PD, PR, T>(r, tmin, tmax, c, cnt, distinct);
+        int64_t c[NB], mn, mx;
+        int cnt;
+        step_points<PD, PR, T>(r, tmin, tmax, c, cnt, mn, mx);
         const int32_t k0 = key_of<PD, PR>(T, tmin, score_at<PD, PR>(tmin, r, wsum, noprio), r, n);
-        // key of the step starting at c[j], evaluated at its first instant (equal expiries give equal keys)
+        // key of the step starting at an expiry, evaluated at its first instant
         if (!multi) {
             Step1 v;
-            v.bp = c[0];
+            v.bp = mn;
             v.k0 = k0;
-            v.k1 = key_of<PD, PR>(T, c[0], score_at<PD, PR>(c[0], r, wsum, noprio), r, n);
+            v.k1 = key_of<PD, PR>(T, mn, score_at<PD, PR>(mn, r, wsum, noprio), r, n);
             st.single[(int64_t)T * st.npad + sh.gb[T][0] + slot] = v;
-        } else {
+        } else {  // rare: sort the expiries (equal ones give equal keys)
+#pragma unroll
+            for (int i = 0; i < NB; ++i)  // odd-even transposition sort (static indices)
+#pragma unroll
+                for (int j = i & 1; j + 1 < NB; j += 2) {
+                    const int64_t x = c[j], y = c[j + 1];
+                    c[j] = min(x, y);
+                    c[j + 1] = max(x, y);
+                }
             VRec<NB> v;
             v.cnt = cnt;
             v.key[0] = k0;
