@@ -107,7 +107,7 @@ struct crane_dyn {
     DevBuf<unsigned long long> mH, mbs;  // merge-form greedy (merge.hip)
     DevBuf<int32_t> mflag, mapos, mtk;
     DevBuf<int64_t> mFs, mIs, mgi;
-    DevBuf<int32_t> sperm, shdr;  // K3 step path scratch (step.hip)
+    DevBuf<int32_t> sperm, scnt;  // K3 step path scratch (step.hip)
     DevBuf<int64_t> stile, spnow;
     DevBuf<unsigned char> svrec;
     DevBuf<Step1> sstep1;
@@ -277,7 +277,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
     h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
     h->mFs.release(); h->mIs.release(); h->mgi.release();
-    h->sperm.release(); h->shdr.release(); h->stile.release(); h->spnow.release(); h->svrec.release(); h->sstep1.release();
+    h->sperm.release(); h->scnt.release(); h->stile.release(); h->spnow.release(); h->svrec.release(); h->sstep1.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -466,20 +466,23 @@ static int eval_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint
     if (!matrix && k3_variant() == 5 && h->N < kStepMaxNodes && P < (1LL << 31)) {
         // step path: K3p (pod partition, key init, header reset) -> [K1 +] K3a (step
         // tables; fused into the node pass when the records are stale) -> K3s (pairs)
-        const StepGeometry g = step_geometry(P, h->N);
+        const char* fe = getenv("CRANE_K1_FUSE");
+        const bool fuse = h->rec_dirty && !(fe && fe[0] == '0');
+        const int32_t bs = fuse ? k1_threads() : kStepSeg;  // producer workgroup size
+        const int32_t nblk = (int32_t)((h->N + bs - 1) / bs);
+        const StepGeometry g = step_geometry(P, h->N, nblk);
         HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
         HIPTRY(h, h->stile.reserve((size_t)(2 * g.ntiles)));
         HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
-        HIPTRY(h, h->shdr.reserve((size_t)kHdrLen));
+        HIPTRY(h, h->scnt.reserve((size_t)std::max<int32_t>(nblk, 1) * 6));  // cnt [nblk][4] + flat [nblk][2]
         HIPTRY(h, h->sstep1.reserve((size_t)(2 * g.npad)));
         HIPTRY(h, h->svrec.reserve((size_t)(2 * g.npad) * step_vrec_bytes(h->shape)));
-        StepTables stt{h->shdr.p, h->sstep1.p, h->svrec.p, g.cap, g.npad};
+        StepTables stt{h->scnt.p, h->scnt.p + (size_t)nblk * 4, h->sstep1.p, h->svrec.p, g.npad, bs, nblk};
         HIPTRY(h, prof_begin(h, st));
         HIPTRY(h, launch_step_pods(d_now, d_flags, P, d_keys, stt, g, h->sperm.p, h->spnow.p, h->stile.p, st));
         HIPTRY(h, prof_mark(h, st, "k3p_pods"));
         if (P == 0) return CRANE_OK;
-        const char* fe = getenv("CRANE_K1_FUSE");
-        if (h->rec_dirty && !(fe && fe[0] == '0')) {
+        if (fuse) {
             K1Step ks{h->stile.p, (int32_t)g.ntiles, h->dp.noprio, h->dp.wsum, stt};
             int rc = node_pass_locked(h, st, nullptr, &ks);
             if (rc) return rc;
@@ -695,8 +698,8 @@ int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod
             HIPTRY(h, h->mFs.reserve((size_t)std::max<int64_t>(nF, 1)));
             HIPTRY(h, h->mIs.reserve((size_t)std::max<int64_t>(nI, 1)));
             HIPTRY(h, h->mapos.reserve((size_t)std::max<int64_t>(Pd, 1)));
-            HIPTRY(h, h->mtk.reserve((size_t)P));
-            HIPTRY(h, h->mgi.reserve((size_t)std::max<int64_t>(nI, 1)));
+            HIPTRY(h, h->mtk.reserve((size_t)std::max<int64_t>(nI, 1)));
+            HIPTRY(h, h->mgi.reserve((size_t)std::max<int64_t>(nI, 1) + 1));
             if (nF) HIPTRY(h, launch_merge_stream(h->gbase.p, h->gleaf.p, h->gcnt.p, N, ma, 0, vF, nF, h->mbs.p,
                                                   h->mFs.p, st));
             if (nI) HIPTRY(h, launch_merge_stream(h->gbase.p, h->gleaf.p, h->gcnt.p, N, ma, 1, vI, nI, h->mbs.p,

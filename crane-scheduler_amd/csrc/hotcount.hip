@@ -15,6 +15,8 @@
 // Order inside a bin is not deterministic; counts are.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "dyn_types.hpp"
 #include "kernels.hpp"
 
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(kHT) void k2d_bin_hist(const uint32_t* __restrict__
 // LDS atomic (one atomic per wave for the wave's most common key).
 constexpr int kXPer = 8;     // bindings per thread in X
 constexpr int kXChunk = kHT * kXPer;
-constexpr int kYSplits = 8;  // workgroups per bin in Y
+constexpr int kYSplits = 16;  // workgroups per bin in Y (Zipf-hot bins want many, each pays a prologue)
 
 // LDS atomicAdd of `add` to a[key] for every active lane, the lanes sharing the
 // first active lane's key merged into one atomic; returns each lane's old value
@@ -186,6 +188,24 @@ __device__ __forceinline__ uint32_t wave_lds_add(uint32_t* a, uint32_t key, bool
     const uint32_t base = __shfl(old, lead);
     if (act && key != kl) return atomicAdd(&a[key], 1u);
     return base + rank;
+}
+
+// exclusive workgroup scan (kHT threads): wave scans + a scan of the wave totals
+__device__ __forceinline__ uint32_t wg_excl_scan_u32(uint32_t v, uint32_t* part) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) part[w] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+#pragma unroll
+    for (int i = 0; i < kHT / 64; ++i) pre += i < w ? part[i] : 0u;
+    __syncthreads();
+    return pre + x - v;
 }
 
 __global__ __launch_bounds__(kHT) void k2x_partition(const int32_t* __restrict__ bnode,
@@ -221,18 +241,10 @@ __global__ __launch_bounds__(kHT) void k2x_partition(const int32_t* __restrict__
     __syncthreads();
     // exclusive scan of hist over bins (each thread a contiguous run of bins)
     const int per = (g.nbins + kHT - 1) / kHT;
-    const int lo = threadIdx.x * per, hi = min(g.nbins, lo + per);
+    const int lo = min(g.nbins, (int)threadIdx.x * per), hi = min(g.nbins, lo + per);
     uint32_t sum = 0;
     for (int i = lo; i < hi; ++i) sum += hist[i];
-    part[threadIdx.x] = sum;
-    __syncthreads();
-    for (int o = 1; o < kHT; o <<= 1) {  // Hillis-Steele over the 256 partials
-        const uint32_t y = (int)threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += y;
-        __syncthreads();
-    }
-    uint32_t run = part[threadIdx.x] - sum;
+    uint32_t run = wg_excl_scan_u32(sum, part);
     for (int i = lo; i < hi; ++i) {
         const uint32_t c = hist[i];
         off[i] = run;
@@ -260,36 +272,30 @@ __global__ __launch_bounds__(kHT) void k2y_bin_hist(const uint32_t* __restrict__
     uint32_t* off = scan + g.nblk + 1;
     for (int i = threadIdx.x; i < W * binw; i += kHT) hist[i] = 0;
     // scan of the bin's per-source-region counts
-    const int per = (g.nblk + kHT - 1) / kHT;
-    const int lo = threadIdx.x * per, hi = min(g.nblk, lo + per);
-    uint32_t sum = 0;
-    for (int i = lo; i < hi; ++i) {
-        const uint32_t c = C[(int64_t)bin * g.nblk + i];
-        scan[i] = c;
+    // (coalesced: consecutive threads read consecutive regions' counts)
+    for (int i = threadIdx.x; i < g.nblk; i += kHT) {
+        scan[i] = C[(int64_t)bin * g.nblk + i];
         off[i] = O[(int64_t)bin * g.nblk + i];
-        sum += c;
     }
-    part[threadIdx.x] = sum;
     __syncthreads();
-    for (int o = 1; o < kHT; o <<= 1) {
-        const uint32_t y = (int)threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += y;
-        __syncthreads();
-    }
-    uint32_t run = part[threadIdx.x] - sum;
+    const int per = (g.nblk + kHT - 1) / kHT;
+    const int lo = min(g.nblk, (int)threadIdx.x * per), hi = min(g.nblk, lo + per);
+    uint32_t sum = 0;
+    for (int i = lo; i < hi; ++i) sum += scan[i];
+    uint32_t run = wg_excl_scan_u32(sum, part);
     for (int i = lo; i < hi; ++i) {
         const uint32_t c = scan[i];
         scan[i] = run;
         run += c;
     }
-    if (threadIdx.x == kHT - 1) scan[g.nblk] = part[kHT - 1];
+    if (threadIdx.x == kHT - 1) scan[g.nblk] = run;
     __syncthreads();
     const uint32_t len = scan[g.nblk];
     // an even share of the bin's entries: Zipf-hot bins spread over the splits
     const uint32_t e_lo = (uint32_t)((uint64_t)len * split / gridDim.y);
     const uint32_t e_hi = (uint32_t)((uint64_t)len * (split + 1) / gridDim.y);
-    // each lane walks e = e_lo + tid, + kHT, ... advancing its source region as it goes
+    // each lane walks e = e_lo + tid, + kHT, ... advancing its source region as it
+    // goes; kXPer entries per batch, their loads issued together
     uint32_t e = e_lo + threadIdx.x;
     int blk = 0;
     if (e < e_hi) {  // first region: binary search, then forward steps
@@ -301,16 +307,23 @@ __global__ __launch_bounds__(kHT) void k2y_bin_hist(const uint32_t* __restrict__
         }
         blk = l;
     }
-    for (uint32_t e0 = e_lo; e0 < e_hi; e0 += kHT) {
-        const bool act = e < e_hi;
-        uint32_t v = 0;
-        if (act) {
-            while (scan[blk + 1] <= e) ++blk;
-            v = region[(int64_t)blk * kXChunk + off[blk] + (e - scan[blk])];
+    for (uint32_t e0 = e_lo; e0 < e_hi; e0 += kHT * kXPer) {
+        uint32_t v[kXPer];
+#pragma unroll
+        for (int u = 0; u < kXPer; ++u) {
+            const uint32_t eu = e + u * kHT;
+            v[u] = 0xFFFFFFFFu;
+            if (eu < e_hi) {
+                while (scan[blk + 1] <= eu) ++blk;
+                v[u] = region[(int64_t)blk * kXChunk + off[blk] + (eu - scan[blk])];
+            }
         }
-        const uint32_t key = (v >> 24) * binw + (v & 0xFFFFFF);
-        (void)wave_lds_add(hist, key, act);
-        e += kHT;
+#pragma unroll
+        for (int u = 0; u < kXPer; ++u) {
+            const bool act = v[u] != 0xFFFFFFFFu;
+            (void)wave_lds_add(hist, act ? (v[u] >> 24) * binw + (v[u] & 0xFFFFFF) : 0u, act);
+        }
+        e += kHT * kXPer;
     }
     __syncthreads();
     // buckets are zero on entry (K1 zeroes what it consumes): add the non-zero
@@ -351,8 +364,12 @@ hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64
         hipLaunchKernelGGL(k2x_partition, dim3(g.nblk), dim3(kHT), sizeof(uint32_t) * 2 * g.nbins, st, bnode, bts, B,
                            N, cut, g, C, O, region);
     const size_t lds = sizeof(uint32_t) * ((size_t)cut.n_win * ((size_t)1 << g.bb) + 2 * (size_t)g.nblk + 1);
+    static const int ysplits = [] {
+        const char* e = getenv("CRANE_K2Y_SPLITS");
+        return e && atoi(e) > 0 ? atoi(e) : kYSplits;
+    }();
     if (which & 2)
-        hipLaunchKernelGGL(k2y_bin_hist, dim3(g.nbins, kYSplits), dim3(kHT), lds, st, region, C, O, g, cut.n_win, N,
+        hipLaunchKernelGGL(k2y_bin_hist, dim3(g.nbins, ysplits), dim3(kHT), lds, st, region, C, O, g, cut.n_win, N,
                            buckets);
     return hipGetLastError();
 }

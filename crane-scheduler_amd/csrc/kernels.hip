@@ -215,12 +215,13 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     if (STEP) {
         batch_range_reduce<kK1Threads>(pmn, pmx, smn, smx, tmin, tmax);
         if (n < N) step_count<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, ssh, so);
-        step_reserve<kK1Threads>(so, ssh, step.st);  // (its barriers also order lrec)
-        // stepped nodes (a few %) rebuild their record from the LDS copy of the NodeRec
+        step_publish<kK1Threads>(so, ssh, step.st);  // (its barrier also orders lrec)
+        // stepped nodes (a few %) build their record from the LDS copy of the NodeRec
         if (n < N && (so.slot0 >= 0 || so.slot1 >= 0))
-            step_emit<PD, PR>(lrec[threadIdx.x], n, tmin, tmax, step.wsum, step.noprio, ssh, so, step.st);
+            step_emit<PD, PR>(lrec[threadIdx.x], n, tmin, tmax, step.wsum, step.noprio, so, step.st);
+    } else {
+        __syncthreads();
     }
-    __syncthreads();
     const int64_t nvalid = min((int64_t)kK1Threads, N - first);
     const int64_t nvec = nvalid * (int64_t)sizeof(Rec) / 16;
     const uint4* src = reinterpret_cast<const uint4*>(smem);
@@ -407,11 +408,15 @@ __global__ __launch_bounds__(kK3Threads) void k3_eval(const NodeRec<PD, PR>* __r
 }
 
 // ---------------------------------------------------------------- launchers
+int k1_threads() {
+    const char* e = getenv("CRANE_K1_THREADS");
+    return e && atoi(e) == 256 ? 256 : 128;
+}
+
 template <int PD, int PR>
 static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t st) {
     if (a.N <= 0) return hipSuccess;
-    const char* e = getenv("CRANE_K1_THREADS");
-    const int T = e && atoi(e) == 256 ? 256 : 128;
+    const int T = k1_threads();
     const unsigned grid = (unsigned)((a.N + T - 1) / T);
     const size_t lds = sizeof(NodeRec<PD, PR>) * T;
     const K1Step sa = step ? *step : K1Step{};

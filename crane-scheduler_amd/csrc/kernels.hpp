@@ -55,9 +55,9 @@ int64_t merge_bsum_len(int64_t N, int vlo);
 hipError_t launch_merge_stream(const int64_t* base, const uint8_t* leaf, const uint32_t* cnt, int64_t N,
                                const MergeArgs& a, int T, int vlo, int64_t cap, unsigned long long* bs,
                                int64_t* stream, hipStream_t st);
-// scratch: apos [Pd], tk [P], gi [nI]
+// scratch: apos [Pd], q [nI], gi [nI + 1]
 hipError_t launch_merge_assign(const int64_t* Fs, int64_t nF, const int64_t* Is, int64_t nI, const uint8_t* flags,
-                               int64_t P, int64_t Pd, int32_t* apos, int32_t* tk, int64_t* gi, int64_t* chosen,
+                               int64_t P, int64_t Pd, int32_t* apos, int32_t* q, int64_t* gi, int64_t* chosen,
                                hipStream_t st);
 
 // Bin-partitioned K2 (hotcount.hip)
@@ -106,26 +106,28 @@ struct alignas(16) VRec {  // 16-byte multiple: K3s stages records with 16-byte 
     int32_t key[NB + 1];
     int32_t cnt;
 };
-// The stepped lists are split into kStepSub sub-lists (workgroup b of the
-// producing kernel appends to sub-list b % kStepSub) so that no counter takes
-// more than a few dozen global atomics.  Header (int32) per sub-list:
-// [flat max kind 0, flat max kind 1, Step1 count kind 0, VRec count kind 0,
-//  Step1 count kind 1, VRec count kind 1, -, -].  K3p resets it.
-constexpr int kStepSub = 64;
-constexpr int kHdrFlat = 0, kHdrN1 = 2, kHdrStride = 8, kHdrLen = kStepSub * kHdrStride;
+// Step tables, one region per producer workgroup b (K1: bs = 128 nodes, K3a:
+// 256): its flat-key maxima flat[b][kind], its record counts cnt[b][L]
+// (L = 2 * kind + 0: Step1, 1: VRec) and its records at b * bs + slot of each
+// list.  Producers need no global atomics; K3s scans the counts of the
+// producer blocks it covers.
 struct StepTables {
-    int32_t* hdr;    // [kStepSub][kHdrStride]
-    Step1* single;   // [2][kStepSub][cap] per pod kind and sub-list (order is irrelevant: K3s takes a max)
-    void* multi;     // [2][kStepSub][cap] VRec<NB>
-    int64_t cap;     // records per sub-list: >= the nodes of the workgroups that map to it
-    int64_t npad;    // kStepSub * cap, per kind
+    int32_t* cnt;    // [nblk][4]
+    int32_t* flat;   // [nblk][2], -1 = no flat feasible node
+    Step1* single;   // [2][npad] per pod kind
+    void* multi;     // [2][npad] VRec<NB>
+    int64_t npad;    // per-kind stride >= nblk * bs
+    int32_t bs;      // nodes per producer workgroup
+    int32_t nblk;    // producer workgroups
 };
 struct StepGeometry {
-    int64_t nseg, npad, cap, ntiles, ngroups;
-    int32_t R;  // K3s workgroups per 64-pod group
+    int64_t nseg, npad, ntiles, ngroups;
+    int32_t R;  // K3s workgroups per 256-pod group (R is raised until each covers <= kK3sMaxBlk producer blocks)
 };
+constexpr int kK3sMaxBlk = 1024;
 size_t step_vrec_bytes(int shape);
-StepGeometry step_geometry(int64_t P, int64_t N);
+StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk);
+int k1_threads();  // K1 workgroup size (128, or 256 with CRANE_K1_THREADS=256)
 // K3p: perm, pnow [ntiles * 1024], tile_mm [2 * ntiles]; initialises keys[0..P) to -1 and the step header
 hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys,
                             const StepTables& st, const StepGeometry& g, int32_t* perm, int64_t* pnow,

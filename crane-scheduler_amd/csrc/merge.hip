@@ -129,7 +129,8 @@ __global__ __launch_bounds__(kMT) void m2_bsum(const int64_t* __restrict__ base,
 // ---------------------------------------------------------------- M3 (one workgroup)
 // Exclusive scan in place.  Each thread owns a contiguous run of the array and
 // reads it in batches of 8 independent loads; one workgroup scan of the run sums.
-__device__ __forceinline__ unsigned long long wg_excl_scan_u64(unsigned long long v, unsigned long long* part) {
+__device__ __forceinline__ unsigned long long wg_excl_scan_u64(unsigned long long v, unsigned long long* part,
+                                                               unsigned long long* total = nullptr) {
     // 1024 threads: wave scans, then a scan of the 16 wave totals
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     unsigned long long x = v;
@@ -148,13 +149,17 @@ __device__ __forceinline__ unsigned long long wg_excl_scan_u64(unsigned long lon
             if ((int)threadIdx.x >= o) u += y;
         }
         if (threadIdx.x < kM5T / 64) part[kM5T / 64 + threadIdx.x] = u - t;
+        if (threadIdx.x == kM5T / 64 - 1) part[2 * (kM5T / 64)] = u;
     }
     __syncthreads();
-    return part[kM5T / 64 + w] + x - v;
+    if (total) *total = part[2 * (kM5T / 64)];
+    const unsigned long long r = part[kM5T / 64 + w] + x - v;
+    __syncthreads();  // part is reused by the next call
+    return r;
 }
 
 __global__ __launch_bounds__(kM5T) void m3_scan(unsigned long long* __restrict__ v, int64_t len) {
-    __shared__ unsigned long long part[2 * (kM5T / 64)];
+    __shared__ unsigned long long part[2 * (kM5T / 64) + 1];
     const int64_t per = (len + kM5T - 1) / kM5T;
     const int64_t lo = min(len, (int64_t)threadIdx.x * per), hi = min(len, lo + per);
     unsigned long long s = 0;
@@ -228,32 +233,31 @@ __global__ __launch_bounds__(kMT) void m4_place(const int64_t* __restrict__ base
 }
 
 // ---------------------------------------------------------------- M5
-// M5a: positions a[m] of the DaemonSet pods (pod order); zero the I-taker marks.
-// One workgroup; each thread owns a contiguous run of pods (batched loads).
+// M5a: positions a[m] of the DaemonSet pods (pod order).  One workgroup: the
+// flags go to LDS with coalesced loads (in tiles of kM5Tile pods), then each
+// thread takes a contiguous run of the tile, one workgroup scan per tile.
+constexpr int kM5Tile = 96 * 1024;
+
 __global__ __launch_bounds__(kM5T) void m5a_compact(const uint8_t* __restrict__ flags, int64_t P,
-                                                    int32_t* __restrict__ apos, int32_t* __restrict__ tk) {
-    __shared__ unsigned long long part[2 * (kM5T / 64)];
-    const int64_t per = ((P + kM5T - 1) / kM5T + 7) & ~7LL;
-    const int64_t lo = min(P, (int64_t)threadIdx.x * per), hi = min(P, lo + per);
-    unsigned long long c = 0;
-    for (int64_t i0 = lo; i0 < hi; i0 += 8) {
-        uint8_t f[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) f[u] = i0 + u < hi ? flags[i0 + u] : 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) c += f[u] & 1u;
-    }
-    int32_t run = (int32_t)wg_excl_scan_u64(c, part);
-    for (int64_t i0 = lo; i0 < hi; i0 += 8) {
-        uint8_t f[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) f[u] = i0 + u < hi ? flags[i0 + u] : 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (i0 + u < hi) {
-                tk[i0 + u] = 0;
-                if (f[u] & 1u) apos[run++] = (int32_t)(i0 + u);
-            }
+                                                    int32_t* __restrict__ apos) {
+    __shared__ unsigned long long part[2 * (kM5T / 64) + 1];
+    __shared__ uint8_t lf[kM5Tile];
+    int64_t run = 0;
+    for (int64_t t0 = 0; t0 < P; t0 += kM5Tile) {
+        const int32_t nt = (int32_t)min((int64_t)kM5Tile, P - t0);
+#pragma unroll 8
+        for (int32_t i = threadIdx.x; i < nt; i += kM5T) lf[i] = flags[t0 + i] & 1u;
+        __syncthreads();
+        const int32_t per = (nt + kM5T - 1) / kM5T;
+        const int32_t lo = min(nt, (int32_t)threadIdx.x * per), hi = min(nt, lo + per);
+        unsigned long long c = 0;
+        for (int32_t i = lo; i < hi; ++i) c += lf[i];
+        unsigned long long tot;
+        int64_t pos = run + (int64_t)wg_excl_scan_u64(c, part, &tot);
+        for (int32_t i = lo; i < hi; ++i)
+            if (lf[i]) apos[pos++] = (int32_t)(t0 + i);
+        run += (int64_t)tot;
+        __syncthreads();  // lf is rewritten by the next tile
     }
 }
 
@@ -281,13 +285,16 @@ __global__ __launch_bounds__(kMT) void m5b_thresholds(const int64_t* __restrict_
     gi[i] = l2 - i;
 }
 
-// M5c: m_i = i + prefix-max(g_i - i); mark tk[a_{m_i}] = i + 1 for m_i < Pd (one workgroup)
+// M5c: m_i = i + prefix-max(g_i - i), strictly increasing in i; the I-takers
+// are i = 0 .. K-1 (m_i < Pd), at pods q_i = a_{m_i}, increasing (one workgroup)
 __global__ __launch_bounds__(kM5T) void m5c_takers(const int64_t* __restrict__ gi, int64_t nI,
                                                    const int32_t* __restrict__ apos, int64_t Pd,
-                                                   int32_t* __restrict__ tk) {
+                                                   int32_t* __restrict__ q, int64_t* __restrict__ K) {
     __shared__ int64_t part[kM5T];
+    __shared__ unsigned long long kmax;
+    if (threadIdx.x == 0) kmax = 0;
     const int64_t per = (nI + kM5T - 1) / kM5T;
-    const int64_t lo = threadIdx.x * per, hi = min(nI, lo + per);
+    const int64_t lo = min(nI, (int64_t)threadIdx.x * per), hi = min(nI, lo + per);
     int64_t s = INT64_MIN;
     for (int64_t i = lo; i < hi; ++i) s = max(s, gi[i]);
     part[threadIdx.x] = s;
@@ -302,45 +309,34 @@ __global__ __launch_bounds__(kM5T) void m5c_takers(const int64_t* __restrict__ g
     for (int64_t i = lo; i < hi; ++i) {
         run = max(run, gi[i]);
         const int64_t m = i + run;
-        if (m < Pd) tk[apos[m]] = (int32_t)(i + 1);
-    }
-}
-
-// M5d: pod order scan of the I-taker marks -> chosen node per pod (one
-// workgroup; contiguous runs of pods per thread, batched loads)
-__global__ __launch_bounds__(kM5T) void m5d_assign(const int64_t* __restrict__ Fs, int64_t nF,
-                                                   const int64_t* __restrict__ Is, const int32_t* __restrict__ tk,
-                                                   int64_t P, int64_t* __restrict__ chosen) {
-    __shared__ unsigned long long part[2 * (kM5T / 64)];
-    const int64_t per = ((P + kM5T - 1) / kM5T + 7) & ~7LL;
-    const int64_t lo = min(P, (int64_t)threadIdx.x * per), hi = min(P, lo + per);
-    unsigned long long c = 0;
-    for (int64_t i0 = lo; i0 < hi; i0 += 8) {
-        int32_t t[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = i0 + u < hi ? tk[i0 + u] : 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) c += t[u] > 0;
-    }
-    int64_t run = (int64_t)wg_excl_scan_u64(c, part);  // I-takers before this run
-    for (int64_t i0 = lo; i0 < hi; i0 += 8) {
-        int32_t t[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = i0 + u < hi ? tk[i0 + u] : 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int64_t p = i0 + u;
-            if (p >= hi) continue;
-            int64_t key = -1;
-            if (t[u] > 0) {
-                key = Is[t[u] - 1];
-                ++run;
-            } else if (p - run < nF) {
-                key = Fs[p - run];
-            }
-            chosen[p] = key < 0 ? -1 : (int64_t)(0xFFFFFFFFull - ((uint64_t)key & 0xFFFFFFFFull));
+        if (m < Pd) {
+            q[i] = apos[m];
+            atomicMax(&kmax, (unsigned long long)(i + 1));
         }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) *K = (int64_t)kmax;
+}
+
+// M5d: chosen node per pod, all pods in parallel.  Pod p is I-taker i iff
+// q_i = p; otherwise it takes F[p - #(I-takers before p)].
+__global__ __launch_bounds__(kMT) void m5d_assign(const int64_t* __restrict__ Fs, int64_t nF,
+                                                  const int64_t* __restrict__ Is, const int32_t* __restrict__ q,
+                                                  const int64_t* __restrict__ Kp, int64_t P,
+                                                  int64_t* __restrict__ chosen) {
+    const int64_t p = (int64_t)blockIdx.x * kMT + threadIdx.x;
+    if (p >= P) return;
+    const int64_t K = *Kp;
+    int64_t lo = 0, hi = K;  // first i with q_i >= p
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (q[mid] < p) lo = mid + 1;
+        else hi = mid;
+    }
+    int64_t key = -1;
+    if (lo < K && q[lo] == p) key = Is[lo];
+    else if (p - lo < nF) key = Fs[p - lo];
+    chosen[p] = key < 0 ? -1 : (int64_t)(0xFFFFFFFFull - ((uint64_t)key & 0xFFFFFFFFull));
 }
 
 // no DaemonSet pods: pod p takes F[p]
@@ -378,18 +374,20 @@ hipError_t launch_merge_stream(const int64_t* base, const uint8_t* leaf, const u
 }
 
 hipError_t launch_merge_assign(const int64_t* Fs, int64_t nF, const int64_t* Is, int64_t nI, const uint8_t* flags,
-                               int64_t P, int64_t Pd, int32_t* apos, int32_t* tk, int64_t* gi, int64_t* chosen,
+                               int64_t P, int64_t Pd, int32_t* apos, int32_t* q, int64_t* gi, int64_t* chosen,
                                hipStream_t st) {
     if (P <= 0) return hipSuccess;
+    const unsigned pb = (unsigned)((P + kMT - 1) / kMT);
     if (Pd == 0 || nI == 0) {  // no DaemonSet pod can take an infeasible node: pod p takes F[p]
-        hipLaunchKernelGGL(m5z_direct, dim3((unsigned)((P + kMT - 1) / kMT)), dim3(kMT), 0, st, Fs, nF, P, chosen);
+        hipLaunchKernelGGL(m5z_direct, dim3(pb), dim3(kMT), 0, st, Fs, nF, P, chosen);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(m5a_compact, dim3(1), dim3(kM5T), 0, st, flags, P, apos, tk);
+    int64_t* K = gi + nI;  // scratch: gi [nI] then K
+    hipLaunchKernelGGL(m5a_compact, dim3(1), dim3(kM5T), 0, st, flags, P, apos);
     hipLaunchKernelGGL(m5b_thresholds, dim3((unsigned)((nI + kMT - 1) / kMT)), dim3(kMT), 0, st, Fs, nF, Is, nI,
                        apos, Pd, gi);
-    hipLaunchKernelGGL(m5c_takers, dim3(1), dim3(kM5T), 0, st, gi, nI, apos, Pd, tk);
-    hipLaunchKernelGGL(m5d_assign, dim3(1), dim3(kM5T), 0, st, Fs, nF, Is, tk, P, chosen);
+    hipLaunchKernelGGL(m5c_takers, dim3(1), dim3(kM5T), 0, st, gi, nI, apos, Pd, q, K);
+    hipLaunchKernelGGL(m5d_assign, dim3(pb), dim3(kMT), 0, st, Fs, nF, Is, q, K, P, chosen);
     return hipGetLastError();
 }
 

@@ -42,8 +42,7 @@ constexpr int kPodTile = 1024;
 __global__ __launch_bounds__(kPodTile) void k3p_pods(const int64_t* __restrict__ now,
                                                      const uint8_t* __restrict__ flags, int64_t P,
                                                      int32_t* __restrict__ perm, int64_t* __restrict__ pnow,
-                                                     int64_t* __restrict__ tile_mm, long long* __restrict__ keys,
-                                                     int32_t* __restrict__ hdr) {
+                                                     int64_t* __restrict__ tile_mm, long long* __restrict__ keys) {
     __shared__ int32_t cn[kPodTile / 64], cd[kPodTile / 64];
     __shared__ int64_t wmn[kPodTile / 64], wmx[kPodTile / 64];
     const int64_t t = blockIdx.x;
@@ -53,8 +52,6 @@ __global__ __launch_bounds__(kPodTile) void k3p_pods(const int64_t* __restrict__
     const int64_t tn = live ? now[p] : 0;
     if (live) keys[p] = -1;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (t == 0 && threadIdx.x < kHdrLen)  // step-table header: flat maxima -1, counts 0
-        hdr[threadIdx.x] = (threadIdx.x % kHdrStride) < kHdrN1 ? -1 : 0;
     const uint64_t mn_mask = __ballot(live && !ds), md_mask = __ballot(ds);
     const uint64_t lt = (1ull << lane) - 1ull;
     int64_t mn = live ? tn : INT64_MAX, mx = live ? tn : INT64_MIN;
@@ -113,8 +110,8 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
         r = rec[n];
         step_count<PD, PR>(r, n, tmin, tmax, wsum, noprio, sh, o);
     }
-    step_reserve<kStepSeg>(o, sh, st);
-    if (n < N && (o.slot0 >= 0 || o.slot1 >= 0)) step_emit<PD, PR>(r, n, tmin, tmax, wsum, noprio, sh, o, st);
+    step_publish<kStepSeg>(o, sh, st);
+    if (n < N && (o.slot0 >= 0 || o.slot1 >= 0)) step_emit<PD, PR>(r, n, tmin, tmax, wsum, noprio, o, st);
 }
 
 // ---------------------------------------------------------------- K3s
@@ -129,28 +126,31 @@ constexpr int kK3sThreads = kK3sWaves * 64;
 constexpr int kK3sS1 = 512;  // Step1 records staged per round and pod kind (8 KB)
 constexpr int kK3sVR = 32;   // VRec records staged per round and pod kind
 
-// global position in the [kStepSub][cap] layout of element i of the concatenated sub-lists
-__device__ __forceinline__ int64_t sub_pos(const int32_t* pre, int32_t i, int64_t cap) {
-    int lo = 0;
-#pragma unroll
-    for (int h = 32; h >= 1; h >>= 1)
-        if (pre[lo + h] <= i) lo += h;
-    return (int64_t)lo * cap + (i - pre[lo]);
+// position in the per-producer-block layout of element i of the concatenation
+// of blocks b0 + 0 .. m-1 (pre: exclusive prefix of their counts, pre[m] = total)
+__device__ __forceinline__ int64_t blk_pos(const int32_t* pre, int32_t m, int32_t i, int32_t b0, int32_t bs) {
+    int lo = 0, hi = m - 1;  // largest j with pre[j] <= i
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    return (int64_t)(b0 + lo) * bs + (i - pre[lo]);
 }
 
-// The four stepped lists: L = 2 * kind + (0: Step1, 1: VRec); header column kHdrN1 + L.
+// The four stepped lists: L = 2 * kind + (0: Step1, 1: VRec).
 template <int NB>
 __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int32_t* __restrict__ perm,
                                                         const int64_t* __restrict__ pnow, int64_t P,
                                                         int64_t node_offset, int32_t R,
                                                         long long* __restrict__ keys) {
-    static_assert(kStepSub == 64 && kK3sWaves == 4, "one wave scans each list's sub-list lengths");
+    static_assert(kK3sWaves == 4, "one wave scans each list's counts");
     static_assert(sizeof(VRec<NB>) % 16 == 0, "VRec must be a whole number of int4");
     constexpr int kVRI4 = (int)(sizeof(VRec<NB>) / 16);
     __shared__ int4 l1[2][kK3sS1];
     __shared__ VRec<NB> lv[2][kK3sVR];
-    __shared__ int32_t pre[4][kStepSub + 1];
-    __shared__ int32_t flat[2][kK3sWaves];
+    __shared__ int32_t pre[4][kK3sMaxBlk + 1];
+    __shared__ int32_t fl[2][kK3sWaves];
     __shared__ int64_t wr[2][2][kK3sWaves];  // per kind and wave: min, max pod time
     __shared__ int32_t nin[2], umax[2];      // staged in-range records, uniform maximum (per kind)
     const int64_t b = blockIdx.x;
@@ -162,22 +162,31 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     const bool live = slot < P;
     const int32_t praw = live ? perm[slot] : 0;
     const int64_t tnow = live ? pnow[slot] : 0;
-    // header: wave w scans list w's sub-list lengths; the flat maxima ride along
+    // producer blocks [b0, b0 + m) of this slice: their counts, scanned per list
+    // (wave w scans list w), and their flat maxima
+    const int32_t per = (st.nblk + R - 1) / R;
+    const int32_t b0 = min(st.nblk, r * per), m = min(st.nblk, b0 + per) - b0;
     {
-        const int32_t* h = st.hdr + lane * kHdrStride;
-        const int32_t c = h[kHdrN1 + w];
-        int32_t f = w < 2 ? h[kHdrFlat + w] : -1;
-        int32_t x = c;
+        int32_t carry = 0;
+        for (int32_t j0 = 0; j0 < m; j0 += 64) {
+            const int32_t j = j0 + lane;
+            const int32_t c = j < m ? st.cnt[(int64_t)(b0 + j) * 4 + w] : 0;
+            int32_t x = c;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(x, o);
-            if (lane >= o) x += y;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t y = __shfl_up(x, o);
+                if (lane >= o) x += y;
+            }
+            if (j < m) pre[w][j] = carry + x - c;
+            carry += __shfl(x, 63);
         }
+        if (lane == 0) pre[w][m] = carry;
+        int32_t f = -1;
+        if (w < 2)
+            for (int32_t j = lane; j < m; j += 64) f = max(f, st.flat[(int64_t)(b0 + j) * 2 + w]);
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) f = max(f, __shfl_xor(f, o));
-        pre[w][lane] = x - c;
-        if (lane == 63) pre[w][64] = x;
-        if (lane == 0) flat[0][w] = f;
+        if (lane == 0 && w < 2) fl[w][0] = f;
     }
     const bool ds = praw < 0;
     const int32_t pod = praw & 0x7FFFFFFF;
@@ -209,16 +218,14 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         tlo[T] = min(min(wr[T][0][0], wr[T][0][1]), min(wr[T][0][2], wr[T][0][3]));
         thi[T] = max(max(wr[T][1][0], wr[T][1][1]), max(wr[T][1][2], wr[T][1][3]));
     }
-    // the flat maxima enter once per pod (slice 0)
-    int32_t best_n = r == 0 ? flat[0][0] : -1, best_d = r == 0 ? flat[0][1] : -1;
+    // the flat maxima of this slice's producer blocks hold for every pod of the kind
+    int32_t best_n = fl[0][0], best_d = fl[1][0];
     // this workgroup's slice [lo, hi) of each list (lists of a kind without pods here: empty)
     int32_t lo[4], hi[4];
 #pragma unroll
     for (int L = 0; L < 4; ++L) {
-        const int32_t n = ((L < 2) ? bn : bd) ? pre[L][64] : 0;
-        const int32_t per = (n + R - 1) / R;
-        lo[L] = min(n, r * per);
-        hi[L] = min(n, lo[L] + per);
+        lo[L] = 0;
+        hi[L] = ((L < 2) ? bn : bd) ? pre[L][m] : 0;
     }
     int32_t um0 = -1, um1 = -1;  // this thread's share of the uniform maxima
     for (bool first = true;; first = false) {
@@ -251,8 +258,8 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
                 const int32_t g4 = f - t1, j = g4 / kVRI4, wd4 = g4 - j * kVRI4;
                 one[u] = f < t1;
                 kind[u] = T;
-                src[u] = one[u] ? g1 + sub_pos(pre[2 * T], lo1 + f, st.cap)
-                                : reinterpret_cast<const int4*>(gv + sub_pos(pre[2 * T + 1], lov + j, st.cap)) + wd4;
+                src[u] = one[u] ? g1 + blk_pos(pre[2 * T], m, lo1 + f, b0, st.bs)
+                                : reinterpret_cast<const int4*>(gv + blk_pos(pre[2 * T + 1], m, lov + j, b0, st.bs)) + wd4;
                 dst[u] = reinterpret_cast<int4*>(&lv[T][j]) + wd4;
             }
             int4 q[4];
@@ -340,19 +347,19 @@ size_t step_vrec_bytes(int shape) {
     }
 }
 
-StepGeometry step_geometry(int64_t P, int64_t N) {
+StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk) {
     StepGeometry g{};
     g.nseg = (N + kStepSeg - 1) / kStepSeg;
-    g.npad = g.nseg * kStepSeg;
-    // sub-list capacity: workgroups b = s, s + kStepSub, ... of K3a (256 nodes) or K1 (128)
-    g.cap = (N + kStepSub * 256 - 1) / (kStepSub * 256) * 256;
-    g.npad = g.cap * kStepSub;
+    g.npad = g.nseg * kStepSeg;  // >= nblk * bs for bs = 128 or 256
     g.ntiles = (P + kPodTile - 1) / kPodTile;
     g.ngroups = (P + kK3sThreads - 1) / kK3sThreads;
-    // R workgroups per 256-pod group: ~512 workgroups in all, at most 64 per group
+    // R workgroups per 256-pod group: ~512 workgroups in all, at most 64 per group,
+    // and enough that each covers at most kK3sMaxBlk producer blocks
     const char* e = getenv("CRANE_K3S_BLOCKS");
     const int64_t target = e && atoi(e) > 0 ? atoi(e) : 512;
-    g.R = (int32_t)std::min<int64_t>(64, std::max<int64_t>(1, target / std::max<int64_t>(g.ngroups, 1)));
+    int64_t R = std::min<int64_t>(64, std::max<int64_t>(1, target / std::max<int64_t>(g.ngroups, 1)));
+    R = std::max<int64_t>(R, (nblk + kK3sMaxBlk - 1) / kK3sMaxBlk);
+    g.R = (int32_t)R;
     return g;
 }
 
@@ -369,7 +376,7 @@ hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P,
                             int64_t* tile_mm, hipStream_t s) {
     if (P <= 0) return hipSuccess;
     hipLaunchKernelGGL(k3p_pods, dim3((unsigned)g.ntiles), dim3(kPodTile), 0, s, now, flags, P, perm, pnow, tile_mm,
-                       keys, st.hdr);
+                       keys);
     return hipGetLastError();
 }
 

@@ -103,7 +103,6 @@ struct StepSlots {
 // Workgroup-shared counters of the step epilogue.
 struct StepShared {
     int32_t lc[2][2];   // records per kind: [Step1, VRec]
-    int32_t gb[2][2];   // reserved list offsets
     int32_t fm[2][16];  // per-wave flat maxima (<= 1024 threads)
 };
 
@@ -149,10 +148,10 @@ __device__ __forceinline__ void step_count(const NodeRec<PD, PR>& r, int64_t n, 
     kind(std::integral_constant<int, 1>{}, o.flat1, o.slot1, o.multi1);
 }
 
-// Phase 2: write node n's record(s) at the reserved positions (after step_reserve).
+// Phase 2: write node n's record(s) into the workgroup's region.
 template <int PD, int PR>
 __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
-                                          double wsum, int32_t noprio, const StepShared& sh, const StepSlots& o,
+                                          double wsum, int32_t noprio, const StepSlots& o,
                                           const StepTables& st) {
     constexpr int NB = PR + 2;
     auto kind = [&](auto Tc, int32_t slot, bool multi) {
@@ -168,7 +167,7 @@ __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, i
             v.bp = mn;
             v.k0 = k0;
             v.k1 = key_of<PD, PR>(T, mn, score_at<PD, PR>(mn, r, wsum, noprio), r, n);
-            st.single[(int64_t)T * st.npad + sh.gb[T][0] + slot] = v;
+            st.single[(int64_t)T * st.npad + (int64_t)blockIdx.x * st.bs + slot] = v;
         } else {  // rare: sort the expiries (equal ones give equal keys)
 #pragma unroll
             for (int i = 0; i < NB; ++i)  // odd-even transposition sort (static indices)
@@ -186,18 +185,18 @@ __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, i
                 v.bp[j] = c[j];  // INT64_MAX past cnt: never selected
                 v.key[j + 1] = j < cnt ? key_of<PD, PR>(T, c[j], score_at<PD, PR>(c[j], r, wsum, noprio), r, n) : -1;
             }
-            reinterpret_cast<VRec<NB>*>(st.multi)[(int64_t)T * st.npad + sh.gb[T][1] + slot] = v;
+            reinterpret_cast<VRec<NB>*>(st.multi)[(int64_t)T * st.npad + (int64_t)blockIdx.x * st.bs + slot] = v;
         }
     };
     kind(std::integral_constant<int, 0>{}, o.slot0, o.multi0);
     kind(std::integral_constant<int, 1>{}, o.slot1, o.multi1);
 }
 
-// Workgroup epilogue part 1: flat max -> one atomicMax per kind, list spans
-// reserved with one atomicAdd per (kind, list).  Every thread calls it
-// (contains barriers); sh.lc must have been zeroed before step_count.
+// Workgroup epilogue: the workgroup's flat-key maxima and record counts go to
+// its own slots of the step tables (plain stores, no global atomics).  Every
+// thread calls it (barrier); sh.lc must have been zeroed before step_count.
 template <int BS>
-__device__ __forceinline__ void step_reserve(const StepSlots& o, StepShared& sh, const StepTables& st) {
+__device__ __forceinline__ void step_publish(const StepSlots& o, StepShared& sh, const StepTables& st) {
     auto wmax = [&](int T, int32_t m) {
 #pragma unroll
         for (int s = 32; s >= 1; s >>= 1) m = max(m, __shfl_xor(m, s));
@@ -206,20 +205,16 @@ __device__ __forceinline__ void step_reserve(const StepSlots& o, StepShared& sh,
     wmax(0, o.flat0);
     wmax(1, o.flat1);
     __syncthreads();
-    int32_t* hdr = st.hdr + (blockIdx.x % kStepSub) * kHdrStride;  // this workgroup's sub-list
     if (threadIdx.x < 2) {
         const int T = threadIdx.x;
         int32_t m = sh.fm[T][0];
 #pragma unroll
         for (int i = 1; i < BS / 64; ++i) m = max(m, sh.fm[T][i]);
-        if (m >= 0) atomicMax(&hdr[kHdrFlat + T], m);
+        st.flat[(int64_t)blockIdx.x * 2 + T] = m;
     } else if (threadIdx.x < 6) {
-        const int T = (threadIdx.x - 2) >> 1, k = (threadIdx.x - 2) & 1;
-        // offset inside the sub-list; the sub-list starts at (blockIdx % kStepSub) * cap
-        sh.gb[T][k] = (sh.lc[T][k] ? atomicAdd(&hdr[kHdrN1 + 2 * T + k], sh.lc[T][k]) : 0) +
-                      (int32_t)((blockIdx.x % kStepSub) * st.cap);
+        const int L = threadIdx.x - 2;
+        st.cnt[(int64_t)blockIdx.x * 4 + L] = sh.lc[L >> 1][L & 1];
     }
-    __syncthreads();
 }
 
 }  // namespace crane
