@@ -159,28 +159,40 @@ __device__ __forceinline__ unsigned long long wg_excl_scan_u64(unsigned long lon
 }
 
 __global__ __launch_bounds__(kM5T) void m3_scan(unsigned long long* __restrict__ v, int64_t len) {
+    // tiles of 8 x 1024 values: coalesced loads into LDS, each thread scans 8
+    // consecutive values, one workgroup scan per tile, coalesced stores
+    constexpr int kTile = 8 * kM5T;
     __shared__ unsigned long long part[2 * (kM5T / 64) + 1];
-    const int64_t per = (len + kM5T - 1) / kM5T;
-    const int64_t lo = min(len, (int64_t)threadIdx.x * per), hi = min(len, lo + per);
-    unsigned long long s = 0;
-    for (int64_t i0 = lo; i0 < hi; i0 += 8) {
-        unsigned long long x[8];
+    __shared__ unsigned long long lv[kTile];
+    unsigned long long run = 0;
+    for (int64_t t0 = 0; t0 < len; t0 += kTile) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = i0 + u < hi ? v[i0 + u] : 0ull;
+        for (int u = 0; u < 8; ++u) {
+            const int64_t i = t0 + u * kM5T + threadIdx.x;
+            lv[u * kM5T + threadIdx.x] = i < len ? v[i] : 0ull;
+        }
+        __syncthreads();
+        unsigned long long x[8], c = 0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s += x[u];
-    }
-    unsigned long long run = wg_excl_scan_u64(s, part);
-    for (int64_t i0 = lo; i0 < hi; i0 += 8) {
-        unsigned long long x[8];
+        for (int u = 0; u < 8; ++u) {
+            x[u] = lv[threadIdx.x * 8 + u];
+            c += x[u];
+        }
+        unsigned long long tot;
+        unsigned long long e = run + wg_excl_scan_u64(c, part, &tot);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = i0 + u < hi ? v[i0 + u] : 0ull;
+        for (int u = 0; u < 8; ++u) {
+            lv[threadIdx.x * 8 + u] = e;
+            e += x[u];
+        }
+        __syncthreads();
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (i0 + u < hi) {
-                v[i0 + u] = run;
-                run += x[u];
-            }
+        for (int u = 0; u < 8; ++u) {
+            const int64_t i = t0 + u * kM5T + threadIdx.x;
+            if (i < len) v[i] = lv[u * kM5T + threadIdx.x];
+        }
+        run += tot;
+        __syncthreads();
     }
 }
 
