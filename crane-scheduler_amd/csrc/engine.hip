@@ -410,10 +410,14 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         HIPTRY(h, h->k2_cnt.reserve((size_t)g.nbins * (size_t)g.nchunks));
         HIPTRY(h, h->k2_tot.reserve((size_t)g.nbins));
         HIPTRY(h, h->k2_sorted.reserve((size_t)h->B));
+        HIPTRY(h, prof_begin(h, st));
         HIPTRY(h, launch_hot_count_binned(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, g, h->k2_cnt.p,
                                           h->k2_tot.p, h->k2_sorted.p, st));
+        HIPTRY(h, prof_mark(h, st, "k2_binned (4 kernels)"));
     } else {
+        HIPTRY(h, prof_begin(h, st));
         HIPTRY(h, launch_hot_count(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, st));
+        HIPTRY(h, prof_mark(h, st, "k2_hot_count (hash)"));
     }
     h->buckets_zero = false;
     h->counts_pending = true;

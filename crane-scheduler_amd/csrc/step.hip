@@ -115,14 +115,18 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
 }
 
 // ---------------------------------------------------------------- K3s
-// Workgroup = 4 waves x 64 pods (256 consecutive pods of K3p's partitioned
-// order); the R workgroups of a pod group split each stepped list.  A
-// workgroup stages its slice of the list in LDS with coalesced loads (one
-// memory latency for the slice), then every wave walks the slice with
-// broadcast LDS reads: per (pod, one-step node) a 64-bit compare, a select and
-// a max.  One 64-bit atomicMax per pod per workgroup merges the slices.
+// Workgroup = 4 waves x 64 lanes x 4 pods per lane (one 1024-pod tile of
+// K3p's partitioned order: lane l of wave w holds pods u * 256 + w * 64 + l);
+// the R workgroups of a tile split the producer blocks.  A workgroup reads its
+// blocks' records with coalesced loads: a one-step record whose step lies
+// outside the tile's time range gives the same key to all of the tile's pods
+// of its kind (one max), the others are staged in LDS and every lane walks
+// them with broadcast LDS reads (per pod: 64-bit compare, select, max).  One
+// 64-bit atomicMax per pod per workgroup merges the slices.
 constexpr int kK3sWaves = 4;
 constexpr int kK3sThreads = kK3sWaves * 64;
+constexpr int kK3sPPL = 4;                          // pods per lane
+constexpr int kK3sPods = kK3sThreads * kK3sPPL;     // pods per workgroup (= kPodTile)
 constexpr int kK3sS1 = 512;  // Step1 records staged per round and pod kind (8 KB)
 constexpr int kK3sVR = 32;   // VRec records staged per round and pod kind
 
@@ -157,11 +161,19 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     const int32_t r = (int32_t)(b % R);
     const int64_t grp = b / R;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // K3p wrote the pods in partitioned order: two independent coalesced loads
-    const int64_t slot = grp * kK3sThreads + threadIdx.x;
-    const bool live = slot < P;
-    const int32_t praw = live ? perm[slot] : 0;
-    const int64_t tnow = live ? pnow[slot] : 0;
+    // K3p wrote the pods in partitioned order: coalesced loads
+    bool live[kK3sPPL], ds[kK3sPPL];
+    int32_t pod[kK3sPPL];
+    int64_t tnow[kK3sPPL];
+#pragma unroll
+    for (int u = 0; u < kK3sPPL; ++u) {
+        const int64_t slot = grp * kK3sPods + u * kK3sThreads + threadIdx.x;
+        live[u] = slot < P;
+        const int32_t praw = live[u] ? perm[slot] : 0;
+        tnow[u] = live[u] ? pnow[slot] : 0;
+        ds[u] = praw < 0;
+        pod[u] = praw & 0x7FFFFFFF;
+    }
     // producer blocks [b0, b0 + m) of this slice: their counts, scanned per list
     // (wave w scans list w), and their flat maxima
     const int32_t per = (st.nblk + R - 1) / R;
@@ -188,15 +200,24 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         for (int o = 32; o >= 1; o >>= 1) f = max(f, __shfl_xor(f, o));
         if (lane == 0 && w < 2) fl[w][0] = f;
     }
-    const bool ds = praw < 0;
-    const int32_t pod = praw & 0x7FFFFFFF;
-    const bool wn = __ballot(live && !ds) != 0, wd = __ballot(ds) != 0;
+    bool ln = false, ld = false;  // this lane has pods of kind 0 / 1
+#pragma unroll
+    for (int u = 0; u < kK3sPPL; ++u) {
+        ln |= live[u] && !ds[u];
+        ld |= ds[u];
+    }
+    const bool wn = __ballot(ln) != 0, wd = __ballot(ld) != 0;
     // the workgroup's pod time range per kind: a record whose step lies outside it
     // gives the same key to every pod of that kind here (one max, no per-lane work)
 #pragma unroll
     for (int T = 0; T < 2; ++T) {
-        const bool mine = live && (T ? ds : !ds);
-        int64_t mn = mine ? tnow : INT64_MAX, mx = mine ? tnow : INT64_MIN;
+        int64_t mn = INT64_MAX, mx = INT64_MIN;
+#pragma unroll
+        for (int u = 0; u < kK3sPPL; ++u) {
+            const bool mine = live[u] && (T ? ds[u] : !ds[u]);
+            mn = mine ? min(mn, tnow[u]) : mn;
+            mx = mine ? max(mx, tnow[u]) : mx;
+        }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
             mn = min(mn, (int64_t)__shfl_xor((long long)mn, o));
@@ -211,7 +232,7 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         nin[threadIdx.x] = 0;
         umax[threadIdx.x] = -1;
     }
-    const bool bn = __syncthreads_or(live && !ds), bd = __syncthreads_or(ds);  // (also orders the LDS above)
+    const bool bn = __syncthreads_or(ln), bd = __syncthreads_or(ld);  // (also orders the LDS above)
     int64_t tlo[2], thi[2];
 #pragma unroll
     for (int T = 0; T < 2; ++T) {
@@ -219,7 +240,12 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         thi[T] = max(max(wr[T][1][0], wr[T][1][1]), max(wr[T][1][2], wr[T][1][3]));
     }
     // the flat maxima of this slice's producer blocks hold for every pod of the kind
-    int32_t best_n = fl[0][0], best_d = fl[1][0];
+    int32_t best_n[kK3sPPL], best_d[kK3sPPL];
+#pragma unroll
+    for (int u = 0; u < kK3sPPL; ++u) {
+        best_n[u] = fl[0][0];
+        best_d[u] = fl[1][0];
+    }
     // this workgroup's slice [lo, hi) of each list (lists of a kind without pods here: empty)
     int32_t lo[4], hi[4];
 #pragma unroll
@@ -285,37 +311,39 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
             }
         }
         __syncthreads();
-#pragma unroll
-        for (int T = 0; T < 2; ++T) {
-            if (!(T ? wd : wn)) continue;
-            int32_t best = T ? best_d : best_n;
+        auto walk = [&](int T, int32_t* best) {
             const int32_t n1 = nin[T];
             int32_t i = 0;
-            for (; i + 8 <= n1; i += 8) {
-                int4 q[8];
+            for (; i + 4 <= n1; i += 4) {
+                int4 q[4];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) q[u] = l1[T][i + u];  // broadcast LDS reads
+                for (int v = 0; v < 4; ++v) q[v] = l1[T][i + v];  // broadcast LDS reads
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q[u].y << 32) | (uint32_t)q[u].x);
-                    best = max(best, tnow >= bp ? q[u].w : q[u].z);
+                for (int v = 0; v < 4; ++v) {
+                    const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q[v].y << 32) | (uint32_t)q[v].x);
+#pragma unroll
+                    for (int u = 0; u < kK3sPPL; ++u) best[u] = max(best[u], tnow[u] >= bp ? q[v].w : q[v].z);
                 }
             }
             for (; i < n1; ++i) {
                 const int4 q = l1[T][i];
                 const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q.y << 32) | (uint32_t)q.x);
-                best = max(best, tnow >= bp ? q.w : q.z);
+#pragma unroll
+                for (int u = 0; u < kK3sPPL; ++u) best[u] = max(best[u], tnow[u] >= bp ? q.w : q.z);
             }
             for (int32_t j = 0; j < take[2 * T + 1]; ++j) {
                 const VRec<NB>& v = lv[T][j];
-                int32_t k = v.key[0];
 #pragma unroll
-                for (int s = 0; s < NB; ++s) k = tnow >= v.bp[s] ? v.key[s + 1] : k;
-                best = max(best, k);
+                for (int u = 0; u < kK3sPPL; ++u) {
+                    int32_t k = v.key[0];
+#pragma unroll
+                    for (int s = 0; s < NB; ++s) k = tnow[u] >= v.bp[s] ? v.key[s + 1] : k;
+                    best[u] = max(best[u], k);
+                }
             }
-            if (T) best_d = best;
-            else best_n = best;
-        }
+        };
+        if (wn) walk(0, best_n);
+        if (wd) walk(1, best_d);
 #pragma unroll
         for (int L = 0; L < 4; ++L) lo[L] += take[L];
     }
@@ -330,11 +358,15 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         if (um1 >= 0) atomicMax(&umax[1], um1);
     }
     __syncthreads();
-    const int32_t best = ds ? max(best_d, umax[1]) : max(best_n, umax[0]);
-    if (live && best >= 0) {
-        const int64_t sc = best >> 24;
-        const int64_t n = 0xFFFFFF - (best & 0xFFFFFF);
-        atomicMax(&keys[pod], (long long)((sc << 32) | (int64_t)(0xFFFFFFFFull - (uint64_t)(node_offset + n))));
+#pragma unroll
+    for (int u = 0; u < kK3sPPL; ++u) {
+        const int32_t best = ds[u] ? max(best_d[u], umax[1]) : max(best_n[u], umax[0]);
+        if (live[u] && best >= 0) {
+            const int64_t sc = best >> 24;
+            const int64_t n = 0xFFFFFF - (best & 0xFFFFFF);
+            atomicMax(&keys[pod[u]],
+                      (long long)((sc << 32) | (int64_t)(0xFFFFFFFFull - (uint64_t)(node_offset + n))));
+        }
     }
 }
 
@@ -352,11 +384,11 @@ StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk) {
     g.nseg = (N + kStepSeg - 1) / kStepSeg;
     g.npad = g.nseg * kStepSeg;  // >= nblk * bs for bs = 128 or 256
     g.ntiles = (P + kPodTile - 1) / kPodTile;
-    g.ngroups = (P + kK3sThreads - 1) / kK3sThreads;
-    // R workgroups per 256-pod group: ~512 workgroups in all, at most 64 per group,
+    g.ngroups = (P + kK3sPods - 1) / kK3sPods;
+    // R workgroups per 1024-pod group: ~512 workgroups in all, at most 64 per group,
     // and enough that each covers at most kK3sMaxBlk producer blocks
     const char* e = getenv("CRANE_K3S_BLOCKS");
-    const int64_t target = e && atoi(e) > 0 ? atoi(e) : 512;
+    const int64_t target = e && atoi(e) > 0 ? atoi(e) : 1024;
     int64_t R = std::min<int64_t>(64, std::max<int64_t>(1, target / std::max<int64_t>(g.ngroups, 1)));
     R = std::max<int64_t>(R, (nblk + kK3sMaxBlk - 1) / kK3sMaxBlk);
     g.R = (int32_t)R;

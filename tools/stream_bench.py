@@ -1,13 +1,16 @@
-"""HBM roofline of the streaming kernels at large N, cold cache.
+"""HBM roofline of the streaming kernels of one scheduling step at large N, cold cache.
 
-    python tools/stream_bench.py [--nodes 4000000] [--bindings 16000000] [--reps 5]
+    python tools/stream_bench.py [--nodes 4000000] [--bindings 16000000] [--pods 10000] [--reps 5]
 
-K1 (node pass) and K2 (hot-value counts) are timed separately with HIP events;
-between reps a 1 GiB scratch buffer is written so the 256 MiB Infinity Cache
-holds none of the inputs (MI355X_MICROARCH.md, Infinity Cache).
-Algorithmic bytes (DESIGN.md §4):
-  K1: 16*M (val+ts SoA) + 8*W (buckets read + zeroed) + sizeof(NodeRec) per node
-  K2: 12 per binding (int32 node + int64 ts) + 4*W per node (bucket counts)
+One step = K2 refresh (k2x_partition + k2y_bin_hist, or the binned / hash
+variants) then a keys-only eval (k3p_pods, k1_node_pass+k3a_steps, k3s_eval).
+Stage times come from the engine's own HIP events (crane_dyn_set_profiling).
+Before the refresh and before the eval a 1 GiB scratch buffer is written, so
+the 256 MiB Infinity Cache holds none of the inputs (MI355X_MICROARCH.md).
+Algorithmic bytes (DESIGN.md section 4):
+  k2x_partition           : 12 per binding read + 4 per in-window binding written
+  k2y_bin_hist            : 4 per in-window binding read + 4*W per node (window counts)
+  k1_node_pass(+k3a_steps): 16*M (val+ts SoA) + 8*W (buckets read + zeroed) + sizeof(NodeRec) + 8 (hot value) per node
 """
 import argparse
 import json
@@ -26,14 +29,16 @@ from crane_dyn import synth  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--nodes", type=int, default=4_000_000)
 ap.add_argument("--bindings", type=int, default=16_000_000)
+ap.add_argument("--pods", type=int, default=10_000)
 ap.add_argument("--reps", type=int, default=5)
-ap.add_argument("--k1-threads", default="128,256")
-ap.add_argument("--k2", default="binned,hash")
+ap.add_argument("--k2", default="part,binned,hash")
 args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
 spec = cd.default_policy_spec()
-c = synth.make_cluster(spec, args.nodes, 1, n_bindings=args.bindings, seed=7)
+N, B, P = args.nodes, args.bindings, args.pods
+c = synth.make_cluster(spec, N, P, n_bindings=B, seed=7)
+c.now, c.ds = synth.make_pods(P, seed=8)
 eng = cd.Engine(cd.Policy(spec), 0)
 val, ts, _ = c.rows(eng.metric_names)
 eng.upload_nodes(val, ts, c.hv, c.hv_ts)
@@ -41,43 +46,53 @@ eng.upload_bindings(c.b_node, c.b_ts)
 st = torch.cuda.Stream(dev)
 torch.cuda.set_stream(st)
 sh = st.cuda_stream
+d_now = torch.from_numpy(c.now).to(dev)
+d_flags = torch.from_numpy(c.ds).to(dev)
+d_keys = torch.empty(P, dtype=torch.int64, device=dev)
 scratch = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
-M, W, N, B = len(eng.metric_names), len(spec["hotValue"]), args.nodes, args.bindings
-REC = 160
-k1_bytes = N * (16 * M + 8 * W + REC)
-k2_bytes = B * 12 + 4 * W * N
-t1, t2 = [], []
-t1v = {v: [] for v in args.k1_threads.split(",")}
-t2v = {v: [] for v in args.k2.split(",")}
-for r in range(args.reps + 1):
-    for v, k2 in zip(list(t1v) * len(t2v), sorted(list(t2v) * len(t1v))):
-        os.environ["CRANE_K1_THREADS"] = v
-        os.environ["CRANE_K2"] = k2
+M, W = len(eng.metric_names), len(spec["hotValue"])
+REC = 160  # sizeof(NodeRec<4, 6>)
+now = int(synth.NOW0_NS)
+max_tr = max(tr for tr, _ in spec["hotValue"]) // 10**9
+b_in = int((c.b_ts > now // 10**9 - max_tr).sum())
+alg = {
+    "k2_binned (4 kernels)": B * 12 + 4 * W * N,
+    "k2_hot_count (hash)": B * 12 + 4 * W * N,
+    "k2x_partition": B * 12 + b_in * 4,
+    "k2y_bin_hist": b_in * 4 + 4 * W * N,
+    "k1_node_pass+k3a_steps": N * (16 * M + 8 * W + REC + 8),
+}
+res = {}
+keys_ref = None
+for k2 in args.k2.split(","):
+    os.environ["CRANE_K2"] = k2
+    acc = {}
+    for r in range(args.reps + 1):
         scratch.fill_(r & 0xFF)
-        a, b, d = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-        a.record(st)
-        eng.refresh_hot_values_async(synth.NOW0_NS, synth.NOW0_NS, sh)  # K2 (+ bucket memset on the first rep)
-        b.record(st)
+        eng.set_profiling(True)
+        eng.refresh_hot_values_async(now, now, sh)
+        t_k2 = eng.stage_times()
         scratch.fill_((r + 7) & 0xFF)
-        c0 = torch.cuda.Event(enable_timing=True)
-        c0.record(st)
-        eng.node_pass_async(sh)  # K1
-        d.record(st)
-        d.synchronize()
+        eng.set_profiling(True)
+        eng.eval_keys_async(d_now, d_flags, d_keys, sh)
+        t_ev = eng.stage_times()
         if r:  # rep 0 is warmup
-            t2v[k2].append(a.elapsed_time(b))
-            t1v[v].append(c0.elapsed_time(d))
-best = min(t1v, key=lambda v: np.median(t1v[v]))
-t1 = t1v[best]
-best2 = min(t2v, key=lambda v: np.median(t2v[v]))
-t2 = t2v[best2]
-k1 = float(np.median(t1))
-k2 = float(np.median(t2))
-out = {"nodes": N, "bindings": B, "cold_cache": "1 GiB scratch write before each kernel",
-       "k1_by_threads_ms": {v: round(float(np.median(x)), 4) for v, x in t1v.items()}, "k1_threads": best,
-       "k2_by_mode_ms": {v: round(float(np.median(x)), 4) for v, x in t2v.items()}, "k2_mode": best2,
-       "k1_node_pass": {"ms": round(k1, 4), "alg_bytes": k1_bytes, "GBps": round(k1_bytes / k1 / 1e6, 1),
-                        "frac_of_8TBps": round(k1_bytes / k1 / 1e6 / 8000, 4)},
-       "k2_hot_count": {"ms": round(k2, 4), "alg_bytes": k2_bytes, "GBps": round(k2_bytes / k2 / 1e6, 1),
-                        "frac_of_8TBps": round(k2_bytes / k2 / 1e6 / 8000, 4)}}
+            for name, t in t_k2 + t_ev:
+                acc.setdefault(name, []).append(t)
+    eng.set_profiling(False)
+    keys = d_keys.cpu().numpy()
+    if keys_ref is None:
+        keys_ref = keys
+    assert np.array_equal(keys, keys_ref), f"K2 mode {k2} changed the choices"
+    stages = {}
+    for name, v in acc.items():
+        ms = float(np.median(v))
+        e = {"ms": round(ms, 4)}
+        if name in alg:
+            gbs = alg[name] / (ms * 1e-3) / 1e9
+            e.update({"alg_bytes": alg[name], "GBps": round(gbs, 1), "frac_of_8TBps": round(gbs / 8000, 4)})
+        stages[name] = e
+    res[k2] = stages
+out = {"nodes": N, "bindings": B, "bindings_in_window": b_in, "pods": P,
+       "cold_cache": "1 GiB scratch write before the refresh and before the eval", "by_k2_mode": res}
 print(json.dumps(out))
