@@ -30,6 +30,15 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+# engine stage name -> (kernel name prefix, suffix) in the rocprofv3 summary
+STAGE_KERNEL = {
+    "k1_node_pass+k3a_steps": ("crane::k1_node_pass<", "true>"),
+    "k1_node_pass": ("crane::k1_node_pass<", "false>"),
+    "k2x_partition": ("crane::k2x_partition", ""),
+    "k2y_bin_hist": ("crane::k2y_bin_hist", ""),
+    "k3p_pods": ("crane::k3p_pods", ""),
+}
 
 
 def parse():
@@ -180,9 +189,20 @@ def main():
                            "frac": round(gbs / HBM_PEAK_GBS, 4), "ms": round(t, 4),
                            "alg_bytes": int(alg[name][0]), "bytes": alg[name][1]}
     dom = max(stage_ms, key=stage_ms.get) if stage_ms else None
+    # HBM traffic per launch from the committed PMC summary of this bench
+    # (tools/gpu_pmc.sh: separate FETCH_SIZE / WRITE_SIZE passes, KiB, FETCH_SIZE x2 on gfx950)
+    pmc = {}
+    if os.path.exists(PMC_SUMMARY):
+        pmc = json.load(open(PMC_SUMMARY))
+    for name, e in roofs.items():
+        pre, suf = STAGE_KERNEL.get(name, (None, ""))
+        hits = [v for k, v in pmc.items() if pre and k.startswith(pre) and k.endswith(suf) and "traffic_bytes" in v]
+        e["traffic"] = int(hits[0]["traffic_bytes"]) if hits else None
     roof = None
     if dom in roofs:
-        roof = dict(roofs[dom], kernel=dom, traffic=None)
+        roof = dict(roofs[dom], kernel=dom)
+        if roof.get("traffic") is not None:
+            roof["traffic_source"] = os.path.relpath(PMC_SUMMARY, ROOT)
     elif dom:
         roof = {"bound": None, "kernel": dom, "ms": round(stage_ms[dom], 4), "note": "no HBM roofline for this stage"}
     greedy = None

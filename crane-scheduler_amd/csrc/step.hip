@@ -150,13 +150,12 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
                                                         long long* __restrict__ keys) {
     static_assert(kK3sWaves == 4, "one wave scans each list's counts");
     static_assert(sizeof(VRec<NB>) % 16 == 0, "VRec must be a whole number of int4");
-    constexpr int kVRI4 = (int)(sizeof(VRec<NB>) / 16);
     __shared__ int4 l1[2][kK3sS1];
     __shared__ VRec<NB> lv[2][kK3sVR];
     __shared__ int32_t pre[4][kK3sMaxBlk + 1];
     __shared__ int32_t fl[2][kK3sWaves];
     __shared__ int64_t wr[2][2][kK3sWaves];  // per kind and wave: min, max pod time
-    __shared__ int32_t nin[2], umax[2];      // staged in-range records, uniform maximum (per kind)
+    __shared__ int32_t nin[2], nvr[2], umax[2];  // staged one-step / multi-step records, uniform maximum (per kind)
     const int64_t b = blockIdx.x;
     const int32_t r = (int32_t)(b % R);
     const int64_t grp = b / R;
@@ -229,7 +228,7 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         }
     }
     if (threadIdx.x < 2) {
-        nin[threadIdx.x] = 0;
+        nin[threadIdx.x] = nvr[threadIdx.x] = 0;
         umax[threadIdx.x] = -1;
     }
     const bool bn = __syncthreads_or(ln), bd = __syncthreads_or(ld);  // (also orders the LDS above)
@@ -261,44 +260,32 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         if (take[0] + take[1] + take[2] + take[3] == 0) break;
         if (!first) {
             __syncthreads();  // the previous round's readers are done
-            if (threadIdx.x < 2) nin[threadIdx.x] = 0;
+            if (threadIdx.x < 2) nin[threadIdx.x] = nvr[threadIdx.x] = 0;
             __syncthreads();
         }
-        // one pass over [S1 kind 0 | VR kind 0 (int4 words) | S1 kind 1 | VR kind 1]:
-        // one-step records outside the pod range fold into the uniform maxima, the
-        // rest (and every multi-step record) are staged in LDS
-        const int32_t e1 = take[0], e2 = e1 + take[1] * kVRI4, e3 = e2 + take[2], e4 = e3 + take[3] * kVRI4;
+        // one-step records of both kinds [S1 kind 0 | S1 kind 1]: a record whose step
+        // lies outside the tile's time range folds into the uniform maxima, the rest
+        // are staged in LDS
+        const int32_t e2 = take[0], e4 = e2 + take[2];
         for (int32_t i0 = threadIdx.x; i0 < e4; i0 += 4 * kK3sThreads) {
             const int4* src[4];
-            bool one[4];
-            int kind[4];
-            int4* dst[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {  // addresses first (branches only select pointers)
+            for (int u = 0; u < 4; ++u) {  // addresses first, then 4 loads in flight
                 const int32_t e = min(i0 + u * kK3sThreads, e4 - 1);  // past the end: repeat the last element
                 const int T = e >= e2;
-                const int32_t f = T ? e - e2 : e;  // offset within the kind
-                const int32_t t1 = T ? take[2] : take[0], lo1 = T ? lo[2] : lo[0], lov = T ? lo[3] : lo[1];
-                const int4* g1 = reinterpret_cast<const int4*>(st.single + (int64_t)T * st.npad);
-                const VRec<NB>* gv = reinterpret_cast<const VRec<NB>*>(st.multi) + (int64_t)T * st.npad;
-                const int32_t g4 = f - t1, j = g4 / kVRI4, wd4 = g4 - j * kVRI4;
-                one[u] = f < t1;
-                kind[u] = T;
-                src[u] = one[u] ? g1 + blk_pos(pre[2 * T], m, lo1 + f, b0, st.bs)
-                                : reinterpret_cast<const int4*>(gv + blk_pos(pre[2 * T + 1], m, lov + j, b0, st.bs)) + wd4;
-                dst[u] = reinterpret_cast<int4*>(&lv[T][j]) + wd4;
+                const int32_t f = T ? e - e2 : e;
+                const int32_t lo1 = T ? lo[2] : lo[0];  // selects, not indexing: keeps lo in registers
+                src[u] = reinterpret_cast<const int4*>(st.single + (int64_t)T * st.npad) +
+                         blk_pos(pre[2 * T], m, lo1 + f, b0, st.bs);
             }
             int4 q[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) q[u] = *src[u];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                if (i0 + u * kK3sThreads >= e4) continue;
-                if (!one[u]) {
-                    *dst[u] = q[u];
-                    continue;
-                }
-                const int T = kind[u];
+                const int32_t e = i0 + u * kK3sThreads;
+                if (e >= e4) continue;
+                const int T = e >= e2;
                 const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q[u].y << 32) | (uint32_t)q[u].x);
                 const int64_t lo_t = T ? tlo[1] : tlo[0], hi_t = T ? thi[1] : thi[0];
                 if (bp <= lo_t || bp > hi_t) {  // every pod of the kind here is on one side of the step
@@ -308,6 +295,31 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
                 } else {
                     l1[T][atomicAdd(&nin[T], 1)] = q[u];
                 }
+            }
+        }
+        // multi-step records [VR kind 0 | VR kind 1], one thread per record: one with
+        // no step inside the tile's time range folds (its key at the range start),
+        // the rest are staged
+        const int32_t v2 = take[1], v4 = v2 + take[3];
+        for (int32_t e = threadIdx.x; e < v4; e += kK3sThreads) {
+            const int T = e >= v2;
+            const int32_t f = T ? e - v2 : e;
+            const int32_t lov = T ? lo[3] : lo[1];
+            const VRec<NB> v = reinterpret_cast<const VRec<NB>*>(st.multi)[(int64_t)T * st.npad +
+                                                                       blk_pos(pre[2 * T + 1], m, lov + f, b0, st.bs)];
+            const int64_t lo_t = T ? tlo[1] : tlo[0], hi_t = T ? thi[1] : thi[0];
+            int32_t k = v.key[0];
+            bool inside = false;
+#pragma unroll
+            for (int s2 = 0; s2 < NB; ++s2) {
+                k = lo_t >= v.bp[s2] ? v.key[s2 + 1] : k;
+                inside |= v.bp[s2] > lo_t && v.bp[s2] <= hi_t;
+            }
+            if (!inside) {
+                if (T) um1 = max(um1, k);
+                else um0 = max(um0, k);
+            } else {
+                lv[T][atomicAdd(&nvr[T], 1)] = v;
             }
         }
         __syncthreads();
@@ -331,7 +343,7 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
 #pragma unroll
                 for (int u = 0; u < kK3sPPL; ++u) best[u] = max(best[u], tnow[u] >= bp ? q.w : q.z);
             }
-            for (int32_t j = 0; j < take[2 * T + 1]; ++j) {
+            for (int32_t j = 0; j < nvr[T]; ++j) {
                 const VRec<NB>& v = lv[T][j];
 #pragma unroll
                 for (int u = 0; u < kK3sPPL; ++u) {
