@@ -131,20 +131,59 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     __shared__ int64_t smn[kK1Threads / 64], smx[kK1Threads / 64];
     __shared__ StepShared ssh;
     int64_t tmin = 0, tmax = 0, pmn = 0, pmx = 0;
-    if (STEP) {
-        if (threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
-        batch_range_load<kK1Threads>(step.tile_mm, step.ntiles, pmn, pmx);  // reduced after the SoA loads
-    }
+    if (STEP && threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
     StepSlots so;
     Rec r;
+    int64_t pt[PD], qt[PR];
+    double pv[PD], qv[PR];
+    uint32_t bc[kMaxWin];
+    double hvl = 0.0;
+    int64_t hvt = kTsInvalid;
+    if (n < N) {
+        // every load first, unconditionally (rows past npd/npr read row 0 and are
+        // ignored), so a wave has them all in flight at once; compute after
+#pragma unroll
+        for (int k = 0; k < PD; ++k) {
+            pt[k] = kTsInvalid;
+            pv[k] = 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < PR; ++k) {
+            qt[k] = kTsInvalid;
+            qv[k] = 0.0;
+        }
+        if (pol.n_slots > 0) {  // (val/ts are null without metrics)
+#pragma unroll
+            for (int k = 0; k < PD; ++k) {
+                const int64_t row = k < pol.npd ? pol.pred_slot[k] : 0;
+                pt[k] = ts[row * N + n];
+                pv[k] = val[row * N + n];
+            }
+#pragma unroll
+            for (int k = 0; k < PR; ++k) {
+                const int64_t row = k < pol.npr ? pol.prio_slot[k] : 0;
+                qt[k] = ts[row * N + n];
+                qv[k] = val[row * N + n];
+            }
+        }
+        if (buckets) {
+#pragma unroll
+            for (int b = 0; b < kMaxWin; ++b) bc[b] = b < pol.n_win ? buckets[(int64_t)b * N + n] : 0u;
+        }
+        if (!buckets && hv) {
+            hvl = hv[n];
+            hvt = hv_ts ? hv_ts[n] : hv_ts_counts;  // null: the binding-log value of an earlier pass
+        }
+    }
+    // the batch time range partials: issued after the SoA loads, reduced after the compute
+    if (STEP) batch_range_load<kK1Threads>(step.tile_mm, step.ntiles, pmn, pmx);
     if (n < N) {
 #pragma unroll
         for (int k = 0; k < PD; ++k) {
             int64_t e = kTsInvalid;
             if (k < pol.npd) {
-                const int64_t row = pol.pred_slot[k];
-                const int64_t t = ts[row * N + n];
-                const double u = val[row * N + n];
+                const int64_t t = pt[k];
+                const double u = pv[k];
                 const double lim = pol.pred_limit[k];
                 // isOverLoad (stats.go:94-112): usable (stats.go:51-76), limit != 0, u > limit
                 const bool over = t != kTsInvalid && !(u < 0.0) && lim != 0.0 && u > lim;
@@ -157,9 +196,8 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
             int64_t e = kTsInvalid;
             double term = 0.0;
             if (k < pol.npr) {
-                const int64_t row = pol.prio_slot[k];
-                const int64_t t = ts[row * N + n];
-                const double u = val[row * N + n];
+                const int64_t t = qt[k];
+                const double u = qv[k];
                 if (t != kTsInvalid && !(u < 0.0)) {
                     e = sat_add(t, pol.prio_dur[k]);
                     // getScore (stats.go:89): (1. - usage) * Weight * float64(MaxNodeScore)
@@ -173,15 +211,16 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
         if (buckets) {
             // annotateNodeHotValue (node.go:113-121): value += count / p.Count (Go int division)
             // window w counts the bindings of buckets >= its cutoff rank (K2)
-            uint32_t bc[kMaxWin];
-            for (int b = 0; b < pol.n_win; ++b) {
-                bc[b] = buckets[(int64_t)b * N + n];
-                buckets[(int64_t)b * N + n] = 0;  // consumed: leaves the buckets zeroed for the next K2
-            }
+#pragma unroll
+            for (int b = 0; b < kMaxWin; ++b)  // consumed: leaves the buckets zeroed for the next K2
+                if (b < pol.n_win) buckets[(int64_t)b * N + n] = 0;
             int64_t v = 0;
-            for (int w = 0; w < pol.n_win; ++w) {
+#pragma unroll
+            for (int w = 0; w < kMaxWin; ++w) {
+                if (w >= pol.n_win) break;
                 int64_t c = 0;
-                for (int b = pol.win_pos[w]; b < pol.n_win; ++b) c += bc[b];
+#pragma unroll
+                for (int b = 0; b < kMaxWin; ++b) c += (b >= pol.win_pos[w] && b < pol.n_win) ? bc[b] : 0u;
                 if (cnt_out) cnt_out[(int64_t)w * N + n] = (uint32_t)c;
                 v += c / pol.win_count[w];
             }
@@ -191,8 +230,8 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
             r.pen = go_int(h * 10.0);
             r.e_hv = v >= 0 ? sat_add(hv_ts_counts, kHotActiveNs) : kTsInvalid;
         } else if (hv) {
-            const double h = hv[n];
-            const int64_t t = hv_ts ? hv_ts[n] : hv_ts_counts;  // null: the binding-log value of an earlier pass
+            const double h = hvl;
+            const int64_t t = hvt;
             r.pen = go_int(h * 10.0);
             r.e_hv = (t != kTsInvalid && !(h < 0.0)) ? sat_add(t, kHotActiveNs) : kTsInvalid;
         } else {
