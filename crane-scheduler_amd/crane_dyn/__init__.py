@@ -63,8 +63,10 @@ def _load():
         "crane_dyn_upload_nodes": (C.c_int, [vp, C.c_int64, C.c_int64, vp, vp, vp, vp]),
         "crane_dyn_upload_bindings": (C.c_int, [vp, C.c_int64, vp, vp]),
         "crane_dyn_refresh_hot_values": (C.c_int, [vp, C.c_int64, C.c_int64]),
+        "crane_dyn_hot_values": (C.c_int, [vp, C.c_int64, vp]),
         "crane_dyn_eval": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, vp]),
         "crane_dyn_eval_keys_async": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp]),
+        "crane_dyn_step_keys_async": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp, vp]),
         "crane_dyn_refresh_hot_values_async": (C.c_int, [vp, C.c_int64, C.c_int64, vp]),
         "crane_dyn_node_pass_async": (C.c_int, [vp, vp]),
         "crane_dyn_greedy": (C.c_int, [vp, C.c_int64, C.c_int64, vp, vp]),
@@ -87,9 +89,9 @@ ABI_SYMBOLS = (
     "crane_policy_load_file", "crane_policy_load_bytes", "crane_policy_view", "crane_policy_free",
     "crane_tz_offset", "crane_parse_annotation", "crane_parse_annotations", "crane_dyn_create", "crane_dyn_destroy", "crane_dyn_last_error",
     "crane_dyn_num_metrics", "crane_dyn_metric_name", "crane_dyn_upload_nodes", "crane_dyn_upload_bindings",
-    "crane_dyn_refresh_hot_values", "crane_dyn_eval", "crane_dyn_eval_keys_async",
+    "crane_dyn_refresh_hot_values", "crane_dyn_eval", "crane_dyn_eval_keys_async", "crane_dyn_step_keys_async",
     "crane_dyn_refresh_hot_values_async", "crane_dyn_node_pass_async", "crane_dyn_greedy", "crane_dyn_key_node",
-    "crane_dyn_set_profiling", "crane_dyn_stage_times",
+    "crane_dyn_set_profiling", "crane_dyn_stage_times", "crane_dyn_hot_values",
     "crane_dyn_version",
 )
 
@@ -264,6 +266,12 @@ class Engine:
     def refresh_hot_values(self, now_ns, hv_ts_ns=None):
         self._check(lib.crane_dyn_refresh_hot_values(self.h, int(now_ns), int(now_ns if hv_ts_ns is None else hv_ts_ns)))
 
+    def hot_values(self):
+        """Per-node hot value as Score uses it (controller side, node.go:113-121)."""
+        out = np.empty(self.n_nodes, np.float64)
+        self._check(lib.crane_dyn_hot_values(self.h, self.n_nodes, _ptr(out)))
+        return out
+
     def eval(self, now_ns, pod_flags=None, matrix=False):
         """Returns (first_fail[P,N] or None, score[P,N] or None, chosen[P], chosen_score[P])."""
         now = np.ascontiguousarray(now_ns, np.int64).reshape(-1)
@@ -305,6 +313,14 @@ class Engine:
         if n < 0:
             self._check(n)
         return [(names[i].decode(), ms[i]) for i in range(n)]
+
+    def step_keys_async(self, now_ns, hv_ts_ns, d_now, d_flags, d_keys, stream=None):
+        """One scheduling step: hot-value refresh at now_ns + keys-only eval (torch CUDA tensors)."""
+        P = d_now.numel()
+        assert d_keys.numel() == P and d_now.dtype.itemsize == 8 and d_keys.dtype.itemsize == 8
+        self._check(lib.crane_dyn_step_keys_async(self.h, int(now_ns), int(hv_ts_ns), P, C.c_void_p(d_now.data_ptr()),
+                                                  None if d_flags is None else C.c_void_p(d_flags.data_ptr()),
+                                                  C.c_void_p(d_keys.data_ptr()), stream))
 
     def greedy(self, n_pods, now_ns, pod_flags=None):
         fl = None if pod_flags is None else np.ascontiguousarray(pod_flags, np.uint8)

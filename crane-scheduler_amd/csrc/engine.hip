@@ -70,6 +70,8 @@ struct crane_dyn {
     std::string err;
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;  // second queue: K3p overlaps K2 in crane_dyn_step_keys_async
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // policy
     DevPolicy dp{};
     int shape = kShape16x16;
@@ -226,6 +228,9 @@ int crane_dyn_create(const crane_policy* pol, int32_t device, crane_dyn** out) {
     h->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
     if (e != hipSuccess) {
         h->hipfail(e, "hipSetDevice/hipStreamCreate");
         h->N = -2;
@@ -278,6 +283,12 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
     h->mFs.release(); h->mIs.release(); h->mgi.release();
     h->sperm.release(); h->scnt.release(); h->stile.release(); h->spnow.release(); h->svrec.release(); h->sstep1.release();
+    if (h->side) {
+        (void)hipStreamSynchronize(h->side);
+        (void)hipStreamDestroy(h->side);
+    }
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -463,44 +474,71 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
     return CRANE_OK;
 }
 
+// ---- keys-only step path (step.hip): K3p -> [K1 +] K3a -> K3s
+struct StepPlan {
+    StepGeometry g;
+    StepTables stt;
+    bool fuse;  // K3a fused into the node pass (records stale)
+};
+
+static bool step_path_ok(const crane_dyn* h, int64_t P) {
+    return k3_variant() == 5 && h->N >= 0 && h->N < kStepMaxNodes && P < (1LL << 31);
+}
+
+static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
+    const char* fe = getenv("CRANE_K1_FUSE");
+    sp.fuse = h->rec_dirty && !(fe && fe[0] == '0');
+    const int32_t bs = sp.fuse ? k1_threads() : kStepSeg;  // producer workgroup size
+    const int32_t nblk = (int32_t)((h->N + bs - 1) / bs);
+    sp.g = step_geometry(P, h->N, nblk);
+    const StepGeometry& g = sp.g;
+    HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
+    HIPTRY(h, h->stile.reserve((size_t)(2 * g.ntiles)));
+    HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
+    HIPTRY(h, h->scnt.reserve((size_t)std::max<int32_t>(nblk, 1) * 6));  // cnt [nblk][4] + flat [nblk][2]
+    HIPTRY(h, h->sstep1.reserve((size_t)(2 * g.npad)));
+    HIPTRY(h, h->svrec.reserve((size_t)(2 * g.npad) * step_vrec_bytes(h->shape)));
+    sp.stt = StepTables{h->scnt.p, h->scnt.p + (size_t)nblk * 4, h->sstep1.p, h->svrec.p, g.npad, bs, nblk};
+    return CRANE_OK;
+}
+
+static int step_pods(crane_dyn* h, const StepPlan& sp, int64_t P, const int64_t* d_now, const uint8_t* d_flags,
+                     long long* d_keys, hipStream_t st) {
+    HIPTRY(h, prof_begin(h, st));
+    HIPTRY(h, launch_step_pods(d_now, d_flags, P, d_keys, sp.stt, sp.g, h->sperm.p, h->spnow.p, h->stile.p, st));
+    HIPTRY(h, prof_mark(h, st, "k3p_pods"));
+    return CRANE_OK;
+}
+
+static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_keys, hipStream_t st) {
+    if (P == 0) return CRANE_OK;
+    if (sp.fuse) {
+        K1Step ks{h->stile.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, sp.stt};
+        int rc = node_pass_locked(h, st, nullptr, &ks);
+        if (rc) return rc;
+    } else {
+        if (h->rec_dirty) {
+            int rc = node_pass_locked(h, st);
+            if (rc) return rc;
+        }
+        HIPTRY(h, launch_step_nodes(h->shape, h->rec.p, h->N, h->dp.wsum, h->dp.noprio, sp.stt, sp.g, h->stile.p, st));
+        HIPTRY(h, prof_mark(h, st, "k3a_steps"));
+    }
+    HIPTRY(h, launch_step_pairs(h->shape, h->N, h->node_offset, P, d_keys, sp.stt, sp.g, h->sperm.p, h->spnow.p, st));
+    HIPTRY(h, prof_mark(h, st, "k3s_eval"));
+    return CRANE_OK;
+}
+
 static int eval_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags, long long* d_keys,
                        int8_t* d_ff, int64_t* d_score, hipStream_t st) {
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
     const bool matrix = d_ff || d_score;
-    if (!matrix && k3_variant() == 5 && h->N < kStepMaxNodes && P < (1LL << 31)) {
-        // step path: K3p (pod partition, key init, header reset) -> [K1 +] K3a (step
-        // tables; fused into the node pass when the records are stale) -> K3s (pairs)
-        const char* fe = getenv("CRANE_K1_FUSE");
-        const bool fuse = h->rec_dirty && !(fe && fe[0] == '0');
-        const int32_t bs = fuse ? k1_threads() : kStepSeg;  // producer workgroup size
-        const int32_t nblk = (int32_t)((h->N + bs - 1) / bs);
-        const StepGeometry g = step_geometry(P, h->N, nblk);
-        HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
-        HIPTRY(h, h->stile.reserve((size_t)(2 * g.ntiles)));
-        HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
-        HIPTRY(h, h->scnt.reserve((size_t)std::max<int32_t>(nblk, 1) * 6));  // cnt [nblk][4] + flat [nblk][2]
-        HIPTRY(h, h->sstep1.reserve((size_t)(2 * g.npad)));
-        HIPTRY(h, h->svrec.reserve((size_t)(2 * g.npad) * step_vrec_bytes(h->shape)));
-        StepTables stt{h->scnt.p, h->scnt.p + (size_t)nblk * 4, h->sstep1.p, h->svrec.p, g.npad, bs, nblk};
-        HIPTRY(h, prof_begin(h, st));
-        HIPTRY(h, launch_step_pods(d_now, d_flags, P, d_keys, stt, g, h->sperm.p, h->spnow.p, h->stile.p, st));
-        HIPTRY(h, prof_mark(h, st, "k3p_pods"));
-        if (P == 0) return CRANE_OK;
-        if (fuse) {
-            K1Step ks{h->stile.p, (int32_t)g.ntiles, h->dp.noprio, h->dp.wsum, stt};
-            int rc = node_pass_locked(h, st, nullptr, &ks);
-            if (rc) return rc;
-        } else {
-            if (h->rec_dirty) {
-                int rc = node_pass_locked(h, st);
-                if (rc) return rc;
-            }
-            HIPTRY(h, launch_step_nodes(h->shape, h->rec.p, h->N, h->dp.wsum, h->dp.noprio, stt, g, h->stile.p, st));
-            HIPTRY(h, prof_mark(h, st, "k3a_steps"));
-        }
-        HIPTRY(h, launch_step_pairs(h->shape, h->N, h->node_offset, P, d_keys, stt, g, h->sperm.p, h->spnow.p, st));
-        HIPTRY(h, prof_mark(h, st, "k3s_eval"));
-        return CRANE_OK;
+    if (!matrix && step_path_ok(h, P)) {
+        StepPlan sp;
+        int rc = step_plan(h, P, sp);
+        if (!rc) rc = step_pods(h, sp, P, d_now, d_flags, d_keys, st);
+        if (!rc) rc = step_rest(h, sp, P, d_keys, st);
+        return rc;
     }
     if (h->rec_dirty) {
         int rc = node_pass_locked(h, st);
@@ -529,6 +567,32 @@ int crane_dyn_refresh_hot_values(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns)
     return CRANE_OK;
 }
 
+int crane_dyn_hot_values(crane_dyn* h, int64_t n, double* hv_out) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before reading hot values");
+    if (n != h->N || (n > 0 && !hv_out)) return h->fail(CRANE_E_INVALID, "hv_out must hold one value per node");
+    if (n == 0) return CRANE_OK;
+    HIPTRY(h, hipSetDevice(h->device));
+    const double* src = nullptr;
+    if (h->hv_from_counts) {
+        if (h->counts_pending) {  // the node pass consumes the counts and keeps the values
+            int rc = node_pass_locked(h, h->stream);
+            if (rc) return rc;
+        }
+        src = h->hvc.p;
+    } else if (h->have_hv) {
+        src = h->hv.p;
+    }
+    if (src) {
+        HIPTRY(h, hipMemcpyAsync(hv_out, src, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
+        HIPTRY(h, hipStreamSynchronize(h->stream));
+    } else {
+        for (int64_t i = 0; i < n; ++i) hv_out[i] = 0.0;
+    }
+    return CRANE_OK;
+}
+
 int crane_dyn_refresh_hot_values_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, void* stream) {
     if (!h) return CRANE_E_INVALID;
     std::lock_guard<std::mutex> g(h->mu);
@@ -552,6 +616,47 @@ int crane_dyn_eval_keys_async(crane_dyn* h, int64_t P, const int64_t* d_now, con
     HIPTRY(h, hipSetDevice(h->device));
     return eval_locked(h, P, d_now, d_flags, reinterpret_cast<long long*>(d_keys), nullptr, nullptr,
                        stream ? (hipStream_t)stream : h->stream);
+}
+
+int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, int64_t P, const int64_t* d_now,
+                              const uint8_t* d_flags, int64_t* d_keys, void* stream) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (P < 0 || (P > 0 && (!d_now || !d_keys))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
+    if (P > (int64_t)0x7FFFFFFF * 256) return h->fail(CRANE_E_INVALID, "too many pods");
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
+    HIPTRY(h, hipSetDevice(h->device));
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    long long* keys = reinterpret_cast<long long*>(d_keys);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIPTRY(h, hipStreamIsCapturing(st, &cap));
+    // refresh sets rec_dirty: plan after it (the plan only reads N, P and whether the records are stale)
+    // Overlapping K3p with K2 on the second queue measured slower at config 3 (65 vs 55 us per
+    // step: the cross-queue event waits cost more than the 4.5-us K3p), so it is opt-in.
+    const char* ov = getenv("CRANE_STEP_OVERLAP");
+    const bool want = ov && ov[0] == '1';
+    const bool overlap = want && h->side && !h->prof && cap == hipStreamCaptureStatusNone && step_path_ok(h, P) &&
+                         P > 0;
+    if (!overlap) {
+        int rc = hot_values_locked(h, now_ns, hv_ts_ns, st);
+        if (!rc) rc = eval_locked(h, P, d_now, d_flags, keys, nullptr, nullptr, st);
+        return rc;
+    }
+    // K3p depends only on the pods: it runs on the side stream while K2 runs on st.
+    // The fork event orders it after everything already on st (the previous step's K3s
+    // reads the buffers K3p rewrites; the caller's writes of d_now / d_flags).
+    HIPTRY(h, hipEventRecord(h->ev_fork, st));
+    HIPTRY(h, hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    int rc = hot_values_locked(h, now_ns, hv_ts_ns, st);
+    if (rc) return rc;
+    StepPlan sp;
+    rc = step_plan(h, P, sp);
+    if (rc) return rc;
+    rc = step_pods(h, sp, P, d_now, d_flags, keys, h->side);
+    if (rc) return rc;
+    HIPTRY(h, hipEventRecord(h->ev_join, h->side));
+    HIPTRY(h, hipStreamWaitEvent(st, h->ev_join, 0));
+    return step_rest(h, sp, P, keys, st);
 }
 
 int crane_dyn_eval(crane_dyn* h, int64_t P, const int64_t* now_ns, const uint8_t* pod_flags, int8_t* first_fail,

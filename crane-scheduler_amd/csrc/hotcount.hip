@@ -168,7 +168,8 @@ __global__ __launch_bounds__(kHT) void k2d_bin_hist(const uint32_t* __restrict__
 //                atomics into the (zeroed) buckets.
 // Zipf-hot keys: both kernels aggregate equal keys within a wave before the
 // LDS atomic (one atomic per wave for the wave's most common key).
-constexpr int kXPer = 8;     // bindings per thread in X
+constexpr int kXPer = 8;     // bindings per thread in X (16 measured slower: fewer workgroups in flight)
+constexpr int kYPer = 8;     // entries per thread and batch in Y
 constexpr int kXChunk = kHT * kXPer;
 constexpr int kYSplits = 16;  // workgroups per bin in Y (Zipf-hot bins want many, each pays a prologue)
 
@@ -295,7 +296,7 @@ __global__ __launch_bounds__(kHT) void k2y_bin_hist(const uint32_t* __restrict__
     const uint32_t e_lo = (uint32_t)((uint64_t)len * split / gridDim.y);
     const uint32_t e_hi = (uint32_t)((uint64_t)len * (split + 1) / gridDim.y);
     // each lane walks e = e_lo + tid, + kHT, ... advancing its source region as it
-    // goes; kXPer entries per batch, their loads issued together
+    // goes; kYPer entries per batch, their loads issued together
     uint32_t e = e_lo + threadIdx.x;
     int blk = 0;
     if (e < e_hi) {  // first region: binary search, then forward steps
@@ -307,10 +308,10 @@ __global__ __launch_bounds__(kHT) void k2y_bin_hist(const uint32_t* __restrict__
         }
         blk = l;
     }
-    for (uint32_t e0 = e_lo; e0 < e_hi; e0 += kHT * kXPer) {
-        uint32_t v[kXPer];
+    for (uint32_t e0 = e_lo; e0 < e_hi; e0 += kHT * kYPer) {
+        uint32_t v[kYPer];
 #pragma unroll
-        for (int u = 0; u < kXPer; ++u) {
+        for (int u = 0; u < kYPer; ++u) {
             const uint32_t eu = e + u * kHT;
             v[u] = 0xFFFFFFFFu;
             if (eu < e_hi) {
@@ -319,11 +320,11 @@ __global__ __launch_bounds__(kHT) void k2y_bin_hist(const uint32_t* __restrict__
             }
         }
 #pragma unroll
-        for (int u = 0; u < kXPer; ++u) {
+        for (int u = 0; u < kYPer; ++u) {
             const bool act = v[u] != 0xFFFFFFFFu;
             (void)wave_lds_add(hist, act ? (v[u] >> 24) * binw + (v[u] & 0xFFFFFF) : 0u, act);
         }
-        e += kHT * kXPer;
+        e += kHT * kYPer;
     }
     __syncthreads();
     // buckets are zero on entry (K1 zeroes what it consumes): add the non-zero

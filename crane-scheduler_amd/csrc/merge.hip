@@ -41,12 +41,17 @@ constexpr int kMT = 256;     // node-block size of M1, M2, M4
 constexpr int kM5T = 1024;   // single-workgroup kernels of M5
 constexpr int kLevels = 101; // scores 0..100
 
-__device__ __forceinline__ int64_t stair_v(const uint32_t* c, int64_t k, const MergeArgs& a) {
-    int64_t v = 0;
-#pragma unroll
-    for (int w = 0; w < kMaxWin; ++w)  // static indices: c stays in registers
-        if (w < a.n_win) v += ((int64_t)c[w] + (a.win_inc[w] ? k : 0)) / a.win_count[w];
-    return v;
+// x / C and x % C for x >= 0, C > 0: 32-bit unsigned division when both fit
+// (always, at realistic binding counts), 64-bit otherwise
+__device__ __forceinline__ void udivmod(int64_t x, int64_t C, int64_t& q, int64_t& r) {
+    if (((uint64_t)x | (uint64_t)C) <= 0xFFFFFFFFull) {
+        const uint32_t xq = (uint32_t)x / (uint32_t)C;
+        q = xq;
+        r = (int64_t)((uint32_t)x - xq * (uint32_t)C);
+    } else {
+        q = x / C;
+        r = x - q * C;
+    }
 }
 
 // Runs of a node's staircase s(k), k = 0 .. cap-1, in order (levels non-increasing).
@@ -55,16 +60,21 @@ struct RunIter {
     uint32_t c[kMaxWin];
     __device__ bool next(const MergeArgs& a, int& lvl, int64_t& len) {
         if (k >= cap) return false;
-        const int64_t f = base - 10 * stair_v(c, k, a);  // no wrap: base >= INT64_MIN + 2^40 (M1 flag)
-        lvl = (int)(f < 0 ? 0 : (f > 100 ? 100 : f));
-        int64_t d = INT64_MAX;
-        if (lvl > 0)
+        // hot value sum_w (c_w + k) / C_w (node.go:117) and, per window that a binding
+        // enters, the bindings until its quotient grows
+        int64_t v = 0, d = INT64_MAX;
 #pragma unroll
-            for (int w = 0; w < kMaxWin; ++w)
-                if (w < a.n_win && a.win_inc[w]) {
-                    const int64_t C = a.win_count[w];
-                    d = min(d, C - ((int64_t)c[w] + k) % C);  // bindings until this window's quotient grows
-                }
+        for (int w = 0; w < kMaxWin; ++w)  // static indices: c stays in registers
+            if (w < a.n_win) {
+                const int64_t C = a.win_count[w];
+                int64_t q, rem;
+                udivmod((int64_t)c[w] + (a.win_inc[w] ? k : 0), C, q, rem);
+                v += q;
+                if (a.win_inc[w]) d = min(d, C - rem);
+            }
+        const int64_t f = base - 10 * v;  // no wrap: base >= INT64_MIN + 2^40 (M1 flag)
+        lvl = (int)(f < 0 ? 0 : (f > 100 ? 100 : f));
+        if (lvl == 0) d = INT64_MAX;  // clamped at 0 from here on
         len = min(d, cap - k);
         k += len;
         return true;

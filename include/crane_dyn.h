@@ -124,6 +124,13 @@ int crane_dyn_upload_bindings(crane_dyn *h, int64_t n, const int32_t *node, cons
  * as the node_hot_value annotation, stamped hv_ts_ns, from now on. */
 int crane_dyn_refresh_hot_values(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns);
 
+/* Controller side (annotateNodeHotValue, node.go:113-121): the hot value of
+ * every node of the shard as the Score phase uses it — after a refresh, the
+ * binding-log value sum_w count_w / Count_w (an integer, written by the
+ * controller as strconv.Itoa); otherwise the uploaded annotation value (0 if
+ * none).  hv_out holds n = the shard's node count values. */
+int crane_dyn_hot_values(crane_dyn *h, int64_t n, double *hv_out);
+
 /* Evaluate a pod batch against the current shard.  now_ns[p] is pod p's
  * time.Now(); pod_flags[p] carries CRANE_POD_* bits (NULL = 0).
  * Outputs (any may be NULL):
@@ -144,6 +151,13 @@ int crane_dyn_eval(crane_dyn *h, int64_t n_pods, const int64_t *now_ns, const ui
  * max) gives the global choice. */
 int crane_dyn_eval_keys_async(crane_dyn *h, int64_t n_pods, const int64_t *d_now_ns,
                               const uint8_t *d_pod_flags, int64_t *d_keys, void *stream);
+/* One scheduling step, asynchronous on `stream`: hot values from the bindings
+ * at now_ns (as crane_dyn_refresh_hot_values_async) then the keys-only
+ * evaluation of the pod batch (as crane_dyn_eval_keys_async).  With
+ * CRANE_STEP_OVERLAP=1 the pod-only work runs on an engine-internal second
+ * queue while the hot values are counted. */
+int crane_dyn_step_keys_async(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns, int64_t n_pods,
+                              const int64_t *d_now_ns, const uint8_t *d_pod_flags, int64_t *d_keys, void *stream);
 /* Asynchronous pieces of one scheduling step on `stream`:
  * hot values from bindings (K2) and the node pass (K1). */
 int crane_dyn_refresh_hot_values_async(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns, void *stream);

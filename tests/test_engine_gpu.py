@@ -246,3 +246,58 @@ def test_config3_full_size_parity():
     # host-API path agrees with the device-resident path on a slice
     _, _, ch, cs = eng.eval(c.now[:512], c.ds[:512])
     assert np.array_equal(ch, node[:512]) and np.array_equal(cs, score[:512])
+
+
+def test_hot_values_readback_matches_controller():
+    """crane_dyn_hot_values after a refresh = the controller's annotateNodeHotValue
+    (node.go:113-121) over the binding log, per node; before any refresh it is the
+    uploaded annotation value."""
+    from oracle import oracle as O
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 5000, 1, n_bindings=200_000, seed=31)
+    eng = engine_for(spec, c)
+    assert np.array_equal(eng.hot_values(), c.hv)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    now = int(synth.NOW0_NS)
+    eng.refresh_hot_values(now, now)
+    _, hv = O.hot_values(spec, c.b_node, c.b_ts, c.n_nodes, now // 10**9)
+    assert np.array_equal(eng.hot_values(), hv.astype(np.float64))
+    _ = eng.eval(c.now[:1], c.ds[:1])  # consumed by the node pass: still the same values
+    assert np.array_equal(eng.hot_values(), hv.astype(np.float64))
+
+
+def test_config4_shard_parity():
+    """BASELINE config 4, one rank's shard (125k nodes, node_offset 3 x 125k) x 100k pods
+    spread over 100 s: the step tables carry many one- and multi-step nodes and K3s
+    stages them over several rounds; a 160-pod sample (incl. DaemonSet pods) is
+    checked against the oracle bit for bit, global indices include the offset."""
+    import torch
+    spec = cd.default_policy_spec()
+    N, P, off = 125_000, 100_000, 3 * 125_000
+    c = synth.make_cluster(spec, N, P, n_bindings=1_000_000, seed=20254215)
+    eng = cd.Engine(cd.Policy(spec), 0)
+    val, ts, _ = c.rows(eng.metric_names)
+    eng.upload_nodes(val, ts, c.hv, c.hv_ts, node_offset=off)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    now_sync = int(synth.NOW0_NS)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    d_keys = torch.empty(P, dtype=torch.int64, device=dev)
+    with torch.cuda.stream(st):
+        eng.step_keys_async(now_sync, now_sync, d_now, d_flags, d_keys, st.cuda_stream)
+    st.synchronize()
+    keys = d_keys.cpu().numpy()
+    node = np.where(keys < 0, -1, 0xFFFFFFFF - (keys & 0xFFFFFFFF))
+    score = np.where(keys < 0, -1, keys >> 32)
+    _, hv = O.hot_values(spec, c.b_node, c.b_ts, N, now_sync // 10**9)
+    hv_over = (hv.astype(np.float64), np.full(N, now_sync, np.int64))
+    sample = np.unique(np.concatenate([np.arange(16), np.linspace(0, P - 1, 128).astype(int),
+                                       np.flatnonzero(c.ds)[::max(1, int(c.ds.sum()) // 16)][:16]]))
+    offm, osc, och = oracle_soa(spec, c, now=c.now[sample], ds=c.ds[sample], hv_override=hv_over)
+    assert np.array_equal(node[sample], np.where(och < 0, -1, och + off))
+    for i, p in enumerate(sample):
+        feas = (offm[i] < 0) | bool(c.ds[p])
+        assert score[p] == (osc[i][feas].max() if feas.any() else -1)
+    assert ((score >= 0) & (score <= 100)).all()

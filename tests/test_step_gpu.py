@@ -177,3 +177,32 @@ def test_hot_values_kept_after_consumption():
     off, osc, och = oracle_soa(spec, c, hv_override=_oracle_hv(spec, c, now))
     assert np.array_equal(ch1, och) and np.array_equal(ch2, och)
     assert np.array_equal(ff, off) and np.array_equal(sc, osc)
+
+
+@pytest.mark.parametrize("overlap", ["0", "1"])
+def test_step_keys_async_matches_oracle(overlap, monkeypatch):
+    """crane_dyn_step_keys_async replayed (serial, and with K3p on the engine's second
+    queue overlapping K2): each step equals the oracle with binding-log hot values;
+    with stage profiling on (serial path) too."""
+    import torch
+    monkeypatch.setenv("CRANE_STEP_OVERLAP", overlap)
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 30000, 5000, n_bindings=300_000, seed=27, pod_step_ns=2_000_000, ds_frac=0.02)
+    eng = engine_for(spec, c)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    now = int(synth.NOW0_NS)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
+    _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=_oracle_hv(spec, c, now))
+    with torch.cuda.stream(st):
+        for rep in range(4):
+            eng.set_profiling(rep == 3)
+            eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
+            st.synchronize()
+            ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
+            assert np.array_equal(ch, och), rep
+    names = [n for n, _ in eng.stage_times()]
+    assert names == ["k2x_partition", "k2y_bin_hist", "k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
