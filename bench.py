@@ -36,6 +36,7 @@ STAGE_KERNEL = {
     "k1_node_pass+k3a_steps": ("crane::k1_node_pass<", "true>"),
     "k1_node_pass": ("crane::k1_node_pass<", "false>"),
     "k2x_partition": ("crane::k2x_partition", ""),
+    "k2x_partition+k3p_pods": ("crane::k2x_pods", ""),
     "k2y_bin_hist": ("crane::k2y_bin_hist", ""),
     "k3p_pods": ("crane::k3p_pods", ""),
 }
@@ -171,13 +172,20 @@ def main():
     rec_bytes = -(-(24 + 16 * pr_ + 8 + 8 * pd_) // 16) * 16  # sizeof(NodeRec<PD,PR>)
     max_tr_s = max(tr for tr, _ in spec["hotValue"]) // 10**9
     b_in = int((c.b_ts > now_sync // 10**9 - max_tr_s).sum())  # bindings inside the widest window
+    # the fused keys-only node pass leaves the records in LDS (CRANE_K1_KEEP_REC=1 writes them)
+    keep_rec = os.environ.get("CRANE_K1_KEEP_REC") == "1"
+    k2x_b = B * 12 + b_in * 4
+    k3p_b = P * (8 + 1 + 4 + 8 + 8)
     alg = {
-        "k2x_partition": (B * 12 + b_in * 4, "bindings read (int32 node + int64 ts) + kept entries written"),
+        "k2x_partition": (k2x_b, "bindings read (int32 node + int64 ts) + kept entries written"),
+        "k2x_partition+k3p_pods": (k2x_b + k3p_b, "bindings read + kept entries written; pod now + flag read, "
+                                                  "partition + keys written"),
         "k2y_bin_hist": (b_in * 4 + 4 * W * N, "kept entries read + window counts added"),
-        "k1_node_pass+k3a_steps": (N * (16 * M + 8 * W + rec_bytes + 8),
-                                   "SoA (value, ts) read + buckets read and zeroed + NodeRec + hot value written"),
-        "k1_node_pass": (N * (16 * M + 8 * W + rec_bytes + 8), "as above"),
-        "k3p_pods": (P * (8 + 1 + 4 + 8 + 8), "pod now + flag read, partition + keys written"),
+        "k1_node_pass+k3a_steps": (N * (16 * M + 8 * W + 8 + (rec_bytes if keep_rec else 0)),
+                                   "SoA (value, ts) read + buckets read and zeroed + hot value written"
+                                   + (" + NodeRec written" if keep_rec else "")),
+        "k1_node_pass": (N * (16 * M + 8 * W + rec_bytes + 8), "SoA + buckets + NodeRec + hot value"),
+        "k3p_pods": (k3p_b, "pod now + flag read, partition + keys written"),
     }
     roofs = {}
     for name, t in stage_ms.items():

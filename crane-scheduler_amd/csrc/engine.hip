@@ -371,7 +371,11 @@ static hipError_t prof_begin(crane_dyn* h, hipStream_t st) {
     return h->prof && h->nev == 0 ? prof_mark(h, st, "begin") : hipSuccess;
 }
 
-static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hipStream_t st) {
+// pods (optional): the step path's pod preparation, launched together with K2x
+// when the partitioned K2 runs (*pods_done reports whether it did).
+static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hipStream_t st,
+                             const PodPrep* pods = nullptr, bool* pods_done = nullptr) {
+    if (pods_done) *pods_done = false;
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before refreshing hot values");
     DevPolicy& dp = h->dp;
     HotCutoffs cut{};
@@ -403,8 +407,9 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         HIPTRY(h, h->k2_sorted.reserve(hot_part_scratch(gp)));
         HIPTRY(h, prof_begin(h, st));
         HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, h->k2_sorted.p, st,
-                                        1));
-        HIPTRY(h, prof_mark(h, st, "k2x_partition"));
+                                        1, pods));
+        HIPTRY(h, prof_mark(h, st, pods ? "k2x_partition+k3p_pods" : "k2x_partition"));
+        if (pods_done) *pods_done = pods != nullptr;
         HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, h->k2_sorted.p, st,
                                         2));
         HIPTRY(h, prof_mark(h, st, "k2y_bin_hist"));
@@ -448,7 +453,12 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
     a.N = h->N;
     a.val = h->val.p;
     a.ts = h->ts.p;
-    a.out = h->rec.p;
+    // the fused keys-only step reads its records from LDS; writing them out
+    // (160 B/node of the pass's 280) is left to the next pass that reads them
+    // (CRANE_K1_KEEP_REC=1 keeps them)
+    const char* kr = getenv("CRANE_K1_KEEP_REC");
+    const bool keep = !step || (kr && kr[0] == '1');
+    a.out = keep ? h->rec.p : nullptr;
     a.hv_ts_counts = h->hv_ts_counts;
     const bool consume = h->hv_from_counts && h->counts_pending;
     if (cnt_out && !consume) return h->fail(CRANE_E_STATE, "per-window counts need a hot-value refresh first");
@@ -470,7 +480,7 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
         h->buckets_zero = true;  // K1 zeroed what it read
         h->counts_pending = false;
     }
-    h->rec_dirty = false;
+    h->rec_dirty = !keep;
     return CRANE_OK;
 }
 
@@ -637,6 +647,22 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
     const bool want = ov && ov[0] == '1';
     const bool overlap = want && h->side && !h->prof && cap == hipStreamCaptureStatusNone && step_path_ok(h, P) &&
                          P > 0;
+    if (!overlap && step_path_ok(h, P) && P > 0) {
+        // K3p rides in K2x's launch (when the partitioned K2 runs); the refresh
+        // leaves the records stale, so plan for the fused node pass
+        h->rec_dirty = true;
+        StepPlan sp;
+        int rc = step_plan(h, P, sp);
+        if (rc) return rc;
+        const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys};
+        bool pods_done = false;
+        const char* mp = getenv("CRANE_K2X_PODS");  // 0: K3p in its own launch (A/B)
+        const bool ride = !(mp && mp[0] == '0');
+        rc = hot_values_locked(h, now_ns, hv_ts_ns, st, ride ? &pp : nullptr, &pods_done);
+        if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, st);
+        if (!rc) rc = step_rest(h, sp, P, keys, st);
+        return rc;
+    }
     if (!overlap) {
         int rc = hot_values_locked(h, now_ns, hv_ts_ns, st);
         if (!rc) rc = eval_locked(h, P, d_now, d_flags, keys, nullptr, nullptr, st);

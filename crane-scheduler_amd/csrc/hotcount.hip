@@ -19,6 +19,7 @@
 
 #include "dyn_types.hpp"
 #include "kernels.hpp"
+#include "pods.hpp"
 
 namespace crane {
 
@@ -209,15 +210,15 @@ __device__ __forceinline__ uint32_t wg_excl_scan_u32(uint32_t v, uint32_t* part)
     return pre + x - v;
 }
 
-__global__ __launch_bounds__(kHT) void k2x_partition(const int32_t* __restrict__ bnode,
-                                                     const int64_t* __restrict__ bts, int64_t B, int64_t N,
-                                                     HotCutoffs cut, HotPart g, uint32_t* __restrict__ C,
-                                                     uint32_t* __restrict__ O, uint32_t* __restrict__ region) {
+__device__ __forceinline__ void k2x_body(const int32_t blk, const int32_t* __restrict__ bnode,
+                                         const int64_t* __restrict__ bts, int64_t B, int64_t N, const HotCutoffs& cut,
+                                         const HotPart& g, uint32_t* __restrict__ C, uint32_t* __restrict__ O,
+                                         uint32_t* __restrict__ region) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];  // hist [nbins], off [nbins]
     __shared__ uint32_t part[kHT];
     uint32_t* hist = sh;
     uint32_t* off = sh + g.nbins;
-    const int64_t b0 = (int64_t)blockIdx.x * kXChunk + threadIdx.x;
+    const int64_t b0 = (int64_t)blk * kXChunk + threadIdx.x;
     int32_t nd[kXPer];
     int64_t ts[kXPer];
 #pragma unroll
@@ -249,15 +250,33 @@ __global__ __launch_bounds__(kHT) void k2x_partition(const int32_t* __restrict__
     for (int i = lo; i < hi; ++i) {
         const uint32_t c = hist[i];
         off[i] = run;
-        C[(int64_t)i * g.nblk + blockIdx.x] = c;
-        O[(int64_t)i * g.nblk + blockIdx.x] = run;
+        C[(int64_t)i * g.nblk + blk] = c;
+        O[(int64_t)i * g.nblk + blk] = run;
         run += c;
     }
     __syncthreads();
-    uint32_t* reg = region + (int64_t)blockIdx.x * kXChunk;
+    uint32_t* reg = region + (int64_t)blk * kXChunk;
 #pragma unroll
     for (int u = 0; u < kXPer; ++u)
         if (bin[u] >= 0) reg[off[bin[u]] + pos[u]] = ent[u];
+}
+
+__global__ __launch_bounds__(kHT) void k2x_partition(const int32_t* __restrict__ bnode,
+                                                     const int64_t* __restrict__ bts, int64_t B, int64_t N,
+                                                     HotCutoffs cut, HotPart g, uint32_t* __restrict__ C,
+                                                     uint32_t* __restrict__ O, uint32_t* __restrict__ region) {
+    k2x_body((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, C, O, region);
+}
+
+// K2x and the step path's pod preparation (K3p) in one launch: the two are
+// independent, so the pod tiles ride as extra workgroups behind the
+// partition's (one kernel boundary fewer per scheduling step).
+__global__ __launch_bounds__(kHT) void k2x_pods(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
+                                                int64_t B, int64_t N, HotCutoffs cut, HotPart g,
+                                                uint32_t* __restrict__ C, uint32_t* __restrict__ O,
+                                                uint32_t* __restrict__ region, PodPrep pp) {
+    if ((int32_t)blockIdx.x < g.nblk) k2x_body((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, C, O, region);
+    else k3p_tile256((int64_t)blockIdx.x - g.nblk, pp);
 }
 
 __global__ __launch_bounds__(kHT) void k2y_bin_hist(const uint32_t* __restrict__ region,
@@ -358,14 +377,17 @@ size_t hot_part_scratch(const HotPart& g) { return (size_t)g.cap + 2 * (size_t)g
 
 hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                  const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* scratch,
-                                 hipStream_t st, int which) {
+                                 hipStream_t st, int which, const PodPrep* pods) {
     static const hipError_t attr =
         hipFuncSetAttribute((const void*)k2y_bin_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     if (attr != hipSuccess) return attr;
     uint32_t* region = scratch;
     uint32_t* C = scratch + g.cap;
     uint32_t* O = C + (size_t)g.nbins * g.nblk;
-    if (which & 1)
+    if ((which & 1) && pods && pods->P > 0)
+        hipLaunchKernelGGL(k2x_pods, dim3((unsigned)(g.nblk + pods->ntiles)), dim3(kHT), sizeof(uint32_t) * 2 * g.nbins,
+                           st, bnode, bts, B, N, cut, g, C, O, region, *pods);
+    else if (which & 1)
         hipLaunchKernelGGL(k2x_partition, dim3(g.nblk), dim3(kHT), sizeof(uint32_t) * 2 * g.nbins, st, bnode, bts, B,
                            N, cut, g, C, O, region);
     const size_t lds = sizeof(uint32_t) * ((size_t)cut.n_win * ((size_t)1 << g.bb) + 2 * (size_t)g.nblk + 1);

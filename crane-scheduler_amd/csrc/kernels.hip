@@ -261,6 +261,7 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     } else {
         __syncthreads();
     }
+    if (!out) return;  // keys-only step: the records are rebuilt when a matrix/greedy pass needs them
     const int64_t nvalid = min((int64_t)kK1Threads, N - first);
     const int64_t nvec = nvalid * (int64_t)sizeof(Rec) / 16;
     const uint4* src = reinterpret_cast<const uint4*>(smem);

@@ -86,9 +86,20 @@ struct HotPart {
 HotPart hot_part_geometry(int64_t B, int64_t N, int32_t W);
 size_t hot_part_scratch(const HotPart& g);  // uint32 entries: region + C + O
 // Adds into buckets[W][N], which must be zero on entry.  Scratch needs no initialisation.
+// The step path's pod preparation (K3p) for 1024-pod tiles, as it rides in K2x's launch.
+struct PodPrep {
+    const int64_t* now;
+    const uint8_t* flags;
+    int64_t P, ntiles;
+    int32_t* perm;
+    int64_t* pnow;
+    int64_t* tile_mm;
+    long long* keys;
+};
+// pods (optional, with which & 1): K3p's tiles run as extra workgroups of the K2x launch
 hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                  const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* scratch,
-                                 hipStream_t st, int which = 3);  // 1: k2x, 2: k2y
+                                 hipStream_t st, int which = 3, const PodPrep* pods = nullptr);  // 1: k2x, 2: k2y
 
 // K3 step path (step.hip): per-batch node step tables + pair eval.
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
@@ -168,7 +179,7 @@ struct K1Args {
     const int64_t* hv_ts;   // [N] or null
     uint32_t* buckets;      // [W][N] K2 window-rank buckets or null
     int64_t hv_ts_counts;   // stamp of binding-log hot values
-    void* out;              // NodeRec [N]
+    void* out;              // NodeRec [N], or null (keys-only step: records not kept)
     uint32_t* cnt_out;      // [W][N] per-window counts (greedy) or null
     double* hvc_out;        // [N] hot values from the buckets, or null
 };

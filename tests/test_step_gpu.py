@@ -179,15 +179,17 @@ def test_hot_values_kept_after_consumption():
     assert np.array_equal(ff, off) and np.array_equal(sc, osc)
 
 
-@pytest.mark.parametrize("overlap", ["0", "1"])
-def test_step_keys_async_matches_oracle(overlap, monkeypatch):
-    """crane_dyn_step_keys_async replayed (serial, and with K3p on the engine's second
-    queue overlapping K2): each step equals the oracle with binding-log hot values;
-    with stage profiling on (serial path) too."""
+@pytest.mark.parametrize("overlap,ride,pods", [("0", "1", 5000), ("0", "0", 5000), ("1", "1", 5000),
+                                               ("0", "1", 1), ("0", "1", 300), ("0", "1", 2048)])
+def test_step_keys_async_matches_oracle(overlap, ride, pods, monkeypatch):
+    """crane_dyn_step_keys_async replayed (serial with K3p riding in K2x's launch or in
+    its own, and with K3p on the engine's second queue overlapping K2): each step
+    equals the oracle with binding-log hot values; with stage profiling on too."""
     import torch
     monkeypatch.setenv("CRANE_STEP_OVERLAP", overlap)
+    monkeypatch.setenv("CRANE_K2X_PODS", ride)
     spec = cd.default_policy_spec()
-    c = synth.make_cluster(spec, 30000, 5000, n_bindings=300_000, seed=27, pod_step_ns=2_000_000, ds_frac=0.02)
+    c = synth.make_cluster(spec, 30000, pods, n_bindings=300_000, seed=27, pod_step_ns=2_000_000, ds_frac=0.02)
     eng = engine_for(spec, c)
     eng.upload_bindings(c.b_node, c.b_ts)
     now = int(synth.NOW0_NS)
@@ -205,4 +207,36 @@ def test_step_keys_async_matches_oracle(overlap, monkeypatch):
             ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
             assert np.array_equal(ch, och), rep
     names = [n for n, _ in eng.stage_times()]
-    assert names == ["k2x_partition", "k2y_bin_hist", "k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
+    if ride == "1":  # (stage profiling runs the serial path, overlap or not)
+        assert names == ["k2x_partition+k3p_pods", "k2y_bin_hist", "k1_node_pass+k3a_steps", "k3s_eval"], names
+    else:
+        assert names == ["k2x_partition", "k2y_bin_hist", "k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
+
+
+@pytest.mark.parametrize("keep", ["0", "1"])
+def test_records_rebuilt_after_keys_step(keep, monkeypatch):
+    """The fused keys-only step does not write the node records (CRANE_K1_KEEP_REC=1
+    does): a matrix eval and a greedy pass after it rebuild them from the kept
+    binding-log hot values and still equal the oracle."""
+    import torch
+    monkeypatch.setenv("CRANE_K1_KEEP_REC", keep)
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 4000, 700, n_bindings=50_000, seed=28, pod_step_ns=3_000_000, ds_frac=0.05)
+    eng = engine_for(spec, c)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    now = int(synth.NOW0_NS)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
+    off, osc, och = oracle_soa(spec, c, hv_override=_oracle_hv(spec, c, now))
+    with torch.cuda.stream(st):
+        eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
+        st.synchronize()
+    ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
+    assert np.array_equal(ch, och)
+    ff, sc, ch2, _ = eng.eval(c.now, c.ds, matrix=True)
+    assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch2, och)
+    _, _, ch3, _ = eng.eval(c.now, c.ds)  # keys-only again, records clean now
+    assert np.array_equal(ch3, och)
