@@ -37,6 +37,8 @@ STAGE_KERNEL = {
     "k1_node_pass": ("crane::k1_node_pass<", "false>"),
     "k2x_partition": ("crane::k2x_partition", ""),
     "k2x_partition+k3p_pods": ("crane::k2x_pods", ""),
+    "k2x_dedupe+k3p_pods": ("crane::k2x_dedupe_pods", ""),
+    "k2x_dedupe": ("crane::k2x_dedupe(", ""),
     "k2y_bin_hist": ("crane::k2y_bin_hist", ""),
     "k3p_pods": ("crane::k3p_pods", ""),
 }
@@ -176,13 +178,29 @@ def main():
     keep_rec = os.environ.get("CRANE_K1_KEEP_REC") == "1"
     k2x_b = B * 12 + b_in * 4
     k3p_b = P * (8 + 1 + 4 + 8 + 8)
+    # dedupe-form K2: one 4-byte entry per distinct (2048-binding region, node, window rank),
+    # a (count, offset) pair per (node block, region); the node pass reads both
+    dedupe = os.environ.get("CRANE_K2", "dedupe") == "dedupe"
+    cut = np.sort(np.array([now_sync // 10**9 - tr // 10**9 for tr, _ in spec["hotValue"]], np.int64))
+    jr = (c.b_ts[:, None] > cut[None, :]).sum(1)
+    okb = (jr > 0) & (c.b_node >= 0) & (c.b_node < N)
+    reg = np.arange(B, dtype=np.int64) // 2048
+    E = int(np.unique((reg[okb] * (N + 1) + c.b_node[okb]) * 8 + jr[okb] - 1).size) if B else 0
+    k1_bs = int(os.environ.get("CRANE_K1_THREADS", "128"))
+    co_b = 8 * (-(-N // k1_bs)) * (-(-B // 2048))
+    k2d_b = B * 12 + E * 4 + co_b
     alg = {
+        "k2x_dedupe": (k2d_b, "bindings read + distinct (region, node, bucket) entries + count/offset written"),
+        "k2x_dedupe+k3p_pods": (k2d_b + k3p_b, "bindings read + distinct entries + count/offset written; pod now + "
+                                               "flag read, partition + keys written"),
         "k2x_partition": (k2x_b, "bindings read (int32 node + int64 ts) + kept entries written"),
         "k2x_partition+k3p_pods": (k2x_b + k3p_b, "bindings read + kept entries written; pod now + flag read, "
                                                   "partition + keys written"),
         "k2y_bin_hist": (b_in * 4 + 4 * W * N, "kept entries read + window counts added"),
-        "k1_node_pass+k3a_steps": (N * (16 * M + 8 * W + 8 + (rec_bytes if keep_rec else 0)),
-                                   "SoA (value, ts) read + buckets read and zeroed + hot value written"
+        "k1_node_pass+k3a_steps": ((N * (16 * M + 8 + (rec_bytes if keep_rec else 0))
+                                    + (E * 4 + co_b if dedupe else N * 8 * W)),
+                                   "SoA (value, ts) read + hot value written + "
+                                   + ("K2 entries and count/offset read" if dedupe else "buckets read and zeroed")
                                    + (" + NodeRec written" if keep_rec else "")),
         "k1_node_pass": (N * (16 * M + 8 * W + rec_bytes + 8), "SoA + buckets + NodeRec + hot value"),
         "k3p_pods": (k3p_b, "pod now + flag read, partition + keys written"),

@@ -88,6 +88,8 @@ struct crane_dyn {
     bool rec_dirty = true;
     bool buckets_zero = false;  // K1 consumes (zeroes) the buckets K2 filled
     bool counts_pending = false;  // buckets hold K2 counts no node pass has consumed yet
+    bool hx_pending = false;      // ... in the dedupe form: per-block entries in k2_sorted (hx_g)
+    HotPart hx_g{};
     int64_t B = 0;
     DevBuf<double> val, hv;
     DevBuf<int64_t> ts, hv_ts;
@@ -399,7 +401,24 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     if (nb > h->buckets.n) h->buckets_zero = false;
     HIPTRY(h, h->buckets.reserve(nb));
     const char* k2e = getenv("CRANE_K2");
-    const std::string mode = k2e ? k2e : "part";
+    const std::string mode = k2e ? k2e : "dedupe";
+    h->hx_pending = false;
+    const HotPart gx = hot_dedupe_geometry(h->B, h->N, dp.n_win, k1_threads());
+    if (mode == "dedupe" && gx.ok) {
+        // one launch (+ K3p); the node pass counts its own block's entries (no buckets)
+        HIPTRY(h, h->k2_sorted.reserve(hot_part_scratch(gx)));
+        HIPTRY(h, prof_begin(h, st));
+        HIPTRY(h, launch_hot_count_dedupe(h->bnode.p, h->bts.p, h->B, h->N, cut, gx, h->k2_sorted.p, st, pods));
+        HIPTRY(h, prof_mark(h, st, pods ? "k2x_dedupe+k3p_pods" : "k2x_dedupe"));
+        if (pods_done) *pods_done = pods != nullptr;
+        h->hx_g = gx;
+        h->hx_pending = true;
+        h->counts_pending = true;
+        h->hv_from_counts = true;
+        h->hv_ts_counts = hv_ts_ns;
+        h->rec_dirty = true;
+        return CRANE_OK;
+    }
     const HotPart gp = hot_part_geometry(h->B, h->N, dp.n_win);
     if (mode == "part" && gp.ok) {
         // two kernels adding into zeroed buckets (K1 zeroes what it consumed)
@@ -443,6 +462,11 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     return CRANE_OK;
 }
 
+// K1's workgroup size: the dedupe-form K2 bins nodes by it
+static int k1_bs(const crane_dyn* h) {
+    return h->hv_from_counts && h->counts_pending && h->hx_pending ? 1 << h->hx_g.bb : k1_threads();
+}
+
 // K1 (optionally with the K3 step tables fused in).  Hot values: pending K2
 // counts (consumed), else the values the last consuming pass kept, else the
 // uploaded annotation.
@@ -464,7 +488,15 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
     if (cnt_out && !consume) return h->fail(CRANE_E_STATE, "per-window counts need a hot-value refresh first");
     if (consume) {
         HIPTRY(h, h->hvc.reserve((size_t)std::max<int64_t>(h->N, 1)));
-        a.buckets = h->buckets.p;
+        if (h->hx_pending) {
+            const HotPart& g = h->hx_g;
+            a.hx_region = h->k2_sorted.p;
+            a.hx_C = h->k2_sorted.p + g.cap;
+            a.hx_O = a.hx_C + (size_t)g.nbins * g.nblk;
+            a.hx_nblk = g.nblk;
+        } else {
+            a.buckets = h->buckets.p;
+        }
         a.cnt_out = cnt_out;
         a.hvc_out = h->hvc.p;
     } else if (h->hv_from_counts) {
@@ -473,12 +505,14 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
         a.hv = h->hv.p;
         a.hv_ts = h->hv_ts.p;
     }
+    a.threads = k1_bs(h);
     HIPTRY(h, prof_begin(h, st));
     HIPTRY(h, launch_node_pass(h->shape, a, st, step));
     HIPTRY(h, prof_mark(h, st, step ? "k1_node_pass+k3a_steps" : "k1_node_pass"));
     if (consume) {
-        h->buckets_zero = true;  // K1 zeroed what it read
+        if (!h->hx_pending) h->buckets_zero = true;  // K1 zeroed what it read
         h->counts_pending = false;
+        h->hx_pending = false;
     }
     h->rec_dirty = !keep;
     return CRANE_OK;
@@ -498,7 +532,7 @@ static bool step_path_ok(const crane_dyn* h, int64_t P) {
 static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     const char* fe = getenv("CRANE_K1_FUSE");
     sp.fuse = h->rec_dirty && !(fe && fe[0] == '0');
-    const int32_t bs = sp.fuse ? k1_threads() : kStepSeg;  // producer workgroup size
+    const int32_t bs = sp.fuse ? k1_bs(h) : kStepSeg;  // producer workgroup size
     const int32_t nblk = (int32_t)((h->N + bs - 1) / bs);
     sp.g = step_geometry(P, h->N, nblk);
     const StepGeometry& g = sp.g;

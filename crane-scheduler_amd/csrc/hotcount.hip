@@ -172,6 +172,7 @@ __global__ __launch_bounds__(kHT) void k2d_bin_hist(const uint32_t* __restrict__
 constexpr int kXPer = 8;     // bindings per thread in X (16 measured slower: fewer workgroups in flight)
 constexpr int kYPer = 8;     // entries per thread and batch in Y
 constexpr int kXChunk = kHT * kXPer;
+static_assert(kXChunk == kHxRegion, "K1 reads the dedupe regions with this stride");
 constexpr int kYSplits = 16;  // workgroups per bin in Y (Zipf-hot bins want many, each pays a prologue)
 
 // LDS atomicAdd of `add` to a[key] for every active lane, the lanes sharing the
@@ -354,6 +355,178 @@ __global__ __launch_bounds__(kHT) void k2y_bin_hist(const uint32_t* __restrict__
             const uint32_t c = hist[w * binw + i];
             if (c && n0 + i < N) atomicAdd(&buckets[(int64_t)w * N + n0 + i], c);
         }
+}
+
+// ---------------------------------------------------------------- dedupe form
+// X' partition_dedupe : as X, but each workgroup first aggregates its 2048
+//                bindings per (node, bucket) in an LDS hash table and writes one
+//                entry per distinct pair: local node | bucket << 16 | count << 19.
+//                Bins are the node pass's producer blocks (2^bb = K1's
+//                workgroup size), so there is no Y: the node pass (kernels.hip,
+//                K1Args::hx_*) counts its own block's entries into LDS.
+// Aggregation bounds a Zipf-hot node to one entry per source region, so every
+// bin's entry list stays short (the partitioned form needs 16 Y workgroups per
+// bin for the hottest bins instead).
+constexpr int kDSlots = 4096;  // 2 slots per binding: an empty or matching slot always exists
+
+// Adds `add` to key's count; a lane that inserts a new key also counts it in its
+// bin and returns its slot (else -1).
+__device__ __forceinline__ int32_t hash_add(int32_t* hkey, uint32_t* hcnt, uint32_t* hist, int bb, int32_t key,
+                                            uint32_t add) {
+    uint32_t h = ((uint32_t)key * 2654435761u) >> (32 - 12);
+    for (;;) {  // ends: <= 2048 distinct keys in 4096 slots
+        int32_t k = __hip_atomic_load(&hkey[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (k == -1) {
+            const int32_t old = atomicCAS(&hkey[h], -1, key);
+            if (old == -1) {
+                atomicAdd(&hcnt[h], add);
+                atomicAdd(&hist[(key >> 3) >> bb], 1u);
+                return (int32_t)h;
+            }
+            k = old;
+        }
+        if (k == key) {
+            atomicAdd(&hcnt[h], add);
+            return -1;
+        }
+        h = (h + 1) & (kDSlots - 1);
+    }
+}
+
+__device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __restrict__ bnode,
+                                         const int64_t* __restrict__ bts, int64_t B, int64_t N, const HotCutoffs& cut,
+                                         const HotPart& g, uint32_t* __restrict__ C, uint32_t* __restrict__ O,
+                                         uint32_t* __restrict__ region) {
+    // hkey, hcnt [kDSlots], hist, off [nbins], uniq u16 [kXChunk]
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+    __shared__ uint32_t part[kHT];
+    __shared__ uint32_t nuniq;
+    int32_t* hkey = reinterpret_cast<int32_t*>(sh);
+    uint32_t* hcnt = sh + kDSlots;
+    uint32_t* hist = hcnt + kDSlots;
+    uint32_t* off = hist + g.nbins;
+    uint16_t* uniq = reinterpret_cast<uint16_t*>(off + g.nbins);
+    const int64_t b0 = (int64_t)blk * kXChunk + threadIdx.x;
+    int32_t nd[kXPer];
+    int64_t ts[kXPer];
+#pragma unroll
+    for (int u = 0; u < kXPer; ++u) {
+        const int64_t b = b0 + u * kHT;
+        nd[u] = b < B ? bnode[b] : -1;
+        ts[u] = b < B ? bts[b] : INT64_MIN;
+    }
+    for (int i = threadIdx.x; i < kDSlots; i += kHT) {
+        hkey[i] = -1;
+        hcnt[i] = 0;
+    }
+    for (int i = threadIdx.x; i < g.nbins; i += kHT) hist[i] = 0;
+    if (threadIdx.x == 0) nuniq = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int u = 0; u < kXPer; ++u) {
+        const int j = window_rank(ts[u], cut);
+        const bool ok = nd[u] >= 0 && (int64_t)nd[u] < N && j > 0;  // binding.go:85-91
+        const int32_t key = ok ? nd[u] * 8 + (j - 1) : -1;
+        // the lanes sharing the first active lane's key add once
+        const uint64_t am = __ballot(ok);
+        if (am == 0) continue;
+        const int lead = __ffsll((long long)am) - 1;
+        const int32_t kl = __shfl(key, lead);
+        const uint64_t m = __ballot(ok && key == kl);
+        // (kl, count) rides on the lead lane; every other lane adds its own key once
+        const bool mine = lane == lead || (ok && key != kl);
+        const int32_t slot =
+            mine ? hash_add(hkey, hcnt, hist, g.bb, lane == lead ? kl : key, lane == lead ? (uint32_t)__popcll(m) : 1u)
+                 : -1;
+        // new keys: one append per wave to the distinct-key list
+        const uint64_t nm = __ballot(slot >= 0);
+        if (nm) {
+            const int l0 = __ffsll((long long)nm) - 1;
+            uint32_t base = 0;
+            if (lane == l0) base = atomicAdd(&nuniq, (uint32_t)__popcll(nm));
+            base = __shfl(base, l0);
+            if (slot >= 0) uniq[base + __popcll(nm & ((1ull << lane) - 1ull))] = (uint16_t)slot;
+        }
+    }
+    __syncthreads();
+    const int per = (g.nbins + kHT - 1) / kHT;
+    const int lo = min(g.nbins, (int)threadIdx.x * per), hi = min(g.nbins, lo + per);
+    uint32_t sum = 0;
+    for (int i = lo; i < hi; ++i) sum += hist[i];
+    uint32_t run = wg_excl_scan_u32(sum, part);
+    for (int i = lo; i < hi; ++i) {
+        const uint32_t c = hist[i];
+        off[i] = run;
+        C[(int64_t)i * g.nblk + blk] = c;
+        O[(int64_t)i * g.nblk + blk] = run;
+        run += c;
+    }
+    __syncthreads();
+    uint32_t* reg = region + (int64_t)blk * kXChunk;
+    const uint32_t mask = (1u << g.bb) - 1;
+    const uint32_t nu = nuniq;
+    for (uint32_t i = threadIdx.x; i < nu; i += kHT) {
+        const int s = uniq[i];
+        const int32_t k = hkey[s];
+        const uint32_t p = atomicAdd(&off[(k >> 3) >> g.bb], 1u);
+        reg[p] = ((uint32_t)(k >> 3) & mask) | ((uint32_t)(k & 7) << 16) | (hcnt[s] << 19);
+    }
+}
+
+__global__ __launch_bounds__(kHT) void k2x_dedupe(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
+                                                  int64_t B, int64_t N, HotCutoffs cut, HotPart g,
+                                                  uint32_t* __restrict__ C, uint32_t* __restrict__ O,
+                                                  uint32_t* __restrict__ region) {
+    k2d_body((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, C, O, region);
+}
+
+__global__ __launch_bounds__(kHT) void k2x_dedupe_pods(const int32_t* __restrict__ bnode,
+                                                       const int64_t* __restrict__ bts, int64_t B, int64_t N,
+                                                       HotCutoffs cut, HotPart g, uint32_t* __restrict__ C,
+                                                       uint32_t* __restrict__ O, uint32_t* __restrict__ region,
+                                                       PodPrep pp) {
+    if ((int32_t)blockIdx.x < g.nblk) k2d_body((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, C, O, region);
+    else k3p_tile256((int64_t)blockIdx.x - g.nblk, pp);
+}
+
+HotPart hot_dedupe_geometry(int64_t B, int64_t N, int32_t W, int32_t bs) {
+    HotPart g{};
+    int bb = 0;
+    while ((1 << bb) < bs) ++bb;
+    g.bb = bb;
+    g.nbins = (int32_t)((N + bs - 1) / bs);
+    g.nblk = (int32_t)((B + kXChunk - 1) / kXChunk);
+    g.cap = (int64_t)g.nblk * kXChunk;
+    // key nd*8+bucket in int32; hash + bin LDS <= 96 KiB; count/offset matrices <= 2^22 entries
+    g.ok = N > 0 && B > 0 && (1 << bb) == bs && bb <= 16 && W >= 1 && W <= kMaxWin && N < (1LL << 27) &&
+           g.nbins <= 8192 && (double)g.nbins * (double)g.nblk <= (double)(1 << 22);
+    return g;
+}
+
+hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
+                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
+                                   const PodPrep* pods) {
+    static const hipError_t attr = [] {
+        hipError_t e = hipFuncSetAttribute((const void*)k2x_dedupe, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           100 * 1024);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)k2x_dedupe_pods, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    100 * 1024);
+        return e;
+    }();
+    if (attr != hipSuccess) return attr;
+    uint32_t* region = scratch;
+    uint32_t* C = scratch + g.cap;
+    uint32_t* O = C + (size_t)g.nbins * g.nblk;
+    const size_t lds = sizeof(uint32_t) * (2 * (size_t)kDSlots + 2 * (size_t)g.nbins) + sizeof(uint16_t) * kXChunk;
+    if (pods && pods->P > 0)
+        hipLaunchKernelGGL(k2x_dedupe_pods, dim3((unsigned)(g.nblk + pods->ntiles)), dim3(kHT), lds, st, bnode, bts,
+                           B, N, cut, g, C, O, region, *pods);
+    else
+        hipLaunchKernelGGL(k2x_dedupe, dim3((unsigned)g.nblk), dim3(kHT), lds, st, bnode, bts, B, N, cut, g, C, O,
+                           region);
+    return hipGetLastError();
 }
 
 HotPart hot_part_geometry(int64_t B, int64_t N, int32_t W) {

@@ -132,6 +132,8 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     __shared__ StepShared ssh;
     int64_t tmin = 0, tmax = 0, pmn = 0, pmx = 0;
     if (STEP && threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+    __shared__ uint32_t hxh[kMaxWin][kK1Threads];  // dedupe-form K2: this block's window-rank buckets
+    const bool hx = a.hx_region != nullptr;
     StepSlots so;
     Rec r;
     int64_t pt[PD], qt[PR];
@@ -170,10 +172,49 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
 #pragma unroll
             for (int b = 0; b < kMaxWin; ++b) bc[b] = b < pol.n_win ? buckets[(int64_t)b * N + n] : 0u;
         }
-        if (!buckets && hv) {
+        if (!buckets && !hx && hv) {
             hvl = hv[n];
             hvt = hv_ts ? hv_ts[n] : hv_ts_counts;  // null: the binding-log value of an earlier pass
         }
+    }
+    if (hx) {
+        // this block's (node, bucket, count) entries from every K2 source region
+        // (dedupe form): C/O of up to kHxPer regions per lane, then their first
+        // kHxFirst entries, all loads in flight together; longer runs loop
+        constexpr int kHxPer = 4, kHxFirst = 4;
+        for (int b = 0; b < kMaxWin; ++b) hxh[b][threadIdx.x] = 0;
+        __syncthreads();
+        const int64_t row = (int64_t)blockIdx.x * a.hx_nblk;
+        for (int i0 = 0; i0 < a.hx_nblk; i0 += kK1Threads * kHxPer) {
+            uint32_t c[kHxPer], o[kHxPer];
+#pragma unroll
+            for (int u = 0; u < kHxPer; ++u) {
+                const int i = i0 + u * kK1Threads + threadIdx.x;
+                c[u] = i < a.hx_nblk ? a.hx_C[row + i] : 0u;
+                o[u] = i < a.hx_nblk ? a.hx_O[row + i] : 0u;
+            }
+            uint32_t v[kHxPer][kHxFirst];
+#pragma unroll
+            for (int u = 0; u < kHxPer; ++u) {
+                const uint32_t* src = a.hx_region + (int64_t)(i0 + u * kK1Threads + threadIdx.x) * kHxRegion + o[u];
+#pragma unroll
+                for (int k = 0; k < kHxFirst; ++k) v[u][k] = (uint32_t)k < c[u] ? src[k] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kHxPer; ++u) {
+#pragma unroll
+                for (int k = 0; k < kHxFirst; ++k)
+                    if ((uint32_t)k < c[u]) atomicAdd(&hxh[(v[u][k] >> 16) & 7][v[u][k] & 0xFFFF], v[u][k] >> 19);
+                const uint32_t* src = a.hx_region + (int64_t)(i0 + u * kK1Threads + threadIdx.x) * kHxRegion + o[u];
+                for (uint32_t k = kHxFirst; k < c[u]; ++k) {
+                    const uint32_t w = src[k];
+                    atomicAdd(&hxh[(w >> 16) & 7][w & 0xFFFF], w >> 19);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < kMaxWin; ++b) bc[b] = b < pol.n_win ? hxh[b][threadIdx.x] : 0u;
     }
     // the batch time range partials: issued after the SoA loads, reduced after the compute
     if (STEP) batch_range_load<kK1Threads>(step.tile_mm, step.ntiles, pmn, pmx);
@@ -208,12 +249,14 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
             r.e_prio[k] = e;
             r.t[k] = term;
         }
-        if (buckets) {
+        if (buckets || hx) {
             // annotateNodeHotValue (node.go:113-121): value += count / p.Count (Go int division)
             // window w counts the bindings of buckets >= its cutoff rank (K2)
+            if (buckets) {
 #pragma unroll
-            for (int b = 0; b < kMaxWin; ++b)  // consumed: leaves the buckets zeroed for the next K2
-                if (b < pol.n_win) buckets[(int64_t)b * N + n] = 0;
+                for (int b = 0; b < kMaxWin; ++b)  // consumed: leaves the buckets zeroed for the next K2
+                    if (b < pol.n_win) buckets[(int64_t)b * N + n] = 0;
+            }
             int64_t v = 0;
 #pragma unroll
             for (int w = 0; w < kMaxWin; ++w) {
@@ -456,7 +499,8 @@ int k1_threads() {
 template <int PD, int PR>
 static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t st) {
     if (a.N <= 0) return hipSuccess;
-    const int T = k1_threads();
+    const int T = a.threads ? a.threads : k1_threads();
+    if (T != 128 && T != 256) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((a.N + T - 1) / T);
     const size_t lds = sizeof(NodeRec<PD, PR>) * T;
     const K1Step sa = step ? *step : K1Step{};

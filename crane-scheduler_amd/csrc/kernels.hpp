@@ -96,6 +96,13 @@ struct PodPrep {
     int64_t* tile_mm;
     long long* keys;
 };
+// Dedupe form: one launch (K2x' [+ K3p]); bins = the node pass's workgroups (bs
+// nodes), consumed by K1 through K1Args::hx_*.  Region stride kHxRegion entries.
+constexpr int kHxRegion = 2048;
+HotPart hot_dedupe_geometry(int64_t B, int64_t N, int32_t W, int32_t bs);
+hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
+                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
+                                   const PodPrep* pods = nullptr);
 // pods (optional, with which & 1): K3p's tiles run as extra workgroups of the K2x launch
 hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                  const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* scratch,
@@ -182,6 +189,13 @@ struct K1Args {
     void* out;              // NodeRec [N], or null (keys-only step: records not kept)
     uint32_t* cnt_out;      // [W][N] per-window counts (greedy) or null
     double* hvc_out;        // [N] hot values from the buckets, or null
+    // dedupe-form K2 output (instead of buckets): per K1 workgroup b, region r holds
+    // hx_C[b*hx_nblk + r] entries at hx_region[r*kHxRegion + hx_O[b*hx_nblk + r]]
+    const uint32_t* hx_region;
+    const uint32_t* hx_C;
+    const uint32_t* hx_O;
+    int32_t hx_nblk;
+    int32_t threads;        // workgroup size (0: k1_threads())
 };
 // step (optional): also build the K3 step tables of a pod batch (K3a fused).
 hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr);

@@ -143,7 +143,7 @@ def test_hot_values_vs_oracle(kats):
     assert sc[0, 0] == 50  # hv = 5 (SURVEY KAT-11)
 
 
-@pytest.mark.parametrize("k2", ["part", "binned", "hash"])
+@pytest.mark.parametrize("k2", ["dedupe", "part", "binned", "hash"])
 @pytest.mark.parametrize("n_nodes,n_bind,seed", [(1000, 50_000, 1), (20_000, 300_000, 2), (100, 10, 3),
                                                  (70_000, 2_000_000, 4)])
 def test_hot_values_random(n_nodes, n_bind, seed, k2, monkeypatch):
@@ -162,6 +162,43 @@ def test_hot_values_random(n_nodes, n_bind, seed, k2, monkeypatch):
     ff, sc, ch, _ = eng.eval(c.now, c.ds, matrix=True)
     off, osc, och = oracle_soa(spec, c, hv_override=(cnt_hv.astype(np.float64), np.full(n_nodes, now, np.int64)))
     assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch, och)
+
+
+@pytest.mark.parametrize("threads", ["128", "256"])
+@pytest.mark.parametrize("case", ["one_hot_node", "eight_windows", "last_node"])
+def test_hot_values_dedupe_edges(case, threads, monkeypatch):
+    """Dedupe-form K2 (per-workgroup (node, bucket) aggregation, counts read by the
+    node pass) at its packing limits: a region whose 2048 bindings all hit one node
+    (count field), eight windows (bucket field), the shard's last node and bindings
+    past the shard; 128- and 256-node bins."""
+    monkeypatch.setenv("CRANE_K2", "dedupe")
+    monkeypatch.setenv("CRANE_K1_THREADS", threads)
+    m = 60 * 10**9
+    spec = cd.default_policy_spec()
+    n_nodes, n_bind = 5000, 200_000
+    if case == "eight_windows":
+        spec["hotValue"] = [(k * 40 * 10**9, c) for k, c in zip(range(1, 9), [1, 2, 3, 5, 7, 11, 13, 1])]
+    c = synth.make_cluster(spec, n_nodes, 64, n_bindings=n_bind, seed=31, pod_step_ns=5_000_000_000)
+    bn = c.b_node.copy()
+    if case == "one_hot_node":
+        bn[: 3 * 2048 + 5] = 4321  # whole source regions on one node
+        bn[-4096:] = 17
+    if case == "last_node":
+        bn[::3] = n_nodes - 1
+        bn[1::7] = n_nodes  # past the shard: ignored
+        bn[2::11] = -3
+    eng = engine_for(spec, c)
+    eng.upload_bindings(bn, c.b_ts)
+    now = int(c.now[0])
+    for rep in range(2):  # a second refresh after the first was consumed
+        eng.refresh_hot_values(now, now)
+        _, cnt_hv = O.hot_values(spec, bn, c.b_ts, n_nodes, now // 10**9)
+        ff, sc, ch, _ = eng.eval(c.now, c.ds, matrix=True)
+        off, osc, och = oracle_soa(spec, c, hv_override=(cnt_hv.astype(np.float64),
+                                                         np.full(n_nodes, now, np.int64)))
+        assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch, och), rep
+    eng.refresh_hot_values(now, now)  # read back before any node pass consumed it
+    assert np.array_equal(eng.hot_values(), cnt_hv.astype(np.float64))
 
 
 def test_division_exactness_sweep(k3_variant):

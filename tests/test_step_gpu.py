@@ -208,9 +208,34 @@ def test_step_keys_async_matches_oracle(overlap, ride, pods, monkeypatch):
             assert np.array_equal(ch, och), rep
     names = [n for n, _ in eng.stage_times()]
     if ride == "1":  # (stage profiling runs the serial path, overlap or not)
-        assert names == ["k2x_partition+k3p_pods", "k2y_bin_hist", "k1_node_pass+k3a_steps", "k3s_eval"], names
+        assert names == ["k2x_dedupe+k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
     else:
-        assert names == ["k2x_partition", "k2y_bin_hist", "k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
+        assert names == ["k2x_dedupe", "k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
+
+
+@pytest.mark.parametrize("k2", ["dedupe", "part", "binned"])
+def test_step_keys_async_k2_forms(k2, monkeypatch):
+    """The combined step with each K2 form (dedupe: counts consumed by the fused node
+    pass from per-block entries; part / binned: buckets) equals the oracle, replayed."""
+    import torch
+    monkeypatch.setenv("CRANE_K2", k2)
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 20000, 3000, n_bindings=400_000, seed=29, pod_step_ns=2_000_000, ds_frac=0.03)
+    eng = engine_for(spec, c)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    now = int(synth.NOW0_NS)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
+    _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=_oracle_hv(spec, c, now))
+    with torch.cuda.stream(st):
+        for rep in range(3):
+            eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
+            st.synchronize()
+            ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
+            assert np.array_equal(ch, och), rep
 
 
 @pytest.mark.parametrize("keep", ["0", "1"])
