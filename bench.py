@@ -31,17 +31,24 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
-# engine stage name -> (kernel name prefix, suffix) in the rocprofv3 summary
+# engine stage name -> kernel name in the rocprofv3 PMC summary (templates: prefix + suffix)
 STAGE_KERNEL = {
     "k1_node_pass+k3a_steps": ("crane::k1_node_pass<", "true>"),
     "k1_node_pass": ("crane::k1_node_pass<", "false>"),
-    "k2x_partition": ("crane::k2x_partition", ""),
-    "k2x_partition+k3p_pods": ("crane::k2x_pods", ""),
-    "k2x_dedupe+k3p_pods": ("crane::k2x_dedupe_pods", ""),
-    "k2x_dedupe": ("crane::k2x_dedupe(", ""),
-    "k2y_bin_hist": ("crane::k2y_bin_hist", ""),
-    "k3p_pods": ("crane::k3p_pods", ""),
+    "k2x_partition": ("crane::k2x_partition", None),
+    "k2x_partition+k3p_pods": ("crane::k2x_pods", None),
+    "k2x_dedupe+k3p_pods": ("crane::k2x_dedupe_pods", None),
+    "k2x_dedupe": ("crane::k2x_dedupe", None),
+    "k2y_bin_hist": ("crane::k2y_bin_hist", None),
+    "k3p_pods": ("crane::k3p_pods", None),
 }
+
+
+def _stage_match(name, kernel):
+    pre, suf = STAGE_KERNEL.get(name, (None, None))
+    if pre is None:
+        return False
+    return kernel == pre if suf is None else kernel.startswith(pre) and kernel.endswith(suf)
 
 
 def parse():
@@ -186,7 +193,7 @@ def main():
     okb = (jr > 0) & (c.b_node >= 0) & (c.b_node < N)
     reg = np.arange(B, dtype=np.int64) // 2048
     E = int(np.unique((reg[okb] * (N + 1) + c.b_node[okb]) * 8 + jr[okb] - 1).size) if B else 0
-    k1_bs = int(os.environ.get("CRANE_K1_THREADS", "128"))
+    k1_bs = int(os.environ.get("CRANE_K1_THREADS", "256"))
     co_b = 8 * (-(-N // k1_bs)) * (-(-B // 2048))
     k2d_b = B * 12 + E * 4 + co_b
     alg = {
@@ -219,8 +226,7 @@ def main():
     if os.path.exists(PMC_SUMMARY):
         pmc = json.load(open(PMC_SUMMARY))
     for name, e in roofs.items():
-        pre, suf = STAGE_KERNEL.get(name, (None, ""))
-        hits = [v for k, v in pmc.items() if pre and k.startswith(pre) and k.endswith(suf) and "traffic_bytes" in v]
+        hits = [v for k, v in pmc.items() if _stage_match(name, k) and "traffic_bytes" in v]
         e["traffic"] = int(hits[0]["traffic_bytes"]) if hits else None
     roof = None
     if dom in roofs:

@@ -491,8 +491,7 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
         if (h->hx_pending) {
             const HotPart& g = h->hx_g;
             a.hx_region = h->k2_sorted.p;
-            a.hx_C = h->k2_sorted.p + g.cap;
-            a.hx_O = a.hx_C + (size_t)g.nbins * g.nblk;
+            a.hx_CO = h->k2_sorted.p + g.cap;
             a.hx_nblk = g.nblk;
         } else {
             a.buckets = h->buckets.p;

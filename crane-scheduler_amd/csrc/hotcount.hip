@@ -395,8 +395,7 @@ __device__ __forceinline__ int32_t hash_add(int32_t* hkey, uint32_t* hcnt, uint3
 
 __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __restrict__ bnode,
                                          const int64_t* __restrict__ bts, int64_t B, int64_t N, const HotCutoffs& cut,
-                                         const HotPart& g, uint32_t* __restrict__ C, uint32_t* __restrict__ O,
-                                         uint32_t* __restrict__ region) {
+                                         const HotPart& g, uint32_t* __restrict__ CO, uint32_t* __restrict__ region) {
     // hkey, hcnt [kDSlots], hist, off [nbins], uniq u16 [kXChunk]
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     __shared__ uint32_t part[kHT];
@@ -458,10 +457,11 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     for (int i = lo; i < hi; ++i) {
         const uint32_t c = hist[i];
         off[i] = run;
-        C[(int64_t)i * g.nblk + blk] = c;
-        O[(int64_t)i * g.nblk + blk] = run;
         run += c;
     }
+    __syncthreads();
+    // this region's row of (count | offset << 16) per node block: coalesced
+    for (int i = threadIdx.x; i < g.nbins; i += kHT) CO[(int64_t)blk * g.nbins + i] = hist[i] | (off[i] << 16);
     __syncthreads();
     uint32_t* reg = region + (int64_t)blk * kXChunk;
     const uint32_t mask = (1u << g.bb) - 1;
@@ -476,17 +476,15 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
 
 __global__ __launch_bounds__(kHT) void k2x_dedupe(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
                                                   int64_t B, int64_t N, HotCutoffs cut, HotPart g,
-                                                  uint32_t* __restrict__ C, uint32_t* __restrict__ O,
-                                                  uint32_t* __restrict__ region) {
-    k2d_body((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, C, O, region);
+                                                  uint32_t* __restrict__ CO, uint32_t* __restrict__ region) {
+    k2d_body((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
 }
 
 __global__ __launch_bounds__(kHT) void k2x_dedupe_pods(const int32_t* __restrict__ bnode,
                                                        const int64_t* __restrict__ bts, int64_t B, int64_t N,
-                                                       HotCutoffs cut, HotPart g, uint32_t* __restrict__ C,
-                                                       uint32_t* __restrict__ O, uint32_t* __restrict__ region,
-                                                       PodPrep pp) {
-    if ((int32_t)blockIdx.x < g.nblk) k2d_body((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, C, O, region);
+                                                       HotCutoffs cut, HotPart g, uint32_t* __restrict__ CO,
+                                                       uint32_t* __restrict__ region, PodPrep pp) {
+    if ((int32_t)blockIdx.x < g.nblk) k2d_body((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
     else k3p_tile256((int64_t)blockIdx.x - g.nblk, pp);
 }
 
@@ -517,14 +515,13 @@ hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int
     }();
     if (attr != hipSuccess) return attr;
     uint32_t* region = scratch;
-    uint32_t* C = scratch + g.cap;
-    uint32_t* O = C + (size_t)g.nbins * g.nblk;
+    uint32_t* CO = scratch + g.cap;  // [nblk][nbins]
     const size_t lds = sizeof(uint32_t) * (2 * (size_t)kDSlots + 2 * (size_t)g.nbins) + sizeof(uint16_t) * kXChunk;
     if (pods && pods->P > 0)
         hipLaunchKernelGGL(k2x_dedupe_pods, dim3((unsigned)(g.nblk + pods->ntiles)), dim3(kHT), lds, st, bnode, bts,
-                           B, N, cut, g, C, O, region, *pods);
+                           B, N, cut, g, CO, region, *pods);
     else
-        hipLaunchKernelGGL(k2x_dedupe, dim3((unsigned)g.nblk), dim3(kHT), lds, st, bnode, bts, B, N, cut, g, C, O,
+        hipLaunchKernelGGL(k2x_dedupe, dim3((unsigned)g.nblk), dim3(kHT), lds, st, bnode, bts, B, N, cut, g, CO,
                            region);
     return hipGetLastError();
 }

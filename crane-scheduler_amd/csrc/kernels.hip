@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kK2Threads) void k2_hot_count(const int32_t* __rest
 // One thread per node.  Reads the parsed SoA (and K2 buckets), writes the
 // node's NodeRec into LDS, then the workgroup streams its records out with
 // 16-byte coalesced stores.
-// block size: 128 by default, CRANE_K1_THREADS=256 selects the wide variant
+// block size: 256 by default, CRANE_K1_THREADS=128 selects the narrow variant
 // STEP: also build the K3 step tables of the pod batch (K3a fused, step.hip):
 // the record is classified straight from registers.
 template <int PD, int PR, int kK1Threads, bool STEP>
@@ -126,7 +126,8 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     using Rec = NodeRec<PD, PR>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Rec* lrec = reinterpret_cast<Rec*>(smem);
-    const int64_t first = (int64_t)blockIdx.x * kK1Threads;
+    const int64_t blk = xcd_block(blockIdx.x, gridDim.x);  // this workgroup's block of nodes
+    const int64_t first = blk * kK1Threads;
     const int64_t n = first + threadIdx.x;
     __shared__ int64_t smn[kK1Threads / 64], smx[kK1Threads / 64];
     __shared__ StepShared ssh;
@@ -184,14 +185,14 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
         constexpr int kHxPer = 4, kHxFirst = 4;
         for (int b = 0; b < kMaxWin; ++b) hxh[b][threadIdx.x] = 0;
         __syncthreads();
-        const int64_t row = (int64_t)blockIdx.x * a.hx_nblk;
         for (int i0 = 0; i0 < a.hx_nblk; i0 += kK1Threads * kHxPer) {
             uint32_t c[kHxPer], o[kHxPer];
 #pragma unroll
             for (int u = 0; u < kHxPer; ++u) {
                 const int i = i0 + u * kK1Threads + threadIdx.x;
-                c[u] = i < a.hx_nblk ? a.hx_C[row + i] : 0u;
-                o[u] = i < a.hx_nblk ? a.hx_O[row + i] : 0u;
+                const uint32_t co = i < a.hx_nblk ? a.hx_CO[(int64_t)i * gridDim.x + blk] : 0u;
+                c[u] = co & 0xFFFF;
+                o[u] = co >> 16;
             }
             uint32_t v[kHxPer][kHxFirst];
 #pragma unroll
@@ -297,10 +298,10 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     if (STEP) {
         batch_range_reduce<kK1Threads>(pmn, pmx, smn, smx, tmin, tmax);
         if (n < N) step_count<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, ssh, so);
-        step_publish<kK1Threads>(so, ssh, step.st);  // (its barrier also orders lrec)
+        step_publish<kK1Threads>(so, ssh, step.st, blk);  // (its barrier also orders lrec)
         // stepped nodes (a few %) build their record from the LDS copy of the NodeRec
         if (n < N && (so.slot0 >= 0 || so.slot1 >= 0))
-            step_emit<PD, PR>(lrec[threadIdx.x], n, tmin, tmax, step.wsum, step.noprio, so, step.st);
+            step_emit<PD, PR>(lrec[threadIdx.x], n, tmin, tmax, step.wsum, step.noprio, so, step.st, blk);
     } else {
         __syncthreads();
     }
@@ -492,8 +493,11 @@ __global__ __launch_bounds__(kK3Threads) void k3_eval(const NodeRec<PD, PR>* __r
 
 // ---------------------------------------------------------------- launchers
 int k1_threads() {
+    // 256 by default: half the node blocks, so half the dedupe-form K2's (count,
+    // offset) matrix and of K3s's producer-block scans (config 3: 0.0429 vs 0.0442 ms
+    // per step); CRANE_K1_THREADS=128 selects the narrow variant
     const char* e = getenv("CRANE_K1_THREADS");
-    return e && atoi(e) == 256 ? 256 : 128;
+    return e && atoi(e) == 128 ? 128 : 256;
 }
 
 template <int PD, int PR>

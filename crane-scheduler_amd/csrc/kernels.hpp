@@ -145,7 +145,7 @@ struct StepGeometry {
 constexpr int kK3sMaxBlk = 1024;
 size_t step_vrec_bytes(int shape);
 StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk);
-int k1_threads();  // K1 workgroup size (128, or 256 with CRANE_K1_THREADS=256)
+int k1_threads();  // K1 workgroup size (256, or 128 with CRANE_K1_THREADS=128)
 // K3p: perm, pnow [ntiles * 1024], tile_mm [2 * ntiles]; initialises keys[0..P) to -1 and the step header
 hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys,
                             const StepTables& st, const StepGeometry& g, int32_t* perm, int64_t* pnow,
@@ -189,11 +189,11 @@ struct K1Args {
     void* out;              // NodeRec [N], or null (keys-only step: records not kept)
     uint32_t* cnt_out;      // [W][N] per-window counts (greedy) or null
     double* hvc_out;        // [N] hot values from the buckets, or null
-    // dedupe-form K2 output (instead of buckets): per K1 workgroup b, region r holds
-    // hx_C[b*hx_nblk + r] entries at hx_region[r*kHxRegion + hx_O[b*hx_nblk + r]]
+    // dedupe-form K2 output (instead of buckets): for K1 node block b (of nb) and K2
+    // region r, hx_CO[r*nb + b] = count | offset << 16 of b's entries at
+    // hx_region[r*kHxRegion + offset]
     const uint32_t* hx_region;
-    const uint32_t* hx_C;
-    const uint32_t* hx_O;
+    const uint32_t* hx_CO;
     int32_t hx_nblk;
     int32_t threads;        // workgroup size (0: k1_threads())
 };

@@ -110,8 +110,8 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
         r = rec[n];
         step_count<PD, PR>(r, n, tmin, tmax, wsum, noprio, sh, o);
     }
-    step_publish<kStepSeg>(o, sh, st);
-    if (n < N && (o.slot0 >= 0 || o.slot1 >= 0)) step_emit<PD, PR>(r, n, tmin, tmax, wsum, noprio, o, st);
+    step_publish<kStepSeg>(o, sh, st, blockIdx.x);
+    if (n < N && (o.slot0 >= 0 || o.slot1 >= 0)) step_emit<PD, PR>(r, n, tmin, tmax, wsum, noprio, o, st, blockIdx.x);
 }
 
 // ---------------------------------------------------------------- K3s

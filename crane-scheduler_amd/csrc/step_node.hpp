@@ -19,6 +19,14 @@
 
 namespace crane {
 
+// Producer block of workgroup b of nb: workgroups are dispatched round-robin
+// over the 8 XCDs, so XCD x gets a contiguous run of blocks (its L2 then
+// shares the cache lines of neighbouring blocks' inputs).  A bijection on [0, nb).
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+    const int64_t x = b & 7, q = b >> 3, per = nb >> 3, rem = nb & 7;
+    return x * per + (x < rem ? x : rem) + q;
+}
+
 __device__ __forceinline__ int32_t pack_key(int32_t f, int64_t n) { return (f << 24) | (int32_t)(0xFFFFFF - n); }
 
 // Exact clamped Score of (pod at time t, node) — the literal int64 restatement
@@ -152,7 +160,7 @@ __device__ __forceinline__ void step_count(const NodeRec<PD, PR>& r, int64_t n, 
 template <int PD, int PR>
 __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
                                           double wsum, int32_t noprio, const StepSlots& o,
-                                          const StepTables& st) {
+                                          const StepTables& st, int64_t blk) {
     constexpr int NB = PR + 2;
     auto kind = [&](auto Tc, int32_t slot, bool multi) {
         constexpr int T = decltype(Tc)::value;
@@ -167,7 +175,7 @@ __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, i
             v.bp = mn;
             v.k0 = k0;
             v.k1 = key_of<PD, PR>(T, mn, score_at<PD, PR>(mn, r, wsum, noprio), r, n);
-            st.single[(int64_t)T * st.npad + (int64_t)blockIdx.x * st.bs + slot] = v;
+            st.single[(int64_t)T * st.npad + blk * st.bs + slot] = v;
         } else {  // rare: sort the expiries (equal ones give equal keys)
 #pragma unroll
             for (int i = 0; i < NB; ++i)  // odd-even transposition sort (static indices)
@@ -185,7 +193,7 @@ __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, i
                 v.bp[j] = c[j];  // INT64_MAX past cnt: never selected
                 v.key[j + 1] = j < cnt ? key_of<PD, PR>(T, c[j], score_at<PD, PR>(c[j], r, wsum, noprio), r, n) : -1;
             }
-            reinterpret_cast<VRec<NB>*>(st.multi)[(int64_t)T * st.npad + (int64_t)blockIdx.x * st.bs + slot] = v;
+            reinterpret_cast<VRec<NB>*>(st.multi)[(int64_t)T * st.npad + blk * st.bs + slot] = v;
         }
     };
     kind(std::integral_constant<int, 0>{}, o.slot0, o.multi0);
@@ -193,10 +201,10 @@ __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, i
 }
 
 // Workgroup epilogue: the workgroup's flat-key maxima and record counts go to
-// its own slots of the step tables (plain stores, no global atomics).  Every
+// its own slots (producer block blk) of the step tables (plain stores, no global atomics).  Every
 // thread calls it (barrier); sh.lc must have been zeroed before step_count.
 template <int BS>
-__device__ __forceinline__ void step_publish(const StepSlots& o, StepShared& sh, const StepTables& st) {
+__device__ __forceinline__ void step_publish(const StepSlots& o, StepShared& sh, const StepTables& st, int64_t blk) {
     auto wmax = [&](int T, int32_t m) {
 #pragma unroll
         for (int s = 32; s >= 1; s >>= 1) m = max(m, __shfl_xor(m, s));
@@ -210,10 +218,10 @@ __device__ __forceinline__ void step_publish(const StepSlots& o, StepShared& sh,
         int32_t m = sh.fm[T][0];
 #pragma unroll
         for (int i = 1; i < BS / 64; ++i) m = max(m, sh.fm[T][i]);
-        st.flat[(int64_t)blockIdx.x * 2 + T] = m;
+        st.flat[blk * 2 + T] = m;
     } else if (threadIdx.x < 6) {
         const int L = threadIdx.x - 2;
-        st.cnt[(int64_t)blockIdx.x * 4 + L] = sh.lc[L >> 1][L & 1];
+        st.cnt[blk * 4 + L] = sh.lc[L >> 1][L & 1];
     }
 }
 

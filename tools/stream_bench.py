@@ -10,7 +10,10 @@ the 256 MiB Infinity Cache holds none of the inputs (MI355X_MICROARCH.md).
 Algorithmic bytes:
   k2x_partition           : 12 per binding read + 4 per in-window binding written
   k2y_bin_hist            : 4 per in-window binding read + 4*W per node (window counts)
-  k1_node_pass(+k3a_steps): 16*M (val+ts SoA) + 8*W (buckets read + zeroed) + sizeof(NodeRec) + 8 (hot value) per node
+  k1_node_pass+k3a_steps  : 16*M (val+ts SoA) + 8*W (buckets read + zeroed) + 8 (hot value) per node
+                            (+ sizeof(NodeRec) with CRANE_K1_KEEP_REC=1: the keys-only pass keeps them in LDS)
+  k1_node_pass            : the same + sizeof(NodeRec) (CRANE_K1_FUSE=0: records written, then K3a)
+  k3a_steps               : sizeof(NodeRec) read per node
 """
 import argparse
 import json
@@ -31,7 +34,7 @@ ap.add_argument("--nodes", type=int, default=4_000_000)
 ap.add_argument("--bindings", type=int, default=16_000_000)
 ap.add_argument("--pods", type=int, default=10_000)
 ap.add_argument("--reps", type=int, default=5)
-ap.add_argument("--k2", default="part,binned,hash")
+ap.add_argument("--k2", default="dedupe,binned,hash")
 args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -60,7 +63,9 @@ alg = {
     "k2_hot_count (hash)": B * 12 + 4 * W * N,
     "k2x_partition": B * 12 + b_in * 4,
     "k2y_bin_hist": b_in * 4 + 4 * W * N,
-    "k1_node_pass+k3a_steps": N * (16 * M + 8 * W + REC + 8),
+    "k1_node_pass+k3a_steps": N * (16 * M + 8 * W + 8 + (REC if os.environ.get("CRANE_K1_KEEP_REC") == "1" else 0)),
+    "k1_node_pass": N * (16 * M + 8 * W + REC + 8),
+    "k3a_steps": N * REC,
 }
 res = {}
 keys_ref = None
@@ -93,6 +98,6 @@ for k2 in args.k2.split(","):
             e.update({"alg_bytes": alg[name], "GBps": round(gbs, 1), "frac_of_8TBps": round(gbs / 8000, 4)})
         stages[name] = e
     res[k2] = stages
-out = {"nodes": N, "bindings": B, "bindings_in_window": b_in, "pods": P,
+out = {"env": {k: v for k, v in os.environ.items() if k.startswith("CRANE_") and k != "CRANE_K2"}, "nodes": N, "bindings": B, "bindings_in_window": b_in, "pods": P,
        "cold_cache": "1 GiB scratch write before the refresh and before the eval", "by_k2_mode": res}
 print(json.dumps(out))
