@@ -132,7 +132,10 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     __shared__ int64_t smn[kK1Threads / 64], smx[kK1Threads / 64];
     __shared__ StepShared ssh;
     int64_t tmin = 0, tmax = 0, pmn = 0, pmx = 0;
+    __shared__ int32_t nq;                      // stepped (node, kind) items queued for the emit
+    __shared__ uint32_t q[STEP ? 2 * kK1Threads : 1];
     if (STEP && threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+    if (STEP && threadIdx.x == 0) nq = 0;
     __shared__ uint32_t hxh[kMaxWin][kK1Threads];  // dedupe-form K2: this block's window-rank buckets
     const bool hx = a.hx_region != nullptr;
     StepSlots so;
@@ -293,15 +296,23 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
         slow |= r.e_hv != kTsInvalid && !pen_fast;
         r.pen32 = pen_fast ? (int32_t)r.pen : 0;
         r.flags = slow ? kRecSlow : 0;
-        lrec[threadIdx.x] = r;
+        if (out) lrec[threadIdx.x] = r;
     }
     if (STEP) {
         batch_range_reduce<kK1Threads>(pmn, pmx, smn, smx, tmin, tmax);
         if (n < N) step_count<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, ssh, so);
-        step_publish<kK1Threads>(so, ssh, step.st, blk);  // (its barrier also orders lrec)
-        // stepped nodes (a few %) build their record from the LDS copy of the NodeRec
-        if (n < N && (so.slot0 >= 0 || so.slot1 >= 0))
-            step_emit<PD, PR>(lrec[threadIdx.x], n, tmin, tmax, step.wsum, step.noprio, so, step.st, blk);
+        if (so.slot0 >= 0 || so.slot1 >= 0) {  // stepped (a few %): record to LDS, items to the queue
+            if (!out) lrec[threadIdx.x] = r;
+            step_queue(so, &nq, q);
+        }
+        step_publish<kK1Threads>(so, ssh, step.st, blk);  // (its barrier also orders lrec and the queue)
+        // the queued items are built densely by the first lanes of the workgroup
+        for (int w = threadIdx.x; w < nq; w += kK1Threads) {
+            const uint32_t it = q[w];
+            const int o = (int)(it & 0xFFF);
+            step_emit_one<PD, PR>(lrec[o], first + o, (int)((it >> 12) & 1), (int32_t)(it >> 14), ((it >> 13) & 1) != 0,
+                                  tmin, tmax, step.wsum, step.noprio, step.st, blk);
+        }
     } else {
         __syncthreads();
     }

@@ -200,6 +200,68 @@ __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, i
     kind(std::integral_constant<int, 1>{}, o.slot1, o.multi1);
 }
 
+// Phase 2, one (node, kind) item with the kind at run time: the fused node pass
+// compacts its stepped items into a workgroup list (step_queue) so a few lanes
+// of one wave build every record, instead of each wave paying both kinds' and
+// both record forms' code paths whenever one of its lanes is stepped.
+template <int PD, int PR>
+__device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t n, int T, int32_t slot, bool multi,
+                                              int64_t tmin, int64_t tmax, double wsum, int32_t noprio,
+                                              const StepTables& st, int64_t blk) {
+    constexpr int NB = PR + 2;
+    int64_t c[NB];
+#pragma unroll
+    for (int k = 0; k < PR; ++k) c[k] = r.e_prio[k];
+    c[PR] = r.e_hv;
+    c[PR + 1] = T == 0 ? r.e_fail : INT64_MIN;  // DaemonSet pods bypass the Filter
+    int cnt = 0;
+    int64_t mn = INT64_MAX;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const bool in = c[j] > tmin && c[j] <= tmax;
+        c[j] = in ? c[j] : INT64_MAX;
+        cnt += in;
+        mn = min(mn, c[j]);
+    }
+    auto key = [&](int64_t t) {  // key_of for the run-time kind
+        const int32_t f = score_at<PD, PR>(t, r, wsum, noprio);
+        return (T == 1 || !(t < r.e_fail)) ? pack_key(f, n) : -1;
+    };
+    const int32_t k0 = key(tmin);
+    if (!multi) {
+        Step1 v;
+        v.bp = mn;
+        v.k0 = k0;
+        v.k1 = key(mn);
+        st.single[(int64_t)T * st.npad + blk * st.bs + slot] = v;
+    } else {
+#pragma unroll
+        for (int i = 0; i < NB; ++i)  // odd-even transposition sort (static indices)
+#pragma unroll
+            for (int j = i & 1; j + 1 < NB; j += 2) {
+                const int64_t x = c[j], y = c[j + 1];
+                c[j] = min(x, y);
+                c[j + 1] = max(x, y);
+            }
+        VRec<NB> v;
+        v.cnt = cnt;
+        v.key[0] = k0;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            v.bp[j] = c[j];
+            v.key[j + 1] = j < cnt ? key(c[j]) : -1;
+        }
+        reinterpret_cast<VRec<NB>*>(st.multi)[(int64_t)T * st.npad + blk * st.bs + slot] = v;
+    }
+}
+
+// Work item of the compacted emit: owner thread | kind << 12 | multi << 13 | slot << 14.
+__device__ __forceinline__ void step_queue(const StepSlots& o, int32_t* nq, uint32_t* q) {
+    if (o.slot0 >= 0) q[atomicAdd(nq, 1)] = threadIdx.x | ((uint32_t)o.multi0 << 13) | ((uint32_t)o.slot0 << 14);
+    if (o.slot1 >= 0)
+        q[atomicAdd(nq, 1)] = threadIdx.x | (1u << 12) | ((uint32_t)o.multi1 << 13) | ((uint32_t)o.slot1 << 14);
+}
+
 // Workgroup epilogue: the workgroup's flat-key maxima and record counts go to
 // its own slots (producer block blk) of the step tables (plain stores, no global atomics).  Every
 // thread calls it (barrier); sh.lc must have been zeroed before step_count.
