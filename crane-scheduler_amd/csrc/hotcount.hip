@@ -193,7 +193,8 @@ __device__ __forceinline__ uint32_t wave_lds_add(uint32_t* a, uint32_t key, bool
     return base + rank;
 }
 
-// exclusive workgroup scan (kHT threads): wave scans + a scan of the wave totals
+// exclusive workgroup scan (BT threads): wave scans + a scan of the wave totals
+template <int BT = kHT>
 __device__ __forceinline__ uint32_t wg_excl_scan_u32(uint32_t v, uint32_t* part) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t x = v;
@@ -206,7 +207,7 @@ __device__ __forceinline__ uint32_t wg_excl_scan_u32(uint32_t v, uint32_t* part)
     __syncthreads();
     uint32_t pre = 0;
 #pragma unroll
-    for (int i = 0; i < kHT / 64; ++i) pre += i < w ? part[i] : 0u;
+    for (int i = 0; i < BT / 64; ++i) pre += i < w ? part[i] : 0u;
     __syncthreads();
     return pre + x - v;
 }
@@ -393,12 +394,14 @@ __device__ __forceinline__ int32_t hash_add(int32_t* hkey, uint32_t* hcnt, uint3
     }
 }
 
+template <int BT>
 __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __restrict__ bnode,
                                          const int64_t* __restrict__ bts, int64_t B, int64_t N, const HotCutoffs& cut,
                                          const HotPart& g, uint32_t* __restrict__ CO, uint32_t* __restrict__ region) {
     // hkey, hcnt [kDSlots], hist, off [nbins], uniq u16 [kXChunk]
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
-    __shared__ uint32_t part[kHT];
+    constexpr int kPer = kXChunk / BT;  // bindings per thread
+    __shared__ uint32_t part[BT];
     __shared__ uint32_t nuniq;
     int32_t* hkey = reinterpret_cast<int32_t*>(sh);
     uint32_t* hcnt = sh + kDSlots;
@@ -406,24 +409,24 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     uint32_t* off = hist + g.nbins;
     uint16_t* uniq = reinterpret_cast<uint16_t*>(off + g.nbins);
     const int64_t b0 = (int64_t)blk * kXChunk + threadIdx.x;
-    int32_t nd[kXPer];
-    int64_t ts[kXPer];
+    int32_t nd[kPer];
+    int64_t ts[kPer];
 #pragma unroll
-    for (int u = 0; u < kXPer; ++u) {
-        const int64_t b = b0 + u * kHT;
+    for (int u = 0; u < kPer; ++u) {
+        const int64_t b = b0 + u * BT;
         nd[u] = b < B ? bnode[b] : -1;
         ts[u] = b < B ? bts[b] : INT64_MIN;
     }
-    for (int i = threadIdx.x; i < kDSlots; i += kHT) {
+    for (int i = threadIdx.x; i < kDSlots; i += BT) {
         hkey[i] = -1;
         hcnt[i] = 0;
     }
-    for (int i = threadIdx.x; i < g.nbins; i += kHT) hist[i] = 0;
+    for (int i = threadIdx.x; i < g.nbins; i += BT) hist[i] = 0;
     if (threadIdx.x == 0) nuniq = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int u = 0; u < kXPer; ++u) {
+    for (int u = 0; u < kPer; ++u) {
         const int j = window_rank(ts[u], cut);
         const bool ok = nd[u] >= 0 && (int64_t)nd[u] < N && j > 0;  // binding.go:85-91
         const int32_t key = ok ? nd[u] * 8 + (j - 1) : -1;
@@ -449,11 +452,11 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
         }
     }
     __syncthreads();
-    const int per = (g.nbins + kHT - 1) / kHT;
+    const int per = (g.nbins + BT - 1) / BT;
     const int lo = min(g.nbins, (int)threadIdx.x * per), hi = min(g.nbins, lo + per);
     uint32_t sum = 0;
     for (int i = lo; i < hi; ++i) sum += hist[i];
-    uint32_t run = wg_excl_scan_u32(sum, part);
+    uint32_t run = wg_excl_scan_u32<BT>(sum, part);
     for (int i = lo; i < hi; ++i) {
         const uint32_t c = hist[i];
         off[i] = run;
@@ -461,12 +464,12 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     }
     __syncthreads();
     // this region's row of (count | offset << 16) per node block: coalesced
-    for (int i = threadIdx.x; i < g.nbins; i += kHT) CO[(int64_t)blk * g.nbins + i] = hist[i] | (off[i] << 16);
+    for (int i = threadIdx.x; i < g.nbins; i += BT) CO[(int64_t)blk * g.nbins + i] = hist[i] | (off[i] << 16);
     __syncthreads();
     uint32_t* reg = region + (int64_t)blk * kXChunk;
     const uint32_t mask = (1u << g.bb) - 1;
     const uint32_t nu = nuniq;
-    for (uint32_t i = threadIdx.x; i < nu; i += kHT) {
+    for (uint32_t i = threadIdx.x; i < nu; i += BT) {
         const int s = uniq[i];
         const int32_t k = hkey[s];
         const uint32_t p = atomicAdd(&off[(k >> 3) >> g.bb], 1u);
@@ -474,18 +477,22 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     }
 }
 
-__global__ __launch_bounds__(kHT) void k2x_dedupe(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
+// 512 threads (4 bindings each): the launch is one round of workgroups at
+// config 3, so its time is one workgroup's dependent chain; wider workgroups halve it
+constexpr int kDT = 512;
+
+__global__ __launch_bounds__(kDT) void k2x_dedupe(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
                                                   int64_t B, int64_t N, HotCutoffs cut, HotPart g,
                                                   uint32_t* __restrict__ CO, uint32_t* __restrict__ region) {
-    k2d_body((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
+    k2d_body<kDT>((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
 }
 
-__global__ __launch_bounds__(kHT) void k2x_dedupe_pods(const int32_t* __restrict__ bnode,
+__global__ __launch_bounds__(kDT) void k2x_dedupe_pods(const int32_t* __restrict__ bnode,
                                                        const int64_t* __restrict__ bts, int64_t B, int64_t N,
                                                        HotCutoffs cut, HotPart g, uint32_t* __restrict__ CO,
                                                        uint32_t* __restrict__ region, PodPrep pp) {
-    if ((int32_t)blockIdx.x < g.nblk) k2d_body((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
-    else k3p_tile256((int64_t)blockIdx.x - g.nblk, pp);
+    if ((int32_t)blockIdx.x < g.nblk) k2d_body<kDT>((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
+    else k3p_tile<kDT>((int64_t)blockIdx.x - g.nblk, pp);
 }
 
 HotPart hot_dedupe_geometry(int64_t B, int64_t N, int32_t W, int32_t bs) {
@@ -518,10 +525,10 @@ hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int
     uint32_t* CO = scratch + g.cap;  // [nblk][nbins]
     const size_t lds = sizeof(uint32_t) * (2 * (size_t)kDSlots + 2 * (size_t)g.nbins) + sizeof(uint16_t) * kXChunk;
     if (pods && pods->P > 0)
-        hipLaunchKernelGGL(k2x_dedupe_pods, dim3((unsigned)(g.nblk + pods->ntiles)), dim3(kHT), lds, st, bnode, bts,
+        hipLaunchKernelGGL(k2x_dedupe_pods, dim3((unsigned)(g.nblk + pods->ntiles)), dim3(kDT), lds, st, bnode, bts,
                            B, N, cut, g, CO, region, *pods);
     else
-        hipLaunchKernelGGL(k2x_dedupe, dim3((unsigned)g.nblk), dim3(kHT), lds, st, bnode, bts, B, N, cut, g, CO,
+        hipLaunchKernelGGL(k2x_dedupe, dim3((unsigned)g.nblk), dim3(kDT), lds, st, bnode, bts, B, N, cut, g, CO,
                            region);
     return hipGetLastError();
 }

@@ -13,8 +13,10 @@
 
 namespace crane {
 
-__device__ __forceinline__ void k3p_tile256(const int64_t t, const PodPrep& pp) {
-    constexpr int kT = 256, kU = 1024 / kT, kG = kU * (kT / 64);  // pods per lane, (u, wave) groups
+template <int kT>
+__device__ __forceinline__ void k3p_tile(const int64_t t, const PodPrep& pp) {
+    static_assert(1024 % kT == 0 && kT >= 64, "a tile is 1024 pods");
+    constexpr int kU = 1024 / kT, kG = kU * (kT / 64);  // pods per lane, (u, wave) groups
     __shared__ int32_t cn[kG], cd[kG];
     __shared__ int64_t wmn[kT / 64], wmx[kT / 64];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -86,5 +88,7 @@ __device__ __forceinline__ void k3p_tile256(const int64_t t, const PodPrep& pp) 
         pp.tile_mm[2 * t + 1] = b;
     }
 }
+
+__device__ __forceinline__ void k3p_tile256(const int64_t t, const PodPrep& pp) { k3p_tile<256>(t, pp); }
 
 }  // namespace crane
