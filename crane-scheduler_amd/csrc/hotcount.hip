@@ -477,9 +477,9 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     }
 }
 
-// 512 threads (4 bindings each): the launch is one round of workgroups at
-// config 3, so its time is one workgroup's dependent chain; wider workgroups halve it
-constexpr int kDT = 512;
+// 1024 threads (2 bindings each): the launch is one round of workgroups at
+// config 3, so its time is one workgroup's dependent chain; wider workgroups shorten it (256 -> 512 -> 1024: 15.6 -> 11.9 -> 11.3 us)
+constexpr int kDT = 1024;
 
 __global__ __launch_bounds__(kDT) void k2x_dedupe(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
                                                   int64_t B, int64_t N, HotCutoffs cut, HotPart g,
