@@ -145,6 +145,19 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     uint32_t bc[kMaxWin];
     double hvl = 0.0;
     int64_t hvt = kTsInvalid;
+    // dedupe-form K2: the count/offset words of this block's first source
+    // regions go out before the SoA loads, so the dependent entry loads below
+    // wait on them, not on the whole SoA batch
+    constexpr int kHxPer = 4, kHxFirst = 4;
+    uint32_t co0[kHxPer];
+    if (hx) {
+#pragma unroll
+        for (int u = 0; u < kHxPer; ++u) {
+            const int i = u * kK1Threads + threadIdx.x;
+            co0[u] = i < a.hx_nblk ? a.hx_CO[(int64_t)i * gridDim.x + blk] : 0u;
+        }
+        for (int b = 0; b < kMaxWin; ++b) hxh[b][threadIdx.x] = 0;
+    }
     if (n < N) {
         // every load first, unconditionally (rows past npd/npr read row 0 and are
         // ignored), so a wave has them all in flight at once; compute after
@@ -185,15 +198,12 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
         // this block's (node, bucket, count) entries from every K2 source region
         // (dedupe form): C/O of up to kHxPer regions per lane, then their first
         // kHxFirst entries, all loads in flight together; longer runs loop
-        constexpr int kHxPer = 4, kHxFirst = 4;
-        for (int b = 0; b < kMaxWin; ++b) hxh[b][threadIdx.x] = 0;
-        __syncthreads();
         for (int i0 = 0; i0 < a.hx_nblk; i0 += kK1Threads * kHxPer) {
             uint32_t c[kHxPer], o[kHxPer];
 #pragma unroll
             for (int u = 0; u < kHxPer; ++u) {
                 const int i = i0 + u * kK1Threads + threadIdx.x;
-                const uint32_t co = i < a.hx_nblk ? a.hx_CO[(int64_t)i * gridDim.x + blk] : 0u;
+                const uint32_t co = i0 == 0 ? co0[u] : i < a.hx_nblk ? a.hx_CO[(int64_t)i * gridDim.x + blk] : 0u;
                 c[u] = co & 0xFFFF;
                 o[u] = co >> 16;
             }
@@ -204,6 +214,7 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
 #pragma unroll
                 for (int k = 0; k < kHxFirst; ++k) v[u][k] = (uint32_t)k < c[u] ? src[k] : 0u;
             }
+            if (i0 == 0) __syncthreads();  // hxh zeroed by every thread (uniform trip count)
 #pragma unroll
             for (int u = 0; u < kHxPer; ++u) {
 #pragma unroll
