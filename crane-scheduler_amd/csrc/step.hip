@@ -397,11 +397,15 @@ StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk) {
     g.npad = g.nseg * kStepSeg;  // >= nblk * bs for bs = 128 or 256
     g.ntiles = (P + kPodTile - 1) / kPodTile;
     g.ngroups = (P + kK3sPods - 1) / kK3sPods;
-    // R workgroups per 1024-pod group: ~512 workgroups in all, at most 64 per group,
+    // R workgroups per 1024-pod group: ~1024 workgroups in all, at most 48 per group,
     // and enough that each covers at most kK3sMaxBlk producer blocks
     const char* e = getenv("CRANE_K3S_BLOCKS");
     const int64_t target = e && atoi(e) > 0 ? atoi(e) : 1024;
-    int64_t R = std::min<int64_t>(64, std::max<int64_t>(1, target / std::max<int64_t>(g.ngroups, 1)));
+    // at most kR slices per group: past ~48 the per-workgroup prologue (producer counts,
+    // pod loads) outweighs the shorter slices (config 3, 10 groups: R 64 -> 48 = 14.9 -> 13.6 us)
+    const char* re = getenv("CRANE_K3S_RMAX");
+    const int64_t kR = re && atoi(re) > 0 ? atoi(re) : 48;
+    int64_t R = std::min<int64_t>(kR, std::max<int64_t>(1, target / std::max<int64_t>(g.ngroups, 1)));
     R = std::max<int64_t>(R, (nblk + kK3sMaxBlk - 1) / kK3sMaxBlk);
     g.R = (int32_t)R;
     return g;
