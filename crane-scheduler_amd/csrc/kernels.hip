@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     // dedupe-form K2: the count/offset words of this block's first source
     // regions go out before the SoA loads, so the dependent entry loads below
     // wait on them, not on the whole SoA batch
-    constexpr int kHxPer = 4, kHxFirst = 4;
+    constexpr int kHxPer = 4, kHxFirst = 4, kHxRun = 8;
     uint32_t co0[kHxPer];
     if (hx) {
 #pragma unroll
@@ -220,10 +220,16 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
 #pragma unroll
                 for (int k = 0; k < kHxFirst; ++k)
                     if ((uint32_t)k < c[u]) atomicAdd(&hxh[(v[u][k] >> 16) & 7][v[u][k] & 0xFFFF], v[u][k] >> 19);
+                // long runs (the Zipf-hot blocks: ~100 entries per region) in chunks of
+                // kHxRun independent loads, not one load latency per entry
                 const uint32_t* src = a.hx_region + (int64_t)(i0 + u * kK1Threads + threadIdx.x) * kHxRegion + o[u];
-                for (uint32_t k = kHxFirst; k < c[u]; ++k) {
-                    const uint32_t w = src[k];
-                    atomicAdd(&hxh[(w >> 16) & 7][w & 0xFFFF], w >> 19);
+                for (uint32_t k0 = kHxFirst; k0 < c[u]; k0 += kHxRun) {
+                    uint32_t w[kHxRun];
+#pragma unroll
+                    for (int j = 0; j < kHxRun; ++j) w[j] = k0 + j < c[u] ? src[k0 + j] : 0u;
+#pragma unroll
+                    for (int j = 0; j < kHxRun; ++j)
+                        if (k0 + j < c[u]) atomicAdd(&hxh[(w[j] >> 16) & 7][w[j] & 0xFFFF], w[j] >> 19);
                 }
             }
         }
