@@ -287,8 +287,8 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
                 for (int b = 0; b < kMaxWin; ++b) c += (b >= pol.win_pos[w] && b < pol.n_win) ? bc[b] : 0u;
                 if (cnt_out) cnt_out[(int64_t)w * N + n] = (uint32_t)c;
                 // Go int division (truncates toward 0); counts fit 32 bits in practice: u32 divide
-                const int32_t cw = pol.win_count[w];
-                if (cw > 0 && c <= 0xFFFFFFFFLL)
+                const int64_t cw = pol.win_count[w];
+                if (cw > 0 && cw <= 0xFFFFFFFFLL && c <= 0xFFFFFFFFLL)
                     v += (int64_t)((uint32_t)c / (uint32_t)cw);
                 else
                     v += c / cw;

@@ -165,12 +165,14 @@ def test_hot_values_random(n_nodes, n_bind, seed, k2, monkeypatch):
 
 
 @pytest.mark.parametrize("threads", ["128", "256"])
-@pytest.mark.parametrize("case", ["one_hot_node", "eight_windows", "last_node"])
+@pytest.mark.parametrize("case", ["one_hot_node", "eight_windows", "last_node", "odd_counts"])
 def test_hot_values_dedupe_edges(case, threads, monkeypatch):
     """Dedupe-form K2 (per-workgroup (node, bucket) aggregation, counts read by the
     node pass) at its packing limits: a region whose 2048 bindings all hit one node
     (count field), eight windows (bucket field), the shard's last node and bindings
-    past the shard; 128- and 256-node bins."""
+    past the shard; 128- and 256-node bins.  odd_counts: hotValue.count negative
+    and past 32 bits (the node pass divides in u32 only when both operands fit;
+    Go's int64 division truncates toward zero otherwise, node.go:117)."""
     monkeypatch.setenv("CRANE_K2", "dedupe")
     monkeypatch.setenv("CRANE_K1_THREADS", threads)
     m = 60 * 10**9
@@ -178,9 +180,11 @@ def test_hot_values_dedupe_edges(case, threads, monkeypatch):
     n_nodes, n_bind = 5000, 200_000
     if case == "eight_windows":
         spec["hotValue"] = [(k * 40 * 10**9, c) for k, c in zip(range(1, 9), [1, 2, 3, 5, 7, 11, 13, 1])]
+    if case == "odd_counts":
+        spec["hotValue"] = [(5 * m, -3), (1 * m, 2**32 + 1), (3 * m, 7)]
     c = synth.make_cluster(spec, n_nodes, 64, n_bindings=n_bind, seed=31, pod_step_ns=5_000_000_000)
     bn = c.b_node.copy()
-    if case == "one_hot_node":
+    if case in ("one_hot_node", "odd_counts"):
         bn[: 3 * 2048 + 5] = 4321  # whole source regions on one node
         bn[-4096:] = 17
     if case == "last_node":
