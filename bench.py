@@ -260,6 +260,7 @@ def main():
         geng.close()
 
     cpu = None
+    host_parse = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
         cp = min(args.cpu_pods, P)
@@ -270,8 +271,23 @@ def main():
         cpu = {"value": round(cp * N / dt, 1), "unit": "pod-node evals/s", "cores": args.cpu_threads, "kind": "port",
                "sample": f"{cp} pods x {N} nodes, string mode (re-parse every annotation per call like stats.go), "
                          f"{args.cpu_threads} threads, {dt:.1f}s"}
-        # the sample's choices must agree with the GPU (hot values: CPU sees the annotation hv,
-        # GPU the binding-log hv, so compare against a fresh GPU eval without the refresh)
+        # the once-per-sync host parse of the same snapshot's annotation
+        # strings into the SoA the engine uploads (crane_parse_annotations, C++ threads)
+        snap = cd.SnapshotStrings(eng.metric_names, ann)
+        host_parse = {"strings": len(snap), "nodes": N}
+        for label, th in (("threads_16", args.cpu_threads), ("threads_all", 0)):
+            snap.parse(synth.SHANGHAI, th)
+            reps = []
+            for _ in range(3):
+                t1 = time.perf_counter()
+                snap.parse(synth.SHANGHAI, th)
+                reps.append(time.perf_counter() - t1)
+            dtp = float(np.median(reps))
+            host_parse[label] = {"ms_per_sync": round(dtp * 1e3, 2), "strings_per_s": round(len(snap) / dtp, 1)}
+        pv, pt, _, _ = snap.soa()
+        okm = c.rows(eng.metric_names)[2].astype(bool)
+        host_parse["matches_generator_soa"] = bool(np.array_equal(pt[okm], ts[okm]) and np.array_equal(pv[okm],
+                                                                                                       val[okm]))
     if rank == 0:
         line = {
             "metric": "pod-node filter+score evals/sec",
@@ -297,6 +313,7 @@ def main():
             "roofline_stages": roofs,
             "cpu_baseline": cpu,
             "greedy": greedy,
+            "host_parse": host_parse,
             "chosen_sample": [int(x) for x in keys[:4]],
         }
         print(json.dumps(line), flush=True)

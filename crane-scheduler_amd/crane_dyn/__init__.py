@@ -188,23 +188,42 @@ def parse_annotation(s: str, tz_offset_s: int):
     return v.value, t.value
 
 
+class SnapshotStrings:
+    """A node snapshot's annotation strings encoded once, row-major [M+1][N] (the
+    metrics, then node_hot_value; None = key missing), for repeated bulk parses
+    through crane_parse_annotations (the once-per-sync parse of SURVEY §8f row 2)."""
+
+    def __init__(self, metric_names, nodes):
+        self.M, self.N = len(metric_names), len(nodes)
+        keys = list(metric_names) + ["node_hot_value"]
+        self._enc = [None if x is None else x.encode() for x in (a.get(k) for k in keys for a in nodes)]
+        self._strs = (C.c_char_p * max(1, len(self._enc)))(*self._enc)
+        self._lens = np.array([0 if x is None else len(x) for x in self._enc], dtype=np.uint64)
+        self.val = np.zeros(len(self._enc))
+        self.ts = np.empty(len(self._enc), np.int64)
+
+    def __len__(self):
+        return len(self._enc)
+
+    def parse(self, tz_offset_s, threads=0):
+        """Parse every string into self.val / self.ts (flat [M+1][N]); host threads <= 0 = all."""
+        rc = lib.crane_parse_annotations(len(self._enc), C.cast(self._strs, C.c_void_p), _ptr(self._lens),
+                                         tz_offset_s, _ptr(self.val), _ptr(self.ts), threads)
+        if rc:
+            raise CraneError(rc, "bulk annotation parse")
+
+    def soa(self):
+        """(val[M][N], ts[M][N], hv[N], hv_ts[N]) from the last parse."""
+        M, N = self.M, self.N
+        val, ts = self.val.reshape(M + 1, N), self.ts.reshape(M + 1, N)
+        return val[:M].copy(), ts[:M].copy(), val[M].copy(), ts[M].copy()
+
+
 def parse_nodes(metric_names, nodes, tz_offset_s, threads=0):
     """Node annotation dicts -> SoA (val[M][N], ts[M][N], hv[N], hv_ts[N]) in one bulk parse."""
-    M, N = len(metric_names), len(nodes)
-    keys = list(metric_names) + ["node_hot_value"]
-    raw = [a.get(k) for k in keys for a in nodes]  # row-major [M+1][N]
-    enc = [None if x is None else x.encode() for x in raw]
-    strs = (C.c_char_p * max(1, len(enc)))(*enc)
-    lens = np.array([0 if x is None else len(x) for x in enc], dtype=np.uint64)
-    val = np.zeros(len(enc))
-    ts = np.empty(len(enc), np.int64)
-    rc = lib.crane_parse_annotations(len(enc), C.cast(strs, C.c_void_p), _ptr(lens), tz_offset_s, _ptr(val), _ptr(ts),
-                                     threads)
-    if rc:
-        raise CraneError(rc, "bulk annotation parse")
-    val = val.reshape(M + 1, N)
-    ts = ts.reshape(M + 1, N)
-    return val[:M].copy(), ts[:M].copy(), val[M].copy(), ts[M].copy()
+    snap = SnapshotStrings(metric_names, nodes)
+    snap.parse(tz_offset_s, threads)
+    return snap.soa()
 
 
 def key_node(key: int):

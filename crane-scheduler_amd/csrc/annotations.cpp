@@ -66,6 +66,36 @@ bool underscores_ok(const char* s, size_t n) {
 bool crane_go_parse_float(const char* s, size_t n, double* out) {
     *out = 0;
     if (n == 0) return false;
+    // Fast path for the controller's own formats ([-]d+[.d*], FormatFloat 'f' /
+    // Itoa): with the decimal mantissa <= 2^53 and at most 22 fraction digits,
+    // mantissa / 10^k is one correctly rounded IEEE division of two exact
+    // doubles, i.e. the same double strtod (and Go) return.  Anything else falls
+    // through to the full grammar below.
+    {
+        static const double p10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                       1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+        size_t i = (s[0] == '-' || s[0] == '+') ? 1 : 0;
+        const size_t d0 = i;
+        uint64_t mant = 0;
+        int nd = 0, frac = -1;
+        for (; i < n; ++i) {
+            const char c = s[i];
+            if (digit(c)) {
+                if (++nd > 19) break;
+                mant = mant * 10 + (uint64_t)(c - '0');
+                if (frac >= 0) ++frac;
+            } else if (c == '.' && frac < 0 && i > d0) {
+                frac = 0;
+            } else {
+                break;
+            }
+        }
+        if (i == n && nd > 0 && mant <= (1ull << 53) && frac <= 22) {
+            const double v = frac > 0 ? (double)mant / p10[frac] : (double)mant;
+            *out = s[0] == '-' ? -v : v;
+            return true;
+        }
+    }
     // special(): [+-]inf|infinity (case-folded), unsigned nan
     {
         size_t off = 0;

@@ -85,3 +85,41 @@ def test_bulk_parse_matches_single(cluster_small):
                 assert ts[m, n] == cd.CRANE_TS_INVALID
         if "node_hot_value" in nodes[n]:
             assert (hv[n], hv_ts[n]) == cd.parse_annotation(nodes[n]["node_hot_value"], 8 * 3600)
+
+
+def test_snapshot_parse_matches_generator_soa():
+    """Bulk parse of a synthetic snapshot's annotation strings reproduces the generator's own
+    SoA: well-formed values bit-exact, missing/malformed keys CRANE_TS_INVALID, negatives kept
+    (the engine rejects them like stats.go:71-73); thread count does not change the result."""
+    from crane_dyn import synth
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 3000, 1, seed=7)
+    snap = cd.SnapshotStrings(c.metric_names, c.annotations())
+    snap.parse(synth.SHANGHAI, threads=1)
+    val, ts, hv, hv_ts = snap.soa()
+    snap.parse(synth.SHANGHAI, threads=4)
+    v4, t4, _, _ = snap.soa()
+    assert np.array_equal(ts, t4) and np.array_equal(val.view(np.int64), v4.view(np.int64))
+    ok = c.ok.astype(bool)
+    assert np.array_equal(ts[ok], c.ts[ok]) and np.array_equal(val[ok], c.val[ok])
+    assert (ts[~ok] == cd.CRANE_TS_INVALID).all()
+    assert (val[ok] < 0).any()
+    assert np.array_equal(hv, c.hv) and np.array_equal(hv_ts, c.hv_ts)
+
+
+def test_parse_float_fast_path_matches_correct_rounding():
+    """The decimal fast path (mantissa <= 2^53, <= 22 fraction digits) must return the
+    correctly rounded double, i.e. what strconv.ParseFloat (and Python's float) return."""
+    rng = np.random.default_rng(11)
+    cases = ["0", "-0", "+7", "1.", "0.00000", "-0.00000", "9007199254740992", "9007199254740993",
+             "0.1", "0.30000", "1.23456789012345678", "123456789012345678901", "1e5", ".5", "-.5",
+             "4503599627370497.5", "0.0000000000000000000001", "0.00000000000000000000001"]
+    cases += [f"{x:.5f}" for x in rng.random(2000) * 1.2]
+    cases += [f"{x:.{k}f}" for x, k in zip(rng.random(2000) * 10.0 ** rng.integers(0, 12, 2000),
+                                           rng.integers(0, 23, 2000))]
+    cases += [str(int(x)) for x in rng.integers(0, 2**62, 500)]
+    for s in cases:
+        v, t = cd.parse_annotation(s + ",2026-10-15T20:00:00Z", 8 * 3600)
+        assert t == 1792065600 * 10**9, s
+        want = float(s)
+        assert v == want and np.signbit(v) == np.signbit(want), (s, v, want)
