@@ -260,7 +260,7 @@ def main():
         geng.close()
 
     cpu = None
-    host_parse = None
+    host_parse = ctl = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
         cp = min(args.cpu_pods, P)
@@ -284,6 +284,24 @@ def main():
                 reps.append(time.perf_counter() - t1)
             dtp = float(np.median(reps))
             host_parse[label] = {"ms_per_sync": round(dtp * 1e3, 2), "strings_per_s": round(len(snap) / dtp, 1)}
+        # the controller's per-sync hot-value annotation pass
+        # (node.go:113-121 over binding.go:81-97) as K2+K1 plus the 8 B/node readback,
+        # checked bit-exact against the oracle's count over the full binding log
+        eng.refresh_hot_values(now_sync)
+        eng.hot_values()
+        reps = []
+        for _ in range(5):
+            t1 = time.perf_counter()
+            eng.refresh_hot_values(now_sync)
+            ghv = eng.hot_values()
+            reps.append(time.perf_counter() - t1)
+        t1 = time.perf_counter()
+        _, ohv = O.hot_values(spec, c.b_node, c.b_ts, N, now_sync // 10**9)
+        ocpu = time.perf_counter() - t1
+        ctl = {"workload": f"{B}-entry binding log -> {N} node hot values", "gpu_ms": round(float(np.median(reps)) * 1e3, 3),
+               "timing": "host wall incl. K2 + K1 + D2H of hot values", "oracle_cpu_ms": round(ocpu * 1e3, 2),
+               "oracle": "C restatement, one pass over the log (the reference scans the log once per node: O(N*B))",
+               "matches_oracle": bool(np.array_equal(ghv, ohv.astype(np.float64)))}
         pv, pt, _, _ = snap.soa()
         okm = c.rows(eng.metric_names)[2].astype(bool)
         host_parse["matches_generator_soa"] = bool(np.array_equal(pt[okm], ts[okm]) and np.array_equal(pv[okm],
@@ -314,6 +332,7 @@ def main():
             "cpu_baseline": cpu,
             "greedy": greedy,
             "host_parse": host_parse,
+            "controller_hot_values": ctl,
             "chosen_sample": [int(x) for x in keys[:4]],
         }
         print(json.dumps(line), flush=True)
