@@ -72,7 +72,7 @@ def test_engine_rejects_bad_policy():
 
 
 def test_bulk_parse_matches_single(cluster_small):
-    nodes = cluster_small["nodes"] * 50  # > 4096 strings: threaded path
+    nodes = cluster_small["nodes"] * 50
     names = ["cpu_usage_avg_5m", "cpu_usage_max_avg_1h", "cpu_usage_max_avg_1d", "mem_usage_avg_5m",
              "mem_usage_max_avg_1h", "mem_usage_max_avg_1d"]
     val, ts, hv, hv_ts = cd.parse_nodes(names, nodes, 8 * 3600)
@@ -93,7 +93,7 @@ def test_snapshot_parse_matches_generator_soa():
     (the engine rejects them like stats.go:71-73); thread count does not change the result."""
     from crane_dyn import synth
     spec = cd.default_policy_spec()
-    c = synth.make_cluster(spec, 3000, 1, seed=7)
+    c = synth.make_cluster(spec, 12000, 1, seed=7)  # 84k strings: 2 threads of >= 32k
     snap = cd.SnapshotStrings(c.metric_names, c.annotations())
     snap.parse(synth.SHANGHAI, threads=1)
     val, ts, hv, hv_ts = snap.soa()
