@@ -197,8 +197,11 @@ class SnapshotStrings:
         self.M, self.N = len(metric_names), len(nodes)
         keys = list(metric_names) + ["node_hot_value"]
         self._enc = [None if x is None else x.encode() for x in (a.get(k) for k in keys for a in nodes)]
-        self._strs = (C.c_char_p * max(1, len(self._enc)))(*self._enc)
+        # one contiguous buffer, as the cgo shim builds it, NULL = key missing
         self._lens = np.array([0 if x is None else len(x) for x in self._enc], dtype=np.uint64)
+        self._buf = C.create_string_buffer(b"".join(x for x in self._enc if x is not None), int(self._lens.sum()) + 1)
+        offs = np.concatenate(([0], np.cumsum(self._lens)[:-1])).astype(np.uint64) if len(self._enc) else self._lens
+        self._strs = np.where([x is not None for x in self._enc], C.addressof(self._buf) + offs, 0).astype(np.uint64)
         self.val = np.zeros(len(self._enc))
         self.ts = np.empty(len(self._enc), np.int64)
 
@@ -207,7 +210,7 @@ class SnapshotStrings:
 
     def parse(self, tz_offset_s, threads=0):
         """Parse every string into self.val / self.ts (flat [M+1][N]); host threads <= 0 = all."""
-        rc = lib.crane_parse_annotations(len(self._enc), C.cast(self._strs, C.c_void_p), _ptr(self._lens),
+        rc = lib.crane_parse_annotations(len(self._enc), _ptr(self._strs), _ptr(self._lens),
                                          tz_offset_s, _ptr(self.val), _ptr(self.ts), threads)
         if rc:
             raise CraneError(rc, "bulk annotation parse")
