@@ -211,6 +211,33 @@ int64_t civil_days(int64_t y, int m, int d) {
 // offset.  Layout chunks (go1.17 time/format.go): stdLongYear '-' stdZeroMonth
 // '-' stdZeroDay 'T' stdHour ':' stdZeroMinute ':' stdZeroSecond [.frac] 'Z'.
 bool crane_go_parse_time(const char* s, size_t n, int64_t tz_offset_s, int64_t* out_ns) {
+    // Fast path for the exact 20-byte stamp the controller writes: fixed
+    // digit/separator positions, same range checks, and a per-thread memo of
+    // the last date (a snapshot's stamps share a handful of days), so the
+    // calendar arithmetic runs once per distinct date.  Anything else (a
+    // fraction, one-digit hour, bad byte) takes the general path below.
+    if (n == 20) {
+        auto d2 = [&](int i) { return (s[i] - '0') * 10 + (s[i + 1] - '0'); };
+        bool ok = s[4] == '-' && s[7] == '-' && s[10] == 'T' && s[13] == ':' && s[16] == ':' && s[19] == 'Z';
+        for (int i : {0, 1, 2, 3, 5, 6, 8, 9, 11, 12, 14, 15, 17, 18}) ok = ok && digit(s[i]);
+        if (ok) {
+            const int year = d2(0) * 100 + d2(2), mon = d2(5), day = d2(8), hour = d2(11), min = d2(14),
+                      sec = d2(17);
+            if (mon < 1 || mon > 12 || hour > 23 || min > 59 || sec > 59) return false;
+            thread_local int memo_key = -1;
+            thread_local int64_t memo_days = 0;
+            const int key = (year * 16 + mon) * 32 + day;
+            if (key != memo_key) {
+                if (day < 1 || day > month_days(mon, year)) return false;
+                memo_days = civil_days(year, mon, day);
+                memo_key = key;
+            }
+            const __int128 t = (__int128)(memo_days * 86400 + hour * 3600 + min * 60 + sec - tz_offset_s) * 1000000000;
+            const __int128 lo = (__int128)INT64_MIN / 2, hi = (__int128)INT64_MAX / 2;  // as below
+            *out_ns = (int64_t)(t < lo ? lo : (t > hi ? hi : t));
+            return true;
+        }
+    }
     if (n < 4 || !digit(s[0])) return false;
     int year = 0;
     for (int k = 0; k < 4; ++k) {

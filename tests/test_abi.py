@@ -123,3 +123,28 @@ def test_parse_float_fast_path_matches_correct_rounding():
         assert t == 1792065600 * 10**9, s
         want = float(s)
         assert v == want and np.signbit(v) == np.signbit(want), (s, v, want)
+
+
+def test_parse_time_fixed_layout_matches_oracle():
+    """The 20-byte stamp fast path (fixed positions, per-thread date memo) against the oracle's
+    general ParseInLocation restatement: random fields in and out of range, far years
+    (saturated ns), corrupted bytes, and repeated dates in one bulk parse (the memo)."""
+    rng = np.random.default_rng(5)
+    strs = []
+    for _ in range(3000):
+        y = int(rng.choice([rng.integers(0, 10000), rng.integers(1990, 2100)]))
+        f = [y, rng.integers(0, 14), rng.integers(0, 33), rng.integers(0, 26), rng.integers(0, 62),
+             rng.integers(0, 62)]
+        s = "%04d-%02d-%02dT%02d:%02d:%02dZ" % tuple(int(x) for x in f)
+        if rng.random() < 0.1:
+            i = int(rng.integers(0, 20))
+            s = s[:i] + chr(int(rng.integers(32, 127))) + s[i + 1:]
+        strs.append("0.5," + s)
+    strs += ["0.5,2024-02-29T00:00:00Z", "0.5,2023-02-29T00:00:00Z", "0.5,2023-02-28T23:59:59Z"] * 3
+    nodes = [{"m": s} for s in strs]
+    val, ts, _, _ = cd.parse_nodes(["m"], nodes, 8 * 3600, threads=1)
+    for n, s in enumerate(strs):
+        ok, _, ots = O.parse_annotation(s, 8 * 3600)
+        assert (ts[0, n] != cd.CRANE_TS_INVALID) == ok, s
+        if ok:
+            assert ts[0, n] == ots, s
