@@ -271,6 +271,14 @@ def main():
         cpu = {"value": round(cp * N / dt, 1), "unit": "pod-node evals/s", "cores": args.cpu_threads, "kind": "port",
                "sample": f"{cp} pods x {N} nodes, string mode (re-parse every annotation per call like stats.go), "
                          f"{args.cpu_threads} threads, {dt:.1f}s"}
+        # the stronger CPU data point, pre-parsed SoA (no string work per call)
+        okr = c.rows(eng.metric_names)[2]
+        t1 = time.perf_counter()
+        O.eval_soa(spec, eng.metric_names, okr, val, ts, np.ones(N, np.uint8), c.hv, c.hv_ts, c.now[:cp], c.ds[:cp],
+                   threads=args.cpu_threads, want_matrix=False)
+        dts = time.perf_counter() - t1
+        cpu["soa_mode"] = {"value": round(cp * N / dts, 1), "unit": "pod-node evals/s", "cores": args.cpu_threads,
+                           "sample": f"{cp} pods x {N} nodes, pre-parsed SoA, {dts:.1f}s"}
         # the once-per-sync host parse of the same snapshot's annotation
         # strings into the SoA the engine uploads (crane_parse_annotations, C++ threads)
         snap = cd.SnapshotStrings(eng.metric_names, ann)
