@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libcrane_dyn.so")
+# CRANE_DYN_LIB: an alternative build of the same library (build-time A/B of kernel constants)
+LIB_PATH = os.environ.get("CRANE_DYN_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libcrane_dyn.so")
 
 CRANE_TS_INVALID = -(2**63)
 CRANE_POD_DAEMONSET = 1

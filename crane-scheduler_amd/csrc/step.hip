@@ -127,7 +127,10 @@ constexpr int kK3sWaves = 4;
 constexpr int kK3sThreads = kK3sWaves * 64;
 constexpr int kK3sPPL = 4;                          // pods per lane
 constexpr int kK3sPods = kK3sThreads * kK3sPPL;     // pods per workgroup (= kPodTile)
-constexpr int kK3sS1 = 512;  // Step1 records staged per round and pod kind (8 KB)
+#ifndef CRANE_K3S_S1
+#define CRANE_K3S_S1 512  // build-time A/B knob
+#endif
+constexpr int kK3sS1 = CRANE_K3S_S1;  // Step1 records staged per round and pod kind (512: 8 KB)
 constexpr int kK3sVR = 32;   // VRec records staged per round and pod kind
 
 // position in the per-producer-block layout of element i of the concatenation
