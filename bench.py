@@ -1,23 +1,36 @@
-"""Benchmark of the Dynamic-plugin hot path on MI355X (BASELINE.json config 3 per GPU).
+"""Benchmark of the Dynamic-plugin hot path on MI355X (BASELINE.json configs).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3|4] [--no-cpu-baseline] [--no-extras]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-One step = one scheduling batch of the reference's hot path over one shard:
+Headline (the JSON line's `value`): one step = one scheduling batch of the
+reference's hot path over one node shard, keys-only (chosen node per pod):
   K2 hot values from the shard's 1M-entry binding log (binding.go:81-97, node.go:113-121)
   K1 node pass over the shard's parsed annotations (stats.go:51-112 pod-invariant parts)
   K3 Filter + Score + argmax for every (pod, node) pair (plugins.go:39-98, selectHost)
   RCCL int64 max all-reduce of the per-pod packed keys across node shards (N > 1)
-Each rank owns config 3's 100k nodes (node indices rank*100k + i) and every
-rank scores the same 10k pods: weak scaling, value = pods * total nodes / step.
+Config 3 (default): each rank owns 100k nodes, all ranks score the same 10k pods
+(weak scaling).  Config 4: the 1M nodes are split over the ranks, 100k pods
+(strong scaling).  `value` counts pairs resolved per second: every (pod, node)
+pair's Filter + Score is decided exactly, but the step path only evaluates a
+node per pod where one of its expiries falls inside the batch,
+so it is a full-rescan-equivalent rate.  The true per-pair rate (every pair's
+result materialised in HBM) is the `matrix_*` legs' `evals_per_s`.
 Inputs are resident in HBM before timing; data is synthetic (crane_dyn/synth.py).
+
+Kernel times are the kernels' own dispatch-stamped durations
+(crane_dyn_set_profiling), the quantity rocprofv3 --kernel-trace reports.
 """
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -29,26 +42,92 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
-# engine stage name -> kernel name in the rocprofv3 PMC summary (templates: prefix + suffix)
-STAGE_KERNEL = {
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+PMC_DIR = os.path.join(ROOT, "profiles", "pmc")
+DROPIN = os.path.join(ROOT, "crane-scheduler_amd", "lib", "dropin_bench")
+# kernel timer name -> rocprofv3 kernel name (prefix, suffix) for the PMC lookup
+KERNEL_PMC = {
     "k1_node_pass+k3a_steps": ("crane::k1_node_pass<", "true>"),
     "k1_node_pass": ("crane::k1_node_pass<", "false>"),
-    "k2x_partition": ("crane::k2x_partition", None),
-    "k2x_partition+k3p_pods": ("crane::k2x_pods", None),
-    "k2x_dedupe+k3p_pods": ("crane::k2x_dedupe_pods", None),
-    "k2x_dedupe": ("crane::k2x_dedupe", None),
-    "k2y_bin_hist": ("crane::k2y_bin_hist", None),
-    "k3p_pods": ("crane::k3p_pods", None),
+    "k2x_dedupe+k3p_pods": ("crane::k2x_dedupe_pods", ""),
+    "k2x_dedupe": ("crane::k2x_dedupe", ""),
+    "k3p_pods": ("crane::k3p_pods", ""),
+    "k3s_eval": ("crane::k3s_eval<", ">"),
+    "k3m_matrix+keys": ("crane::k3m_matrix<", "true, true>"),
+    "k3m_matrix": ("crane::k3m_matrix<", "true, false>"),
 }
 
 
-def _stage_match(name, kernel):
-    pre, suf = STAGE_KERNEL.get(name, (None, None))
-    if pre is None:
-        return False
-    return kernel == pre if suf is None else kernel.startswith(pre) and kernel.endswith(suf)
+def src_hash():
+    """Hash of every source the engine's kernels are built from: PMC summaries are valid for it only."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "crane-scheduler_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "crane-scheduler_amd", "csrc", "*.hpp")) +
+                   glob.glob(os.path.join(ROOT, "crane-scheduler_amd", "csrc", "*.cpp")) +
+                   glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:12]
+
+
+def pmc_summary(config, shash):
+    """PMC summary of this config taken on these kernel sources (tools/gpu_pmc.sh), or None."""
+    p = os.path.join(PMC_DIR, f"config{config}_{shash}.json")
+    return (json.load(open(p)), os.path.relpath(p, ROOT)) if os.path.exists(p) else (None, None)
+
+
+def pmc_traffic(pmc, name):
+    if not pmc or name not in KERNEL_PMC:
+        return None
+    pre, suf = KERNEL_PMC[name]
+    hits = [v for k, v in pmc.get("kernels", {}).items()
+            if k.startswith(pre) and k.endswith(suf) and (suf or k == pre) and "traffic_bytes" in v]
+    return int(hits[0]["traffic_bytes"]) if hits else None
+
+
+def effective_cpus():
+    """CPUs this process may use: its affinity mask, capped by a cgroup v2 quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def roof(alg_bytes, ms, what, traffic=None, extra=None):
+    gbs = alg_bytes / (ms * 1e-3) / 1e9
+    r = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(gbs / HBM_PEAK_GBS, 4), "ms": round(ms, 4), "alg_bytes": int(alg_bytes), "bytes": what,
+         "traffic": traffic}
+    if extra:
+        r.update(extra)
+    return r
+
+
+def kernel_times(eng, fn, reps):
+    """Mean dispatch-stamped duration per kernel name over `reps` calls of fn()."""
+    acc = {}
+    eng.set_profiling(True)
+    for _ in range(reps):
+        fn()
+        for name, t in eng.stage_times():
+            acc.setdefault(name, []).append(t)
+    eng.set_profiling(False)
+    return {k: float(np.mean(v)) for k, v in acc.items()}
 
 
 def parse():
@@ -56,14 +135,166 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, choices=(3, 4))
     ap.add_argument("--cpu-pods", type=int, default=1920, help="pods in the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16, help="upstream kube-scheduler parallelism")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-greedy", action="store_true", help="skip the config-5 sequential-greedy measurement")
+    ap.add_argument("--no-extras", action="store_true", help="headline step only (matrix / drop-in / controller legs off)")
+    ap.add_argument("--leg", default="all", choices=("all", "matrix2", "matrix3"),
+                    help="matrix2 / matrix3: only that per-pair leg (for per-kernel PMC passes)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as a captured graph (measured slower than eager launches on ROCm 7.2)")
     return ap.parse_args()
+
+
+# ------------------------------------------------------------------ legs
+def matrix_leg(cd, spec, dev, stream, label, val, ts, hv, hv_ts, now, ds, steps, pmc=None):
+    """Per-pair path: the full first-fail and score matrices (int8, [P][N] in HBM) and the
+    chosen node of every pod, one K3m launch per batch (node records resident: the node pass
+    runs once per snapshot sync)."""
+    N, P = val.shape[1], len(now)
+    eng = cd.Engine(cd.Policy(spec), dev.index)
+    eng.upload_nodes(val, ts, hv, hv_ts)
+    d_now = torch.from_numpy(now).to(dev)
+    d_flags = torch.from_numpy(ds).to(dev)
+    d_ff = torch.empty((P, N), dtype=torch.int8, device=dev)
+    d_sc = torch.empty((P, N), dtype=torch.int8, device=dev)
+    d_keys = torch.empty(P, dtype=torch.int64, device=dev)
+    sh = stream.cuda_stream
+    t1 = time.perf_counter()
+    eng.node_pass_async(sh)
+    stream.synchronize()
+    sync_ms = (time.perf_counter() - t1) * 1e3
+
+    def step():
+        eng.eval_matrix_async(d_now, d_flags, d_ff, d_sc, d_keys, stream=sh)
+
+    for _ in range(3):
+        step()
+    stream.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    stream.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    kt = kernel_times(eng, step, max(3, steps // 2))
+    # the chosen nodes agree with the keys-only step path on the same batch
+    d_k2 = torch.empty(P, dtype=torch.int64, device=dev)
+    eng.eval_keys_async(d_now, d_flags, d_k2, sh)
+    stream.synchronize()
+    same = bool(torch.equal(d_keys, d_k2))
+    pd_, pr_ = len(spec["predicate"]), len(spec["priority"])
+    pd_, pr_ = (4, 6) if pd_ <= 4 and pr_ <= 6 else ((8, 8) if pd_ <= 8 and pr_ <= 8 else (16, 16))
+    rec = -(-(24 + 16 * pr_ + 8 * pd_) // 16) * 16  # sizeof(NodeRec<PD, PR>)
+    kname = "k3m_matrix+keys"
+    kms = kt.get(kname, ms)
+    alg = N * rec + P * (8 + 1 + 8) + 2 * P * N
+    r = roof(alg, kms, "node records read once + pod now/flag read + keys + first-fail and score matrices "
+                       "(int8) written", pmc_traffic(pmc, kname), {"kernel": kname})
+    eff = P * N * 112 / (kms * 1e-3) / 1e9
+    out = {"workload": label, "nodes": N, "pods": P, "ms": round(ms, 4), "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
+           "evals_per_s": round(P * N / (ms * 1e-3), 1), "kernel_evals_per_s": round(P * N / (kms * 1e-3), 1),
+           "placements_per_s": round(P / (ms * 1e-3), 1), "roofline": r,
+           "effective_GBps_112B_per_eval": round(eff, 1),
+           "node_pass_ms_per_sync": round(sync_ms, 3), "chosen_equal_step_path": same,
+           "outputs": "first_fail int8 [P][N], score int8 [P][N], keys int64 [P] (device)"}
+    eng.close()
+    del d_ff, d_sc
+    return out
+
+
+def dropin_leg(cd, spec, ann, now, ds, ref_chosen, threads):
+    """Per-pod cycle of the C++ plugin mirror as the framework drives it (tools/dropin_bench.cpp)."""
+    if not os.path.exists(DROPIN):
+        return {"error": f"{DROPIN} not built"}
+    with tempfile.TemporaryDirectory() as d:
+        pol = {"apiVersion": "scheduler.policy.crane.io/v1alpha1", "kind": "DynamicSchedulerPolicy",
+               "spec": {"syncPolicy": [{"name": n, "period": f"{p // 10**9}s"} for n, p in spec["syncPolicy"]],
+                        "predicate": [{"name": n, "maxLimitPecent": v} for n, v in spec["predicate"]],
+                        "priority": [{"name": n, "weight": v} for n, v in spec["priority"]],
+                        "hotValue": [{"timeRange": f"{t // 10**9}s", "count": c} for t, c in spec["hotValue"]]}}
+        pp = os.path.join(d, "policy.json")
+        json.dump(pol, open(pp, "w"))
+        sp = os.path.join(d, "snap.tsv")
+        with open(sp, "w") as f:
+            for i, a in enumerate(ann):
+                f.write(f"N\tnode-{i}\n")
+                for k, v in a.items():
+                    f.write(f"A\t{k}\t{v}\n")
+        pd = os.path.join(d, "pods.tsv")
+        with open(pd, "w") as f:
+            for p in range(len(now)):
+                f.write(f"P\tpod-{p}\t{int(now[p])}\t{int(ds[p])}\n")
+        env = dict(os.environ, TZ="Asia/Shanghai")
+        r = subprocess.run([DROPIN, pp, sp, pd, str(threads)], capture_output=True, text=True, timeout=600, env=env)
+    if r.returncode != 0:
+        return {"error": r.stderr[-500:]}
+    o = json.loads(r.stdout.strip().splitlines()[-1])
+    ch = o.pop("chosen")
+    o["matches_engine_chosen"] = bool(np.array_equal(np.array(ch), ref_chosen))
+    o["dropin_ms_per_pod"] = o["cycle_ms_median"]
+    o["workload"] = (f"{o['nodes']} nodes x {o['pods']} pods, one scheduling cycle per pod: Filter on every node + "
+                     f"Score on every feasible node from {o['threads']} threads + selectHost, through "
+                     "include/crane_dyn_plugin.hpp (per-cycle int8 rows from crane_dyn_eval_compact)")
+    return o
+
+
+def controller_leg(cd, O, synth, spec, dev, c, N, B):
+    """Controller per-sync hot values (node.go:113-121 over binding.go:81-123) with the
+    engine keeping BindingRecords: append one second of bindings (the synthetic log's rate)
+    + BindingsGC + K2/K1 + readback, host wall incl. the H2D of the appended slots; and the
+    full-replace form (12 B x B uploaded per sync)."""
+    eng = cd.Engine(cd.Policy(spec), dev.index)
+    val, ts, _ = c.rows(eng.metric_names)
+    eng.upload_nodes(val, ts, c.hv, c.hv_ts)
+    gc = max(tr for tr, _ in spec["hotValue"])  # controller.go:57
+    eng.binding_records(B, gc)
+    eng.add_bindings(c.b_node, c.b_ts)
+    rng = np.random.default_rng(5)
+    per_s = max(1, B // 600)
+    ops, nodes, args = [np.zeros(B, np.uint8)], [c.b_node], [c.b_ts]
+    reps = []
+    for s in range(1, 7):
+        bn = c.b_node[rng.integers(0, B, per_s)]
+        bt = np.full(per_s, synth.NOW0 + s, np.int64)
+        now_ns = (synth.NOW0 + s) * 10**9
+        t1 = time.perf_counter()
+        eng.add_bindings(bn, bt)
+        eng.gc_bindings(now_ns)
+        eng.refresh_hot_values(now_ns, now_ns)
+        hv = eng.hot_values()
+        if s > 1:
+            reps.append(time.perf_counter() - t1)
+        ops += [np.zeros(per_s, np.uint8), np.ones(1, np.uint8)]
+        nodes += [bn, np.zeros(1, np.int32)]
+        args += [bt, np.array([synth.NOW0 + s], np.int64)]
+    t1 = time.perf_counter()
+    on, ot = O.binding_heap(B, gc, np.concatenate(ops), np.concatenate(nodes), np.concatenate(args))
+    _, ohv = O.hot_values(spec, on, ot, N, synth.NOW0 + 6)
+    ocpu = time.perf_counter() - t1
+    ok = bool(np.array_equal(hv, ohv.astype(np.float64))) and eng.binding_count() == len(on)
+    # full replace of the log per sync (upload + K2 + K1 + readback)
+    now_ns = int(synth.NOW0_NS)
+    full = []
+    for r in range(4):
+        t1 = time.perf_counter()
+        eng.upload_bindings(c.b_node, c.b_ts)
+        eng.refresh_hot_values(now_ns, now_ns)
+        eng.hot_values()
+        if r:
+            full.append(time.perf_counter() - t1)
+    eng.close()
+    return {"workload": f"{B}-entry BindingRecords heap -> {N} node hot values per controller sync",
+            "append_sync_ms": round(float(np.median(reps)) * 1e3, 3),
+            "append_sync": f"add {per_s} bindings + BindingsGC + K2/K1 + D2H of the hot values, host wall "
+                           "(incl. the H2D of the changed log slots)",
+            "full_replace_sync_ms": round(float(np.median(full)) * 1e3, 3),
+            "full_replace_sync": f"upload all {B} bindings (12 MB H2D) + K2/K1 + D2H, host wall",
+            "oracle_cpu_ms": round(ocpu * 1e3, 2),
+            "oracle": "C restatement of the container/heap BindingRecords replay + one pass over the heap "
+                      "(the reference scans the heap once per node: O(N*B))",
+            "matches_oracle": ok}
 
 
 def main():
@@ -80,11 +311,26 @@ def main():
     import crane_dyn as cd
     from crane_dyn import synth
 
+    shash = src_hash()
+    spec = cd.default_policy_spec()
+    if args.leg != "all":
+        stream = torch.cuda.Stream(dev)
+        torch.cuda.set_stream(stream)
+        cid = 2 if args.leg == "matrix2" else 3
+        cm = synth.make_cluster(spec, synth.CONFIGS[cid]["nodes"], synth.CONFIGS[cid]["pods"], seed=20250215 + cid)
+        names = cd.Engine(cd.Policy(spec), local).metric_names
+        vm, tm, _ = cm.rows(names)
+        pmc_m, _ = pmc_summary("2" if cid == 2 else "3m", shash)
+        out = matrix_leg(cd, spec, dev, stream, f"config{cid} full matrices", vm, tm, cm.hv, cm.hv_ts, cm.now, cm.ds,
+                         args.steps, pmc_m)
+        print(json.dumps({"leg": args.leg, "src_hash": shash, **out}), flush=True)
+        return
+
     cfg = synth.CONFIGS[args.config]
     N, P, B = cfg["nodes"], cfg["pods"], cfg["bindings"]
-    if args.config == 4:  # 1M nodes x 100k pods over 8 GPUs: one rank holds N/8
-        N = N // 8
-    spec = cd.default_policy_spec()
+    strong = args.config == 4  # 1M nodes x 100k pods split over the ranks
+    if strong:
+        N = N // world
     c = synth.make_cluster(spec, N, P, n_bindings=B, seed=20250215 + args.config * 1000 + rank)
     # the pod batch is the same on every shard (only nodes and bindings are per rank)
     c.now, c.ds = synth.make_pods(P, seed=20250215 + args.config)
@@ -101,39 +347,17 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
-    def step(e=None, collective=True):
-        if e:
-            e[0].record(stream)
-        # K2 (k2x, k2y) + K3p on a second queue, then K1+K3a (fused node pass), K3s
-        eng.step_keys_async(now_sync, now_sync, d_now, d_flags, d_keys, sh)
-        if e:
-            e[1].record(stream)
+    def step(collective=True):
+        eng.step_keys_async(now_sync, now_sync, d_now, d_flags, d_keys, sh)  # K2x+K3p, K1+K3a, K3s
         if world > 1 and collective:
-            dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)       # RCCL over xGMI
-        if e:
-            e[2].record(stream)
+            dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)  # RCCL over xGMI
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    # per-stage times from eager passes: HIP events around the engine call, and the
-    # engine's own per-kernel events (crane_dyn_set_profiling; while it is on, the
-    # engine runs the step's kernels back to back on one queue)
-    eng.set_profiling(True)
-    stages = {}
-    for k in range(args.steps):
-        step(ev[k])
-        for name, t in eng.stage_times():
-            stages.setdefault(name, []).append(t)
-    eng.set_profiling(False)
-    torch.cuda.synchronize(dev)
     graph = None
     if args.graph:
-        # one scheduling batch = one graph replay: K2 + K1 + K3 launches captured once,
-        # inputs (pods, binding log, node SoA) stay in device buffers updated in place
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=stream):
             step(collective=False)
@@ -146,13 +370,13 @@ def main():
         else:
             graph.replay()
             if world > 1:
-                dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)  # RCCL over xGMI
+                dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(args.steps):
+    for _ in range(args.steps):
         timed_step()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -163,78 +387,74 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_step = elapsed * 1e3 / args.steps
-    step_ms_prof = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
-    ar_ms = float(np.mean([b.elapsed_time(c_) for _, b, c_ in ev]))
-    stage_ms = {k: float(np.mean(v)) for k, v in stages.items()}
-
     keys = d_keys.cpu().numpy()
-    evals = P * N * world
+    # per-kernel durations (dispatch-stamped) of the same step, outside the timed region
+    kt = kernel_times(eng, lambda: step(collective=False), args.steps)
+    ar_ms = None
+    if world > 1:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(10):
+            dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ar_ms = e0.elapsed_time(e1) / 10
+
+    evals = P * (N * world if not strong else N * world)
     value = evals / (ms_step / 1e3)
     placements = P / (ms_step / 1e3)
 
-    # Rooflines per kernel stage: ALGORITHMIC bytes per launch / the
-    # stage's mean duration from the engine's HIP events above.  The dominant stage is `roofline`.
+    # Rooflines per kernel: ALGORITHMIC bytes per launch / the kernel's
+    # mean dispatch-stamped duration.  K3s re-reads L2-resident step records: not HBM-priced.
     M = len(eng.metric_names)
     W = len(spec["hotValue"])
-    PD, PR = len(spec["predicate"]), len(spec["priority"])
-    pd_, pr_ = (4, 6) if PD <= 4 and PR <= 6 else ((8, 8) if PD <= 8 and PR <= 8 else (16, 16))
-    rec_bytes = -(-(24 + 16 * pr_ + 8 + 8 * pd_) // 16) * 16  # sizeof(NodeRec<PD,PR>)
-    max_tr_s = max(tr for tr, _ in spec["hotValue"]) // 10**9
-    b_in = int((c.b_ts > now_sync // 10**9 - max_tr_s).sum())  # bindings inside the widest window
-    # the fused keys-only node pass leaves the records in LDS (CRANE_K1_KEEP_REC=1 writes them)
-    keep_rec = os.environ.get("CRANE_K1_KEEP_REC") == "1"
-    k2x_b = B * 12 + b_in * 4
-    k3p_b = P * (8 + 1 + 4 + 8 + 8)
-    # dedupe-form K2: one 4-byte entry per distinct (2048-binding region, node, window rank),
-    # a (count, offset) pair per (node block, region); the node pass reads both
-    dedupe = os.environ.get("CRANE_K2", "dedupe") == "dedupe"
     cut = np.sort(np.array([now_sync // 10**9 - tr // 10**9 for tr, _ in spec["hotValue"]], np.int64))
     jr = (c.b_ts[:, None] > cut[None, :]).sum(1)
     okb = (jr > 0) & (c.b_node >= 0) & (c.b_node < N)
     reg = np.arange(B, dtype=np.int64) // 2048
+    # dedupe-form K2: one 4-byte entry per distinct (2048-binding region, node, window rank),
+    # a (count, offset) word per (node block, region); the node pass reads both
     E = int(np.unique((reg[okb] * (N + 1) + c.b_node[okb]) * 8 + jr[okb] - 1).size) if B else 0
-    k1_bs = int(os.environ.get("CRANE_K1_THREADS", "256"))
-    co_b = 8 * (-(-N // k1_bs)) * (-(-B // 2048))
+    co_b = 4 * (-(-N // 256)) * (-(-B // 2048))
+    k3p_b = P * (8 + 1 + 4 + 8 + 8)
     k2d_b = B * 12 + E * 4 + co_b
     alg = {
         "k2x_dedupe": (k2d_b, "bindings read + distinct (region, node, bucket) entries + count/offset written"),
         "k2x_dedupe+k3p_pods": (k2d_b + k3p_b, "bindings read + distinct entries + count/offset written; pod now + "
                                                "flag read, partition + keys written"),
-        "k2x_partition": (k2x_b, "bindings read (int32 node + int64 ts) + kept entries written"),
-        "k2x_partition+k3p_pods": (k2x_b + k3p_b, "bindings read + kept entries written; pod now + flag read, "
-                                                  "partition + keys written"),
-        "k2y_bin_hist": (b_in * 4 + 4 * W * N, "kept entries read + window counts added"),
-        "k1_node_pass+k3a_steps": ((N * (16 * M + 8 + (rec_bytes if keep_rec else 0))
-                                    + (E * 4 + co_b if dedupe else N * 8 * W)),
-                                   "SoA (value, ts) read + hot value written + "
-                                   + ("K2 entries and count/offset read" if dedupe else "buckets read and zeroed")
-                                   + (" + NodeRec written" if keep_rec else "")),
-        "k1_node_pass": (N * (16 * M + 8 * W + rec_bytes + 8), "SoA + buckets + NodeRec + hot value"),
+        "k1_node_pass+k3a_steps": (N * (16 * M + 8) + E * 4 + co_b,
+                                   "SoA (value, ts) read + hot value written + K2 entries and count/offset read"),
         "k3p_pods": (k3p_b, "pod now + flag read, partition + keys written"),
     }
+    pmc, pmc_src = pmc_summary(args.config, shash)
     roofs = {}
-    for name, t in stage_ms.items():
+    for name, t in kt.items():
         if name in alg and t > 0:
-            gbs = alg[name][0] / (t * 1e-3) / 1e9
-            roofs[name] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(gbs / HBM_PEAK_GBS, 4), "ms": round(t, 4),
-                           "alg_bytes": int(alg[name][0]), "bytes": alg[name][1]}
-    dom = max(stage_ms, key=stage_ms.get) if stage_ms else None
-    # HBM traffic per launch from the committed PMC summary of this bench
-    # (tools/gpu_pmc.sh: separate FETCH_SIZE / WRITE_SIZE passes, KiB, FETCH_SIZE x2 on gfx950)
-    pmc = {}
-    if os.path.exists(PMC_SUMMARY):
-        pmc = json.load(open(PMC_SUMMARY))
-    for name, e in roofs.items():
-        hits = [v for k, v in pmc.items() if _stage_match(name, k) and "traffic_bytes" in v]
-        e["traffic"] = int(hits[0]["traffic_bytes"]) if hits else None
-    roof = None
-    if dom in roofs:
-        roof = dict(roofs[dom], kernel=dom)
-        if roof.get("traffic") is not None:
-            roof["traffic_source"] = os.path.relpath(PMC_SUMMARY, ROOT)
-    elif dom:
-        roof = {"bound": None, "kernel": dom, "ms": round(stage_ms[dom], 4), "note": "no HBM roofline for this stage"}
+            roofs[name] = roof(alg[name][0], t, alg[name][1], pmc_traffic(pmc, name))
+    dom = max(kt, key=kt.get) if kt else None
+    rname = dom if dom in roofs else (max(roofs, key=lambda k: kt[k]) if roofs else None)
+    roofline = dict(roofs[rname], kernel=rname, dominant_kernel=dom) if rname else None
+    if roofline is not None:
+        roofline["traffic_source"] = pmc_src if roofline.get("traffic") is not None else None
+        if rname != dom:
+            roofline["note"] = (f"the longest kernel ({dom}, {kt[dom]:.4f} ms) re-reads L2-resident step records "
+                                "per pod tile and has no HBM roofline; this is the longest HBM-priced kernel")
+
+    extras = {}
+    if world == 1 and rank == 0 and not args.no_extras:
+        # BASELINE config 2 and the per-pair rate at config 3: every pair's result in HBM
+        c2 = synth.make_cluster(spec, synth.CONFIGS[2]["nodes"], synth.CONFIGS[2]["pods"], seed=20250215 + 2)
+        v2, t2, _ = c2.rows(eng.metric_names)
+        pmc2, _ = pmc_summary("2", shash)
+        extras["matrix_config2"] = matrix_leg(
+            cd, spec, dev, stream, "config2: 5000 nodes x 1000 pods, full first-fail + score matrices + chosen node",
+            v2, t2, c2.hv, c2.hv_ts, c2.now, c2.ds, max(args.steps, 20), pmc2)
+        if args.config == 3:
+            extras["matrix_config3"] = matrix_leg(
+                cd, spec, dev, stream, "config3 nodes/pods (100000 x 10000), node_hot_value annotations: full "
+                "first-fail + score matrices (2 x 1 GB int8) + chosen node", val, ts, c.hv, c.hv_ts, c.now, c.ds, 10,
+                pmc_summary("3m", shash)[0])
+
     greedy = None
     if world == 1 and not args.no_greedy:
         # BASELINE config 5: 100k nodes x 50k pods placed sequentially, each binding
@@ -260,30 +480,41 @@ def main():
         geng.close()
 
     cpu = None
-    host_parse = ctl = None
+    host_parse = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
-        cp = min(args.cpu_pods, P)
         ann = c.annotations()
-        t1 = time.perf_counter()
-        _, _, och = O.eval_strings(spec, ann, c.now[:cp], c.ds[:cp], threads=args.cpu_threads, want_matrix=False)
-        dt = time.perf_counter() - t1
-        cpu = {"value": round(cp * N / dt, 1), "unit": "pod-node evals/s", "cores": args.cpu_threads, "kind": "port",
-               "sample": f"{cp} pods x {N} nodes, string mode (re-parse every annotation per call like stats.go), "
-                         f"{args.cpu_threads} threads, {dt:.1f}s"}
-        # the stronger CPU data point, pre-parsed SoA (no string work per call)
+        ncpu = effective_cpus()
+        legs = {}
+        for label, th in (("threads_16", args.cpu_threads), ("threads_all", ncpu)):
+            cp = min(P, max(64, args.cpu_pods * th // args.cpu_threads))
+            t1 = time.perf_counter()
+            O.eval_strings(spec, ann, c.now[:cp], c.ds[:cp], threads=th, want_matrix=False)
+            dt = time.perf_counter() - t1
+            legs[label] = {"value": round(cp * N / dt, 1), "cores": th,
+                           "sample": f"{cp} pods x {N} nodes, {th} threads, {dt:.1f}s"}
         okr = c.rows(eng.metric_names)[2]
+        cp = min(P, args.cpu_pods)
         t1 = time.perf_counter()
         O.eval_soa(spec, eng.metric_names, okr, val, ts, np.ones(N, np.uint8), c.hv, c.hv_ts, c.now[:cp], c.ds[:cp],
                    threads=args.cpu_threads, want_matrix=False)
         dts = time.perf_counter() - t1
-        cpu["soa_mode"] = {"value": round(cp * N / dts, 1), "unit": "pod-node evals/s", "cores": args.cpu_threads,
-                           "sample": f"{cp} pods x {N} nodes, pre-parsed SoA, {dts:.1f}s"}
+        cpu = {"value": legs["threads_16"]["value"], "unit": "pod-node evals/s", "cores": args.cpu_threads,
+               "kind": "port",
+               "sample": f"{legs['threads_16']['sample']}; string mode: every Filter/Score call re-parses its "
+                         "annotations like stats.go:51-76 (oracle/crane_oracle.c)",
+               "cpu_model": cpu_model(), "nproc": os.cpu_count(), "effective_cpus": ncpu,
+               "all_cores": legs["threads_all"],
+               "note": "C restatement, not the Go plugin (no Go toolchain, SURVEY 8c); it resolves the fixed-offset "
+                       "zone once instead of utils.GetLocation's time.LoadLocation on every call (utils.go:35-45), "
+                       "so it is a stronger baseline than the reference",
+               "soa_mode": {"value": round(cp * N / dts, 1), "unit": "pod-node evals/s", "cores": args.cpu_threads,
+                            "sample": f"{cp} pods x {N} nodes, pre-parsed SoA, {dts:.1f}s"}}
         # the once-per-sync host parse of the same snapshot's annotation
         # strings into the SoA the engine uploads (crane_parse_annotations, C++ threads)
         snap = cd.SnapshotStrings(eng.metric_names, ann)
         host_parse = {"strings": len(snap), "nodes": N}
-        for label, th in (("threads_16", args.cpu_threads), ("threads_all", 0)):
+        for label, th in (("threads_16", args.cpu_threads), ("threads_all", ncpu)):
             snap.parse(synth.SHANGHAI, th)
             reps = []
             for _ in range(3):
@@ -291,40 +522,33 @@ def main():
                 snap.parse(synth.SHANGHAI, th)
                 reps.append(time.perf_counter() - t1)
             dtp = float(np.median(reps))
-            host_parse[label] = {"ms_per_sync": round(dtp * 1e3, 2), "strings_per_s": round(len(snap) / dtp, 1)}
-        # the controller's per-sync hot-value annotation pass
-        # (node.go:113-121 over binding.go:81-97) as K2+K1 plus the 8 B/node readback,
-        # checked bit-exact against the oracle's count over the full binding log
-        eng.refresh_hot_values(now_sync)
-        eng.hot_values()
-        reps = []
-        for _ in range(5):
-            t1 = time.perf_counter()
-            eng.refresh_hot_values(now_sync)
-            ghv = eng.hot_values()
-            reps.append(time.perf_counter() - t1)
-        t1 = time.perf_counter()
-        _, ohv = O.hot_values(spec, c.b_node, c.b_ts, N, now_sync // 10**9)
-        ocpu = time.perf_counter() - t1
-        ctl = {"workload": f"{B}-entry binding log -> {N} node hot values", "gpu_ms": round(float(np.median(reps)) * 1e3, 3),
-               "timing": "host wall incl. K2 + K1 + D2H of hot values", "oracle_cpu_ms": round(ocpu * 1e3, 2),
-               "oracle": "C restatement, one pass over the log (the reference scans the log once per node: O(N*B))",
-               "matches_oracle": bool(np.array_equal(ghv, ohv.astype(np.float64)))}
+            host_parse[label] = {"ms_per_sync": round(dtp * 1e3, 2), "strings_per_s": round(len(snap) / dtp, 1),
+                                 "threads": th}
         pv, pt, _, _ = snap.soa()
-        okm = c.rows(eng.metric_names)[2].astype(bool)
+        okm = okr.astype(bool)
         host_parse["matches_generator_soa"] = bool(np.array_equal(pt[okm], ts[okm]) and np.array_equal(pv[okm],
                                                                                                        val[okm]))
+        if not args.no_extras and args.config == 3:
+            # the drop-in plugin cycle, and the controller's hot-value sync
+            ae = _annot_engine(cd, spec, local, val, ts, c)
+            _, _, ref_ch, _ = ae.eval(c.now[:64], c.ds[:64])
+            ae.close()
+            extras["dropin"] = dropin_leg(cd, spec, ann, c.now[:64], c.ds[:64], ref_ch, args.cpu_threads)
+            extras["controller_hot_values"] = controller_leg(cd, O, synth, spec, dev, c, N, B)
+
     if rank == 0:
         line = {
             "metric": "pod-node filter+score evals/sec",
             "value": round(value, 1),
             "unit": "evals/s",
+            "value_kind": "pairs resolved per second, full-rescan equivalent (step path: keys only; the per-pair "
+                          "rate with every pair's result in HBM is matrix_*.evals_per_s)",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
@@ -333,20 +557,29 @@ def main():
                        "nodes_per_gpu": N, "pods": P, "bindings_per_gpu": B, "parallelism": f"node-shard x{world}",
                        "launch": "eager" if graph is None else "hipGraph replay per batch"},
             "placements_per_s": round(placements, 1),
-            "kernel_ms": {"step_profiled_serial": round(step_ms_prof, 4), "allreduce": round(ar_ms, 4)},
-            "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
-            "roofline": roof,
-            "roofline_stages": roofs,
+            "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
+            "allreduce_ms": None if ar_ms is None else round(ar_ms, 4),
+            "roofline": roofline,
+            "roofline_kernels": roofs,
+            "src_hash": shash,
             "cpu_baseline": cpu,
             "greedy": greedy,
             "host_parse": host_parse,
-            "controller_hot_values": ctl,
             "chosen_sample": [int(x) for x in keys[:4]],
         }
+        line.update(extras)
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def _annot_engine(cd, spec, device, val, ts, c):
+    """An engine holding the snapshot with its node_hot_value annotations (no binding log),
+    as the plugin mirror syncs it."""
+    e = cd.Engine(cd.Policy(spec), device)
+    e.upload_nodes(val, ts, c.hv, c.hv_ts)
+    return e
 
 
 if __name__ == "__main__":

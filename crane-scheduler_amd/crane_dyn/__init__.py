@@ -12,8 +12,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# CRANE_DYN_LIB: an alternative build of the same library (build-time A/B of kernel constants)
-LIB_PATH = os.environ.get("CRANE_DYN_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libcrane_dyn.so")
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libcrane_dyn.so")
 
 CRANE_TS_INVALID = -(2**63)
 CRANE_POD_DAEMONSET = 1
@@ -63,6 +62,16 @@ def _load():
         "crane_dyn_metric_name": (C.c_char_p, [vp, C.c_int32]),
         "crane_dyn_upload_nodes": (C.c_int, [vp, C.c_int64, C.c_int64, vp, vp, vp, vp]),
         "crane_dyn_upload_bindings": (C.c_int, [vp, C.c_int64, vp, vp]),
+        "crane_dyn_binding_records": (C.c_int, [vp, C.c_int64, C.c_int64]),
+        "crane_dyn_add_bindings": (C.c_int, [vp, C.c_int64, vp, vp]),
+        "crane_dyn_gc_bindings": (C.c_int, [vp, C.c_int64]),
+        "crane_dyn_binding_count": (C.c_int64, [vp]),
+        "crane_dyn_eval_compact": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, vp]),
+        "crane_dyn_eval_matrix_async": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, C.c_int64, vp, vp]),
+        "crane_dyn_set_option": (C.c_int, [vp, C.c_char_p, C.c_int64]),
+        "crane_translate_event": (C.c_int, [C.c_char_p, C.c_size_t, C.c_int32, C.c_int64, C.c_int64, P(C.c_char_p),
+                                            P(C.c_size_t), P(C.c_char_p), P(C.c_size_t), P(C.c_char_p),
+                                            P(C.c_size_t), P(C.c_int64)]),
         "crane_dyn_refresh_hot_values": (C.c_int, [vp, C.c_int64, C.c_int64]),
         "crane_dyn_hot_values": (C.c_int, [vp, C.c_int64, vp]),
         "crane_dyn_eval": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, vp]),
@@ -93,7 +102,9 @@ ABI_SYMBOLS = (
     "crane_dyn_refresh_hot_values", "crane_dyn_eval", "crane_dyn_eval_keys_async", "crane_dyn_step_keys_async",
     "crane_dyn_refresh_hot_values_async", "crane_dyn_node_pass_async", "crane_dyn_greedy", "crane_dyn_key_node",
     "crane_dyn_set_profiling", "crane_dyn_stage_times", "crane_dyn_hot_values",
-    "crane_dyn_version",
+    "crane_dyn_version", "crane_dyn_binding_records", "crane_dyn_add_bindings", "crane_dyn_gc_bindings",
+    "crane_dyn_binding_count", "crane_dyn_eval_compact", "crane_dyn_eval_matrix_async", "crane_dyn_set_option",
+    "crane_translate_event",
 )
 
 
@@ -230,6 +241,24 @@ def parse_nodes(metric_names, nodes, tz_offset_s, threads=0):
     return snap.soa()
 
 
+def translate_event(message: str, count: int, event_time_ns: int, last_timestamp_ns: int):
+    """translateEventToBinding (event.go:118-145): (namespace, pod, node, Timestamp) or None."""
+    b = message.encode()
+    node, ns, pod = C.c_char_p(), C.c_char_p(), C.c_char_p()
+    nl, nsl, pl, ts = C.c_size_t(), C.c_size_t(), C.c_size_t(), C.c_int64()
+    buf = C.create_string_buffer(b, len(b))
+    rc = lib.crane_translate_event(buf, len(b), count, event_time_ns, last_timestamp_ns, C.byref(node), C.byref(nl),
+                                   C.byref(ns), C.byref(nsl), C.byref(pod), C.byref(pl), C.byref(ts))
+    if rc:
+        return None
+    base = C.addressof(buf)
+
+    def get(p, n):
+        off = C.cast(p, C.c_void_p).value - base
+        return b[off:off + n.value].decode("utf-8", "surrogateescape")
+    return get(ns, nsl), get(pod, pl), get(node, nl), ts.value
+
+
 def key_node(key: int):
     s = C.c_int64()
     n = lib.crane_dyn_key_node(int(key), C.byref(s))
@@ -286,6 +315,27 @@ class Engine:
             raise ValueError("node/ts_s length mismatch")
         self._check(lib.crane_dyn_upload_bindings(self.h, len(node), _ptr(node), _ptr(ts_s)))
 
+    # BindingRecords kept by the engine (binding.go:50-123)
+    def binding_records(self, size, gc_time_range_ns):
+        self._check(lib.crane_dyn_binding_records(self.h, int(size), int(gc_time_range_ns)))
+
+    def add_bindings(self, node, ts_s):
+        node = np.ascontiguousarray(node, np.int32)
+        ts_s = np.ascontiguousarray(ts_s, np.int64)
+        if node.shape != ts_s.shape:
+            raise ValueError("node/ts_s length mismatch")
+        self._check(lib.crane_dyn_add_bindings(self.h, len(node), _ptr(node), _ptr(ts_s)))
+
+    def gc_bindings(self, now_ns):
+        self._check(lib.crane_dyn_gc_bindings(self.h, int(now_ns)))
+
+    def binding_count(self):
+        return lib.crane_dyn_binding_count(self.h)
+
+    def set_option(self, name, value):
+        """Alternative kernel forms of the same results (tests / A-B only), see crane_dyn.h."""
+        self._check(lib.crane_dyn_set_option(self.h, name.encode(), int(value)))
+
     def refresh_hot_values(self, now_ns, hv_ts_ns=None):
         self._check(lib.crane_dyn_refresh_hot_values(self.h, int(now_ns), int(now_ns if hv_ts_ns is None else hv_ts_ns)))
 
@@ -295,19 +345,29 @@ class Engine:
         self._check(lib.crane_dyn_hot_values(self.h, self.n_nodes, _ptr(out)))
         return out
 
-    def eval(self, now_ns, pod_flags=None, matrix=False):
-        """Returns (first_fail[P,N] or None, score[P,N] or None, chosen[P], chosen_score[P])."""
+    def eval(self, now_ns, pod_flags=None, matrix=False, compact=False):
+        """Returns (first_fail[P,N] or None, score[P,N] or None, chosen[P], chosen_score[P]);
+        compact: int8 scores (crane_dyn_eval_compact)."""
         now = np.ascontiguousarray(now_ns, np.int64).reshape(-1)
         P, N = len(now), self.n_nodes
         fl = None if pod_flags is None else np.ascontiguousarray(pod_flags, np.uint8).reshape(-1)
         if fl is not None and len(fl) != P:
             raise ValueError("pod_flags length mismatch")
         ff = np.empty((P, N), np.int8) if matrix else None
-        sc = np.empty((P, N), np.int64) if matrix else None
+        sc = np.empty((P, N), np.int8 if compact else np.int64) if matrix else None
         ch = np.empty(P, np.int64)
         cs = np.empty(P, np.int64)
-        self._check(lib.crane_dyn_eval(self.h, P, _ptr(now), _ptr(fl), _ptr(ff), _ptr(sc), _ptr(ch), _ptr(cs)))
+        fn = lib.crane_dyn_eval_compact if compact else lib.crane_dyn_eval
+        self._check(fn(self.h, P, _ptr(now), _ptr(fl), _ptr(ff), _ptr(sc), _ptr(ch), _ptr(cs)))
         return ff, sc, ch, cs
+
+    def eval_matrix_async(self, d_now, d_flags, d_ff, d_score, d_keys=None, ld=None, stream=None):
+        """Device matrices (torch int8 [P][ld], either may be None) and optional keys int64[P]."""
+        P = d_now.numel()
+        ld = self.n_nodes if ld is None else ld
+        vp = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+        self._check(lib.crane_dyn_eval_matrix_async(self.h, P, vp(d_now), vp(d_flags), vp(d_ff), vp(d_score), ld,
+                                                    vp(d_keys), stream))
 
     # device-resident pipeline (torch tensors on the engine's device)
     def refresh_hot_values_async(self, now_ns, hv_ts_ns, stream=None):

@@ -45,7 +45,8 @@ def allreduce_keys(keys, group=None):
 
 
 class ShardedEngine:
-    """One rank's shard: an Engine holding nodes [lo, hi) of a cluster, plus the combine step."""
+    """One rank's shard: an Engine holding nodes [lo, hi) of a cluster (global indices in
+    its keys), the bindings of those nodes, and the combine step."""
 
     def __init__(self, policy, n_nodes_total, world, rank, device=0):
         from crane_dyn import Engine
@@ -62,6 +63,18 @@ class ShardedEngine:
             m = (b_node >= lo) & (b_node < hi)
             self.engine.upload_bindings((b_node[m] - lo).astype(np.int32), b_ts[m])
 
-    def schedule(self, d_now, d_flags, d_keys, stream=None, group=None):
+    def step_keys(self, now_ns, hv_ts_ns, d_now, d_flags, d_keys, stream=None):
+        """This shard's keys for the pod batch: hot values from its bindings, then Filter + Score + argmax."""
+        self.engine.step_keys_async(now_ns, hv_ts_ns, d_now, d_flags, d_keys, stream)
+
+    def eval_keys(self, d_now, d_flags, d_keys, stream=None):
+        """This shard's keys with the current hot values."""
         self.engine.eval_keys_async(d_now, d_flags, d_keys, stream)
+
+    def schedule(self, now_ns, hv_ts_ns, d_now, d_flags, d_keys, stream=None, group=None):
+        """One batch across all ranks: local step, then the MAX all-reduce (the global choice)."""
+        self.step_keys(now_ns, hv_ts_ns, d_now, d_flags, d_keys, stream)
         return allreduce_keys(d_keys, group)
+
+    def close(self):
+        self.engine.close()

@@ -47,34 +47,14 @@ struct DevPolicy {
 // key, malformed value, negative value) and, for predicates, "not over the
 // limit" — so predicate k fails iff now < e_pred[k], and the Filter rejects
 // iff now < e_fail = max_k e_pred[k] (some overloaded predicate is fresh).
-// The hot part (first) is all the pod x node kernel reads on its fast path.
 template <int PD, int PR>
 struct alignas(16) NodeRec {
-    // --- hot
     int64_t e_fail;      // max over overloaded predicates of ts+dur, INT64_MIN if none
     int64_t e_hv;        // hot value annotation ts + 5m, INT64_MIN if unusable
-    int32_t pen32;       // int(hotValue*10) when 0 <= it < 2^30 (fast path), else 0
-    int32_t flags;       // kRecSlow: take the exact int64 path for this node
+    int64_t pen;         // int(hotValue * 10), plugins.go:91
     int64_t e_prio[PR];  // ts+dur of the priority's metric, INT64_MIN if unusable
     double t[PR];        // ((1 - usage) * weight) * 100, stats.go:89 (no FMA)
-    // --- cold (first-fail outputs and the exact path)
-    int64_t pen;         // int(hotValue * 10), plugins.go:91
     int64_t e_pred[PD];  // ts+dur if usage > maxLimitPecent (and limit != 0), else INT64_MIN
 };
-
-// NodeRec.flags: a term is non-finite, pen is outside [0, 2^30), or the policy
-// has no priorities.
-constexpr int32_t kRecSlow = 1;
-// K3 fast path: |int(score/weight)| < 2^30 and 0 <= pen < 2^30, so the
-// reference's int64 "score - pen" cannot wrap and fits in int32.
-constexpr double kFastLim = 1073741824.0;
-// Exact int(score/weight) without a division (K3 "threshold" path, weight sum
-// W > 0): T[k] = smallest double s with RN(s/W) >= k, k = 1..kQMax+1, T[0] =
-// -inf.  trunc(s * RN(1/W)) is within 1 of trunc(RN(s/W)), and two compares
-// against T fix it up.  Lanes with s * RN(1/W) >= kQFast take the exact path.
-constexpr int kQMax = 127;
-constexpr double kQFast = 125.0;
-// K1 marks a node slow when a term is this large, keeping the sum finite.
-constexpr double kTermMax = 1152921504606846976.0;  // 2^60
 
 }  // namespace crane

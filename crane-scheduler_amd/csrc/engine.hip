@@ -4,9 +4,10 @@
 // Reference mapping (/root/reference):
 //   crane_dyn_create      NewDynamicScheduler      pkg/plugins/dynamic/plugins.go:105-120
 //   policy flattening     getActiveDuration        pkg/plugins/dynamic/stats.go:140-150
-//   crane_dyn_eval        Filter + Score + select  plugins.go:39-98 (+ upstream selectHost)
+//   crane_dyn_eval*       Filter + Score + select  plugins.go:39-98 (+ upstream selectHost)
 //   refresh_hot_values    GetLastNodeBindingCount  pkg/controller/annotator/binding.go:81-97
 //                         annotateNodeHotValue     pkg/controller/annotator/node.go:113-121
+//   binding records       BindingRecords heap      binding.go:50-123 (bindings.cpp)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -19,6 +20,7 @@
 #include <vector>
 
 #include "../../include/crane_dyn.h"
+#include "bindings.hpp"
 #include "dyn_types.hpp"
 #include "kernels.hpp"
 
@@ -49,6 +51,30 @@ struct DevBuf {
     }
 };
 
+// pinned host staging (D2H of the matrix rows, H2D of binding-record slots)
+template <typename T>
+struct HostBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t reserve(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        if (p) {
+            hipError_t e = hipHostFree(p);
+            p = nullptr;
+            n = 0;
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipHostMalloc((void**)&p, std::max<size_t>(want, 1) * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = std::max<size_t>(want, 1);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
 // Go: int64(d.Seconds()) (binding.go:85)
 int64_t go_seconds_trunc(int64_t d) {
     const int64_t sec = d / 1000000000LL, nsec = d % 1000000000LL;
@@ -63,15 +89,33 @@ int64_t floor_div(int64_t a, int64_t b) {
     return q;
 }
 
+// Engine options: fixed defaults; crane_dyn_set_option changes them per engine
+// (tests and A/B tools only — nothing reads the environment).
+struct Options {
+    int k2_form = 0;          // 0: dedupe (binned / hash when it does not fit), 1: binned, 2: hash
+    int k1_threads = 256;     // K1 workgroup size (the dedupe K2 bins nodes by it): 128 or 256
+    bool k1_keep_rec = false; // the fused keys-only step also writes the node records
+    bool k1_fuse = true;      // K3a (step tables) fused into the node pass
+    bool k3p_in_k2 = true;    // K3p rides as extra workgroups of the K2x launch
+    int keys_path = 0;        // 0: step path when it applies, 1: the per-pair kernel (K3m keys)
+    int greedy_form = 0;      // 0: merge form when every hotValue count > 0, 1: sequential kernel
+};
+
 }  // namespace
+
+struct crane_dyn;
+
+struct EngineTimer final : KernelTimer {
+    crane_dyn* h = nullptr;
+    void next(const char* name, hipEvent_t* start, hipEvent_t* stop) override;
+};
 
 struct crane_dyn {
     std::mutex mu;
     std::string err;
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;  // second queue: K3p overlaps K2 in crane_dyn_step_keys_async
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    Options opt;
     // policy
     DevPolicy dp{};
     int shape = kShape16x16;
@@ -86,11 +130,16 @@ struct crane_dyn {
     bool hv_from_counts = false;
     int64_t hv_ts_counts = 0;
     bool rec_dirty = true;
-    bool buckets_zero = false;  // K1 consumes (zeroes) the buckets K2 filled
+    bool buckets_zero = false;    // K1 consumes (zeroes) the buckets K2 filled
     bool counts_pending = false;  // buckets hold K2 counts no node pass has consumed yet
     bool hx_pending = false;      // ... in the dedupe form: per-block entries in k2_sorted (hx_g)
     HotPart hx_g{};
+    // binding log on the device: B slots (node < 0 = empty slot)
     int64_t B = 0;
+    BindingHeap heap;             // BindingRecords restatement (crane_dyn_binding_records mode)
+    bool heap_mode = false;
+    HostBuf<int32_t> hnode;       // pinned mirror of the slots in heap mode
+    HostBuf<int64_t> hts;
     DevBuf<double> val, hv;
     DevBuf<int64_t> ts, hv_ts;
     DevBuf<unsigned char> rec;
@@ -103,7 +152,10 @@ struct crane_dyn {
     DevBuf<long long> keys;
     DevBuf<int8_t> ff;
     DevBuf<int64_t> score;
-    DevBuf<uint32_t> k2_cnt, k2_tot, k2_sorted;  // bin-partitioned K2 scratch
+    DevBuf<int8_t> score8;
+    HostBuf<int8_t> stage8;
+    HostBuf<long long> stagek;
+    DevBuf<uint32_t> k2_cnt, k2_tot, k2_sorted;  // K2 scratch
     DevBuf<double> hvc;                           // [N] binding-log hot values of the last consuming K1
     DevBuf<uint32_t> gcnt;  // greedy: per-window counts [W][N]
     DevBuf<int64_t> gbase, gchosen;
@@ -115,13 +167,13 @@ struct crane_dyn {
     DevBuf<int64_t> stile, spnow;
     DevBuf<unsigned char> svrec;
     DevBuf<Step1> sstep1;
-    DevBuf<double> thr;  // quotient thresholds (K3 division-free path), empty if unusable
-    double inv_w = 0.0;
-    // stage timing (crane_dyn_set_profiling)
+    // kernel timing (crane_dyn_set_profiling)
     bool prof = false;
-    std::vector<hipEvent_t> ev;    // pool
-    std::vector<const char*> ev_name;  // ev_name[i]: stage ending at event i (ev_name[0] unused)
-    int nev = 0;
+    EngineTimer timer;
+    std::vector<hipEvent_t> ev;           // pool, two per timed launch
+    std::vector<const char*> ev_name;     // ev_name[i]: kernel of events 2i, 2i + 1
+    int nk = 0;
+    hipError_t timer_err = hipSuccess;
 
     int fail(int code, const std::string& m) {
         err = m;
@@ -132,6 +184,38 @@ struct crane_dyn {
         return CRANE_E_HIP;
     }
 };
+
+void EngineTimer::next(const char* name, hipEvent_t* start, hipEvent_t* stop) {
+    if ((int)h->ev.size() < 2 * (h->nk + 1)) {
+        for (int i = 0; i < 2; ++i) {
+            hipEvent_t e;
+            hipError_t r = hipEventCreate(&e);
+            if (r != hipSuccess) {
+                h->timer_err = r;
+                return;
+            }
+            h->ev.push_back(e);
+        }
+        h->ev_name.push_back(nullptr);
+    }
+    h->ev_name[h->nk] = name;
+    *start = h->ev[2 * h->nk];
+    *stop = h->ev[2 * h->nk + 1];
+    ++h->nk;
+}
+
+namespace {
+
+// Every ABI entry that enqueues work holds the engine mutex and installs the
+// engine's kernel timer on the calling thread while profiling is on.
+struct Locked {
+    std::lock_guard<std::mutex> g;
+    KernelTimer* prev;
+    explicit Locked(crane_dyn* h) : g(h->mu), prev(tl_ktimer) { tl_ktimer = h->prof ? &h->timer : nullptr; }
+    ~Locked() { tl_ktimer = prev; }
+};
+
+}  // namespace
 
 #define HIPTRY(h, expr)                                        \
     do {                                                       \
@@ -203,9 +287,224 @@ static int flatten_policy(crane_dyn* h, const crane_policy* pol) {
     return CRANE_OK;
 }
 
+// ------------------------------------------------------------- pipeline pieces
+
+// pods (optional): the step path's pod preparation, launched together with K2x
+// when the dedupe K2 runs (*pods_done reports whether it did).
+static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hipStream_t st,
+                             const PodPrep* pods = nullptr, bool* pods_done = nullptr) {
+    if (pods_done) *pods_done = false;
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before refreshing hot values");
+    DevPolicy& dp = h->dp;
+    HotCutoffs cut{};
+    cut.n_win = dp.n_win;
+    // time.Now().UTC().Unix() - int64(timeRange.Seconds())   (binding.go:85)
+    const int64_t now_unix = floor_div(now_ns, 1000000000LL);
+    int64_t c[kMaxWin];
+    int order[kMaxWin];
+    for (int w = 0; w < dp.n_win; ++w) {
+        const int64_t trs = go_seconds_trunc(h->hot_tr[w]);
+        c[w] = now_unix - trs;
+        order[w] = w;
+    }
+    std::stable_sort(order, order + dp.n_win, [&](int a, int b) { return c[a] < c[b]; });
+    for (int r = 0; r < dp.n_win; ++r) {
+        cut.sorted[r] = c[order[r]];
+        dp.win_pos[order[r]] = r;
+        dp.win_cut_sorted[r] = c[order[r]];
+    }
+    h->hx_pending = false;
+    h->counts_pending = true;
+    h->hv_from_counts = true;
+    h->hv_ts_counts = hv_ts_ns;
+    h->rec_dirty = true;
+    const HotPart gx = hot_dedupe_geometry(h->B, h->N, dp.n_win, h->opt.k1_threads);
+    if (h->opt.k2_form == 0 && gx.ok) {
+        // one launch (+ K3p); the node pass counts its own block's entries (no buckets)
+        HIPTRY(h, h->k2_sorted.reserve(hot_dedupe_scratch(gx)));
+        HIPTRY(h, launch_hot_count_dedupe(h->bnode.p, h->bts.p, h->B, h->N, cut, gx, h->k2_sorted.p, st, pods));
+        if (pods_done) *pods_done = pods != nullptr && pods->P > 0;
+        h->hx_g = gx;
+        h->hx_pending = true;
+        return CRANE_OK;
+    }
+    const size_t nb = (size_t)std::max(1, dp.n_win) * (size_t)std::max<int64_t>(h->N, 1);
+    if (nb > h->buckets.n) h->buckets_zero = false;
+    HIPTRY(h, h->buckets.reserve(nb));
+    if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
+    const HotBins g = hot_bins_geometry(h->B, h->N, dp.n_win);
+    if (g.ok && h->opt.k2_form != 2) {
+        HIPTRY(h, h->k2_cnt.reserve((size_t)g.nbins * (size_t)g.nchunks));
+        HIPTRY(h, h->k2_tot.reserve((size_t)g.nbins));
+        HIPTRY(h, h->k2_sorted.reserve((size_t)std::max<int64_t>(h->B, 1)));
+        HIPTRY(h, launch_hot_count_binned(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, g, h->k2_cnt.p,
+                                          h->k2_tot.p, h->k2_sorted.p, st));
+    } else {
+        HIPTRY(h, launch_hot_count(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, st));
+    }
+    h->buckets_zero = false;
+    return CRANE_OK;
+}
+
+// K1's workgroup size: the dedupe-form K2 bins nodes by it
+static int k1_bs(const crane_dyn* h) {
+    return h->hv_from_counts && h->counts_pending && h->hx_pending ? 1 << h->hx_g.bb : h->opt.k1_threads;
+}
+
+// K1 (optionally with the K3 step tables fused in).  Hot values: pending K2
+// counts (consumed), else the values the last consuming pass kept, else the
+// uploaded annotation.
+static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nullptr, const K1Step* step = nullptr) {
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before the node pass");
+    K1Args a{};
+    a.pol = h->dp;
+    a.N = h->N;
+    a.val = h->val.p;
+    a.ts = h->ts.p;
+    // the fused keys-only step reads its records from LDS; writing them out
+    // (160 B/node of the pass's 280) is left to the next pass that reads them
+    const bool keep = !step || h->opt.k1_keep_rec;
+    a.out = keep ? h->rec.p : nullptr;
+    a.hv_ts_counts = h->hv_ts_counts;
+    const bool consume = h->hv_from_counts && h->counts_pending;
+    if (cnt_out && !consume) return h->fail(CRANE_E_STATE, "per-window counts need a hot-value refresh first");
+    if (consume) {
+        HIPTRY(h, h->hvc.reserve((size_t)std::max<int64_t>(h->N, 1)));
+        if (h->hx_pending) {
+            const HotPart& g = h->hx_g;
+            a.hx_region = h->k2_sorted.p;
+            a.hx_CO = h->k2_sorted.p + g.cap;
+            a.hx_nblk = g.nblk;
+        } else {
+            a.buckets = h->buckets.p;
+        }
+        a.cnt_out = cnt_out;
+        a.hvc_out = h->hvc.p;
+    } else if (h->hv_from_counts) {
+        a.hv = h->hvc.p;  // hv_ts null: stamped hv_ts_counts
+    } else if (h->have_hv) {
+        a.hv = h->hv.p;
+        a.hv_ts = h->hv_ts.p;
+    }
+    a.threads = k1_bs(h);
+    HIPTRY(h, launch_node_pass(h->shape, a, st, step));
+    if (consume) {
+        if (!h->hx_pending) h->buckets_zero = true;  // K1 zeroed what it read
+        h->counts_pending = false;
+        h->hx_pending = false;
+    }
+    h->rec_dirty = !keep;
+    return CRANE_OK;
+}
+
+// ---- keys-only step path (step.hip): K3p -> [K1 +] K3a -> K3s
+struct StepPlan {
+    StepGeometry g;
+    StepTables stt;
+    bool fuse;  // K3a fused into the node pass (records stale)
+};
+
+static bool step_path_ok(const crane_dyn* h, int64_t P) {
+    return h->opt.keys_path == 0 && h->N >= 0 && h->N < kStepMaxNodes && P < (1LL << 31);
+}
+
+static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
+    sp.fuse = h->rec_dirty && h->opt.k1_fuse;
+    const int32_t bs = sp.fuse ? k1_bs(h) : kStepSeg;  // producer workgroup size
+    const int32_t nblk = (int32_t)((h->N + bs - 1) / bs);
+    sp.g = step_geometry(P, h->N, nblk);
+    const StepGeometry& g = sp.g;
+    HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
+    HIPTRY(h, h->stile.reserve((size_t)(2 * g.ntiles)));
+    HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
+    HIPTRY(h, h->scnt.reserve((size_t)std::max<int32_t>(nblk, 1) * 6));  // cnt [nblk][4] + flat [nblk][2]
+    HIPTRY(h, h->sstep1.reserve((size_t)(2 * g.npad)));
+    HIPTRY(h, h->svrec.reserve((size_t)(2 * g.npad) * step_vrec_bytes(h->shape)));
+    sp.stt = StepTables{h->scnt.p, h->scnt.p + (size_t)nblk * 4, h->sstep1.p, h->svrec.p, g.npad, bs, nblk};
+    return CRANE_OK;
+}
+
+static int step_pods(crane_dyn* h, const StepPlan& sp, int64_t P, const int64_t* d_now, const uint8_t* d_flags,
+                     long long* d_keys, hipStream_t st) {
+    HIPTRY(h, launch_step_pods(d_now, d_flags, P, d_keys, sp.g, h->sperm.p, h->spnow.p, h->stile.p, st));
+    return CRANE_OK;
+}
+
+static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_keys, hipStream_t st) {
+    if (P == 0) return CRANE_OK;
+    if (sp.fuse) {
+        K1Step ks{h->stile.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, sp.stt};
+        int rc = node_pass_locked(h, st, nullptr, &ks);
+        if (rc) return rc;
+    } else {
+        if (h->rec_dirty) {
+            int rc = node_pass_locked(h, st);
+            if (rc) return rc;
+        }
+        HIPTRY(h, launch_step_nodes(h->shape, h->rec.p, h->N, h->dp.wsum, h->dp.noprio, sp.stt, sp.g, h->stile.p, st));
+    }
+    HIPTRY(h, launch_step_pairs(h->shape, h->N, h->node_offset, P, d_keys, sp.stt, sp.g, h->sperm.p, h->spnow.p, st));
+    return CRANE_OK;
+}
+
+// The per-pair kernel (K3m): first-fail / score matrices [P][ld] and/or keys.
+static int matrix_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags, long long* d_keys,
+                         int8_t* d_ff, void* d_score, bool score_i64, int64_t ld, hipStream_t st) {
+    if (h->rec_dirty) {
+        int rc = node_pass_locked(h, st);
+        if (rc) return rc;
+    }
+    if (d_keys && P > 0) HIPTRY(h, hipMemsetAsync(d_keys, 0xFF, sizeof(long long) * (size_t)P, st));
+    MatrixArgs a{};
+    a.rec = h->rec.p;
+    a.N = h->N;
+    a.node_offset = h->node_offset;
+    a.now = d_now;
+    a.flags = d_flags;
+    a.P = P;
+    a.ld = ld;
+    a.wsum = h->dp.wsum;
+    a.noprio = h->dp.noprio;
+    a.first_fail = d_ff;
+    a.score = d_score;
+    a.score_i64 = score_i64 ? 1 : 0;
+    a.keys = d_keys;
+    std::memcpy(a.pred_orig, h->pred_orig, sizeof a.pred_orig);
+    HIPTRY(h, launch_matrix(h->shape, a, st));
+    return CRANE_OK;
+}
+
+static int keys_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags, long long* d_keys,
+                       hipStream_t st) {
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
+    if (step_path_ok(h, P)) {
+        StepPlan sp;
+        int rc = step_plan(h, P, sp);
+        if (!rc) rc = step_pods(h, sp, P, d_now, d_flags, d_keys, st);
+        if (!rc) rc = step_rest(h, sp, P, d_keys, st);
+        return rc;
+    }
+    return matrix_locked(h, P, d_now, d_flags, d_keys, nullptr, nullptr, false, 0, st);
+}
+
+// Re-upload the dirty binding-record slots of the heap mode (pinned mirror -> device).
+static int flush_heap_slots(crane_dyn* h) {
+    std::vector<std::pair<int64_t, int64_t>> runs;
+    h->heap.take_dirty_runs(&runs);
+    for (const auto& r : runs) {
+        const size_t n = (size_t)(r.second - r.first);
+        HIPTRY(h, hipMemcpyAsync(h->bnode.p + r.first, h->hnode.p + r.first, n * sizeof(int32_t),
+                                 hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipMemcpyAsync(h->bts.p + r.first, h->hts.p + r.first, n * sizeof(int64_t), hipMemcpyHostToDevice,
+                                 h->stream));
+    }
+    if (!runs.empty()) HIPTRY(h, hipStreamSynchronize(h->stream));  // the mirror may change after we return
+    return CRANE_OK;
+}
+
 extern "C" {
 
-const char* crane_dyn_version(void) { return "crane_dyn 0.1 gfx950"; }
+const char* crane_dyn_version(void) { return "crane_dyn 0.2 gfx950"; }
 
 int64_t crane_dyn_key_node(int64_t key, int64_t* score) {
     if (key < 0) {
@@ -220,52 +519,23 @@ int crane_dyn_create(const crane_policy* pol, int32_t device, crane_dyn** out) {
     if (!out) return CRANE_E_INVALID;
     *out = nullptr;
     crane_dyn* h = new crane_dyn();
+    h->timer.h = h;
+    // the handle is returned even on failure so the caller can read the error; it is
+    // flagged unusable (N = -2) and must still be destroyed
+    *out = h;
     int rc = flatten_policy(h, pol);
     if (rc) {
-        // keep the handle so the caller can read the error, but flag it unusable
         h->N = -2;
-        *out = h;
         return rc;
     }
     h->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
     if (e != hipSuccess) {
         h->hipfail(e, "hipSetDevice/hipStreamCreate");
         h->N = -2;
-        *out = h;
         return CRANE_E_HIP;
     }
-    // quotient thresholds T[k] = min{s : RN(s/W) >= k} for the division-free K3 path
-    const double W = h->dp.wsum;
-    if (!h->dp.noprio && W > 0 && std::isfinite(W)) {
-        std::vector<double> T(kQMax + 1);
-        T[0] = -INFINITY;
-        const uint64_t inf_bits = 0x7FF0000000000000ull;
-        for (int k = 1; k <= kQMax; ++k) {
-            uint64_t lo = 0, hi = inf_bits;  // predicate false at lo=+0, true at +inf
-            while (hi - lo > 1) {
-                const uint64_t mid = lo + (hi - lo) / 2;
-                double sm;
-                std::memcpy(&sm, &mid, 8);
-                if (sm / W >= (double)k) hi = mid;
-                else lo = mid;
-            }
-            std::memcpy(&T[k], &hi, 8);
-        }
-        e = h->thr.reserve(T.size());
-        if (e == hipSuccess) e = hipMemcpy(h->thr.p, T.data(), sizeof(double) * T.size(), hipMemcpyHostToDevice);
-        if (e != hipSuccess) {
-            h->hipfail(e, "threshold table");
-            h->N = -2;
-            return CRANE_E_HIP;
-        }
-        h->inv_w = 1.0 / W;
-    }
-    *out = h;
     return CRANE_OK;
 }
 
@@ -279,18 +549,13 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->ev.clear();
     h->val.release(); h->hv.release(); h->ts.release(); h->hv_ts.release(); h->rec.release();
     h->buckets.release(); h->bnode.release(); h->bts.release(); h->now.release(); h->flags.release();
-    h->keys.release(); h->ff.release(); h->score.release(); h->thr.release();
+    h->keys.release(); h->ff.release(); h->score.release(); h->score8.release();
+    h->stage8.release(); h->stagek.release(); h->hnode.release(); h->hts.release();
     h->k2_cnt.release(); h->k2_tot.release(); h->k2_sorted.release(); h->hvc.release();
     h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
     h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
     h->mFs.release(); h->mIs.release(); h->mgi.release();
     h->sperm.release(); h->scnt.release(); h->stile.release(); h->spnow.release(); h->svrec.release(); h->sstep1.release();
-    if (h->side) {
-        (void)hipStreamSynchronize(h->side);
-        (void)hipStreamDestroy(h->side);
-    }
-    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -305,10 +570,29 @@ const char* crane_dyn_metric_name(const crane_dyn* h, int32_t slot) {
     return h->slot_names[slot].c_str();
 }
 
+int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
+    if (!h || !name) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    const std::string n = name;
+    Options& o = h->opt;
+    auto range = [&](int64_t lo, int64_t hi) { return value >= lo && value <= hi; };
+    if (n == "k2_form" && range(0, 2)) o.k2_form = (int)value;
+    else if (n == "k1_threads" && (value == 128 || value == 256)) o.k1_threads = (int)value;
+    else if (n == "k1_keep_records" && range(0, 1)) o.k1_keep_rec = value != 0;
+    else if (n == "k1_fuse_steps" && range(0, 1)) o.k1_fuse = value != 0;
+    else if (n == "k3p_in_k2" && range(0, 1)) o.k3p_in_k2 = value != 0;
+    else if (n == "keys_path" && range(0, 1)) o.keys_path = (int)value;
+    else if (n == "greedy_form" && range(0, 1)) o.greedy_form = (int)value;
+    else return h->fail(CRANE_E_INVALID, "unknown option or value: " + n + "=" + std::to_string(value));
+    // a pending dedupe-form count is bound to the K1 block size it was binned by
+    h->rec_dirty = true;
+    return CRANE_OK;
+}
+
 int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const double* val, const int64_t* ts,
                            const double* hv, const int64_t* hv_ts) {
     if (!h) return CRANE_E_INVALID;
-    std::lock_guard<std::mutex> g(h->mu);
+    Locked lk(h);
     if (h->N == -2) return h->fail(CRANE_E_STATE, "engine was not created successfully");
     if (n < 0 || n > 0xFFFFFFFFLL || node_offset < 0 || node_offset + n > 0xFFFFFFFFLL)
         return h->fail(CRANE_E_INVALID, "node count/offset out of range (global indices must fit 32 bits)");
@@ -335,13 +619,15 @@ int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const d
     h->node_offset = node_offset;
     h->have_hv = hv != nullptr;
     h->hv_from_counts = false;
+    h->counts_pending = false;
+    h->hx_pending = false;
     h->rec_dirty = true;
     return CRANE_OK;
 }
 
 int crane_dyn_upload_bindings(crane_dyn* h, int64_t n, const int32_t* node, const int64_t* ts_s) {
     if (!h) return CRANE_E_INVALID;
-    std::lock_guard<std::mutex> g(h->mu);
+    Locked lk(h);
     if (h->N == -2) return h->fail(CRANE_E_STATE, "engine was not created successfully");
     if (n < 0 || (n > 0 && (!node || !ts_s))) return h->fail(CRANE_E_INVALID, "bad binding arrays");
     HIPTRY(h, hipSetDevice(h->device));
@@ -353,256 +639,63 @@ int crane_dyn_upload_bindings(crane_dyn* h, int64_t n, const int32_t* node, cons
     }
     HIPTRY(h, hipStreamSynchronize(h->stream));
     h->B = n;
+    h->heap_mode = false;
+    h->heap.reset(0, 0);
     return CRANE_OK;
 }
 
-// Stage-timing marks: an event before the first stage, then one after each.
-static hipError_t prof_mark(crane_dyn* h, hipStream_t st, const char* name) {
-    if (!h->prof) return hipSuccess;
-    if ((int)h->ev.size() <= h->nev) {
-        hipEvent_t e;
-        hipError_t r = hipEventCreate(&e);
-        if (r != hipSuccess) return r;
-        h->ev.push_back(e);
-        h->ev_name.push_back(nullptr);
+int crane_dyn_binding_records(crane_dyn* h, int64_t size, int64_t gc_time_range_ns) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    if (h->N == -2) return h->fail(CRANE_E_STATE, "engine was not created successfully");
+    // size 0 would pop an empty heap in AddBinding (binding.go:73-75); size < 0 never evicts
+    if (size <= 0 || size > 0x7FFFFFFF) return h->fail(CRANE_E_INVALID, "binding heap size must be in [1, 2^31)");
+    HIPTRY(h, hipSetDevice(h->device));
+    HIPTRY(h, h->hnode.reserve((size_t)size));
+    HIPTRY(h, h->hts.reserve((size_t)size));
+    HIPTRY(h, h->bnode.reserve((size_t)size));
+    HIPTRY(h, h->bts.reserve((size_t)size));
+    for (int64_t i = 0; i < size; ++i) {
+        h->hnode.p[i] = -1;
+        h->hts.p[i] = 0;
     }
-    h->ev_name[h->nev] = name;
-    return hipEventRecord(h->ev[h->nev++], st);
-}
-static hipError_t prof_begin(crane_dyn* h, hipStream_t st) {
-    return h->prof && h->nev == 0 ? prof_mark(h, st, "begin") : hipSuccess;
-}
-
-// pods (optional): the step path's pod preparation, launched together with K2x
-// when the partitioned K2 runs (*pods_done reports whether it did).
-static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hipStream_t st,
-                             const PodPrep* pods = nullptr, bool* pods_done = nullptr) {
-    if (pods_done) *pods_done = false;
-    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before refreshing hot values");
-    DevPolicy& dp = h->dp;
-    HotCutoffs cut{};
-    cut.n_win = dp.n_win;
-    // time.Now().UTC().Unix() - int64(timeRange.Seconds())   (binding.go:85)
-    const int64_t now_unix = floor_div(now_ns, 1000000000LL);
-    int64_t c[kMaxWin];
-    int order[kMaxWin];
-    for (int w = 0; w < dp.n_win; ++w) {
-        const int64_t trs = go_seconds_trunc(h->hot_tr[w]);
-        c[w] = now_unix - trs;
-        order[w] = w;
-    }
-    std::stable_sort(order, order + dp.n_win, [&](int a, int b) { return c[a] < c[b]; });
-    for (int r = 0; r < dp.n_win; ++r) {
-        cut.sorted[r] = c[order[r]];
-        dp.win_pos[order[r]] = r;
-        dp.win_cut_sorted[r] = c[order[r]];
-    }
-    const size_t nb = (size_t)std::max(1, dp.n_win) * (size_t)std::max<int64_t>(h->N, 1);
-    if (nb > h->buckets.n) h->buckets_zero = false;
-    HIPTRY(h, h->buckets.reserve(nb));
-    const char* k2e = getenv("CRANE_K2");
-    const std::string mode = k2e ? k2e : "dedupe";
-    h->hx_pending = false;
-    const HotPart gx = hot_dedupe_geometry(h->B, h->N, dp.n_win, k1_threads());
-    if (mode == "dedupe" && gx.ok) {
-        // one launch (+ K3p); the node pass counts its own block's entries (no buckets)
-        HIPTRY(h, h->k2_sorted.reserve(hot_part_scratch(gx)));
-        HIPTRY(h, prof_begin(h, st));
-        HIPTRY(h, launch_hot_count_dedupe(h->bnode.p, h->bts.p, h->B, h->N, cut, gx, h->k2_sorted.p, st, pods));
-        HIPTRY(h, prof_mark(h, st, pods ? "k2x_dedupe+k3p_pods" : "k2x_dedupe"));
-        if (pods_done) *pods_done = pods != nullptr;
-        h->hx_g = gx;
-        h->hx_pending = true;
-        h->counts_pending = true;
-        h->hv_from_counts = true;
-        h->hv_ts_counts = hv_ts_ns;
-        h->rec_dirty = true;
-        return CRANE_OK;
-    }
-    const HotPart gp = hot_part_geometry(h->B, h->N, dp.n_win);
-    if (mode == "part" && gp.ok) {
-        // two kernels adding into zeroed buckets (K1 zeroes what it consumed)
-        if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
-        HIPTRY(h, h->k2_sorted.reserve(hot_part_scratch(gp)));
-        HIPTRY(h, prof_begin(h, st));
-        HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, h->k2_sorted.p, st,
-                                        1, pods));
-        HIPTRY(h, prof_mark(h, st, pods ? "k2x_partition+k3p_pods" : "k2x_partition"));
-        if (pods_done) *pods_done = pods != nullptr;
-        HIPTRY(h, launch_hot_count_part(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, gp, h->k2_sorted.p, st,
-                                        2));
-        HIPTRY(h, prof_mark(h, st, "k2y_bin_hist"));
-        h->counts_pending = true;
-        h->buckets_zero = false;
-        h->hv_from_counts = true;
-        h->hv_ts_counts = hv_ts_ns;
-        h->rec_dirty = true;
-        return CRANE_OK;
-    }
-    if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
-    const HotBins g = hot_bins_geometry(h->B, h->N, dp.n_win);
-    if (g.ok && mode != "hash") {
-        HIPTRY(h, h->k2_cnt.reserve((size_t)g.nbins * (size_t)g.nchunks));
-        HIPTRY(h, h->k2_tot.reserve((size_t)g.nbins));
-        HIPTRY(h, h->k2_sorted.reserve((size_t)h->B));
-        HIPTRY(h, prof_begin(h, st));
-        HIPTRY(h, launch_hot_count_binned(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, g, h->k2_cnt.p,
-                                          h->k2_tot.p, h->k2_sorted.p, st));
-        HIPTRY(h, prof_mark(h, st, "k2_binned (4 kernels)"));
-    } else {
-        HIPTRY(h, prof_begin(h, st));
-        HIPTRY(h, launch_hot_count(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, st));
-        HIPTRY(h, prof_mark(h, st, "k2_hot_count (hash)"));
-    }
-    h->buckets_zero = false;
-    h->counts_pending = true;
-    h->hv_from_counts = true;
-    h->hv_ts_counts = hv_ts_ns;
-    h->rec_dirty = true;
+    HIPTRY(h, hipMemcpyAsync(h->bnode.p, h->hnode.p, sizeof(int32_t) * size, hipMemcpyHostToDevice, h->stream));
+    HIPTRY(h, hipMemcpyAsync(h->bts.p, h->hts.p, sizeof(int64_t) * size, hipMemcpyHostToDevice, h->stream));
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    h->heap.reset(size, gc_time_range_ns);
+    h->heap.bind(h->hnode.p, h->hts.p);
+    h->heap_mode = true;
+    h->B = size;
     return CRANE_OK;
 }
 
-// K1's workgroup size: the dedupe-form K2 bins nodes by it
-static int k1_bs(const crane_dyn* h) {
-    return h->hv_from_counts && h->counts_pending && h->hx_pending ? 1 << h->hx_g.bb : k1_threads();
+int crane_dyn_add_bindings(crane_dyn* h, int64_t n, const int32_t* node, const int64_t* ts_s) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    if (!h->heap_mode) return h->fail(CRANE_E_STATE, "crane_dyn_binding_records first");
+    if (n < 0 || (n > 0 && (!node || !ts_s))) return h->fail(CRANE_E_INVALID, "bad binding arrays");
+    HIPTRY(h, hipSetDevice(h->device));
+    for (int64_t i = 0; i < n; ++i) h->heap.add(node[i], ts_s[i]);
+    return flush_heap_slots(h);
 }
 
-// K1 (optionally with the K3 step tables fused in).  Hot values: pending K2
-// counts (consumed), else the values the last consuming pass kept, else the
-// uploaded annotation.
-static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nullptr, const K1Step* step = nullptr) {
-    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before the node pass");
-    K1Args a{};
-    a.pol = h->dp;
-    a.N = h->N;
-    a.val = h->val.p;
-    a.ts = h->ts.p;
-    // the fused keys-only step reads its records from LDS; writing them out
-    // (160 B/node of the pass's 280) is left to the next pass that reads them
-    // (CRANE_K1_KEEP_REC=1 keeps them)
-    const char* kr = getenv("CRANE_K1_KEEP_REC");
-    const bool keep = !step || (kr && kr[0] == '1');
-    a.out = keep ? h->rec.p : nullptr;
-    a.hv_ts_counts = h->hv_ts_counts;
-    const bool consume = h->hv_from_counts && h->counts_pending;
-    if (cnt_out && !consume) return h->fail(CRANE_E_STATE, "per-window counts need a hot-value refresh first");
-    if (consume) {
-        HIPTRY(h, h->hvc.reserve((size_t)std::max<int64_t>(h->N, 1)));
-        if (h->hx_pending) {
-            const HotPart& g = h->hx_g;
-            a.hx_region = h->k2_sorted.p;
-            a.hx_CO = h->k2_sorted.p + g.cap;
-            a.hx_nblk = g.nblk;
-        } else {
-            a.buckets = h->buckets.p;
-        }
-        a.cnt_out = cnt_out;
-        a.hvc_out = h->hvc.p;
-    } else if (h->hv_from_counts) {
-        a.hv = h->hvc.p;  // hv_ts null: stamped hv_ts_counts
-    } else if (h->have_hv) {
-        a.hv = h->hv.p;
-        a.hv_ts = h->hv_ts.p;
-    }
-    a.threads = k1_bs(h);
-    HIPTRY(h, prof_begin(h, st));
-    HIPTRY(h, launch_node_pass(h->shape, a, st, step));
-    HIPTRY(h, prof_mark(h, st, step ? "k1_node_pass+k3a_steps" : "k1_node_pass"));
-    if (consume) {
-        if (!h->hx_pending) h->buckets_zero = true;  // K1 zeroed what it read
-        h->counts_pending = false;
-        h->hx_pending = false;
-    }
-    h->rec_dirty = !keep;
-    return CRANE_OK;
+int crane_dyn_gc_bindings(crane_dyn* h, int64_t now_ns) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    if (!h->heap_mode) return h->fail(CRANE_E_STATE, "crane_dyn_binding_records first");
+    HIPTRY(h, hipSetDevice(h->device));
+    h->heap.gc(floor_div(now_ns, 1000000000LL));
+    return flush_heap_slots(h);
 }
 
-// ---- keys-only step path (step.hip): K3p -> [K1 +] K3a -> K3s
-struct StepPlan {
-    StepGeometry g;
-    StepTables stt;
-    bool fuse;  // K3a fused into the node pass (records stale)
-};
-
-static bool step_path_ok(const crane_dyn* h, int64_t P) {
-    return k3_variant() == 5 && h->N >= 0 && h->N < kStepMaxNodes && P < (1LL << 31);
-}
-
-static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
-    const char* fe = getenv("CRANE_K1_FUSE");
-    sp.fuse = h->rec_dirty && !(fe && fe[0] == '0');
-    const int32_t bs = sp.fuse ? k1_bs(h) : kStepSeg;  // producer workgroup size
-    const int32_t nblk = (int32_t)((h->N + bs - 1) / bs);
-    sp.g = step_geometry(P, h->N, nblk);
-    const StepGeometry& g = sp.g;
-    HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
-    HIPTRY(h, h->stile.reserve((size_t)(2 * g.ntiles)));
-    HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
-    HIPTRY(h, h->scnt.reserve((size_t)std::max<int32_t>(nblk, 1) * 6));  // cnt [nblk][4] + flat [nblk][2]
-    HIPTRY(h, h->sstep1.reserve((size_t)(2 * g.npad)));
-    HIPTRY(h, h->svrec.reserve((size_t)(2 * g.npad) * step_vrec_bytes(h->shape)));
-    sp.stt = StepTables{h->scnt.p, h->scnt.p + (size_t)nblk * 4, h->sstep1.p, h->svrec.p, g.npad, bs, nblk};
-    return CRANE_OK;
-}
-
-static int step_pods(crane_dyn* h, const StepPlan& sp, int64_t P, const int64_t* d_now, const uint8_t* d_flags,
-                     long long* d_keys, hipStream_t st) {
-    HIPTRY(h, prof_begin(h, st));
-    HIPTRY(h, launch_step_pods(d_now, d_flags, P, d_keys, sp.stt, sp.g, h->sperm.p, h->spnow.p, h->stile.p, st));
-    HIPTRY(h, prof_mark(h, st, "k3p_pods"));
-    return CRANE_OK;
-}
-
-static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_keys, hipStream_t st) {
-    if (P == 0) return CRANE_OK;
-    if (sp.fuse) {
-        K1Step ks{h->stile.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, sp.stt};
-        int rc = node_pass_locked(h, st, nullptr, &ks);
-        if (rc) return rc;
-    } else {
-        if (h->rec_dirty) {
-            int rc = node_pass_locked(h, st);
-            if (rc) return rc;
-        }
-        HIPTRY(h, launch_step_nodes(h->shape, h->rec.p, h->N, h->dp.wsum, h->dp.noprio, sp.stt, sp.g, h->stile.p, st));
-        HIPTRY(h, prof_mark(h, st, "k3a_steps"));
-    }
-    HIPTRY(h, launch_step_pairs(h->shape, h->N, h->node_offset, P, d_keys, sp.stt, sp.g, h->sperm.p, h->spnow.p, st));
-    HIPTRY(h, prof_mark(h, st, "k3s_eval"));
-    return CRANE_OK;
-}
-
-static int eval_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags, long long* d_keys,
-                       int8_t* d_ff, int64_t* d_score, hipStream_t st) {
-    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
-    const bool matrix = d_ff || d_score;
-    if (!matrix && step_path_ok(h, P)) {
-        StepPlan sp;
-        int rc = step_plan(h, P, sp);
-        if (!rc) rc = step_pods(h, sp, P, d_now, d_flags, d_keys, st);
-        if (!rc) rc = step_rest(h, sp, P, d_keys, st);
-        return rc;
-    }
-    if (h->rec_dirty) {
-        int rc = node_pass_locked(h, st);
-        if (rc) return rc;
-    }
-    HIPTRY(h, prof_begin(h, st));
-    HIPTRY(h, hipMemsetAsync(d_keys, 0xFF, sizeof(long long) * (size_t)P, st));
-    HIPTRY(h, prof_mark(h, st, "keys_init"));
-    MatrixOut mo{};
-    mo.first_fail = d_ff;
-    mo.score = d_score;
-    std::memcpy(mo.pred_orig, h->pred_orig, sizeof mo.pred_orig);
-    HIPTRY(h, launch_eval(h->shape, h->rec.p, h->N, h->node_offset, d_now, d_flags, P, h->dp.wsum, h->dp.noprio,
-                          d_keys, mo, h->inv_w, h->thr.n ? h->thr.p : nullptr, st));
-    HIPTRY(h, prof_mark(h, st, "k3_eval"));
-    return CRANE_OK;
+int64_t crane_dyn_binding_count(const crane_dyn* h) {
+    if (!h) return CRANE_E_INVALID;
+    return h->heap_mode ? h->heap.len() : h->B;
 }
 
 int crane_dyn_refresh_hot_values(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns) {
     if (!h) return CRANE_E_INVALID;
-    std::lock_guard<std::mutex> g(h->mu);
+    Locked lk(h);
     HIPTRY(h, hipSetDevice(h->device));
     int rc = hot_values_locked(h, now_ns, hv_ts_ns, h->stream);
     if (rc) return rc;
@@ -612,7 +705,7 @@ int crane_dyn_refresh_hot_values(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns)
 
 int crane_dyn_hot_values(crane_dyn* h, int64_t n, double* hv_out) {
     if (!h) return CRANE_E_INVALID;
-    std::lock_guard<std::mutex> g(h->mu);
+    Locked lk(h);
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before reading hot values");
     if (n != h->N || (n > 0 && !hv_out)) return h->fail(CRANE_E_INVALID, "hv_out must hold one value per node");
     if (n == 0) return CRANE_OK;
@@ -638,14 +731,14 @@ int crane_dyn_hot_values(crane_dyn* h, int64_t n, double* hv_out) {
 
 int crane_dyn_refresh_hot_values_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, void* stream) {
     if (!h) return CRANE_E_INVALID;
-    std::lock_guard<std::mutex> g(h->mu);
+    Locked lk(h);
     HIPTRY(h, hipSetDevice(h->device));
     return hot_values_locked(h, now_ns, hv_ts_ns, stream ? (hipStream_t)stream : h->stream);
 }
 
 int crane_dyn_node_pass_async(crane_dyn* h, void* stream) {
     if (!h) return CRANE_E_INVALID;
-    std::lock_guard<std::mutex> g(h->mu);
+    Locked lk(h);
     HIPTRY(h, hipSetDevice(h->device));
     return node_pass_locked(h, stream ? (hipStream_t)stream : h->stream);
 }
@@ -653,108 +746,107 @@ int crane_dyn_node_pass_async(crane_dyn* h, void* stream) {
 int crane_dyn_eval_keys_async(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags,
                               int64_t* d_keys, void* stream) {
     if (!h) return CRANE_E_INVALID;
-    std::lock_guard<std::mutex> g(h->mu);
+    Locked lk(h);
     if (P < 0 || (P > 0 && (!d_now || !d_keys))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
-    if (P > (int64_t)0x7FFFFFFF * 256) return h->fail(CRANE_E_INVALID, "too many pods");
     HIPTRY(h, hipSetDevice(h->device));
-    return eval_locked(h, P, d_now, d_flags, reinterpret_cast<long long*>(d_keys), nullptr, nullptr,
+    return keys_locked(h, P, d_now, d_flags, reinterpret_cast<long long*>(d_keys),
                        stream ? (hipStream_t)stream : h->stream);
+}
+
+int crane_dyn_eval_matrix_async(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags,
+                                int8_t* d_first_fail, int8_t* d_score, int64_t ld, int64_t* d_keys, void* stream) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    if (P < 0 || (P > 0 && !d_now)) return h->fail(CRANE_E_INVALID, "bad pod arrays");
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
+    if ((d_first_fail || d_score) && ld < h->N) return h->fail(CRANE_E_INVALID, "ld must be >= the node count");
+    HIPTRY(h, hipSetDevice(h->device));
+    return matrix_locked(h, P, d_now, d_flags, reinterpret_cast<long long*>(d_keys), d_first_fail, d_score, false, ld,
+                         stream ? (hipStream_t)stream : h->stream);
 }
 
 int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, int64_t P, const int64_t* d_now,
                               const uint8_t* d_flags, int64_t* d_keys, void* stream) {
     if (!h) return CRANE_E_INVALID;
-    std::lock_guard<std::mutex> g(h->mu);
+    Locked lk(h);
     if (P < 0 || (P > 0 && (!d_now || !d_keys))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
-    if (P > (int64_t)0x7FFFFFFF * 256) return h->fail(CRANE_E_INVALID, "too many pods");
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
     HIPTRY(h, hipSetDevice(h->device));
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     long long* keys = reinterpret_cast<long long*>(d_keys);
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    HIPTRY(h, hipStreamIsCapturing(st, &cap));
-    // refresh sets rec_dirty: plan after it (the plan only reads N, P and whether the records are stale)
-    // Overlapping K3p with K2 on the second queue measured slower at config 3 (65 vs 55 us per
-    // step: the cross-queue event waits cost more than the 4.5-us K3p), so it is opt-in.
-    const char* ov = getenv("CRANE_STEP_OVERLAP");
-    const bool want = ov && ov[0] == '1';
-    const bool overlap = want && h->side && !h->prof && cap == hipStreamCaptureStatusNone && step_path_ok(h, P) &&
-                         P > 0;
-    if (!overlap && step_path_ok(h, P) && P > 0) {
-        // K3p rides in K2x's launch (when the partitioned K2 runs); the refresh
-        // leaves the records stale, so plan for the fused node pass
-        h->rec_dirty = true;
-        StepPlan sp;
-        int rc = step_plan(h, P, sp);
-        if (rc) return rc;
-        const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys};
-        bool pods_done = false;
-        const char* mp = getenv("CRANE_K2X_PODS");  // 0: K3p in its own launch (A/B)
-        const bool ride = !(mp && mp[0] == '0');
-        rc = hot_values_locked(h, now_ns, hv_ts_ns, st, ride ? &pp : nullptr, &pods_done);
-        if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, st);
-        if (!rc) rc = step_rest(h, sp, P, keys, st);
-        return rc;
-    }
-    if (!overlap) {
+    if (!step_path_ok(h, P) || P == 0) {
         int rc = hot_values_locked(h, now_ns, hv_ts_ns, st);
-        if (!rc) rc = eval_locked(h, P, d_now, d_flags, keys, nullptr, nullptr, st);
+        if (!rc) rc = keys_locked(h, P, d_now, d_flags, keys, st);
         return rc;
     }
-    // K3p depends only on the pods: it runs on the side stream while K2 runs on st.
-    // The fork event orders it after everything already on st (the previous step's K3s
-    // reads the buffers K3p rewrites; the caller's writes of d_now / d_flags).
-    HIPTRY(h, hipEventRecord(h->ev_fork, st));
-    HIPTRY(h, hipStreamWaitEvent(h->side, h->ev_fork, 0));
-    int rc = hot_values_locked(h, now_ns, hv_ts_ns, st);
-    if (rc) return rc;
+    // the refresh leaves the records stale: plan for the fused node pass; K3p rides in
+    // K2x's launch when the dedupe K2 runs
+    h->rec_dirty = true;
     StepPlan sp;
-    rc = step_plan(h, P, sp);
+    int rc = step_plan(h, P, sp);
     if (rc) return rc;
-    rc = step_pods(h, sp, P, d_now, d_flags, keys, h->side);
-    if (rc) return rc;
-    HIPTRY(h, hipEventRecord(h->ev_join, h->side));
-    HIPTRY(h, hipStreamWaitEvent(st, h->ev_join, 0));
-    return step_rest(h, sp, P, keys, st);
+    const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys};
+    bool pods_done = false;
+    rc = hot_values_locked(h, now_ns, hv_ts_ns, st, h->opt.k3p_in_k2 ? &pp : nullptr, &pods_done);
+    if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, st);
+    if (!rc) rc = step_rest(h, sp, P, keys, st);
+    return rc;
 }
 
-int crane_dyn_eval(crane_dyn* h, int64_t P, const int64_t* now_ns, const uint8_t* pod_flags, int8_t* first_fail,
-                   int64_t* score, int64_t* chosen, int64_t* chosen_score) {
-    if (!h) return CRANE_E_INVALID;
-    std::lock_guard<std::mutex> g(h->mu);
+// Host-pointer evaluation: the matrices go through device scratch in pod slices of
+// at most ~64M entries; chosen nodes come from the same kernel's keys.
+static int eval_host(crane_dyn* h, int64_t P, const int64_t* now_ns, const uint8_t* pod_flags, int8_t* first_fail,
+                     void* score, bool score_i64, int64_t* chosen, int64_t* chosen_score) {
     if (P < 0 || (P > 0 && !now_ns)) return h->fail(CRANE_E_INVALID, "bad pod arrays");
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
     HIPTRY(h, hipSetDevice(h->device));
     const int64_t N = h->N;
     const bool matrix = first_fail || score;
-    // bound the matrix scratch to ~64M entries per pass
     int64_t pc = P;
     if (matrix && N > 0) pc = std::max<int64_t>(1, std::min<int64_t>(P, (int64_t)(64LL << 20) / N));
     if (pc <= 0) pc = 1;
     HIPTRY(h, h->now.reserve((size_t)pc));
     HIPTRY(h, h->flags.reserve((size_t)pc));
     HIPTRY(h, h->keys.reserve((size_t)pc));
-    if (first_fail) HIPTRY(h, h->ff.reserve((size_t)(pc * std::max<int64_t>(N, 1))));
-    if (score) HIPTRY(h, h->score.reserve((size_t)(pc * std::max<int64_t>(N, 1))));
-    std::vector<long long> hk((size_t)pc);
+    HIPTRY(h, h->stagek.reserve((size_t)pc));
+    const size_t cells = (size_t)(pc * std::max<int64_t>(N, 1));
+    if (first_fail) HIPTRY(h, h->ff.reserve(cells));
+    if (score && score_i64) HIPTRY(h, h->score.reserve(cells));
+    if (score && !score_i64) HIPTRY(h, h->score8.reserve(cells));
+    const bool compact = !score_i64;  // compact rows come back through pinned staging
+    if (compact && matrix) HIPTRY(h, h->stage8.reserve(2 * cells));
     for (int64_t p0 = 0; p0 < P; p0 += pc) {
         const int64_t np = std::min(pc, P - p0);
         HIPTRY(h, hipMemcpyAsync(h->now.p, now_ns + p0, sizeof(int64_t) * np, hipMemcpyHostToDevice, h->stream));
         if (pod_flags)
             HIPTRY(h, hipMemcpyAsync(h->flags.p, pod_flags + p0, np, hipMemcpyHostToDevice, h->stream));
-        int rc = eval_locked(h, np, h->now.p, pod_flags ? h->flags.p : nullptr, h->keys.p,
-                             first_fail ? h->ff.p : nullptr, score ? h->score.p : nullptr, h->stream);
+        int rc;
+        if (!matrix) {
+            rc = keys_locked(h, np, h->now.p, pod_flags ? h->flags.p : nullptr, h->keys.p, h->stream);
+        } else {
+            void* sdev = !score ? nullptr : score_i64 ? (void*)h->score.p : (void*)h->score8.p;
+            rc = matrix_locked(h, np, h->now.p, pod_flags ? h->flags.p : nullptr, h->keys.p,
+                               first_fail ? h->ff.p : nullptr, sdev, score_i64, N, h->stream);
+        }
         if (rc) return rc;
-        HIPTRY(h, hipMemcpyAsync(hk.data(), h->keys.p, sizeof(long long) * np, hipMemcpyDeviceToHost, h->stream));
+        HIPTRY(h, hipMemcpyAsync(h->stagek.p, h->keys.p, sizeof(long long) * np, hipMemcpyDeviceToHost, h->stream));
+        const size_t cnt = (size_t)(np * N);
         if (first_fail && N > 0)
-            HIPTRY(h, hipMemcpyAsync(first_fail + p0 * N, h->ff.p, (size_t)(np * N), hipMemcpyDeviceToHost, h->stream));
-        if (score && N > 0)
-            HIPTRY(h, hipMemcpyAsync(score + p0 * N, h->score.p, sizeof(int64_t) * np * N, hipMemcpyDeviceToHost,
-                                     h->stream));
+            HIPTRY(h, hipMemcpyAsync(compact ? (void*)h->stage8.p : (void*)(first_fail + p0 * N), h->ff.p, cnt,
+                                     hipMemcpyDeviceToHost, h->stream));
+        if (score && N > 0) {
+            if (score_i64)
+                HIPTRY(h, hipMemcpyAsync(static_cast<int64_t*>(score) + p0 * N, h->score.p, sizeof(int64_t) * cnt,
+                                         hipMemcpyDeviceToHost, h->stream));
+            else
+                HIPTRY(h, hipMemcpyAsync(h->stage8.p + cells, h->score8.p, cnt, hipMemcpyDeviceToHost, h->stream));
+        }
         HIPTRY(h, hipStreamSynchronize(h->stream));
+        if (compact && first_fail && N > 0) std::memcpy(first_fail + p0 * N, h->stage8.p, cnt);
+        if (compact && score && N > 0) std::memcpy(static_cast<int8_t*>(score) + p0 * N, h->stage8.p + cells, cnt);
         for (int64_t i = 0; i < np; ++i) {
             int64_t s;
-            const int64_t nd = crane_dyn_key_node(hk[i], &s);
+            const int64_t nd = crane_dyn_key_node(h->stagek.p[i], &s);
             if (chosen) chosen[p0 + i] = nd;
             if (chosen_score) chosen_score[p0 + i] = s;
         }
@@ -762,32 +854,53 @@ int crane_dyn_eval(crane_dyn* h, int64_t P, const int64_t* now_ns, const uint8_t
     return CRANE_OK;
 }
 
+int crane_dyn_eval(crane_dyn* h, int64_t P, const int64_t* now_ns, const uint8_t* pod_flags, int8_t* first_fail,
+                   int64_t* score, int64_t* chosen, int64_t* chosen_score) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    return eval_host(h, P, now_ns, pod_flags, first_fail, score, true, chosen, chosen_score);
+}
+
+int crane_dyn_eval_compact(crane_dyn* h, int64_t P, const int64_t* now_ns, const uint8_t* pod_flags,
+                           int8_t* first_fail, int8_t* score, int64_t* chosen, int64_t* chosen_score) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    return eval_host(h, P, now_ns, pod_flags, first_fail, score, false, chosen, chosen_score);
+}
+
 int crane_dyn_set_profiling(crane_dyn* h, int on) {
     if (!h) return CRANE_E_INVALID;
     std::lock_guard<std::mutex> g(h->mu);
     h->prof = on != 0;
-    h->nev = 0;
+    h->nk = 0;
+    h->timer_err = hipSuccess;
     return CRANE_OK;
 }
 
 int crane_dyn_stage_times(crane_dyn* h, int32_t max, const char** names, double* ms) {
     if (!h) return CRANE_E_INVALID;
     std::lock_guard<std::mutex> g(h->mu);
+    if (h->timer_err != hipSuccess) {
+        const hipError_t e = h->timer_err;
+        h->timer_err = hipSuccess;
+        h->nk = 0;
+        return h->hipfail(e, "kernel timer events");
+    }
     int n = 0;
-    if (h->nev > 0) HIPTRY(h, hipEventSynchronize(h->ev[h->nev - 1]));
-    for (int i = 1; i < h->nev && n < max; ++i, ++n) {
+    for (int i = 0; i < h->nk && n < max; ++i, ++n) {
+        HIPTRY(h, hipEventSynchronize(h->ev[2 * i + 1]));
         float t = 0.f;
-        HIPTRY(h, hipEventElapsedTime(&t, h->ev[i - 1], h->ev[i]));
+        HIPTRY(h, hipEventElapsedTime(&t, h->ev[2 * i], h->ev[2 * i + 1]));
         if (names) names[n] = h->ev_name[i];
         if (ms) ms[n] = t;
     }
-    h->nev = 0;
+    h->nk = 0;
     return n;
 }
 
 int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod_flags, int64_t* chosen) {
     if (!h) return CRANE_E_INVALID;
-    std::lock_guard<std::mutex> g(h->mu);
+    Locked lk(h);
     if (P < 0 || (P > 0 && !chosen)) return h->fail(CRANE_E_INVALID, "bad pod arrays");
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before greedy placement");
     if (h->N > kGreedyMaxNodes) return h->fail(CRANE_E_INVALID, "greedy mode supports up to 64^4 nodes");
@@ -819,8 +932,7 @@ int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod
     HIPTRY(h, h->gflags.reserve((size_t)std::max<int64_t>(P, 1)));
     if (pod_flags && P > 0) HIPTRY(h, hipMemcpyAsync(h->gflags.p, pod_flags, P, hipMemcpyHostToDevice, st));
     // Merge form (merge.hip) when every hotValue count is positive; else the sequential kernel
-    const char* ge = getenv("CRANE_GREEDY");
-    bool merge = !(ge && std::strcmp(ge, "seq") == 0) && N > 0 && P > 0;
+    bool merge = h->opt.greedy_form == 0 && N > 0 && P > 0;
     for (int w = 0; w < W; ++w) merge = merge && a.win_count[w] > 0;
     bool done = false;
     if (merge) {
@@ -829,7 +941,6 @@ int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod
             for (int64_t p = 0; p < P; ++p) Pd += pod_flags[p] & 1;
         HIPTRY(h, launch_greedy(h->shape, h->rec.p, N, h->gcnt.p, a, h->gbase.p, h->gleaf.p, P, nullptr, nullptr, st,
                                 kGreedyPrep));
-        HIPTRY(h, prof_mark(h, st, "greedy_prep"));
         MergeArgs ma{};
         ma.n_win = W;
         for (int w = 0; w < W; ++w) {
@@ -839,7 +950,6 @@ int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod
         HIPTRY(h, h->mH.reserve(2 * 101));
         HIPTRY(h, h->mflag.reserve(1));
         HIPTRY(h, launch_merge_hist(h->gbase.p, h->gleaf.p, h->gcnt.p, N, ma, P, Pd, h->mH.p, h->mflag.p, st));
-        HIPTRY(h, prof_mark(h, st, "m1_hist"));
         unsigned long long Hh[2 * 101];
         int32_t flag = 1;
         HIPTRY(h, hipMemcpyAsync(Hh, h->mH.p, sizeof Hh, hipMemcpyDeviceToHost, st));
@@ -872,17 +982,14 @@ int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod
                                                   h->mFs.p, st));
             if (nI) HIPTRY(h, launch_merge_stream(h->gbase.p, h->gleaf.p, h->gcnt.p, N, ma, 1, vI, nI, h->mbs.p,
                                                   h->mIs.p, st));
-            HIPTRY(h, prof_mark(h, st, "m2_m4_merge_stream"));
             HIPTRY(h, launch_merge_assign(h->mFs.p, nF, h->mIs.p, nI, h->gflags.p, P, Pd, h->mapos.p, h->mtk.p,
                                           h->mgi.p, h->gchosen.p, st));
-            HIPTRY(h, prof_mark(h, st, "m5_merge_assign"));
             done = true;
         }
     }
     if (!done)
         HIPTRY(h, launch_greedy(h->shape, h->rec.p, N, h->gcnt.p, a, h->gbase.p, h->gleaf.p, P,
                                 pod_flags ? h->gflags.p : nullptr, h->gchosen.p, st, merge ? kGreedyRun : kGreedyBoth));
-    if (!done) HIPTRY(h, prof_mark(h, st, "greedy_run"));
     if (P > 0) HIPTRY(h, hipMemcpyAsync(chosen, h->gchosen.p, sizeof(int64_t) * P, hipMemcpyDeviceToHost, st));
     HIPTRY(h, hipStreamSynchronize(st));
     for (int64_t p = 0; p < P; ++p)

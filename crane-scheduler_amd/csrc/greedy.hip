@@ -273,9 +273,8 @@ static hipError_t launch_greedy_t(const void* rec, int64_t N, uint32_t* cnt, con
                                   int what) {
     if (N > kGreedyMaxNodes) return hipErrorInvalidValue;
     if (N > 0 && (what & kGreedyPrep)) {
-        hipLaunchKernelGGL((greedy_prep<PD, PR>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st,
-                           static_cast<const NodeRec<PD, PR>*>(rec), N, cnt, a, base, leaf);
-        hipError_t e = hipGetLastError();
+        hipError_t e = klaunch("greedy_prep", greedy_prep<PD, PR>, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st,
+                               static_cast<const NodeRec<PD, PR>*>(rec), N, cnt, a, base, leaf);
         if (e != hipSuccess) return e;
     }
     if (!(what & kGreedyRun)) return hipSuccess;
@@ -291,17 +290,16 @@ static hipError_t launch_greedy_t(const void* rec, int64_t N, uint32_t* cnt, con
         static const hipError_t attr = hipFuncSetAttribute((const void*)greedy_run<L>,                          \
                                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
         if (attr != hipSuccess) return attr;                                                                    \
-        hipLaunchKernelGGL(greedy_run<L>, dim3(1), dim3(256), lds, st, N, leaf, base, cnt, a, P, flags, chosen, \
-                           (int32_t)in_lds);                                                                    \
+        return klaunch("greedy_run", greedy_run<L>, dim3(1), dim3(256), lds, st, N, leaf, base, cnt, a, P, flags, \
+                       chosen, (int32_t)in_lds);                                                                \
     } while (0)
     switch (nlev) {
-        case 1: GREEDY_LAUNCH(1); break;
-        case 2: GREEDY_LAUNCH(2); break;
-        case 3: GREEDY_LAUNCH(3); break;
-        default: GREEDY_LAUNCH(4); break;
+        case 1: GREEDY_LAUNCH(1);
+        case 2: GREEDY_LAUNCH(2);
+        case 3: GREEDY_LAUNCH(3);
+        default: GREEDY_LAUNCH(4);
     }
 #undef GREEDY_LAUNCH
-    return hipGetLastError();
 }
 
 hipError_t launch_greedy(int shape, const void* rec, int64_t N, uint32_t* cnt, const GreedyArgs& a, int64_t* base,

@@ -1,21 +1,26 @@
-// hotcount.hip — K2 as a bin-partitioned, LDS-staged segmented count.
+// hotcount.hip — K2: binding records -> per-node window counts, two forms.
 //
-// Same result as kernels.hip's hash K2: buckets[j][n] += #bindings of node n
-// whose timestamp lies in exactly the windows of sorted-cutoff ranks 0..j
-// (binding.go:85-91), from which K1 forms GetLastNodeBindingCount per window.
-// Instead of scattered device-scope atomics (≈17x slower than contiguous ones
-// on MI355X), bindings are first partitioned by node range ("bins" of 2^BB
-// nodes), then each bin is counted in a dense LDS histogram and flushed with
-// contiguous atomics (lane i -> node i).
-//   A  bin_count : chunk of bindings -> per-(bin, chunk) counts
-//   B  bin_scan  : per bin, exclusive scan over chunks + bin total
-//   C  scatter   : chunk of bindings -> bin-contiguous packed entries
-//                  (local node | bucket << 24)
-//   D  bin_hist  : (bin, split) -> LDS histogram [W][2^BB] -> buckets
+// Each binding b counts for node n in the windows whose cutoff (now_unix -
+// int64(timeRange.Seconds()), binding.go:85) is < ts_b; with the cutoffs
+// sorted that set is a prefix 0..j-1, so one count per binding goes to bucket
+// j-1 and K1 forms GetLastNodeBindingCount per window by suffix sums.
+//
+// Dedupe form (default, one launch): each 1024-thread workgroup aggregates a
+//   2048-binding region per (node, bucket) in an LDS hash and writes one entry
+//   per distinct pair, binned by K1 node block, plus a coalesced row of
+//   (count, offset) words; K1 counts its own block's entries in LDS.  No global
+//   atomics, no bucket matrix.
+// Binned form (when the count/offset matrix would pass 2^22 words, e.g. 4M nodes
+//   x 16M bindings): bindings partitioned by node range ("bins" of 2^BB nodes),
+//   each bin counted in a dense LDS histogram and flushed with contiguous
+//   atomics (lane i -> node i) into the bucket matrix K1 reads and zeroes.
+//     A  bin_count : chunk of bindings -> per-(bin, chunk) counts
+//     B  bin_scan  : per bin, exclusive scan over chunks + bin total
+//     C  scatter   : chunk of bindings -> bin-contiguous packed entries
+//                    (local node | bucket << 24)
+//     D  bin_hist  : (bin, split) -> LDS histogram [W][2^BB] -> buckets
 // Order inside a bin is not deterministic; counts are.
 #include <hip/hip_runtime.h>
-
-#include <cstdlib>
 
 #include "dyn_types.hpp"
 #include "kernels.hpp"
@@ -157,41 +162,7 @@ __global__ __launch_bounds__(kHT) void k2d_bin_hist(const uint32_t* __restrict__
         }
 }
 
-// ---------------------------------------------------------------- two-kernel form
-// X  partition : workgroup b takes 2048 bindings (8 per thread, loads issued
-//                together), counts the in-window ones per node bin in LDS,
-//                scans the bins and writes (local node | bucket << 24) entries
-//                bin-contiguously into ITS OWN 2048-entry region; per bin it
-//                publishes (count, offset) in C/O[bin][b].  No global atomics.
-// Y  bin_hist  : kYSplits workgroups per bin: scan of C[bin][*] in LDS, an
-//                even share of the bin's entries walked across the source
-//                regions, an LDS histogram [W][2^bb], flushed with contiguous
-//                atomics into the (zeroed) buckets.
-// Zipf-hot keys: both kernels aggregate equal keys within a wave before the
-// LDS atomic (one atomic per wave for the wave's most common key).
-constexpr int kXPer = 8;     // bindings per thread in X (16 measured slower: fewer workgroups in flight)
-constexpr int kYPer = 8;     // entries per thread and batch in Y
-constexpr int kXChunk = kHT * kXPer;
-static_assert(kXChunk == kHxRegion, "K1 reads the dedupe regions with this stride");
-constexpr int kYSplits = 16;  // workgroups per bin in Y (Zipf-hot bins want many, each pays a prologue)
-
-// LDS atomicAdd of `add` to a[key] for every active lane, the lanes sharing the
-// first active lane's key merged into one atomic; returns each lane's old value
-// (+ its rank among the merged lanes).
-__device__ __forceinline__ uint32_t wave_lds_add(uint32_t* a, uint32_t key, bool act) {
-    const uint64_t am = __ballot(act);
-    if (am == 0) return 0;
-    const int lead = __ffsll((long long)am) - 1;
-    const uint32_t kl = __shfl(key, lead);
-    const uint64_t m = __ballot(act && key == kl);
-    const int lane = threadIdx.x & 63;
-    const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
-    uint32_t old = 0;
-    if (lane == lead) old = atomicAdd(&a[kl], (uint32_t)__popcll(m));
-    const uint32_t base = __shfl(old, lead);
-    if (act && key != kl) return atomicAdd(&a[key], 1u);
-    return base + rank;
-}
+constexpr int kXChunk = kHxRegion;  // bindings per dedupe-form workgroup (K1 reads the regions with this stride)
 
 // exclusive workgroup scan (BT threads): wave scans + a scan of the wave totals
 template <int BT = kHT>
@@ -210,152 +181,6 @@ __device__ __forceinline__ uint32_t wg_excl_scan_u32(uint32_t v, uint32_t* part)
     for (int i = 0; i < BT / 64; ++i) pre += i < w ? part[i] : 0u;
     __syncthreads();
     return pre + x - v;
-}
-
-__device__ __forceinline__ void k2x_body(const int32_t blk, const int32_t* __restrict__ bnode,
-                                         const int64_t* __restrict__ bts, int64_t B, int64_t N, const HotCutoffs& cut,
-                                         const HotPart& g, uint32_t* __restrict__ C, uint32_t* __restrict__ O,
-                                         uint32_t* __restrict__ region) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];  // hist [nbins], off [nbins]
-    __shared__ uint32_t part[kHT];
-    uint32_t* hist = sh;
-    uint32_t* off = sh + g.nbins;
-    const int64_t b0 = (int64_t)blk * kXChunk + threadIdx.x;
-    int32_t nd[kXPer];
-    int64_t ts[kXPer];
-#pragma unroll
-    for (int u = 0; u < kXPer; ++u) {
-        const int64_t b = b0 + u * kHT;
-        nd[u] = b < B ? bnode[b] : -1;
-        ts[u] = b < B ? bts[b] : INT64_MIN;
-    }
-    for (int i = threadIdx.x; i < g.nbins; i += kHT) hist[i] = 0;
-    __syncthreads();
-    uint32_t ent[kXPer], pos[kXPer];
-    int32_t bin[kXPer];
-    const uint32_t mask = (1u << g.bb) - 1;
-#pragma unroll
-    for (int u = 0; u < kXPer; ++u) {
-        const int j = window_rank(ts[u], cut);
-        const bool ok = nd[u] >= 0 && (int64_t)nd[u] < N && j > 0;  // binding.go:85-91
-        bin[u] = ok ? nd[u] >> g.bb : -1;
-        ent[u] = ((uint32_t)nd[u] & mask) | ((uint32_t)(j - 1) << 24);
-        pos[u] = wave_lds_add(hist, ok ? (uint32_t)bin[u] : 0u, ok);
-    }
-    __syncthreads();
-    // exclusive scan of hist over bins (each thread a contiguous run of bins)
-    const int per = (g.nbins + kHT - 1) / kHT;
-    const int lo = min(g.nbins, (int)threadIdx.x * per), hi = min(g.nbins, lo + per);
-    uint32_t sum = 0;
-    for (int i = lo; i < hi; ++i) sum += hist[i];
-    uint32_t run = wg_excl_scan_u32(sum, part);
-    for (int i = lo; i < hi; ++i) {
-        const uint32_t c = hist[i];
-        off[i] = run;
-        C[(int64_t)i * g.nblk + blk] = c;
-        O[(int64_t)i * g.nblk + blk] = run;
-        run += c;
-    }
-    __syncthreads();
-    uint32_t* reg = region + (int64_t)blk * kXChunk;
-#pragma unroll
-    for (int u = 0; u < kXPer; ++u)
-        if (bin[u] >= 0) reg[off[bin[u]] + pos[u]] = ent[u];
-}
-
-__global__ __launch_bounds__(kHT) void k2x_partition(const int32_t* __restrict__ bnode,
-                                                     const int64_t* __restrict__ bts, int64_t B, int64_t N,
-                                                     HotCutoffs cut, HotPart g, uint32_t* __restrict__ C,
-                                                     uint32_t* __restrict__ O, uint32_t* __restrict__ region) {
-    k2x_body((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, C, O, region);
-}
-
-// K2x and the step path's pod preparation (K3p) in one launch: the two are
-// independent, so the pod tiles ride as extra workgroups behind the
-// partition's (one kernel boundary fewer per scheduling step).
-__global__ __launch_bounds__(kHT) void k2x_pods(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
-                                                int64_t B, int64_t N, HotCutoffs cut, HotPart g,
-                                                uint32_t* __restrict__ C, uint32_t* __restrict__ O,
-                                                uint32_t* __restrict__ region, PodPrep pp) {
-    if ((int32_t)blockIdx.x < g.nblk) k2x_body((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, C, O, region);
-    else k3p_tile256((int64_t)blockIdx.x - g.nblk, pp);
-}
-
-__global__ __launch_bounds__(kHT) void k2y_bin_hist(const uint32_t* __restrict__ region,
-                                                    const uint32_t* __restrict__ C, const uint32_t* __restrict__ O,
-                                                    HotPart g, int32_t W, int64_t N,
-                                                    uint32_t* __restrict__ buckets) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];  // hist [W][2^bb], scan [nblk + 1], off [nblk]
-    __shared__ uint32_t part[kHT];
-    const int bin = blockIdx.x, split = blockIdx.y;
-    const int binw = 1 << g.bb;
-    uint32_t* hist = sh;
-    uint32_t* scan = sh + W * binw;
-    uint32_t* off = scan + g.nblk + 1;
-    for (int i = threadIdx.x; i < W * binw; i += kHT) hist[i] = 0;
-    // scan of the bin's per-source-region counts
-    // (coalesced: consecutive threads read consecutive regions' counts)
-    for (int i = threadIdx.x; i < g.nblk; i += kHT) {
-        scan[i] = C[(int64_t)bin * g.nblk + i];
-        off[i] = O[(int64_t)bin * g.nblk + i];
-    }
-    __syncthreads();
-    const int per = (g.nblk + kHT - 1) / kHT;
-    const int lo = min(g.nblk, (int)threadIdx.x * per), hi = min(g.nblk, lo + per);
-    uint32_t sum = 0;
-    for (int i = lo; i < hi; ++i) sum += scan[i];
-    uint32_t run = wg_excl_scan_u32(sum, part);
-    for (int i = lo; i < hi; ++i) {
-        const uint32_t c = scan[i];
-        scan[i] = run;
-        run += c;
-    }
-    if (threadIdx.x == kHT - 1) scan[g.nblk] = run;
-    __syncthreads();
-    const uint32_t len = scan[g.nblk];
-    // an even share of the bin's entries: Zipf-hot bins spread over the splits
-    const uint32_t e_lo = (uint32_t)((uint64_t)len * split / gridDim.y);
-    const uint32_t e_hi = (uint32_t)((uint64_t)len * (split + 1) / gridDim.y);
-    // each lane walks e = e_lo + tid, + kHT, ... advancing its source region as it
-    // goes; kYPer entries per batch, their loads issued together
-    uint32_t e = e_lo + threadIdx.x;
-    int blk = 0;
-    if (e < e_hi) {  // first region: binary search, then forward steps
-        int l = 0, h = g.nblk - 1;
-        while (l < h) {
-            const int mid = (l + h + 1) >> 1;
-            if (scan[mid] <= e) l = mid;
-            else h = mid - 1;
-        }
-        blk = l;
-    }
-    for (uint32_t e0 = e_lo; e0 < e_hi; e0 += kHT * kYPer) {
-        uint32_t v[kYPer];
-#pragma unroll
-        for (int u = 0; u < kYPer; ++u) {
-            const uint32_t eu = e + u * kHT;
-            v[u] = 0xFFFFFFFFu;
-            if (eu < e_hi) {
-                while (scan[blk + 1] <= eu) ++blk;
-                v[u] = region[(int64_t)blk * kXChunk + off[blk] + (eu - scan[blk])];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kYPer; ++u) {
-            const bool act = v[u] != 0xFFFFFFFFu;
-            (void)wave_lds_add(hist, act ? (v[u] >> 24) * binw + (v[u] & 0xFFFFFF) : 0u, act);
-        }
-        e += kHT * kYPer;
-    }
-    __syncthreads();
-    // buckets are zero on entry (K1 zeroes what it consumes): add the non-zero
-    // counts, lane i -> node i (contiguous atomics)
-    const int64_t n0 = (int64_t)bin << g.bb;
-    for (int w = 0; w < W; ++w)
-        for (int i = threadIdx.x; i < binw; i += kHT) {
-            const uint32_t c = hist[w * binw + i];
-            if (c && n0 + i < N) atomicAdd(&buckets[(int64_t)w * N + n0 + i], c);
-        }
 }
 
 // ---------------------------------------------------------------- dedupe form
@@ -525,58 +350,13 @@ hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int
     uint32_t* CO = scratch + g.cap;  // [nblk][nbins]
     const size_t lds = sizeof(uint32_t) * (2 * (size_t)kDSlots + 2 * (size_t)g.nbins) + sizeof(uint16_t) * kXChunk;
     if (pods && pods->P > 0)
-        hipLaunchKernelGGL(k2x_dedupe_pods, dim3((unsigned)(g.nblk + pods->ntiles)), dim3(kDT), lds, st, bnode, bts,
-                           B, N, cut, g, CO, region, *pods);
-    else
-        hipLaunchKernelGGL(k2x_dedupe, dim3((unsigned)g.nblk), dim3(kDT), lds, st, bnode, bts, B, N, cut, g, CO,
-                           region);
-    return hipGetLastError();
+        return klaunch("k2x_dedupe+k3p_pods", k2x_dedupe_pods, dim3((unsigned)(g.nblk + pods->ntiles)), dim3(kDT), lds,
+                       st, bnode, bts, B, N, cut, g, CO, region, *pods);
+    return klaunch("k2x_dedupe", k2x_dedupe, dim3((unsigned)g.nblk), dim3(kDT), lds, st, bnode, bts, B, N, cut, g, CO,
+                   region);
 }
 
-HotPart hot_part_geometry(int64_t B, int64_t N, int32_t W) {
-    HotPart g{};
-    int bb = 10;
-    while (((N + (1LL << bb) - 1) >> bb) > 4096) ++bb;
-    g.bb = bb;
-    g.nbins = (int32_t)((N + (1LL << bb) - 1) >> bb);
-    g.nblk = (int32_t)((B + kXChunk - 1) / kXChunk);
-    g.cap = (int64_t)g.nblk * kXChunk;  // region entries
-    const size_t ylds = 4 * ((size_t)W * ((size_t)1 << bb) + 2 * (size_t)g.nblk + 1);
-    // the count/offset matrices grow as nbins * nblk (every Y workgroup reads a
-    // row of nblk): past ~2^20 entries the binned K2 is faster (measured at
-    // 4M nodes x 16M bindings: 2.8 ms vs 0.39 ms)
-    g.ok = N > 0 && B > 0 && bb <= 24 && W >= 1 && ylds <= 150 * 1024 &&
-           (double)g.nbins * (double)g.nblk <= (double)(1 << 20);
-    return g;
-}
-
-size_t hot_part_scratch(const HotPart& g) { return (size_t)g.cap + 2 * (size_t)g.nbins * (size_t)g.nblk; }
-
-hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
-                                 const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* scratch,
-                                 hipStream_t st, int which, const PodPrep* pods) {
-    static const hipError_t attr =
-        hipFuncSetAttribute((const void*)k2y_bin_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    if (attr != hipSuccess) return attr;
-    uint32_t* region = scratch;
-    uint32_t* C = scratch + g.cap;
-    uint32_t* O = C + (size_t)g.nbins * g.nblk;
-    if ((which & 1) && pods && pods->P > 0)
-        hipLaunchKernelGGL(k2x_pods, dim3((unsigned)(g.nblk + pods->ntiles)), dim3(kHT), sizeof(uint32_t) * 2 * g.nbins,
-                           st, bnode, bts, B, N, cut, g, C, O, region, *pods);
-    else if (which & 1)
-        hipLaunchKernelGGL(k2x_partition, dim3(g.nblk), dim3(kHT), sizeof(uint32_t) * 2 * g.nbins, st, bnode, bts, B,
-                           N, cut, g, C, O, region);
-    const size_t lds = sizeof(uint32_t) * ((size_t)cut.n_win * ((size_t)1 << g.bb) + 2 * (size_t)g.nblk + 1);
-    static const int ysplits = [] {
-        const char* e = getenv("CRANE_K2Y_SPLITS");
-        return e && atoi(e) > 0 ? atoi(e) : kYSplits;
-    }();
-    if (which & 2)
-        hipLaunchKernelGGL(k2y_bin_hist, dim3(g.nbins, ysplits), dim3(kHT), lds, st, region, C, O, g, cut.n_win, N,
-                           buckets);
-    return hipGetLastError();
-}
+size_t hot_dedupe_scratch(const HotPart& g) { return (size_t)g.cap + (size_t)g.nbins * (size_t)g.nblk; }
 
 HotBins hot_bins_geometry(int64_t B, int64_t N, int32_t W) {
     HotBins g{};
@@ -604,14 +384,18 @@ hipError_t launch_hot_count_binned(const int32_t* bnode, const int64_t* bts, int
         hipFuncSetAttribute((const void*)k2d_bin_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
     if (attr != hipSuccess) return attr;
     const size_t lds_bins = sizeof(uint32_t) * g.nbins;
-    hipLaunchKernelGGL(k2a_bin_count, dim3(g.nchunks), dim3(kHT), lds_bins, st, bnode, bts, B, N, cut, g, chunk_cnt);
-    hipLaunchKernelGGL(k2b_bin_scan, dim3(g.nbins), dim3(kHT), 0, st, chunk_cnt, g, bin_tot);
-    hipLaunchKernelGGL(k2c_scatter, dim3(g.nchunks), dim3(kHT), lds_bins, st, bnode, bts, B, N, cut, g, chunk_cnt,
-                       bin_tot, sorted);
+    hipError_t e = klaunch("k2a_bin_count", k2a_bin_count, dim3(g.nchunks), dim3(kHT), lds_bins, st, bnode, bts, B, N,
+                           cut, g, chunk_cnt);
+    if (e == hipSuccess)
+        e = klaunch("k2b_bin_scan", k2b_bin_scan, dim3(g.nbins), dim3(kHT), 0, st, chunk_cnt, g, bin_tot);
+    if (e == hipSuccess)
+        e = klaunch("k2c_scatter", k2c_scatter, dim3(g.nchunks), dim3(kHT), lds_bins, st, bnode, bts, B, N, cut, g,
+                    (const uint32_t*)chunk_cnt, (const uint32_t*)bin_tot, sorted);
     const size_t lds_hist = sizeof(uint32_t) * (size_t)cut.n_win * ((size_t)1 << g.bb);
-    hipLaunchKernelGGL(k2d_bin_hist, dim3(g.nbins, g.splits), dim3(kHT), lds_hist, st, sorted, bin_tot, g, cut.n_win,
-                       N, buckets);
-    return hipGetLastError();
+    if (e == hipSuccess)
+        e = klaunch("k2d_bin_hist", k2d_bin_hist, dim3(g.nbins, g.splits), dim3(kHT), lds_hist, st,
+                    (const uint32_t*)sorted, (const uint32_t*)bin_tot, g, cut.n_win, N, buckets);
+    return e;
 }
 
 }  // namespace crane

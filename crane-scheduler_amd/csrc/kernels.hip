@@ -1,23 +1,22 @@
 // kernels.hip — CDNA4 (gfx950) kernels of the Dynamic plugin hot path.
 //
-//   K2 hot_count : binding records -> per-node window counts (LDS-aggregated)
+//   K2 hot_count : binding records -> per-node window counts (LDS-aggregated;
+//                  the fallback form, see hotcount.hip for the default)
 //   K1 node_pass : parsed annotation SoA (+ K2 counts) -> NodeRec per node
-//   K3 eval      : pods x nodes Filter + Score + per-pod argmax
 //
 // Numerics follow /root/reference/pkg/plugins/dynamic/stats.go and plugins.go
 // bit for bit: fp64 in the reference's operation order, no FMA contraction
 // (built with -ffp-contract=off), Go's float64->int conversion and wrapping
-// int64 arithmetic.  Wave = 64 lanes; K3 puts 64 PODS on a wave so every node
-// record is wave-uniform and arrives through scalar loads.
+// int64 arithmetic.
 #include <hip/hip_runtime.h>
-
-#include <cstdlib>
 
 #include "dyn_types.hpp"
 #include "kernels.hpp"
 #include "step_node.hpp"
 
 namespace crane {
+
+thread_local KernelTimer* tl_ktimer = nullptr;
 
 // Go int(float64) on amd64 (CVTTSD2SQ): NaN and out-of-range -> INT64_MIN.
 // Used by stats.go:135 (int(score/weight)) and plugins.go:91 (int(hv*10)).
@@ -108,7 +107,7 @@ __global__ __launch_bounds__(kK2Threads) void k2_hot_count(const int32_t* __rest
 // One thread per node.  Reads the parsed SoA (and K2 buckets), writes the
 // node's NodeRec into LDS, then the workgroup streams its records out with
 // 16-byte coalesced stores.
-// block size: 256 by default, CRANE_K1_THREADS=128 selects the narrow variant
+// block size: 256 (the dedupe-form K2 bins nodes by it) or 128
 // STEP: also build the K3 step tables of the pod batch (K3a fused, step.hip):
 // the record is classified straight from registers.
 template <int PD, int PR, int kK1Threads, bool STEP>
@@ -311,13 +310,6 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
 #pragma unroll
         for (int k = 0; k < PD; ++k) e_fail = max(e_fail, r.e_pred[k]);
         r.e_fail = e_fail;
-        bool slow = pol.noprio != 0;
-#pragma unroll
-        for (int k = 0; k < PR; ++k) slow |= !(__builtin_fabs(r.t[k]) < kTermMax);  // NaN/Inf/huge
-        const bool pen_fast = r.pen >= 0 && r.pen < (1LL << 30);
-        slow |= r.e_hv != kTsInvalid && !pen_fast;
-        r.pen32 = pen_fast ? (int32_t)r.pen : 0;
-        r.flags = slow ? kRecSlow : 0;
         if (out) lrec[threadIdx.x] = r;
     }
     if (STEP) {
@@ -346,211 +338,21 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     for (int64_t i = threadIdx.x; i < nvec; i += kK1Threads) dst[i] = src[i];
 }
 
-// ---------------------------------------------------------------- K3
-// blockIdx.x -> 256 pods (4 waves x 64), blockIdx.y -> a chunk of nodes.
-// Every lane walks the chunk's nodes in ascending order keeping a packed
-// 32-bit running key (score << 24 | ~local index) — max keeps the first node
-// with the highest score (lowest-index tie-break) — and one 64-bit atomicMax
-// per pod merges chunks.  The NodeRec address depends only on the loop
-// counter, so it is wave-uniform and arrives through s_load into SGPRs.
-constexpr int kK3Threads = 256;
-
-// Exact reference semantics in 64-bit, for the rare lanes/nodes the fast
-// path cannot take (non-finite usage, |score| >= 2^30, huge or NaN hot value).
-template <int PD, int PR>
-__device__ __attribute__((noinline)) int32_t score_exact(int64_t tnow, const NodeRec<PD, PR>& r, double wsum,
-                                                         int32_t noprio) {
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < PR; ++k)
-        if (tnow < r.e_prio[k]) s += r.t[k];  // stats.go:124-133, policy order
-    const int64_t base = noprio ? 0 : go_int(s / wsum);  // stats.go:135
-    const int64_t pen = tnow < r.e_hv ? r.pen : 0;
-    int64_t f = (int64_t)((uint64_t)base - (uint64_t)pen);  // plugins.go:91, Go int64 wraps
-    return (int32_t)(f < 0 ? 0 : (f > 100 ? 100 : f));     // NormalizeScore (utils.go:58-68)
-}
-
-// A node record's fields as the loop consumes them (wave-uniform -> SGPRs).
-template <int PD, int PR>
-struct RecRegs {
-    int64_t e_fail, e_hv;
-    int32_t pen32, flags;
-    int64_t e_prio[PR];
-    double t[PR];
-};
-
-template <int PD, int PR>
-__device__ __forceinline__ RecRegs<PD, PR> load_rec(const NodeRec<PD, PR>& r) {
-    RecRegs<PD, PR> x;
-    x.e_fail = r.e_fail;
-#pragma unroll
-    for (int k = 0; k < PR; ++k) {
-        x.e_prio[k] = r.e_prio[k];
-        x.t[k] = r.t[k];
-    }
-    x.e_hv = r.e_hv;
-    x.pen32 = r.pen32;
-    x.flags = r.flags;
-    return x;
-}
-
-// Filter + Score of one (pod, node) pair; returns the packed running key
-// (score << 24 | 0xFFFFFF - i), or -1 when the pod may not go to the node.
-template <int PD, int PR, bool DIVT = false>
-__device__ __forceinline__ int32_t eval_pair(int64_t tnow, bool ds, const RecRegs<PD, PR>& x,
-                                             const NodeRec<PD, PR>& r, int32_t i, double wsum, int32_t noprio,
-                                             int32_t* score_out, double inv_w = 0.0, const double* thr = nullptr) {
-    // Filter (plugins.go:55-66): some predicate fresh and over its limit
-    const bool fail = tnow < x.e_fail;
-    // getNodeScore (stats.go:124-135): fresh terms summed in policy order.
-    // fma(1.0, t, s) == s + t exactly; fma(0.0, t, s) == s for finite t
-    // (s is never -0.0), so a 0/1 mask replaces the select of the sum.
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < PR; ++k) {
-        const double m = tnow < x.e_prio[k] ? 1.0 : 0.0;
-        s = __builtin_fma(m, x.t[k], s);
-    }
-    int32_t base;
-    bool in_range;
-    if constexpr (DIVT) {
-        // trunc(RN(s/W)) from q0 = RN(s * RN(1/W)): within 1, fixed by the thresholds.
-        // For RN(s/W) < 1 this yields 0, which clamps to the same final score
-        // as the reference's (<= 0) base since the penalty is >= 0 here.
-        const double q0 = s * inv_w;
-        in_range = q0 < kQFast;  // false for NaN; negative q0 clamps to k0 = 0
-        int32_t k0;
-        asm("v_cvt_i32_f64 %0, %1" : "=v"(k0) : "v"(q0));
-        k0 = min(max(k0, 0), kQMax - 1);
-        base = k0 + (s >= thr[k0 + 1] ? 1 : 0) - (s < thr[k0] ? 1 : 0);
-    } else {
-        const double q = s / wsum;
-        in_range = __builtin_fabs(q) < kFastLim;  // false for NaN
-        // v_cvt_i32_f64 truncates (saturating; lanes out of range take the exact path below)
-        asm("v_cvt_i32_f64 %0, %1" : "=v"(base) : "v"(q));
-    }
-    // score - int(hotValue*10), NormalizeScore to [0,100] (plugins.go:91-93)
-    const int32_t pen = tnow < x.e_hv ? x.pen32 : 0;
-    int32_t f = min(max(base - pen, 0), 100);
-    if ((x.flags & kRecSlow) || !in_range) f = score_exact<PD, PR>(tnow, r, wsum, noprio);
-    if (score_out) *score_out = f;
-    const bool feasible = ds || !fail;
-    return feasible ? ((f << 24) | (0xFFFFFF - i)) : -1;
-}
-
-// V: 0 = plain loop, 1 = next record prefetched into SGPRs during the current
-// one, 2 = two nodes per iteration.
-template <int PD, int PR, bool MATRIX, int V>
-__global__ __launch_bounds__(kK3Threads) void k3_eval(const NodeRec<PD, PR>* __restrict__ rec, int32_t N,
-                                                      int32_t chunk, int64_t node_offset,
-                                                      const int64_t* __restrict__ now, const uint8_t* __restrict__ flags,
-                                                      int64_t P, double wsum, int32_t noprio,
-                                                      long long* __restrict__ keys, MatrixOut mo, double inv_w,
-                                                      const double* __restrict__ thr_g) {
-    // V4: V3 + division-free threshold quotient (thr_g has kQMax + 1 entries)
-    constexpr bool DIVT = V == 4;
-    __shared__ double thr[DIVT ? kQMax + 1 : 1];
-    if constexpr (DIVT) {
-        for (int k = threadIdx.x; k <= kQMax; k += kK3Threads) thr[k] = thr_g[k];
-        __syncthreads();
-    }
-    // V3: 1-D grid, XCD-aware.  Workgroups are dealt round-robin over the 8
-    // XCDs (b % 8 shares an XCD), so give every XCD its own 1/8 of the node
-    // chunks: each XCD's L2 then holds 1/8 of the record table.
-    int64_t pg, ch;
-    if constexpr (V == 3 || V == 4) {
-        const int64_t b = blockIdx.x, slot = b >> 3, pgs = (P + kK3Threads - 1) / kK3Threads;
-        pg = slot % pgs;
-        ch = (b & 7) + 8 * (slot / pgs);
-    } else {
-        pg = blockIdx.x;
-        ch = blockIdx.y;
-    }
-    const int64_t pod = pg * kK3Threads + threadIdx.x;
-    const bool live = pod < P;
-    const int64_t tnow = live ? now[pod] : INT64_MIN;
-    const bool ds = live && flags && (flags[pod] & 1u);
-    const int32_t n0 = (int32_t)min((int64_t)N, ch * chunk);
-    const int32_t cnt = min(N - n0, chunk);
-    const NodeRec<PD, PR>* __restrict__ r0 = rec + n0;
-    int32_t best = -1;
-    if constexpr (MATRIX) {
-        for (int32_t i = 0; i < cnt; ++i) {
-            const RecRegs<PD, PR> x = load_rec(r0[i]);
-            int32_t f;
-            best = max(best, eval_pair<PD, PR, DIVT>(tnow, ds, x, r0[i], i, wsum, noprio, &f, inv_w, thr));
-            if (live) {
-                int8_t ff = -1;
-                if (!ds) {
-#pragma unroll
-                    for (int k = PD - 1; k >= 0; --k)
-                        if (tnow < r0[i].e_pred[k]) ff = mo.pred_orig[k];
-                }
-                const int64_t n = n0 + i;
-                if (mo.first_fail) mo.first_fail[pod * N + n] = ff;
-                if (mo.score) mo.score[pod * N + n] = f;
-            }
-        }
-    } else if constexpr (V == 1) {
-        if (cnt > 0) {
-            RecRegs<PD, PR> cur = load_rec(r0[0]);
-            for (int32_t i = 0; i < cnt; ++i) {
-                const int32_t j = i + 1 < cnt ? i + 1 : i;
-                const RecRegs<PD, PR> nxt = load_rec(r0[j]);
-                best = max(best, eval_pair<PD, PR>(tnow, ds, cur, r0[i], i, wsum, noprio, nullptr));
-                cur = nxt;
-            }
-        }
-    } else if constexpr (V == 2) {
-        int32_t i = 0;
-        for (; i + 1 < cnt; i += 2) {
-            const RecRegs<PD, PR> a = load_rec(r0[i]);
-            const RecRegs<PD, PR> b = load_rec(r0[i + 1]);
-            const int32_t ka = eval_pair<PD, PR>(tnow, ds, a, r0[i], i, wsum, noprio, nullptr);
-            const int32_t kb = eval_pair<PD, PR>(tnow, ds, b, r0[i + 1], i + 1, wsum, noprio, nullptr);
-            best = max(best, max(ka, kb));
-        }
-        if (i < cnt) best = max(best, eval_pair<PD, PR>(tnow, ds, load_rec(r0[i]), r0[i], i, wsum, noprio, nullptr));
-    } else {
-        for (int32_t i = 0; i < cnt; ++i)
-            best = max(best, eval_pair<PD, PR, DIVT>(tnow, ds, load_rec(r0[i]), r0[i], i, wsum, noprio, nullptr,
-                                                     inv_w, thr));
-    }
-    if (live && best >= 0) {
-        const int64_t sc = best >> 24;
-        const int64_t n = n0 + (0xFFFFFF - (best & 0xFFFFFF));
-        const long long key = (long long)((sc << 32) | (int64_t)(0xFFFFFFFFull - (uint64_t)(node_offset + n)));
-        atomicMax(&keys[pod], key);
-    }
-}
-
 // ---------------------------------------------------------------- launchers
-int k1_threads() {
-    // 256 by default: half the node blocks, so half the dedupe-form K2's (count,
-    // offset) matrix and of K3s's producer-block scans (config 3: 0.0429 vs 0.0442 ms
-    // per step); CRANE_K1_THREADS=128 selects the narrow variant
-    const char* e = getenv("CRANE_K1_THREADS");
-    return e && atoi(e) == 128 ? 128 : 256;
-}
-
 template <int PD, int PR>
 static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t st) {
     if (a.N <= 0) return hipSuccess;
-    const int T = a.threads ? a.threads : k1_threads();
+    const int T = a.threads;
     if (T != 128 && T != 256) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((a.N + T - 1) / T);
     const size_t lds = sizeof(NodeRec<PD, PR>) * T;
     const K1Step sa = step ? *step : K1Step{};
-#define K1_LAUNCH(TT, S) hipLaunchKernelGGL((k1_node_pass<PD, PR, TT, S>), dim3(grid), dim3(TT), lds, st, a, sa)
-    if (T == 256) {
-        if (step) K1_LAUNCH(256, true);
-        else K1_LAUNCH(256, false);
-    } else {
-        if (step) K1_LAUNCH(128, true);
-        else K1_LAUNCH(128, false);
-    }
-#undef K1_LAUNCH
-    return hipGetLastError();
+    const char* nm = step ? "k1_node_pass+k3a_steps" : "k1_node_pass";
+    if (T == 256)
+        return step ? klaunch(nm, k1_node_pass<PD, PR, 256, true>, dim3(grid), dim3(256), lds, st, a, sa)
+                    : klaunch(nm, k1_node_pass<PD, PR, 256, false>, dim3(grid), dim3(256), lds, st, a, sa);
+    return step ? klaunch(nm, k1_node_pass<PD, PR, 128, true>, dim3(grid), dim3(128), lds, st, a, sa)
+                : klaunch(nm, k1_node_pass<PD, PR, 128, false>, dim3(grid), dim3(128), lds, st, a, sa);
 }
 
 hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step) {
@@ -578,80 +380,8 @@ hipError_t launch_hot_count(const int32_t* bnode, const int64_t* bts, int64_t B,
     static const hipError_t attr =
         hipFuncSetAttribute((const void*)k2_hot_count, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(k2_hot_count, dim3(grid), dim3(kK2Threads), lds, st, bnode, bts, B, N, cut, buckets);
-    return hipGetLastError();
-}
-
-// Tuning knobs read per launch (for A/B runs): CRANE_K3_VARIANT, CRANE_K3_ROUNDS.
-static int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e && *e ? atoi(e) : dflt;
-}
-int k3_variant() { return env_int("CRANE_K3_VARIANT", 5); }
-
-int64_t eval_chunk_nodes(int64_t P, int64_t N) {
-    // Size the grid to whole residency rounds: 256 CUs x 8 blocks of 4 waves
-    // (8 waves/SIMD at <= 64 VGPRs) = 2048 resident blocks per round.
-    int rounds = env_int("CRANE_K3_ROUNDS", 16);
-    if (rounds < 1) rounds = 16;
-    const int64_t pod_blocks = (P + kK3Threads - 1) / kK3Threads;
-    int64_t chunks = (2048LL * rounds) / pod_blocks;
-    if (chunks < 1) chunks = 1;
-    int64_t chunk = (N + chunks - 1) / chunks;
-    if (chunk < 64) chunk = 64;
-    if (chunk > (1 << 24)) chunk = 1 << 24;  // the running key keeps 24 bits of local index
-    return chunk;
-}
-
-template <int PD, int PR>
-static hipError_t launch_k3_t(const void* rec, int64_t N, int64_t node_offset, const int64_t* now,
-                              const uint8_t* flags, int64_t P, double wsum, int32_t noprio, long long* keys,
-                              const MatrixOut& mo, double inv_w, const double* thr, hipStream_t st) {
-    if (P <= 0 || N <= 0) return hipSuccess;
-    if (N > 0x7FFFFFFF) return hipErrorInvalidValue;
-    const int64_t chunk = eval_chunk_nodes(P, N);
-    const dim3 grid((unsigned)((P + kK3Threads - 1) / kK3Threads), (unsigned)((N + chunk - 1) / chunk));
-    const auto* r = static_cast<const NodeRec<PD, PR>*>(rec);
-    const int32_t n32 = (int32_t)N, c32 = (int32_t)chunk;
-    const bool matrix = mo.first_fail || mo.score;
-    int v = k3_variant();
-    if (v == 5) v = 4;  // the step path (step.hip) serves keys-only launches; matrix output uses V4
-    if (v == 4 && !thr) v = 3;  // no threshold table for this policy (weight sum <= 0 or no priorities)
-    if (matrix && (v == 1 || v == 2)) v = 0;
-    // V3/V4 use a 1-D XCD-swizzled grid with the chunk count padded to a multiple of 8
-    const unsigned chunks8 = (grid.y + 7) / 8 * 8;
-    const dim3 g1(grid.x * chunks8), blk(kK3Threads);
-#define K3_LAUNCH(M, V, G)                                                                                     \
-    hipLaunchKernelGGL((k3_eval<PD, PR, M, V>), G, blk, 0, st, r, n32, c32, node_offset, now, flags, P, wsum, \
-                       noprio, keys, mo, inv_w, thr)
-    if (matrix) {
-        if (v == 4) K3_LAUNCH(true, 4, g1);
-        else if (v == 3) K3_LAUNCH(true, 3, g1);
-        else K3_LAUNCH(true, 0, grid);
-    } else {
-        switch (v) {
-            case 1: K3_LAUNCH(false, 1, grid); break;
-            case 2: K3_LAUNCH(false, 2, grid); break;
-            case 3: K3_LAUNCH(false, 3, g1); break;
-            case 4: K3_LAUNCH(false, 4, g1); break;
-            default: K3_LAUNCH(false, 0, grid); break;
-        }
-    }
-#undef K3_LAUNCH
-    return hipGetLastError();
-}
-
-hipError_t launch_eval(int shape, const void* rec, int64_t N, int64_t node_offset, const int64_t* now,
-                       const uint8_t* flags, int64_t P, double wsum, int32_t noprio, long long* keys,
-                       const MatrixOut& mo, double inv_w, const double* thr, hipStream_t st) {
-    switch (shape) {
-        case kShape4x6:
-            return launch_k3_t<4, 6>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, mo, inv_w, thr, st);
-        case kShape8x8:
-            return launch_k3_t<8, 8>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, mo, inv_w, thr, st);
-        default:
-            return launch_k3_t<16, 16>(rec, N, node_offset, now, flags, P, wsum, noprio, keys, mo, inv_w, thr, st);
-    }
+    return klaunch("k2_hot_count", k2_hot_count, dim3(grid), dim3(kK2Threads), lds, st, bnode, bts, B, N, cut,
+                   buckets);
 }
 
 }  // namespace crane

@@ -1,5 +1,6 @@
-// kernels.hpp — host-side launch interface of kernels.hip.
+// kernels.hpp — host-side launch interface of the engine's kernels.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -10,17 +11,54 @@ namespace crane {
 // NodeRec template instances (max predicates x max priorities).
 enum { kShape4x6 = 0, kShape8x8 = 1, kShape16x16 = 2 };
 
+// ---------------------------------------------------------------- launches
+// Kernel timing (crane_dyn_set_profiling): while a KernelTimer is installed on
+// the calling thread, every launch gets a (start, stop) event pair that the
+// runtime stamps from the dispatch itself (hipExtLaunchKernel), i.e. the
+// kernel's own begin -> end as rocprofv3 --kernel-trace reports it.
+struct KernelTimer {
+    virtual ~KernelTimer() = default;
+    virtual void next(const char* name, hipEvent_t* start, hipEvent_t* stop) = 0;
+};
+extern thread_local KernelTimer* tl_ktimer;
+
+template <typename... KArgs, typename... Args>
+inline hipError_t klaunch(const char* name, void (*kernel)(KArgs...), dim3 grid, dim3 block, size_t lds,
+                          hipStream_t st, Args... args) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (tl_ktimer) tl_ktimer->next(name, &a, &b);
+    hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, st, a, b, 0u, static_cast<KArgs>(args)...);
+    return hipGetLastError();
+}
+
 struct HotCutoffs {
     int32_t n_win;
     int32_t pad;
     int64_t sorted[kMaxWin];  // ascending now_unix - int64(timeRange.Seconds())
 };
 
-struct MatrixOut {
-    int8_t* first_fail;  // [P][N] or null
-    int64_t* score;      // [P][N] or null
+// ---------------------------------------------------------------- K3m (matrix.hip)
+// Per-pair Filter + Score of every (pod, node): first failing predicate and
+// score matrices [P][ld] (row p, column = local node), and/or the per-pod
+// packed keys (max over the shard's feasible nodes).
+struct MatrixArgs {
+    const void* rec;        // NodeRec [N]
+    int64_t N, node_offset;
+    const int64_t* now;     // [P]
+    const uint8_t* flags;   // [P] or null
+    int64_t P;
+    int64_t ld;             // row stride of the output matrices (>= N)
+    double wsum;
+    int32_t noprio;
+    int32_t pad;
+    int8_t* first_fail;     // [P][ld] or null: -1 = Filter Success, else policy predicate index
+    void* score;            // [P][ld] int8 or int64 (score_i64), or null
+    int32_t score_i64;
+    int32_t pad2;
+    long long* keys;        // [P] or null: max-combined (atomicMax, keys must be initialised to -1)
     int8_t pred_orig[kMaxPred];  // device predicate -> policy predicate index
 };
+hipError_t launch_matrix(int shape, const MatrixArgs& a, hipStream_t st);
 
 // Sequential greedy (greedy.hip)
 constexpr int64_t kGreedyMaxNodes = 64LL * 64 * 64 * 64;
@@ -60,7 +98,8 @@ hipError_t launch_merge_assign(const int64_t* Fs, int64_t nF, const int64_t* Is,
                                int64_t P, int64_t Pd, int32_t* apos, int32_t* q, int64_t* gi, int64_t* chosen,
                                hipStream_t st);
 
-// Bin-partitioned K2 (hotcount.hip)
+// ---------------------------------------------------------------- K2 (hotcount.hip, kernels.hip)
+// Bin-partitioned K2 (four kernels, bucket matrix): the form for large node counts.
 constexpr int kMaxBins = 4096;
 struct HotBins {
     int32_t bb;       // log2(nodes per bin)
@@ -73,19 +112,18 @@ HotBins hot_bins_geometry(int64_t B, int64_t N, int32_t W);
 hipError_t launch_hot_count_binned(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                    const HotCutoffs& cut, uint32_t* buckets, const HotBins& g, uint32_t* chunk_cnt,
                                    uint32_t* bin_tot, uint32_t* sorted, hipStream_t st);
+// LDS-hash K2 (one kernel, global atomics into the bucket matrix): the fallback of any shape.
+hipError_t launch_hot_count(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N, const HotCutoffs& cut,
+                            uint32_t* buckets, hipStream_t st);
 
-// Two-kernel partitioned K2 (hotcount.hip): each partition workgroup writes
-// its in-window bindings bin-contiguously into its own region and publishes
-// per-bin (count, offset); no global atomics besides the final bucket adds.
+// Dedupe form (default): one launch (K2x' [+ K3p]); bins = the node pass's workgroups
+// (bs nodes), consumed by K1 through K1Args::hx_*.  Region stride kHxRegion entries.
 struct HotPart {
     int32_t bb, nbins;  // 2^bb nodes per bin
     int64_t cap;        // region entries (nblk * 2048)
     int32_t nblk;       // partition workgroups
     bool ok;
 };
-HotPart hot_part_geometry(int64_t B, int64_t N, int32_t W);
-size_t hot_part_scratch(const HotPart& g);  // uint32 entries: region + C + O
-// Adds into buckets[W][N], which must be zero on entry.  Scratch needs no initialisation.
 // The step path's pod preparation (K3p) for 1024-pod tiles, as it rides in K2x's launch.
 struct PodPrep {
     const int64_t* now;
@@ -96,19 +134,14 @@ struct PodPrep {
     int64_t* tile_mm;
     long long* keys;
 };
-// Dedupe form: one launch (K2x' [+ K3p]); bins = the node pass's workgroups (bs
-// nodes), consumed by K1 through K1Args::hx_*.  Region stride kHxRegion entries.
 constexpr int kHxRegion = 2048;
 HotPart hot_dedupe_geometry(int64_t B, int64_t N, int32_t W, int32_t bs);
+size_t hot_dedupe_scratch(const HotPart& g);  // uint32 entries: regions + count/offset matrix
 hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                    const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
                                    const PodPrep* pods = nullptr);
-// pods (optional, with which & 1): K3p's tiles run as extra workgroups of the K2x launch
-hipError_t launch_hot_count_part(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
-                                 const HotCutoffs& cut, uint32_t* buckets, const HotPart& g, uint32_t* scratch,
-                                 hipStream_t st, int which = 3, const PodPrep* pods = nullptr);  // 1: k2x, 2: k2y
 
-// K3 step path (step.hip): per-batch node step tables + pair eval.
+// ---------------------------------------------------------------- K3 step path (step.hip)
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
 constexpr int64_t kStepMaxNodes = 1LL << 24;  // packed key keeps 24 bits of node index
 // A node whose key changes once inside the batch: key k0 for now < bp, k1 after.
@@ -124,8 +157,8 @@ struct alignas(16) VRec {  // 16-byte multiple: K3s stages records with 16-byte 
     int32_t key[NB + 1];
     int32_t cnt;
 };
-// Step tables, one region per producer workgroup b (K1: bs = 128 nodes, K3a:
-// 256): its flat-key maxima flat[b][kind], its record counts cnt[b][L]
+// Step tables, one region per producer workgroup b (K1: bs = 128/256 nodes,
+// K3a: 256): its flat-key maxima flat[b][kind], its record counts cnt[b][L]
 // (L = 2 * kind + 0: Step1, 1: VRec) and its records at b * bs + slot of each
 // list.  Producers need no global atomics; K3s scans the counts of the
 // producer blocks it covers.
@@ -140,16 +173,14 @@ struct StepTables {
 };
 struct StepGeometry {
     int64_t nseg, npad, ntiles, ngroups;
-    int32_t R;  // K3s workgroups per 256-pod group (R is raised until each covers <= kK3sMaxBlk producer blocks)
+    int32_t R;  // K3s workgroups per 1024-pod group (raised until each covers <= kK3sMaxBlk producer blocks)
 };
 constexpr int kK3sMaxBlk = 1024;
 size_t step_vrec_bytes(int shape);
 StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk);
-int k1_threads();  // K1 workgroup size (256, or 128 with CRANE_K1_THREADS=128)
-// K3p: perm, pnow [ntiles * 1024], tile_mm [2 * ntiles]; initialises keys[0..P) to -1 and the step header
+// K3p: perm, pnow [ntiles * 1024], tile_mm [2 * ntiles]; initialises keys[0..P) to -1
 hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys,
-                            const StepTables& st, const StepGeometry& g, int32_t* perm, int64_t* pnow,
-                            int64_t* tile_mm, hipStream_t s);
+                            const StepGeometry& g, int32_t* perm, int64_t* pnow, int64_t* tile_mm, hipStream_t s);
 // K3a: step tables from NodeRecs in HBM (after K3p)
 hipError_t launch_step_nodes(int shape, const void* rec, int64_t N, double wsum, int32_t noprio,
                              const StepTables& st, const StepGeometry& g, const int64_t* tile_mm, hipStream_t s);
@@ -165,18 +196,13 @@ struct K1Step {
     double wsum;
     StepTables st;
 };
-int k3_variant();
 
 size_t node_rec_bytes(int shape);
-int64_t eval_chunk_nodes(int64_t P, int64_t N);
 
-hipError_t launch_hot_count(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N, const HotCutoffs& cut,
-                            uint32_t* buckets, hipStream_t st);
-// K1 zeroes the buckets it consumes (so the next K2 needs no memset); with
-// cnt_out it also stores the per-window counts [W][N].
+// ---------------------------------------------------------------- K1 (kernels.hip)
 // K1 node pass arguments.  Hot value source: buckets (K2 counts, consumed:
-// zeroed, the value kept in hvc_out) > hv with hv_ts (annotation; hv_ts null:
-// every node stamped hv_ts_counts) > none.
+// zeroed, the value kept in hvc_out) or the dedupe-form entries (hx_*) > hv with
+// hv_ts (annotation; hv_ts null: every node stamped hv_ts_counts) > none.
 struct K1Args {
     DevPolicy pol;
     int64_t N;
@@ -195,13 +221,9 @@ struct K1Args {
     const uint32_t* hx_region;
     const uint32_t* hx_CO;
     int32_t hx_nblk;
-    int32_t threads;        // workgroup size (0: k1_threads())
+    int32_t threads;        // workgroup size: 128 or 256
 };
 // step (optional): also build the K3 step tables of a pod batch (K3a fused).
 hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr);
-// thr: device table of kQMax + 1 quotient thresholds (null = divide); inv_w = RN(1/wsum)
-hipError_t launch_eval(int shape, const void* rec, int64_t N, int64_t node_offset, const int64_t* now,
-                       const uint8_t* flags, int64_t P, double wsum, int32_t noprio, long long* keys,
-                       const MatrixOut& mo, double inv_w, const double* thr, hipStream_t st);
 
 }  // namespace crane

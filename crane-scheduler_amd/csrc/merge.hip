@@ -376,10 +376,9 @@ hipError_t launch_merge_hist(const int64_t* base, const uint8_t* leaf, const uin
     hipError_t e = hipMemsetAsync(H, 0, sizeof(unsigned long long) * 2 * kLevels, st);
     if (e == hipSuccess) e = hipMemsetAsync(flag, 0, sizeof(int32_t), st);
     if (e != hipSuccess) return e;
-    if (N > 0)
-        hipLaunchKernelGGL(m1_hist, dim3((unsigned)((N + kMT - 1) / kMT)), dim3(kMT), 0, st, base, leaf, cnt, N, a,
-                           capF, capI, H, flag);
-    return hipGetLastError();
+    if (N <= 0) return hipSuccess;
+    return klaunch("m1_hist", m1_hist, dim3((unsigned)((N + kMT - 1) / kMT)), dim3(kMT), 0, st, base, leaf, cnt, N, a,
+                   capF, capI, H, flag);
 }
 
 int64_t merge_bsum_len(int64_t N, int vlo) { return (int64_t)(101 - vlo) * ((N + kMT - 1) / kMT); }
@@ -389,10 +388,12 @@ hipError_t launch_merge_stream(const int64_t* base, const uint8_t* leaf, const u
                                int64_t* stream, hipStream_t st) {
     if (N <= 0 || cap <= 0) return hipSuccess;
     const unsigned nb = (unsigned)((N + kMT - 1) / kMT);
-    hipLaunchKernelGGL(m2_bsum, dim3(nb), dim3(kMT), 0, st, base, leaf, cnt, N, a, T, vlo, cap, bs);
-    hipLaunchKernelGGL(m3_scan, dim3(1), dim3(kM5T), 0, st, bs, merge_bsum_len(N, vlo));
-    hipLaunchKernelGGL(m4_place, dim3(nb), dim3(kMT), 0, st, base, leaf, cnt, N, a, T, vlo, cap, bs, stream);
-    return hipGetLastError();
+    hipError_t e = klaunch("m2_bsum", m2_bsum, dim3(nb), dim3(kMT), 0, st, base, leaf, cnt, N, a, T, vlo, cap, bs);
+    if (e == hipSuccess) e = klaunch("m3_scan", m3_scan, dim3(1), dim3(kM5T), 0, st, bs, merge_bsum_len(N, vlo));
+    if (e == hipSuccess)
+        e = klaunch("m4_place", m4_place, dim3(nb), dim3(kMT), 0, st, base, leaf, cnt, N, a, T, vlo, cap,
+                    (const unsigned long long*)bs, stream);
+    return e;
 }
 
 hipError_t launch_merge_assign(const int64_t* Fs, int64_t nF, const int64_t* Is, int64_t nI, const uint8_t* flags,
@@ -401,16 +402,20 @@ hipError_t launch_merge_assign(const int64_t* Fs, int64_t nF, const int64_t* Is,
     if (P <= 0) return hipSuccess;
     const unsigned pb = (unsigned)((P + kMT - 1) / kMT);
     if (Pd == 0 || nI == 0) {  // no DaemonSet pod can take an infeasible node: pod p takes F[p]
-        hipLaunchKernelGGL(m5z_direct, dim3(pb), dim3(kMT), 0, st, Fs, nF, P, chosen);
-        return hipGetLastError();
+        return klaunch("m5z_direct", m5z_direct, dim3(pb), dim3(kMT), 0, st, Fs, nF, P, chosen);
     }
     int64_t* K = gi + nI;  // scratch: gi [nI] then K
-    hipLaunchKernelGGL(m5a_compact, dim3(1), dim3(kM5T), 0, st, flags, P, apos);
-    hipLaunchKernelGGL(m5b_thresholds, dim3((unsigned)((nI + kMT - 1) / kMT)), dim3(kMT), 0, st, Fs, nF, Is, nI,
-                       apos, Pd, gi);
-    hipLaunchKernelGGL(m5c_takers, dim3(1), dim3(kM5T), 0, st, gi, nI, apos, Pd, q, K);
-    hipLaunchKernelGGL(m5d_assign, dim3(pb), dim3(kMT), 0, st, Fs, nF, Is, q, K, P, chosen);
-    return hipGetLastError();
+    hipError_t e = klaunch("m5a_compact", m5a_compact, dim3(1), dim3(kM5T), 0, st, flags, P, apos);
+    if (e == hipSuccess)
+        e = klaunch("m5b_thresholds", m5b_thresholds, dim3((unsigned)((nI + kMT - 1) / kMT)), dim3(kMT), 0, st, Fs, nF,
+                    Is, nI, (const int32_t*)apos, Pd, gi);
+    if (e == hipSuccess)
+        e = klaunch("m5c_takers", m5c_takers, dim3(1), dim3(kM5T), 0, st, (const int64_t*)gi, nI,
+                    (const int32_t*)apos, Pd, q, K);
+    if (e == hipSuccess)
+        e = klaunch("m5d_assign", m5d_assign, dim3(pb), dim3(kMT), 0, st, Fs, nF, Is, (const int32_t*)q,
+                    (const int64_t*)K, P, chosen);
+    return e;
 }
 
 }  // namespace crane

@@ -28,7 +28,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 
 #include "dyn_types.hpp"
 #include "kernels.hpp"
@@ -127,11 +126,10 @@ constexpr int kK3sWaves = 4;
 constexpr int kK3sThreads = kK3sWaves * 64;
 constexpr int kK3sPPL = 4;                          // pods per lane
 constexpr int kK3sPods = kK3sThreads * kK3sPPL;     // pods per workgroup (= kPodTile)
-#ifndef CRANE_K3S_S1
-#define CRANE_K3S_S1 512  // build-time A/B knob
-#endif
-constexpr int kK3sS1 = CRANE_K3S_S1;  // Step1 records staged per round and pod kind (512: 8 KB)
+constexpr int kK3sS1 = 512;  // Step1 records staged per round and pod kind (8 KB; 128..1024 measured slower at config 4)
 constexpr int kK3sVR = 32;   // VRec records staged per round and pod kind
+static_assert(kK3sS1 >= 64 && kK3sS1 % 64 == 0, "the staging rounds must make progress");
+static_assert(2 * kK3sS1 * 16 + 2 * kK3sVR * 240 + 4 * 4 * (kK3sMaxBlk + 1) <= 64 * 1024, "K3s LDS budget");
 
 // position in the per-producer-block layout of element i of the concatenation
 // of blocks b0 + 0 .. m-1 (pre: exclusive prefix of their counts, pre[m] = total)
@@ -400,15 +398,12 @@ StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk) {
     g.npad = g.nseg * kStepSeg;  // >= nblk * bs for bs = 128 or 256
     g.ntiles = (P + kPodTile - 1) / kPodTile;
     g.ngroups = (P + kK3sPods - 1) / kK3sPods;
-    // R workgroups per 1024-pod group: ~1024 workgroups in all, at most 48 per group,
-    // and enough that each covers at most kK3sMaxBlk producer blocks
-    const char* e = getenv("CRANE_K3S_BLOCKS");
-    const int64_t target = e && atoi(e) > 0 ? atoi(e) : 1024;
-    // at most kR slices per group: past ~48 the per-workgroup prologue (producer counts,
-    // pod loads) outweighs the shorter slices (config 3, 10 groups: R 64 -> 48 = 14.9 -> 13.6 us)
-    const char* re = getenv("CRANE_K3S_RMAX");
-    const int64_t kR = re && atoi(re) > 0 ? atoi(re) : 48;
-    int64_t R = std::min<int64_t>(kR, std::max<int64_t>(1, target / std::max<int64_t>(g.ngroups, 1)));
+    // R workgroups per 1024-pod group: ~1024 workgroups in all, at most 48 per group
+    // (past ~48 the per-workgroup prologue — producer counts, pod loads — outweighs the
+    // shorter slices: config 3, 10 groups, R 64 -> 48 = 14.9 -> 13.6 us), and enough
+    // that each covers at most kK3sMaxBlk producer blocks
+    constexpr int64_t kTarget = 1024, kR = 48;
+    int64_t R = std::min<int64_t>(kR, std::max<int64_t>(1, kTarget / std::max<int64_t>(g.ngroups, 1)));
     R = std::max<int64_t>(R, (nblk + kK3sMaxBlk - 1) / kK3sMaxBlk);
     g.R = (int32_t)R;
     return g;
@@ -417,18 +412,15 @@ StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk) {
 template <int PD, int PR>
 static hipError_t launch_steps_t(const void* rec, int64_t N, double wsum, int32_t noprio, const StepTables& st,
                                  const StepGeometry& g, const int64_t* tile_mm, hipStream_t s) {
-    hipLaunchKernelGGL((k3a_steps<PD, PR>), dim3((unsigned)g.nseg), dim3(kStepSeg), 0, s,
-                       static_cast<const NodeRec<PD, PR>*>(rec), N, tile_mm, (int32_t)g.ntiles, wsum, noprio, st);
-    return hipGetLastError();
+    return klaunch("k3a_steps", k3a_steps<PD, PR>, dim3((unsigned)g.nseg), dim3(kStepSeg), 0, s,
+                   static_cast<const NodeRec<PD, PR>*>(rec), N, tile_mm, (int32_t)g.ntiles, wsum, noprio, st);
 }
 
 hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys,
-                            const StepTables& st, const StepGeometry& g, int32_t* perm, int64_t* pnow,
-                            int64_t* tile_mm, hipStream_t s) {
+                            const StepGeometry& g, int32_t* perm, int64_t* pnow, int64_t* tile_mm, hipStream_t s) {
     if (P <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k3p_pods, dim3((unsigned)g.ntiles), dim3(kPodTile), 0, s, now, flags, P, perm, pnow, tile_mm,
-                       keys);
-    return hipGetLastError();
+    return klaunch("k3p_pods", k3p_pods, dim3((unsigned)g.ntiles), dim3(kPodTile), 0, s, now, flags, P, perm, pnow,
+                   tile_mm, keys);
 }
 
 hipError_t launch_step_nodes(int shape, const void* rec, int64_t N, double wsum, int32_t noprio,
@@ -449,15 +441,12 @@ hipError_t launch_step_pairs(int shape, int64_t N, int64_t node_offset, int64_t 
     const dim3 grid((unsigned)(g.ngroups * g.R)), blk(kK3sThreads);
     switch (shape) {
         case kShape4x6:
-            hipLaunchKernelGGL((k3s_eval<6 + 2>), grid, blk, 0, s, st, perm, pnow, P, node_offset, g.R, keys);
-            break;
+            return klaunch("k3s_eval", k3s_eval<6 + 2>, grid, blk, 0, s, st, perm, pnow, P, node_offset, g.R, keys);
         case kShape8x8:
-            hipLaunchKernelGGL((k3s_eval<8 + 2>), grid, blk, 0, s, st, perm, pnow, P, node_offset, g.R, keys);
-            break;
+            return klaunch("k3s_eval", k3s_eval<8 + 2>, grid, blk, 0, s, st, perm, pnow, P, node_offset, g.R, keys);
         default:
-            hipLaunchKernelGGL((k3s_eval<16 + 2>), grid, blk, 0, s, st, perm, pnow, P, node_offset, g.R, keys);
+            return klaunch("k3s_eval", k3s_eval<16 + 2>, grid, blk, 0, s, st, perm, pnow, P, node_offset, g.R, keys);
     }
-    return hipGetLastError();
 }
 
 }  // namespace crane

@@ -11,6 +11,8 @@
  *   - NewDynamicScheduler            pkg/plugins/dynamic/plugins.go:105-120
  *   - LoadPolicyFromFile/loadPolicy  pkg/plugins/dynamic/policyfile.go:11-33
  *   - BindingRecords.GetLastNodeBindingCount  pkg/controller/annotator/binding.go:81-97
+ *   - BindingRecords.AddBinding / BindingsGC    binding.go:69-78, 100-123
+ *   - translateEventToBinding        pkg/controller/annotator/event.go:118-145
  *   - annotateNodeHotValue           pkg/controller/annotator/node.go:113-121
  *   - upstream selectHost (argmax; lowest node index wins ties — declared
  *     deviation from upstream's random tie-break)
@@ -18,7 +20,9 @@
  * Conventions: every function returns 0 on success and a negative CRANE_E_*
  * code on failure; crane_dyn_last_error() then describes it.  Callers own all
  * host arrays; the engine copies them during the call and keeps no pointer.
- * Calls on one engine are serialised by an internal mutex.
+ * Calls on one engine are serialised by an internal mutex.  Nothing in the
+ * engine reads the environment; crane_dyn_set_option (tests / A-B tools only)
+ * selects alternative kernel forms of the same results.
  */
 #ifndef CRANE_DYN_H
 #define CRANE_DYN_H
@@ -116,8 +120,24 @@ int crane_dyn_upload_nodes(crane_dyn *h, int64_t n_nodes, int64_t node_offset,
 
 /* Upload the binding records (BindingRecords heap content, binding.go:14-19):
  * node = LOCAL node index of the shard (<0 or >= n_nodes: matches no node),
- * ts_s = Binding.Timestamp (Unix seconds). */
+ * ts_s = Binding.Timestamp (Unix seconds).  Replaces the whole log (and ends
+ * the heap mode below). */
 int crane_dyn_upload_bindings(crane_dyn *h, int64_t n, const int32_t *node, const int64_t *ts_s);
+
+/* Heap mode: the engine keeps BindingRecords itself (binding.go:50-123) and the
+ * controller feeds it binding by binding.
+ *   crane_dyn_binding_records = NewBindingRecords(size, gcTimeRange)
+ *     (controller.go:57: size = --binding-heap-size, gcTimeRange = the largest
+ *     hotValue timeRange); clears the log.  size must be in [1, 2^31).
+ *   crane_dyn_add_bindings    = n x AddBinding in order (a full heap pops its
+ *     minimum Timestamp first, binding.go:69-78); only the changed log slots
+ *     are copied to the device.
+ *   crane_dyn_gc_bindings     = BindingsGC at now_ns (binding.go:100-123).
+ *   crane_dyn_binding_count   = the heap's Len() (the log length outside heap mode). */
+int crane_dyn_binding_records(crane_dyn *h, int64_t size, int64_t gc_time_range_ns);
+int crane_dyn_add_bindings(crane_dyn *h, int64_t n, const int32_t *node, const int64_t *ts_s);
+int crane_dyn_gc_bindings(crane_dyn *h, int64_t now_ns);
+int64_t crane_dyn_binding_count(const crane_dyn *h);
 
 /* Recompute every node's hot value from the uploaded bindings as the
  * controller does at `now_ns` (binding.go:81-97, node.go:113-121) and use it
@@ -142,6 +162,15 @@ int crane_dyn_hot_values(crane_dyn *h, int64_t n, double *hv_out);
  *   chosen_score[p]    : that node's score (-1 when none). */
 int crane_dyn_eval(crane_dyn *h, int64_t n_pods, const int64_t *now_ns, const uint8_t *pod_flags,
                    int8_t *first_fail, int64_t *score, int64_t *chosen, int64_t *chosen_score);
+/* The same with the score matrix as int8 (scores lie in [0,100]): 2 bytes per
+ * (pod, node) instead of 9 cross PCIe — the form the plugin shim uses per pod. */
+int crane_dyn_eval_compact(crane_dyn *h, int64_t n_pods, const int64_t *now_ns, const uint8_t *pod_flags,
+                           int8_t *first_fail, int8_t *score, int64_t *chosen, int64_t *chosen_score);
+/* Device-resident matrix form, asynchronous on `stream`: d_first_fail[p*ld + i]
+ * and d_score[p*ld + i] (int8) as crane_dyn_eval, any may be NULL; d_keys (NULL
+ * = none) as crane_dyn_eval_keys_async. */
+int crane_dyn_eval_matrix_async(crane_dyn *h, int64_t n_pods, const int64_t *d_now_ns, const uint8_t *d_pod_flags,
+                                int8_t *d_first_fail, int8_t *d_score, int64_t ld, int64_t *d_keys, void *stream);
 
 /* Device-resident variant for batched pipelines: all pointers are device
  * pointers, work is enqueued on `stream` (hipStream_t; NULL = engine stream)
@@ -153,9 +182,7 @@ int crane_dyn_eval_keys_async(crane_dyn *h, int64_t n_pods, const int64_t *d_now
                               const uint8_t *d_pod_flags, int64_t *d_keys, void *stream);
 /* One scheduling step, asynchronous on `stream`: hot values from the bindings
  * at now_ns (as crane_dyn_refresh_hot_values_async) then the keys-only
- * evaluation of the pod batch (as crane_dyn_eval_keys_async).  With
- * CRANE_STEP_OVERLAP=1 the pod-only work runs on an engine-internal second
- * queue while the hot values are counted. */
+ * evaluation of the pod batch (as crane_dyn_eval_keys_async). */
 int crane_dyn_step_keys_async(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns, int64_t n_pods,
                               const int64_t *d_now_ns, const uint8_t *d_pod_flags, int64_t *d_keys, void *stream);
 /* Asynchronous pieces of one scheduling step on `stream`:
@@ -163,11 +190,12 @@ int crane_dyn_step_keys_async(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns, in
 int crane_dyn_refresh_hot_values_async(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns, void *stream);
 int crane_dyn_node_pass_async(crane_dyn *h, void *stream);
 
-/* Stage timing for benchmarks and profiling: while enabled, the engine records
- * a HIP event on the work stream after each kernel stage it enqueues (and one
- * before the first).  crane_dyn_stage_times() waits for the recorded events,
- * writes up to `max` (name, milliseconds) pairs in enqueue order, returns the
- * number of stages and clears the list.  Enabling also clears it. */
+/* Kernel timing for benchmarks and profiling: while enabled, every kernel the
+ * engine launches carries a start/stop event pair stamped by the dispatch
+ * itself (hipExtLaunchKernel), i.e. the kernel's own duration as rocprofv3
+ * reports it.  crane_dyn_stage_times() waits for them, writes up to `max`
+ * (kernel name, milliseconds) pairs in launch order, returns the number of
+ * kernels and clears the list.  Enabling also clears it. */
 int crane_dyn_set_profiling(crane_dyn *h, int on);
 int crane_dyn_stage_times(crane_dyn *h, int32_t max, const char **names, double *ms);
 
@@ -183,6 +211,25 @@ int64_t crane_dyn_key_node(int64_t key, int64_t *score);
 
 /* Build/version info string (static storage). */
 const char *crane_dyn_version(void);
+
+/* Alternative kernel forms of the same results, for tests and A/B tools:
+ *   "k2_form" 0 dedupe (default) | 1 binned | 2 hash   "k1_threads" 256 | 128
+ *   "k1_keep_records" 0 | 1   "k1_fuse_steps" 1 | 0   "k3p_in_k2" 1 | 0
+ *   "keys_path" 0 step path | 1 per-pair kernel   "greedy_form" 0 merge | 1 sequential */
+int crane_dyn_set_option(crane_dyn *h, const char *name, int64_t value);
+
+/* ------------------------------------------------------------------ events
+ * translateEventToBinding (event.go:118-145): a Scheduled event's message
+ * "Successfully assigned <namespace>/<pod> to <node>" (fmt.Fscanf with two %s)
+ * and its timestamps -> the Binding the controller records.  Timestamp =
+ * EventTime.Unix() when count == 0, else LastTimestamp.Unix() (times in Unix
+ * ns here).  On success *node / *node_len point into msg, and likewise the
+ * namespace ("" for a key without '/') and pod name.  Returns CRANE_E_PARSE
+ * for a message that does not scan or a key with more than one '/'
+ * (cache.SplitMetaNamespaceKey). */
+int crane_translate_event(const char *msg, size_t n, int32_t count, int64_t event_time_ns, int64_t last_timestamp_ns,
+                          const char **node, size_t *node_len, const char **ns, size_t *ns_len, const char **pod,
+                          size_t *pod_len, int64_t *ts_s);
 
 #ifdef __cplusplus
 }

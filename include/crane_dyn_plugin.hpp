@@ -12,8 +12,15 @@
 //   IsDaemonsetPod                                    pkg/utils/utils.go:17-24
 // The k8s framework types are reduced to what the plugin touches.  Instead of
 // re-parsing annotations per call (stats.go:51-76), the plugin parses a node
-// snapshot once (Sync) and answers a pod's Filter/Score calls from one engine
-// evaluation of that pod against every node, cached per scheduling cycle.
+// snapshot once per generation (Sync: one bulk, threaded crane_parse_annotations
+// call) and answers a pod's Filter/Score calls from one engine evaluation of
+// that pod against every node (crane_dyn_eval_compact: int8 first-fail and
+// score rows), made once per scheduling cycle and kept in the CycleState.
+//
+// Threading: the framework calls Filter/Score for one pod from 16 goroutines.
+// The first call of a cycle computes the cycle's row under std::call_once; every
+// call after that reads the immutable row (and the immutable name -> index map
+// of the snapshot generation it was computed against) without taking a lock.
 #pragma once
 
 #include <chrono>
@@ -24,6 +31,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <typeinfo>
 #include <unordered_map>
 #include <utility>
@@ -81,10 +89,35 @@ class NodeInfo {
 
 // One scheduling cycle of one pod (framework.CycleState).  time.Now() for the
 // whole cycle (the reference calls it per Filter/Score call; declared deviation).
+// The Dynamic plugin's per-cycle row lives here (as plugins keep cycle data in
+// the framework's CycleState); Clone() (preemption dry runs) shares it.
 struct CycleState {
     int64_t now_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
                          std::chrono::system_clock::now().time_since_epoch())
                          .count();
+    CycleState() = default;
+    CycleState(const CycleState&) = delete;
+    CycleState& operator=(const CycleState&) = delete;
+    std::unique_ptr<CycleState> Clone() const {
+        std::unique_ptr<CycleState> c(new CycleState());
+        c->now_ns = now_ns;
+        std::lock_guard<std::mutex> g(clone_mu_);
+        if (dyn_done_) {
+            c->dyn_row_ = dyn_row_;
+            c->dyn_err_ = dyn_err_;
+            std::call_once(c->dyn_once_, [] {});
+            c->dyn_done_ = true;
+        }
+        return c;
+    }
+
+   private:
+    friend class DynamicScheduler;
+    mutable std::once_flag dyn_once_;
+    mutable std::mutex clone_mu_;
+    bool dyn_done_ = false;
+    std::shared_ptr<const void> dyn_row_;
+    std::string dyn_err_;
 };
 
 // The handle's snapshot lister (SnapshotSharedLister().NodeInfos()).
@@ -158,103 +191,134 @@ class DynamicScheduler {
         const Row* row;
         int64_t idx;
         if (!row_for(state, pod, node->Name, &row, &idx, &err)) return {0, NewStatus(Code::Error, err)};
-        return {row->score[(size_t)idx], Status()};
+        return {(int64_t)row->score[(size_t)idx], Status()};
     }
 
     // Re-parse the snapshot's annotations into the engine (once per generation).
     bool Sync(std::string* err) {
         std::lock_guard<std::mutex> g(mu_);
-        return sync_locked(err);
+        return sync_locked(err) != nullptr;
     }
+
+    // host threads of the once-per-sync annotation parse (<= 0: all hardware threads)
+    void SetParseThreads(int32_t n) { parse_threads_ = n; }
 
     friend std::pair<std::unique_ptr<DynamicScheduler>, std::string> NewDynamicScheduler(const Object& plArgs,
                                                                                          const Handle& h);
 
    private:
+    // one synced snapshot generation: node name -> engine index (immutable once published)
+    struct Synced {
+        uint64_t generation;
+        std::unordered_map<std::string, int64_t> index;
+    };
+    // one cycle's answers for every node of `snap` (immutable once published)
     struct Row {
-        const CycleState* cycle;
+        std::shared_ptr<const Synced> snap;
         std::vector<int8_t> first_fail;
-        std::vector<int64_t> score;
+        std::vector<int8_t> score;
     };
 
     DynamicScheduler() = default;
 
-    bool sync_locked(std::string* err) {
+    std::shared_ptr<const Synced> sync_locked(std::string* err) {
         if (!handle_.snapshot) {
             *err = "no snapshot";
-            return false;
+            return nullptr;
         }
         const uint64_t gen = handle_.snapshot->Generation();
-        if (synced_ && gen == generation_) return true;
+        if (synced_ && synced_->generation == gen) return synced_;
         const auto nodes = handle_.snapshot->List();
         const int32_t M = crane_dyn_num_metrics(eng_);
         const size_t N = nodes.size();
-        std::vector<double> val((size_t)M * N, 0.0), hv(N, 0.0);
-        std::vector<int64_t> ts((size_t)M * N, CRANE_TS_INVALID), hv_ts(N, CRANE_TS_INVALID);
-        index_.clear();
+        auto snap = std::make_shared<Synced>();
+        snap->generation = gen;
+        snap->index.reserve(N);
+        // rows [metric slot 0..M-1, node_hot_value] x N of annotation strings (NULL = key missing)
+        std::vector<const char*> strs((size_t)(M + 1) * N, nullptr);
+        std::vector<size_t> lens((size_t)(M + 1) * N, 0);
+        std::vector<std::string> keys;
+        for (int32_t m = 0; m < M; ++m) keys.emplace_back(crane_dyn_metric_name(eng_, m));
+        keys.emplace_back(NodeHotValue);
         for (size_t n = 0; n < N; ++n) {
-            index_[nodes[n]->Name] = (int64_t)n;
+            snap->index.emplace(nodes[n]->Name, (int64_t)n);
             const auto& a = nodes[n]->Annotations;
-            for (int32_t m = 0; m < M; ++m) {
-                auto it = a.find(crane_dyn_metric_name(eng_, m));
-                if (it != a.end())
-                    crane_parse_annotation(it->second.data(), it->second.size(), tz_, &val[(size_t)m * N + n],
-                                           &ts[(size_t)m * N + n]);
+            for (int32_t m = 0; m <= M; ++m) {
+                auto it = a.find(keys[(size_t)m]);
+                if (it == a.end()) continue;
+                strs[(size_t)m * N + n] = it->second.data();
+                lens[(size_t)m * N + n] = it->second.size();
             }
-            auto it = a.find(NodeHotValue);
-            if (it != a.end()) crane_parse_annotation(it->second.data(), it->second.size(), tz_, &hv[n], &hv_ts[n]);
         }
-        if (crane_dyn_upload_nodes(eng_, (int64_t)N, 0, val.data(), ts.data(), hv.data(), hv_ts.data())) {
+        std::vector<double> val((size_t)(M + 1) * N);
+        std::vector<int64_t> ts((size_t)(M + 1) * N);
+        if (crane_parse_annotations((int64_t)strs.size(), strs.data(), lens.data(), tz_, val.data(), ts.data(),
+                                    parse_threads_)) {
+            *err = "annotation parse failed";
+            return nullptr;
+        }
+        const double* hv = val.data() + (size_t)M * N;
+        const int64_t* hv_ts = ts.data() + (size_t)M * N;
+        if (crane_dyn_upload_nodes(eng_, (int64_t)N, 0, val.data(), ts.data(), hv, hv_ts)) {
             *err = crane_dyn_last_error(eng_);
-            return false;
+            return nullptr;
         }
-        generation_ = gen;
-        synced_ = true;
-        rows_.clear();
-        return true;
+        synced_ = std::move(snap);
+        return synced_;
     }
 
+    // The cycle's row (computed by the first caller of the cycle), and the node's index in it.
     bool row_for(CycleState& state, const Pod& pod, const std::string& node_name, const Row** row, int64_t* idx,
                  std::string* err) {
-        std::lock_guard<std::mutex> g(mu_);
-        if (!sync_locked(err)) return false;
-        auto ni = index_.find(node_name);
-        if (ni == index_.end()) {
+        std::call_once(state.dyn_once_, [&] {
+            std::string e;
+            std::shared_ptr<Row> r = compute_row(state.now_ns, pod, &e);
+            std::lock_guard<std::mutex> g(state.clone_mu_);
+            state.dyn_row_ = r;
+            state.dyn_err_ = e;
+            state.dyn_done_ = true;
+        });
+        const Row* r = static_cast<const Row*>(state.dyn_row_.get());
+        if (!r) {
+            *err = state.dyn_err_;
+            return false;
+        }
+        auto ni = r->snap->index.find(node_name);
+        if (ni == r->snap->index.end()) {
             *err = "node \"" + node_name + "\" not in the synced snapshot";
             return false;
         }
-        const std::string key = pod.UID.empty() ? pod.Namespace + "/" + pod.Name : pod.UID;
-        auto it = rows_.find(key);
-        if (it == rows_.end() || it->second.cycle != &state) {
-            Row r;
-            r.cycle = &state;
-            const size_t N = index_.size();
-            r.first_fail.assign(N, -1);
-            r.score.assign(N, 0);
-            const uint8_t flag = IsDaemonsetPod(pod) ? CRANE_POD_DAEMONSET : 0;
-            int64_t chosen, chosen_score;
-            if (crane_dyn_eval(eng_, 1, &state.now_ns, &flag, r.first_fail.data(), r.score.data(), &chosen,
-                               &chosen_score)) {
-                *err = crane_dyn_last_error(eng_);
-                return false;
-            }
-            if (rows_.size() > 4096) rows_.clear();
-            it = rows_.insert_or_assign(key, std::move(r)).first;
-        }
-        *row = &it->second;
+        *row = r;
         *idx = ni->second;
         return true;
+    }
+
+    std::shared_ptr<Row> compute_row(int64_t now_ns, const Pod& pod, std::string* err) {
+        std::lock_guard<std::mutex> g(mu_);  // one engine: the sync and the evaluation are serial
+        std::shared_ptr<const Synced> snap = sync_locked(err);
+        if (!snap) return nullptr;
+        auto r = std::make_shared<Row>();
+        r->snap = snap;
+        const size_t N = snap->index.size();
+        r->first_fail.assign(N, -1);
+        r->score.assign(N, 0);
+        const uint8_t flag = IsDaemonsetPod(pod) ? CRANE_POD_DAEMONSET : 0;
+        int64_t chosen, chosen_score;
+        if (crane_dyn_eval_compact(eng_, 1, &now_ns, &flag, r->first_fail.data(), r->score.data(), &chosen,
+                                   &chosen_score)) {
+            *err = crane_dyn_last_error(eng_);
+            return nullptr;
+        }
+        return r;
     }
 
     Handle handle_;
     crane_policy_doc* doc_ = nullptr;
     crane_dyn* eng_ = nullptr;
     int64_t tz_ = 8 * 3600;
+    int32_t parse_threads_ = 16;  // the framework's parallelism (upstream default)
     std::mutex mu_;
-    bool synced_ = false;
-    uint64_t generation_ = 0;
-    std::unordered_map<std::string, int64_t> index_;
-    std::unordered_map<std::string, Row> rows_;
+    std::shared_ptr<const Synced> synced_;
 };
 
 // NewDynamicScheduler (plugins.go:105-120): the same error strings.

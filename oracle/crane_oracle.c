@@ -616,3 +616,88 @@ int or_greedy(const or_policy *pol, int32_t K, const char *const *key_names,
     free(cnt); free(hvi); free(hv_ok); free(hv); free(hv_ts); free(pr); free(qr); free(feas); free(sc);
     return 0;
 }
+
+/* ------------------------------------------------------------------ */
+/* BindingRecords (pkg/controller/annotator/binding.go:50-123) over go1.17
+ * container/heap (src/container/heap/heap.go): Push = append + up(n-1),
+ * Pop = Swap(0, n-1) + down(0, n-1) + remove last; Less = Timestamp <.
+ * ops[i] = 0: AddBinding{node[i], Timestamp arg[i]} (pops the minimum first
+ * when Len() == size, binding.go:69-78); ops[i] = 1: BindingsGC at
+ * time.Now().UTC().Unix() = arg[i] (binding.go:100-123).  The final heap array
+ * (Go's slice order) goes to out_node/out_ts, its length to *out_len.
+ * Returns -1 for size <= 0 (AddBinding on a 0-size heap pops an empty heap).  */
+typedef struct {
+    int32_t node;
+    int64_t ts;
+} or_binding;
+
+static void bh_swap(or_binding *h, int64_t i, int64_t j) {
+    or_binding t = h[i];
+    h[i] = h[j];
+    h[j] = t;
+}
+static void bh_up(or_binding *h, int64_t j) {
+    for (;;) {
+        int64_t i = (j - 1) / 2; /* parent; Go truncates (-1)/2 to 0 */
+        if (i == j || !(h[j].ts < h[i].ts)) break;
+        bh_swap(h, i, j);
+        j = i;
+    }
+}
+static void bh_down(or_binding *h, int64_t i0, int64_t n) {
+    int64_t i = i0;
+    for (;;) {
+        int64_t j1 = 2 * i + 1;
+        if (j1 >= n || j1 < 0) break;
+        int64_t j = j1;
+        int64_t j2 = j1 + 1;
+        if (j2 < n && h[j2].ts < h[j1].ts) j = j2;
+        if (!(h[j].ts < h[i].ts)) break;
+        bh_swap(h, i, j);
+        i = j;
+    }
+}
+static or_binding bh_pop(or_binding *h, int64_t *len) {
+    int64_t n = *len - 1;
+    bh_swap(h, 0, n);
+    bh_down(h, 0, n);
+    *len = n;
+    return h[n];
+}
+static void bh_push(or_binding *h, int64_t *len, or_binding b) {
+    h[*len] = b;
+    (*len)++;
+    bh_up(h, *len - 1);
+}
+
+int or_binding_heap(int64_t size, int64_t gc_tr_ns, int64_t n_ops, const uint8_t *ops, const int32_t *node,
+                    const int64_t *arg, int64_t *out_len, int32_t *out_node, int64_t *out_ts) {
+    if (size <= 0) return -1;
+    or_binding *h = (or_binding *)malloc(sizeof(or_binding) * (size_t)(size + 1));
+    if (!h) return -2;
+    int64_t len = 0;
+    for (int64_t i = 0; i < n_ops; ++i) {
+        if (ops[i] == 0) {
+            if (len == size) (void)bh_pop(h, &len);
+            or_binding b = {node[i], arg[i]};
+            bh_push(h, &len, b);
+        } else {
+            if (gc_tr_ns == 0) continue;
+            int64_t timeline = arg[i] - or_go_duration_seconds_trunc(gc_tr_ns);
+            while (len > 0) {
+                or_binding b = bh_pop(h, &len);
+                if (b.ts > timeline) {
+                    bh_push(h, &len, b);
+                    break;
+                }
+            }
+        }
+    }
+    *out_len = len;
+    for (int64_t i = 0; i < len; ++i) {
+        out_node[i] = h[i].node;
+        out_ts[i] = h[i].ts;
+    }
+    free(h);
+    return 0;
+}

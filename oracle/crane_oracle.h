@@ -103,6 +103,12 @@ int or_greedy(const or_policy *pol, int32_t K, const char *const *key_names,
               int64_t B, const int32_t *b_node, const int64_t *b_ts,
               int64_t P, int64_t now_ns, const uint8_t *pod_ds, int64_t *chosen);
 
+/* BindingRecords (binding.go:50-123) over go1.17 container/heap: ops[i] = 0
+ * AddBinding{node[i], arg[i]}, 1 BindingsGC at unix time arg[i].  Final heap
+ * slice -> out_*; -1 for size <= 0. */
+int or_binding_heap(int64_t size, int64_t gc_tr_ns, int64_t n_ops, const uint8_t *ops, const int32_t *node,
+                    const int64_t *arg, int64_t *out_len, int32_t *out_node, int64_t *out_ts);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,8 @@ def lib():
         L.or_greedy.argtypes = [P(_Policy), C.c_int32, P(C.c_char_p), C.c_int64, P(C.c_uint8), P(C.c_double),
                                 P(C.c_int64), C.c_int64, P(C.c_int32), P(C.c_int64), C.c_int64, C.c_int64,
                                 P(C.c_uint8), P(C.c_int64)]
+        L.or_binding_heap.argtypes = [C.c_int64, C.c_int64, C.c_int64, P(C.c_uint8), P(C.c_int32), P(C.c_int64),
+                                      P(C.c_int64), P(C.c_int32), P(C.c_int64)]
         _lib = L
     return _lib
 
@@ -206,3 +208,20 @@ def greedy(pol, key_names, ok, val, ts, b_node, b_ts, now_ns, P, ds=None):
     if rc:
         raise ZeroDivisionError("hotValue count is 0")
     return ch
+
+
+def binding_heap(size, gc_tr_ns, ops, node, arg):
+    """BindingRecords restated over container/heap: ops 0 = AddBinding(node, ts=arg),
+    1 = BindingsGC(now_unix=arg).  Returns the final heap (node[], ts[]) in slice order."""
+    ops = np.ascontiguousarray(ops, np.uint8)
+    node = np.ascontiguousarray(node, np.int32)
+    arg = np.ascontiguousarray(arg, np.int64)
+    cap = max(int(size), 1)
+    on = np.empty(cap, np.int32)
+    ot = np.empty(cap, np.int64)
+    n = C.c_int64()
+    rc = lib().or_binding_heap(int(size), int(gc_tr_ns), len(ops), _ptr(ops, C.c_uint8), _ptr(node, C.c_int32),
+                               _ptr(arg, C.c_int64), C.byref(n), _ptr(on, C.c_int32), _ptr(ot, C.c_int64))
+    if rc:
+        raise ValueError("binding heap size must be positive")
+    return on[:n.value].copy(), ot[:n.value].copy()

@@ -8,7 +8,10 @@
 //   pod <uid> <now_ns> <ds>  run Filter + Score of this pod on every node
 //   nilnode <uid> <now_ns>   Filter with NodeInfo(nullptr)
 //   missing <uid> <now_ns> <name>  Score of a node absent from the snapshot
+//   mt <uid> <now_ns> <ds>   as pod, but Filter/Score called from 16 threads at once, half
+//                            of them on a Clone() of the cycle state (preemption dry runs)
 #include <iostream>
+#include <thread>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -19,6 +22,7 @@ using namespace crane::dynamic;
 
 struct Snap : Snapshot {
     std::vector<Node> nodes;
+    // (linear Get: small test snapshots)
     uint64_t gen = 1;
     std::vector<const Node*> List() const override {
         std::vector<const Node*> v;
@@ -76,6 +80,40 @@ int main() {
         } else if (f[0] == "anno") {
             snap.nodes.back().Annotations[f[1]] = f.size() > 2 ? f[2] : "";
             snap.gen++;
+        } else if (f[0] == "mt") {
+            Pod pod;
+            pod.UID = pod.Name = f[1];
+            if (f[3] == "1") pod.OwnerReferences.push_back({"DaemonSet", "ds"});
+            CycleState st;
+            st.now_ns = std::stoll(f[2]);
+            const size_t N = snap.nodes.size();
+            std::vector<Status> fs(N);
+            std::vector<std::pair<int64_t, Status>> ss(N);
+            std::vector<std::thread> th;
+            // threads 8..15 work on a clone taken before the first call (it evaluates the pod
+            // itself); a second clone is taken after the cycle's row exists (it shares it)
+            std::unique_ptr<CycleState> clone = st.Clone();
+            for (int t = 0; t < 16; ++t)
+                th.emplace_back([&, t] {
+                    CycleState* s = t < 8 ? &st : clone.get();
+                    for (size_t i = t; i < N; i += 16) {
+                        fs[i] = ds->Filter(*s, pod, NodeInfo(&snap.nodes[i]));
+                        ss[i] = ds->Score(*s, pod, snap.nodes[i].Name);
+                    }
+                });
+            for (auto& x : th) x.join();
+            for (size_t i = 0; i < N; ++i) {
+                std::cout << "F\t" << pod.UID << "\t" << snap.nodes[i].Name << "\t" << (int)fs[i].code() << "\t"
+                          << fs[i].message() << "\n";
+                std::cout << "S\t" << pod.UID << "\t" << snap.nodes[i].Name << "\t" << ss[i].first << "\t"
+                          << (int)ss[i].second.code() << "\t" << ss[i].second.message() << "\n";
+            }
+            // a clone of the evaluated cycle answers like its parent
+            std::unique_ptr<CycleState> late = st.Clone();
+            for (size_t i = 0; i < N; ++i)
+                if (ds->Filter(*late, pod, NodeInfo(&snap.nodes[i])).code() != fs[i].code() ||
+                    ds->Score(*late, pod, snap.nodes[i].Name).first != ss[i].first)
+                    std::cout << "CLONE_MISMATCH\t" << i << "\n";
         } else if (f[0] == "pod" || f[0] == "nilnode" || f[0] == "missing") {
             Pod pod;
             pod.UID = f[1];

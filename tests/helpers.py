@@ -8,8 +8,10 @@ from oracle import oracle as O
 SH = 8 * 3600
 
 
-def engine_for(spec, cluster=None, device=0):
+def engine_for(spec, cluster=None, device=0, opts=None):
     eng = cd.Engine(cd.Policy(spec), device)
+    for k, v in (opts or {}).items():
+        eng.set_option(k, v)
     if cluster is not None:
         val, ts, _ = cluster.rows(eng.metric_names)
         eng.upload_nodes(val, ts, cluster.hv, cluster.hv_ts)

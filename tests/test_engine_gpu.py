@@ -11,15 +11,11 @@ from helpers import SH, engine_for, oracle_soa
 
 pytestmark = pytest.mark.gpu
 
-# K3 variants (kernels.hip): 0 plain, 1 prefetch, 2 unroll-2, 3 XCD swizzle, 4 swizzle + division-free quotient,
-# 5 step path (step.hip) for keys-only launches (matrix launches use 4)
-VARIANTS = ["0", "1", "2", "3", "4", "5"]
-
-
-@pytest.fixture(params=VARIANTS)
-def k3_variant(request, monkeypatch):
-    monkeypatch.setenv("CRANE_K3_VARIANT", request.param)
-    return request.param
+# keys-only evaluations: 0 = the step path (step.hip), 1 = the per-pair kernel (matrix.hip);
+# matrix outputs always come from the per-pair kernel
+@pytest.fixture(params=[0, 1], ids=["keys_step", "keys_pair"])
+def kp(request):
+    return {"keys_path": request.param}
 
 cd = pytest.importorskip("crane_dyn")
 from crane_dyn import synth  # noqa: E402
@@ -55,25 +51,27 @@ def test_golden_cluster(cluster_small):
 
 
 @pytest.mark.parametrize("n_nodes,n_pods,seed", [(1, 1, 1), (100, 1, 2), (257, 33, 3), (5000, 64, 4), (3000, 700, 5)])
-def test_random_vs_oracle(n_nodes, n_pods, seed, k3_variant):
+def test_random_vs_oracle(n_nodes, n_pods, seed, kp):
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, n_nodes, n_pods, seed=seed, pod_step_ns=1_700_000_000)
-    eng = engine_for(spec, c)
+    eng = engine_for(spec, c, opts=kp)
     ff, sc, ch, cs = eng.eval(c.now, c.ds, matrix=True)
     off, osc, och = oracle_soa(spec, c)
     assert np.array_equal(ff, off)
     assert np.array_equal(sc, osc)
     assert np.array_equal(ch, och)
+    _, _, ch2, cs2 = eng.eval(c.now, c.ds)  # keys only
+    assert np.array_equal(ch2, och) and np.array_equal(cs2, cs)
     # chosen score equals the max feasible score
     for p in range(n_pods):
         feas = (off[p] < 0)
         assert cs[p] == (osc[p][feas].max() if feas.any() else -1)
 
 
-def test_keys_only_matches_matrix(k3_variant):
+def test_keys_only_matches_matrix(kp):
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 20000, 300, seed=11, pod_step_ns=3_000_000_000)
-    eng = engine_for(spec, c)
+    eng = engine_for(spec, c, opts=kp)
     _, _, ch_m, cs_m = eng.eval(c.now, c.ds, matrix=True)
     _, _, ch, cs = eng.eval(c.now, c.ds, matrix=False)
     assert np.array_equal(ch, ch_m) and np.array_equal(cs, cs_m)
@@ -97,7 +95,7 @@ def test_no_hot_value_and_empty_shard():
     assert (ch == -1).all() and (cs == -1).all()
 
 
-def test_policy_variants(k3_variant):
+def test_policy_variants(kp):
     """Non-default policy shapes exercise the 8x8 and 16x16 NodeRec kernels and skipped entries."""
     m = 60 * 10**9
     base = cd.default_policy_spec()
@@ -119,12 +117,13 @@ def test_policy_variants(k3_variant):
     specs.append(s)
     for i, spec in enumerate(specs):
         c = synth.make_cluster(spec, 777, 40, seed=100 + i, pod_step_ns=20_000_000_000)
-        eng = engine_for(spec, c)
+        eng = engine_for(spec, c, opts=kp)
         ff, sc, ch, _ = eng.eval(c.now, c.ds, matrix=True)
         off, osc, och = oracle_soa(spec, c)
         assert np.array_equal(ff, off), i
         assert np.array_equal(sc, osc), i
         assert np.array_equal(ch, och), i
+        assert np.array_equal(eng.eval(c.now, c.ds)[2], och), i
 
 
 def test_hot_values_vs_oracle(kats):
@@ -143,18 +142,17 @@ def test_hot_values_vs_oracle(kats):
     assert sc[0, 0] == 50  # hv = 5 (SURVEY KAT-11)
 
 
-@pytest.mark.parametrize("k2", ["dedupe", "part", "binned", "hash"])
+@pytest.mark.parametrize("k2", [0, 1, 2], ids=["dedupe", "binned", "hash"])
 @pytest.mark.parametrize("n_nodes,n_bind,seed", [(1000, 50_000, 1), (20_000, 300_000, 2), (100, 10, 3),
                                                  (70_000, 2_000_000, 4)])
-def test_hot_values_random(n_nodes, n_bind, seed, k2, monkeypatch):
-    monkeypatch.setenv("CRANE_K2", k2)
+def test_hot_values_random(n_nodes, n_bind, seed, k2):
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, n_nodes, 16, n_bindings=n_bind, seed=seed, pod_step_ns=10_000_000_000)
     # include bindings for nodes outside the shard
     bn = c.b_node.copy()
     bn[::97] = -1
     bn[1::101] = n_nodes + 5
-    eng = engine_for(spec, c)
+    eng = engine_for(spec, c, opts={"k2_form": k2})
     eng.upload_bindings(bn, c.b_ts)
     now = int(c.now[0])
     eng.refresh_hot_values(now, now)
@@ -164,17 +162,15 @@ def test_hot_values_random(n_nodes, n_bind, seed, k2, monkeypatch):
     assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch, och)
 
 
-@pytest.mark.parametrize("threads", ["128", "256"])
+@pytest.mark.parametrize("threads", [128, 256])
 @pytest.mark.parametrize("case", ["one_hot_node", "eight_windows", "last_node", "odd_counts"])
-def test_hot_values_dedupe_edges(case, threads, monkeypatch):
+def test_hot_values_dedupe_edges(case, threads):
     """Dedupe-form K2 (per-workgroup (node, bucket) aggregation, counts read by the
     node pass) at its packing limits: a region whose 2048 bindings all hit one node
     (count field), eight windows (bucket field), the shard's last node and bindings
     past the shard; 128- and 256-node bins.  odd_counts: hotValue.count negative
     and past 32 bits (the node pass divides in u32 only when both operands fit;
     Go's int64 division truncates toward zero otherwise, node.go:117)."""
-    monkeypatch.setenv("CRANE_K2", "dedupe")
-    monkeypatch.setenv("CRANE_K1_THREADS", threads)
     m = 60 * 10**9
     spec = cd.default_policy_spec()
     n_nodes, n_bind = 5000, 200_000
@@ -191,7 +187,7 @@ def test_hot_values_dedupe_edges(case, threads, monkeypatch):
         bn[::3] = n_nodes - 1
         bn[1::7] = n_nodes  # past the shard: ignored
         bn[2::11] = -3
-    eng = engine_for(spec, c)
+    eng = engine_for(spec, c, opts={"k2_form": 0, "k1_threads": threads})
     eng.upload_bindings(bn, c.b_ts)
     now = int(c.now[0])
     for rep in range(2):  # a second refresh after the first was consumed
@@ -205,7 +201,7 @@ def test_hot_values_dedupe_edges(case, threads, monkeypatch):
     assert np.array_equal(eng.hot_values(), cnt_hv.astype(np.float64))
 
 
-def test_division_exactness_sweep(k3_variant):
+def test_division_exactness_sweep(kp):
     """Dense random usages: int(score/weight) must match the CPU bit for bit (KAT-3/4 FMA traps)."""
     spec = cd.default_policy_spec()
     rng = np.random.default_rng(5)
@@ -216,7 +212,7 @@ def test_division_exactness_sweep(k3_variant):
     c.val = np.select([dec == 1, dec == 2], [np.round(r, 1), np.round(r, 2)], np.round(r, 3))  # 1-3 decimals
     c.ts[:] = synth.NOW0_NS
     c.hv_ts[:] = synth.TS_INVALID
-    eng = engine_for(spec, c)
+    eng = engine_for(spec, c, opts=kp)
     _, sc, _, _ = eng.eval(c.now, c.ds, matrix=True)
     off, osc, och = oracle_soa(spec, c)
     assert np.array_equal(sc, osc)
@@ -224,8 +220,8 @@ def test_division_exactness_sweep(k3_variant):
     assert ch[0] == och[0] and cs[0] == osc[0][(off[0] < 0) | bool(c.ds[0])].max()
 
 
-def test_quotient_threshold_adversarial(k3_variant):
-    """Single-priority policies whose score/weight lands exactly on, and one ulp around, integers."""
+def test_quotient_adversarial(kp):
+    """Two-priority policies whose score/weight lands exactly on, and one ulp around, integers."""
     m = 60 * 10**9
     rng = np.random.default_rng(17)
     for w in (0.3, 1.7, 2.0, 0.1, 3.0):
@@ -244,10 +240,46 @@ def test_quotient_threshold_adversarial(k3_variant):
         c.val[1] = np.abs(rng.choice([0.0, 0.5, 1.0, 1.5], N))
         c.ts[:] = synth.NOW0_NS
         c.hv_ts[:] = synth.TS_INVALID
-        eng = engine_for(spec, c)
+        eng = engine_for(spec, c, opts=kp)
         _, sc, _, _ = eng.eval(c.now, c.ds, matrix=True)
-        _, osc, _ = oracle_soa(spec, c)
+        _, osc, och = oracle_soa(spec, c)
         assert np.array_equal(sc, osc), w
+        assert np.array_equal(eng.eval(c.now, c.ds)[2], och), w
+
+
+def test_config2_full_matrix():
+    """BASELINE config 2 exactly (5,000 nodes x 1,000 pods, default policy, no binding
+    log): the full first-fail and score matrices and every chosen node against the
+    oracle bit for bit, through the host API (int64 and compact int8 scores), the
+    device-resident matrix form, and the keys-only step path."""
+    import torch
+    cfg = synth.CONFIGS[2]
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, cfg["nodes"], cfg["pods"], seed=20250215 + 2)
+    eng = engine_for(spec, c)
+    off, osc, och = oracle_soa(spec, c)
+    ff, sc, ch, cs = eng.eval(c.now, c.ds, matrix=True)
+    assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch, och)
+    ff8, sc8, ch8, cs8 = eng.eval(c.now, c.ds, matrix=True, compact=True)
+    assert np.array_equal(ff8, off) and np.array_equal(sc8.astype(np.int64), osc)
+    assert np.array_equal(ch8, och) and np.array_equal(cs8, cs)
+    _, _, chk, csk = eng.eval(c.now, c.ds)  # keys-only: the step path
+    assert np.array_equal(chk, och) and np.array_equal(csk, cs)
+    dev = torch.device("cuda", 0)
+    P, N = cfg["pods"], cfg["nodes"]
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    ld = N + 64  # padded rows
+    d_ff = torch.full((P, ld), 77, dtype=torch.int8, device=dev)
+    d_sc = torch.full((P, ld), 77, dtype=torch.int8, device=dev)
+    d_keys = torch.empty(P, dtype=torch.int64, device=dev)
+    eng.eval_matrix_async(d_now, d_flags, d_ff, d_sc, d_keys, ld=ld)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_ff[:, :N].cpu().numpy(), off) and np.array_equal(d_sc[:, :N].cpu().numpy(), osc)
+    assert (d_ff[:, N:] == 77).all() and (d_sc[:, N:] == 77).all()  # padding untouched
+    from crane_dyn.shard import unpack_keys
+    node, score = unpack_keys(d_keys.cpu().numpy())
+    assert np.array_equal(node, och) and np.array_equal(score, cs)
 
 
 @pytest.mark.slow

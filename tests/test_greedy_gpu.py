@@ -15,11 +15,19 @@ from helpers import engine_for  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 
+_OPTS = {}
+
+
 @pytest.fixture(autouse=True, params=["merge", "seq"])
-def greedy_mode(request, monkeypatch):
+def greedy_mode(request):
     """merge: merge.hip (default); seq: the one-workgroup sequential kernel (greedy.hip)."""
-    monkeypatch.setenv("CRANE_GREEDY", request.param)
-    return request.param
+    _OPTS["greedy_form"] = 0 if request.param == "merge" else 1
+    yield request.param
+    _OPTS.clear()
+
+
+def _engine(spec, c=None):
+    return engine_for(spec, c, opts=_OPTS)
 
 
 def _oracle(spec, c, P, now):
@@ -33,7 +41,7 @@ def test_greedy_vs_oracle(N, P, B, seed):
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, N, P, n_bindings=B, seed=seed, ds_frac=0.05)
     now = int(synth.NOW0_NS) + 1234567
-    eng = engine_for(spec, c)
+    eng = _engine(spec, c)
     eng.upload_bindings(c.b_node, c.b_ts)
     ch = eng.greedy(P, now, c.ds)
     och = _oracle(spec, c, P, now)
@@ -46,7 +54,7 @@ def test_greedy_global_leaves():
     N, P = 200_000, 3000
     c = synth.make_cluster(spec, N, P, n_bindings=100_000, seed=9)
     now = int(synth.NOW0_NS)
-    eng = engine_for(spec, c)
+    eng = _engine(spec, c)
     eng.upload_bindings(c.b_node, c.b_ts)
     ch = eng.greedy(P, now, c.ds)
     assert np.array_equal(ch, _oracle(spec, c, P, now))
@@ -59,7 +67,7 @@ def test_greedy_edge_policies():
     for i, spec in enumerate(specs):
         c = synth.make_cluster(spec, 300, 400, n_bindings=5000, seed=40 + i)
         now = int(synth.NOW0_NS)
-        eng = engine_for(spec, c)
+        eng = _engine(spec, c)
         eng.upload_bindings(c.b_node, c.b_ts)
         ch = eng.greedy(400, now, c.ds)
         assert np.array_equal(ch, _oracle(spec, c, 400, now)), i
@@ -69,7 +77,7 @@ def test_greedy_then_eval_consistent():
     """greedy leaves the engine usable: a later eval recomputes node records."""
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 500, 50, n_bindings=3000, seed=8)
-    eng = engine_for(spec, c)
+    eng = _engine(spec, c)
     eng.upload_bindings(c.b_node, c.b_ts)
     eng.greedy(50, int(c.now[0]), c.ds)
     eng.upload_nodes(*c.rows(eng.metric_names)[:2], c.hv, c.hv_ts)
@@ -87,7 +95,7 @@ def test_greedy_daemonset_mixes(ds_frac, feas_all):
     N, P = 3000, 4000
     c = synth.make_cluster(spec, N, P, n_bindings=30000, seed=61, ds_frac=ds_frac)
     now = int(synth.NOW0_NS)
-    eng = engine_for(spec, c)
+    eng = _engine(spec, c)
     eng.upload_bindings(c.b_node, c.b_ts)
     assert np.array_equal(eng.greedy(P, now, c.ds), _oracle(spec, c, P, now))
 
@@ -99,7 +107,7 @@ def test_greedy_no_feasible_node():
     c = synth.make_cluster(spec, N, P, n_bindings=2000, seed=62, ds_frac=0.2, invalid=False)
     c.ts[:] = synth.NOW0_NS  # all fresh, so every node is over the tiny limit
     now = int(synth.NOW0_NS)
-    eng = engine_for(spec, c)
+    eng = _engine(spec, c)
     eng.upload_bindings(c.b_node, c.b_ts)
     ch = eng.greedy(P, now, c.ds)
     assert np.array_equal(ch, _oracle(spec, c, P, now))
@@ -112,7 +120,7 @@ def test_greedy_many_pods_per_node():
     N, P = 37, 3000
     c = synth.make_cluster(spec, N, P, n_bindings=500, seed=63, ds_frac=0.05)
     now = int(synth.NOW0_NS)
-    eng = engine_for(spec, c)
+    eng = _engine(spec, c)
     eng.upload_bindings(c.b_node, c.b_ts)
     assert np.array_equal(eng.greedy(P, now, c.ds), _oracle(spec, c, P, now))
 
@@ -125,23 +133,23 @@ def test_greedy_windows_shapes():
         spec = dict(base, hotValue=hot)
         c = synth.make_cluster(spec, 800, 1500, n_bindings=20000, seed=70 + i, ds_frac=0.05)
         now = int(synth.NOW0_NS)
-        eng = engine_for(spec, c)
+        eng = _engine(spec, c)
         eng.upload_bindings(c.b_node, c.b_ts)
         assert np.array_equal(eng.greedy(1500, now, c.ds), _oracle(spec, c, 1500, now)), i
 
 
 @pytest.mark.slow
-def test_greedy_config5_merge_equals_sequential(greedy_mode, monkeypatch):
+def test_greedy_config5_merge_equals_sequential(greedy_mode):
     """BASELINE config 5 size (100k nodes x 50k pods): merge form == sequential kernel, bit for bit."""
     if greedy_mode != "merge":
         pytest.skip("compares both modes itself")
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 100_000, 50_000, n_bindings=1_000_000, seed=20255215)
     now = int(synth.NOW0_NS)
-    eng = engine_for(spec, c)
+    eng = _engine(spec, c)
     eng.upload_bindings(c.b_node, c.b_ts)
     a = eng.greedy(50_000, now, c.ds)
-    monkeypatch.setenv("CRANE_GREEDY", "seq")
+    eng.set_option("greedy_form", 1)
     b = eng.greedy(50_000, now, c.ds)
     assert np.array_equal(a, b)
     assert (a >= 0).all()

@@ -18,7 +18,7 @@ def driver(tmp_path_factory):
     if not os.path.exists(os.path.join(LIB_DIR, "libcrane_dyn.so")):
         pytest.skip("libcrane_dyn.so not built")
     exe = str(tmp_path_factory.mktemp("drv") / "plugin_driver")
-    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(ROOT, "include"),
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-pthread", "-I", os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tests", "cpp", "plugin_driver.cpp"), "-L", LIB_DIR, "-lcrane_dyn",
                     "-Wl,-rpath," + LIB_DIR, "-o", exe], check=True)
     return exe
@@ -91,3 +91,28 @@ def test_golden_cluster_through_plugin(driver, cluster_small, tmp_path):
             assert s[3] == str(c["expect_score"][p][n])
     assert F[-1][3:] == [str(ERROR), "node not found"]
     assert S[-1][3:5] == ["0", str(ERROR)] and S[-1][5].startswith('getting node "ghost" from Snapshot: ')
+
+
+@pytest.mark.gpu
+def test_concurrent_filter_score_and_clones(driver, cluster_small, tmp_path):
+    """16 threads call Filter/Score of one pod at once (the framework's parallelism), one of
+    them on a Clone() of the cycle state: the same answers as the serial calls, one engine
+    evaluation per cycle, and the clone answers like its parent."""
+    c = cluster_small
+    pol = policy_from_json(c["policy"])
+    lines = [f"policy\t{write_policy(tmp_path, pol)}"]
+    for i, a in enumerate(c["nodes"]):
+        lines.append(f"node\tnode-{i}")
+        lines += [f"anno\t{k}\t{v}" for k, v in a.items()]
+    for p, pod in enumerate(c["pods"][:6]):
+        lines.append(f"pod\tp{p}\t{pod['now_ns']}\t{int(pod['daemonset'])}")
+        lines.append(f"mt\tp{p}\t{pod['now_ns']}\t{int(pod['daemonset'])}")
+    out = run(driver, "\n".join(lines) + "\n")
+    assert not [o for o in out if o[0] == "CLONE_MISMATCH"]
+    N = len(c["nodes"])
+    body = [o for o in out if o[0] in ("F", "S")]
+    for p in range(6):
+        serial = body[(2 * p) * 2 * N:(2 * p + 1) * 2 * N]
+        threaded = body[(2 * p + 1) * 2 * N:(2 * p + 2) * 2 * N]
+        key = lambda r: (r[0], r[2])  # noqa: E731
+        assert sorted(serial, key=key) == sorted(threaded, key=key), p

@@ -1,0 +1,103 @@
+"""Node sharding through real engines: S engines on one GPU, each holding a
+contiguous node range (node_offset) and only its own nodes' bindings, combined
+by a host max over their packed keys (the RCCL MAX all-reduce's operation),
+equal the unsharded engine and the oracle — with forced equal-score ties across
+shard boundaries, whose winner must be the lowest GLOBAL index (key packing
+(score << 32) | (0xFFFFFFFF - global node), step.hip / matrix.hip).
+Reference: plugins.go:39-98 + upstream selectHost; binding.go:81-97."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+cd = pytest.importorskip("crane_dyn")
+from crane_dyn import shard, synth  # noqa: E402
+from helpers import oracle_soa  # noqa: E402
+
+
+def _tied_cluster(n_nodes, n_pods, seed, n_bind):
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, n_nodes, n_pods, n_bindings=n_bind, seed=seed, pod_step_ns=3_000_000)
+    # copies of node 3 in later shards: equal metrics, equal hot values
+    for dst in (n_nodes // 2 + 1, n_nodes - 5):
+        c.val[:, dst], c.ts[:, dst], c.ok[:, dst] = c.val[:, 3], c.ts[:, 3], c.ok[:, 3]
+        c.hv[dst], c.hv_ts[dst] = c.hv[3], c.hv_ts[3]
+    # every metric fresh and low on the copies: they are among the best nodes
+    for n in (3, n_nodes // 2 + 1, n_nodes - 5):
+        c.val[:, n], c.ok[:, n], c.ts[:, n] = 0.0, 1, synth.NOW0_NS
+        c.hv[n], c.hv_ts[n] = 0.0, synth.NOW0_NS
+    return spec, c
+
+
+@pytest.mark.parametrize("S,keys_path", [(8, 0), (3, 0), (8, 1)])
+def test_sharded_engines_equal_unsharded(S, keys_path):
+    import torch
+    n_nodes, n_pods = 40_003, 2_500
+    spec, c = _tied_cluster(n_nodes, n_pods, 20260 + S, 0)
+    dev = torch.device("cuda", 0)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    pol = cd.Policy(spec)
+    full = cd.Engine(pol, 0)
+    val, ts, _ = c.rows(full.metric_names)
+    full.upload_nodes(val, ts, c.hv, c.hv_ts)
+    ref = torch.empty(n_pods, dtype=torch.int64, device=dev)
+    full.eval_keys_async(d_now, d_flags, ref)
+    combined = torch.full((n_pods,), -1, dtype=torch.int64, device=dev)
+    for r in range(S):
+        se = shard.ShardedEngine(pol, n_nodes, S, r, 0)
+        se.engine.set_option("keys_path", keys_path)
+        se.upload(val, ts, c.hv, c.hv_ts)
+        k = torch.empty(n_pods, dtype=torch.int64, device=dev)
+        se.eval_keys(d_now, d_flags, k)
+        torch.cuda.synchronize()
+        combined = torch.maximum(combined, k)
+        se.close()
+    torch.cuda.synchronize()
+    assert torch.equal(combined, ref)
+    node, score = shard.unpack_keys(combined.cpu().numpy())
+    _, _, och = oracle_soa(spec, c, want_matrix=False)
+    assert np.array_equal(node, och)
+    assert (node == 3).sum() > 0  # the tie across shards was decided for the lowest global index
+    assert not np.isin(node, [n_nodes // 2 + 1, n_nodes - 5]).any()
+
+
+def test_sharded_step_with_binding_logs():
+    """Each shard counts only its own nodes' bindings (re-indexed locally, ShardedEngine.upload):
+    the combined step_keys equals the unsharded step and the oracle with binding-log hot values."""
+    import torch
+    from oracle import oracle as O
+    n_nodes, n_pods, S = 30_011, 3_000, 8
+    spec, c = _tied_cluster(n_nodes, n_pods, 777, 300_000)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    pol = cd.Policy(spec)
+    now = int(synth.NOW0_NS)
+    full = cd.Engine(pol, 0)
+    val, ts, _ = c.rows(full.metric_names)
+    full.upload_nodes(val, ts, c.hv, c.hv_ts)
+    full.upload_bindings(c.b_node, c.b_ts)
+    ref = torch.empty(n_pods, dtype=torch.int64, device=dev)
+    full.step_keys_async(now, now, d_now, d_flags, ref, st.cuda_stream)
+    combined = torch.full((n_pods,), -1, dtype=torch.int64, device=dev)
+    shards = [shard.ShardedEngine(pol, n_nodes, S, r, 0) for r in range(S)]
+    for se in shards:
+        se.upload(val, ts, c.hv, c.hv_ts, c.b_node, c.b_ts)
+    for rep in range(2):
+        ks = []
+        for se in shards:
+            k = torch.empty(n_pods, dtype=torch.int64, device=dev)
+            se.step_keys(now, now, d_now, d_flags, k, st.cuda_stream)
+            ks.append(k)
+        st.synchronize()
+        combined = torch.stack(ks).max(0).values
+        assert torch.equal(combined, ref), rep
+    _, hv = O.hot_values(spec, c.b_node, c.b_ts, n_nodes, now // 10**9)
+    _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=(hv.astype(np.float64),
+                                                                   np.full(n_nodes, now, np.int64)))
+    node, _ = shard.unpack_keys(combined.cpu().numpy())
+    assert np.array_equal(node, och)
+    for se in shards:
+        se.close()

@@ -20,11 +20,6 @@ cd = pytest.importorskip("crane_dyn")
 from crane_dyn import synth  # noqa: E402
 
 
-@pytest.fixture(autouse=True)
-def _step_variant(monkeypatch):
-    monkeypatch.setenv("CRANE_K3_VARIANT", "5")
-
-
 def _check(spec, c, now, ds):
     eng = engine_for(spec, c)
     _, _, ch, cs = eng.eval(now, ds)
@@ -106,16 +101,14 @@ def test_step_policy_shapes():
         _check(spec, c, c.now, c.ds)
 
 
-def test_step_matches_v4_keys():
-    """Same device-resident keys from the step path and the V4 pair kernel."""
-    import os
+def test_step_matches_pair_keys():
+    """Same keys from the step path and the per-pair kernel (matrix.hip)."""
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 30000, 3000, seed=23, pod_step_ns=5_000_000)
     eng = engine_for(spec, c)
     _, _, ch5, cs5 = eng.eval(c.now, c.ds)
-    os.environ["CRANE_K3_VARIANT"] = "4"
+    eng.set_option("keys_path", 1)
     _, _, ch4, cs4 = eng.eval(c.now, c.ds)
-    os.environ["CRANE_K3_VARIANT"] = "5"
     assert np.array_equal(ch5, ch4) and np.array_equal(cs5, cs4)
 
 
@@ -173,24 +166,21 @@ def test_hot_values_kept_after_consumption():
     eng.refresh_hot_values(now, now)
     _, _, ch1, _ = eng.eval(c.now, c.ds)          # consumes the counts
     eng.greedy(50, now, c.ds[:50])                # refreshes at the same now, leaves records stale
-    ff, sc, ch2, _ = eng.eval(c.now, c.ds, matrix=True)   # K1 again from the kept hot values (V4 path)
+    ff, sc, ch2, _ = eng.eval(c.now, c.ds, matrix=True)   # K1 again from the kept hot values (pair kernel)
     off, osc, och = oracle_soa(spec, c, hv_override=_oracle_hv(spec, c, now))
     assert np.array_equal(ch1, och) and np.array_equal(ch2, och)
     assert np.array_equal(ff, off) and np.array_equal(sc, osc)
 
 
-@pytest.mark.parametrize("overlap,ride,pods", [("0", "1", 5000), ("0", "0", 5000), ("1", "1", 5000),
-                                               ("0", "1", 1), ("0", "1", 300), ("0", "1", 2048)])
-def test_step_keys_async_matches_oracle(overlap, ride, pods, monkeypatch):
-    """crane_dyn_step_keys_async replayed (serial with K3p riding in K2x's launch or in
-    its own, and with K3p on the engine's second queue overlapping K2): each step
-    equals the oracle with binding-log hot values; with stage profiling on too."""
+@pytest.mark.parametrize("ride,pods", [(1, 5000), (0, 5000), (1, 1), (1, 300), (1, 2048)])
+def test_step_keys_async_matches_oracle(ride, pods):
+    """crane_dyn_step_keys_async replayed (K3p riding in K2x's launch or in its own):
+    each step equals the oracle with binding-log hot values; with kernel timing on
+    too (dispatch-stamped events name every kernel of the step)."""
     import torch
-    monkeypatch.setenv("CRANE_STEP_OVERLAP", overlap)
-    monkeypatch.setenv("CRANE_K2X_PODS", ride)
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 30000, pods, n_bindings=300_000, seed=27, pod_step_ns=2_000_000, ds_frac=0.02)
-    eng = engine_for(spec, c)
+    eng = engine_for(spec, c, opts={"k3p_in_k2": ride})
     eng.upload_bindings(c.b_node, c.b_ts)
     now = int(synth.NOW0_NS)
     dev = torch.device("cuda", 0)
@@ -206,22 +196,23 @@ def test_step_keys_async_matches_oracle(overlap, ride, pods, monkeypatch):
             st.synchronize()
             ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
             assert np.array_equal(ch, och), rep
-    names = [n for n, _ in eng.stage_times()]
-    if ride == "1":  # (stage profiling runs the serial path, overlap or not)
+    times = eng.stage_times()
+    names = [n for n, _ in times]
+    if ride:
         assert names == ["k2x_dedupe+k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
     else:
         assert names == ["k2x_dedupe", "k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
+    assert all(0 < t < 50 for _, t in times), times
 
 
-@pytest.mark.parametrize("k2", ["dedupe", "part", "binned"])
-def test_step_keys_async_k2_forms(k2, monkeypatch):
+@pytest.mark.parametrize("k2", [0, 1, 2], ids=["dedupe", "binned", "hash"])
+def test_step_keys_async_k2_forms(k2):
     """The combined step with each K2 form (dedupe: counts consumed by the fused node
-    pass from per-block entries; part / binned: buckets) equals the oracle, replayed."""
+    pass from per-block entries; binned / hash: buckets) equals the oracle, replayed."""
     import torch
-    monkeypatch.setenv("CRANE_K2", k2)
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 20000, 3000, n_bindings=400_000, seed=29, pod_step_ns=2_000_000, ds_frac=0.03)
-    eng = engine_for(spec, c)
+    eng = engine_for(spec, c, opts={"k2_form": k2})
     eng.upload_bindings(c.b_node, c.b_ts)
     now = int(synth.NOW0_NS)
     dev = torch.device("cuda", 0)
@@ -238,16 +229,15 @@ def test_step_keys_async_k2_forms(k2, monkeypatch):
             assert np.array_equal(ch, och), rep
 
 
-@pytest.mark.parametrize("keep", ["0", "1"])
-def test_records_rebuilt_after_keys_step(keep, monkeypatch):
-    """The fused keys-only step does not write the node records (CRANE_K1_KEEP_REC=1
-    does): a matrix eval and a greedy pass after it rebuild them from the kept
-    binding-log hot values and still equal the oracle."""
+@pytest.mark.parametrize("keep", [0, 1])
+def test_records_rebuilt_after_keys_step(keep):
+    """The fused keys-only step does not write the node records (option
+    k1_keep_records does): a matrix eval and a greedy pass after it rebuild them from
+    the kept binding-log hot values and still equal the oracle."""
     import torch
-    monkeypatch.setenv("CRANE_K1_KEEP_REC", keep)
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 4000, 700, n_bindings=50_000, seed=28, pod_step_ns=3_000_000, ds_frac=0.05)
-    eng = engine_for(spec, c)
+    eng = engine_for(spec, c, opts={"k1_keep_records": keep})
     eng.upload_bindings(c.b_node, c.b_ts)
     now = int(synth.NOW0_NS)
     dev = torch.device("cuda", 0)

@@ -1,23 +1,31 @@
-# rocprofv3 PMC passes over a short bench (one counter group per pass, --pmc only,
-# no trace domains; FETCH_SIZE and WRITE_SIZE cannot share a pass).  Stops on any
-# fault/timeout exit code.  Usage: bash tools/gpu_pmc.sh <tag>
+# rocprofv3 PMC passes over short bench runs (one counter group per pass, --pmc
+# only, no trace domains; FETCH_SIZE and WRITE_SIZE cannot share a pass), one
+# summary per workload keyed by the kernel-source hash, so bench.py attaches
+# traffic only to lines measured on the same kernels and config:
+#   profiles/pmc/config3_<hash>.json   headline step, config 3
+#   profiles/pmc/config2_<hash>.json   per-pair matrix leg, config 2
+#   profiles/pmc/config3m_<hash>.json  per-pair matrix leg at config 3 size
+# Stops on any fault/timeout exit code.  Usage: bash tools/gpu_pmc.sh <tag> [workloads]
 cd "$GRAFT_REPO_ROOT"
-TAG=${1:-r01}
-OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_$TAG
-mkdir -p $OUT
+TAG=${1:-pmc}
+WL=${2:-"3 2 3m"}
 export TMPDIR=/tmp
-CMD="python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-greedy"
-run() {  # name counters...
-    local name=$1; shift
-    timeout -s KILL 180 rocprofv3 --pmc "$@" --output-format csv -d $OUT -o $name -- $CMD > $OUT/$name.log 2>&1
-    local rc=$?
-    echo "$name rc=$rc" >> $OUT/status.txt
-    case $rc in 124|134|137|139) exit $rc;; esac
-    return 0
-}
-run fetch FETCH_SIZE
-run write WRITE_SIZE
-run valu SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY
-run l2 TCC_HIT_sum TCC_MISS_sum
-python3 tools/pmc_summary.py $OUT > $OUT/summary.json
+for w in $WL; do
+    OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_${TAG}_$w
+    mkdir -p $OUT
+    case $w in
+        2) CMD="python3 $GRAFT_REPO_ROOT/bench.py --leg matrix2 --steps 5";;
+        3m) CMD="python3 $GRAFT_REPO_ROOT/bench.py --leg matrix3 --steps 3";;
+        *) CMD="python3 $GRAFT_REPO_ROOT/bench.py --config $w --steps 5 --warmup 1 --no-cpu-baseline --no-greedy --no-extras";;
+    esac
+    for pass in "fetch FETCH_SIZE" "write WRITE_SIZE" "valu SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY" "l2 TCC_HIT_sum TCC_MISS_sum"; do
+        set -- $pass
+        name=$1; shift
+        timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d $OUT -o $name -- $CMD > $OUT/$name.log 2>&1
+        rc=$?
+        echo "$w $name rc=$rc" >> $OUT/status.txt
+        case $rc in 124|134|137|139) exit $rc;; esac
+    done
+    python3 tools/pmc_summary.py $OUT --config $w > $OUT/summary.json || exit 1
+done
 exit 0

@@ -2,18 +2,15 @@
 
     python tools/stream_bench.py [--nodes 4000000] [--bindings 16000000] [--pods 10000] [--reps 5]
 
-One step = K2 refresh (k2x_partition + k2y_bin_hist, or the binned / hash
-variants) then a keys-only eval (k3p_pods, k1_node_pass+k3a_steps, k3s_eval).
-Stage times come from the engine's own HIP events (crane_dyn_set_profiling).
-Before the refresh and before the eval a 1 GiB scratch buffer is written, so
-the 256 MiB Infinity Cache holds none of the inputs (MI355X_MICROARCH.md).
+One step = K2 refresh (the binned form at this size, or the hash form) then a
+keys-only eval (k3p_pods, k1_node_pass+k3a_steps, k3s_eval).  Kernel times come
+from the engine's dispatch-stamped events (crane_dyn_set_profiling).  Before
+the refresh and before the eval a 1 GiB scratch buffer is written, so the
+256 MiB Infinity Cache holds none of the inputs (MI355X_MICROARCH.md).
 Algorithmic bytes:
-  k2x_partition           : 12 per binding read + 4 per in-window binding written
-  k2y_bin_hist            : 4 per in-window binding read + 4*W per node (window counts)
+  k2 (all K2 kernels)     : 12 per binding read + 4*W per node (window counts written)
   k1_node_pass+k3a_steps  : 16*M (val+ts SoA) + 8*W (buckets read + zeroed) + 8 (hot value) per node
-                            (+ sizeof(NodeRec) with CRANE_K1_KEEP_REC=1: the keys-only pass keeps them in LDS)
-  k1_node_pass            : the same + sizeof(NodeRec) (CRANE_K1_FUSE=0: records written, then K3a)
-  k3a_steps               : sizeof(NodeRec) read per node
+                            (+ sizeof(NodeRec) with --keep-records: the keys-only pass keeps them in LDS)
 """
 import argparse
 import json
@@ -34,7 +31,8 @@ ap.add_argument("--nodes", type=int, default=4_000_000)
 ap.add_argument("--bindings", type=int, default=16_000_000)
 ap.add_argument("--pods", type=int, default=10_000)
 ap.add_argument("--reps", type=int, default=5)
-ap.add_argument("--k2", default="dedupe,binned,hash")
+ap.add_argument("--k2", default="auto,hash")
+ap.add_argument("--keep-records", action="store_true")
 args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -43,6 +41,7 @@ N, B, P = args.nodes, args.bindings, args.pods
 c = synth.make_cluster(spec, N, P, n_bindings=B, seed=7)
 c.now, c.ds = synth.make_pods(P, seed=8)
 eng = cd.Engine(cd.Policy(spec), 0)
+eng.set_option("k1_keep_records", int(args.keep_records))
 val, ts, _ = c.rows(eng.metric_names)
 eng.upload_nodes(val, ts, c.hv, c.hv_ts)
 eng.upload_bindings(c.b_node, c.b_ts)
@@ -59,18 +58,13 @@ now = int(synth.NOW0_NS)
 max_tr = max(tr for tr, _ in spec["hotValue"]) // 10**9
 b_in = int((c.b_ts > now // 10**9 - max_tr).sum())
 alg = {
-    "k2_binned (4 kernels)": B * 12 + 4 * W * N,
-    "k2_hot_count (hash)": B * 12 + 4 * W * N,
-    "k2x_partition": B * 12 + b_in * 4,
-    "k2y_bin_hist": b_in * 4 + 4 * W * N,
-    "k1_node_pass+k3a_steps": N * (16 * M + 8 * W + 8 + (REC if os.environ.get("CRANE_K1_KEEP_REC") == "1" else 0)),
-    "k1_node_pass": N * (16 * M + 8 * W + REC + 8),
-    "k3a_steps": N * REC,
+    "k2 (all K2 kernels)": B * 12 + 4 * W * N,
+    "k1_node_pass+k3a_steps": N * (16 * M + 8 * W + 8 + (REC if args.keep_records else 0)),
 }
 res = {}
 keys_ref = None
 for k2 in args.k2.split(","):
-    os.environ["CRANE_K2"] = k2
+    eng.set_option("k2_form", {"auto": 0, "binned": 1, "hash": 2}[k2])
     acc = {}
     for r in range(args.reps + 1):
         scratch.fill_(r & 0xFF)
@@ -84,6 +78,7 @@ for k2 in args.k2.split(","):
         if r:  # rep 0 is warmup
             for name, t in t_k2 + t_ev:
                 acc.setdefault(name, []).append(t)
+            acc.setdefault("k2 (all K2 kernels)", []).append(sum(t for _, t in t_k2))
     eng.set_profiling(False)
     keys = d_keys.cpu().numpy()
     if keys_ref is None:
@@ -98,6 +93,6 @@ for k2 in args.k2.split(","):
             e.update({"alg_bytes": alg[name], "GBps": round(gbs, 1), "frac_of_8TBps": round(gbs / 8000, 4)})
         stages[name] = e
     res[k2] = stages
-out = {"env": {k: v for k, v in os.environ.items() if k.startswith("CRANE_") and k != "CRANE_K2"}, "nodes": N, "bindings": B, "bindings_in_window": b_in, "pods": P,
+out = {"keep_records": args.keep_records, "nodes": N, "bindings": B, "bindings_in_window": b_in, "pods": P,
        "cold_cache": "1 GiB scratch write before the refresh and before the eval", "by_k2_mode": res}
 print(json.dumps(out))
