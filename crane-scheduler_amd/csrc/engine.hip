@@ -7,7 +7,7 @@
 //   crane_dyn_eval*       Filter + Score + select  plugins.go:39-98 (+ upstream selectHost)
 //   refresh_hot_values    GetLastNodeBindingCount  pkg/controller/annotator/binding.go:81-97
 //                         annotateNodeHotValue     pkg/controller/annotator/node.go:113-121
-//   binding records       BindingRecords heap      binding.go:50-123 (bindings.cpp)
+//   binding records       BindingRecords heap      binding.go:50-123 (bindings.hpp)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -99,6 +99,8 @@ struct Options {
     bool k3p_in_k2 = true;    // K3p rides as extra workgroups of the K2x launch
     int keys_path = 0;        // 0: step path when it applies, 1: the per-pair kernel (K3m keys)
     int greedy_form = 0;      // 0: merge form when every hotValue count > 0, 1: sequential kernel
+    int matrix_vec = 0;       // K3m nodes per lane: 0 automatic, 1 / 4 / 8 / 16
+    int matrix_chunk = 0;     // K3m pods per workgroup: 0 automatic
 };
 
 }  // namespace
@@ -454,7 +456,6 @@ static int matrix_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const ui
         int rc = node_pass_locked(h, st);
         if (rc) return rc;
     }
-    if (d_keys && P > 0) HIPTRY(h, hipMemsetAsync(d_keys, 0xFF, sizeof(long long) * (size_t)P, st));
     MatrixArgs a{};
     a.rec = h->rec.p;
     a.N = h->N;
@@ -469,7 +470,10 @@ static int matrix_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const ui
     a.score = d_score;
     a.score_i64 = score_i64 ? 1 : 0;
     a.keys = d_keys;
+    a.matrix_vec = h->opt.matrix_vec;
+    a.matrix_chunk = h->opt.matrix_chunk;
     std::memcpy(a.pred_orig, h->pred_orig, sizeof a.pred_orig);
+    if (d_keys && P > 0) HIPTRY(h, hipMemsetAsync(d_keys, 0xFF, sizeof(long long) * (size_t)P, st));
     HIPTRY(h, launch_matrix(h->shape, a, st));
     return CRANE_OK;
 }
@@ -583,6 +587,8 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "k3p_in_k2" && range(0, 1)) o.k3p_in_k2 = value != 0;
     else if (n == "keys_path" && range(0, 1)) o.keys_path = (int)value;
     else if (n == "greedy_form" && range(0, 1)) o.greedy_form = (int)value;
+    else if (n == "matrix_vec" && (value == 0 || value == 1 || value == 4 || value == 8 || value == 16)) o.matrix_vec = (int)value;
+    else if (n == "matrix_chunk" && range(0, 1024)) o.matrix_chunk = (int)value;
     else return h->fail(CRANE_E_INVALID, "unknown option or value: " + n + "=" + std::to_string(value));
     // a pending dedupe-form count is bound to the K1 block size it was binned by
     h->rec_dirty = true;

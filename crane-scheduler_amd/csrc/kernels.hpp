@@ -56,6 +56,8 @@ struct MatrixArgs {
     int32_t score_i64;
     int32_t pad2;
     long long* keys;        // [P] or null: max-combined (atomicMax, keys must be initialised to -1)
+    int32_t matrix_vec;     // 0: automatic geometry; 1 / 4 / 8 nodes per lane (A/B)
+    int32_t matrix_chunk;   // 0: automatic; pods per workgroup (A/B)
     int8_t pred_orig[kMaxPred];  // device predicate -> policy predicate index
 };
 hipError_t launch_matrix(int shape, const MatrixArgs& a, hipStream_t st);
