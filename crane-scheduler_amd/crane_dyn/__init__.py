@@ -69,6 +69,7 @@ def _load():
         "crane_dyn_eval_compact": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, vp]),
         "crane_dyn_eval_matrix_async": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, C.c_int64, vp, vp]),
         "crane_dyn_set_option": (C.c_int, [vp, C.c_char_p, C.c_int64]),
+        "crane_dyn_debug_trace": (C.c_int64, [vp, C.c_int32, C.c_int64, vp]),
         "crane_translate_event": (C.c_int, [C.c_char_p, C.c_size_t, C.c_int32, C.c_int64, C.c_int64, P(C.c_char_p),
                                             P(C.c_size_t), P(C.c_char_p), P(C.c_size_t), P(C.c_char_p),
                                             P(C.c_size_t), P(C.c_int64)]),
@@ -104,7 +105,7 @@ ABI_SYMBOLS = (
     "crane_dyn_set_profiling", "crane_dyn_stage_times", "crane_dyn_hot_values",
     "crane_dyn_version", "crane_dyn_binding_records", "crane_dyn_add_bindings", "crane_dyn_gc_bindings",
     "crane_dyn_binding_count", "crane_dyn_eval_compact", "crane_dyn_eval_matrix_async", "crane_dyn_set_option",
-    "crane_translate_event",
+    "crane_translate_event", "crane_dyn_debug_trace",
 )
 
 
@@ -328,6 +329,14 @@ class Engine:
 
     def gc_bindings(self, now_ns):
         self._check(lib.crane_dyn_gc_bindings(self.h, int(now_ns)))
+
+    def debug_trace(self, which, n_wgs):
+        """Phase stamps [n_wgs][8] (100 MHz) of the last K2x (0) / K1 (1) / K3s (2) launch (option "trace")."""
+        out = np.zeros(n_wgs * 8, np.uint64)
+        n = lib.crane_dyn_debug_trace(self.h, which, len(out), _ptr(out))
+        if n < 0:
+            self._check(n)
+        return out.reshape(n_wgs, 8)
 
     def binding_count(self):
         return lib.crane_dyn_binding_count(self.h)

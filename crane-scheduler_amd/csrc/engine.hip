@@ -101,7 +101,9 @@ struct Options {
     int greedy_form = 0;      // 0: merge form when every hotValue count > 0, 1: sequential kernel
     int matrix_vec = 0;       // K3m nodes per lane: 0 automatic, 1 / 4 / 8 / 16
     int matrix_chunk = 0;     // K3m pods per workgroup: 0 automatic
+    bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
 };
+constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
 
 }  // namespace
 
@@ -165,10 +167,12 @@ struct crane_dyn {
     DevBuf<unsigned long long> mH, mbs;  // merge-form greedy (merge.hip)
     DevBuf<int32_t> mflag, mapos, mtk;
     DevBuf<int64_t> mFs, mIs, mgi;
+    DevBuf<unsigned long long> trace;  // [3][kTraceWgs][8] phase stamps (option "trace")
     DevBuf<int32_t> sperm, scnt;  // K3 step path scratch (step.hip)
     DevBuf<int64_t> stile, spnow;
-    DevBuf<unsigned char> svrec;
+    DevBuf<Mid> smid;
     DevBuf<Step1> sstep1;
+    DevBuf<int32_t> spm1, ssm0;   // prefix / suffix key maxima of the sorted Step1 records
     // kernel timing (crane_dyn_set_profiling)
     bool prof = false;
     EngineTimer timer;
@@ -177,6 +181,9 @@ struct crane_dyn {
     int nk = 0;
     hipError_t timer_err = hipSuccess;
 
+    unsigned long long* trace_region(int which) {
+        return opt.trace && trace.p ? trace.p + (size_t)which * kTraceWgs * 8 : nullptr;
+    }
     int fail(int code, const std::string& m) {
         err = m;
         return code;
@@ -320,7 +327,8 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     h->hv_from_counts = true;
     h->hv_ts_counts = hv_ts_ns;
     h->rec_dirty = true;
-    const HotPart gx = hot_dedupe_geometry(h->B, h->N, dp.n_win, h->opt.k1_threads);
+    HotPart gx = hot_dedupe_geometry(h->B, h->N, dp.n_win, h->opt.k1_threads);
+    gx.trace = gx.nblk <= kTraceWgs ? h->trace_region(0) : nullptr;
     if (h->opt.k2_form == 0 && gx.ok) {
         // one launch (+ K3p); the node pass counts its own block's entries (no buckets)
         HIPTRY(h, h->k2_sorted.reserve(hot_dedupe_scratch(gx)));
@@ -389,6 +397,7 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
         a.hv_ts = h->hv_ts.p;
     }
     a.threads = k1_bs(h);
+    a.trace = (h->N + a.threads - 1) / a.threads <= kTraceWgs ? h->trace_region(1) : nullptr;
     HIPTRY(h, launch_node_pass(h->shape, a, st, step));
     if (consume) {
         if (!h->hx_pending) h->buckets_zero = true;  // K1 zeroed what it read
@@ -420,9 +429,27 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     HIPTRY(h, h->stile.reserve((size_t)(2 * g.ntiles)));
     HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
     HIPTRY(h, h->scnt.reserve((size_t)std::max<int32_t>(nblk, 1) * 6));  // cnt [nblk][4] + flat [nblk][2]
-    HIPTRY(h, h->sstep1.reserve((size_t)(2 * g.npad)));
-    HIPTRY(h, h->svrec.reserve((size_t)(2 * g.npad) * step_vrec_bytes(h->shape)));
-    sp.stt = StepTables{h->scnt.p, h->scnt.p + (size_t)nblk * 4, h->sstep1.p, h->svrec.p, g.npad, bs, nblk};
+    // per kind and producer block: 2 * bs one-step records, bs * (breakpoints - 1) middle pieces
+    const int64_t s1pad = 2 * g.npad, mstride = (int64_t)bs * (step_breakpoints(h->shape) - 1);
+    const int64_t mpad = (int64_t)nblk * mstride;
+    HIPTRY(h, h->sstep1.reserve((size_t)(2 * s1pad)));
+    HIPTRY(h, h->spm1.reserve((size_t)(2 * s1pad)));
+    HIPTRY(h, h->ssm0.reserve((size_t)(2 * s1pad)));
+    HIPTRY(h, h->smid.reserve((size_t)(2 * mpad)));
+    StepTables& t = sp.stt;
+    t = StepTables{};
+    t.cnt = h->scnt.p;
+    t.flat = h->scnt.p + (size_t)nblk * 4;
+    t.single = h->sstep1.p;
+    t.pm1 = h->spm1.p;
+    t.sm0 = h->ssm0.p;
+    t.mid = h->smid.p;
+    t.s1pad = s1pad;
+    t.mpad = mpad;
+    t.bs = bs;
+    t.nblk = nblk;
+    t.mstride = (int32_t)mstride;
+    t.trace = g.ngroups * g.R <= kTraceWgs ? h->trace_region(2) : nullptr;
     return CRANE_OK;
 }
 
@@ -559,7 +586,9 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
     h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
     h->mFs.release(); h->mIs.release(); h->mgi.release();
-    h->sperm.release(); h->scnt.release(); h->stile.release(); h->spnow.release(); h->svrec.release(); h->sstep1.release();
+    h->trace.release();
+    h->sperm.release(); h->scnt.release(); h->stile.release(); h->spnow.release(); h->smid.release(); h->sstep1.release();
+    h->spm1.release(); h->ssm0.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -589,10 +618,31 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "greedy_form" && range(0, 1)) o.greedy_form = (int)value;
     else if (n == "matrix_vec" && (value == 0 || value == 1 || value == 4 || value == 8 || value == 16)) o.matrix_vec = (int)value;
     else if (n == "matrix_chunk" && range(0, 1024)) o.matrix_chunk = (int)value;
+    else if (n == "trace" && range(0, 1)) {
+        o.trace = value != 0;
+        if (o.trace) {
+            hipError_t e = hipSetDevice(h->device);
+            if (e == hipSuccess) e = h->trace.reserve((size_t)3 * kTraceWgs * 8);
+            if (e == hipSuccess) e = hipMemset(h->trace.p, 0, sizeof(unsigned long long) * h->trace.n);
+            if (e != hipSuccess) return h->hipfail(e, "trace buffer");
+        }
+    }
     else return h->fail(CRANE_E_INVALID, "unknown option or value: " + n + "=" + std::to_string(value));
     // a pending dedupe-form count is bound to the K1 block size it was binned by
     h->rec_dirty = true;
     return CRANE_OK;
+}
+
+int64_t crane_dyn_debug_trace(crane_dyn* h, int32_t which, int64_t max, uint64_t* out) {
+    if (!h || which < 0 || which > 2 || max < 0 || (max > 0 && !out)) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (!h->opt.trace || !h->trace.p) return h->fail(CRANE_E_STATE, "option \"trace\" is off");
+    const int64_t n = std::min<int64_t>(max, kTraceWgs * 8);
+    HIPTRY(h, hipSetDevice(h->device));
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    HIPTRY(h, hipDeviceSynchronize());
+    HIPTRY(h, hipMemcpy(out, h->trace_region(which), sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+    return n;
 }
 
 int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const double* val, const int64_t* ts,

@@ -233,6 +233,7 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     uint32_t* hist = hcnt + kDSlots;
     uint32_t* off = hist + g.nbins;
     uint16_t* uniq = reinterpret_cast<uint16_t*>(off + g.nbins);
+    CRANE_TSTAMP(g.trace, blk, 0);
     const int64_t b0 = (int64_t)blk * kXChunk + threadIdx.x;
     int32_t nd[kPer];
     int64_t ts[kPer];
@@ -249,6 +250,7 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     for (int i = threadIdx.x; i < g.nbins; i += BT) hist[i] = 0;
     if (threadIdx.x == 0) nuniq = 0;
     __syncthreads();
+    CRANE_TSTAMP(g.trace, blk, 1);
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
@@ -277,6 +279,7 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
         }
     }
     __syncthreads();
+    CRANE_TSTAMP(g.trace, blk, 2);
     const int per = (g.nbins + BT - 1) / BT;
     const int lo = min(g.nbins, (int)threadIdx.x * per), hi = min(g.nbins, lo + per);
     uint32_t sum = 0;
@@ -291,6 +294,7 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     // this region's row of (count | offset << 16) per node block: coalesced
     for (int i = threadIdx.x; i < g.nbins; i += BT) CO[(int64_t)blk * g.nbins + i] = hist[i] | (off[i] << 16);
     __syncthreads();
+    CRANE_TSTAMP(g.trace, blk, 3);
     uint32_t* reg = region + (int64_t)blk * kXChunk;
     const uint32_t mask = (1u << g.bb) - 1;
     const uint32_t nu = nuniq;
@@ -300,6 +304,7 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
         const uint32_t p = atomicAdd(&off[(k >> 3) >> g.bb], 1u);
         reg[p] = ((uint32_t)(k >> 3) & mask) | ((uint32_t)(k & 7) << 16) | (hcnt[s] << 19);
     }
+    CRANE_TSTAMP(g.trace, blk, 4);
 }
 
 // 1024 threads (2 bindings each): the launch is one round of workgroups at

@@ -126,6 +126,7 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Rec* lrec = reinterpret_cast<Rec*>(smem);
     const int64_t blk = xcd_block(blockIdx.x, gridDim.x);  // this workgroup's block of nodes
+    CRANE_TSTAMP(a.trace, blockIdx.x, 0);
     const int64_t first = blk * kK1Threads;
     const int64_t n = first + threadIdx.x;
     __shared__ int64_t smn[kK1Threads / 64], smx[kK1Threads / 64];
@@ -133,6 +134,11 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     int64_t tmin = 0, tmax = 0, pmn = 0, pmx = 0;
     __shared__ int32_t nq;                      // stepped (node, kind) items queued for the emit
     __shared__ uint32_t q[STEP ? 2 * kK1Threads : 1];
+    __shared__ int32_t qm[STEP ? 2 * kK1Threads : 1];  // first middle-piece slot of queued items
+    // one-step records per kind (2 per node at most): staging; sorted copy over the records'
+    // LDS once the emit has read them (or past them when the records are written out)
+    __shared__ Step1 s1l[STEP ? 4 * kK1Threads : 1];
+    Step1* s1s = reinterpret_cast<Step1*>(smem + (out ? sizeof(Rec) * kK1Threads : 0));
     if (STEP && threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
     if (STEP && threadIdx.x == 0) nq = 0;
     __shared__ uint32_t hxh[kMaxWin][kK1Threads];  // dedupe-form K2: this block's window-rank buckets
@@ -236,6 +242,7 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
 #pragma unroll
         for (int b = 0; b < kMaxWin; ++b) bc[b] = b < pol.n_win ? hxh[b][threadIdx.x] : 0u;
     }
+    CRANE_TSTAMP(a.trace, blockIdx.x, 1);
     // the batch time range partials: issued after the SoA loads, reduced after the compute
     if (STEP) batch_range_load<kK1Threads>(step.tile_mm, step.ntiles, pmn, pmx);
     if (n < N) {
@@ -312,24 +319,29 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
         r.e_fail = e_fail;
         if (out) lrec[threadIdx.x] = r;
     }
+    CRANE_TSTAMP(a.trace, blockIdx.x, 2);
     if (STEP) {
         batch_range_reduce<kK1Threads>(pmn, pmx, smn, smx, tmin, tmax);
         if (n < N) step_count<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, ssh, so);
         if (so.slot0 >= 0 || so.slot1 >= 0) {  // stepped (a few %): record to LDS, items to the queue
             if (!out) lrec[threadIdx.x] = r;
-            step_queue(so, &nq, q);
+            step_queue(so, &nq, q, qm);
         }
         step_publish<kK1Threads>(so, ssh, step.st, blk);  // (its barrier also orders lrec and the queue)
+        CRANE_TSTAMP(a.trace, blockIdx.x, 3);
         // the queued items are built densely by the first lanes of the workgroup
         for (int w = threadIdx.x; w < nq; w += kK1Threads) {
             const uint32_t it = q[w];
             const int o = (int)(it & 0xFFF);
-            step_emit_one<PD, PR>(lrec[o], first + o, (int)((it >> 12) & 1), (int32_t)(it >> 14), ((it >> 13) & 1) != 0,
-                                  tmin, tmax, step.wsum, step.noprio, step.st, blk);
+            step_emit_one<PD, PR>(lrec[o], first + o, (int)((it >> 12) & 1), (int32_t)(it >> 14), qm[w],
+                                  ((it >> 13) & 1) != 0, tmin, tmax, step.wsum, step.noprio, step.st, blk, s1l);
         }
+        __syncthreads();
+        step_sort_publish<kK1Threads>(s1l, s1s, ssh, step.st, blk);
     } else {
         __syncthreads();
     }
+    CRANE_TSTAMP(a.trace, blockIdx.x, 4);
     if (!out) return;  // keys-only step: the records are rebuilt when a matrix/greedy pass needs them
     const int64_t nvalid = min((int64_t)kK1Threads, N - first);
     const int64_t nvec = nvalid * (int64_t)sizeof(Rec) / 16;
@@ -345,7 +357,9 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
     const int T = a.threads;
     if (T != 128 && T != 256) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((a.N + T - 1) / T);
-    const size_t lds = sizeof(NodeRec<PD, PR>) * T;
+    // + the sorted one-step records past the node records when both are kept (kernel above)
+    static_assert(sizeof(NodeRec<PD, PR>) >= 4 * sizeof(Step1), "sorted records fit over the node records");
+    const size_t lds = sizeof(NodeRec<PD, PR>) * T + (step && a.out ? 4 * sizeof(Step1) * T : 0);
     const K1Step sa = step ? *step : K1Step{};
     const char* nm = step ? "k1_node_pass+k3a_steps" : "k1_node_pass";
     if (T == 256)

@@ -31,6 +31,14 @@ inline hipError_t klaunch(const char* name, void (*kernel)(KArgs...), dim3 grid,
     return hipGetLastError();
 }
 
+// Phase trace (engine option "trace", crane_dyn_debug_trace): when non-null, thread 0
+// of every workgroup stores s_memrealtime stamps (100 MHz) at the kernel's phase
+// boundaries into trace[8 * workgroup + k].
+#define CRANE_TSTAMP(tr, wg, k)                                                        \
+    do {                                                                               \
+        if ((tr) && threadIdx.x == 0) (tr)[8 * (int64_t)(wg) + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
 struct HotCutoffs {
     int32_t n_win;
     int32_t pad;
@@ -125,6 +133,7 @@ struct HotPart {
     int64_t cap;        // region entries (nblk * 2048)
     int32_t nblk;       // partition workgroups
     bool ok;
+    unsigned long long* trace;  // phase trace or null
 };
 // The step path's pod preparation (K3p) for 1024-pod tiles, as it rides in K2x's launch.
 struct PodPrep {
@@ -151,34 +160,42 @@ struct alignas(16) Step1 {
     int64_t bp;
     int32_t k0, k1;
 };
-// A node whose key changes more than once: cnt ascending expiries in
-// (tmin, tmax], padded with INT64_MAX; key[j] holds for bp[j-1] <= now < bp[j].
-template <int NB>
-struct alignas(16) VRec {  // 16-byte multiple: K3s stages records with 16-byte copies
-    int64_t bp[NB];
-    int32_t key[NB + 1];
-    int32_t cnt;
+// A middle piece of a node whose key changes more than once in the batch: the
+// key on [s, e) (step_node.hpp).
+struct alignas(8) Mid {
+    int64_t s, e;
+    int32_t key;
+    int32_t pad;
 };
 // Step tables, one region per producer workgroup b (K1: bs = 128/256 nodes,
 // K3a: 256): its flat-key maxima flat[b][kind], its record counts cnt[b][L]
-// (L = 2 * kind + 0: Step1, 1: VRec) and its records at b * bs + slot of each
-// list.  Producers need no global atomics; K3s scans the counts of the
-// producer blocks it covers.
+// (L = 2 * kind + 0: one-step records, 1: middle pieces), its one-step records
+// sorted by step time with their prefix / suffix key maxima
+// (step_sort_publish) and its middle pieces.  Producers need no global
+// atomics; K3s reads the producer blocks it covers.
 struct StepTables {
     int32_t* cnt;    // [nblk][4]
     int32_t* flat;   // [nblk][2], -1 = no flat feasible node
-    Step1* single;   // [2][npad] per pod kind
-    void* multi;     // [2][npad] VRec<NB>
-    int64_t npad;    // per-kind stride >= nblk * bs
+    Step1* single;   // kind T, block b: 2 * bs records at s1_at(T, b), sorted by bp
+    int32_t* pm1;    // same indexing: prefix max of k1 (after-step keys) over the sorted records
+    int32_t* sm0;    // same indexing: suffix max of k0 (before-step keys)
+    Mid* mid;        // kind T, block b: mstride pieces at T * mpad + b * mstride
+    int64_t s1pad, mpad;  // per-kind strides
     int32_t bs;      // nodes per producer workgroup
     int32_t nblk;    // producer workgroups
+    int32_t mstride; // middle pieces per block region (bs * (breakpoints per node - 1))
+    int32_t pad;
+    unsigned long long* trace;  // K3s phase trace or null
 };
+__host__ __device__ inline int64_t s1_at(const StepTables& st, int T, int64_t b) {
+    return T * st.s1pad + b * 2 * st.bs;
+}
 struct StepGeometry {
     int64_t nseg, npad, ntiles, ngroups;
     int32_t R;  // K3s workgroups per 1024-pod group (raised until each covers <= kK3sMaxBlk producer blocks)
 };
-constexpr int kK3sMaxBlk = 1024;
-size_t step_vrec_bytes(int shape);
+constexpr int kK3sMaxBlk = 256;  // producer blocks per K3s workgroup (one lane each)
+int step_breakpoints(int shape);  // in-range expiries per node and kind at most: PR + 2
 StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk);
 // K3p: perm, pnow [ntiles * 1024], tile_mm [2 * ntiles]; initialises keys[0..P) to -1
 hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys,
@@ -224,6 +241,7 @@ struct K1Args {
     const uint32_t* hx_CO;
     int32_t hx_nblk;
     int32_t threads;        // workgroup size: 128 or 256
+    unsigned long long* trace;  // phase trace or null
 };
 // step (optional): also build the K3 step tables of a pod batch (K3a fused).
 hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr);

@@ -18,13 +18,14 @@
 //   K3p  pods  : DaemonSet partition per 1024-pod tile (so waves are uniform),
 //                key init, per-tile min/max of now, step-table header reset
 //   K3a  nodes : per node, both pod kinds (Filter applies / DaemonSet bypass,
-//                utils.go:17-24): flat key -> workgroup max -> one atomicMax
-//                per workgroup; stepped node -> record appended to a compact
-//                list (one atomicAdd per workgroup reserves the space)
-//   K3s  pairs : 256 pods per workgroup (4 waves, one pod per lane), R
-//                workgroups per pod group split the stepped lists; a slice is
-//                staged in LDS and read back with broadcast reads; one 64-bit
-//                atomicMax per pod per workgroup; lowest node index wins ties
+//                utils.go:17-24): flat key -> workgroup max; stepped node ->
+//                its key pieces (one-step records sorted per workgroup with
+//                prefix / suffix key maxima, middle pieces), step_node.hpp
+//   K3s  pairs : a 1024-pod tile per workgroup (4 pods per lane), R workgroups
+//                per tile split the producer blocks (one lane per block):
+//                binary searches find the records stepping inside the tile's
+//                time range, one prefix and one suffix maximum give the key of
+//                all others; one 64-bit atomicMax per pod per workgroup
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -99,6 +100,7 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
                                                       double wsum, int32_t noprio, StepTables st) {
     __shared__ int64_t smn[kStepSeg / 64], smx[kStepSeg / 64];
     __shared__ StepShared sh;
+    __shared__ Step1 s1l[4 * kStepSeg], s1s[4 * kStepSeg];  // one-step records per kind: staging, sorted
     if (threadIdx.x < 4) sh.lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
     int64_t tmin, tmax;
     batch_range<kStepSeg>(tile_mm, ntiles, smn, smx, tmin, tmax);  // (its barrier orders the lc reset)
@@ -110,54 +112,58 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
         step_count<PD, PR>(r, n, tmin, tmax, wsum, noprio, sh, o);
     }
     step_publish<kStepSeg>(o, sh, st, blockIdx.x);
-    if (n < N && (o.slot0 >= 0 || o.slot1 >= 0)) step_emit<PD, PR>(r, n, tmin, tmax, wsum, noprio, o, st, blockIdx.x);
+    if (n < N && (o.slot0 >= 0 || o.slot1 >= 0)) step_emit<PD, PR>(r, n, tmin, tmax, wsum, noprio, o, st, blockIdx.x, s1l);
+    __syncthreads();
+    step_sort_publish<kStepSeg>(s1l, s1s, sh, st, blockIdx.x);
 }
 
 // ---------------------------------------------------------------- K3s
-// Workgroup = 4 waves x 64 lanes x 4 pods per lane (one 1024-pod tile of
-// K3p's partitioned order: lane l of wave w holds pods u * 256 + w * 64 + l);
-// the R workgroups of a tile split the producer blocks.  A workgroup reads its
-// blocks' records with coalesced loads: a one-step record whose step lies
-// outside the tile's time range gives the same key to all of the tile's pods
-// of its kind (one max), the others are staged in LDS and every lane walks
-// them with broadcast LDS reads (per pod: 64-bit compare, select, max).  One
-// 64-bit atomicMax per pod per workgroup merges the slices.
+// Workgroup = 4 waves x 64 lanes x 4 pods per lane (one 1024-pod tile of K3p's
+// partitioned order: lane l of wave w holds pods u * 256 + w * 64 + l); the R
+// workgroups of a tile split the producer blocks, one lane per block.
+// One-step records: each block's are sorted by step time bp with prefix maxima
+// of the after-step key (pm1) and suffix maxima of the before-step key (sm0)
+// (step_sort_publish).  For the tile's pod time range [lo, hi] (per pod kind)
+// a lane finds by two binary searches the block's records stepping inside
+// (lo, hi]; every pod of the tile sees the key after the step of each earlier
+// record (one prefix maximum) and the key before the step of each later one
+// (one suffix maximum).  The records inside are staged in LDS and every lane
+// evaluates them for its 4 pods (64-bit compare, select, max).  Middle pieces
+// [s, e) of multi-step nodes: one covering the whole range gives its key to
+// every pod of the tile, one overlapping it partly is staged and evaluated per
+// pod (s <= now < e).  One 64-bit atomicMax per pod per workgroup merges the
+// slices.
 constexpr int kK3sWaves = 4;
 constexpr int kK3sThreads = kK3sWaves * 64;
 constexpr int kK3sPPL = 4;                          // pods per lane
 constexpr int kK3sPods = kK3sThreads * kK3sPPL;     // pods per workgroup (= kPodTile)
-constexpr int kK3sS1 = 512;  // Step1 records staged per round and pod kind (8 KB; 128..1024 measured slower at config 4)
-constexpr int kK3sVR = 32;   // VRec records staged per round and pod kind
-static_assert(kK3sS1 >= 64 && kK3sS1 % 64 == 0, "the staging rounds must make progress");
-static_assert(2 * kK3sS1 * 16 + 2 * kK3sVR * 240 + 4 * 4 * (kK3sMaxBlk + 1) <= 64 * 1024, "K3s LDS budget");
+constexpr int kK3sS1 = 512;  // one-step records staged per round and pod kind (8 KB)
+constexpr int kK3sMP = 128;  // middle pieces staged per round and pod kind
+static_assert(kK3sMaxBlk <= kK3sThreads, "one lane per producer block");
 
-// position in the per-producer-block layout of element i of the concatenation
-// of blocks b0 + 0 .. m-1 (pre: exclusive prefix of their counts, pre[m] = total)
-__device__ __forceinline__ int64_t blk_pos(const int32_t* pre, int32_t m, int32_t i, int32_t b0, int32_t bs) {
-    int lo = 0, hi = m - 1;  // largest j with pre[j] <= i
+// number of the n sorted step times at base[] that are <= t (upper bound)
+__device__ __forceinline__ int32_t count_le(const Step1* __restrict__ base, int32_t n, int64_t t) {
+    int32_t lo = 0, hi = n;
     while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (pre[mid] <= i) lo = mid;
-        else hi = mid - 1;
+        const int32_t mid = (lo + hi) >> 1;
+        if (base[mid].bp <= t) lo = mid + 1;
+        else hi = mid;
     }
-    return (int64_t)(b0 + lo) * bs + (i - pre[lo]);
+    return lo;
 }
 
-// The four stepped lists: L = 2 * kind + (0: Step1, 1: VRec).
-template <int NB>
 __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int32_t* __restrict__ perm,
                                                         const int64_t* __restrict__ pnow, int64_t P,
                                                         int64_t node_offset, int32_t R,
                                                         long long* __restrict__ keys) {
-    static_assert(kK3sWaves == 4, "one wave scans each list's counts");
-    static_assert(sizeof(VRec<NB>) % 16 == 0, "VRec must be a whole number of int4");
+    static_assert(kK3sWaves == 4, "per-wave partials below");
     __shared__ int4 l1[2][kK3sS1];
-    __shared__ VRec<NB> lv[2][kK3sVR];
-    __shared__ int32_t pre[4][kK3sMaxBlk + 1];
-    __shared__ int32_t fl[2][kK3sWaves];
-    __shared__ int64_t wr[2][2][kK3sWaves];  // per kind and wave: min, max pod time
-    __shared__ int32_t nin[2], nvr[2], umax[2];  // staged one-step / multi-step records, uniform maximum (per kind)
+    __shared__ Mid lm[2][kK3sMP];
+    __shared__ int32_t spart[2][kK3sWaves], mpart[2][kK3sWaves];  // straddling records / pieces per wave
+    __shared__ int64_t wr[2][2][kK3sWaves];      // per kind and wave: min, max pod time
+    __shared__ int32_t umax[2];
     const int64_t b = blockIdx.x;
+    CRANE_TSTAMP(st.trace, b, 0);
     const int32_t r = (int32_t)(b % R);
     const int64_t grp = b / R;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -174,31 +180,20 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         ds[u] = praw < 0;
         pod[u] = praw & 0x7FFFFFFF;
     }
-    // producer blocks [b0, b0 + m) of this slice: their counts, scanned per list
-    // (wave w scans list w), and their flat maxima
+    // producer blocks [b0, b0 + m) of this slice; thread j < m owns block b0 + j
     const int32_t per = (st.nblk + R - 1) / R;
     const int32_t b0 = min(st.nblk, r * per), m = min(st.nblk, b0 + per) - b0;
-    {
-        int32_t carry = 0;
-        for (int32_t j0 = 0; j0 < m; j0 += 64) {
-            const int32_t j = j0 + lane;
-            const int32_t c = j < m ? st.cnt[(int64_t)(b0 + j) * 4 + w] : 0;
-            int32_t x = c;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t y = __shfl_up(x, o);
-                if (lane >= o) x += y;
-            }
-            if (j < m) pre[w][j] = carry + x - c;
-            carry += __shfl(x, 63);
-        }
-        if (lane == 0) pre[w][m] = carry;
-        int32_t f = -1;
-        if (w < 2)
-            for (int32_t j = lane; j < m; j += 64) f = max(f, st.flat[(int64_t)(b0 + j) * 2 + w]);
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) f = max(f, __shfl_xor(f, o));
-        if (lane == 0 && w < 2) fl[w][0] = f;
+    const bool own = (int32_t)threadIdx.x < m;
+    const int64_t ob = b0 + threadIdx.x;
+    int32_t cnt1[2] = {0, 0}, cntm[2] = {0, 0}, flat[2] = {-1, -1};
+    if (own) {
+        const int4 c = reinterpret_cast<const int4*>(st.cnt)[ob];  // [records kind 0, pieces 0, records 1, pieces 1]
+        cnt1[0] = c.x;
+        cntm[0] = c.y;
+        cnt1[1] = c.z;
+        cntm[1] = c.w;
+        flat[0] = st.flat[ob * 2];
+        flat[1] = st.flat[ob * 2 + 1];
     }
     bool ln = false, ld = false;  // this lane has pods of kind 0 / 1
 #pragma unroll
@@ -207,8 +202,7 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         ld |= ds[u];
     }
     const bool wn = __ballot(ln) != 0, wd = __ballot(ld) != 0;
-    // the workgroup's pod time range per kind: a record whose step lies outside it
-    // gives the same key to every pod of that kind here (one max, no per-lane work)
+    // the workgroup's pod time range per kind
 #pragma unroll
     for (int T = 0; T < 2; ++T) {
         int64_t mn = INT64_MAX, mx = INT64_MIN;
@@ -228,10 +222,7 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
             wr[T][1][w] = mx;
         }
     }
-    if (threadIdx.x < 2) {
-        nin[threadIdx.x] = nvr[threadIdx.x] = 0;
-        umax[threadIdx.x] = -1;
-    }
+    if (threadIdx.x < 2) umax[threadIdx.x] = -1;
     const bool bn = __syncthreads_or(ln), bd = __syncthreads_or(ld);  // (also orders the LDS above)
     int64_t tlo[2], thi[2];
 #pragma unroll
@@ -239,128 +230,154 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         tlo[T] = min(min(wr[T][0][0], wr[T][0][1]), min(wr[T][0][2], wr[T][0][3]));
         thi[T] = max(max(wr[T][1][0], wr[T][1][1]), max(wr[T][1][2], wr[T][1][3]));
     }
-    // the flat maxima of this slice's producer blocks hold for every pod of the kind
+    // one-step records of the owned block: the ones stepping inside (lo, hi], and the
+    // uniform key of all others; a kind without pods here takes nothing
+    int32_t s_lo[2], s_n[2];
+    // this thread's share of the uniform maxima (a kind without pods here is never read)
+    int32_t um0 = flat[0], um1 = flat[1];
+    {
+        int32_t jl[2], jh[2];
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {  // the four searches are independent chains
+            const bool any = T ? bd : bn;
+            const Step1* base = st.single + s1_at(st, T, ob);
+            const int32_t n = own && any ? cnt1[T] : 0;
+            jl[T] = count_le(base, n, tlo[T]);
+            jh[T] = count_le(base, n, thi[T]);
+        }
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+            const int64_t base = s1_at(st, T, ob);
+            const bool any = own && (T ? bd : bn);
+            int32_t u = -1;
+            if (any && jl[T] > 0) u = st.pm1[base + jl[T] - 1];
+            if (any && jh[T] < cnt1[T]) u = max(u, st.sm0[base + jh[T]]);
+            if (T) um1 = max(um1, u);
+            else um0 = max(um0, u);
+            if (!any) flat[T] = -1;
+            s_lo[T] = jl[T];
+            s_n[T] = any ? jh[T] - jl[T] : 0;
+        }
+    }
+    // middle pieces of the owned block: covering [lo, hi] -> uniform key, overlapping
+    // it partly -> counted here, staged below
+    int32_t m_n[2] = {0, 0};
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+        const bool any = own && (T ? bd : bn);
+        const Mid* mp = st.mid + (int64_t)T * st.mpad + ob * st.mstride;
+        const int32_t n = any ? cntm[T] : 0;
+        int32_t u = -1;
+        for (int32_t i = 0; i < n; ++i) {
+            const Mid p = mp[i];
+            if (p.s <= tlo[T] && p.e > thi[T]) u = max(u, p.key);
+            else m_n[T] += p.s <= thi[T] && p.e > tlo[T];
+        }
+        if (T) um1 = max(um1, u);
+        else um0 = max(um0, u);
+    }
+    CRANE_TSTAMP(st.trace, b, 1);
+    // exclusive prefix of the straddling counts over the owned blocks (per kind)
+    int32_t s_off[2], s_tot[2], m_off[2], m_tot[2];
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+        int32_t x = s_n[T], y = m_n[T];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t xs = __shfl_up(x, o), ys = __shfl_up(y, o);
+            if (lane >= o) {
+                x += xs;
+                y += ys;
+            }
+        }
+        if (lane == 63) {
+            spart[T][w] = x;
+            mpart[T][w] = y;
+        }
+        s_off[T] = x - s_n[T];
+        m_off[T] = y - m_n[T];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+        int32_t pre = 0, tot = 0, mpre = 0, mtot = 0;
+#pragma unroll
+        for (int i = 0; i < kK3sWaves; ++i) {
+            pre += i < w ? spart[T][i] : 0;
+            tot += spart[T][i];
+            mpre += i < w ? mpart[T][i] : 0;
+            mtot += mpart[T][i];
+        }
+        s_off[T] += pre;
+        s_tot[T] = tot;
+        m_off[T] += mpre;
+        m_tot[T] = mtot;
+    }
     int32_t best_n[kK3sPPL], best_d[kK3sPPL];
 #pragma unroll
-    for (int u = 0; u < kK3sPPL; ++u) {
-        best_n[u] = fl[0][0];
-        best_d[u] = fl[1][0];
-    }
-    // this workgroup's slice [lo, hi) of each list (lists of a kind without pods here: empty)
-    int32_t lo[4], hi[4];
-#pragma unroll
-    for (int L = 0; L < 4; ++L) {
-        lo[L] = 0;
-        hi[L] = ((L < 2) ? bn : bd) ? pre[L][m] : 0;
-    }
-    int32_t um0 = -1, um1 = -1;  // this thread's share of the uniform maxima
-    for (bool first = true;; first = false) {
-        int32_t take[4];
-#pragma unroll
-        for (int L = 0; L < 4; ++L) take[L] = min((L & 1) ? kK3sVR : kK3sS1, hi[L] - lo[L]);
-        if (take[0] + take[1] + take[2] + take[3] == 0) break;
-        if (!first) {
-            __syncthreads();  // the previous round's readers are done
-            if (threadIdx.x < 2) nin[threadIdx.x] = nvr[threadIdx.x] = 0;
-            __syncthreads();
-        }
-        // one-step records of both kinds [S1 kind 0 | S1 kind 1]: a record whose step
-        // lies outside the tile's time range folds into the uniform maxima, the rest
-        // are staged in LDS
-        const int32_t e2 = take[0], e4 = e2 + take[2];
-        for (int32_t i0 = threadIdx.x; i0 < e4; i0 += 4 * kK3sThreads) {
-            const int4* src[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {  // addresses first, then 4 loads in flight
-                const int32_t e = min(i0 + u * kK3sThreads, e4 - 1);  // past the end: repeat the last element
-                const int T = e >= e2;
-                const int32_t f = T ? e - e2 : e;
-                const int32_t lo1 = T ? lo[2] : lo[0];  // selects, not indexing: keeps lo in registers
-                src[u] = reinterpret_cast<const int4*>(st.single + (int64_t)T * st.npad) +
-                         blk_pos(pre[2 * T], m, lo1 + f, b0, st.bs);
-            }
+    for (int u = 0; u < kK3sPPL; ++u) best_n[u] = best_d[u] = -1;
+    auto walk1 = [&](int T, int32_t n1, int32_t* best) {
+        int32_t i = 0;
+        for (; i + 4 <= n1; i += 4) {
             int4 q[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) q[u] = *src[u];
+            for (int v = 0; v < 4; ++v) q[v] = l1[T][i + v];  // broadcast LDS reads
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int32_t e = i0 + u * kK3sThreads;
-                if (e >= e4) continue;
-                const int T = e >= e2;
-                const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q[u].y << 32) | (uint32_t)q[u].x);
-                const int64_t lo_t = T ? tlo[1] : tlo[0], hi_t = T ? thi[1] : thi[0];
-                if (bp <= lo_t || bp > hi_t) {  // every pod of the kind here is on one side of the step
-                    const int32_t k = bp <= lo_t ? q[u].w : q[u].z;
-                    if (T) um1 = max(um1, k);
-                    else um0 = max(um0, k);
-                } else {
-                    l1[T][atomicAdd(&nin[T], 1)] = q[u];
-                }
+            for (int v = 0; v < 4; ++v) {
+                const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q[v].y << 32) | (uint32_t)q[v].x);
+#pragma unroll
+                for (int u = 0; u < kK3sPPL; ++u) best[u] = max(best[u], tnow[u] >= bp ? q[v].w : q[v].z);
             }
         }
-        // multi-step records [VR kind 0 | VR kind 1], one thread per record: one with
-        // no step inside the tile's time range folds (its key at the range start),
-        // the rest are staged
-        const int32_t v2 = take[1], v4 = v2 + take[3];
-        for (int32_t e = threadIdx.x; e < v4; e += kK3sThreads) {
-            const int T = e >= v2;
-            const int32_t f = T ? e - v2 : e;
-            const int32_t lov = T ? lo[3] : lo[1];
-            const VRec<NB> v = reinterpret_cast<const VRec<NB>*>(st.multi)[(int64_t)T * st.npad +
-                                                                       blk_pos(pre[2 * T + 1], m, lov + f, b0, st.bs)];
-            const int64_t lo_t = T ? tlo[1] : tlo[0], hi_t = T ? thi[1] : thi[0];
-            int32_t k = v.key[0];
-            bool inside = false;
+        for (; i < n1; ++i) {
+            const int4 q = l1[T][i];
+            const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q.y << 32) | (uint32_t)q.x);
 #pragma unroll
-            for (int s2 = 0; s2 < NB; ++s2) {
-                k = lo_t >= v.bp[s2] ? v.key[s2 + 1] : k;
-                inside |= v.bp[s2] > lo_t && v.bp[s2] <= hi_t;
-            }
-            if (!inside) {
-                if (T) um1 = max(um1, k);
-                else um0 = max(um0, k);
-            } else {
-                lv[T][atomicAdd(&nvr[T], 1)] = v;
+            for (int u = 0; u < kK3sPPL; ++u) best[u] = max(best[u], tnow[u] >= bp ? q.w : q.z);
+        }
+    };
+    // one-step records stepping inside the tile's range: rounds of kK3sS1 per kind
+    for (int32_t r0 = 0; r0 < max(s_tot[0], s_tot[1]); r0 += kK3sS1) {
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {  // the owning lane copies its records of window [r0, r0 + kK3sS1)
+            const int32_t a = max(s_off[T], r0), e = min(s_off[T] + s_n[T], r0 + kK3sS1);
+            const int4* src = reinterpret_cast<const int4*>(st.single + s1_at(st, T, ob)) + s_lo[T];
+            for (int32_t g = a; g < e; ++g) l1[T][g - r0] = src[g - s_off[T]];
+        }
+        __syncthreads();
+        if (wn) walk1(0, min(kK3sS1, max(0, s_tot[0] - r0)), best_n);
+        if (wd) walk1(1, min(kK3sS1, max(0, s_tot[1] - r0)), best_d);
+        __syncthreads();
+    }
+    // middle pieces overlapping the tile's range partly: rounds of kK3sMP per kind; the
+    // owning lane re-reads its block's pieces and stages those of the window
+    auto walkm = [&](int T, int32_t n, int32_t* best) {
+        for (int32_t j = 0; j < n; ++j) {
+            const Mid p = lm[T][j];
+#pragma unroll
+            for (int u = 0; u < kK3sPPL; ++u) best[u] = max(best[u], tnow[u] >= p.s && tnow[u] < p.e ? p.key : -1);
+        }
+    };
+    for (int32_t r0 = 0; r0 < max(m_tot[0], m_tot[1]); r0 += kK3sMP) {
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+            if (m_n[T] == 0 || m_off[T] + m_n[T] <= r0 || m_off[T] >= r0 + kK3sMP) continue;
+            const Mid* mp = st.mid + (int64_t)T * st.mpad + ob * st.mstride;
+            int32_t g = m_off[T];
+            for (int32_t i = 0; i < cntm[T]; ++i) {
+                const Mid p = mp[i];
+                if ((p.s <= tlo[T] && p.e > thi[T]) || !(p.s <= thi[T] && p.e > tlo[T])) continue;
+                if (g >= r0 && g < r0 + kK3sMP) lm[T][g - r0] = p;
+                ++g;
             }
         }
         __syncthreads();
-        auto walk = [&](int T, int32_t* best) {
-            const int32_t n1 = nin[T];
-            int32_t i = 0;
-            for (; i + 4 <= n1; i += 4) {
-                int4 q[4];
-#pragma unroll
-                for (int v = 0; v < 4; ++v) q[v] = l1[T][i + v];  // broadcast LDS reads
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q[v].y << 32) | (uint32_t)q[v].x);
-#pragma unroll
-                    for (int u = 0; u < kK3sPPL; ++u) best[u] = max(best[u], tnow[u] >= bp ? q[v].w : q[v].z);
-                }
-            }
-            for (; i < n1; ++i) {
-                const int4 q = l1[T][i];
-                const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q.y << 32) | (uint32_t)q.x);
-#pragma unroll
-                for (int u = 0; u < kK3sPPL; ++u) best[u] = max(best[u], tnow[u] >= bp ? q.w : q.z);
-            }
-            for (int32_t j = 0; j < nvr[T]; ++j) {
-                const VRec<NB>& v = lv[T][j];
-#pragma unroll
-                for (int u = 0; u < kK3sPPL; ++u) {
-                    int32_t k = v.key[0];
-#pragma unroll
-                    for (int s = 0; s < NB; ++s) k = tnow[u] >= v.bp[s] ? v.key[s + 1] : k;
-                    best[u] = max(best[u], k);
-                }
-            }
-        };
-        if (wn) walk(0, best_n);
-        if (wd) walk(1, best_d);
-#pragma unroll
-        for (int L = 0; L < 4; ++L) lo[L] += take[L];
+        if (wn) walkm(0, min(kK3sMP, max(0, m_tot[0] - r0)), best_n);
+        if (wd) walkm(1, min(kK3sMP, max(0, m_tot[1] - r0)), best_d);
+        __syncthreads();
     }
-    // uniform maxima: wave reduce, one LDS atomic per wave and kind
+    CRANE_TSTAMP(st.trace, b, 2);
+    // uniform maxima (flat keys, prefix / suffix maxima, folded records): wave reduce, one LDS atomic per wave
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
         um0 = max(um0, __shfl_xor(um0, o));
@@ -371,6 +388,7 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         if (um1 >= 0) atomicMax(&umax[1], um1);
     }
     __syncthreads();
+    CRANE_TSTAMP(st.trace, b, 3);
 #pragma unroll
     for (int u = 0; u < kK3sPPL; ++u) {
         const int32_t best = ds[u] ? max(best_d[u], umax[1]) : max(best_n[u], umax[0]);
@@ -381,14 +399,15 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
                       (long long)((sc << 32) | (int64_t)(0xFFFFFFFFull - (uint64_t)(node_offset + n))));
         }
     }
+    CRANE_TSTAMP(st.trace, b, 4);
 }
 
 // ---------------------------------------------------------------- launchers
-size_t step_vrec_bytes(int shape) {
+int step_breakpoints(int shape) {
     switch (shape) {
-        case kShape4x6: return sizeof(VRec<6 + 2>);
-        case kShape8x8: return sizeof(VRec<8 + 2>);
-        default: return sizeof(VRec<16 + 2>);
+        case kShape4x6: return 6 + 2;
+        case kShape8x8: return 8 + 2;
+        default: return 16 + 2;
     }
 }
 
@@ -398,12 +417,11 @@ StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk) {
     g.npad = g.nseg * kStepSeg;  // >= nblk * bs for bs = 128 or 256
     g.ntiles = (P + kPodTile - 1) / kPodTile;
     g.ngroups = (P + kK3sPods - 1) / kK3sPods;
-    // R workgroups per 1024-pod group: ~1024 workgroups in all, at most 48 per group
-    // (past ~48 the per-workgroup prologue — producer counts, pod loads — outweighs the
-    // shorter slices: config 3, 10 groups, R 64 -> 48 = 14.9 -> 13.6 us), and enough
-    // that each covers at most kK3sMaxBlk producer blocks
-    constexpr int64_t kTarget = 1024, kR = 48;
-    int64_t R = std::min<int64_t>(kR, std::max<int64_t>(1, kTarget / std::max<int64_t>(g.ngroups, 1)));
+    // R workgroups per 1024-pod tile: about kTarget workgroups in all, and enough that
+    // each covers at most kK3sMaxBlk producer blocks (one lane per block)
+    constexpr int64_t kTarget = 256;
+    int64_t R = std::max<int64_t>(1, kTarget / std::max<int64_t>(g.ngroups, 1));
+    R = std::min<int64_t>(R, std::max<int32_t>(nblk, 1));
     R = std::max<int64_t>(R, (nblk + kK3sMaxBlk - 1) / kK3sMaxBlk);
     g.R = (int32_t)R;
     return g;
@@ -437,16 +455,10 @@ hipError_t launch_step_nodes(int shape, const void* rec, int64_t N, double wsum,
 hipError_t launch_step_pairs(int shape, int64_t N, int64_t node_offset, int64_t P, long long* keys,
                              const StepTables& st, const StepGeometry& g, const int32_t* perm, const int64_t* pnow,
                              hipStream_t s) {
+    (void)shape;
     if (P <= 0 || N <= 0) return hipSuccess;
     const dim3 grid((unsigned)(g.ngroups * g.R)), blk(kK3sThreads);
-    switch (shape) {
-        case kShape4x6:
-            return klaunch("k3s_eval", k3s_eval<6 + 2>, grid, blk, 0, s, st, perm, pnow, P, node_offset, g.R, keys);
-        case kShape8x8:
-            return klaunch("k3s_eval", k3s_eval<8 + 2>, grid, blk, 0, s, st, perm, pnow, P, node_offset, g.R, keys);
-        default:
-            return klaunch("k3s_eval", k3s_eval<16 + 2>, grid, blk, 0, s, st, perm, pnow, P, node_offset, g.R, keys);
-    }
+    return klaunch("k3s_eval", k3s_eval, grid, blk, 0, s, st, perm, pnow, P, node_offset, g.R, keys);
 }
 
 }  // namespace crane

@@ -98,19 +98,29 @@ __device__ __forceinline__ void batch_range(const int64_t* __restrict__ tile_mm,
 }
 
 // Per node and pod kind: the flat key (-1 if stepped or never feasible) and,
-// for a stepped node, its slot in the workgroup's span of the kind's list.
+// for a stepped node, its slots in the workgroup's spans of the kind's lists.
 // Phase 1 (step_count) only classifies — cheap and register-light, so it can
 // run inside the node pass; phase 2 (step_emit) rebuilds the record of a
 // stepped node after the workgroup has reserved its list spans.
+//
+// A stepped node's key is piecewise constant over the batch: key_0 before its
+// first in-range expiry c_0, key_j on [c_{j-1}, c_j), key_m from c_{m-1} on.
+// It is published as pieces: two one-step records for the half-lines —
+// (bp c_0: key_0 before, -1 after) and (bp c_{m-1}: -1 before, key_m after),
+// or one (bp c_0: key_0 before, key_1 after) when m = 1 — and m - 1 middle
+// pieces [c_j, c_{j+1}) with their keys.  The max over a node's pieces covering
+// a time is its key then (a piece covers nothing outside its interval, -1).
 struct StepSlots {
     int32_t flat0 = -1, flat1 = -1;
-    int32_t slot0 = -1, slot1 = -1;  // >= 0: stepped
+    int32_t slot0 = -1, slot1 = -1;    // >= 0: stepped (first one-step record slot)
+    int32_t mslot0 = 0, mslot1 = 0;    // first middle-piece slot
+    int8_t nb0 = 0, nb1 = 0;           // in-range expiries (with repeats): one-step record iff 1 distinct
     bool multi0 = false, multi1 = false;
 };
 
 // Workgroup-shared counters of the step epilogue.
 struct StepShared {
-    int32_t lc[2][2];   // records per kind: [Step1, VRec]
+    int32_t lc[2][2];   // per kind: [one-step records, middle pieces]
     int32_t fm[2][16];  // per-wave flat maxima (<= 1024 threads)
 };
 
@@ -138,76 +148,35 @@ __device__ __forceinline__ void step_points(const NodeRec<PD, PR>& r, int64_t tm
 }
 
 // Phase 1.  A node with one distinct in-range expiry (a predicate's expiry
-// equals its metric's priority expiry when both use one metric) is a Step1.
+// equals its metric's priority expiry when both use one metric) is one record;
+// otherwise two half-line records and cnt - 1 middle-piece slots are reserved
+// (repeated expiries give empty pieces, harmless: they cover no time).
 template <int PD, int PR>
 __device__ __forceinline__ void step_count(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
                                            double wsum, int32_t noprio, StepShared& sh, StepSlots& o) {
     const int32_t s0 = score_at<PD, PR>(tmin, r, wsum, noprio);
-    auto kind = [&](auto Tc, int32_t& flat, int32_t& slot, bool& multi) {
+    auto kind = [&](auto Tc, int32_t& flat, int32_t& slot, int32_t& mslot, int8_t& nb, bool& multi) {
         constexpr int T = decltype(Tc)::value;
         int64_t c[PR + 2], mn, mx;
         int cnt;
         step_points<PD, PR, T>(r, tmin, tmax, c, cnt, mn, mx);
         flat = cnt == 0 ? key_of<PD, PR>(T, tmin, s0, r, n) : -1;
-        multi = mn != mx;
-        slot = cnt == 0 ? -1 : atomicAdd(&sh.lc[T][multi ? 1 : 0], 1);
+        multi = cnt > 0 && mn != mx;  // (cnt == 0: mn = INT64_MAX, mx = INT64_MIN)
+        nb = (int8_t)cnt;
+        slot = cnt == 0 ? -1 : atomicAdd(&sh.lc[T][0], multi ? 2 : 1);
+        mslot = multi ? atomicAdd(&sh.lc[T][1], cnt - 1) : 0;
     };
-    kind(std::integral_constant<int, 0>{}, o.flat0, o.slot0, o.multi0);
-    kind(std::integral_constant<int, 1>{}, o.flat1, o.slot1, o.multi1);
+    kind(std::integral_constant<int, 0>{}, o.flat0, o.slot0, o.mslot0, o.nb0, o.multi0);
+    kind(std::integral_constant<int, 1>{}, o.flat1, o.slot1, o.mslot1, o.nb1, o.multi1);
 }
 
-// Phase 2: write node n's record(s) into the workgroup's region.
+// Phase 2, one (node, kind): the node's one-step records go to the workgroup's LDS
+// staging s1l[T * 2 * bs + slot] (step_sort_publish writes them out sorted), its
+// middle pieces straight to st.mid.
 template <int PD, int PR>
-__device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
-                                          double wsum, int32_t noprio, const StepSlots& o,
-                                          const StepTables& st, int64_t blk) {
-    constexpr int NB = PR + 2;
-    auto kind = [&](auto Tc, int32_t slot, bool multi) {
-        constexpr int T = decltype(Tc)::value;
-        if (slot < 0) return;
-        int64_t c[NB], mn, mx;
-        int cnt;
-        step_points<PD, PR, T>(r, tmin, tmax, c, cnt, mn, mx);
-        const int32_t k0 = key_of<PD, PR>(T, tmin, score_at<PD, PR>(tmin, r, wsum, noprio), r, n);
-        // key of the step starting at an expiry, evaluated at its first instant
-        if (!multi) {
-            Step1 v;
-            v.bp = mn;
-            v.k0 = k0;
-            v.k1 = key_of<PD, PR>(T, mn, score_at<PD, PR>(mn, r, wsum, noprio), r, n);
-            st.single[(int64_t)T * st.npad + blk * st.bs + slot] = v;
-        } else {  // rare: sort the expiries (equal ones give equal keys)
-#pragma unroll
-            for (int i = 0; i < NB; ++i)  // odd-even transposition sort (static indices)
-#pragma unroll
-                for (int j = i & 1; j + 1 < NB; j += 2) {
-                    const int64_t x = c[j], y = c[j + 1];
-                    c[j] = min(x, y);
-                    c[j + 1] = max(x, y);
-                }
-            VRec<NB> v;
-            v.cnt = cnt;
-            v.key[0] = k0;
-#pragma unroll
-            for (int j = 0; j < NB; ++j) {
-                v.bp[j] = c[j];  // INT64_MAX past cnt: never selected
-                v.key[j + 1] = j < cnt ? key_of<PD, PR>(T, c[j], score_at<PD, PR>(c[j], r, wsum, noprio), r, n) : -1;
-            }
-            reinterpret_cast<VRec<NB>*>(st.multi)[(int64_t)T * st.npad + blk * st.bs + slot] = v;
-        }
-    };
-    kind(std::integral_constant<int, 0>{}, o.slot0, o.multi0);
-    kind(std::integral_constant<int, 1>{}, o.slot1, o.multi1);
-}
-
-// Phase 2, one (node, kind) item with the kind at run time: the fused node pass
-// compacts its stepped items into a workgroup list (step_queue) so a few lanes
-// of one wave build every record, instead of each wave paying both kinds' and
-// both record forms' code paths whenever one of its lanes is stepped.
-template <int PD, int PR>
-__device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t n, int T, int32_t slot, bool multi,
-                                              int64_t tmin, int64_t tmax, double wsum, int32_t noprio,
-                                              const StepTables& st, int64_t blk) {
+__device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t n, int T, int32_t slot,
+                                              int32_t mslot, bool multi, int64_t tmin, int64_t tmax, double wsum,
+                                              int32_t noprio, const StepTables& st, int64_t blk, Step1* s1l) {
     constexpr int NB = PR + 2;
     int64_t c[NB];
 #pragma unroll
@@ -223,43 +192,81 @@ __device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t 
         cnt += in;
         mn = min(mn, c[j]);
     }
-    auto key = [&](int64_t t) {  // key_of for the run-time kind
+    auto key = [&](int64_t t) {  // key_of for the run-time kind, at the first instant of a step
         const int32_t f = score_at<PD, PR>(t, r, wsum, noprio);
         return (T == 1 || !(t < r.e_fail)) ? pack_key(f, n) : -1;
     };
+    Step1* s1 = s1l + T * 2 * st.bs;
     const int32_t k0 = key(tmin);
     if (!multi) {
         Step1 v;
         v.bp = mn;
         v.k0 = k0;
         v.k1 = key(mn);
-        st.single[(int64_t)T * st.npad + blk * st.bs + slot] = v;
-    } else {
-#pragma unroll
-        for (int i = 0; i < NB; ++i)  // odd-even transposition sort (static indices)
-#pragma unroll
-            for (int j = i & 1; j + 1 < NB; j += 2) {
-                const int64_t x = c[j], y = c[j + 1];
-                c[j] = min(x, y);
-                c[j + 1] = max(x, y);
-            }
-        VRec<NB> v;
-        v.cnt = cnt;
-        v.key[0] = k0;
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            v.bp[j] = c[j];
-            v.key[j + 1] = j < cnt ? key(c[j]) : -1;
-        }
-        reinterpret_cast<VRec<NB>*>(st.multi)[(int64_t)T * st.npad + blk * st.bs + slot] = v;
+        s1[slot] = v;
+        return;
     }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)  // odd-even transposition sort (static indices)
+#pragma unroll
+        for (int j = i & 1; j + 1 < NB; j += 2) {
+            const int64_t x = c[j], y = c[j + 1];
+            c[j] = min(x, y);
+            c[j + 1] = max(x, y);
+        }
+    Mid* md = st.mid + (int64_t)T * st.mpad + blk * st.mstride + mslot;
+    int32_t kprev = k0;
+    int64_t last = c[0];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        if (j >= cnt) continue;
+        const int32_t kj = key(c[j]);  // the key from c[j] on
+        if (j + 1 < cnt) {
+            Mid p;
+            p.s = c[j];
+            p.e = c[j + 1];
+            p.key = kj;
+            p.pad = 0;
+            md[j] = p;
+        }
+        last = c[j];
+        kprev = kj;
+    }
+    Step1 a, b;
+    a.bp = c[0];
+    a.k0 = k0;
+    a.k1 = -1;
+    b.bp = last;
+    b.k0 = -1;
+    b.k1 = kprev;
+    s1[slot] = a;
+    s1[slot + 1] = b;
 }
 
-// Work item of the compacted emit: owner thread | kind << 12 | multi << 13 | slot << 14.
-__device__ __forceinline__ void step_queue(const StepSlots& o, int32_t* nq, uint32_t* q) {
-    if (o.slot0 >= 0) q[atomicAdd(nq, 1)] = threadIdx.x | ((uint32_t)o.multi0 << 13) | ((uint32_t)o.slot0 << 14);
+// Phase 2 for every kind of a node (the stand-alone K3a).
+template <int PD, int PR>
+__device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
+                                          double wsum, int32_t noprio, const StepSlots& o,
+                                          const StepTables& st, int64_t blk, Step1* s1l) {
+    if (o.slot0 >= 0)
+        step_emit_one<PD, PR>(r, n, 0, o.slot0, o.mslot0, o.multi0, tmin, tmax, wsum, noprio, st, blk, s1l);
     if (o.slot1 >= 0)
-        q[atomicAdd(nq, 1)] = threadIdx.x | (1u << 12) | ((uint32_t)o.multi1 << 13) | ((uint32_t)o.slot1 << 14);
+        step_emit_one<PD, PR>(r, n, 1, o.slot1, o.mslot1, o.multi1, tmin, tmax, wsum, noprio, st, blk, s1l);
+}
+
+// Work item of the compacted emit: owner thread | kind << 12 | multi << 13 | slot << 14,
+// and its first middle-piece slot in qm.
+__device__ __forceinline__ void step_queue(const StepSlots& o, int32_t* nq, uint32_t* q, int32_t* qm) {
+    if (o.slot0 >= 0) {
+        const int i = atomicAdd(nq, 1);
+        q[i] = threadIdx.x | ((uint32_t)o.multi0 << 13) | ((uint32_t)o.slot0 << 14);
+        qm[i] = o.mslot0;
+    }
+    if (o.slot1 >= 0) {
+        const int i = atomicAdd(nq, 1);
+        q[i] = threadIdx.x | (1u << 12) | ((uint32_t)o.multi1 << 13) | ((uint32_t)o.slot1 << 14);
+        qm[i] = o.mslot1;
+    }
 }
 
 // Workgroup epilogue: the workgroup's flat-key maxima and record counts go to
@@ -284,6 +291,91 @@ __device__ __forceinline__ void step_publish(const StepSlots& o, StepShared& sh,
     } else if (threadIdx.x < 6) {
         const int L = threadIdx.x - 2;
         st.cnt[blk * 4 + L] = sh.lc[L >> 1][L & 1];
+    }
+}
+
+// After every Step1 record of the workgroup is in s1l (and a barrier): per pod kind,
+// the records sorted by step time bp go to the workgroup's region of st.single, with
+// pm1[i] = max of k1 over sorted records 0..i (the keys after their steps) and
+// sm0[i] = max of k0 over records i..n-1 (the keys before their steps).  K3s then
+// finds, per pod tile [lo, hi], the records that step inside it by binary search and
+// takes every other record's key from one prefix and one suffix maximum.
+// srt: LDS scratch [2 * BS].  Every thread calls it (barriers).
+template <int BS>
+__device__ __forceinline__ void step_sort_publish(const Step1* s1l, Step1* srt, const StepShared& sh,
+                                                  const StepTables& st, int64_t blk) {
+    constexpr int CAP = 2 * BS;  // one-step records per kind and block
+    const int n0 = sh.lc[0][0], n1 = sh.lc[1][0];
+    // rank sort (ties by slot): typically a few dozen records per kind
+    for (int i = threadIdx.x; i < n0 + n1; i += BS) {
+        const int T = i >= n0;
+        const int k = T ? i - n0 : i;
+        const int n = T ? n1 : n0;
+        const Step1* a = s1l + T * CAP;
+        const Step1 v = a[k];
+        int rank = 0;
+        for (int j = 0; j < n; ++j) {
+            const int64_t b = a[j].bp;
+            rank += (b < v.bp) || (b == v.bp && j < k);
+        }
+        srt[T * CAP + rank] = v;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n0 + n1; i += BS) {
+        const int T = i >= n0;
+        const int k = T ? i - n0 : i;
+        st.single[s1_at(st, T, blk) + k] = srt[T * CAP + k];
+    }
+    // prefix max of k1 / suffix max of k0: wave T scans kind T, CAP / 64 records per lane
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int U = CAP / 64;
+    static_assert(CAP % 64 == 0, "whole records per lane");
+    if (w < 2) {
+        const int T = w, n = T ? n1 : n0;
+        const Step1* a = srt + T * CAP;
+        int32_t k1[U], k0[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = U * lane + u;
+            k1[u] = i < n ? a[i].k1 : -1;
+            k0[u] = i < n ? a[i].k0 : -1;
+        }
+        int32_t p1 = -1, s0 = -1;  // lane totals
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            p1 = max(p1, k1[u]);
+            s0 = max(s0, k0[u]);
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {  // inclusive max scans: prefix (up), suffix (down)
+            const int32_t x = __shfl_up(p1, o), y = __shfl_down(s0, o);
+            if (lane >= o) p1 = max(p1, x);
+            if (lane + o < 64) s0 = max(s0, y);
+        }
+        int32_t run = __shfl_up(p1, 1);  // exclusive prefix of the lane totals
+        if (lane == 0) run = -1;
+        int32_t sun = __shfl_down(s0, 1);  // exclusive suffix
+        if (lane == 63) sun = -1;
+        int32_t pm[U], sm[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            run = max(run, k1[u]);
+            pm[u] = run;
+        }
+#pragma unroll
+        for (int u = U - 1; u >= 0; --u) {
+            sun = max(sun, k0[u]);
+            sm[u] = sun;
+        }
+        const int64_t base = s1_at(st, T, blk);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = U * lane + u;
+            if (i < n) {
+                st.pm1[base + i] = pm[u];
+                st.sm0[base + i] = sm[u];
+            }
+        }
     }
 }
 

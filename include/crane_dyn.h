@@ -216,8 +216,13 @@ const char *crane_dyn_version(void);
  *   "k2_form" 0 dedupe (default) | 1 binned | 2 hash   "k1_threads" 256 | 128
  *   "k1_keep_records" 0 | 1   "k1_fuse_steps" 1 | 0   "k3p_in_k2" 1 | 0
  *   "keys_path" 0 step path | 1 per-pair kernel   "greedy_form" 0 merge | 1 sequential
- *   "matrix_vec" 0 auto | 1 | 4 | 8 nodes per lane   "matrix_chunk" 0 auto | pods per workgroup (<= 1024) */
+ *   "matrix_vec" 0 auto | 1 | 4 | 8 | 16 nodes per lane   "matrix_chunk" 0 auto | pods per workgroup (<= 1024)
+ *   "trace" 0 | 1: phase stamps of the step kernels (crane_dyn_debug_trace) */
 int crane_dyn_set_option(crane_dyn *h, const char *name, int64_t value);
+/* Phase stamps of the last K2x (which = 0), K1 (1) or K3s (2) launch with option
+ * "trace" on: out[8 * workgroup + k] = s_memrealtime (100 MHz) at phase k.
+ * Returns the number of entries copied (<= max). */
+int64_t crane_dyn_debug_trace(crane_dyn *h, int32_t which, int64_t max, uint64_t *out);
 
 /* ------------------------------------------------------------------ events
  * translateEventToBinding (event.go:118-145): a Scheduled event's message

@@ -1,0 +1,80 @@
+"""Per-workgroup phase timing of the step kernels (engine option "trace").
+
+    python tools/trace_step.py [--config 3|4] [--reps 5]
+
+Every workgroup of K2x (dedupe), K1 (+K3a) and K3s stamps s_memrealtime (100 MHz,
+10 ns) at its phase boundaries; per kernel this prints the spread of workgroup
+start times, each phase's duration (median / p90 / max over workgroups) and the
+span first start -> last end, so the critical path of a launch can be read off.
+Phases:
+  K2x: 0 start | 1 bindings loaded + LDS cleared | 2 (node, bucket) aggregated | 3 counts/offsets written | 4 entries written
+  K1 : 0 start | 1 SoA + K2 entries in (LDS counts) | 2 record computed | 3 step tables published | 4 stepped records emitted
+  K3s: 0 start | 1 pods + producer counts in | 2 record rounds done | 3 uniform maxima reduced | 4 keys merged
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "crane-scheduler_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import crane_dyn as cd  # noqa: E402
+from crane_dyn import synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", type=int, default=3)
+ap.add_argument("--reps", type=int, default=5)
+args = ap.parse_args()
+dev = torch.device("cuda", 0)
+st = torch.cuda.Stream(dev)
+torch.cuda.set_stream(st)
+spec = cd.default_policy_spec()
+cfg = synth.CONFIGS[args.config]
+N, P, B = cfg["nodes"], cfg["pods"], cfg["bindings"]
+if args.config == 4:
+    N //= 8
+c = synth.make_cluster(spec, N, P, n_bindings=B, seed=20250215 + args.config * 1000)
+c.now, c.ds = synth.make_pods(P, seed=20250215 + args.config)
+eng = cd.Engine(cd.Policy(spec), 0)
+val, ts, _ = c.rows(eng.metric_names)
+eng.upload_nodes(val, ts, c.hv, c.hv_ts)
+eng.upload_bindings(c.b_node, c.b_ts)
+d_now = torch.from_numpy(c.now).to(dev)
+d_flags = torch.from_numpy(c.ds).to(dev)
+d_keys = torch.empty(P, dtype=torch.int64, device=dev)
+now = int(synth.NOW0_NS)
+for _ in range(3):
+    eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
+eng.set_option("trace", 1)
+nwg = {0: -(-B // 2048), 1: -(-N // 256)}
+res = {}
+acc = {k: [] for k in ("K2x", "K1", "K3s")}
+for r in range(args.reps):
+    eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
+    st.synchronize()
+    for which, name in ((0, "K2x"), (1, "K1"), (2, "K3s")):
+        t = eng.debug_trace(which, 65536).astype(np.int64)
+        t = t[t[:, 0] > 0]
+        acc[name].append(t)
+    eng.set_option("trace", 1)  # clears the buffer for the next rep
+out = {"config": args.config, "nodes": N, "pods": P, "bindings": B, "unit": "us"}
+for name, runs in acc.items():
+    spans, phases, starts, ends = [], {k: [] for k in range(4)}, [], []
+    for t in runs:
+        t0 = t[:, 0].min()
+        spans.append((t[:, 4].max() - t0) / 100.0)
+        starts.append((t[:, 0] - t0) / 100.0)
+        ends.append((t[:, 4] - t0) / 100.0)
+        for k in range(4):
+            phases[k].append((t[:, k + 1] - t[:, k]) / 100.0)
+    cat = lambda xs: np.concatenate(xs)  # noqa: E731
+    q = lambda x: {"med": round(float(np.median(x)), 2), "p90": round(float(np.percentile(x, 90)), 2),  # noqa: E731
+                   "max": round(float(np.max(x)), 2)}
+    out[name] = {"workgroups": int(len(runs[0])), "span": round(float(np.median(spans)), 2),
+                 "start": q(cat(starts)), "end": q(cat(ends)),
+                 "phases": {f"{k}->{k + 1}": q(cat(phases[k])) for k in range(4)}}
+print(json.dumps(out))
