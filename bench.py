@@ -456,7 +456,7 @@ def main():
                 pmc_summary("3m", shash)[0])
 
     greedy = None
-    if world == 1 and not args.no_greedy:
+    if world == 1 and not args.no_greedy and not args.no_extras:
         # BASELINE config 5: 100k nodes x 50k pods placed sequentially, each binding
         # raising the chosen node's hot value before the next pod (one GPU).
         g5 = synth.CONFIGS[5]
@@ -481,7 +481,8 @@ def main():
 
     cpu = None
     host_parse = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 3:
+        # (the headline configuration only: config 4's 1M-node annotation strings alone take minutes to build)
         from oracle import oracle as O
         ann = c.annotations()
         ncpu = effective_cpus()

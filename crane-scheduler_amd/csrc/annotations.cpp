@@ -223,12 +223,12 @@ bool crane_go_parse_time(const char* s, size_t n, int64_t tz_offset_s, int64_t* 
         if (ok) {
             const int year = d2(0) * 100 + d2(2), mon = d2(5), day = d2(8), hour = d2(11), min = d2(14),
                       sec = d2(17);
-            if (mon < 1 || mon > 12 || hour > 23 || min > 59 || sec > 59) return false;
+            if (mon < 1 || mon > 12 || day < 1 || day > 31 || hour > 23 || min > 59 || sec > 59) return false;
             thread_local int memo_key = -1;
             thread_local int64_t memo_days = 0;
-            const int key = (year * 16 + mon) * 32 + day;
+            const int key = (year * 16 + mon) * 32 + day;  // one key per (year, mon, day): day <= 31
             if (key != memo_key) {
-                if (day < 1 || day > month_days(mon, year)) return false;
+                if (day > month_days(mon, year)) return false;
                 memo_days = civil_days(year, mon, day);
                 memo_key = key;
             }

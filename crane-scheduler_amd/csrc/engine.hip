@@ -101,6 +101,8 @@ struct Options {
     int greedy_form = 0;      // 0: merge form when every hotValue count > 0, 1: sequential kernel
     int matrix_vec = 0;       // K3m nodes per lane: 0 automatic, 1 / 4 / 8 / 16
     int matrix_chunk = 0;     // K3m pods per workgroup: 0 automatic
+    int step_rows = 1;        // 1: producers write per-tile record ranges for K3s, 0: K3s searches
+    int k3s_blocks = 0;       // K3s producer blocks per workgroup aimed for: 0 automatic
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
@@ -173,6 +175,7 @@ struct crane_dyn {
     DevBuf<Mid> smid;
     DevBuf<Step1> sstep1;
     DevBuf<int32_t> spm1, ssm0;   // prefix / suffix key maxima of the sorted Step1 records
+    DevBuf<int4> srows;           // per (pod tile, producer block): uniform keys + record ranges
     // kernel timing (crane_dyn_set_profiling)
     bool prof = false;
     EngineTimer timer;
@@ -423,10 +426,10 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     sp.fuse = h->rec_dirty && h->opt.k1_fuse;
     const int32_t bs = sp.fuse ? k1_bs(h) : kStepSeg;  // producer workgroup size
     const int32_t nblk = (int32_t)((h->N + bs - 1) / bs);
-    sp.g = step_geometry(P, h->N, nblk);
+    sp.g = step_geometry(P, h->N, nblk, h->opt.k3s_blocks);
     const StepGeometry& g = sp.g;
     HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
-    HIPTRY(h, h->stile.reserve((size_t)(2 * g.ntiles)));
+    HIPTRY(h, h->stile.reserve((size_t)(kTileStat * g.ntiles)));
     HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
     HIPTRY(h, h->scnt.reserve((size_t)std::max<int32_t>(nblk, 1) * 6));  // cnt [nblk][4] + flat [nblk][2]
     // per kind and producer block: 2 * bs one-step records, bs * (breakpoints - 1) middle pieces
@@ -449,6 +452,13 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     t.bs = bs;
     t.nblk = nblk;
     t.mstride = (int32_t)mstride;
+    t.ntiles = (int32_t)g.ntiles;
+    t.tiles = h->stile.p;
+    const int64_t nrows = g.ntiles * (int64_t)nblk;
+    if (h->opt.step_rows && nrows <= kStepRowsMax) {
+        HIPTRY(h, h->srows.reserve((size_t)std::max<int64_t>(nrows, 1)));
+        t.rows = h->srows.p;
+    }
     t.trace = g.ngroups * g.R <= kTraceWgs ? h->trace_region(2) : nullptr;
     return CRANE_OK;
 }
@@ -472,7 +482,7 @@ static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_k
         }
         HIPTRY(h, launch_step_nodes(h->shape, h->rec.p, h->N, h->dp.wsum, h->dp.noprio, sp.stt, sp.g, h->stile.p, st));
     }
-    HIPTRY(h, launch_step_pairs(h->shape, h->N, h->node_offset, P, d_keys, sp.stt, sp.g, h->sperm.p, h->spnow.p, st));
+    HIPTRY(h, launch_step_pairs(h->shape, h->N, h->node_offset, P, d_keys, sp.stt, sp.g, h->sperm.p, h->spnow.p, h->stile.p, st));
     return CRANE_OK;
 }
 
@@ -588,7 +598,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->mFs.release(); h->mIs.release(); h->mgi.release();
     h->trace.release();
     h->sperm.release(); h->scnt.release(); h->stile.release(); h->spnow.release(); h->smid.release(); h->sstep1.release();
-    h->spm1.release(); h->ssm0.release();
+    h->spm1.release(); h->ssm0.release(); h->srows.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -618,6 +628,8 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "greedy_form" && range(0, 1)) o.greedy_form = (int)value;
     else if (n == "matrix_vec" && (value == 0 || value == 1 || value == 4 || value == 8 || value == 16)) o.matrix_vec = (int)value;
     else if (n == "matrix_chunk" && range(0, 1024)) o.matrix_chunk = (int)value;
+    else if (n == "step_rows" && range(0, 1)) o.step_rows = (int)value;
+    else if (n == "k3s_blocks" && range(0, 256)) o.k3s_blocks = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
         if (o.trace) {

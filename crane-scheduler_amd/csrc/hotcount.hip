@@ -22,6 +22,8 @@
 // Order inside a bin is not deterministic; counts are.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "dyn_types.hpp"
 #include "kernels.hpp"
 #include "pods.hpp"
@@ -322,7 +324,10 @@ __global__ __launch_bounds__(kDT) void k2x_dedupe_pods(const int32_t* __restrict
                                                        HotCutoffs cut, HotPart g, uint32_t* __restrict__ CO,
                                                        uint32_t* __restrict__ region, PodPrep pp) {
     if ((int32_t)blockIdx.x < g.nblk) k2d_body<kDT>((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
-    else k3p_tile<kDT>((int64_t)blockIdx.x - g.nblk, pp);
+    else {
+        extern __shared__ __attribute__((aligned(16))) unsigned char k3p_lds[];
+        k3p_tile<kDT>((int64_t)blockIdx.x - g.nblk, pp, k3p_lds);
+    }
 }
 
 HotPart hot_dedupe_geometry(int64_t B, int64_t N, int32_t W, int32_t bs) {
@@ -353,7 +358,8 @@ hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int
     if (attr != hipSuccess) return attr;
     uint32_t* region = scratch;
     uint32_t* CO = scratch + g.cap;  // [nblk][nbins]
-    const size_t lds = sizeof(uint32_t) * (2 * (size_t)kDSlots + 2 * (size_t)g.nbins) + sizeof(uint16_t) * kXChunk;
+    size_t lds = sizeof(uint32_t) * (2 * (size_t)kDSlots + 2 * (size_t)g.nbins) + sizeof(uint16_t) * kXChunk;
+    if (pods && pods->P > 0) lds = std::max(lds, kK3pLds);
     if (pods && pods->P > 0)
         return klaunch("k2x_dedupe+k3p_pods", k2x_dedupe_pods, dim3((unsigned)(g.nblk + pods->ntiles)), dim3(kDT), lds,
                        st, bnode, bts, B, N, cut, g, CO, region, *pods);

@@ -244,7 +244,11 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     }
     CRANE_TSTAMP(a.trace, blockIdx.x, 1);
     // the batch time range partials: issued after the SoA loads, reduced after the compute
-    if (STEP) batch_range_load<kK1Threads>(step.tile_mm, step.ntiles, pmn, pmx);
+    int64_t tpre = 0;  // this thread's first tile-row bound (step_tile_rows)
+    if (STEP) {
+        batch_range_load<kK1Threads>(step.tile_mm, step.ntiles, pmn, pmx);
+        if (step.st.rows) tile_prefetch(step.st, &tpre);
+    }
     if (n < N) {
 #pragma unroll
         for (int k = 0; k < PD; ++k) {
@@ -337,7 +341,10 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
                                   ((it >> 13) & 1) != 0, tmin, tmax, step.wsum, step.noprio, step.st, blk, s1l);
         }
         __syncthreads();
+        CRANE_TSTAMP(a.trace, blockIdx.x, 5);
         step_sort_publish<kK1Threads>(s1l, s1s, ssh, step.st, blk);
+        CRANE_TSTAMP(a.trace, blockIdx.x, 6);
+        if (step.st.rows) step_tile_rows<kK1Threads>(s1l, s1s, ssh, step.st, blk, &tpre);
     } else {
         __syncthreads();
     }

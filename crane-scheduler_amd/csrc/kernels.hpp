@@ -34,9 +34,13 @@ inline hipError_t klaunch(const char* name, void (*kernel)(KArgs...), dim3 grid,
 // Phase trace (engine option "trace", crane_dyn_debug_trace): when non-null, thread 0
 // of every workgroup stores s_memrealtime stamps (100 MHz) at the kernel's phase
 // boundaries into trace[8 * workgroup + k].
-#define CRANE_TSTAMP(tr, wg, k)                                                        \
-    do {                                                                               \
-        if ((tr) && threadIdx.x == 0) (tr)[8 * (int64_t)(wg) + (k)] = __builtin_amdgcn_s_memrealtime(); \
+// (stamp 0 also records the workgroup's XCD in slot 7: HW_REG_XCC_ID, hwreg id 20)
+#define CRANE_TSTAMP(tr, wg, k)                                                                      \
+    do {                                                                                             \
+        if ((tr) && threadIdx.x == 0) {                                                              \
+            (tr)[8 * (int64_t)(wg) + (k)] = __builtin_amdgcn_s_memrealtime();                        \
+            if ((k) == 0) (tr)[8 * (int64_t)(wg) + 7] = (unsigned)__builtin_amdgcn_s_getreg(63508) & 15u; \
+        }                                                                                            \
     } while (0)
 
 struct HotCutoffs {
@@ -135,7 +139,8 @@ struct HotPart {
     bool ok;
     unsigned long long* trace;  // phase trace or null
 };
-// The step path's pod preparation (K3p) for 1024-pod tiles, as it rides in K2x's launch.
+// The step path's pod preparation (K3p, pods.hpp) for 1024-pod tiles.
+constexpr int kTileStat = 8;  // int64 per tile: min/max now per kind, pods per kind, pad
 struct PodPrep {
     const int64_t* now;
     const uint8_t* flags;
@@ -184,9 +189,15 @@ struct StepTables {
     int32_t bs;      // nodes per producer workgroup
     int32_t nblk;    // producer workgroups
     int32_t mstride; // middle pieces per block region (bs * (breakpoints per node - 1))
-    int32_t pad;
+    int32_t ntiles;  // pod tiles of the batch (K3p)
+    const int64_t* tiles;  // K3p's tile stats (kTileStat per tile)
+    // per (pod tile t, block b) at rows[t * nblk + b], or null (K3s searches itself):
+    // {uniform key kind 0, kind 1, jl0 | jh0 << 16, jl1 | jh1 << 16}; [jl, jh) = the
+    // block's sorted one-step records stepping inside the tile's range of that kind
+    int4* rows;
     unsigned long long* trace;  // K3s phase trace or null
 };
+constexpr int64_t kStepRowsMax = 1LL << 24;  // tile x block rows (256 MiB); larger batches: K3s searches
 __host__ __device__ inline int64_t s1_at(const StepTables& st, int T, int64_t b) {
     return T * st.s1pad + b * 2 * st.bs;
 }
@@ -196,8 +207,8 @@ struct StepGeometry {
 };
 constexpr int kK3sMaxBlk = 256;  // producer blocks per K3s workgroup (one lane each)
 int step_breakpoints(int shape);  // in-range expiries per node and kind at most: PR + 2
-StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk);
-// K3p: perm, pnow [ntiles * 1024], tile_mm [2 * ntiles]; initialises keys[0..P) to -1
+StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk, int32_t blk_per_wg = 0);
+// K3p: perm, pnow [ntiles * 1024], tile_mm [kTileStat * ntiles]; initialises keys[0..P) to -1
 hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys,
                             const StepGeometry& g, int32_t* perm, int64_t* pnow, int64_t* tile_mm, hipStream_t s);
 // K3a: step tables from NodeRecs in HBM (after K3p)
@@ -206,10 +217,10 @@ hipError_t launch_step_nodes(int shape, const void* rec, int64_t N, double wsum,
 // K3s: (pod, stepped node) pairs + flat maxima -> keys (after K3a or K1's STEP form)
 hipError_t launch_step_pairs(int shape, int64_t N, int64_t node_offset, int64_t P, long long* keys,
                              const StepTables& st, const StepGeometry& g, const int32_t* perm, const int64_t* pnow,
-                             hipStream_t s);
+                             const int64_t* tile_mm, hipStream_t s);
 // K1's fused step form: the node pass also builds the step tables of a pod batch
 struct K1Step {
-    const int64_t* tile_mm;  // K3p's per-tile time range
+    const int64_t* tile_mm;  // K3p's per-tile stats (kTileStat)
     int32_t ntiles;
     int32_t noprio;
     double wsum;

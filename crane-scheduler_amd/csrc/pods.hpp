@@ -1,9 +1,14 @@
-// pods.hpp — K3p's pod-batch preparation for one 1024-pod tile, with a
-// 256-thread workgroup (4 pods per lane), so it can share a launch with K2x
-// (hotcount.hip).  Same outputs as k3p_pods (step.hip): keys[p] = -1; the
-// tile's pods partitioned non-DaemonSet first, each kind in ascending pod
-// order (perm: pod index, bit 31 = DaemonSet; pnow: its time); tile_mm = the
-// tile's min/max of now.
+// pods.hpp — K3p: the step path's pod-batch preparation for one 1024-pod tile,
+// with a kT-thread workgroup, so it can run stand-alone (k3p_pods, step.hip,
+// kT = 1024) or ride in K2x's launch (hotcount.hip).  Outputs: keys[p] = -1;
+// the tile's pods sorted by (kind, now, pod) — non-DaemonSet pods first — as
+// perm (pod index, bit 31 = DaemonSet) and pnow (its time); the tile's stats
+// row tile_mm[kTileStat * t + i]: i = 0/1 min/max now of kind 0, 2/3 of kind 1
+// (INT64_MAX / INT64_MIN for a kind without pods), 4/5 pod counts per kind.
+// A tile whose times already ascend in pod order is sorted by a stable kind
+// partition; any other by a bitonic sort in LDS.  K3s relies on the sort: the
+// pods of one kind that a step record or a middle piece selects in a tile are
+// a contiguous slot range.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -13,82 +18,121 @@
 
 namespace crane {
 
+constexpr size_t kK3pLds = 1024 * (sizeof(uint64_t) + sizeof(uint32_t));  // sort keys + tags
+
+// lexicographic (class, time, slot): class and slot live in the tag (class << 30 | slot)
+__device__ __forceinline__ bool pod_gt(uint64_t ka, uint32_t va, uint64_t kb, uint32_t vb) {
+    return (va >> 30) != (vb >> 30) ? va > vb : (ka != kb ? ka > kb : va > vb);
+}
+
 template <int kT>
-__device__ __forceinline__ void k3p_tile(const int64_t t, const PodPrep& pp) {
+__device__ __forceinline__ void k3p_tile(const int64_t t, const PodPrep& pp, unsigned char* lds) {
     static_assert(1024 % kT == 0 && kT >= 64, "a tile is 1024 pods");
     constexpr int kU = 1024 / kT, kG = kU * (kT / 64);  // pods per lane, (u, wave) groups
-    __shared__ int32_t cn[kG], cd[kG];
-    __shared__ int64_t wmn[kT / 64], wmx[kT / 64];
+    constexpr uint64_t kSign = 1ull << 63;
+    __shared__ int32_t gcn[kG], gcd[kG];
+    uint64_t* ku = reinterpret_cast<uint64_t*>(lds);            // now ^ sign: unsigned order = signed order
+    uint32_t* kv = reinterpret_cast<uint32_t*>(lds + 8 * 1024);  // class (0 pod, 1 DaemonSet, 2 none) << 30 | slot
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t lt = (1ull << lane) - 1ull;
+    const int64_t pend = min(pp.P, (t + 1) * 1024);
+    bool live[kU], ds[kU], inorder = true;
     int64_t tn[kU];
-    bool live[kU], ds[kU];
-    int64_t mn = INT64_MAX, mx = INT64_MIN;
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-        const int64_t p = t * 1024 + u * kT + threadIdx.x;  // pod order = (u, wave, lane)
-        live[u] = p < pp.P;
+        const int64_t p = t * 1024 + u * kT + threadIdx.x;  // natural order = (u, wave, lane)
+        live[u] = p < pend;
         ds[u] = live[u] && pp.flags && (pp.flags[p] & 1u);
         tn[u] = live[u] ? pp.now[p] : 0;
+        if (p + 1 < pend) inorder &= tn[u] <= pp.now[p + 1];
+        if (live[u]) pp.keys[p] = -1;
     }
-    uint64_t mnm[kU], mdm[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-        const int64_t p = t * 1024 + u * kT + threadIdx.x;
-        if (live[u]) {
-            pp.keys[p] = -1;
-            mn = min(mn, tn[u]);
-            mx = max(mx, tn[u]);
-        }
-        mnm[u] = __ballot(live[u] && !ds[u]);
-        mdm[u] = __ballot(ds[u]);
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        mn = min(mn, (int64_t)__shfl_xor((long long)mn, o));
-        mx = max(mx, (int64_t)__shfl_xor((long long)mx, o));
-    }
-    if (lane == 0) {
+    if (__syncthreads_and(inorder)) {
+        // times already ascending (a queue drained in order): a stable kind partition sorts the tile
+        uint64_t mnm[kU], mdm[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            cn[u * (kT / 64) + w] = __popcll(mnm[u]);
-            cd[u * (kT / 64) + w] = __popcll(mdm[u]);
+            mnm[u] = __ballot(live[u] && !ds[u]);
+            mdm[u] = __ballot(ds[u]);
+            if (lane == 0) {
+                gcn[u * (kT / 64) + w] = __popcll(mnm[u]);
+                gcd[u * (kT / 64) + w] = __popcll(mdm[u]);
+            }
         }
-        wmn[w] = mn;
-        wmx[w] = mx;
-    }
-    __syncthreads();
-    int32_t tot_n = 0;
+        __syncthreads();
+        int32_t tot_n = 0;
 #pragma unroll
-    for (int i = 0; i < kG; ++i) tot_n += cn[i];
+        for (int i = 0; i < kG; ++i) tot_n += gcn[i];
+        const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int gi = u * (kT / 64) + w, i = u * kT + threadIdx.x;
+            int32_t pre_n = 0, pre_d = 0;
+            for (int k = 0; k < gi; ++k) {
+                pre_n += gcn[k];
+                pre_d += gcd[k];
+            }
+            const int pos = !live[u] ? i
+                            : ds[u]  ? tot_n + pre_d + __popcll(mdm[u] & lt)
+                                     : pre_n + __popcll(mnm[u] & lt);
+            ku[pos] = live[u] ? (uint64_t)tn[u] ^ kSign : ~0ull;
+            kv[pos] = ((live[u] ? (ds[u] ? 1u : 0u) : 2u) << 30) | (uint32_t)i;
+        }
+        __syncthreads();
+    } else {
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int i = u * kT + threadIdx.x;
+            ku[i] = live[u] ? (uint64_t)tn[u] ^ kSign : ~0ull;
+            kv[i] = ((live[u] ? (ds[u] ? 1u : 0u) : 2u) << 30) | (uint32_t)i;
+        }
+        __syncthreads();
+        // bitonic sort of the 1024 (key, tag) pairs in LDS: 55 compare-exchange passes
+        for (int k = 2; k <= 1024; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int q = threadIdx.x; q < 512; q += kT) {
+                    const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1)), l = i | j;
+                    const uint64_t ka = ku[i], kb = ku[l];
+                    const uint32_t va = kv[i], vb = kv[l];
+                    if (pod_gt(ka, va, kb, vb) == ((i & k) == 0)) {
+                        ku[i] = kb;
+                        ku[l] = ka;
+                        kv[i] = vb;
+                        kv[l] = va;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-        const int gi = u * (kT / 64) + w;
-        int32_t pre_n = 0, pre_d = 0;
-        for (int i = 0; i < gi; ++i) {
-            pre_n += cn[i];
-            pre_d += cd[i];
-        }
-        if (live[u]) {
-            const int64_t p = t * 1024 + u * kT + threadIdx.x;
-            const int32_t pos =
-                ds[u] ? tot_n + pre_d + __popcll(mdm[u] & lt) : pre_n + __popcll(mnm[u] & lt);
-            pp.perm[t * 1024 + pos] = (int32_t)p | (ds[u] ? (int32_t)0x80000000 : 0);  // bit 31: DaemonSet
-            pp.pnow[t * 1024 + pos] = tn[u];
+        const int i = u * kT + threadIdx.x;
+        const uint32_t v = kv[i];
+        if ((v >> 30) < 2u) {
+            pp.perm[t * 1024 + i] = (int32_t)(t * 1024 + (v & 1023u)) | ((v >> 30) ? (int32_t)0x80000000 : 0);
+            pp.pnow[t * 1024 + i] = (int64_t)(ku[i] ^ kSign);
         }
     }
     if (threadIdx.x == 0) {
-        int64_t a = INT64_MAX, b = INT64_MIN;
-#pragma unroll
-        for (int i = 0; i < kT / 64; ++i) {
-            a = min(a, wmn[i]);
-            b = max(b, wmx[i]);
-        }
-        pp.tile_mm[2 * t] = a;
-        pp.tile_mm[2 * t + 1] = b;
+        // kind boundaries: first slot of class >= 1 and of class 2
+        auto first_class = [&](uint32_t c) {
+            int lo = 0, hi = 1024;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if ((kv[mid] >> 30) < c) lo = mid + 1;
+                else hi = mid;
+            }
+            return lo;
+        };
+        const int e0 = first_class(1), e1 = first_class(2);
+        int64_t* ts = pp.tile_mm + kTileStat * t;
+        ts[0] = e0 > 0 ? (int64_t)(ku[0] ^ kSign) : INT64_MAX;
+        ts[1] = e0 > 0 ? (int64_t)(ku[e0 - 1] ^ kSign) : INT64_MIN;
+        ts[2] = e1 > e0 ? (int64_t)(ku[e0] ^ kSign) : INT64_MAX;
+        ts[3] = e1 > e0 ? (int64_t)(ku[e1 - 1] ^ kSign) : INT64_MIN;
+        ts[4] = e0;
+        ts[5] = e1 - e0;
     }
 }
-
-__device__ __forceinline__ void k3p_tile256(const int64_t t, const PodPrep& pp) { k3p_tile<256>(t, pp); }
 
 }  // namespace crane

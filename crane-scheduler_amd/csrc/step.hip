@@ -15,23 +15,26 @@
 // in K3a; K3s resolves the remaining (pod, stepped node) pairs by selecting
 // each pod's step: a 64-bit compare + select + max per pair.
 //
-//   K3p  pods  : DaemonSet partition per 1024-pod tile (so waves are uniform),
-//                key init, per-tile min/max of now, step-table header reset
+//   K3p  pods  : per 1024-pod tile, pods sorted by (kind, now) (pods.hpp),
+//                key init, per-tile time range and counts per kind
 //   K3a  nodes : per node, both pod kinds (Filter applies / DaemonSet bypass,
 //                utils.go:17-24): flat key -> workgroup max; stepped node ->
 //                its key pieces (one-step records sorted per workgroup with
 //                prefix / suffix key maxima, middle pieces), step_node.hpp
-//   K3s  pairs : a 1024-pod tile per workgroup (4 pods per lane), R workgroups
-//                per tile split the producer blocks (one lane per block):
-//                binary searches find the records stepping inside the tile's
-//                time range, one prefix and one suffix maximum give the key of
-//                all others; one 64-bit atomicMax per pod per workgroup
+//   K3s  pairs : a 1024-pod tile per workgroup, R workgroups per tile split
+//                the producer blocks: binary searches find each block's
+//                records stepping inside the tile's time range, one prefix and
+//                one suffix maximum give the key of all others; a record inside
+//                splits the tile's sorted pods of its kind into two slot ranges
+//                (a middle piece cuts out one), applied as range maxima on an
+//                LDS segment tree; one 64-bit atomicMax per pod per workgroup
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 
 #include "dyn_types.hpp"
 #include "kernels.hpp"
+#include "pods.hpp"
 #include "step_node.hpp"
 
 namespace crane {
@@ -39,56 +42,9 @@ namespace crane {
 // ---------------------------------------------------------------- K3p
 constexpr int kPodTile = 1024;
 
-__global__ __launch_bounds__(kPodTile) void k3p_pods(const int64_t* __restrict__ now,
-                                                     const uint8_t* __restrict__ flags, int64_t P,
-                                                     int32_t* __restrict__ perm, int64_t* __restrict__ pnow,
-                                                     int64_t* __restrict__ tile_mm, long long* __restrict__ keys) {
-    __shared__ int32_t cn[kPodTile / 64], cd[kPodTile / 64];
-    __shared__ int64_t wmn[kPodTile / 64], wmx[kPodTile / 64];
-    const int64_t t = blockIdx.x;
-    const int64_t p = t * kPodTile + threadIdx.x;
-    const bool live = p < P;
-    const bool ds = live && flags && (flags[p] & 1u);
-    const int64_t tn = live ? now[p] : 0;
-    if (live) keys[p] = -1;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t mn_mask = __ballot(live && !ds), md_mask = __ballot(ds);
-    const uint64_t lt = (1ull << lane) - 1ull;
-    int64_t mn = live ? tn : INT64_MAX, mx = live ? tn : INT64_MIN;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        mn = min(mn, (int64_t)__shfl_xor((long long)mn, o));
-        mx = max(mx, (int64_t)__shfl_xor((long long)mx, o));
-    }
-    if (lane == 0) {
-        cn[w] = __popcll(mn_mask);
-        cd[w] = __popcll(md_mask);
-        wmn[w] = mn;
-        wmx[w] = mx;
-    }
-    __syncthreads();
-    int32_t pre_n = 0, pre_d = 0, tot_n = 0;
-    for (int i = 0; i < kPodTile / 64; ++i) {
-        if (i < w) {
-            pre_n += cn[i];
-            pre_d += cd[i];
-        }
-        tot_n += cn[i];
-    }
-    if (live) {
-        const int32_t pos = ds ? tot_n + pre_d + __popcll(md_mask & lt) : pre_n + __popcll(mn_mask & lt);
-        perm[t * kPodTile + pos] = (int32_t)p | (ds ? (int32_t)0x80000000 : 0);  // bit 31: DaemonSet
-        pnow[t * kPodTile + pos] = tn;
-    }
-    if (threadIdx.x == 0) {
-        int64_t a = INT64_MAX, b = INT64_MIN;
-        for (int i = 0; i < kPodTile / 64; ++i) {
-            a = min(a, wmn[i]);
-            b = max(b, wmx[i]);
-        }
-        tile_mm[2 * t] = a;
-        tile_mm[2 * t + 1] = b;
-    }
+__global__ __launch_bounds__(kPodTile) void k3p_pods(PodPrep pp) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    k3p_tile<kPodTile>(blockIdx.x, pp, lds);
 }
 
 // ---------------------------------------------------------------- K3a
@@ -115,283 +71,252 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
     if (n < N && (o.slot0 >= 0 || o.slot1 >= 0)) step_emit<PD, PR>(r, n, tmin, tmax, wsum, noprio, o, st, blockIdx.x, s1l);
     __syncthreads();
     step_sort_publish<kStepSeg>(s1l, s1s, sh, st, blockIdx.x);
+    if (st.rows) {
+        int64_t pre;
+        tile_prefetch(st, &pre);
+        step_tile_rows<kStepSeg>(s1l, s1s, sh, st, blockIdx.x, &pre);
+    }
 }
 
 // ---------------------------------------------------------------- K3s
-// Workgroup = 4 waves x 64 lanes x 4 pods per lane (one 1024-pod tile of K3p's
-// partitioned order: lane l of wave w holds pods u * 256 + w * 64 + l); the R
-// workgroups of a tile split the producer blocks, one lane per block.
+// Workgroup = 4 waves, one 1024-pod tile of K3p's sorted order (thread x holds
+// slots u * 256 + x); kind 0 pods are slots [0, cn), kind 1 [cn, cn + cd),
+// each sorted by now.  The R workgroups of a tile split the producer blocks:
+// m per workgroup, LPB lanes per block (the block's leader does the searches,
+// all its lanes share the record work).
 // One-step records: each block's are sorted by step time bp with prefix maxima
 // of the after-step key (pm1) and suffix maxima of the before-step key (sm0)
-// (step_sort_publish).  For the tile's pod time range [lo, hi] (per pod kind)
-// a lane finds by two binary searches the block's records stepping inside
-// (lo, hi]; every pod of the tile sees the key after the step of each earlier
-// record (one prefix maximum) and the key before the step of each later one
-// (one suffix maximum).  The records inside are staged in LDS and every lane
-// evaluates them for its 4 pods (64-bit compare, select, max).  Middle pieces
-// [s, e) of multi-step nodes: one covering the whole range gives its key to
-// every pod of the tile, one overlapping it partly is staged and evaluated per
-// pod (s <= now < e).  One 64-bit atomicMax per pod per workgroup merges the
-// slices.
+// (step_sort_publish).  For a kind's pod time range [lo, hi] the leader finds
+// by two binary searches the records stepping inside (lo, hi]; every pod of
+// the kind sees the key after the step of each earlier record (one prefix
+// maximum) and the key before the step of each later one (one suffix maximum).
+// A record inside splits the kind's slots at the first pod with now >= bp
+// (binary search over the tile's times in LDS): k0 is a range maximum over the
+// slots before, k1 over the slots from there on.  Middle pieces [s, e) of
+// multi-step nodes: one covering [lo, hi] is uniform, one overlapping it
+// partly is the range maximum over the slots with s <= now < e.  Range maxima
+// go into a segment tree over the 1024 slots (<= 20 LDS atomics each); a pod's
+// key is the max over its leaf's ancestors, the kind's uniform maximum and
+// what the other workgroups of the tile merge: one 64-bit atomicMax per pod
+// per workgroup.
 constexpr int kK3sWaves = 4;
 constexpr int kK3sThreads = kK3sWaves * 64;
 constexpr int kK3sPPL = 4;                          // pods per lane
 constexpr int kK3sPods = kK3sThreads * kK3sPPL;     // pods per workgroup (= kPodTile)
-constexpr int kK3sS1 = 512;  // one-step records staged per round and pod kind (8 KB)
-constexpr int kK3sMP = 128;  // middle pieces staged per round and pod kind
-static_assert(kK3sMaxBlk <= kK3sThreads, "one lane per producer block");
+constexpr int kK3sBlkPerWg = 16;                    // producer blocks per workgroup, aimed for
+static_assert(kK3sMaxBlk <= kK3sThreads, "at least one lane per producer block");
+static_assert(kK3sPods == kPodTile, "a workgroup resolves one K3p tile");
 
-// number of the n sorted step times at base[] that are <= t (upper bound)
-__device__ __forceinline__ int32_t count_le(const Step1* __restrict__ base, int32_t n, int64_t t) {
-    int32_t lo = 0, hi = n;
+// The four counts "records of kind T with bp <= t" (t = the kind's lo, then hi)
+// over a block's sorted one-step records, by a k-ary search of the block's lpb
+// lanes (lanes [lead, lead + lpb) of one wave): each round every lane probes one
+// record per search and a ballot narrows the range to one of lpb + 1 parts;
+// the four searches' loads go out together.  Every lane of the team returns the
+// counts.  (n = 0 for a kind without pods here.)
+__device__ __forceinline__ void team_count_le(const Step1* __restrict__ b0, const Step1* __restrict__ b1,
+                                              const int32_t n[2], const int64_t tl[2], const int64_t th[2], int sub,
+                                              int lpb, int lead, int32_t out[4]) {
+    const uint64_t team = lpb == 64 ? ~0ull : ((1ull << lpb) - 1ull) << lead;
+    int32_t lo[4] = {0, 0, 0, 0}, hi[4] = {n[0], n[0], n[1], n[1]};
+    const int64_t t[4] = {tl[0], th[0], tl[1], th[1]};
+    while ((lo[0] < hi[0]) | (lo[1] < hi[1]) | (lo[2] < hi[2]) | (lo[3] < hi[3])) {  // team-uniform
+        bool le[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int32_t span = hi[q] - lo[q];
+            const int32_t p = lo[q] + (int32_t)((int64_t)span * (sub + 1) / (lpb + 1));  // < hi when span > 0
+            le[q] = span > 0 && (q < 2 ? b0 : b1)[p].bp <= t[q];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int32_t span = hi[q] - lo[q];
+            if (span <= 0) continue;
+            const int k = __popcll(__ballot(le[q]) & team);  // probes with bp <= t (a prefix of the team)
+            const int32_t nlo = k > 0 ? lo[q] + (int32_t)((int64_t)span * k / (lpb + 1)) + 1 : lo[q];
+            const int32_t nhi = k < lpb ? lo[q] + (int32_t)((int64_t)span * (k + 1) / (lpb + 1)) : hi[q];
+            lo[q] = nlo;
+            hi[q] = nhi;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[q] = lo[q];
+}
+
+// first slot in [lo, hi) of the sorted times tt[] with tt >= x (hi if none)
+__device__ __forceinline__ int32_t slot_lower(const int64_t* tt, int32_t lo, int32_t hi, int64_t x) {
     while (lo < hi) {
         const int32_t mid = (lo + hi) >> 1;
-        if (base[mid].bp <= t) lo = mid + 1;
+        if (tt[mid] < x) lo = mid + 1;
         else hi = mid;
     }
     return lo;
 }
 
+// key k as a range maximum over slots [a, b) of the segment tree (leaves at kK3sPods + slot)
+__device__ __forceinline__ void tree_max(int32_t* tree, int32_t a, int32_t b, int32_t k) {
+    for (int32_t l = a + kK3sPods, r = b + kK3sPods; l < r; l >>= 1, r >>= 1) {
+        if (l & 1) atomicMax(&tree[l++], k);
+        if (r & 1) atomicMax(&tree[--r], k);
+    }
+}
+
 __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int32_t* __restrict__ perm,
-                                                        const int64_t* __restrict__ pnow, int64_t P,
+                                                        const int64_t* __restrict__ pnow,
+                                                        const int64_t* __restrict__ tile_mm, int64_t P,
                                                         int64_t node_offset, int32_t R,
                                                         long long* __restrict__ keys) {
-    static_assert(kK3sWaves == 4, "per-wave partials below");
-    __shared__ int4 l1[2][kK3sS1];
-    __shared__ Mid lm[2][kK3sMP];
-    __shared__ int32_t spart[2][kK3sWaves], mpart[2][kK3sWaves];  // straddling records / pieces per wave
-    __shared__ int64_t wr[2][2][kK3sWaves];      // per kind and wave: min, max pod time
+    __shared__ int64_t tt[kK3sPods];         // the tile's pod times (sorted per kind)
+    __shared__ int32_t tree[2 * kK3sPods];   // range maxima: node i covers its leaves' slots
     __shared__ int32_t umax[2];
     const int64_t b = blockIdx.x;
     CRANE_TSTAMP(st.trace, b, 0);
     const int32_t r = (int32_t)(b % R);
     const int64_t grp = b / R;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // K3p wrote the pods in partitioned order: coalesced loads
+    const int lane = threadIdx.x & 63;
+    // the tile's kinds: time range and slot range (K3p)
+    const int64_t* ts = tile_mm + kTileStat * grp;
+    const int64_t tlo[2] = {ts[0], ts[2]}, thi[2] = {ts[1], ts[3]};
+    const int32_t cn = (int32_t)ts[4], cd = (int32_t)ts[5];
+    const int32_t klo[2] = {0, cn}, khi[2] = {cn, cn + cd};
+    // the slice's producer blocks: with R a multiple of 8, workgroup label r % 8 (= its XCD
+    // group, blockIdx % 8) takes the blocks K1 ran in the same group, b = c + 8 k, so their
+    // step tables are read from this XCD's L2; sub-slice r / 8 takes a range of k.  LPB lanes
+    // per block (a power of two <= 64).  (Placement only changes speed: the blocks covered
+    // depend on blockIdx alone.)
+    int32_t xc = 0, stride = 1, k0 = 0, m = 0;
+    if (R % 8 == 0) {
+        xc = r & 7;
+        stride = 8;
+        const int32_t S = R >> 3, s = r >> 3;
+        const int32_t nc = (st.nblk - xc + 7) >> 3, per = ((st.nblk + 7) / 8 + S - 1) / S;
+        k0 = min(nc, s * per);
+        m = min(nc, k0 + per) - k0;
+    } else {
+        const int32_t per = (st.nblk + R - 1) / R;
+        k0 = min(st.nblk, r * per);
+        m = min(st.nblk, k0 + per) - k0;
+    }
+    int32_t lpb = 64;
+    while (lpb > 1 && lpb * m > kK3sThreads) lpb >>= 1;
+    const int32_t j = threadIdx.x / lpb, sub = threadIdx.x & (lpb - 1);
+    const bool own = j < m;
+    const int64_t ob = xc + (int64_t)stride * (k0 + j);
+    const int lead = lane - sub;  // the block's leader lane (same wave)
+    // the block's team: counts (one broadcast load), the searches; the leader adds the
+    // flat maxima and the prefix / suffix maxima to the uniform keys
+    const bool any[2] = {cn > 0, cd > 0};
+    // this slice's loads first (counts, the tile rows), then the pods, so they overlap
+    int4 c = make_int4(0, 0, 0, 0);  // [records kind 0, pieces 0, records 1, pieces 1]
+    int4 row = make_int4(-1, -1, 0, 0);
+    if (own) {
+        c = reinterpret_cast<const int4*>(st.cnt)[ob];
+        if (st.rows) row = st.rows[grp * st.nblk + ob];
+    }
     bool live[kK3sPPL], ds[kK3sPPL];
     int32_t pod[kK3sPPL];
-    int64_t tnow[kK3sPPL];
 #pragma unroll
     for (int u = 0; u < kK3sPPL; ++u) {
-        const int64_t slot = grp * kK3sPods + u * kK3sThreads + threadIdx.x;
+        const int32_t i = u * kK3sThreads + threadIdx.x;
+        const int64_t slot = grp * kK3sPods + i;
         live[u] = slot < P;
         const int32_t praw = live[u] ? perm[slot] : 0;
-        tnow[u] = live[u] ? pnow[slot] : 0;
+        tt[i] = live[u] ? pnow[slot] : INT64_MAX;
         ds[u] = praw < 0;
         pod[u] = praw & 0x7FFFFFFF;
     }
-    // producer blocks [b0, b0 + m) of this slice; thread j < m owns block b0 + j
-    const int32_t per = (st.nblk + R - 1) / R;
-    const int32_t b0 = min(st.nblk, r * per), m = min(st.nblk, b0 + per) - b0;
-    const bool own = (int32_t)threadIdx.x < m;
-    const int64_t ob = b0 + threadIdx.x;
-    int32_t cnt1[2] = {0, 0}, cntm[2] = {0, 0}, flat[2] = {-1, -1};
-    if (own) {
-        const int4 c = reinterpret_cast<const int4*>(st.cnt)[ob];  // [records kind 0, pieces 0, records 1, pieces 1]
-        cnt1[0] = c.x;
-        cntm[0] = c.y;
-        cnt1[1] = c.z;
-        cntm[1] = c.w;
-        flat[0] = st.flat[ob * 2];
-        flat[1] = st.flat[ob * 2 + 1];
-    }
-    bool ln = false, ld = false;  // this lane has pods of kind 0 / 1
-#pragma unroll
-    for (int u = 0; u < kK3sPPL; ++u) {
-        ln |= live[u] && !ds[u];
-        ld |= ds[u];
-    }
-    const bool wn = __ballot(ln) != 0, wd = __ballot(ld) != 0;
-    // the workgroup's pod time range per kind
-#pragma unroll
-    for (int T = 0; T < 2; ++T) {
-        int64_t mn = INT64_MAX, mx = INT64_MIN;
-#pragma unroll
-        for (int u = 0; u < kK3sPPL; ++u) {
-            const bool mine = live[u] && (T ? ds[u] : !ds[u]);
-            mn = mine ? min(mn, tnow[u]) : mn;
-            mx = mine ? max(mx, tnow[u]) : mx;
-        }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            mn = min(mn, (int64_t)__shfl_xor((long long)mn, o));
-            mx = max(mx, (int64_t)__shfl_xor((long long)mx, o));
-        }
-        if (lane == 0) {
-            wr[T][0][w] = mn;
-            wr[T][1][w] = mx;
-        }
-    }
+    for (int i = threadIdx.x; i < 2 * kK3sPods; i += kK3sThreads) tree[i] = -1;
     if (threadIdx.x < 2) umax[threadIdx.x] = -1;
-    const bool bn = __syncthreads_or(ln), bd = __syncthreads_or(ld);  // (also orders the LDS above)
-    int64_t tlo[2], thi[2];
-#pragma unroll
-    for (int T = 0; T < 2; ++T) {
-        tlo[T] = min(min(wr[T][0][0], wr[T][0][1]), min(wr[T][0][2], wr[T][0][3]));
-        thi[T] = max(max(wr[T][1][0], wr[T][1][1]), max(wr[T][1][2], wr[T][1][3]));
-    }
-    // one-step records of the owned block: the ones stepping inside (lo, hi], and the
-    // uniform key of all others; a kind without pods here takes nothing
-    int32_t s_lo[2], s_n[2];
-    // this thread's share of the uniform maxima (a kind without pods here is never read)
-    int32_t um0 = flat[0], um1 = flat[1];
-    {
-        int32_t jl[2], jh[2];
-#pragma unroll
-        for (int T = 0; T < 2; ++T) {  // the four searches are independent chains
-            const bool any = T ? bd : bn;
-            const Step1* base = st.single + s1_at(st, T, ob);
-            const int32_t n = own && any ? cnt1[T] : 0;
-            jl[T] = count_le(base, n, tlo[T]);
-            jh[T] = count_le(base, n, thi[T]);
+    CRANE_TSTAMP(st.trace, b, 5);  // (pods in: the LDS stores waited for them)
+    const int32_t n1[2] = {any[0] ? c.x : 0, any[1] ? c.z : 0}, nm[2] = {any[0] ? c.y : 0, any[1] ? c.w : 0};
+    const Step1* base[2] = {st.single + s1_at(st, 0, ob), st.single + s1_at(st, 1, ob)};
+    int32_t jj[4] = {0, 0, 0, 0};  // jl[0], jh[0], jl[1], jh[1]
+    int32_t um[2] = {-1, -1};
+    if (st.rows) {
+        // the producer wrote this tile's uniform keys and record ranges (step_sort_publish)
+        if (own) {
+            jj[0] = row.z & 0xFFFF;
+            jj[1] = row.z >> 16;
+            jj[2] = row.w & 0xFFFF;
+            jj[3] = row.w >> 16;
+            if (sub == 0) {
+                um[0] = row.x;
+                um[1] = row.y;
+            }
         }
+    } else {
+        if (own) team_count_le(base[0], base[1], n1, tlo, thi, sub, lpb, lead, jj);
+        if (own && sub == 0) {
 #pragma unroll
-        for (int T = 0; T < 2; ++T) {
-            const int64_t base = s1_at(st, T, ob);
-            const bool any = own && (T ? bd : bn);
-            int32_t u = -1;
-            if (any && jl[T] > 0) u = st.pm1[base + jl[T] - 1];
-            if (any && jh[T] < cnt1[T]) u = max(u, st.sm0[base + jh[T]]);
-            if (T) um1 = max(um1, u);
-            else um0 = max(um0, u);
-            if (!any) flat[T] = -1;
-            s_lo[T] = jl[T];
-            s_n[T] = any ? jh[T] - jl[T] : 0;
+            for (int T = 0; T < 2; ++T) {
+                if (!any[T]) continue;
+                const int64_t o = s1_at(st, T, ob);
+                int32_t u = st.flat[ob * 2 + T];
+                if (jj[2 * T] > 0) u = max(u, st.pm1[o + jj[2 * T] - 1]);
+                if (jj[2 * T + 1] < n1[T]) u = max(u, st.sm0[o + jj[2 * T + 1]]);
+                um[T] = u;
+            }
         }
     }
-    // middle pieces of the owned block: covering [lo, hi] -> uniform key, overlapping
-    // it partly -> counted here, staged below
-    int32_t m_n[2] = {0, 0};
-#pragma unroll
-    for (int T = 0; T < 2; ++T) {
-        const bool any = own && (T ? bd : bn);
-        const Mid* mp = st.mid + (int64_t)T * st.mpad + ob * st.mstride;
-        const int32_t n = any ? cntm[T] : 0;
-        int32_t u = -1;
-        for (int32_t i = 0; i < n; ++i) {
-            const Mid p = mp[i];
-            if (p.s <= tlo[T] && p.e > thi[T]) u = max(u, p.key);
-            else m_n[T] += p.s <= thi[T] && p.e > tlo[T];
-        }
-        if (T) um1 = max(um1, u);
-        else um0 = max(um0, u);
-    }
+    __syncthreads();  // tt, tree, umax initialised
     CRANE_TSTAMP(st.trace, b, 1);
-    // exclusive prefix of the straddling counts over the owned blocks (per kind)
-    int32_t s_off[2], s_tot[2], m_off[2], m_tot[2];
-#pragma unroll
-    for (int T = 0; T < 2; ++T) {
-        int32_t x = s_n[T], y = m_n[T];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t xs = __shfl_up(x, o), ys = __shfl_up(y, o);
-            if (lane >= o) {
-                x += xs;
-                y += ys;
-            }
-        }
-        if (lane == 63) {
-            spart[T][w] = x;
-            mpart[T][w] = y;
-        }
-        s_off[T] = x - s_n[T];
-        m_off[T] = y - m_n[T];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int T = 0; T < 2; ++T) {
-        int32_t pre = 0, tot = 0, mpre = 0, mtot = 0;
-#pragma unroll
-        for (int i = 0; i < kK3sWaves; ++i) {
-            pre += i < w ? spart[T][i] : 0;
-            tot += spart[T][i];
-            mpre += i < w ? mpart[T][i] : 0;
-            mtot += mpart[T][i];
-        }
-        s_off[T] += pre;
-        s_tot[T] = tot;
-        m_off[T] += mpre;
-        m_tot[T] = mtot;
-    }
-    int32_t best_n[kK3sPPL], best_d[kK3sPPL];
-#pragma unroll
-    for (int u = 0; u < kK3sPPL; ++u) best_n[u] = best_d[u] = -1;
-    auto walk1 = [&](int T, int32_t n1, int32_t* best) {
-        int32_t i = 0;
-        for (; i + 4 <= n1; i += 4) {
-            int4 q[4];
-#pragma unroll
-            for (int v = 0; v < 4; ++v) q[v] = l1[T][i + v];  // broadcast LDS reads
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q[v].y << 32) | (uint32_t)q[v].x);
-#pragma unroll
-                for (int u = 0; u < kK3sPPL; ++u) best[u] = max(best[u], tnow[u] >= bp ? q[v].w : q[v].z);
-            }
-        }
-        for (; i < n1; ++i) {
-            const int4 q = l1[T][i];
-            const int64_t bp = (int64_t)(((uint64_t)(uint32_t)q.y << 32) | (uint32_t)q.x);
-#pragma unroll
-            for (int u = 0; u < kK3sPPL; ++u) best[u] = max(best[u], tnow[u] >= bp ? q.w : q.z);
-        }
-    };
-    // one-step records stepping inside the tile's range: rounds of kK3sS1 per kind
-    for (int32_t r0 = 0; r0 < max(s_tot[0], s_tot[1]); r0 += kK3sS1) {
-#pragma unroll
-        for (int T = 0; T < 2; ++T) {  // the owning lane copies its records of window [r0, r0 + kK3sS1)
-            const int32_t a = max(s_off[T], r0), e = min(s_off[T] + s_n[T], r0 + kK3sS1);
-            const int4* src = reinterpret_cast<const int4*>(st.single + s1_at(st, T, ob)) + s_lo[T];
-            for (int32_t g = a; g < e; ++g) l1[T][g - r0] = src[g - s_off[T]];
-        }
-        __syncthreads();
-        if (wn) walk1(0, min(kK3sS1, max(0, s_tot[0] - r0)), best_n);
-        if (wd) walk1(1, min(kK3sS1, max(0, s_tot[1] - r0)), best_d);
-        __syncthreads();
-    }
-    // middle pieces overlapping the tile's range partly: rounds of kK3sMP per kind; the
-    // owning lane re-reads its block's pieces and stages those of the window
-    auto walkm = [&](int T, int32_t n, int32_t* best) {
-        for (int32_t j = 0; j < n; ++j) {
-            const Mid p = lm[T][j];
-#pragma unroll
-            for (int u = 0; u < kK3sPPL; ++u) best[u] = max(best[u], tnow[u] >= p.s && tnow[u] < p.e ? p.key : -1);
-        }
-    };
-    for (int32_t r0 = 0; r0 < max(m_tot[0], m_tot[1]); r0 += kK3sMP) {
+    bool upd = false;  // this lane wrote the tree
+    if (own) {
 #pragma unroll
         for (int T = 0; T < 2; ++T) {
-            if (m_n[T] == 0 || m_off[T] + m_n[T] <= r0 || m_off[T] >= r0 + kK3sMP) continue;
-            const Mid* mp = st.mid + (int64_t)T * st.mpad + ob * st.mstride;
-            int32_t g = m_off[T];
-            for (int32_t i = 0; i < cntm[T]; ++i) {
-                const Mid p = mp[i];
-                if ((p.s <= tlo[T] && p.e > thi[T]) || !(p.s <= thi[T] && p.e > tlo[T])) continue;
-                if (g >= r0 && g < r0 + kK3sMP) lm[T][g - r0] = p;
-                ++g;
+            // one-step records stepping inside (lo, hi]: split the kind's slots
+            for (int32_t i = jj[2 * T] + sub; i < jj[2 * T + 1]; i += lpb) {
+                const Step1 q = base[T][i];
+                const int32_t sp = slot_lower(tt, klo[T], khi[T], q.bp);
+                if (q.k0 >= 0) tree_max(tree, klo[T], sp, q.k0);
+                if (q.k1 >= 0) tree_max(tree, sp, khi[T], q.k1);
+                upd = true;
             }
         }
-        __syncthreads();
-        if (wn) walkm(0, min(kK3sMP, max(0, m_tot[0] - r0)), best_n);
-        if (wd) walkm(1, min(kK3sMP, max(0, m_tot[1] - r0)), best_d);
-        __syncthreads();
+    }
+    CRANE_TSTAMP(st.trace, b, 6);  // (thread 0's records done)
+    if (own) {
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+            // middle pieces, 4 loads in flight per lane: covering -> uniform, overlapping partly ->
+            // range maximum over the slots with s <= now < e
+            const Mid* mp = st.mid + (int64_t)T * st.mpad + ob * st.mstride;
+            for (int32_t i0 = sub; i0 < nm[T]; i0 += 4 * lpb) {
+                Mid q[4];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int32_t i = i0 + v * lpb;
+                    if (i < nm[T]) q[v] = mp[i];
+                    else q[v].s = INT64_MAX;  // (matches nothing)
+                }
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const Mid& p = q[v];
+                    if (p.s <= tlo[T] && p.e > thi[T]) um[T] = max(um[T], p.key);
+                    else if (p.s <= thi[T] && p.e > tlo[T]) {
+                        tree_max(tree, slot_lower(tt, klo[T], khi[T], p.s), slot_lower(tt, klo[T], khi[T], p.e),
+                                 p.key);
+                        upd = true;
+                    }
+                }
+            }
+        }
     }
     CRANE_TSTAMP(st.trace, b, 2);
-    // uniform maxima (flat keys, prefix / suffix maxima, folded records): wave reduce, one LDS atomic per wave
+    // uniform maxima: wave reduce, one LDS atomic per wave
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        um0 = max(um0, __shfl_xor(um0, o));
-        um1 = max(um1, __shfl_xor(um1, o));
+    for (int T = 0; T < 2; ++T) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) um[T] = max(um[T], __shfl_xor(um[T], o));
+        if (lane == 0 && um[T] >= 0) atomicMax(&umax[T], um[T]);
     }
-    if (lane == 0) {
-        if (um0 >= 0) atomicMax(&umax[0], um0);
-        if (um1 >= 0) atomicMax(&umax[1], um1);
-    }
-    __syncthreads();
+    const bool tree_used = __syncthreads_or(upd);
     CRANE_TSTAMP(st.trace, b, 3);
 #pragma unroll
     for (int u = 0; u < kK3sPPL; ++u) {
-        const int32_t best = ds[u] ? max(best_d[u], umax[1]) : max(best_n[u], umax[0]);
+        const int32_t i = u * kK3sThreads + threadIdx.x;
+        int32_t best = umax[ds[u] ? 1 : 0];
+        if (tree_used)
+            for (int32_t x = i + kK3sPods; x >= 1; x >>= 1) best = max(best, tree[x]);
         if (live[u] && best >= 0) {
             const int64_t sc = best >> 24;
             const int64_t n = 0xFFFFFF - (best & 0xFFFFFF);
@@ -411,18 +336,27 @@ int step_breakpoints(int shape) {
     }
 }
 
-StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk) {
+StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk, int32_t blk_per_wg) {
     StepGeometry g{};
     g.nseg = (N + kStepSeg - 1) / kStepSeg;
     g.npad = g.nseg * kStepSeg;  // >= nblk * bs for bs = 128 or 256
     g.ntiles = (P + kPodTile - 1) / kPodTile;
     g.ngroups = (P + kK3sPods - 1) / kK3sPods;
-    // R workgroups per 1024-pod tile: about kTarget workgroups in all, and enough that
-    // each covers at most kK3sMaxBlk producer blocks (one lane per block)
-    constexpr int64_t kTarget = 256;
-    int64_t R = std::max<int64_t>(1, kTarget / std::max<int64_t>(g.ngroups, 1));
-    R = std::min<int64_t>(R, std::max<int32_t>(nblk, 1));
+    // R workgroups per 1024-pod tile: about kK3sBlkPerWg producer blocks each while the
+    // launch stays under kMaxWg workgroups (each slice costs an atomic per pod), and at
+    // most kK3sMaxBlk blocks each (at least one lane per block)
+    constexpr int64_t kMaxWg = 2048;
+    const int32_t bpw = blk_per_wg > 0 ? blk_per_wg : kK3sBlkPerWg;
+    int64_t R = (std::max<int32_t>(nblk, 1) + bpw - 1) / bpw;
+    R = std::min<int64_t>(R, std::max<int64_t>(1, kMaxWg / std::max<int64_t>(g.ngroups, 1)));
     R = std::max<int64_t>(R, (nblk + kK3sMaxBlk - 1) / kK3sMaxBlk);
+    if (nblk >= 8) {  // XCD groups (k3s_eval): a multiple of 8 (down while over kMaxWg workgroups),
+                      // each group's slices <= kK3sMaxBlk blocks
+        R = (R + 7) / 8 * 8;
+        if (R * g.ngroups > kMaxWg) R -= 8;
+        R = std::max<int64_t>(8, R);
+        while (((nblk + 7) / 8 + R / 8 - 1) / (R / 8) > kK3sMaxBlk) R += 8;
+    }
     g.R = (int32_t)R;
     return g;
 }
@@ -437,8 +371,8 @@ static hipError_t launch_steps_t(const void* rec, int64_t N, double wsum, int32_
 hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys,
                             const StepGeometry& g, int32_t* perm, int64_t* pnow, int64_t* tile_mm, hipStream_t s) {
     if (P <= 0) return hipSuccess;
-    return klaunch("k3p_pods", k3p_pods, dim3((unsigned)g.ntiles), dim3(kPodTile), 0, s, now, flags, P, perm, pnow,
-                   tile_mm, keys);
+    const PodPrep pp{now, flags, P, g.ntiles, perm, pnow, tile_mm, keys};
+    return klaunch("k3p_pods", k3p_pods, dim3((unsigned)g.ntiles), dim3(kPodTile), kK3pLds, s, pp);
 }
 
 hipError_t launch_step_nodes(int shape, const void* rec, int64_t N, double wsum, int32_t noprio,
@@ -454,11 +388,11 @@ hipError_t launch_step_nodes(int shape, const void* rec, int64_t N, double wsum,
 
 hipError_t launch_step_pairs(int shape, int64_t N, int64_t node_offset, int64_t P, long long* keys,
                              const StepTables& st, const StepGeometry& g, const int32_t* perm, const int64_t* pnow,
-                             hipStream_t s) {
+                             const int64_t* tile_mm, hipStream_t s) {
     (void)shape;
     if (P <= 0 || N <= 0) return hipSuccess;
     const dim3 grid((unsigned)(g.ngroups * g.R)), blk(kK3sThreads);
-    return klaunch("k3s_eval", k3s_eval, grid, blk, 0, s, st, perm, pnow, P, node_offset, g.R, keys);
+    return klaunch("k3s_eval", k3s_eval, grid, blk, 0, s, st, perm, pnow, tile_mm, P, node_offset, g.R, keys);
 }
 
 }  // namespace crane

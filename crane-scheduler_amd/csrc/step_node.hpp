@@ -64,8 +64,9 @@ __device__ __forceinline__ void batch_range_load(const int64_t* __restrict__ til
     mn = INT64_MAX;
     mx = INT64_MIN;
     for (int i = threadIdx.x; i < ntiles; i += BS) {
-        mn = min(mn, tile_mm[2 * i]);
-        mx = max(mx, tile_mm[2 * i + 1]);
+        const int64_t* ts = tile_mm + kTileStat * i;
+        mn = min(mn, min(ts[0], ts[2]));
+        mx = max(mx, max(ts[1], ts[3]));
     }
 }
 template <int BS>
@@ -294,15 +295,30 @@ __device__ __forceinline__ void step_publish(const StepSlots& o, StepShared& sh,
     }
 }
 
+// number of the n sorted records at a[] with bp <= t (upper bound)
+__device__ __forceinline__ int32_t count_le(const Step1* a, int32_t n, int64_t t) {
+    int32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (a[mid].bp <= t) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
 // After every Step1 record of the workgroup is in s1l (and a barrier): per pod kind,
 // the records sorted by step time bp go to the workgroup's region of st.single, with
 // pm1[i] = max of k1 over sorted records 0..i (the keys after their steps) and
-// sm0[i] = max of k0 over records i..n-1 (the keys before their steps).  K3s then
-// finds, per pod tile [lo, hi], the records that step inside it by binary search and
-// takes every other record's key from one prefix and one suffix maximum.
-// srt: LDS scratch [2 * BS].  Every thread calls it (barriers).
+// sm0[i] = max of k0 over records i..n-1 (the keys before their steps).  For a pod
+// tile's range [lo, hi] of a kind, the records stepping inside are [jl, jh) (jl = those
+// with bp <= lo, jh = those with bp <= hi) and every pod of it takes every other
+// record's key from one prefix and one suffix maximum: step_tile_rows writes that
+// uniform key (with the flat maximum) and [jl, jh) per tile into st.rows (when set),
+// so K3s starts from them; without rows K3s searches the records itself.
+// srt: LDS scratch [4 * BS] records; s1l is reused for the maxima.  Every thread calls
+// it (barriers); sh.fm holds the per-wave flat maxima (step_publish).
 template <int BS>
-__device__ __forceinline__ void step_sort_publish(const Step1* s1l, Step1* srt, const StepShared& sh,
+__device__ __forceinline__ void step_sort_publish(Step1* s1l, Step1* srt, const StepShared& sh,
                                                   const StepTables& st, int64_t blk) {
     constexpr int CAP = 2 * BS;  // one-step records per kind and block
     const int n0 = sh.lc[0][0], n1 = sh.lc[1][0];
@@ -314,7 +330,15 @@ __device__ __forceinline__ void step_sort_publish(const Step1* s1l, Step1* srt, 
         const Step1* a = s1l + T * CAP;
         const Step1 v = a[k];
         int rank = 0;
-        for (int j = 0; j < n; ++j) {
+        int j = 0;
+        for (; j + 8 <= n; j += 8) {  // 8 independent LDS reads in flight
+            int64_t b[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) b[u] = a[j + u].bp;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) rank += (b[u] < v.bp) || (b[u] == v.bp && j + u < k);
+        }
+        for (; j < n; ++j) {
             const int64_t b = a[j].bp;
             rank += (b < v.bp) || (b == v.bp && j < k);
         }
@@ -326,56 +350,93 @@ __device__ __forceinline__ void step_sort_publish(const Step1* s1l, Step1* srt, 
         const int k = T ? i - n0 : i;
         st.single[s1_at(st, T, blk) + k] = srt[T * CAP + k];
     }
-    // prefix max of k1 / suffix max of k0: wave T scans kind T, CAP / 64 records per lane
+    // prefix max of k1 / suffix max of k0: wave T scans kind T in chunks of 64 consecutive
+    // records (one per lane) with a carry; also kept in LDS (s1l is free now) for the rows
+    int32_t* pmL = reinterpret_cast<int32_t*>(s1l);  // [2][CAP]
+    int32_t* smL = pmL + 2 * CAP;                     // [2][CAP]
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    constexpr int U = CAP / 64;
-    static_assert(CAP % 64 == 0, "whole records per lane");
     if (w < 2) {
         const int T = w, n = T ? n1 : n0;
         const Step1* a = srt + T * CAP;
-        int32_t k1[U], k0[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = U * lane + u;
-            k1[u] = i < n ? a[i].k1 : -1;
-            k0[u] = i < n ? a[i].k0 : -1;
-        }
-        int32_t p1 = -1, s0 = -1;  // lane totals
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            p1 = max(p1, k1[u]);
-            s0 = max(s0, k0[u]);
-        }
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {  // inclusive max scans: prefix (up), suffix (down)
-            const int32_t x = __shfl_up(p1, o), y = __shfl_down(s0, o);
-            if (lane >= o) p1 = max(p1, x);
-            if (lane + o < 64) s0 = max(s0, y);
-        }
-        int32_t run = __shfl_up(p1, 1);  // exclusive prefix of the lane totals
-        if (lane == 0) run = -1;
-        int32_t sun = __shfl_down(s0, 1);  // exclusive suffix
-        if (lane == 63) sun = -1;
-        int32_t pm[U], sm[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            run = max(run, k1[u]);
-            pm[u] = run;
-        }
-#pragma unroll
-        for (int u = U - 1; u >= 0; --u) {
-            sun = max(sun, k0[u]);
-            sm[u] = sun;
-        }
         const int64_t base = s1_at(st, T, blk);
+        int32_t carry = -1;
+        for (int c0 = 0; c0 < n; c0 += 64) {
+            const int i = c0 + lane;
+            int32_t v = i < n ? a[i].k1 : -1;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = U * lane + u;
-            if (i < n) {
-                st.pm1[base + i] = pm[u];
-                st.sm0[base + i] = sm[u];
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t x = __shfl_up(v, o);
+                if (lane >= o) v = max(v, x);
             }
+            v = max(v, carry);
+            if (i < n) {
+                st.pm1[base + i] = v;
+                pmL[T * CAP + i] = v;
+            }
+            carry = __shfl(v, 63);
         }
+        carry = -1;
+        for (int c0 = (n - 1) & ~63; c0 >= 0 && n > 0; c0 -= 64) {
+            const int i = c0 + lane;
+            int32_t v = i < n ? a[i].k0 : -1;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t y = __shfl_down(v, o);
+                if (lane + o < 64) v = max(v, y);
+            }
+            v = max(v, carry);
+            if (i < n) {
+                st.sm0[base + i] = v;
+                smL[T * CAP + i] = v;
+            }
+            carry = __shfl(v, 0);
+        }
+    }
+}
+
+// The tile rows (st.rows set): per pod tile t, the block's uniform key per kind and
+// the range [jl, jh) of its sorted one-step records stepping inside the tile's range
+// (after step_sort_publish: srt sorted, s1l holding the prefix / suffix maxima).
+// pre: this thread's first item's bound (tile_prefetch, loaded early).  Every thread
+// calls it (barrier).
+__device__ __forceinline__ void tile_prefetch(const StepTables& st, int64_t* pre) {
+    const int x = threadIdx.x;  // item x: tile x / 4, kind (x / 2) % 2, lo / hi
+    *pre = (x >> 2) < st.ntiles ? st.tiles[kTileStat * (x >> 2) + ((x >> 1) & 1) * 2 + (x & 1)] : 0;
+}
+template <int BS>
+__device__ __forceinline__ void step_tile_rows(const Step1* s1l, const Step1* srt, const StepShared& sh,
+                                               const StepTables& st, int64_t blk, const int64_t* pre) {
+    constexpr int CAP = 2 * BS;
+    const int n0 = sh.lc[0][0], n1 = sh.lc[1][0];
+    const int32_t* pmL = reinterpret_cast<const int32_t*>(s1l);
+    const int32_t* smL = pmL + 2 * CAP;
+    __syncthreads();
+    int32_t fl[2];  // the block's flat maxima
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+        fl[T] = sh.fm[T][0];
+#pragma unroll
+        for (int i = 1; i < BS / 64; ++i) fl[T] = max(fl[T], sh.fm[T][i]);
+    }
+    // item i: tile i / 4, kind (i / 2) % 2, bound i % 2 (lo, hi): one LDS search each, the
+    // four items of a tile on adjacent lanes combine by shuffles
+    for (int i0 = 0; i0 < 4 * st.ntiles; i0 += BS) {
+        const int i = i0 + threadIdx.x;
+        const int t = i >> 2, T = (i >> 1) & 1, hi_b = i & 1;
+        const int n = T ? n1 : n0;
+        int32_t c = 0, u = -1;
+        if (t < st.ntiles) {
+            const int64_t v = i0 == 0 ? *pre : st.tiles[kTileStat * t + 2 * T + hi_b];
+            c = count_le(srt + T * CAP, n, v);
+            if (!hi_b && c > 0) u = pmL[T * CAP + c - 1];  // records stepped by lo: keys after
+            if (hi_b && c < n) u = smL[T * CAP + c];       // records stepping after hi: keys before
+        }
+        const int32_t co = __shfl_xor(c, 1), uo = __shfl_xor(u, 1);
+        const int32_t jl = hi_b ? co : c, jh = hi_b ? c : co;
+        // a kind without pods here (lo = INT64_MAX, hi = INT64_MIN) gives jl = n > jh = 0
+        const int32_t um = jl > jh ? -1 : max(fl[T], max(u, uo)), jp = jl > jh ? 0 : (jl | (jh << 16));
+        const int32_t um1 = __shfl_down(um, 2), jp1 = __shfl_down(jp, 2);
+        if ((i & 3) == 0 && t < st.ntiles) st.rows[(int64_t)t * st.nblk + blk] = make_int4(um, um1, jp, jp1);
     }
 }
 

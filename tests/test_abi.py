@@ -141,6 +141,10 @@ def test_parse_time_fixed_layout_matches_oracle():
             s = s[:i] + chr(int(rng.integers(32, 127))) + s[i + 1:]
         strs.append("0.5," + s)
     strs += ["0.5,2024-02-29T00:00:00Z", "0.5,2023-02-29T00:00:00Z", "0.5,2023-02-28T23:59:59Z"] * 3
+    # the memo key of an out-of-range day must not alias the next month's day 1 .. 3:
+    # (2026, 1, 33) once keyed like (2026, 2, 1)
+    strs += ["0.5,2026-02-01T00:00:00Z", "0.5,2026-01-33T00:00:00Z", "0.5,2026-01-32T00:00:00Z",
+             "0.5,2026-03-02T00:00:00Z", "0.5,2026-02-34T00:00:00Z", "0.5,2026-01-00T00:00:00Z"]
     nodes = [{"m": s} for s in strs]
     val, ts, _, _ = cd.parse_nodes(["m"], nodes, 8 * 3600, threads=1)
     for n, s in enumerate(strs):

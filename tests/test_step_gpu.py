@@ -21,14 +21,16 @@ from crane_dyn import synth  # noqa: E402
 
 
 def _check(spec, c, now, ds):
-    eng = engine_for(spec, c)
-    _, _, ch, cs = eng.eval(now, ds)
     off, osc, och = oracle_soa(spec, c, now=now, ds=ds)
-    assert np.array_equal(ch, och)
-    for p in range(len(now)):
-        ok = (off[p] < 0) | bool(ds[p])
-        assert cs[p] == (osc[p][ok].max() if ok.any() else -1), p
-    eng.close()
+    # K3s from the producers' per-tile rows, and searching the records itself
+    for rows in (1, 0):
+        eng = engine_for(spec, c, opts={"step_rows": rows})
+        _, _, ch, cs = eng.eval(now, ds)
+        assert np.array_equal(ch, och), rows
+        for p in range(len(now)):
+            ok = (off[p] < 0) | bool(ds[p])
+            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, p)
+        eng.close()
 
 
 @pytest.mark.parametrize("n_nodes,n_pods,step_ns,ds_frac,seed", [

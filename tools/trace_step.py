@@ -28,6 +28,7 @@ from crane_dyn import synth  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=3)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--opt", action="append", default=[], help="engine option name=value (repeatable)")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 st = torch.cuda.Stream(dev)
@@ -40,6 +41,9 @@ if args.config == 4:
 c = synth.make_cluster(spec, N, P, n_bindings=B, seed=20250215 + args.config * 1000)
 c.now, c.ds = synth.make_pods(P, seed=20250215 + args.config)
 eng = cd.Engine(cd.Policy(spec), 0)
+for o in args.opt:
+    k, v = o.split("=")
+    eng.set_option(k, int(v))
 val, ts, _ = c.rows(eng.metric_names)
 eng.upload_nodes(val, ts, c.hv, c.hv_ts)
 eng.upload_bindings(c.b_node, c.b_ts)
@@ -52,14 +56,21 @@ for _ in range(3):
 eng.set_option("trace", 1)
 nwg = {0: -(-B // 2048), 1: -(-N // 256)}
 res = {}
+xcd = {}
 acc = {k: [] for k in ("K2x", "K1", "K3s")}
 for r in range(args.reps):
     eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
     st.synchronize()
     for which, name in ((0, "K2x"), (1, "K1"), (2, "K3s")):
         t = eng.debug_trace(which, 65536).astype(np.int64)
-        t = t[t[:, 0] > 0]
+        wg = np.nonzero(t[:, 0] > 0)[0]
+        t = t[wg]
         acc[name].append(t)
+        # workgroup -> XCD placement: the XCD of each label (workgroup id % 8), as observed
+        lab = {}
+        for w, x in zip(wg % 8, t[:, 7]):
+            lab.setdefault(int(w), set()).add(int(x))
+        xcd.setdefault(name, []).append({k: sorted(v) for k, v in sorted(lab.items())})
     eng.set_option("trace", 1)  # clears the buffer for the next rep
 out = {"config": args.config, "nodes": N, "pods": P, "bindings": B, "unit": "us"}
 for name, runs in acc.items():
@@ -77,4 +88,10 @@ for name, runs in acc.items():
     out[name] = {"workgroups": int(len(runs[0])), "span": round(float(np.median(spans)), 2),
                  "start": q(cat(starts)), "end": q(cat(ends)),
                  "phases": {f"{k}->{k + 1}": q(cat(phases[k])) for k in range(4)}}
+    subs = {"K3s": {"0->5": (0, 5), "5->1": (5, 1), "1->6": (1, 6), "6->2": (6, 2)},  # pods in, records, pieces
+            "K1": {"3->5": (3, 5), "5->6": (5, 6), "6->4": (6, 4)}}     # emitted, sorted, tile rows
+    if name in subs:
+        sub = subs[name]
+        out[name]["sub"] = {k: q(cat([(t[:, b] - t[:, a]) / 100.0 for t in runs])) for k, (a, b) in sub.items()}
+out["xcd_of_label"] = {k: v[:3] for k, v in xcd.items()}
 print(json.dumps(out))
