@@ -149,6 +149,40 @@ def parse():
 
 
 # ------------------------------------------------------------------ legs
+def select_leg(cd, spec, dev, stream, val, ts, hv, hv_ts, now, ds, reps=3):
+    """Framework-level selection for the config-3 queue with the shipped profile (SURVEY §8f
+    row 4): Dynamic weight 3 + synthetic other plugins (95 % pass their filters, weighted
+    sum in [0, 700]), percentageOfNodesToScore default (adaptive: 5 % of 100k = 5000
+    feasible nodes per pod from a rotating start) and every node scored (100)."""
+    N, P = val.shape[1], len(now)
+    eng = cd.Engine(cd.Policy(spec), dev.index)
+    eng.upload_nodes(val, ts, hv, hv_ts)
+    rng = np.random.default_rng(77)
+    d_now = torch.from_numpy(now).to(dev)
+    d_flags = torch.from_numpy(ds).to(dev)
+    d_ok = torch.from_numpy((rng.random(N) < 0.95).astype(np.uint8)).to(dev)
+    d_ext = torch.from_numpy(rng.integers(0, 8, N).astype(np.int64) * 100).to(dev)
+    ch = torch.empty(P, dtype=torch.int64, device=dev)
+    tot = torch.empty(P, dtype=torch.int64, device=dev)
+    sh = stream.cuda_stream
+    out = {"workload": f"config3 queue: {P} pods x {N} nodes, shipped profile (Dynamic weight 3 + other plugins' "
+                       "filter / weighted score per node), lowest-index ties", "parity": "tests/test_select.py"}
+    for label, pct in (("adaptive_percentage", 0), ("percentage_100", 100)):
+        def step():
+            return eng.select(d_now, d_flags, ch, tot, d_ok, d_ext, 3, pct, 0, 0, stream=sh)
+        step()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            nxt = step()
+        ms = (time.perf_counter() - t0) * 1e3 / reps
+        kt = kernel_times(eng, step, 2)
+        out[label] = {"nodes_per_pod": int(cd.num_feasible_nodes_to_find(N, pct)), "ms": round(ms, 3),
+                      "pods_per_s": round(P / (ms * 1e-3), 1), "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
+                      "next_start": int(nxt), "placed": int((ch >= 0).sum().item())}
+    eng.close()
+    return out
+
+
 def matrix_leg(cd, spec, dev, stream, label, val, ts, hv, hv_ts, now, ds, steps, pmc=None):
     """Per-pair path: the full first-fail and score matrices (int8, [P][N] in HBM) and the
     chosen node of every pod, one K3m launch per batch (node records resident: the node pass
@@ -450,6 +484,7 @@ def main():
             cd, spec, dev, stream, "config2: 5000 nodes x 1000 pods, full first-fail + score matrices + chosen node",
             v2, t2, c2.hv, c2.hv_ts, c2.now, c2.ds, max(args.steps, 20), pmc2)
         if args.config == 3:
+            extras["select_config3"] = select_leg(cd, spec, dev, stream, val, ts, c.hv, c.hv_ts, c.now, c.ds)
             extras["matrix_config3"] = matrix_leg(
                 cd, spec, dev, stream, "config3 nodes/pods (100000 x 10000), node_hot_value annotations: full "
                 "first-fail + score matrices (2 x 1 GB int8) + chosen node", val, ts, c.hv, c.hv_ts, c.now, c.ds, 10,

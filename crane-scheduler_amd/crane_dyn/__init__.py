@@ -69,6 +69,9 @@ def _load():
         "crane_dyn_eval_compact": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, vp]),
         "crane_dyn_eval_matrix_async": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, C.c_int64, vp, vp]),
         "crane_dyn_set_option": (C.c_int, [vp, C.c_char_p, C.c_int64]),
+        "crane_num_feasible_nodes_to_find": (C.c_int64, [C.c_int64, C.c_int32]),
+        "crane_dyn_select": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, C.c_int64, C.c_int32, C.c_int64, C.c_uint64,
+                                       vp, vp, vp, vp, P(C.c_int64), vp]),
         "crane_dyn_debug_trace": (C.c_int64, [vp, C.c_int32, C.c_int64, vp]),
         "crane_translate_event": (C.c_int, [C.c_char_p, C.c_size_t, C.c_int32, C.c_int64, C.c_int64, P(C.c_char_p),
                                             P(C.c_size_t), P(C.c_char_p), P(C.c_size_t), P(C.c_char_p),
@@ -105,12 +108,17 @@ ABI_SYMBOLS = (
     "crane_dyn_set_profiling", "crane_dyn_stage_times", "crane_dyn_hot_values",
     "crane_dyn_version", "crane_dyn_binding_records", "crane_dyn_add_bindings", "crane_dyn_gc_bindings",
     "crane_dyn_binding_count", "crane_dyn_eval_compact", "crane_dyn_eval_matrix_async", "crane_dyn_set_option",
-    "crane_translate_event", "crane_dyn_debug_trace",
+    "crane_translate_event", "crane_dyn_debug_trace", "crane_num_feasible_nodes_to_find", "crane_dyn_select",
 )
 
 
 def _ptr(a):
     return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def num_feasible_nodes_to_find(n_nodes, percentage=0):
+    """kube-scheduler v1.23.3 numFeasibleNodesToFind (crane_num_feasible_nodes_to_find)."""
+    return lib.crane_num_feasible_nodes_to_find(int(n_nodes), int(percentage))
 
 
 # ------------------------------------------------------------------ policy
@@ -377,6 +385,18 @@ class Engine:
         vp = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
         self._check(lib.crane_dyn_eval_matrix_async(self.h, P, vp(d_now), vp(d_flags), vp(d_ff), vp(d_score), ld,
                                                     vp(d_keys), stream))
+
+    def select(self, d_now, d_flags, d_chosen, d_total=None, d_ext_ok=None, d_ext_score=None, dyn_weight=3,
+               percentage=0, start=0, tie_seed=0, d_wstart=None, d_wlen=None, stream=None):
+        """Framework-level selection for the pod queue d_now (crane_dyn_select): torch device
+        tensors; returns the start index after the queue."""
+        P = d_now.numel()
+        vp = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+        nxt = C.c_int64(0)
+        self._check(lib.crane_dyn_select(self.h, P, vp(d_now), vp(d_flags), vp(d_ext_ok), vp(d_ext_score),
+                                         int(dyn_weight), int(percentage), int(start), int(tie_seed), vp(d_chosen),
+                                         vp(d_total), vp(d_wstart), vp(d_wlen), C.byref(nxt), stream))
+        return nxt.value
 
     # device-resident pipeline (torch tensors on the engine's device)
     def refresh_hot_values_async(self, now_ns, hv_ts_ns, stream=None):

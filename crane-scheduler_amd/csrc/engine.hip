@@ -172,6 +172,8 @@ struct crane_dyn {
     DevBuf<unsigned long long> trace;  // [3][kTraceWgs][8] phase stamps (option "trace")
     DevBuf<int32_t> sperm, scnt;  // K3 step path scratch (step.hip)
     DevBuf<int64_t> stile, spnow;
+    DevBuf<int64_t> sel_fth, sel_win, sel_state;  // framework selection (select.hip)
+    DevBuf<long long> sel_keys;
     DevBuf<Mid> smid;
     DevBuf<Step1> sstep1;
     DevBuf<int32_t> spm1, ssm0;   // prefix / suffix key maxima of the sorted Step1 records
@@ -599,6 +601,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->trace.release();
     h->sperm.release(); h->scnt.release(); h->stile.release(); h->spnow.release(); h->smid.release(); h->sstep1.release();
     h->spm1.release(); h->ssm0.release(); h->srows.release();
+    h->sel_fth.release(); h->sel_win.release(); h->sel_state.release(); h->sel_keys.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -831,6 +834,100 @@ int crane_dyn_eval_matrix_async(crane_dyn* h, int64_t P, const int64_t* d_now, c
     HIPTRY(h, hipSetDevice(h->device));
     return matrix_locked(h, P, d_now, d_flags, reinterpret_cast<long long*>(d_keys), d_first_fail, d_score, false, ld,
                          stream ? (hipStream_t)stream : h->stream);
+}
+
+// kube-scheduler v1.23.3 numFeasibleNodesToFind (pkg/scheduler/core/generic_scheduler.go,
+// not in the container): minFeasibleNodesToFind 100, minFeasibleNodesPercentageToFind 5,
+// adaptive percentage 50 - N / 125 when percentageOfNodesToScore <= 0.
+int64_t crane_num_feasible_nodes_to_find(int64_t num_all_nodes, int32_t percentage) {
+    const int64_t n = num_all_nodes;
+    if (n < 100 || percentage >= 100) return n;
+    int64_t pct = percentage;
+    if (pct <= 0) {
+        pct = 50 - n / 125;
+        if (pct < 5) pct = 5;
+    }
+    const int64_t k = n * pct / 100;
+    return k < 100 ? 100 : k;
+}
+
+int crane_dyn_select(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags,
+                     const uint8_t* d_ext_ok, const int64_t* d_ext_score, int64_t dyn_weight, int32_t percentage,
+                     int64_t start, uint64_t tie_seed, int64_t* d_chosen, int64_t* d_total, int64_t* d_wstart,
+                     int64_t* d_wlen, int64_t* next_start, void* stream) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    if (P < 0 || (P > 0 && (!d_now || !d_chosen))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
+    if (dyn_weight < 0 || dyn_weight > (1 << 20)) return h->fail(CRANE_E_INVALID, "dyn_weight must be in [0, 2^20]");
+    if (h->N >= (1LL << 32) || h->node_offset + h->N > (1LL << 32))
+        return h->fail(CRANE_E_INVALID, "selection keys hold 32-bit node indices");
+    const int64_t N = h->N;
+    if (start < 0 || (N > 0 && start >= N)) return h->fail(CRANE_E_INVALID, "start must be in [0, N)");
+    HIPTRY(h, hipSetDevice(h->device));
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    const int64_t K = crane_num_feasible_nodes_to_find(N, percentage);
+    const bool window = K < N;  // otherwise every node is checked for every pod, the start stays
+    if (P == 0 || N == 0) {
+        if (next_start) *next_start = start;
+        if (P > 0) HIPTRY(h, hipMemsetAsync(d_chosen, 0xFF, sizeof(int64_t) * (size_t)P, st));
+        if (P > 0 && d_total) HIPTRY(h, hipMemsetAsync(d_total, 0xFF, sizeof(int64_t) * (size_t)P, st));
+        HIPTRY(h, hipStreamSynchronize(st));
+        return CRANE_OK;
+    }
+    if (h->rec_dirty) {
+        int rc = node_pass_locked(h, st);
+        if (rc) return rc;
+    }
+    SelArgs a{};
+    a.rec = h->rec.p;
+    a.N = N;
+    a.node_offset = h->node_offset;
+    a.now = d_now;
+    a.flags = d_flags;
+    a.P = P;
+    a.wsum = h->dp.wsum;
+    a.noprio = h->dp.noprio;
+    a.ext_ok = d_ext_ok;
+    a.ext_score = d_ext_score;
+    a.w_dyn = dyn_weight;
+    a.seed = tie_seed;
+    a.kb = (uint32_t)(tie_seed * 0x9E3779B97F4A7C15ull >> 32);
+    HIPTRY(h, h->sel_keys.reserve((size_t)P));
+    HIPTRY(h, h->sel_state.reserve(1));
+    a.keys = h->sel_keys.p;
+    int64_t* ws = d_wstart;
+    int64_t* wl = d_wlen;
+    if (window) {
+        HIPTRY(h, h->sel_fth.reserve((size_t)N));
+        if (!ws || !wl) {
+            HIPTRY(h, h->sel_win.reserve((size_t)(2 * P)));
+            if (!ws) ws = h->sel_win.p;
+            if (!wl) wl = h->sel_win.p + P;
+        }
+        HIPTRY(h, launch_select_fth(a, h->shape, h->sel_fth.p, st));
+        HIPTRY(h, launch_select_chain(a, h->sel_fth.p, K, start, ws, wl, h->sel_state.p, st));
+        a.wstart = ws;
+        a.wlen = wl;
+    }
+    HIPTRY(h, hipMemsetAsync(a.keys, 0xFF, sizeof(long long) * (size_t)P, st));
+    HIPTRY(h, launch_select_pairs(h->shape, a, st));
+    HIPTRY(h, launch_select_decode(a, d_chosen, d_total, st));
+    int64_t nxt = start;
+    if (window) HIPTRY(h, hipMemcpyAsync(&nxt, h->sel_state.p, sizeof nxt, hipMemcpyDeviceToHost, st));
+    HIPTRY(h, hipStreamSynchronize(st));
+    if (!window) {  // every pod checked all N nodes: the start advances by N, mod N
+        if (d_wstart) {
+            std::vector<int64_t> v((size_t)P, start);
+            HIPTRY(h, hipMemcpy(d_wstart, v.data(), sizeof(int64_t) * (size_t)P, hipMemcpyHostToDevice));
+        }
+        if (d_wlen) {
+            std::vector<int64_t> v((size_t)P, N);
+            HIPTRY(h, hipMemcpy(d_wlen, v.data(), sizeof(int64_t) * (size_t)P, hipMemcpyHostToDevice));
+        }
+    }
+    if (next_start) *next_start = nxt;
+    return CRANE_OK;
 }
 
 int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, int64_t P, const int64_t* d_now,

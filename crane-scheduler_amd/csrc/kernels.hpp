@@ -74,6 +74,32 @@ struct MatrixArgs {
 };
 hipError_t launch_matrix(int shape, const MatrixArgs& a, hipStream_t st);
 
+// Framework-level selection (select.hip): upstream kube-scheduler's percentageOfNodesToScore
+// window with a rotating start, the weighted sum of Dynamic's score and the other score
+// plugins' (external), and a lowest-index or seeded tie-break.
+struct SelArgs {
+    const void* rec;           // NodeRec [N]
+    int64_t N, node_offset;
+    const int64_t* now;        // [P]
+    const uint8_t* flags;      // [P] or null (bit 0: DaemonSet)
+    int64_t P;
+    double wsum;
+    int32_t noprio;
+    uint32_t kb;               // tie-hash key of the batch (seed != 0)
+    const uint8_t* ext_ok;     // [N] or null: 1 = the other filter plugins pass
+    const int64_t* ext_score;  // [N] or null: the other score plugins' weighted sum, in [0, 2^30)
+    int64_t w_dyn;             // Dynamic's score weight, in [0, 2^20]
+    const int64_t* wstart;     // [P] or null: window start (local node index) per pod
+    const int64_t* wlen;       // [P]: window length (nodes in rotated order)
+    uint64_t seed;             // 0: lowest index wins ties
+    long long* keys;           // [P]: (total << 32) | tie, -1 = no feasible node (initialised to -1)
+};
+hipError_t launch_select_fth(const SelArgs& a, int shape, int64_t* fth, hipStream_t st);
+hipError_t launch_select_chain(const SelArgs& a, const int64_t* fth, int64_t K, int64_t start, int64_t* wstart,
+                               int64_t* wlen, int64_t* next_start, hipStream_t st);
+hipError_t launch_select_pairs(int shape, const SelArgs& a, hipStream_t st);
+hipError_t launch_select_decode(const SelArgs& a, int64_t* chosen, int64_t* total, hipStream_t st);
+
 // Sequential greedy (greedy.hip)
 constexpr int64_t kGreedyMaxNodes = 64LL * 64 * 64 * 64;
 constexpr size_t kGreedyLdsBytes = 160 * 1024;

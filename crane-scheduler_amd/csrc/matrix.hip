@@ -50,29 +50,6 @@ __device__ __forceinline__ int32_t ff_at(int64_t t, const NodeRec<PD, PR>& r, co
     return f;
 }
 
-// [lo, hi): the node's results are constant for every time in it (lo = latest expiry
-// <= t, hi = earliest expiry > t; the comparisons are now < expiry)
-template <int PD, int PR>
-__device__ __forceinline__ void bracket(const NodeRec<PD, PR>& r, int64_t t, int64_t& lo, int64_t& hi) {
-    lo = INT64_MIN;
-    hi = INT64_MAX;
-    auto upd = [&](int64_t e) {
-        if (e <= t) lo = max(lo, e);
-        else hi = min(hi, e);
-    };
-#pragma unroll
-    for (int k = 0; k < PD; ++k) upd(r.e_pred[k]);
-#pragma unroll
-    for (int k = 0; k < PR; ++k) upd(r.e_prio[k]);
-    upd(r.e_hv);
-}
-
-__device__ __forceinline__ int64_t readlane64(int64_t v, int j) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), j);
-    return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-
 __device__ __forceinline__ int32_t wave_max32(int32_t v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));

@@ -98,6 +98,29 @@ __device__ __forceinline__ void batch_range(const int64_t* __restrict__ tile_mm,
     batch_range_reduce<BS>(mn, mx, smn, smx, tmin, tmax);
 }
 
+// [lo, hi): the node's results are constant for every time in it (lo = latest expiry
+// <= t, hi = earliest expiry > t; the comparisons are now < expiry)
+template <int PD, int PR>
+__device__ __forceinline__ void bracket(const NodeRec<PD, PR>& r, int64_t t, int64_t& lo, int64_t& hi) {
+    lo = INT64_MIN;
+    hi = INT64_MAX;
+    auto upd = [&](int64_t e) {
+        if (e <= t) lo = max(lo, e);
+        else hi = min(hi, e);
+    };
+#pragma unroll
+    for (int k = 0; k < PD; ++k) upd(r.e_pred[k]);
+#pragma unroll
+    for (int k = 0; k < PR; ++k) upd(r.e_prio[k]);
+    upd(r.e_hv);
+}
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, int j) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), j);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // Per node and pod kind: the flat key (-1 if stepped or never feasible) and,
 // for a stepped node, its slots in the workgroup's spans of the kind's lists.
 // Phase 1 (step_count) only classifies — cheap and register-light, so it can

@@ -172,6 +172,35 @@ int crane_dyn_eval_compact(crane_dyn *h, int64_t n_pods, const int64_t *now_ns, 
 int crane_dyn_eval_matrix_async(crane_dyn *h, int64_t n_pods, const int64_t *d_now_ns, const uint8_t *d_pod_flags,
                                 int8_t *d_first_fail, int8_t *d_score, int64_t ld, int64_t *d_keys, void *stream);
 
+/* Framework-level selection for a pod queue, in order — what kube-scheduler
+ * v1.23.3 (go.mod:26; pkg/scheduler/core/generic_scheduler.go, not in the
+ * repo) does around the plugin with the shipped profile
+ * (deploy/manifests/dynamic/scheduler-config.yaml:7-16: the default plugins
+ * plus Dynamic, score weight 3):
+ *   - filter: Dynamic's Filter (DaemonSet pods bypass) and d_ext_ok[i] (the
+ *     other filter plugins' verdict per node, NULL = all pass);
+ *   - percentageOfNodesToScore: crane_num_feasible_nodes_to_find(N, percentage)
+ *     feasible nodes are taken per pod from the rotated order starting at the
+ *     running start index (first `start`), which then advances by the nodes
+ *     checked (findNodesThatPassFilters, sequential order); percentage >= 100
+ *     or N < 100 checks every node;
+ *   - score: dyn_weight * Score() + d_ext_score[i] (the other plugins' weighted
+ *     sum, in [0, 2^30); NULL = 0), dyn_weight in [0, 2^20];
+ *   - selectHost: the max total; ties go to the lowest node index (tie_seed 0,
+ *     a declared deviation from upstream's random reservoir) or, tie_seed != 0,
+ *     to a seeded bijective hash of (node index, pod position) — decodable, so
+ *     shards' packed keys still max-combine.
+ * Outputs (device, [n_pods]): d_chosen global node index or -1 (no feasible
+ * node: Unschedulable), d_total (NULL ok) the winning total or -1; d_wstart /
+ * d_wlen (NULL ok) each pod's window (rotated start, nodes checked);
+ * *next_start the start index after the queue (host).  Windows are over this
+ * engine's local node order.  Synchronous on `stream`. */
+int64_t crane_num_feasible_nodes_to_find(int64_t num_all_nodes, int32_t percentage_of_nodes_to_score);
+int crane_dyn_select(crane_dyn *h, int64_t n_pods, const int64_t *d_now_ns, const uint8_t *d_pod_flags,
+                     const uint8_t *d_ext_ok, const int64_t *d_ext_score, int64_t dyn_weight, int32_t percentage,
+                     int64_t start, uint64_t tie_seed, int64_t *d_chosen, int64_t *d_total, int64_t *d_wstart,
+                     int64_t *d_wlen, int64_t *next_start, void *stream);
+
 /* Device-resident variant for batched pipelines: all pointers are device
  * pointers, work is enqueued on `stream` (hipStream_t; NULL = engine stream)
  * and the call returns without synchronising.  keys[p] = (score << 32) |

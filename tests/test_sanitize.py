@@ -1,0 +1,42 @@
+"""AddressSanitizer + UndefinedBehaviorSanitizer build of the host parsers
+(crane-scheduler_amd/csrc/annotations.cpp, policy.cpp, events.cpp) driven by
+tests/cpp/fuzz_parse.cpp: random and mutated annotation values checked against
+the oracle's ParseFloat / ParseInLocation restatement, mutated policy
+documents, mutated scheduler events.  Host code only (no GPU sanitizers)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "crane-scheduler_amd", "csrc")
+SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-g", "-O1"]
+
+
+@pytest.fixture(scope="module")
+def fuzz_exe(tmp_path_factory):
+    if not shutil.which("g++") or not shutil.which("gcc"):
+        pytest.skip("no host compiler")
+    d = tmp_path_factory.mktemp("san")
+    obj = str(d / "oracle.o")
+    subprocess.run(["gcc", "-std=c11", *SAN, "-c", os.path.join(ROOT, "oracle", "crane_oracle.c"), "-o", obj],
+                   check=True)
+    exe = str(d / "fuzz_parse")
+    subprocess.run(["g++", "-std=c++17", *SAN, "-pthread", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "fuzz_parse.cpp"),
+                    *(os.path.join(CSRC, f) for f in ("annotations.cpp", "policy.cpp", "events.cpp")), obj,
+                    "-o", exe, "-lm"], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("seed", [1, 20251016])
+def test_parsers_under_asan_ubsan(fuzz_exe, seed):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([fuzz_exe, "300000", str(seed), os.path.join(ROOT, "tests", "golden", "policy_default.yaml")],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.startswith("ok 300000")
+    # the grammar must keep producing usable values, loadable policies and parsed events
+    f = r.stdout.split()
+    assert int(f[3]) > 50000 and int(f[5]) > 1000 and int(f[7]) > 5000, r.stdout
