@@ -110,6 +110,12 @@ __global__ __launch_bounds__(kK2Threads) void k2_hot_count(const int32_t* __rest
 // block size: 256 (the dedupe-form K2 bins nodes by it) or 128
 // STEP: also build the K3 step tables of the pod batch (K3a fused, step.hip):
 // the record is classified straight from registers.
+// keys-only step: LDS staging for this many stepped records per workgroup (the sorted
+// one-step records reuse it after the emit: 112 x 160 B >= 4 x 256 x 16 B); a node past
+// it builds its own records.  With the buffers below a workgroup takes < 40 KB of LDS,
+// four per CU.
+constexpr int kK1RecCap = 112;
+
 template <int PD, int PR, int kK1Threads, bool STEP>
 __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step) {
     const DevPolicy& pol = a.pol;
@@ -137,11 +143,19 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     __shared__ int32_t qm[STEP ? 2 * kK1Threads : 1];  // first middle-piece slot of queued items
     // one-step records per kind (2 per node at most): staging; sorted copy over the records'
     // LDS once the emit has read them (or past them when the records are written out)
-    __shared__ Step1 s1l[STEP ? 4 * kK1Threads : 1];
+    // (one buffer with the dedupe-form K2 buckets hxh below: those are read before the
+    // step epilogue's first barrier, the staging is written after it)
+    constexpr int kHxWords = kMaxWin * kK1Threads;
+    constexpr int kUnion = (STEP ? 4 * kK1Threads * (int)sizeof(Step1) : 0) > 4 * kHxWords
+                               ? 4 * kK1Threads * (int)sizeof(Step1)
+                               : 4 * kHxWords;
+    __shared__ __attribute__((aligned(16))) unsigned char ush[kUnion];
+    Step1* s1l = reinterpret_cast<Step1*>(ush);
     Step1* s1s = reinterpret_cast<Step1*>(smem + (out ? sizeof(Rec) * kK1Threads : 0));
     if (STEP && threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
-    if (STEP && threadIdx.x == 0) nq = 0;
-    __shared__ uint32_t hxh[kMaxWin][kK1Threads];  // dedupe-form K2: this block's window-rank buckets
+    __shared__ int32_t nrec;  // keys-only step: stepped records staged
+    if (STEP && threadIdx.x == 0) nq = nrec = 0;
+    auto hxh = reinterpret_cast<uint32_t(*)[kK1Threads]>(ush);  // dedupe-form K2: this block's window-rank buckets
     const bool hx = a.hx_region != nullptr;
     StepSlots so;
     Rec r;
@@ -327,9 +341,15 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     if (STEP) {
         batch_range_reduce<kK1Threads>(pmn, pmx, smn, smx, tmin, tmax);
         if (n < N) step_count<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, ssh, so);
+        bool self_emit = false;
         if (so.slot0 >= 0 || so.slot1 >= 0) {  // stepped (a few %): record to LDS, items to the queue
-            if (!out) lrec[threadIdx.x] = r;
-            step_queue(so, &nq, q, qm);
+            int rs = threadIdx.x;
+            if (!out) {  // keys-only: stepped records compacted into kK1RecCap LDS slots
+                rs = atomicAdd(&nrec, 1);
+                if (rs < kK1RecCap) lrec[rs] = r;
+            }
+            if (rs < kK1RecCap || out) step_queue(so, &nq, q, qm, rs);
+            else self_emit = true;  // (past the staging: this thread builds its own records)
         }
         step_publish<kK1Threads>(so, ssh, step.st, blk);  // (its barrier also orders lrec and the queue)
         CRANE_TSTAMP(a.trace, blockIdx.x, 3);
@@ -337,9 +357,11 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
         for (int w = threadIdx.x; w < nq; w += kK1Threads) {
             const uint32_t it = q[w];
             const int o = (int)(it & 0xFFF);
-            step_emit_one<PD, PR>(lrec[o], first + o, (int)((it >> 12) & 1), (int32_t)(it >> 14), qm[w],
-                                  ((it >> 13) & 1) != 0, tmin, tmax, step.wsum, step.noprio, step.st, blk, s1l);
+            step_emit_one<PD, PR>(lrec[it >> 24], first + o, (int)((it >> 12) & 1), (int32_t)((it >> 14) & 0x3FF),
+                                  qm[w], ((it >> 13) & 1) != 0, tmin, tmax, step.wsum, step.noprio, step.st, blk,
+                                  s1l);
         }
+        if (self_emit) step_emit<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, so, step.st, blk, s1l);
         __syncthreads();
         CRANE_TSTAMP(a.trace, blockIdx.x, 5);
         step_sort_publish<kK1Threads>(s1l, s1s, ssh, step.st, blk);
@@ -365,8 +387,13 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
     if (T != 128 && T != 256) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((a.N + T - 1) / T);
     // + the sorted one-step records past the node records when both are kept (kernel above)
-    static_assert(sizeof(NodeRec<PD, PR>) >= 4 * sizeof(Step1), "sorted records fit over the node records");
-    const size_t lds = sizeof(NodeRec<PD, PR>) * T + (step && a.out ? 4 * sizeof(Step1) * T : 0);
+    // records: every node's when written out (+ the sorted one-step records past them); keys-only
+    // step: kK1RecCap stepped records, the sorted one-step records over them after the emit
+    const size_t lds = a.out ? sizeof(NodeRec<PD, PR>) * T + (step ? 4 * sizeof(Step1) * T : 0)
+                             : std::max(sizeof(NodeRec<PD, PR>) * (size_t)std::min(T, kK1RecCap),
+                                        step ? 4 * sizeof(Step1) * T : (size_t)0);
+    if (!a.out && step && sizeof(NodeRec<PD, PR>) * (size_t)std::min(T, kK1RecCap) < 4 * sizeof(Step1) * T)
+        return hipErrorInvalidValue;  // (the sorted records must fit over the staging: see kK1RecCap)
     const K1Step sa = step ? *step : K1Step{};
     const char* nm = step ? "k1_node_pass+k3a_steps" : "k1_node_pass";
     if (T == 256)

@@ -22,9 +22,9 @@
 // Kernels: k_sel_fth (per node feasibility threshold: a non-DaemonSet pod
 // passes every filter iff now >= fth, since Dynamic's Filter fails exactly
 // while now < e_fail, the latest overloaded predicate's expiry); k_sel_chain
-// (one workgroup walks the queue in order: per pod, 8192 rotated positions per
-// round, ballots + an LDS prefix find the numNodesToFind-th feasible node, the
-// window = positions up to it); k_sel_pairs (per (pod, node): feasible, in the
+// (one wave walks the queue in order: per pod, 64 rotated positions per step,
+// a ballot and popcounts find the numNodesToFind-th feasible node, the window =
+// positions up to it, the next pod starts after it); k_sel_pairs (per (pod, node): feasible, in the
 // pod's window, weighted total; lane-cached step results like K3m, matrix.hip;
 // 64-bit keys, wave max, one LDS and one global atomicMax per pod per
 // workgroup); k_sel_decode (key -> node, total).
@@ -78,86 +78,69 @@ __host__ __device__ inline uint32_t tie_decode(uint64_t seed, uint32_t kb, uint3
 }
 
 // ---------------------------------------------------------------- k_sel_fth
+// fth[0][n]: a non-DaemonSet pod passes every filter iff now >= it; fth[1][n]: the
+// same for DaemonSet pods (the other plugins' filters only)
 template <int PD, int PR>
 __global__ __launch_bounds__(256) void k_sel_fth(SelArgs a, int64_t* __restrict__ fth) {
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (n >= a.N) return;
     const bool ok = !a.ext_ok || a.ext_ok[n];
     fth[n] = ok ? static_cast<const NodeRec<PD, PR>*>(a.rec)[n].e_fail : INT64_MAX;
+    fth[a.N + n] = ok ? INT64_MIN : INT64_MAX;
 }
 
 // ---------------------------------------------------------------- k_sel_chain
-constexpr int kChT = 1024, kChU = 8, kChW = kChT / 64;
+// One wave walks the queue: a pod's window is the rotated positions from the running
+// start up to its numNodesToFind-th feasible node, the next pod starts right after,
+// so the walk is one sequential sweep over the rotation.  64 positions per step (one
+// per lane, a ballot, a popcount), kChU steps' loads in flight, no barriers.
+constexpr int kChU = 8;
 
-__global__ __launch_bounds__(kChT) void k_sel_chain(SelArgs a, const int64_t* __restrict__ fth, int64_t K,
-                                                    int64_t start, int64_t* __restrict__ wstart,
-                                                    int64_t* __restrict__ wlen, int64_t* __restrict__ next_start) {
-    __shared__ int32_t cnt[kChU * kChW];  // per (u, wave): feasible count -> exclusive prefix
-    __shared__ int32_t tot;
-    __shared__ int64_t hit;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+__global__ __launch_bounds__(64) void k_sel_chain(SelArgs a, const int64_t* __restrict__ fth, int64_t K,
+                                                  int64_t start, int64_t* __restrict__ wstart,
+                                                  int64_t* __restrict__ wlen, int64_t* __restrict__ next_start) {
+    const int lane = threadIdx.x;
     const uint64_t lt = (1ull << lane) - 1ull;
     const int64_t N = a.N;
     int64_t s = start;
     for (int64_t p = 0; p < a.P; ++p) {
         const int64_t t = a.now[p];
-        const bool d = a.flags && (a.flags[p] & 1u);
+        const int64_t* __restrict__ th = fth + (a.flags && (a.flags[p] & 1u) ? N : 0);
         int64_t found = 0, processed = N;
-        for (int64_t base = 0; base < N; base += (int64_t)kChU * kChT) {
-            uint64_t m[kChU];
-            bool f[kChU];
+        for (int64_t base = 0; base < N; base += 64 * kChU) {
+            int64_t v[kChU];
 #pragma unroll
             for (int u = 0; u < kChU; ++u) {
-                const int64_t pos = base + u * kChT + threadIdx.x;  // rotated position
+                const int64_t pos = base + u * 64 + lane;
                 int64_t n = s + pos;
                 if (n >= N) n -= N;
-                // DaemonSet pods bypass Dynamic's Filter (plugins.go:41-43): the others' only
-                f[u] = pos < N && (d ? (!a.ext_ok || a.ext_ok[n] != 0) : t >= fth[n]);
+                v[u] = pos < N ? th[n] : INT64_MAX;
             }
+            bool done = false;
 #pragma unroll
             for (int u = 0; u < kChU; ++u) {
-                m[u] = __ballot(f[u]);
-                if (lane == 0) cnt[u * kChW + w] = __popcll(m[u]);
-            }
-            if (threadIdx.x == 0) hit = -1;
-            __syncthreads();
-            if (w == 0) {  // exclusive prefix over the kChU * kChW counts, in position order
-                static_assert(kChU * kChW == 128, "two counts per lane");
-                const int32_t c0 = cnt[2 * lane], c1 = cnt[2 * lane + 1];
-                int32_t x = c0 + c1;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int32_t y = __shfl_up(x, o);
-                    if (lane >= o) x += y;
+                const bool f = t >= v[u];
+                const uint64_t m = __ballot(f);
+                const int64_t c = __popcll(m);
+                if (found + c >= K) {  // the K-th feasible position is in this step (wave-uniform)
+                    const bool hitl = f && found + __popcll(m & lt) + 1 == K;
+                    const uint64_t hm = __ballot(hitl);
+                    processed = base + u * 64 + (__ffsll((unsigned long long)hm) - 1) + 1;
+                    done = true;
+                    break;
                 }
-                cnt[2 * lane] = x - c0 - c1;
-                cnt[2 * lane + 1] = x - c1;
-                if (lane == 63) tot = x;
+                found += c;
             }
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < kChU; ++u) {
-                if (!f[u]) continue;
-                const int64_t r = found + cnt[u * kChW + w] + __popcll(m[u] & lt) + 1;  // rank among feasible
-                if (r == K) hit = base + u * kChT + threadIdx.x + 1;
-            }
-            __syncthreads();
-            found += tot;
-            const int64_t h = hit;
-            __syncthreads();  // (cnt, tot, hit are rewritten by the next round / pod)
-            if (h >= 0) {
-                processed = h;
-                break;
-            }
+            if (done) break;
         }
-        if (threadIdx.x == 0) {
+        if (lane == 0) {
             wstart[p] = s;
             wlen[p] = processed;
         }
         s += processed;
         if (s >= N) s -= N;
     }
-    if (threadIdx.x == 0) *next_start = s;
+    if (lane == 0) *next_start = s;
 }
 
 // ---------------------------------------------------------------- k_sel_pairs
@@ -246,10 +229,10 @@ __global__ __launch_bounds__(kSelT) void k_sel_pairs(SelArgs a, int32_t chunk, i
                 if (rel < 0) rel += a.N;
                 in = rel < readlane64(wl, j);
             }
+            const bool feas = ok && in && (d || f);
+            if (!__ballot(feas)) continue;  // (most waves of a pod lie outside its window)
             const uint32_t lo32 = tb ^ (uint32_t)__builtin_amdgcn_readlane((int)cp, j);
-            const long long key = ok && in && (d || f)
-                                      ? (long long)((((int64_t)s * a.w_dyn + ext) << 32) | (int64_t)lo32)
-                                      : -1;
+            const long long key = feas ? (long long)((((int64_t)s * a.w_dyn + ext) << 32) | (int64_t)lo32) : -1;
             const long long k = wave_max64(key);
             if (lane == 0 && k >= 0) atomicMax(&best[q0 + j - p0], (unsigned long long)k + 1ull);
         }
@@ -294,8 +277,7 @@ hipError_t launch_select_fth(const SelArgs& a, int shape, int64_t* fth, hipStrea
 hipError_t launch_select_chain(const SelArgs& a, const int64_t* fth, int64_t K, int64_t start, int64_t* wstart,
                                int64_t* wlen, int64_t* next_start, hipStream_t st) {
     if (a.P <= 0 || a.N <= 0) return hipSuccess;
-    return klaunch("k_sel_chain", k_sel_chain, dim3(1), dim3(kChT), 0, st, a, fth, K, start, wstart, wlen,
-                   next_start);
+    return klaunch("k_sel_chain", k_sel_chain, dim3(1), dim3(64), 0, st, a, fth, K, start, wstart, wlen, next_start);
 }
 
 template <int PD, int PR>

@@ -278,17 +278,18 @@ __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, i
         step_emit_one<PD, PR>(r, n, 1, o.slot1, o.mslot1, o.multi1, tmin, tmax, wsum, noprio, st, blk, s1l);
 }
 
-// Work item of the compacted emit: owner thread | kind << 12 | multi << 13 | slot << 14,
+// Work item of the compacted emit: owner thread | kind << 12 | multi << 13 | slot << 14 | rs << 24,
 // and its first middle-piece slot in qm.
-__device__ __forceinline__ void step_queue(const StepSlots& o, int32_t* nq, uint32_t* q, int32_t* qm) {
+// (rs: the node's record slot in the workgroup's LDS staging, < 256; slot < 1024)
+__device__ __forceinline__ void step_queue(const StepSlots& o, int32_t* nq, uint32_t* q, int32_t* qm, int rs) {
     if (o.slot0 >= 0) {
         const int i = atomicAdd(nq, 1);
-        q[i] = threadIdx.x | ((uint32_t)o.multi0 << 13) | ((uint32_t)o.slot0 << 14);
+        q[i] = threadIdx.x | ((uint32_t)o.multi0 << 13) | ((uint32_t)o.slot0 << 14) | ((uint32_t)rs << 24);
         qm[i] = o.mslot0;
     }
     if (o.slot1 >= 0) {
         const int i = atomicAdd(nq, 1);
-        q[i] = threadIdx.x | (1u << 12) | ((uint32_t)o.multi1 << 13) | ((uint32_t)o.slot1 << 14);
+        q[i] = threadIdx.x | (1u << 12) | ((uint32_t)o.multi1 << 13) | ((uint32_t)o.slot1 << 14) | ((uint32_t)rs << 24);
         qm[i] = o.mslot1;
     }
 }
