@@ -133,13 +133,15 @@ def kernel_times(eng, fn, reps):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, choices=(3, 4))
     ap.add_argument("--cpu-pods", type=int, default=1920, help="pods in the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16, help="upstream kube-scheduler parallelism")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-greedy", action="store_true", help="skip the config-5 sequential-greedy measurement")
+    ap.add_argument("--inflight", type=int, default=4,
+                    help="independent pod batches in flight (engines x HIP streams); 1 = one batch at a time")
     ap.add_argument("--no-extras", action="store_true", help="headline step only (matrix / drop-in / controller legs off)")
     ap.add_argument("--leg", default="all", choices=("all", "matrix2", "matrix3"),
                     help="matrix2 / matrix3: only that per-pair leg (for per-kernel PMC passes)")
@@ -368,27 +370,39 @@ def main():
     c = synth.make_cluster(spec, N, P, n_bindings=B, seed=20250215 + args.config * 1000 + rank)
     # the pod batch is the same on every shard (only nodes and bindings are per rank)
     c.now, c.ds = synth.make_pods(P, seed=20250215 + args.config)
-    eng = cd.Engine(cd.Policy(spec), local)
+    # K independent pod batches in flight (--inflight): K engines, each with its own copy of
+    # the shard's nodes and binding log and its own scratch, on K streams; batch i runs the
+    # whole step on engine i % K, so one batch's latency-bound kernels overlap another's
+    K = max(1, args.inflight)
+    engs = [cd.Engine(cd.Policy(spec), local) for _ in range(K)]
+    eng = engs[0]
     val, ts, _ = c.rows(eng.metric_names)
-    eng.upload_nodes(val, ts, c.hv, c.hv_ts, node_offset=rank * N)
-    eng.upload_bindings(c.b_node, c.b_ts)
+    for e in engs:
+        e.upload_nodes(val, ts, c.hv, c.hv_ts, node_offset=rank * N)
+        e.upload_bindings(c.b_node, c.b_ts)
     d_now = torch.from_numpy(c.now).to(dev)
     d_flags = torch.from_numpy(c.ds).to(dev)
-    d_keys = torch.empty(P, dtype=torch.int64, device=dev)
+    d_keys_k = [torch.empty(P, dtype=torch.int64, device=dev) for _ in range(K)]
+    d_keys = d_keys_k[0]
     now_sync = int(synth.NOW0_NS)
 
-    # a dedicated stream: the default stream's handle is 0, which the C ABI reads as "engine stream"
-    stream = torch.cuda.Stream(dev)
+    # dedicated streams: the default stream's handle is 0, which the C ABI reads as "engine stream"
+    streams = [torch.cuda.Stream(dev) for _ in range(K)]
+    stream = streams[0]
     torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
 
-    def step(collective=True):
-        eng.step_keys_async(now_sync, now_sync, d_now, d_flags, d_keys, sh)  # K2x+K3p, K1+K3a, K3s
-        if world > 1 and collective:
-            dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)  # RCCL over xGMI
+    sh_k = [s_.cuda_stream for s_ in streams]
 
-    for _ in range(args.warmup):
-        step()
+    def step(collective=True, i=0):
+        j = i % K
+        engs[j].step_keys_async(now_sync, now_sync, d_now, d_flags, d_keys_k[j], sh_k[j])
+        if world > 1 and collective:
+            with torch.cuda.stream(streams[j]):  # (the collective waits on the batch's stream)
+                dist.all_reduce(d_keys_k[j], op=dist.ReduceOp.MAX)  # RCCL over xGMI
+
+    for i in range(args.warmup):
+        step(i=i)
     torch.cuda.synchronize(dev)
     graph = None
     if args.graph:
@@ -398,9 +412,9 @@ def main():
         graph.replay()
         torch.cuda.synchronize(dev)
 
-    def timed_step():
+    def timed_step(i):
         if graph is None:
-            step()
+            step(i=i)
         else:
             graph.replay()
             if world > 1:
@@ -410,8 +424,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        timed_step()
+    for i in range(args.steps):
+        timed_step(i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -422,6 +436,14 @@ def main():
         elapsed = float(t.item())
     ms_step = elapsed * 1e3 / args.steps
     keys = d_keys.cpu().numpy()
+    keys_agree = all(torch.equal(d_keys, k) for k in d_keys_k)
+    # one batch's latency: the same step with nothing else in flight (outside the timed region)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    for _ in range(max(10, args.steps // 4)):
+        step()  # (engine 0 only: each batch waits for the previous one on its stream)
+    torch.cuda.synchronize(dev)
+    batch_latency_ms = (time.perf_counter() - t1) * 1e3 / max(10, args.steps // 4)
     # per-kernel durations (dispatch-stamped) of the same step, outside the timed region
     kt = kernel_times(eng, lambda: step(collective=False), args.steps)
     ar_ms = None
@@ -591,7 +613,12 @@ def main():
             "config": {"workload": f"config{args.config}: {N} nodes/GPU x {P} pods, 6 metrics, hot values from "
                                    f"{B}-entry binding log per GPU, README default policy",
                        "nodes_per_gpu": N, "pods": P, "bindings_per_gpu": B, "parallelism": f"node-shard x{world}",
-                       "launch": "eager" if graph is None else "hipGraph replay per batch"},
+                       "launch": ("eager" if graph is None else "hipGraph replay per batch"),
+                       "batches_in_flight": K},
+            "batches_in_flight": {"k": K, "how": "K engines (own copy of the shard's nodes, binding log, scratch) on "
+                                                "K HIP streams, batch i on engine i % K; every batch runs the whole "
+                                                "step", "keys_agree": keys_agree,
+                                  "batch_latency_ms": round(batch_latency_ms, 4)},
             "placements_per_s": round(placements, 1),
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "allreduce_ms": None if ar_ms is None else round(ar_ms, 4),
@@ -605,7 +632,8 @@ def main():
         }
         line.update(extras)
         print(json.dumps(line), flush=True)
-    eng.close()
+    for e in engs:
+        e.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -1,0 +1,66 @@
+"""Throughput of the keys-only step with K independent pod batches in flight: K engines
+(each its own node SoA, binding log and scratch) on K HIP streams, batch i on engine i % K.
+Every batch does the whole step (K2x+K3p, K1+K3a, K3s); the streams let one batch's
+latency-bound kernels overlap another's.  Keys of every engine are checked equal.
+
+    python tools/inflight_probe.py [--config 3] [--steps 200] [--inflight 1,2,3,4]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "crane-scheduler_amd")]
+
+import torch  # noqa: E402
+
+import crane_dyn as cd  # noqa: E402
+from crane_dyn import synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", type=int, default=3)
+ap.add_argument("--steps", type=int, default=200)
+ap.add_argument("--inflight", default="1,2,3,4")
+args = ap.parse_args()
+dev = torch.device("cuda", 0)
+spec = cd.default_policy_spec()
+cfg = synth.CONFIGS[args.config]
+N, P, B = cfg["nodes"], cfg["pods"], cfg["bindings"]
+if args.config == 4:
+    N //= 8
+c = synth.make_cluster(spec, N, P, n_bindings=B, seed=20250215 + args.config * 1000)
+c.now, c.ds = synth.make_pods(P, seed=20250215 + args.config)
+now = int(synth.NOW0_NS)
+out = {"config": args.config, "nodes": N, "pods": P, "bindings": B}
+for K in [int(x) for x in args.inflight.split(",")]:
+    engs, streams, keys = [], [], []
+    for _ in range(K):
+        e = cd.Engine(cd.Policy(spec), 0)
+        val, ts, _ = c.rows(e.metric_names)
+        e.upload_nodes(val, ts, c.hv, c.hv_ts)
+        e.upload_bindings(c.b_node, c.b_ts)
+        engs.append(e)
+        streams.append(torch.cuda.Stream(dev))
+        keys.append(torch.empty(P, dtype=torch.int64, device=dev))
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+
+    def step(i):
+        j = i % K
+        engs[j].step_keys_async(now, now, d_now, d_flags, keys[j], streams[j].cuda_stream)
+
+    for i in range(10):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    same = all(torch.equal(keys[0], k) for k in keys)
+    out[f"inflight{K}"] = {"ms_per_step": round(ms, 4), "keys_equal": same}
+    for e in engs:
+        e.close()
+print(json.dumps(out))
