@@ -899,7 +899,7 @@ int crane_dyn_select(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_
     int64_t* ws = d_wstart;
     int64_t* wl = d_wlen;
     if (window) {
-        HIPTRY(h, h->sel_fth.reserve((size_t)(2 * N)));
+        HIPTRY(h, h->sel_fth.reserve((size_t)N));
         if (!ws || !wl) {
             HIPTRY(h, h->sel_win.reserve((size_t)(2 * P)));
             if (!ws) ws = h->sel_win.p;

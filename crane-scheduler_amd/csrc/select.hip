@@ -22,9 +22,9 @@
 // Kernels: k_sel_fth (per node feasibility threshold: a non-DaemonSet pod
 // passes every filter iff now >= fth, since Dynamic's Filter fails exactly
 // while now < e_fail, the latest overloaded predicate's expiry); k_sel_chain
-// (one wave walks the queue in order: per pod, 64 rotated positions per step,
-// a ballot and popcounts find the numNodesToFind-th feasible node, the window =
-// positions up to it, the next pod starts after it); k_sel_pairs (per (pod, node): feasible, in the
+// (one wave streams the rotated positions once for the whole queue: the next
+// pod's window starts where the last one ended; ballots + a scalar scan over
+// chunk counts find each pod's numNodesToFind-th feasible node); k_sel_pairs (per (pod, node): feasible, in the
 // pod's window, weighted total; lane-cached step results like K3m, matrix.hip;
 // 64-bit keys, wave max, one LDS and one global atomicMax per pod per
 // workgroup); k_sel_decode (key -> node, total).
@@ -78,69 +78,171 @@ __host__ __device__ inline uint32_t tie_decode(uint64_t seed, uint32_t kb, uint3
 }
 
 // ---------------------------------------------------------------- k_sel_fth
-// fth[0][n]: a non-DaemonSet pod passes every filter iff now >= it; fth[1][n]: the
-// same for DaemonSet pods (the other plugins' filters only)
+// A non-DaemonSet pod passes every filter at node n iff now >= fth[n]; a DaemonSet
+// pod (Dynamic bypassed) iff fth[n] != INT64_MAX (the other plugins pass).  Expiries
+// stay below INT64_MAX / 2 + a period (timestamps saturate at INT64_MAX / 2,
+// annotations.cpp), the clamp only makes the encoding unambiguous.
 template <int PD, int PR>
 __global__ __launch_bounds__(256) void k_sel_fth(SelArgs a, int64_t* __restrict__ fth) {
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (n >= a.N) return;
     const bool ok = !a.ext_ok || a.ext_ok[n];
-    fth[n] = ok ? static_cast<const NodeRec<PD, PR>*>(a.rec)[n].e_fail : INT64_MAX;
-    fth[a.N + n] = ok ? INT64_MIN : INT64_MAX;
+    fth[n] = ok ? min(static_cast<const NodeRec<PD, PR>*>(a.rec)[n].e_fail, INT64_MAX - 1) : INT64_MAX;
 }
 
 // ---------------------------------------------------------------- k_sel_chain
-// One wave walks the queue: a pod's window is the rotated positions from the running
-// start up to its numNodesToFind-th feasible node, the next pod starts right after,
-// so the walk is one sequential sweep over the rotation.  64 positions per step (one
-// per lane, a ballot, a popcount), kChU steps' loads in flight, no barriers.
-constexpr int kChU = 8;
+// Pod p's window is the rotated positions from its start up to its K-th feasible
+// node (at most N positions), and pod p + 1 starts right after it, so the whole
+// queue is one sequential sweep over the stream of rotated positions x = 0, 1, ...
+// (node (start + x) mod N), read once.  One workgroup takes the stream in rounds of
+// kChR positions (the next round's loads in flight): every thread ballots its
+// positions for the next kChQ pods at once (each against its own time), the masks
+// go to LDS, and wave 0 resolves the pods in order from the masks alone (each
+// pod's count from its window start, a wave prefix over the round's chunks, the
+// K-th set bit); a round holding more than kChQ pod ends repeats the ballots for
+// the next ones.
+constexpr int kChT = 1024, kChU = 8, kChW = kChT / 64, kChQ = 4;
+constexpr int kChC = kChU * kChW;         // 64-position chunks per round (chunk c = u * kChW + wave)
+constexpr int64_t kChR = 64LL * kChC;     // positions per round
+constexpr int kChPB = 1024;               // pod times cached per block
 
-__global__ __launch_bounds__(64) void k_sel_chain(SelArgs a, const int64_t* __restrict__ fth, int64_t K,
-                                                  int64_t start, int64_t* __restrict__ wstart,
-                                                  int64_t* __restrict__ wlen, int64_t* __restrict__ next_start) {
-    const int lane = threadIdx.x;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    const int64_t N = a.N;
-    int64_t s = start;
-    for (int64_t p = 0; p < a.P; ++p) {
-        const int64_t t = a.now[p];
-        const int64_t* __restrict__ th = fth + (a.flags && (a.flags[p] & 1u) ? N : 0);
-        int64_t found = 0, processed = N;
-        for (int64_t base = 0; base < N; base += 64 * kChU) {
-            int64_t v[kChU];
+__global__ __launch_bounds__(kChT) void k_sel_chain(SelArgs a, const int64_t* __restrict__ fth, int64_t K,
+                                                    int64_t start, int64_t* __restrict__ wstart,
+                                                    int64_t* __restrict__ wlen, int64_t* __restrict__ next_start) {
+    __shared__ unsigned long long msk[kChQ][kChC];
+    __shared__ int64_t ptime[kChPB];
+    __shared__ int8_t pds[kChPB];
+    __shared__ int64_t st_p, st_pstart, st_found;
+    __shared__ int32_t st_more;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t N = a.N, P = a.P;
+    auto load = [&](int64_t* v, int64_t nb) {  // nb: node of the round's first position
 #pragma unroll
-            for (int u = 0; u < kChU; ++u) {
-                const int64_t pos = base + u * 64 + lane;
-                int64_t n = s + pos;
-                if (n >= N) n -= N;
-                v[u] = pos < N ? th[n] : INT64_MAX;
-            }
-            bool done = false;
-#pragma unroll
-            for (int u = 0; u < kChU; ++u) {
-                const bool f = t >= v[u];
-                const uint64_t m = __ballot(f);
-                const int64_t c = __popcll(m);
-                if (found + c >= K) {  // the K-th feasible position is in this step (wave-uniform)
-                    const bool hitl = f && found + __popcll(m & lt) + 1 == K;
-                    const uint64_t hm = __ballot(hitl);
-                    processed = base + u * 64 + (__ffsll((unsigned long long)hm) - 1) + 1;
-                    done = true;
-                    break;
+        for (int u = 0; u < kChU; ++u) {
+            int64_t n = nb + u * kChT + threadIdx.x;
+            n = n < N ? n : (n - N < N ? n - N : n % N);
+            v[u] = fth[n];
+        }
+    };
+    int64_t p = 0, pstart = 0, found = 0, pb0 = -1;
+    int64_t cur[kChU], nxt[kChU];
+    int64_t x0 = 0, nb = start;
+    load(cur, nb);
+    while (p < P) {
+        int64_t nb2 = nb + kChR;
+        nb2 = nb2 < N ? nb2 : nb2 % N;
+        load(nxt, nb2);  // the next round, in flight while this one is resolved
+        bool more = true;
+        while (more && p < P) {
+            if (pb0 < 0 || p + kChQ > pb0 + kChPB) {  // pod times cached for [pb0, pb0 + kChPB)
+                __syncthreads();
+                pb0 = p;
+                if (threadIdx.x < kChPB) {
+                    const int64_t q = pb0 + threadIdx.x;
+                    ptime[threadIdx.x] = q < P ? a.now[q] : 0;
+                    pds[threadIdx.x] = q < P && a.flags ? (int8_t)(a.flags[q] & 1u) : 0;
                 }
-                found += c;
+                __syncthreads();
             }
-            if (done) break;
+            // masks of the round's positions for pods p .. p + kChQ - 1 (positions before the
+            // current pod's start are excluded; each pod's own start is applied by wave 0)
+#pragma unroll
+            for (int q = 0; q < kChQ; ++q) {
+                const int64_t t = ptime[p - pb0 + q];
+                const bool d = pds[p - pb0 + q] != 0;
+#pragma unroll
+                for (int u = 0; u < kChU; ++u) {
+                    const int64_t pos = x0 + u * kChT + threadIdx.x;
+                    const bool f = pos >= pstart && (d ? cur[u] != INT64_MAX : t >= cur[u]);
+                    const unsigned long long m = __ballot(f);
+                    if (lane == 0) msk[q][u * kChW + w] = m;
+                }
+            }
+            __syncthreads();
+            if (w == 0) {
+                // lane L covers chunks 2L, 2L + 1 (positions x0 + 64 c .. + 63)
+                int64_t ps = pstart, fnd = found, pp = p;
+                bool cont = true;  // the last resolved pod ended inside this round
+                for (int q = 0; q < kChQ && pp < P && cont; ++q) {
+                    const int64_t lim = ps + N;  // window: positions [ps, lim)
+                    int32_t cnt2[2];
+                    unsigned long long mm[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int c = 2 * lane + h;
+                        const int64_t c0 = x0 + 64LL * c;
+                        unsigned long long m = msk[q][c];
+                        // keep bits of positions in [ps, lim)
+                        if (c0 + 64 <= ps || c0 >= lim) m = 0;
+                        else {
+                            if (c0 < ps) m &= ~0ull << (ps - c0);
+                            if (c0 + 64 > lim) m &= (lim - c0 >= 64) ? ~0ull : ((1ull << (lim - c0)) - 1ull);
+                        }
+                        mm[h] = m;
+                        cnt2[h] = __popcll(m);
+                    }
+                    int32_t x = cnt2[0] + cnt2[1];
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const int32_t y = __shfl_up(x, o);
+                        if (lane >= o) x += y;
+                    }
+                    const int64_t need = K - fnd;
+                    const int32_t before = x - cnt2[0] - cnt2[1];  // feasible in earlier chunks
+                    // the lane whose chunks hold the need-th feasible position
+                    const bool mine = before < need && x >= need;
+                    const unsigned long long hb = __ballot(mine);
+                    int64_t end = -1;
+                    if (hb) {
+                        const int L = __ffsll(hb) - 1;
+                        if (lane == L) {
+                            int64_t r = need - before;  // rank within this lane's chunks
+                            int h = cnt2[0] >= r ? 0 : 1;
+                            if (h) r -= cnt2[0];
+                            unsigned long long m = mm[h];
+                            for (int64_t i = 1; i < r; ++i) m &= m - 1;  // drop the lowest r - 1 bits
+                            end = x0 + 64LL * (2 * lane + h) + (__ffsll(m) - 1);
+                        }
+                        end = readlane64(end, L);
+                    } else if (lim <= x0 + kChR) {
+                        end = lim - 1;  // fewer than K feasible among the window's N positions
+                    }
+                    if (end >= 0) {
+                        if (lane == 0) {
+                            int64_t s0 = start + ps % N;
+                            wstart[pp] = s0 >= N ? s0 - N : s0;
+                            wlen[pp] = end - ps + 1;
+                        }
+                        ++pp;
+                        ps = end + 1;
+                        fnd = 0;
+                    } else {
+                        fnd += __shfl(x, 63);
+                        cont = false;
+                    }
+                }
+                if (lane == 0) {
+                    st_p = pp;
+                    st_pstart = ps;
+                    st_found = fnd;
+                    st_more = cont && pp < P && ps < x0 + kChR;  // another pod starts in this round
+                }
+            }
+            __syncthreads();
+            p = st_p;
+            pstart = st_pstart;
+            found = st_found;
+            more = st_more != 0;
         }
-        if (lane == 0) {
-            wstart[p] = s;
-            wlen[p] = processed;
-        }
-        s += processed;
-        if (s >= N) s -= N;
+#pragma unroll
+        for (int u = 0; u < kChU; ++u) cur[u] = nxt[u];
+        x0 += kChR;
+        nb = nb2;
     }
-    if (lane == 0) *next_start = s;
+    if (threadIdx.x == 0) {
+        int64_t s0 = start + pstart % N;
+        *next_start = s0 >= N ? s0 - N : s0;
+    }
 }
 
 // ---------------------------------------------------------------- k_sel_pairs
@@ -277,7 +379,8 @@ hipError_t launch_select_fth(const SelArgs& a, int shape, int64_t* fth, hipStrea
 hipError_t launch_select_chain(const SelArgs& a, const int64_t* fth, int64_t K, int64_t start, int64_t* wstart,
                                int64_t* wlen, int64_t* next_start, hipStream_t st) {
     if (a.P <= 0 || a.N <= 0) return hipSuccess;
-    return klaunch("k_sel_chain", k_sel_chain, dim3(1), dim3(64), 0, st, a, fth, K, start, wstart, wlen, next_start);
+    return klaunch("k_sel_chain", k_sel_chain, dim3(1), dim3(kChT), 0, st, a, fth, K, start, wstart, wlen,
+                   next_start);
 }
 
 template <int PD, int PR>
