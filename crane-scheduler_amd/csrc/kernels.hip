@@ -135,9 +135,9 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     CRANE_TSTAMP(a.trace, blockIdx.x, 0);
     const int64_t first = blk * kK1Threads;
     const int64_t n = first + threadIdx.x;
-    __shared__ int64_t smn[kK1Threads / 64], smx[kK1Threads / 64];
     __shared__ StepShared ssh;
-    int64_t tmin = 0, tmax = 0, pmn = 0, pmx = 0;
+    int64_t tmin = 0, tmax = 0;
+    TileBounds tbr;
     __shared__ int32_t nq;                      // stepped (node, kind) items queued for the emit
     __shared__ uint32_t q[STEP ? 2 * kK1Threads : 1];
     __shared__ int32_t qm[STEP ? 2 * kK1Threads : 1];  // first middle-piece slot of queued items
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     // the batch time range partials: issued after the SoA loads, reduced after the compute
     int64_t tpre = 0;  // this thread's first tile-row bound (step_tile_rows)
     if (STEP) {
-        batch_range_load<kK1Threads>(step.tile_mm, step.ntiles, pmn, pmx);
+        batch_range_wave_load(step.tile_mm, step.ntiles, tbr);
         if (step.st.rows) tile_prefetch(step.st, &tpre);
     }
     if (n < N) {
@@ -339,7 +339,9 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     }
     CRANE_TSTAMP(a.trace, blockIdx.x, 2);
     if (STEP) {
-        batch_range_reduce<kK1Threads>(pmn, pmx, smn, smx, tmin, tmax);
+        batch_range_wave_reduce(step.tile_mm, step.ntiles, tbr, tmin, tmax);
+        if (!hx) __syncthreads();  // orders the lc / nq / nrec resets before the counting below
+                                   // (the dedupe form's barriers above already do)
         if (n < N) step_count<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, ssh, so);
         bool self_emit = false;
         if (so.slot0 >= 0 || so.slot1 >= 0) {  // stepped (a few %): record to LDS, items to the queue

@@ -90,6 +90,45 @@ __device__ __forceinline__ void batch_range_reduce(int64_t mn, int64_t mx, int64
         tmax = max(tmax, smx[i]);
     }
 }
+// Per-wave form (no LDS, no barrier): every wave reads all tile stats itself — lane l
+// the tiles l, l + 64, ... — in two parts: batch_range_wave_load keeps the first two
+// tiles' bounds in registers (issued early), batch_range_wave_reduce folds them, reads
+// any further tiles and reduces over the wave.
+struct TileBounds {
+    int64_t mn[2], mx[2];
+};
+__device__ __forceinline__ void batch_range_wave_load(const int64_t* __restrict__ tile_mm, int32_t ntiles,
+                                                      TileBounds& tb) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int i = lane + 64 * h;
+        tb.mn[h] = INT64_MAX;
+        tb.mx[h] = INT64_MIN;
+        if (i < ntiles) {
+            const int64_t* ts = tile_mm + kTileStat * i;
+            tb.mn[h] = min(ts[0], ts[2]);
+            tb.mx[h] = max(ts[1], ts[3]);
+        }
+    }
+}
+__device__ __forceinline__ void batch_range_wave_reduce(const int64_t* __restrict__ tile_mm, int32_t ntiles,
+                                                        const TileBounds& tb, int64_t& tmin, int64_t& tmax) {
+    int64_t mn = min(tb.mn[0], tb.mn[1]), mx = max(tb.mx[0], tb.mx[1]);
+    for (int i = (threadIdx.x & 63) + 128; i < ntiles; i += 64) {
+        const int64_t* ts = tile_mm + kTileStat * i;
+        mn = min(mn, min(ts[0], ts[2]));
+        mx = max(mx, max(ts[1], ts[3]));
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        mn = min(mn, (int64_t)__shfl_xor((long long)mn, o));
+        mx = max(mx, (int64_t)__shfl_xor((long long)mx, o));
+    }
+    tmin = mn;
+    tmax = mx;
+}
+
 template <int BS>
 __device__ __forceinline__ void batch_range(const int64_t* __restrict__ tile_mm, int32_t ntiles, int64_t* smn,
                                             int64_t* smx, int64_t& tmin, int64_t& tmax) {
