@@ -8,6 +8,7 @@
 // per node, and the pod x node kernel (K3) reads NodeRecs through the scalar
 // cache (a record is uniform across the 64 pods of a wave).
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace crane {
@@ -39,7 +40,26 @@ struct DevPolicy {
     int32_t win_pos[kMaxWin];     // window w -> rank of its cutoff in ascending order
     int64_t win_count[kMaxWin];   // hotValue.count
     int64_t win_cut_sorted[kMaxWin];  // ascending cutoffs (set per refresh)
+    // by cutoff rank r (set per refresh): the window, and hotValue.count as an exact u32
+    // division by multiply-high when 1 <= count < 2^32 (win_div_m = 0: int64 division)
+    int32_t win_of_rank[kMaxWin];
+    uint32_t win_div_m[kMaxWin];
+    int32_t win_div_sh[kMaxWin];  // sh1 | sh2 << 8
 };
+
+// n / d for the d the magic (m, sh) was made for (round-up method, exact for every
+// u32 n): t = mulhi(m, n); q = (t + ((n - t) >> sh1)) >> sh2
+__host__ __device__ inline uint32_t div_magic(uint32_t n, uint32_t m, int32_t sh) {
+    const uint32_t t = (uint32_t)(((uint64_t)m * n) >> 32);
+    return (t + ((n - t) >> (sh & 0xFF))) >> (sh >> 8);
+}
+// magic for 1 <= d < 2^32: l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1
+inline void make_div_magic(uint32_t d, uint32_t* m, int32_t* sh) {
+    int l = 0;
+    while (l < 32 && (1ull << l) < d) ++l;
+    *m = (uint32_t)((((uint64_t)1 << 32) * ((1ull << l) - d)) / d + 1);
+    *sh = (l < 1 ? l : 1) | ((l - 1 > 0 ? l - 1 : 0) << 8);
+}
 
 // Pod-invariant per-node record.  All "fresh" tests become `now < expiry`,
 // exactly the reference's now.Before(ts + dur) (stats.go:42-48).  An expiry of

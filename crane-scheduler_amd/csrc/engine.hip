@@ -326,6 +326,11 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         cut.sorted[r] = c[order[r]];
         dp.win_pos[order[r]] = r;
         dp.win_cut_sorted[r] = c[order[r]];
+        dp.win_of_rank[r] = order[r];
+        const int64_t cw = dp.win_count[order[r]];
+        dp.win_div_m[r] = 0;
+        dp.win_div_sh[r] = 0;
+        if (cw >= 1 && cw <= 0xFFFFFFFFLL) make_div_magic((uint32_t)cw, &dp.win_div_m[r], &dp.win_div_sh[r]);
     }
     h->hx_pending = false;
     h->counts_pending = true;

@@ -302,20 +302,21 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
                 for (int b = 0; b < kMaxWin; ++b)  // consumed: leaves the buckets zeroed for the next K2
                     if (b < pol.n_win) buckets[(int64_t)b * N + n] = 0;
             }
+            // window of cutoff rank r counts the buckets >= r: one running suffix sum
             int64_t v = 0;
+            uint64_t suf = 0;
 #pragma unroll
-            for (int w = 0; w < kMaxWin; ++w) {
-                if (w >= pol.n_win) break;
-                int64_t c = 0;
-#pragma unroll
-                for (int b = 0; b < kMaxWin; ++b) c += (b >= pol.win_pos[w] && b < pol.n_win) ? bc[b] : 0u;
-                if (cnt_out) cnt_out[(int64_t)w * N + n] = (uint32_t)c;
-                // Go int division (truncates toward 0); counts fit 32 bits in practice: u32 divide
-                const int64_t cw = pol.win_count[w];
-                if (cw > 0 && cw <= 0xFFFFFFFFLL && c <= 0xFFFFFFFFLL)
-                    v += (int64_t)((uint32_t)c / (uint32_t)cw);
+            for (int r = kMaxWin - 1; r >= 0; --r) {
+                if (r >= pol.n_win) continue;
+                suf += bc[r];
+                const int w = pol.win_of_rank[r];
+                if (cnt_out) cnt_out[(int64_t)w * N + n] = (uint32_t)suf;
+                // Go int division (truncates toward 0): exact multiply-high division when the
+                // count fits 32 bits and hotValue.count is in [1, 2^32)
+                if (pol.win_div_m[r] != 0 && suf <= 0xFFFFFFFFull)
+                    v += (int64_t)div_magic((uint32_t)suf, pol.win_div_m[r], pol.win_div_sh[r]);
                 else
-                    v += c / cw;
+                    v += (int64_t)suf / pol.win_count[w];
             }
             // the plugin re-reads it via ParseFloat (exact) and rejects negatives (stats.go:71-73)
             const double h = (double)v;

@@ -187,29 +187,6 @@ struct StepShared {
     int32_t fm[2][16];  // per-wave flat maxima (<= 1024 threads)
 };
 
-// The node's expiries for kind T with those outside (tmin, tmax] replaced by
-// INT64_MAX; returns their count and the min / max of the in-range ones.
-template <int PD, int PR, int T>
-__device__ __forceinline__ void step_points(const NodeRec<PD, PR>& r, int64_t tmin, int64_t tmax, int64_t* c,
-                                            int& cnt, int64_t& mn, int64_t& mx) {
-    constexpr int NB = PR + 2;
-#pragma unroll
-    for (int k = 0; k < PR; ++k) c[k] = r.e_prio[k];
-    c[PR] = r.e_hv;
-    c[PR + 1] = T == 0 ? r.e_fail : INT64_MIN;  // DaemonSet pods bypass the Filter
-    cnt = 0;
-    mn = INT64_MAX;
-    mx = INT64_MIN;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-        const bool in = c[j] > tmin && c[j] <= tmax;
-        c[j] = in ? c[j] : INT64_MAX;
-        cnt += in;
-        mn = min(mn, c[j]);
-        mx = in ? max(mx, c[j]) : mx;
-    }
-}
-
 // Phase 1.  A node with one distinct in-range expiry (a predicate's expiry
 // equals its metric's priority expiry when both use one metric) is one record;
 // otherwise two half-line records and cnt - 1 middle-piece slots are reserved
@@ -218,11 +195,25 @@ template <int PD, int PR>
 __device__ __forceinline__ void step_count(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
                                            double wsum, int32_t noprio, StepShared& sh, StepSlots& o) {
     const int32_t s0 = score_at<PD, PR>(tmin, r, wsum, noprio);
+    // the in-range expiries both kinds share (priorities, hot value), then e_fail for kind 0
+    int cnt1 = 0;
+    int64_t mn1 = INT64_MAX, mx1 = INT64_MIN;
+    auto add = [&](int64_t e, int& c, int64_t& mn, int64_t& mx) {
+        const bool in = e > tmin && e <= tmax;
+        c += in;
+        mn = in ? min(mn, e) : mn;
+        mx = in ? max(mx, e) : mx;
+    };
+#pragma unroll
+    for (int k = 0; k < PR; ++k) add(r.e_prio[k], cnt1, mn1, mx1);
+    add(r.e_hv, cnt1, mn1, mx1);
+    int cnt0 = cnt1;
+    int64_t mn0 = mn1, mx0 = mx1;
+    add(r.e_fail, cnt0, mn0, mx0);  // DaemonSet pods bypass the Filter
     auto kind = [&](auto Tc, int32_t& flat, int32_t& slot, int32_t& mslot, int8_t& nb, bool& multi) {
         constexpr int T = decltype(Tc)::value;
-        int64_t c[PR + 2], mn, mx;
-        int cnt;
-        step_points<PD, PR, T>(r, tmin, tmax, c, cnt, mn, mx);
+        const int cnt = T ? cnt1 : cnt0;
+        const int64_t mn = T ? mn1 : mn0, mx = T ? mx1 : mx0;
         flat = cnt == 0 ? key_of<PD, PR>(T, tmin, s0, r, n) : -1;
         multi = cnt > 0 && mn != mx;  // (cnt == 0: mn = INT64_MAX, mx = INT64_MIN)
         nb = (int8_t)cnt;

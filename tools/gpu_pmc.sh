@@ -5,6 +5,7 @@
 #   profiles/pmc/config3_<hash>.json   headline step, config 3
 #   profiles/pmc/config2_<hash>.json   per-pair matrix leg, config 2
 #   profiles/pmc/config3m_<hash>.json  per-pair matrix leg at config 3 size
+#   profiles/pmc/config4m_<hash>.json  cold-cache 4M-node pass (tools/stream_bench.py)
 # Stops on any fault/timeout exit code.  Usage: bash tools/gpu_pmc.sh <tag> [workloads]
 cd "$GRAFT_REPO_ROOT"
 TAG=${1:-pmc}
@@ -16,7 +17,8 @@ for w in $WL; do
     case $w in
         2) CMD="python3 $GRAFT_REPO_ROOT/bench.py --leg matrix2 --steps 5";;
         3m) CMD="python3 $GRAFT_REPO_ROOT/bench.py --leg matrix3 --steps 3";;
-        *) CMD="python3 $GRAFT_REPO_ROOT/bench.py --config $w --steps 5 --warmup 1 --no-cpu-baseline --no-greedy --no-extras";;
+        4m) CMD="python3 $GRAFT_REPO_ROOT/tools/stream_bench.py --k2 auto --reps 2";;
+        *) CMD="python3 $GRAFT_REPO_ROOT/bench.py --config $w --steps 5 --warmup 1 --inflight 1 --no-cpu-baseline --no-greedy --no-extras";;
     esac
     for pass in "fetch FETCH_SIZE" "write WRITE_SIZE" "valu SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY" "l2 TCC_HIT_sum TCC_MISS_sum"; do
         set -- $pass
