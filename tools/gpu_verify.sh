@@ -14,5 +14,9 @@ timeout -k 10 300 python tools/stream_bench.py > $OUT/stream.json 2> $OUT/stream
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$OUT/prof -o bench \
     -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-greedy > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; }
+# one batch at a time: the kernels' own durations (what bench.py's kernel_ms / roofline use)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$OUT/prof1 -o bench1 \
+    -- python3 $GRAFT_REPO_ROOT/bench.py --inflight 1 --no-cpu-baseline --no-greedy --no-extras > $OUT/prof1.log 2>&1 || { tail -20 $OUT/prof1.log; exit 1; }
 tail -3 $OUT/pytest_gpu.log; cat $OUT/smoke.log; tail -1 $OUT/bench.log | cut -c1-3000
 python3 tools/kstats.py $OUT/prof/bench_kernel_stats.csv
+python3 tools/kstats.py $OUT/prof1/bench1_kernel_stats.csv
