@@ -103,6 +103,7 @@ struct Options {
     int matrix_chunk = 0;     // K3m pods per workgroup: 0 automatic
     int step_rows = 1;        // 1: producers write per-tile record ranges for K3s, 0: K3s searches
     int k3s_blocks = 0;       // K3s producer blocks per workgroup aimed for: 0 automatic
+    int k2x_threads = 512;    // dedupe K2 workgroup size: 256, 512 or 1024
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
@@ -342,7 +343,8 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     if (h->opt.k2_form == 0 && gx.ok) {
         // one launch (+ K3p); the node pass counts its own block's entries (no buckets)
         HIPTRY(h, h->k2_sorted.reserve(hot_dedupe_scratch(gx)));
-        HIPTRY(h, launch_hot_count_dedupe(h->bnode.p, h->bts.p, h->B, h->N, cut, gx, h->k2_sorted.p, st, pods));
+        HIPTRY(h, launch_hot_count_dedupe(h->bnode.p, h->bts.p, h->B, h->N, cut, gx, h->k2_sorted.p, st, pods,
+                                          h->opt.k2x_threads));
         if (pods_done) *pods_done = pods != nullptr && pods->P > 0;
         h->hx_g = gx;
         h->hx_pending = true;
@@ -638,6 +640,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "matrix_chunk" && range(0, 1024)) o.matrix_chunk = (int)value;
     else if (n == "step_rows" && range(0, 1)) o.step_rows = (int)value;
     else if (n == "k3s_blocks" && range(0, 256)) o.k3s_blocks = (int)value;
+    else if (n == "k2x_threads" && (value == 256 || value == 512 || value == 1024)) o.k2x_threads = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
         if (o.trace) {

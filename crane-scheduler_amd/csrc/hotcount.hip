@@ -309,24 +309,27 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     CRANE_TSTAMP(g.trace, blk, 4);
 }
 
-// 1024 threads (2 bindings each): the launch is one round of workgroups at
-// config 3, so its time is one workgroup's dependent chain; wider workgroups shorten it (256 -> 512 -> 1024: 15.6 -> 11.9 -> 11.3 us)
-constexpr int kDT = 1024;
-
-__global__ __launch_bounds__(kDT) void k2x_dedupe(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
-                                                  int64_t B, int64_t N, HotCutoffs cut, HotPart g,
-                                                  uint32_t* __restrict__ CO, uint32_t* __restrict__ region) {
-    k2d_body<kDT>((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
+// The launch is one round of workgroups at config 3, so one batch's time is one
+// workgroup's dependent chain and wider workgroups shorten it; with several batches
+// in flight the idle waves of the widest cost throughput.  Engine option k2x_threads,
+// default 512 (config 3, one batch / 4 in flight: 1024 -> 0.0399 / 0.0168 ms per
+// step, 512 -> 0.0407 / 0.0141, 256 -> 0.0446 / 0.0147; tools/inflight_sweep.sh).
+template <int BT>
+__global__ __launch_bounds__(BT) void k2x_dedupe(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
+                                                 int64_t B, int64_t N, HotCutoffs cut, HotPart g,
+                                                 uint32_t* __restrict__ CO, uint32_t* __restrict__ region) {
+    k2d_body<BT>((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
 }
 
-__global__ __launch_bounds__(kDT) void k2x_dedupe_pods(const int32_t* __restrict__ bnode,
-                                                       const int64_t* __restrict__ bts, int64_t B, int64_t N,
-                                                       HotCutoffs cut, HotPart g, uint32_t* __restrict__ CO,
-                                                       uint32_t* __restrict__ region, PodPrep pp) {
-    if ((int32_t)blockIdx.x < g.nblk) k2d_body<kDT>((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
+template <int BT>
+__global__ __launch_bounds__(BT) void k2x_dedupe_pods(const int32_t* __restrict__ bnode,
+                                                      const int64_t* __restrict__ bts, int64_t B, int64_t N,
+                                                      HotCutoffs cut, HotPart g, uint32_t* __restrict__ CO,
+                                                      uint32_t* __restrict__ region, PodPrep pp) {
+    if ((int32_t)blockIdx.x < g.nblk) k2d_body<BT>((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
     else {
         extern __shared__ __attribute__((aligned(16))) unsigned char k3p_lds[];
-        k3p_tile<kDT>((int64_t)blockIdx.x - g.nblk, pp, k3p_lds);
+        k3p_tile<BT>((int64_t)blockIdx.x - g.nblk, pp, k3p_lds);
     }
 }
 
@@ -344,14 +347,15 @@ HotPart hot_dedupe_geometry(int64_t B, int64_t N, int32_t W, int32_t bs) {
     return g;
 }
 
-hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
-                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
-                                   const PodPrep* pods) {
+template <int BT>
+static hipError_t launch_dedupe_t(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
+                                  const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
+                                  const PodPrep* pods) {
     static const hipError_t attr = [] {
-        hipError_t e = hipFuncSetAttribute((const void*)k2x_dedupe, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipError_t e = hipFuncSetAttribute((const void*)k2x_dedupe<BT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            100 * 1024);
         if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k2x_dedupe_pods, hipFuncAttributeMaxDynamicSharedMemorySize,
+            e = hipFuncSetAttribute((const void*)k2x_dedupe_pods<BT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     100 * 1024);
         return e;
     }();
@@ -361,10 +365,20 @@ hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int
     size_t lds = sizeof(uint32_t) * (2 * (size_t)kDSlots + 2 * (size_t)g.nbins) + sizeof(uint16_t) * kXChunk;
     if (pods && pods->P > 0) lds = std::max(lds, kK3pLds);
     if (pods && pods->P > 0)
-        return klaunch("k2x_dedupe+k3p_pods", k2x_dedupe_pods, dim3((unsigned)(g.nblk + pods->ntiles)), dim3(kDT), lds,
-                       st, bnode, bts, B, N, cut, g, CO, region, *pods);
-    return klaunch("k2x_dedupe", k2x_dedupe, dim3((unsigned)g.nblk), dim3(kDT), lds, st, bnode, bts, B, N, cut, g, CO,
-                   region);
+        return klaunch("k2x_dedupe+k3p_pods", k2x_dedupe_pods<BT>, dim3((unsigned)(g.nblk + pods->ntiles)), dim3(BT),
+                       lds, st, bnode, bts, B, N, cut, g, CO, region, *pods);
+    return klaunch("k2x_dedupe", k2x_dedupe<BT>, dim3((unsigned)g.nblk), dim3(BT), lds, st, bnode, bts, B, N, cut, g,
+                   CO, region);
+}
+
+hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
+                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
+                                   const PodPrep* pods, int threads) {
+    switch (threads) {
+        case 256: return launch_dedupe_t<256>(bnode, bts, B, N, cut, g, scratch, st, pods);
+        case 512: return launch_dedupe_t<512>(bnode, bts, B, N, cut, g, scratch, st, pods);
+        default: return launch_dedupe_t<1024>(bnode, bts, B, N, cut, g, scratch, st, pods);
+    }
 }
 
 size_t hot_dedupe_scratch(const HotPart& g) { return (size_t)g.cap + (size_t)g.nbins * (size_t)g.nblk; }

@@ -181,7 +181,7 @@ HotPart hot_dedupe_geometry(int64_t B, int64_t N, int32_t W, int32_t bs);
 size_t hot_dedupe_scratch(const HotPart& g);  // uint32 entries: regions + count/offset matrix
 hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                    const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
-                                   const PodPrep* pods = nullptr);
+                                   const PodPrep* pods = nullptr, int threads = 1024);
 
 // ---------------------------------------------------------------- K3 step path (step.hip)
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)

@@ -248,6 +248,7 @@ const char *crane_dyn_version(void);
  *   "matrix_vec" 0 auto | 1 | 4 | 8 | 16 nodes per lane   "matrix_chunk" 0 auto | pods per workgroup (<= 1024)
  *   "step_rows" 1 producers index the records per pod tile | 0 K3s searches them
  *   "k3s_blocks" 0 auto | producer blocks per K3s workgroup aimed for (1..256)
+ *   "k2x_threads" 512 | 1024 | 256: dedupe K2 workgroup size
  *   "trace" 0 | 1: phase stamps of the step kernels (crane_dyn_debug_trace) */
 int crane_dyn_set_option(crane_dyn *h, const char *name, int64_t value);
 /* Phase stamps of the last K2x (which = 0), K1 (1) or K3s (2) launch with option

@@ -162,9 +162,9 @@ def test_hot_values_random(n_nodes, n_bind, seed, k2):
     assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch, och)
 
 
-@pytest.mark.parametrize("threads", [128, 256])
+@pytest.mark.parametrize("threads,k2x", [(128, 512), (256, 512), (256, 1024), (256, 256)])
 @pytest.mark.parametrize("case", ["one_hot_node", "eight_windows", "last_node", "odd_counts"])
-def test_hot_values_dedupe_edges(case, threads):
+def test_hot_values_dedupe_edges(case, threads, k2x):
     """Dedupe-form K2 (per-workgroup (node, bucket) aggregation, counts read by the
     node pass) at its packing limits: a region whose 2048 bindings all hit one node
     (count field), eight windows (bucket field), the shard's last node and bindings
@@ -187,7 +187,7 @@ def test_hot_values_dedupe_edges(case, threads):
         bn[::3] = n_nodes - 1
         bn[1::7] = n_nodes  # past the shard: ignored
         bn[2::11] = -3
-    eng = engine_for(spec, c, opts={"k2_form": 0, "k1_threads": threads})
+    eng = engine_for(spec, c, opts={"k2_form": 0, "k1_threads": threads, "k2x_threads": k2x})
     eng.upload_bindings(bn, c.b_ts)
     now = int(c.now[0])
     for rep in range(2):  # a second refresh after the first was consumed

@@ -23,6 +23,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=3)
 ap.add_argument("--steps", type=int, default=200)
 ap.add_argument("--inflight", default="1,2,3,4")
+ap.add_argument("--opt", action="append", default=[], help="engine option name=value (repeatable)")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 spec = cd.default_policy_spec()
@@ -33,11 +34,14 @@ if args.config == 4:
 c = synth.make_cluster(spec, N, P, n_bindings=B, seed=20250215 + args.config * 1000)
 c.now, c.ds = synth.make_pods(P, seed=20250215 + args.config)
 now = int(synth.NOW0_NS)
-out = {"config": args.config, "nodes": N, "pods": P, "bindings": B}
+out = {"config": args.config, "nodes": N, "pods": P, "bindings": B, "opts": args.opt}
 for K in [int(x) for x in args.inflight.split(",")]:
     engs, streams, keys = [], [], []
     for _ in range(K):
         e = cd.Engine(cd.Policy(spec), 0)
+        for o in args.opt:
+            k_, v_ = o.split("=")
+            e.set_option(k_, int(v_))
         val, ts, _ = c.rows(e.metric_names)
         e.upload_nodes(val, ts, c.hv, c.hv_ts)
         e.upload_bindings(c.b_node, c.b_ts)
