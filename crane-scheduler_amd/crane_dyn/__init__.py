@@ -55,6 +55,13 @@ def _load():
         "crane_tz_offset": (C.c_int, [C.c_char_p, P(C.c_int64)]),
         "crane_parse_annotation": (None, [C.c_char_p, C.c_size_t, C.c_int64, P(C.c_double), P(C.c_int64)]),
         "crane_parse_annotations": (C.c_int, [C.c_int64, vp, vp, C.c_int64, vp, vp, C.c_int32]),
+        "crane_tz_load": (C.c_int, [C.c_char_p, C.c_char_p, P(vp)]),
+        "crane_tz_load_bytes": (C.c_int, [C.c_char_p, C.c_size_t, P(vp)]),
+        "crane_tz_free": (None, [vp]),
+        "crane_tz_lookup": (C.c_int, [vp, C.c_int64, P(C.c_int32), P(C.c_int64), P(C.c_int64)]),
+        "crane_tz_date": (C.c_int64, [vp, C.c_int64]),
+        "crane_parse_annotation_tz": (None, [C.c_char_p, C.c_size_t, vp, P(C.c_double), P(C.c_int64)]),
+        "crane_parse_annotations_tz": (C.c_int, [C.c_int64, vp, vp, vp, vp, vp, C.c_int32]),
         "crane_dyn_create": (C.c_int, [P(_CPolicy), C.c_int32, P(vp)]),
         "crane_dyn_destroy": (C.c_int, [vp]),
         "crane_dyn_last_error": (C.c_char_p, [vp]),
@@ -109,6 +116,8 @@ ABI_SYMBOLS = (
     "crane_dyn_version", "crane_dyn_binding_records", "crane_dyn_add_bindings", "crane_dyn_gc_bindings",
     "crane_dyn_binding_count", "crane_dyn_eval_compact", "crane_dyn_eval_matrix_async", "crane_dyn_set_option",
     "crane_translate_event", "crane_dyn_debug_trace", "crane_num_feasible_nodes_to_find", "crane_dyn_select",
+    "crane_tz_load", "crane_tz_load_bytes", "crane_tz_free", "crane_tz_lookup", "crane_tz_date",
+    "crane_parse_annotation_tz", "crane_parse_annotations_tz",
 )
 
 
@@ -209,6 +218,49 @@ def parse_annotation(s: str, tz_offset_s: int):
     return v.value, t.value
 
 
+class Zone:
+    """An IANA time zone with go1.17's semantics (tz.cpp): Zone(name, zoneinfo_dir) like
+    time.LoadLocation, or Zone(tzif=bytes) like LoadLocationFromTZData."""
+
+    def __init__(self, name=None, zoneinfo_dir=None, tzif=None):
+        h = C.c_void_p()
+        if tzif is not None:
+            rc = lib.crane_tz_load_bytes(tzif, len(tzif), C.byref(h))
+        else:
+            rc = lib.crane_tz_load((name or "").encode(), None if zoneinfo_dir is None else zoneinfo_dir.encode(),
+                                   C.byref(h))
+        if rc:
+            raise CraneError(rc, f"time zone {name!r} not loadable")
+        self.h = h
+
+    def lookup(self, unix_s):
+        """Location.lookup: (offset_s, start_s, end_s) of the zone period holding unix_s."""
+        off, st, en = C.c_int32(), C.c_int64(), C.c_int64()
+        lib.crane_tz_lookup(self.h, int(unix_s), C.byref(off), C.byref(st), C.byref(en))
+        return off.value, st.value, en.value
+
+    def date(self, local_s):
+        """time.Date: wall clock (seconds since the epoch as if UTC) -> Unix seconds."""
+        return lib.crane_tz_date(self.h, int(local_s))
+
+    def parse_annotation(self, s: str):
+        b = s.encode()
+        v, t = C.c_double(), C.c_int64()
+        lib.crane_parse_annotation_tz(b, len(b), self.h, C.byref(v), C.byref(t))
+        return v.value, t.value
+
+    def close(self):
+        if self.h:
+            lib.crane_tz_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class SnapshotStrings:
     """A node snapshot's annotation strings encoded once, row-major [M+1][N] (the
     metrics, then node_hot_value; None = key missing), for repeated bulk parses
@@ -229,10 +281,15 @@ class SnapshotStrings:
     def __len__(self):
         return len(self._enc)
 
-    def parse(self, tz_offset_s, threads=0):
-        """Parse every string into self.val / self.ts (flat [M+1][N]); host threads <= 0 = all."""
-        rc = lib.crane_parse_annotations(len(self._enc), _ptr(self._strs), _ptr(self._lens),
-                                         tz_offset_s, _ptr(self.val), _ptr(self.ts), threads)
+    def parse(self, tz, threads=0):
+        """Parse every string into self.val / self.ts (flat [M+1][N]); tz: a fixed offset in
+        seconds or a Zone; host threads <= 0 = all."""
+        if isinstance(tz, Zone):
+            rc = lib.crane_parse_annotations_tz(len(self._enc), _ptr(self._strs), _ptr(self._lens), tz.h,
+                                                _ptr(self.val), _ptr(self.ts), threads)
+        else:
+            rc = lib.crane_parse_annotations(len(self._enc), _ptr(self._strs), _ptr(self._lens),
+                                             tz, _ptr(self.val), _ptr(self.ts), threads)
         if rc:
             raise CraneError(rc, "bulk annotation parse")
 

@@ -207,10 +207,11 @@ int64_t civil_days(int64_t y, int m, int d) {
 
 }  // namespace
 
-// time.ParseInLocation("2006-01-02T15:04:05Z", s, loc) with loc a fixed
-// offset.  Layout chunks (go1.17 time/format.go): stdLongYear '-' stdZeroMonth
-// '-' stdZeroDay 'T' stdHour ':' stdZeroMinute ':' stdZeroSecond [.frac] 'Z'.
-bool crane_go_parse_time(const char* s, size_t n, int64_t tz_offset_s, int64_t* out_ns) {
+// time.ParseInLocation("2006-01-02T15:04:05Z", s, loc): the wall clock as
+// seconds since the epoch taken as UTC (`local`) and the fraction.  Layout chunks
+// (go1.17 time/format.go): stdLongYear '-' stdZeroMonth '-' stdZeroDay 'T'
+// stdHour ':' stdZeroMinute ':' stdZeroSecond [.frac] 'Z' (a literal).
+static bool parse_local(const char* s, size_t n, int64_t* local, int64_t* nsec_out) {
     // Fast path for the exact 20-byte stamp the controller writes: fixed
     // digit/separator positions, same range checks, and a per-thread memo of
     // the last date (a snapshot's stamps share a handful of days), so the
@@ -232,9 +233,8 @@ bool crane_go_parse_time(const char* s, size_t n, int64_t tz_offset_s, int64_t* 
                 memo_days = civil_days(year, mon, day);
                 memo_key = key;
             }
-            const __int128 t = (__int128)(memo_days * 86400 + hour * 3600 + min * 60 + sec - tz_offset_s) * 1000000000;
-            const __int128 lo = (__int128)INT64_MIN / 2, hi = (__int128)INT64_MAX / 2;  // as below
-            *out_ns = (int64_t)(t < lo ? lo : (t > hi ? hi : t));
+            *local = memo_days * 86400 + hour * 3600 + min * 60 + sec;
+            *nsec_out = 0;
             return true;
         }
     }
@@ -264,12 +264,32 @@ bool crane_go_parse_time(const char* s, size_t n, int64_t tz_offset_s, int64_t* 
     }
     if (!lit(s, n, &p, 'Z') || p != n) return false;
     if (day < 1 || day > month_days(mon, year)) return false;
-    const __int128 t =
-        ((__int128)civil_days(year, mon, day) * 86400 + hour * 3600 + min * 60 + sec - tz_offset_s) * 1000000000 + nsec;
-    // int64 ns spans 1678..2262; saturate so "long ago" stays stale and "far
-    // future" stays fresh, as with Go's wider Time.
+    *local = civil_days(year, mon, day) * 86400 + hour * 3600 + min * 60 + sec;
+    *nsec_out = nsec;
+    return true;
+}
+
+// int64 ns spans 1678..2262; saturate so "long ago" stays stale and "far future"
+// stays fresh, as with Go's wider Time
+static int64_t to_ns(int64_t unix_s, int64_t nsec) {
+    const __int128 t = (__int128)unix_s * 1000000000 + nsec;
     const __int128 lo = (__int128)INT64_MIN / 2, hi = (__int128)INT64_MAX / 2;
-    *out_ns = (int64_t)(t < lo ? lo : (t > hi ? hi : t));
+    return (int64_t)(t < lo ? lo : (t > hi ? hi : t));
+}
+
+// loc a fixed offset
+bool crane_go_parse_time(const char* s, size_t n, int64_t tz_offset_s, int64_t* out_ns) {
+    int64_t local, nsec;
+    if (!parse_local(s, n, &local, &nsec)) return false;
+    *out_ns = to_ns(local - tz_offset_s, nsec);
+    return true;
+}
+
+// loc an IANA zone (tz.cpp: time.Date's offset choice)
+bool crane_go_parse_time_tz(const char* s, size_t n, const crane_tz* tz, int64_t* out_ns) {
+    int64_t local, nsec;
+    if (!parse_local(s, n, &local, &nsec)) return false;
+    *out_ns = to_ns(crane_tz_date(tz, local), nsec);
     return true;
 }
 
@@ -306,7 +326,10 @@ int crane_tz_offset(const char* tz_name, int64_t* offset_s) {
     return CRANE_E_INVALID;
 }
 
-void crane_parse_annotation(const char* s, size_t n, int64_t tz_offset_s, double* value, int64_t* ts_ns) {
+}  // extern "C"
+
+template <class ParseTime>
+static void parse_annotation(const char* s, size_t n, double* value, int64_t* ts_ns, ParseTime&& parse_time) {
     *value = 0;
     *ts_ns = CRANE_TS_INVALID;
     size_t comma = (size_t)-1, ncomma = 0;
@@ -319,15 +342,16 @@ void crane_parse_annotation(const char* s, size_t n, int64_t tz_offset_s, double
     const char* t = s + comma + 1;
     const size_t tn = n - comma - 1;
     int64_t ts;
-    if (tn < 5 || !crane_go_parse_time(t, tn, tz_offset_s, &ts)) return;  // stats.go:31-40
+    if (tn < 5 || !parse_time(t, tn, &ts)) return;  // stats.go:31-40
     double v;
     if (!crane_go_parse_float(s, comma, &v)) return;
     *value = v;
     *ts_ns = ts;
 }
 
-int crane_parse_annotations(int64_t n, const char* const* strs, const size_t* lens, int64_t tz_offset_s,
-                            double* value, int64_t* ts_ns, int32_t n_threads) {
+template <class One>
+static int parse_bulk(int64_t n, const char* const* strs, const size_t* lens, double* value, int64_t* ts_ns,
+                      int32_t n_threads, One&& one) {
     if (n < 0 || (n > 0 && (!strs || !lens || !value || !ts_ns))) return CRANE_E_INVALID;
     int64_t nt = n_threads > 0 ? n_threads : (int64_t)std::thread::hardware_concurrency();
     if (nt < 1) nt = 1;
@@ -341,7 +365,7 @@ int crane_parse_annotations(int64_t n, const char* const* strs, const size_t* le
                 value[i] = 0;
                 ts_ns[i] = CRANE_TS_INVALID;  // key not found (stats.go:52-55)
             } else {
-                crane_parse_annotation(strs[i], lens[i], tz_offset_s, &value[i], &ts_ns[i]);
+                one(strs[i], lens[i], &value[i], &ts_ns[i]);
             }
         }
     };
@@ -353,6 +377,33 @@ int crane_parse_annotations(int64_t n, const char* const* strs, const size_t* le
     for (int64_t t = 0; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
     for (auto& x : th) x.join();
     return CRANE_OK;
+}
+
+extern "C" {
+
+void crane_parse_annotation(const char* s, size_t n, int64_t tz_offset_s, double* value, int64_t* ts_ns) {
+    parse_annotation(s, n, value, ts_ns,
+                     [&](const char* t, size_t tn, int64_t* o) { return crane_go_parse_time(t, tn, tz_offset_s, o); });
+}
+
+void crane_parse_annotation_tz(const char* s, size_t n, const crane_tz* tz, double* value, int64_t* ts_ns) {
+    parse_annotation(s, n, value, ts_ns,
+                     [&](const char* t, size_t tn, int64_t* o) { return crane_go_parse_time_tz(t, tn, tz, o); });
+}
+
+int crane_parse_annotations(int64_t n, const char* const* strs, const size_t* lens, int64_t tz_offset_s,
+                            double* value, int64_t* ts_ns, int32_t n_threads) {
+    return parse_bulk(n, strs, lens, value, ts_ns, n_threads, [&](const char* s, size_t l, double* v, int64_t* t) {
+        crane_parse_annotation(s, l, tz_offset_s, v, t);
+    });
+}
+
+int crane_parse_annotations_tz(int64_t n, const char* const* strs, const size_t* lens, const crane_tz* tz,
+                               double* value, int64_t* ts_ns, int32_t n_threads) {
+    if (!tz) return CRANE_E_INVALID;
+    return parse_bulk(n, strs, lens, value, ts_ns, n_threads, [&](const char* s, size_t l, double* v, int64_t* t) {
+        crane_parse_annotation_tz(s, l, tz, v, t);
+    });
 }
 
 }  // extern "C"

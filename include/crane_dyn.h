@@ -92,6 +92,24 @@ void crane_parse_annotation(const char *s, size_t n, int64_t tz_offset_s, double
  * reference's per-call parsing (stats.go:51-76). */
 int crane_parse_annotations(int64_t n, const char *const *strs, const size_t *lens, int64_t tz_offset_s,
                             double *value, int64_t *ts_ns, int32_t n_threads);
+/* IANA zones (utils.GetLocation = time.LoadLocation($TZ), utils.go:35-45) with
+ * go1.17's semantics (tz.cpp): crane_tz_load reads the TZif file `name` from
+ * zoneinfo_dir, or $ZONEINFO then /usr/share/zoneinfo, /usr/share/lib/zoneinfo,
+ * /usr/lib/locale/TZ ("" and "UTC" = UTC; names with ".." or a leading '/' are
+ * invalid); a wall time becomes an instant as time.Date does, including its
+ * choice for skipped and repeated wall times.  The _tz parsers equal the
+ * fixed-offset ones otherwise.  crane_tz_lookup = Location.lookup (offset of
+ * the zone in effect at unix_s and that period [start, end)); crane_tz_date =
+ * time.Date's wall clock (seconds since the epoch as if UTC) -> Unix seconds. */
+typedef struct crane_tz crane_tz;
+int crane_tz_load(const char *name, const char *zoneinfo_dir, crane_tz **out);
+int crane_tz_load_bytes(const uint8_t *tzif, size_t n, crane_tz **out);
+void crane_tz_free(crane_tz *tz);
+int crane_tz_lookup(const crane_tz *tz, int64_t unix_s, int32_t *offset_s, int64_t *start_s, int64_t *end_s);
+int64_t crane_tz_date(const crane_tz *tz, int64_t local_s);
+void crane_parse_annotation_tz(const char *s, size_t n, const crane_tz *tz, double *value, int64_t *ts_ns);
+int crane_parse_annotations_tz(int64_t n, const char *const *strs, const size_t *lens, const crane_tz *tz,
+                               double *value, int64_t *ts_ns, int32_t n_threads);
 
 /* ------------------------------------------------------------------ engine */
 typedef struct crane_dyn crane_dyn;

@@ -30,6 +30,7 @@
 #include <memory>
 #include <mutex>
 #include <stdexcept>
+#include <cstdlib>
 #include <string>
 #include <thread>
 #include <typeinfo>
@@ -157,6 +158,7 @@ class DynamicScheduler {
     ~DynamicScheduler() {
         if (eng_) crane_dyn_destroy(eng_);
         if (doc_) crane_policy_free(doc_);
+        if (zone_) crane_tz_free(zone_);
     }
     DynamicScheduler(const DynamicScheduler&) = delete;
     DynamicScheduler& operator=(const DynamicScheduler&) = delete;
@@ -252,8 +254,11 @@ class DynamicScheduler {
         }
         std::vector<double> val((size_t)(M + 1) * N);
         std::vector<int64_t> ts((size_t)(M + 1) * N);
-        if (crane_parse_annotations((int64_t)strs.size(), strs.data(), lens.data(), tz_, val.data(), ts.data(),
-                                    parse_threads_)) {
+        const int prc = zone_ ? crane_parse_annotations_tz((int64_t)strs.size(), strs.data(), lens.data(), zone_,
+                                                           val.data(), ts.data(), parse_threads_)
+                              : crane_parse_annotations((int64_t)strs.size(), strs.data(), lens.data(), tz_,
+                                                        val.data(), ts.data(), parse_threads_);
+        if (prc) {
             *err = "annotation parse failed";
             return nullptr;
         }
@@ -315,6 +320,7 @@ class DynamicScheduler {
     Handle handle_;
     crane_policy_doc* doc_ = nullptr;
     crane_dyn* eng_ = nullptr;
+    crane_tz* zone_ = nullptr;  // the IANA zone of $TZ, or null: the fixed offset tz_
     int64_t tz_ = 8 * 3600;
     int32_t parse_threads_ = 16;  // the framework's parallelism (upstream default)
     std::mutex mu_;
@@ -334,8 +340,12 @@ inline std::pair<std::unique_ptr<DynamicScheduler>, std::string> NewDynamicSched
     std::unique_ptr<DynamicScheduler> ds(new DynamicScheduler());
     ds->doc_ = doc;
     ds->handle_ = h;
-    if (crane_tz_offset(nullptr, &ds->tz_))  // utils.GetLocation: $TZ, default Asia/Shanghai
-        return {nullptr, "unsupported time zone in $TZ"};
+    // utils.GetLocation: time.LoadLocation($TZ, default Asia/Shanghai) from tzdata; without
+    // tzdata files the fixed-offset zones (crane_tz_offset) still load
+    const char* tzenv = std::getenv("TZ");
+    const std::string zname = tzenv && *tzenv ? tzenv : "Asia/Shanghai";
+    if (crane_tz_load(zname.c_str(), nullptr, &ds->zone_) && crane_tz_offset(zname.c_str(), &ds->tz_))
+        return {nullptr, "unknown time zone " + zname};
     if (crane_dyn_create(crane_policy_view(doc), h.device, &ds->eng_)) {
         std::string e = ds->eng_ ? crane_dyn_last_error(ds->eng_) : "engine creation failed";
         return {nullptr, "failed to create the Dynamic engine: " + e};

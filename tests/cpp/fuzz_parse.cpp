@@ -13,7 +13,11 @@
 //     ns/pod to node" through crane_translate_event (csrc/events.cpp) — no
 //     crash, parts inside the message.
 //
-//   fuzz_parse <iterations> <seed> <policy.yaml>
+//  4. TZif files (tz.cpp, LoadLocationFromTZData): byte mutations and truncations
+//     of real zone files through crane_tz_load_bytes, lookups and wall-clock
+//     conversions with every zone that loads.
+//
+//   fuzz_parse <iterations> <seed> <policy.yaml> [tzif files...]
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -189,6 +193,47 @@ static int fuzz_events(long iters) {
     return 0;
 }
 
+static long n_tz_ok = 0;
+
+static int fuzz_tzif(long iters, const std::string& base) {
+    for (long it = 0; it < iters; ++it) {
+        std::string s = base;
+        const int k = (int)rnd(4);
+        for (int i = 0; i < k; ++i) {  // byte flips and truncations (headers, counts, footer)
+            if (s.empty()) break;
+            const uint64_t at = rnd(s.size());
+            if (rnd(4) == 0) s = s.substr(0, at);
+            else s[at] = (char)rnd(256);
+        }
+        uint8_t* buf = (uint8_t*)std::malloc(s.size() ? s.size() : 1);
+        std::memcpy(buf, s.data(), s.size());
+        crane_tz* tz = nullptr;
+        const int rc = crane_tz_load_bytes(buf, s.size(), &tz);
+        std::free(buf);
+        if (rc == 0) {
+            ++n_tz_ok;
+            for (int j = 0; j < 8; ++j) {
+                const int64_t t = (int64_t)(rng() % 8000000000ull) - 2000000000;
+                int32_t off;
+                int64_t st, en;
+                // (no containment check: like Go's, a period from the footer rule after the DST
+                // end runs to the year start + 365 days, a day short in leap years)
+                crane_tz_lookup(tz, t, &off, &st, &en);
+                (void)crane_tz_date(tz, t);
+            }
+            double v;
+            int64_t ts;
+            const std::string a = "0.5," + rand_time();
+            crane_parse_annotation_tz(a.data(), a.size(), tz, &v, &ts);
+            crane_tz_free(tz);
+        } else if (tz) {
+            std::fprintf(stderr, "tz error left a zone\n");
+            return 1;
+        }
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 4) return 2;
     const long iters = std::atol(argv[1]);
@@ -199,6 +244,14 @@ int main(int argc, char** argv) {
     int rc = fuzz_annotations(iters);
     if (!rc) rc = fuzz_policy(iters / 10, ss.str());
     if (!rc) rc = fuzz_events(iters / 4);
-    if (!rc) std::printf("ok %ld usable %ld policies %ld events %ld\n", iters, n_usable, n_policy_ok, n_event_ok);
+    for (int i = 4; i < argc && !rc; ++i) {
+        std::ifstream zf(argv[i], std::ios::binary);
+        std::stringstream zs;
+        zs << zf.rdbuf();
+        rc = fuzz_tzif(iters / 100, zs.str());
+    }
+    if (!rc)
+        std::printf("ok %ld usable %ld policies %ld events %ld zones %ld\n", iters, n_usable, n_policy_ok, n_event_ok,
+                    n_tz_ok);
     return rc;
 }

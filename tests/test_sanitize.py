@@ -1,8 +1,9 @@
 """AddressSanitizer + UndefinedBehaviorSanitizer build of the host parsers
-(crane-scheduler_amd/csrc/annotations.cpp, policy.cpp, events.cpp) driven by
-tests/cpp/fuzz_parse.cpp: random and mutated annotation values checked against
-the oracle's ParseFloat / ParseInLocation restatement, mutated policy
-documents, mutated scheduler events.  Host code only (no GPU sanitizers)."""
+(crane-scheduler_amd/csrc/annotations.cpp, policy.cpp, events.cpp, tz.cpp)
+driven by tests/cpp/fuzz_parse.cpp: random and mutated annotation values
+checked against the oracle's ParseFloat / ParseInLocation restatement, mutated
+policy documents, mutated scheduler events, mutated TZif files.  Host code only
+(no GPU sanitizers)."""
 import os
 import shutil
 import subprocess
@@ -25,7 +26,7 @@ def fuzz_exe(tmp_path_factory):
     exe = str(d / "fuzz_parse")
     subprocess.run(["g++", "-std=c++17", *SAN, "-pthread", "-I", os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tests", "cpp", "fuzz_parse.cpp"),
-                    *(os.path.join(CSRC, f) for f in ("annotations.cpp", "policy.cpp", "events.cpp")), obj,
+                    *(os.path.join(CSRC, f) for f in ("annotations.cpp", "policy.cpp", "events.cpp", "tz.cpp")), obj,
                     "-o", exe, "-lm"], check=True)
     return exe
 
@@ -33,8 +34,14 @@ def fuzz_exe(tmp_path_factory):
 @pytest.mark.parametrize("seed", [1, 20251016])
 def test_parsers_under_asan_ubsan(fuzz_exe, seed):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
-    r = subprocess.run([fuzz_exe, "300000", str(seed), os.path.join(ROOT, "tests", "golden", "policy_default.yaml")],
-                       capture_output=True, text=True, env=env, timeout=300)
+    args = [fuzz_exe, "300000", str(seed), os.path.join(ROOT, "tests", "golden", "policy_default.yaml")]
+    try:  # TZif files to mutate (the tzdata package's zoneinfo), if installed
+        import tzdata
+        zi = os.path.join(os.path.dirname(tzdata.__file__), "zoneinfo")
+        args += [os.path.join(zi, z) for z in ("America/New_York", "Australia/Lord_Howe", "Asia/Shanghai")]
+    except ImportError:
+        pass
+    r = subprocess.run(args, capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert r.stdout.startswith("ok 300000")
     # the grammar must keep producing usable values, loadable policies and parsed events
