@@ -142,6 +142,10 @@ def parse():
     ap.add_argument("--no-greedy", action="store_true", help="skip the config-5 sequential-greedy measurement")
     ap.add_argument("--inflight", type=int, default=4,
                     help="independent pod batches in flight (engines x HIP streams); 1 = one batch at a time")
+    ap.add_argument("--ar-group", type=int, default=0,
+                    help="N>1: batches per keys all-reduce (a multiple of --inflight; 0 = 8 x inflight)")
+    ap.add_argument("--rehearse-collective", action="store_true",
+                    help="run the N>1 collective path on one rank (under torchrun)")
     ap.add_argument("--no-extras", action="store_true", help="headline step only (matrix / drop-in / controller legs off)")
     ap.add_argument("--leg", default="all", choices=("all", "matrix2", "matrix3"),
                     help="matrix2 / matrix3: only that per-pair leg (for per-kernel PMC passes)")
@@ -338,7 +342,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # the collective path (RCCL all-reduce of the keys); --rehearse-collective runs it on a
+    # single rank (torchrun --nproc-per-node 1) to exercise it on a one-GPU box
+    coll = world > 1 or args.rehearse_collective
+    if coll:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -393,16 +400,47 @@ def main():
     sh = stream.cuda_stream
 
     sh_k = [s_.cuda_stream for s_ in streams]
+    # N > 1: one RCCL max all-reduce per group of G batches over their keys [G][P], on its
+    # own stream after the group's K streams (the collective's latency and host cost are
+    # per call; rehearsed on one rank: G = 4 / 8 / 16 / 32 -> 0.0272 / 0.0249 / 0.0175 /
+    # 0.0164 ms per batch against 0.0144 without the collective); two key buffers
+    # alternate so a group's batches never overwrite keys a collective still reads
+    G = max(K, args.ar_group or 8 * K) // K * K  # batches per collective, a multiple of K
+    if coll:
+        kbufs = [torch.empty((G, P), dtype=torch.int64, device=dev) for _ in range(2)]
+        cstream = torch.cuda.Stream(dev)
+        ar_done = [None, None]
+        ev_s = [torch.cuda.Event() for _ in range(K)]  # (reused: record() re-arms an event)
+        ev_ar = [torch.cuda.Event(), torch.cuda.Event()]
+
+    def collect(b, nb):
+        for jj in range(min(nb, K)):
+            ev_s[jj].record(streams[jj])
+            cstream.wait_event(ev_s[jj])
+        with torch.cuda.stream(cstream):
+            dist.all_reduce(kbufs[b][:nb], op=dist.ReduceOp.MAX)  # RCCL over xGMI
+        ev_ar[b].record(cstream)
+        ar_done[b] = ev_ar[b]
 
     def step(collective=True, i=0):
         j = i % K
-        engs[j].step_keys_async(now_sync, now_sync, d_now, d_flags, d_keys_k[j], sh_k[j])
-        if world > 1 and collective:
-            with torch.cuda.stream(streams[j]):  # (the collective waits on the batch's stream)
-                dist.all_reduce(d_keys_k[j], op=dist.ReduceOp.MAX)  # RCCL over xGMI
+        if coll and collective:
+            b, row = (i // G) % 2, i % G
+            if row < K and ar_done[b] is not None:  # this buffer's previous collective has read it
+                streams[j].wait_event(ar_done[b])
+            engs[j].step_keys_async(now_sync, now_sync, d_now, d_flags, kbufs[b][row], sh_k[j])
+            if row == G - 1:
+                collect(b, G)
+        else:
+            engs[j].step_keys_async(now_sync, now_sync, d_now, d_flags, d_keys_k[j], sh_k[j])
+
+    def flush(n_steps):  # the last, partial group's collective
+        if coll and n_steps % G:
+            collect((n_steps // G) % 2, n_steps % G)
 
     for i in range(args.warmup):
         step(i=i)
+    flush(args.warmup)
     torch.cuda.synchronize(dev)
     graph = None
     if args.graph:
@@ -417,37 +455,50 @@ def main():
             step(i=i)
         else:
             graph.replay()
-            if world > 1:
+            if coll:
                 dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)
 
-    if world > 1:
+    if coll:  # the timed groups start from fresh buffers
+        ar_done[0] = ar_done[1] = None
+
+    if coll:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
         timed_step(i)
+    if graph is None:
+        flush(args.steps)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if coll:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if coll:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_step = elapsed * 1e3 / args.steps
+    if coll and graph is None:  # the last group's keys (all-reduced over the ranks)
+        last = kbufs[((args.steps - 1) // G) % 2]
+        d_keys = last[0]
+        keys_agree = all(torch.equal(last[0], last[jj]) for jj in range((args.steps - 1) % G + 1))
+    else:
+        keys_agree = all(torch.equal(d_keys, k) for k in d_keys_k)
     keys = d_keys.cpu().numpy()
-    keys_agree = all(torch.equal(d_keys, k) for k in d_keys_k)
     # one batch's latency: the same step with nothing else in flight (outside the timed region)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     for _ in range(max(10, args.steps // 4)):
-        step()  # (engine 0 only: each batch waits for the previous one on its stream)
+        step(collective=False)  # (engine 0 only: each batch waits for the previous one on its stream)
+        if coll:
+            with torch.cuda.stream(streams[0]):
+                dist.all_reduce(d_keys_k[0], op=dist.ReduceOp.MAX)
     torch.cuda.synchronize(dev)
     batch_latency_ms = (time.perf_counter() - t1) * 1e3 / max(10, args.steps // 4)
     # per-kernel durations (dispatch-stamped) of the same step, outside the timed region
     kt = kernel_times(eng, lambda: step(collective=False), args.steps)
     ar_ms = None
-    if world > 1:
+    if coll:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(10):
@@ -617,7 +668,9 @@ def main():
                        "batches_in_flight": K},
             "batches_in_flight": {"k": K, "how": "K engines (own copy of the shard's nodes, binding log, scratch) on "
                                                 "K HIP streams, batch i on engine i % K; every batch runs the whole "
-                                                "step", "keys_agree": keys_agree,
+                                                "step" + (f"; one RCCL max all-reduce per group of {G} batches' keys "
+                                                          f"[{G}][P] on its own stream" if coll else ""),
+                                  "keys_agree": keys_agree,
                                   "batch_latency_ms": round(batch_latency_ms, 4)},
             "placements_per_s": round(placements, 1),
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
@@ -634,7 +687,7 @@ def main():
         print(json.dumps(line), flush=True)
     for e in engs:
         e.close()
-    if world > 1:
+    if coll:
         dist.destroy_process_group()
 
 
