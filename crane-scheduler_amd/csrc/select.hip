@@ -102,6 +102,21 @@ __global__ __launch_bounds__(256) void k_sel_fth(SelArgs a, int64_t* __restrict_
 // K-th set bit); a round holding more than kChQ pod ends repeats the ballots for
 // the next ones.
 constexpr int kChT = 1024, kChU = 8, kChW = kChT / 64, kChQ = 4;
+
+// position of the r-th set bit (r >= 1) of m: halving popcount search
+__device__ __forceinline__ int nth_set_bit(unsigned long long m, int r) {
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const int c = __popcll(m & ((1ull << w) - 1ull));
+        if (c < r) {
+            r -= c;
+            m >>= w;
+            pos += w;
+        }
+    }
+    return pos;
+}
 constexpr int kChC = kChU * kChW;         // 64-position chunks per round (chunk c = u * kChW + wave)
 constexpr int64_t kChR = 64LL * kChC;     // positions per round
 constexpr int kChPB = 1024;               // pod times cached per block
@@ -199,9 +214,7 @@ __global__ __launch_bounds__(kChT) void k_sel_chain(SelArgs a, const int64_t* __
                             int64_t r = need - before;  // rank within this lane's chunks
                             int h = cnt2[0] >= r ? 0 : 1;
                             if (h) r -= cnt2[0];
-                            unsigned long long m = mm[h];
-                            for (int64_t i = 1; i < r; ++i) m &= m - 1;  // drop the lowest r - 1 bits
-                            end = x0 + 64LL * (2 * lane + h) + (__ffsll(m) - 1);
+                            end = x0 + 64LL * (2 * lane + h) + nth_set_bit(mm[h], (int)r);
                         }
                         end = readlane64(end, L);
                     } else if (lim <= x0 + kChR) {
