@@ -348,12 +348,12 @@ StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk, int32_t blk_per_w
     constexpr int64_t kMaxWg = 2048;
     const int32_t bpw = blk_per_wg > 0 ? blk_per_wg : kK3sBlkPerWg;
     int64_t R = (std::max<int32_t>(nblk, 1) + bpw - 1) / bpw;
-    R = std::min<int64_t>(R, std::max<int64_t>(1, kMaxWg / std::max<int64_t>(g.ngroups, 1)));
+    if (blk_per_wg <= 0) R = std::min<int64_t>(R, std::max<int64_t>(1, kMaxWg / std::max<int64_t>(g.ngroups, 1)));
     R = std::max<int64_t>(R, (nblk + kK3sMaxBlk - 1) / kK3sMaxBlk);
     if (nblk >= 8) {  // XCD groups (k3s_eval): a multiple of 8 (down while over kMaxWg workgroups),
                       // each group's slices <= kK3sMaxBlk blocks
         R = (R + 7) / 8 * 8;
-        if (R * g.ngroups > kMaxWg) R -= 8;
+        if (blk_per_wg <= 0 && R * g.ngroups > kMaxWg) R -= 8;
         R = std::max<int64_t>(8, R);
         while (((nblk + 7) / 8 + R / 8 - 1) / (R / 8) > kK3sMaxBlk) R += 8;
     }
