@@ -491,6 +491,23 @@ class Engine:
                                                   None if d_flags is None else C.c_void_p(d_flags.data_ptr()),
                                                   C.c_void_p(d_keys.data_ptr()), stream))
 
+    def step_keys_fn(self, d_now, d_flags, d_keys, stream=None):
+        """step_keys_async bound to fixed device buffers and stream: returns f(now_ns, hv_ts_ns).
+        The pointer conversions happen once, so a loop of steps pays only the C call."""
+        P = d_now.numel()
+        assert d_keys.numel() == P and d_now.dtype.itemsize == 8 and d_keys.dtype.itemsize == 8
+        fn, h = lib.crane_dyn_step_keys_async, self.h
+        pn, pk = C.c_void_p(d_now.data_ptr()), C.c_void_p(d_keys.data_ptr())
+        pf = None if d_flags is None else C.c_void_p(d_flags.data_ptr())
+        check = self._check
+
+        def step(now_ns, hv_ts_ns):
+            rc = fn(h, now_ns, hv_ts_ns, P, pn, pf, pk, stream)
+            if rc:
+                check(rc)
+
+        return step
+
     def greedy(self, n_pods, now_ns, pod_flags=None):
         fl = None if pod_flags is None else np.ascontiguousarray(pod_flags, np.uint8)
         ch = np.empty(n_pods, np.int64)

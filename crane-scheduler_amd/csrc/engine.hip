@@ -104,6 +104,9 @@ struct Options {
     int step_rows = 1;        // 1: producers write per-tile record ranges for K3s, 0: K3s searches
     int k3s_blocks = 0;       // K3s producer blocks per workgroup aimed for: 0 automatic
     int k2x_threads = 512;    // dedupe K2 workgroup size: 256, 512 or 1024
+    int step_lds_cap = 1 << 30;  // K1: one-step records per kind staged in LDS at most (0: always st.stage)
+    int dbg_stop = 0;         // TEMP probe: 1 stop after K1, 2 stop after K2x
+    int dbg_k1_lds = 0;
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
@@ -177,6 +180,7 @@ struct crane_dyn {
     DevBuf<long long> sel_keys;
     DevBuf<Mid> smid;
     DevBuf<Step1> sstep1;
+    DevBuf<Step1> sstage;  // K1's one-step staging past its LDS (StepTables::stage)
     DevBuf<int32_t> spm1, ssm0;   // prefix / suffix key maxima of the sorted Step1 records
     DevBuf<int4> srows;           // per (pod tile, producer block): uniform keys + record ranges
     // kernel timing (crane_dyn_set_profiling)
@@ -409,6 +413,7 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
         a.hv_ts = h->hv_ts.p;
     }
     a.threads = k1_bs(h);
+    a.lds_extra = h->opt.dbg_k1_lds;
     a.trace = (h->N + a.threads - 1) / a.threads <= kTraceWgs ? h->trace_region(1) : nullptr;
     HIPTRY(h, launch_node_pass(h->shape, a, st, step));
     if (consume) {
@@ -445,6 +450,7 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     const int64_t s1pad = 2 * g.npad, mstride = (int64_t)bs * (step_breakpoints(h->shape) - 1);
     const int64_t mpad = (int64_t)nblk * mstride;
     HIPTRY(h, h->sstep1.reserve((size_t)(2 * s1pad)));
+    if (sp.fuse) HIPTRY(h, h->sstage.reserve((size_t)(2 * s1pad)));
     HIPTRY(h, h->spm1.reserve((size_t)(2 * s1pad)));
     HIPTRY(h, h->ssm0.reserve((size_t)(2 * s1pad)));
     HIPTRY(h, h->smid.reserve((size_t)(2 * mpad)));
@@ -453,6 +459,8 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     t.cnt = h->scnt.p;
     t.flat = h->scnt.p + (size_t)nblk * 4;
     t.single = h->sstep1.p;
+    t.stage = sp.fuse ? h->sstage.p : nullptr;
+    t.lds_cap = h->opt.step_lds_cap;
     t.pm1 = h->spm1.p;
     t.sm0 = h->ssm0.p;
     t.mid = h->smid.p;
@@ -491,6 +499,7 @@ static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_k
         }
         HIPTRY(h, launch_step_nodes(h->shape, h->rec.p, h->N, h->dp.wsum, h->dp.noprio, sp.stt, sp.g, h->stile.p, st));
     }
+    if (h->opt.dbg_stop == 1) return CRANE_OK;
     HIPTRY(h, launch_step_pairs(h->shape, h->N, h->node_offset, P, d_keys, sp.stt, sp.g, h->sperm.p, h->spnow.p, h->stile.p, st));
     return CRANE_OK;
 }
@@ -606,7 +615,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
     h->mFs.release(); h->mIs.release(); h->mgi.release();
     h->trace.release();
-    h->sperm.release(); h->scnt.release(); h->stile.release(); h->spnow.release(); h->smid.release(); h->sstep1.release();
+    h->sperm.release(); h->scnt.release(); h->stile.release(); h->spnow.release(); h->smid.release(); h->sstep1.release(); h->sstage.release();
     h->spm1.release(); h->ssm0.release(); h->srows.release();
     h->sel_fth.release(); h->sel_win.release(); h->sel_state.release(); h->sel_keys.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -641,6 +650,9 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "step_rows" && range(0, 1)) o.step_rows = (int)value;
     else if (n == "k3s_blocks" && range(0, 256)) o.k3s_blocks = (int)value;
     else if (n == "k2x_threads" && (value == 256 || value == 512 || value == 1024)) o.k2x_threads = (int)value;
+    else if (n == "dbg_stop") o.dbg_stop = (int)value;
+    else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
+    else if (n == "dbg_k1_lds") o.dbg_k1_lds = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
         if (o.trace) {
@@ -962,6 +974,7 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
     bool pods_done = false;
     rc = hot_values_locked(h, now_ns, hv_ts_ns, st, h->opt.k3p_in_k2 ? &pp : nullptr, &pods_done);
     if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, st);
+    if (h->opt.dbg_stop == 2) return rc;
     if (!rc) rc = step_rest(h, sp, P, keys, st);
     return rc;
 }

@@ -111,13 +111,16 @@ __global__ __launch_bounds__(kK2Threads) void k2_hot_count(const int32_t* __rest
 // STEP: also build the K3 step tables of the pod batch (K3a fused, step.hip):
 // the record is classified straight from registers.
 // keys-only step: LDS staging for this many stepped records per workgroup (the sorted
-// one-step records reuse it after the emit: 112 x 160 B >= 4 x 256 x 16 B); a node past
-// it builds its own records.  With the buffers below a workgroup takes < 40 KB of LDS,
-// four per CU.
+// one-step records reuse it after the emit); a node past it builds its own records.
+// One-step records: LDS staging for kK1S1Cap per kind (a block with more goes through
+// st.stage).  With the buffers below a workgroup takes ~30 KB of LDS, five per CU.
 constexpr int kK1RecCap = 112;
+constexpr int kK1S1Cap = 256;
 
 template <int PD, int PR, int kK1Threads, bool STEP>
-__global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step) {
+// 4x6 shape: registers for 5 waves per SIMD (with the ~30 KB of LDS, 5 workgroups per CU)
+__global__ __launch_bounds__(kK1Threads) __attribute__((amdgpu_waves_per_eu(PD * PR <= 24 ? 5 : 1)))
+void k1_node_pass(K1Args a, K1Step step) {
     const DevPolicy& pol = a.pol;
     const int64_t N = a.N;
     const double* __restrict__ val = a.val;
@@ -141,13 +144,14 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     __shared__ int32_t nq;                      // stepped (node, kind) items queued for the emit
     __shared__ uint32_t q[STEP ? 2 * kK1Threads : 1];
     __shared__ int32_t qm[STEP ? 2 * kK1Threads : 1];  // first middle-piece slot of queued items
-    // one-step records per kind (2 per node at most): staging; sorted copy over the records'
-    // LDS once the emit has read them (or past them when the records are written out)
-    // (one buffer with the dedupe-form K2 buckets hxh below: those are read before the
-    // step epilogue's first barrier, the staging is written after it)
+    // one-step records per kind (2 per node at most, CAP staged in LDS): staging; sorted
+    // copy over the records' LDS once the emit has read them (or past them when the
+    // records are written out) (one buffer with the dedupe-form K2 buckets hxh below:
+    // those are read before the step epilogue's first barrier, the staging is written after it)
+    constexpr int CAP = kK1S1Cap < 2 * kK1Threads ? kK1S1Cap : 2 * kK1Threads;
     constexpr int kHxWords = kMaxWin * kK1Threads;
-    constexpr int kUnion = (STEP ? 4 * kK1Threads * (int)sizeof(Step1) : 0) > 4 * kHxWords
-                               ? 4 * kK1Threads * (int)sizeof(Step1)
+    constexpr int kUnion = (STEP ? 2 * CAP * (int)sizeof(Step1) : 0) > 4 * kHxWords
+                               ? 2 * CAP * (int)sizeof(Step1)
                                : 4 * kHxWords;
     __shared__ __attribute__((aligned(16))) unsigned char ush[kUnion];
     Step1* s1l = reinterpret_cast<Step1*>(ush);
@@ -167,7 +171,7 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
     // dedupe-form K2: the count/offset words of this block's first source
     // regions go out before the SoA loads, so the dependent entry loads below
     // wait on them, not on the whole SoA batch
-    constexpr int kHxPer = 4, kHxFirst = 4, kHxRun = 8;
+    constexpr int kHxPer = 3, kHxFirst = 4, kHxRun = 8;
     uint32_t co0[kHxPer];
     if (hx) {
 #pragma unroll
@@ -356,20 +360,29 @@ __global__ __launch_bounds__(kK1Threads) void k1_node_pass(K1Args a, K1Step step
         }
         step_publish<kK1Threads>(so, ssh, step.st, blk);  // (its barrier also orders lrec and the queue)
         CRANE_TSTAMP(a.trace, blockIdx.x, 3);
+        // one-step records staged in LDS, or (more of a kind than it holds) in st.stage
+        const bool g1 = max(ssh.lc[0][0], ssh.lc[1][0]) > min(CAP, step.st.lds_cap);
+        Step1* s1b = g1 ? step.st.stage + blk * 2 * step.st.bs : s1l;
+        const int64_t kst = g1 ? step.st.s1pad : (int64_t)CAP;
+        // (a node past the staging emits first: its record then dies before the queue's)
+        if (self_emit) step_emit<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, so, step.st, blk, s1b, kst);
         // the queued items are built densely by the first lanes of the workgroup
         for (int w = threadIdx.x; w < nq; w += kK1Threads) {
             const uint32_t it = q[w];
             const int o = (int)(it & 0xFFF);
             step_emit_one<PD, PR>(lrec[it >> 24], first + o, (int)((it >> 12) & 1), (int32_t)((it >> 14) & 0x3FF),
                                   qm[w], ((it >> 13) & 1) != 0, tmin, tmax, step.wsum, step.noprio, step.st, blk,
-                                  s1l);
+                                  s1b, kst);
         }
-        if (self_emit) step_emit<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, so, step.st, blk, s1l);
         __syncthreads();
         CRANE_TSTAMP(a.trace, blockIdx.x, 5);
-        step_sort_publish<kK1Threads>(s1l, s1s, ssh, step.st, blk);
+        if (g1) step_sort_publish_global<kK1Threads>(ssh, step.st, blk);
+        else step_sort_publish<kK1Threads, CAP>(s1l, s1s, ssh, step.st, blk);
         CRANE_TSTAMP(a.trace, blockIdx.x, 6);
-        if (step.st.rows) step_tile_rows<kK1Threads>(s1l, s1s, ssh, step.st, blk, &tpre);
+        if (step.st.rows) {
+            if (g1) step_tile_rows<kK1Threads, CAP, true>(s1l, s1s, ssh, step.st, blk, &tpre);
+            else step_tile_rows<kK1Threads, CAP, false>(s1l, s1s, ssh, step.st, blk, &tpre);
+        }
     } else {
         __syncthreads();
     }
@@ -392,15 +405,15 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
     // + the sorted one-step records past the node records when both are kept (kernel above)
     // records: every node's when written out (+ the sorted one-step records past them); keys-only
     // step: kK1RecCap stepped records, the sorted one-step records over them after the emit
-    const size_t lds = a.out ? sizeof(NodeRec<PD, PR>) * T + (step ? 4 * sizeof(Step1) * T : 0)
-                             : std::max(sizeof(NodeRec<PD, PR>) * (size_t)std::min(T, kK1RecCap),
-                                        step ? 4 * sizeof(Step1) * T : (size_t)0);
-    if (!a.out && step && sizeof(NodeRec<PD, PR>) * (size_t)std::min(T, kK1RecCap) < 4 * sizeof(Step1) * T)
-        return hipErrorInvalidValue;  // (the sorted records must fit over the staging: see kK1RecCap)
+    const size_t s1 = step ? 2 * sizeof(Step1) * (size_t)std::min(kK1S1Cap, 2 * T) : 0;  // sorted copy
+    const size_t lds = a.out ? sizeof(NodeRec<PD, PR>) * T + s1
+                             : std::max(sizeof(NodeRec<PD, PR>) * (size_t)std::min(T, kK1RecCap), s1);
+    if (step && !step->st.stage) return hipErrorInvalidValue;
+    const size_t ldsx = lds + (size_t)a.lds_extra;
     const K1Step sa = step ? *step : K1Step{};
     const char* nm = step ? "k1_node_pass+k3a_steps" : "k1_node_pass";
     if (T == 256)
-        return step ? klaunch(nm, k1_node_pass<PD, PR, 256, true>, dim3(grid), dim3(256), lds, st, a, sa)
+        return step ? klaunch(nm, k1_node_pass<PD, PR, 256, true>, dim3(grid), dim3(256), ldsx, st, a, sa)
                     : klaunch(nm, k1_node_pass<PD, PR, 256, false>, dim3(grid), dim3(256), lds, st, a, sa);
     return step ? klaunch(nm, k1_node_pass<PD, PR, 128, true>, dim3(grid), dim3(128), lds, st, a, sa)
                 : klaunch(nm, k1_node_pass<PD, PR, 128, false>, dim3(grid), dim3(128), lds, st, a, sa);

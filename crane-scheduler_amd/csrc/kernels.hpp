@@ -222,6 +222,10 @@ struct StepTables {
     // block's sorted one-step records stepping inside the tile's range of that kind
     int4* rows;
     unsigned long long* trace;  // K3s phase trace or null
+    // K1's one-step staging for blocks with more records of a kind than its LDS holds
+    // (or than lds_cap, 0 = always): same indexing as single
+    Step1* stage;
+    int32_t lds_cap;
 };
 constexpr int64_t kStepRowsMax = 1LL << 24;  // tile x block rows (256 MiB); larger batches: K3s searches
 __host__ __device__ inline int64_t s1_at(const StepTables& st, int T, int64_t b) {
@@ -278,6 +282,7 @@ struct K1Args {
     const uint32_t* hx_CO;
     int32_t hx_nblk;
     int32_t threads;        // workgroup size: 128 or 256
+    int32_t lds_extra;      // TEMP probe
     unsigned long long* trace;  // phase trace or null
 };
 // step (optional): also build the K3 step tables of a pod batch (K3a fused).

@@ -224,13 +224,15 @@ __device__ __forceinline__ void step_count(const NodeRec<PD, PR>& r, int64_t n, 
     kind(std::integral_constant<int, 1>{}, o.flat1, o.slot1, o.mslot1, o.nb1, o.multi1);
 }
 
-// Phase 2, one (node, kind): the node's one-step records go to the workgroup's LDS
-// staging s1l[T * 2 * bs + slot] (step_sort_publish writes them out sorted), its
-// middle pieces straight to st.mid.
+// Phase 2, one (node, kind): the node's one-step records go to the workgroup's
+// staging s1b[T * kst + slot] (LDS, or st.stage when the block's records exceed the
+// LDS staging; step_sort_publish writes them out sorted), its middle pieces
+// straight to st.mid.
 template <int PD, int PR>
 __device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t n, int T, int32_t slot,
                                               int32_t mslot, bool multi, int64_t tmin, int64_t tmax, double wsum,
-                                              int32_t noprio, const StepTables& st, int64_t blk, Step1* s1l) {
+                                              int32_t noprio, const StepTables& st, int64_t blk, Step1* s1b,
+                                              int64_t kst) {
     constexpr int NB = PR + 2;
     int64_t c[NB];
 #pragma unroll
@@ -250,7 +252,7 @@ __device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t 
         const int32_t f = score_at<PD, PR>(t, r, wsum, noprio);
         return (T == 1 || !(t < r.e_fail)) ? pack_key(f, n) : -1;
     };
-    Step1* s1 = s1l + T * 2 * st.bs;
+    Step1* s1 = s1b + T * kst;
     const int32_t k0 = key(tmin);
     if (!multi) {
         Step1 v;
@@ -301,11 +303,11 @@ __device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t 
 template <int PD, int PR>
 __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
                                           double wsum, int32_t noprio, const StepSlots& o,
-                                          const StepTables& st, int64_t blk, Step1* s1l) {
+                                          const StepTables& st, int64_t blk, Step1* s1b, int64_t kst) {
     if (o.slot0 >= 0)
-        step_emit_one<PD, PR>(r, n, 0, o.slot0, o.mslot0, o.multi0, tmin, tmax, wsum, noprio, st, blk, s1l);
+        step_emit_one<PD, PR>(r, n, 0, o.slot0, o.mslot0, o.multi0, tmin, tmax, wsum, noprio, st, blk, s1b, kst);
     if (o.slot1 >= 0)
-        step_emit_one<PD, PR>(r, n, 1, o.slot1, o.mslot1, o.multi1, tmin, tmax, wsum, noprio, st, blk, s1l);
+        step_emit_one<PD, PR>(r, n, 1, o.slot1, o.mslot1, o.multi1, tmin, tmax, wsum, noprio, st, blk, s1b, kst);
 }
 
 // Work item of the compacted emit: owner thread | kind << 12 | multi << 13 | slot << 14 | rs << 24,
@@ -369,12 +371,12 @@ __device__ __forceinline__ int32_t count_le(const Step1* a, int32_t n, int64_t t
 // record's key from one prefix and one suffix maximum: step_tile_rows writes that
 // uniform key (with the flat maximum) and [jl, jh) per tile into st.rows (when set),
 // so K3s starts from them; without rows K3s searches the records itself.
-// srt: LDS scratch [4 * BS] records; s1l is reused for the maxima.  Every thread calls
-// it (barriers); sh.fm holds the per-wave flat maxima (step_publish).
-template <int BS>
+// s1l: LDS staging [2][CAP] records (CAP >= either kind's count), srt: LDS scratch
+// [2][CAP]; s1l is reused for the maxima.  Every thread calls it (barriers); sh.fm
+// holds the per-wave flat maxima (step_publish).
+template <int BS, int CAP = 2 * BS>
 __device__ __forceinline__ void step_sort_publish(Step1* s1l, Step1* srt, const StepShared& sh,
                                                   const StepTables& st, int64_t blk) {
-    constexpr int CAP = 2 * BS;  // one-step records per kind and block
     const int n0 = sh.lc[0][0], n1 = sh.lc[1][0];
     // rank sort (ties by slot): typically a few dozen records per kind
     for (int i = threadIdx.x; i < n0 + n1; i += BS) {
@@ -448,6 +450,59 @@ __device__ __forceinline__ void step_sort_publish(Step1* s1l, Step1* srt, const 
     }
 }
 
+// The same for a block whose records exceed the LDS staging: staged in st.stage
+// (same indexing as st.single), ranked straight into st.single, maxima into pm1 / sm0.
+template <int BS>
+__device__ __forceinline__ void step_sort_publish_global(const StepShared& sh, const StepTables& st, int64_t blk) {
+    const int n0 = sh.lc[0][0], n1 = sh.lc[1][0];
+    for (int i = threadIdx.x; i < n0 + n1; i += BS) {
+        const int T = i >= n0;
+        const int k = T ? i - n0 : i;
+        const int n = T ? n1 : n0;
+        const Step1* a = st.stage + s1_at(st, T, blk);
+        const Step1 v = a[k];
+        int rank = 0;
+        for (int j = 0; j < n; ++j) {
+            const int64_t b = a[j].bp;
+            rank += (b < v.bp) || (b == v.bp && j < k);
+        }
+        st.single[s1_at(st, T, blk) + rank] = v;
+    }
+    __syncthreads();
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w < 2) {
+        const int T = w, n = T ? n1 : n0;
+        const int64_t base = s1_at(st, T, blk);
+        const Step1* a = st.single + base;
+        int32_t carry = -1;
+        for (int c0 = 0; c0 < n; c0 += 64) {
+            const int i = c0 + lane;
+            int32_t v = i < n ? a[i].k1 : -1;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t x = __shfl_up(v, o);
+                if (lane >= o) v = max(v, x);
+            }
+            v = max(v, carry);
+            if (i < n) st.pm1[base + i] = v;
+            carry = __shfl(v, 63);
+        }
+        carry = -1;
+        for (int c0 = (n - 1) & ~63; c0 >= 0 && n > 0; c0 -= 64) {
+            const int i = c0 + lane;
+            int32_t v = i < n ? a[i].k0 : -1;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t y = __shfl_down(v, o);
+                if (lane + o < 64) v = max(v, y);
+            }
+            v = max(v, carry);
+            if (i < n) st.sm0[base + i] = v;
+            carry = __shfl(v, 0);
+        }
+    }
+}
+
 // The tile rows (st.rows set): per pod tile t, the block's uniform key per kind and
 // the range [jl, jh) of its sorted one-step records stepping inside the tile's range
 // (after step_sort_publish: srt sorted, s1l holding the prefix / suffix maxima).
@@ -457,10 +512,11 @@ __device__ __forceinline__ void tile_prefetch(const StepTables& st, int64_t* pre
     const int x = threadIdx.x;  // item x: tile x / 4, kind (x / 2) % 2, lo / hi
     *pre = (x >> 2) < st.ntiles ? st.tiles[kTileStat * (x >> 2) + ((x >> 1) & 1) * 2 + (x & 1)] : 0;
 }
-template <int BS>
+// G: the block's records went through st.stage (step_sort_publish_global): the
+// searches read st.single / pm1 / sm0 instead of the LDS copies.
+template <int BS, int CAP = 2 * BS, bool G = false>
 __device__ __forceinline__ void step_tile_rows(const Step1* s1l, const Step1* srt, const StepShared& sh,
                                                const StepTables& st, int64_t blk, const int64_t* pre) {
-    constexpr int CAP = 2 * BS;
     const int n0 = sh.lc[0][0], n1 = sh.lc[1][0];
     const int32_t* pmL = reinterpret_cast<const int32_t*>(s1l);
     const int32_t* smL = pmL + 2 * CAP;
@@ -481,9 +537,16 @@ __device__ __forceinline__ void step_tile_rows(const Step1* s1l, const Step1* sr
         int32_t c = 0, u = -1;
         if (t < st.ntiles) {
             const int64_t v = i0 == 0 ? *pre : st.tiles[kTileStat * t + 2 * T + hi_b];
-            c = count_le(srt + T * CAP, n, v);
-            if (!hi_b && c > 0) u = pmL[T * CAP + c - 1];  // records stepped by lo: keys after
-            if (hi_b && c < n) u = smL[T * CAP + c];       // records stepping after hi: keys before
+            if (G) {
+                const int64_t base = s1_at(st, T, blk);
+                c = count_le(st.single + base, n, v);
+                if (!hi_b && c > 0) u = st.pm1[base + c - 1];
+                if (hi_b && c < n) u = st.sm0[base + c];
+            } else {
+                c = count_le(srt + T * CAP, n, v);
+                if (!hi_b && c > 0) u = pmL[T * CAP + c - 1];  // records stepped by lo: keys after
+                if (hi_b && c < n) u = smL[T * CAP + c];       // records stepping after hi: keys before
+            }
         }
         const int32_t co = __shfl_xor(c, 1), uo = __shfl_xor(u, 1);
         const int32_t jl = hi_b ? co : c, jh = hi_b ? c : co;

@@ -22,14 +22,16 @@ from crane_dyn import synth  # noqa: E402
 
 def _check(spec, c, now, ds):
     off, osc, och = oracle_soa(spec, c, now=now, ds=ds)
-    # K3s from the producers' per-tile rows, and searching the records itself
-    for rows in (1, 0):
-        eng = engine_for(spec, c, opts={"step_rows": rows})
+    # K3s from the producers' per-tile rows, and searching the records itself; K1's
+    # one-step records through its LDS staging, through st.stage always (cap 0), or
+    # per block as its counts exceed a small cap
+    for rows, cap in ((1, 1 << 30), (0, 1 << 30), (1, 0), (0, 6), (1, 6)):
+        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap})
         _, _, ch, cs = eng.eval(now, ds)
-        assert np.array_equal(ch, och), rows
+        assert np.array_equal(ch, och), (rows, cap)
         for p in range(len(now)):
             ok = (off[p] < 0) | bool(ds[p])
-            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, p)
+            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, p)
         eng.close()
 
 

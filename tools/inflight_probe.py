@@ -9,6 +9,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -23,6 +24,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=3)
 ap.add_argument("--steps", type=int, default=200)
 ap.add_argument("--inflight", default="1,2,3,4")
+ap.add_argument("--bound", action="store_true", help="pre-bound step functions (Engine.step_keys_fn)")
+ap.add_argument("--threads", action="store_true", help="one host thread per engine enqueues its batches")
 ap.add_argument("--opt", action="append", default=[], help="engine option name=value (repeatable)")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
@@ -34,7 +37,7 @@ if args.config == 4:
 c = synth.make_cluster(spec, N, P, n_bindings=B, seed=20250215 + args.config * 1000)
 c.now, c.ds = synth.make_pods(P, seed=20250215 + args.config)
 now = int(synth.NOW0_NS)
-out = {"config": args.config, "nodes": N, "pods": P, "bindings": B, "opts": args.opt}
+out = {"bound": args.bound, "threads": args.threads, "config": args.config, "nodes": N, "pods": P, "bindings": B, "opts": args.opt}
 for K in [int(x) for x in args.inflight.split(",")]:
     engs, streams, keys = [], [], []
     for _ in range(K):
@@ -51,16 +54,32 @@ for K in [int(x) for x in args.inflight.split(",")]:
     d_now = torch.from_numpy(c.now).to(dev)
     d_flags = torch.from_numpy(c.ds).to(dev)
 
+    fns = [e.step_keys_fn(d_now, d_flags, keys[j], streams[j].cuda_stream) for j, e in enumerate(engs)]
+
     def step(i):
         j = i % K
-        engs[j].step_keys_async(now, now, d_now, d_flags, keys[j], streams[j].cuda_stream)
+        if args.bound:
+            fns[j](now, now)
+        else:
+            engs[j].step_keys_async(now, now, d_now, d_flags, keys[j], streams[j].cuda_stream)
 
     for i in range(10):
         step(i)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
+    if args.threads:
+        def run(j):
+            f = fns[j]
+            for _ in range(j, args.steps, K):
+                f(now, now)
+        th = [threading.Thread(target=run, args=(j,)) for j in range(K)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    else:
+        for i in range(args.steps):
+            step(i)
     t_host = time.perf_counter() - t0  # enqueue time alone
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / args.steps
