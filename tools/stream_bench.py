@@ -5,8 +5,10 @@
 One step = K2 refresh (the binned form at this size, or the hash form) then a
 keys-only eval (k3p_pods, k1_node_pass+k3a_steps, k3s_eval).  Kernel times come
 from the engine's dispatch-stamped events (crane_dyn_set_profiling).  Before
-the refresh and before the eval a 1 GiB scratch buffer is written, so the
-256 MiB Infinity Cache holds none of the inputs (MI355X_MICROARCH.md).
+the refresh and before the eval a 1 GiB scratch buffer is written (--flush write:
+the Infinity Cache is then full of dirty lines that are written back while the
+timed kernels read) or read (--flush read: clean lines), so the 256 MiB Infinity
+Cache holds none of the inputs (MI355X_MICROARCH.md).
 Algorithmic bytes:
   k2 (all K2 kernels)     : 12 per binding read + 4*W per node (window counts written)
   k1_node_pass+k3a_steps  : 16*M (val+ts SoA) + 8*W (buckets read + zeroed) + 8 (hot value) per node
@@ -33,6 +35,9 @@ ap.add_argument("--pods", type=int, default=10_000)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--k2", default="auto,hash")
 ap.add_argument("--keep-records", action="store_true")
+ap.add_argument("--flush", default="write", choices=("write", "read"),
+                help="evict the caches by writing the 1 GiB scratch (its dirty lines are written back during "
+                     "the timed kernels) or by reading it (clean lines)")
 args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -61,17 +66,27 @@ alg = {
     "k2 (all K2 kernels)": B * 12 + 4 * W * N,
     "k1_node_pass+k3a_steps": N * (16 * M + 8 * W + 8 + (REC if args.keep_records else 0)),
 }
+sink = torch.empty(1, dtype=torch.int64, device=dev)
+
+
+def flush(r):
+    if args.flush == "write":
+        scratch.fill_(r & 0xFF)
+    else:
+        torch.sum(scratch.view(torch.int64), dim=0, keepdim=True, out=sink)
+
+
 res = {}
 keys_ref = None
 for k2 in args.k2.split(","):
     eng.set_option("k2_form", {"auto": 0, "binned": 1, "hash": 2}[k2])
     acc = {}
     for r in range(args.reps + 1):
-        scratch.fill_(r & 0xFF)
+        flush(r)
         eng.set_profiling(True)
         eng.refresh_hot_values_async(now, now, sh)
         t_k2 = eng.stage_times()
-        scratch.fill_((r + 7) & 0xFF)
+        flush(r + 7)
         eng.set_profiling(True)
         eng.eval_keys_async(d_now, d_flags, d_keys, sh)
         t_ev = eng.stage_times()
@@ -94,5 +109,5 @@ for k2 in args.k2.split(","):
         stages[name] = e
     res[k2] = stages
 out = {"keep_records": args.keep_records, "nodes": N, "bindings": B, "bindings_in_window": b_in, "pods": P,
-       "cold_cache": "1 GiB scratch write before the refresh and before the eval", "by_k2_mode": res}
+       "cold_cache": f"1 GiB scratch {args.flush} before the refresh and before the eval", "by_k2_mode": res}
 print(json.dumps(out))
