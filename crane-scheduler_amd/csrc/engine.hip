@@ -175,7 +175,7 @@ struct crane_dyn {
     DevBuf<int64_t> mFs, mIs, mgi;
     DevBuf<unsigned long long> trace;  // [3][kTraceWgs][8] phase stamps (option "trace")
     DevBuf<int32_t> sperm, scnt;  // K3 step path scratch (step.hip)
-    DevBuf<int64_t> stile, spnow;
+    DevBuf<int64_t> stile, spnow, sbatch;
     DevBuf<int64_t> sel_fth, sel_win, sel_state;  // framework selection (select.hip)
     DevBuf<long long> sel_keys;
     DevBuf<Mid> smid;
@@ -444,6 +444,10 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     const StepGeometry& g = sp.g;
     HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
     HIPTRY(h, h->stile.reserve((size_t)(kTileStat * g.ntiles)));
+    if (!h->sbatch.p) {  // {tmin, tmax, tile counter}: the counter starts at 0, K3p re-arms it
+        HIPTRY(h, h->sbatch.reserve(4));
+        HIPTRY(h, hipMemset(h->sbatch.p, 0, 4 * sizeof(int64_t)));
+    }
     HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
     HIPTRY(h, h->scnt.reserve((size_t)std::max<int32_t>(nblk, 1) * 6));  // cnt [nblk][4] + flat [nblk][2]
     // per kind and producer block: 2 * bs one-step records, bs * (breakpoints - 1) middle pieces
@@ -482,14 +486,14 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
 
 static int step_pods(crane_dyn* h, const StepPlan& sp, int64_t P, const int64_t* d_now, const uint8_t* d_flags,
                      long long* d_keys, hipStream_t st) {
-    HIPTRY(h, launch_step_pods(d_now, d_flags, P, d_keys, sp.g, h->sperm.p, h->spnow.p, h->stile.p, st));
+    HIPTRY(h, launch_step_pods(d_now, d_flags, P, d_keys, h->sbatch.p, sp.g, h->sperm.p, h->spnow.p, h->stile.p, st));
     return CRANE_OK;
 }
 
 static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_keys, hipStream_t st) {
     if (P == 0) return CRANE_OK;
     if (sp.fuse) {
-        K1Step ks{h->stile.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, sp.stt};
+        K1Step ks{h->stile.p, h->sbatch.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, sp.stt};
         int rc = node_pass_locked(h, st, nullptr, &ks);
         if (rc) return rc;
     } else {
@@ -615,7 +619,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
     h->mFs.release(); h->mIs.release(); h->mgi.release();
     h->trace.release();
-    h->sperm.release(); h->scnt.release(); h->stile.release(); h->spnow.release(); h->smid.release(); h->sstep1.release(); h->sstage.release();
+    h->sperm.release(); h->scnt.release(); h->stile.release(); h->sbatch.release(); h->spnow.release(); h->smid.release(); h->sstep1.release(); h->sstage.release();
     h->spm1.release(); h->ssm0.release(); h->srows.release();
     h->sel_fth.release(); h->sel_win.release(); h->sel_state.release(); h->sel_keys.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -970,7 +974,7 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
     StepPlan sp;
     int rc = step_plan(h, P, sp);
     if (rc) return rc;
-    const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys};
+    const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys, h->sbatch.p};
     bool pods_done = false;
     rc = hot_values_locked(h, now_ns, hv_ts_ns, st, h->opt.k3p_in_k2 ? &pp : nullptr, &pods_done);
     if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, st);

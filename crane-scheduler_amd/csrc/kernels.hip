@@ -140,7 +140,6 @@ void k1_node_pass(K1Args a, K1Step step) {
     const int64_t n = first + threadIdx.x;
     __shared__ StepShared ssh;
     int64_t tmin = 0, tmax = 0;
-    TileBounds tbr;
     __shared__ int32_t nq;                      // stepped (node, kind) items queued for the emit
     __shared__ uint32_t q[STEP ? 2 * kK1Threads : 1];
     __shared__ int32_t qm[STEP ? 2 * kK1Threads : 1];  // first middle-piece slot of queued items
@@ -264,7 +263,8 @@ void k1_node_pass(K1Args a, K1Step step) {
     // the batch time range partials: issued after the SoA loads, reduced after the compute
     int64_t tpre = 0;  // this thread's first tile-row bound (step_tile_rows)
     if (STEP) {
-        batch_range_wave_load(step.tile_mm, step.ntiles, tbr);
+        tmin = step.batch[0];  // K3p folded the batch range
+        tmax = step.batch[1];
         if (step.st.rows) tile_prefetch(step.st, &tpre);
     }
     if (n < N) {
@@ -344,20 +344,13 @@ void k1_node_pass(K1Args a, K1Step step) {
     }
     CRANE_TSTAMP(a.trace, blockIdx.x, 2);
     if (STEP) {
-        batch_range_wave_reduce(step.tile_mm, step.ntiles, tbr, tmin, tmax);
         if (!hx) __syncthreads();  // orders the lc / nq / nrec resets before the counting below
                                    // (the dedupe form's barriers above already do)
-        if (n < N) step_count<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, ssh, so);
-        bool self_emit = false;
-        if (so.slot0 >= 0 || so.slot1 >= 0) {  // stepped (a few %): record to LDS, items to the queue
-            int rs = threadIdx.x;
-            if (!out) {  // keys-only: stepped records compacted into kK1RecCap LDS slots
-                rs = atomicAdd(&nrec, 1);
-                if (rs < kK1RecCap) lrec[rs] = r;
-            }
-            if (rs < kK1RecCap || out) step_queue(so, &nq, q, qm, rs);
-            else self_emit = true;  // (past the staging: this thread builds its own records)
-        }
+        // stepped (a few %): keys-only, the records are compacted into kK1RecCap LDS slots
+        // (a node past them builds its own); the (node, kind) items go to the queue
+        bool self_emit;
+        step_count_queue<PD, PR, kK1RecCap>(r, n < N, n, tmin, tmax, step.wsum, step.noprio, out != nullptr, ssh,
+                                            &nrec, &nq, q, qm, lrec, so, self_emit);
         step_publish<kK1Threads>(so, ssh, step.st, blk);  // (its barrier also orders lrec and the queue)
         CRANE_TSTAMP(a.trace, blockIdx.x, 3);
         // one-step records staged in LDS, or (more of a kind than it holds) in st.stage
@@ -369,6 +362,7 @@ void k1_node_pass(K1Args a, K1Step step) {
         // the queued items are built densely by the first lanes of the workgroup
         for (int w = threadIdx.x; w < nq; w += kK1Threads) {
             const uint32_t it = q[w];
+            if (it == ~0u) continue;  // a self-emitted node's
             const int o = (int)(it & 0xFFF);
             step_emit_one<PD, PR>(lrec[it >> 24], first + o, (int)((it >> 12) & 1), (int32_t)((it >> 14) & 0x3FF),
                                   qm[w], ((it >> 13) & 1) != 0, tmin, tmax, step.wsum, step.noprio, step.st, blk,

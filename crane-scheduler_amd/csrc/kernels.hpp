@@ -175,6 +175,9 @@ struct PodPrep {
     int64_t* pnow;
     int64_t* tile_mm;
     long long* keys;
+    // the batch's time range {tmin, tmax, tile counter (u32)}: the last tile of K3p to finish
+    // folds every tile's stats into it (the counter starts at 0 and is re-armed), or null
+    int64_t* batch;
 };
 constexpr int kHxRegion = 2048;
 HotPart hot_dedupe_geometry(int64_t B, int64_t N, int32_t W, int32_t bs);
@@ -239,7 +242,7 @@ constexpr int kK3sMaxBlk = 256;  // producer blocks per K3s workgroup (one lane 
 int step_breakpoints(int shape);  // in-range expiries per node and kind at most: PR + 2
 StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk, int32_t blk_per_wg = 0);
 // K3p: perm, pnow [ntiles * 1024], tile_mm [kTileStat * ntiles]; initialises keys[0..P) to -1
-hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys,
+hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys, int64_t* batch,
                             const StepGeometry& g, int32_t* perm, int64_t* pnow, int64_t* tile_mm, hipStream_t s);
 // K3a: step tables from NodeRecs in HBM (after K3p)
 hipError_t launch_step_nodes(int shape, const void* rec, int64_t N, double wsum, int32_t noprio,
@@ -251,6 +254,7 @@ hipError_t launch_step_pairs(int shape, int64_t N, int64_t node_offset, int64_t 
 // K1's fused step form: the node pass also builds the step tables of a pod batch
 struct K1Step {
     const int64_t* tile_mm;  // K3p's per-tile stats (kTileStat)
+    const int64_t* batch;    // K3p's folded {tmin, tmax} of the batch
     int32_t ntiles;
     int32_t noprio;
     double wsum;

@@ -132,6 +132,24 @@ __device__ __forceinline__ void k3p_tile(const int64_t t, const PodPrep& pp, uns
         ts[3] = e1 > e0 ? (int64_t)(ku[e1 - 1] ^ kSign) : INT64_MIN;
         ts[4] = e0;
         ts[5] = e1 - e0;
+        if (pp.batch) {
+            // the batch's time range, once for every consumer: the last tile to finish folds
+            // the tiles' stats (its acquire sees every other tile's stores, released by their
+            // increments) and re-arms the counter for the next batch
+            unsigned* ctr = reinterpret_cast<unsigned*>(pp.batch + 2);
+            const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            if (prev + 1u == (unsigned)pp.ntiles) {
+                int64_t mn = INT64_MAX, mx = INT64_MIN;
+                for (int64_t i = 0; i < pp.ntiles; ++i) {
+                    const int64_t* q = pp.tile_mm + kTileStat * i;
+                    mn = min(mn, min(q[0], q[2]));
+                    mx = max(mx, max(q[1], q[3]));
+                }
+                pp.batch[0] = mn;
+                pp.batch[1] = mx;
+                __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
 }
 

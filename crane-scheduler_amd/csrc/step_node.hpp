@@ -29,6 +29,45 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
 
 __device__ __forceinline__ int32_t pack_key(int32_t f, int64_t n) { return (f << 24) | (int32_t)(0xFFFFFF - n); }
 
+// ---- wave primitives on DPP (VALU lane moves, no LDS round trip like ds_bpermute's
+// __shfl*).  Every lane of the 64-lane wave must be active (uniform control flow).
+// dpp_ctrl: quad_perm 0x00-0xFF, row_shr:k 0x110 + k, row_ror:k 0x120 + k, row_bcast:15 0x142,
+// row_bcast:31 0x143; lanes whose source is outside the row keep `id` (bound_ctrl off).
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ int32_t dpp_or(int32_t id, int32_t v) {
+    return __builtin_amdgcn_update_dpp(id, v, CTRL, ROWS, 0xF, false);
+}
+// maximum over the wave, uniform
+__device__ __forceinline__ int32_t wave_max(int32_t v) {
+    v = max(v, dpp_or<0xB1>(v, v));   // quad_perm [1,0,3,2]
+    v = max(v, dpp_or<0x4E>(v, v));   // quad_perm [2,3,0,1]
+    v = max(v, dpp_or<0x124>(v, v));  // row_ror:4
+    v = max(v, dpp_or<0x128>(v, v));  // row_ror:8: every lane holds its row's maximum
+    return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+               max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+// inclusive prefix (lane order) under an associative op with identity id: Hillis-Steele
+// within each row of 16, then rows 1 / 3 take row 0 / 2's total, rows 2-3 rows 0-1's
+template <class Op>
+__device__ __forceinline__ int32_t wave_scan(int32_t v, int32_t id, Op op) {
+    v = op(v, dpp_or<0x111>(id, v));
+    v = op(v, dpp_or<0x112>(id, v));
+    v = op(v, dpp_or<0x114>(id, v));
+    v = op(v, dpp_or<0x118>(id, v));
+    v = op(v, dpp_or<0x142, 0xA>(id, v));
+    v = op(v, dpp_or<0x143, 0xC>(id, v));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
+    return (uint32_t)wave_scan((int32_t)v, 0, [](int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); });
+}
+__device__ __forceinline__ int32_t wave_scan_max(int32_t v) {
+    return wave_scan(v, INT32_MIN, [](int32_t a, int32_t b) { return max(a, b); });
+}
+// lane i takes lane (i ^ 1)'s value / lane i + 2's within its quad (lanes 0, 1 of a quad)
+__device__ __forceinline__ int32_t quad_xor1(int32_t v) { return dpp_or<0xB1>(v, v); }
+__device__ __forceinline__ int32_t quad_down2(int32_t v) { return dpp_or<0xEE>(v, v); }
+
 // Exact clamped Score of (pod at time t, node) — the literal int64 restatement
 // of stats.go:114-138 + plugins.go:91-93, the semantics of K3's eval_pair and
 // score_exact (kernels.hip).
@@ -326,14 +365,108 @@ __device__ __forceinline__ void step_queue(const StepSlots& o, int32_t* nq, uint
     }
 }
 
+// K1's form of step_count + stepped-record staging + step_queue, called by every thread
+// of the workgroup (valid: the thread has a node): the per-lane counts are prefix-summed
+// across the wave (DPP) and one lane takes the wave's spans with one LDS atomic per
+// counter, instead of a chain of per-lane returning atomics.  Slots are assigned in lane
+// order (any order is a valid one: K3s takes maxima).  keep: records written out (the
+// record slot is the thread's; every item queued), else the stepped records are staged in
+// lrec[0, CAP) and a node past the staging builds its own (self_emit; its queue items
+// are marked ~0u).
+template <int PD, int PR, int CAP>
+__device__ __forceinline__ void step_count_queue(const NodeRec<PD, PR>& r, bool valid, int64_t n, int64_t tmin,
+                                                 int64_t tmax, double wsum, int32_t noprio, bool keep,
+                                                 StepShared& sh, int32_t* nrec, int32_t* nq, uint32_t* q,
+                                                 int32_t* qm, NodeRec<PD, PR>* lrec, StepSlots& o,
+                                                 bool& self_emit) {
+    const int32_t s0 = score_at<PD, PR>(tmin, r, wsum, noprio);
+    int cnt1 = 0;
+    int64_t mn1 = INT64_MAX, mx1 = INT64_MIN;
+    auto add = [&](int64_t e, int& c, int64_t& mn, int64_t& mx) {
+        const bool in = e > tmin && e <= tmax;
+        c += in;
+        mn = in ? min(mn, e) : mn;
+        mx = in ? max(mx, e) : mx;
+    };
+#pragma unroll
+    for (int k = 0; k < PR; ++k) add(r.e_prio[k], cnt1, mn1, mx1);
+    add(r.e_hv, cnt1, mn1, mx1);
+    int cnt0 = cnt1;
+    int64_t mn0 = mn1, mx0 = mx1;
+    add(r.e_fail, cnt0, mn0, mx0);  // DaemonSet pods bypass the Filter
+    if (!valid) cnt0 = cnt1 = 0;
+    o.multi0 = cnt0 > 0 && mn0 != mx0;
+    o.multi1 = cnt1 > 0 && mn1 != mx1;
+    o.nb0 = (int8_t)cnt0;
+    o.nb1 = (int8_t)cnt1;
+    o.flat0 = valid && cnt0 == 0 ? key_of<PD, PR>(0, tmin, s0, r, n) : -1;
+    o.flat1 = valid && cnt1 == 0 ? key_of<PD, PR>(1, tmin, s0, r, n) : -1;
+    // per lane: one-step records | middle pieces << 16 per kind; stepped | queue items << 16
+    const uint32_t w0 = (cnt0 ? (o.multi0 ? 2u : 1u) : 0u) | (o.multi0 ? (uint32_t)(cnt0 - 1) << 16 : 0u);
+    const uint32_t w1 = (cnt1 ? (o.multi1 ? 2u : 1u) : 0u) | (o.multi1 ? (uint32_t)(cnt1 - 1) << 16 : 0u);
+    const uint32_t w2 = ((cnt0 | cnt1) ? 1u : 0u) | (((cnt0 ? 1u : 0u) + (cnt1 ? 1u : 0u)) << 16);
+    // exclusive prefixes and the wave's totals (lane 63's inclusive prefix)
+    uint32_t e0 = wave_scan_add(w0);
+    const uint32_t t0 = __builtin_amdgcn_readlane(e0, 63);
+    e0 -= w0;
+    uint32_t e1 = wave_scan_add(w1);
+    const uint32_t t1 = __builtin_amdgcn_readlane(e1, 63);
+    e1 -= w1;
+    uint32_t e2 = wave_scan_add(w2);
+    const uint32_t t2 = __builtin_amdgcn_readlane(e2, 63);
+    e2 -= w2;
+    int32_t b[6] = {0, 0, 0, 0, 0, 0};
+    if ((threadIdx.x & 63) == 63) {
+        if (t0) {
+            b[0] = atomicAdd(&sh.lc[0][0], (int32_t)(t0 & 0xFFFF));
+            b[1] = atomicAdd(&sh.lc[0][1], (int32_t)(t0 >> 16));
+        }
+        if (t1) {
+            b[2] = atomicAdd(&sh.lc[1][0], (int32_t)(t1 & 0xFFFF));
+            b[3] = atomicAdd(&sh.lc[1][1], (int32_t)(t1 >> 16));
+        }
+        if (t2) {
+            b[4] = atomicAdd(nrec, (int32_t)(t2 & 0xFFFF));
+            b[5] = atomicAdd(nq, (int32_t)(t2 >> 16));
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) b[k] = __builtin_amdgcn_readlane(b[k], 63);
+    o.slot0 = cnt0 ? b[0] + (int32_t)(e0 & 0xFFFF) : -1;
+    o.mslot0 = o.multi0 ? b[1] + (int32_t)(e0 >> 16) : 0;
+    o.slot1 = cnt1 ? b[2] + (int32_t)(e1 & 0xFFFF) : -1;
+    o.mslot1 = o.multi1 ? b[3] + (int32_t)(e1 >> 16) : 0;
+    self_emit = false;
+    if (cnt0 | cnt1) {
+        int rs = b[4] + (int32_t)(e2 & 0xFFFF);
+        bool staged = true;
+        if (keep) rs = threadIdx.x;
+        else if (rs < CAP) lrec[rs] = r;
+        else staged = false;
+        int qi = b[5] + (int32_t)(e2 >> 16);
+        if (cnt0) {
+            q[qi] = staged ? threadIdx.x | ((uint32_t)o.multi0 << 13) | ((uint32_t)o.slot0 << 14) | ((uint32_t)rs << 24)
+                           : ~0u;
+            qm[qi] = o.mslot0;
+            ++qi;
+        }
+        if (cnt1) {
+            q[qi] = staged ? threadIdx.x | (1u << 12) | ((uint32_t)o.multi1 << 13) | ((uint32_t)o.slot1 << 14) |
+                                 ((uint32_t)rs << 24)
+                           : ~0u;
+            qm[qi] = o.mslot1;
+        }
+        self_emit = !staged;
+    }
+}
+
 // Workgroup epilogue: the workgroup's flat-key maxima and record counts go to
 // its own slots (producer block blk) of the step tables (plain stores, no global atomics).  Every
 // thread calls it (barrier); sh.lc must have been zeroed before step_count.
 template <int BS>
 __device__ __forceinline__ void step_publish(const StepSlots& o, StepShared& sh, const StepTables& st, int64_t blk) {
     auto wmax = [&](int T, int32_t m) {
-#pragma unroll
-        for (int s = 32; s >= 1; s >>= 1) m = max(m, __shfl_xor(m, s));
+        m = wave_max(m);
         if ((threadIdx.x & 63) == 0) sh.fm[T][threadIdx.x >> 6] = m;
     };
     wmax(0, o.flat0);
@@ -418,34 +551,23 @@ __device__ __forceinline__ void step_sort_publish(Step1* s1l, Step1* srt, const 
         int32_t carry = -1;
         for (int c0 = 0; c0 < n; c0 += 64) {
             const int i = c0 + lane;
-            int32_t v = i < n ? a[i].k1 : -1;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t x = __shfl_up(v, o);
-                if (lane >= o) v = max(v, x);
-            }
-            v = max(v, carry);
+            const int32_t v = max(wave_scan_max(i < n ? a[i].k1 : -1), carry);
             if (i < n) {
                 st.pm1[base + i] = v;
                 pmL[T * CAP + i] = v;
             }
-            carry = __shfl(v, 63);
+            carry = __builtin_amdgcn_readlane(v, 63);
         }
+        // suffix maxima: lane l takes index c0 + 63 - l, so a prefix in lane order
         carry = -1;
         for (int c0 = (n - 1) & ~63; c0 >= 0 && n > 0; c0 -= 64) {
-            const int i = c0 + lane;
-            int32_t v = i < n ? a[i].k0 : -1;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t y = __shfl_down(v, o);
-                if (lane + o < 64) v = max(v, y);
-            }
-            v = max(v, carry);
+            const int i = c0 + 63 - lane;
+            const int32_t v = max(wave_scan_max(i < n ? a[i].k0 : -1), carry);
             if (i < n) {
                 st.sm0[base + i] = v;
                 smL[T * CAP + i] = v;
             }
-            carry = __shfl(v, 0);
+            carry = __builtin_amdgcn_readlane(v, 63);
         }
     }
 }
@@ -477,28 +599,16 @@ __device__ __forceinline__ void step_sort_publish_global(const StepShared& sh, c
         int32_t carry = -1;
         for (int c0 = 0; c0 < n; c0 += 64) {
             const int i = c0 + lane;
-            int32_t v = i < n ? a[i].k1 : -1;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t x = __shfl_up(v, o);
-                if (lane >= o) v = max(v, x);
-            }
-            v = max(v, carry);
+            const int32_t v = max(wave_scan_max(i < n ? a[i].k1 : -1), carry);
             if (i < n) st.pm1[base + i] = v;
-            carry = __shfl(v, 63);
+            carry = __builtin_amdgcn_readlane(v, 63);
         }
         carry = -1;
         for (int c0 = (n - 1) & ~63; c0 >= 0 && n > 0; c0 -= 64) {
-            const int i = c0 + lane;
-            int32_t v = i < n ? a[i].k0 : -1;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t y = __shfl_down(v, o);
-                if (lane + o < 64) v = max(v, y);
-            }
-            v = max(v, carry);
+            const int i = c0 + 63 - lane;
+            const int32_t v = max(wave_scan_max(i < n ? a[i].k0 : -1), carry);
             if (i < n) st.sm0[base + i] = v;
-            carry = __shfl(v, 0);
+            carry = __builtin_amdgcn_readlane(v, 63);
         }
     }
 }
@@ -548,11 +658,11 @@ __device__ __forceinline__ void step_tile_rows(const Step1* s1l, const Step1* sr
                 if (hi_b && c < n) u = smL[T * CAP + c];       // records stepping after hi: keys before
             }
         }
-        const int32_t co = __shfl_xor(c, 1), uo = __shfl_xor(u, 1);
+        const int32_t co = quad_xor1(c), uo = quad_xor1(u);
         const int32_t jl = hi_b ? co : c, jh = hi_b ? c : co;
         // a kind without pods here (lo = INT64_MAX, hi = INT64_MIN) gives jl = n > jh = 0
         const int32_t um = jl > jh ? -1 : max(fl[T], max(u, uo)), jp = jl > jh ? 0 : (jl | (jh << 16));
-        const int32_t um1 = __shfl_down(um, 2), jp1 = __shfl_down(jp, 2);
+        const int32_t um1 = quad_down2(um), jp1 = quad_down2(jp);
         if ((i & 3) == 0 && t < st.ntiles) st.rows[(int64_t)t * st.nblk + blk] = make_int4(um, um1, jp, jp1);
     }
 }

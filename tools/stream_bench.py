@@ -35,9 +35,10 @@ ap.add_argument("--pods", type=int, default=10_000)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--k2", default="auto,hash")
 ap.add_argument("--keep-records", action="store_true")
-ap.add_argument("--flush", default="write", choices=("write", "read"),
+ap.add_argument("--flush", default="read", choices=("write", "read"),
                 help="evict the caches by writing the 1 GiB scratch (its dirty lines are written back during "
                      "the timed kernels) or by reading it (clean lines)")
+ap.add_argument("--opt", action="append", default=[], help="engine option name=value (repeatable)")
 args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -47,6 +48,9 @@ c = synth.make_cluster(spec, N, P, n_bindings=B, seed=7)
 c.now, c.ds = synth.make_pods(P, seed=8)
 eng = cd.Engine(cd.Policy(spec), 0)
 eng.set_option("k1_keep_records", int(args.keep_records))
+for o in args.opt:
+    k, v = o.split("=")
+    eng.set_option(k, int(v))
 val, ts, _ = c.rows(eng.metric_names)
 eng.upload_nodes(val, ts, c.hv, c.hv_ts)
 eng.upload_bindings(c.b_node, c.b_ts)
