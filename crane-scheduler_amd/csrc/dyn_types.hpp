@@ -31,6 +31,7 @@ struct DevPolicy {
     int32_t noprio;   // policy has no priorities at all -> node score 0 (stats.go:116-120)
     int32_t pad0;
     double wsum;      // sum of ALL priority weights in policy order (stats.go:131)
+    double winv;      // 1 / wsum when |wsum| is a normal power of two (exact reciprocal), else 0
     int32_t pred_slot[kMaxPred];
     double pred_limit[kMaxPred];
     int64_t pred_dur[kMaxPred];   // period + 5m (getActiveDuration, stats.go:140-150)

@@ -290,6 +290,12 @@ static int flatten_policy(crane_dyn* h, const crane_policy* pol) {
     if ((int)h->slot_names.size() > kMaxSlots) return h->fail(CRANE_E_INVALID, "more than 32 metric keys");
     dp.n_slots = (int32_t)h->slot_names.size();
     dp.wsum = wsum;
+    {
+        int e = 0;
+        const double m = std::frexp(wsum, &e);  // wsum = m * 2^e
+        dp.winv = (m == 0.5 || m == -0.5) && std::isnormal(wsum) && e - 1 <= 1022 ? std::ldexp(2.0 * m, 1 - e) : 0.0;
+        if (dp.winv != 0.0 && dp.winv * wsum != 1.0) dp.winv = 0.0;
+    }
     dp.noprio = pol->n_prio == 0;
     if (pol->n_hot > kMaxWin) return h->fail(CRANE_E_INVALID, "more than 8 hotValue windows");
     dp.n_win = pol->n_hot;
@@ -493,7 +499,7 @@ static int step_pods(crane_dyn* h, const StepPlan& sp, int64_t P, const int64_t*
 static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_keys, hipStream_t st) {
     if (P == 0) return CRANE_OK;
     if (sp.fuse) {
-        K1Step ks{h->stile.p, h->sbatch.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, sp.stt};
+        K1Step ks{h->stile.p, h->sbatch.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, h->dp.winv, sp.stt};
         int rc = node_pass_locked(h, st, nullptr, &ks);
         if (rc) return rc;
     } else {

@@ -349,8 +349,8 @@ void k1_node_pass(K1Args a, K1Step step) {
         // stepped (a few %): keys-only, the records are compacted into kK1RecCap LDS slots
         // (a node past them builds its own); the (node, kind) items go to the queue
         bool self_emit;
-        step_count_queue<PD, PR, kK1RecCap>(r, n < N, n, tmin, tmax, step.wsum, step.noprio, out != nullptr, ssh,
-                                            &nrec, &nq, q, qm, lrec, so, self_emit);
+        step_count_queue<PD, PR, kK1RecCap>(r, n < N, n, tmin, tmax, step.wsum, step.winv, step.noprio,
+                                            out != nullptr, ssh, &nrec, &nq, q, qm, lrec, so, self_emit);
         step_publish<kK1Threads>(so, ssh, step.st, blk);  // (its barrier also orders lrec and the queue)
         CRANE_TSTAMP(a.trace, blockIdx.x, 3);
         // one-step records staged in LDS, or (more of a kind than it holds) in st.stage
@@ -358,7 +358,8 @@ void k1_node_pass(K1Args a, K1Step step) {
         Step1* s1b = g1 ? step.st.stage + blk * 2 * step.st.bs : s1l;
         const int64_t kst = g1 ? step.st.s1pad : (int64_t)CAP;
         // (a node past the staging emits first: its record then dies before the queue's)
-        if (self_emit) step_emit<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, so, step.st, blk, s1b, kst);
+        if (self_emit)
+            step_emit<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, so, step.st, blk, s1b, kst, step.winv);
         // the queued items are built densely by the first lanes of the workgroup
         for (int w = threadIdx.x; w < nq; w += kK1Threads) {
             const uint32_t it = q[w];
@@ -366,7 +367,7 @@ void k1_node_pass(K1Args a, K1Step step) {
             const int o = (int)(it & 0xFFF);
             step_emit_one<PD, PR>(lrec[it >> 24], first + o, (int)((it >> 12) & 1), (int32_t)((it >> 14) & 0x3FF),
                                   qm[w], ((it >> 13) & 1) != 0, tmin, tmax, step.wsum, step.noprio, step.st, blk,
-                                  s1b, kst);
+                                  s1b, kst, step.winv);
         }
         __syncthreads();
         CRANE_TSTAMP(a.trace, blockIdx.x, 5);

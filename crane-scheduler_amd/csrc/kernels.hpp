@@ -258,6 +258,7 @@ struct K1Step {
     int32_t ntiles;
     int32_t noprio;
     double wsum;
+    double winv;             // 1 / wsum when |wsum| is a power of two, else 0 (score_at)
     StepTables st;
 };
 

@@ -72,14 +72,18 @@ __device__ __forceinline__ int32_t quad_down2(int32_t v) { return dpp_or<0xEE>(v
 // of stats.go:114-138 + plugins.go:91-93, the semantics of K3's eval_pair and
 // score_exact (kernels.hip).
 template <int PD, int PR>
-__device__ __forceinline__ int32_t score_at(int64_t t, const NodeRec<PD, PR>& r, double wsum, int32_t noprio) {
+// winv: 1 / wsum when |wsum| is a power of two (the default policy's weights sum to 2.0), else
+// 0: the reciprocal is then exact and s * winv the same correctly rounded quotient as s / wsum,
+// one multiply instead of the division sequence (a uniform branch).
+__device__ __forceinline__ int32_t score_at(int64_t t, const NodeRec<PD, PR>& r, double wsum, int32_t noprio,
+                                          double winv = 0.0) {
     double s = 0.0;
 #pragma unroll
     for (int k = 0; k < PR; ++k)
         if (t < r.e_prio[k]) s += r.t[k];  // stats.go:124-133, policy order
     int64_t base = 0;
     if (!noprio) {
-        const double q = s / wsum;  // stats.go:135 int(score / weight), Go CVTTSD2SQ
+        const double q = winv != 0.0 ? s * winv : s / wsum;  // stats.go:135 int(score / weight), Go CVTTSD2SQ
         base = (q >= -9223372036854775808.0 && q < 9223372036854775808.0) ? (int64_t)q : INT64_MIN;
     }
     const int64_t pen = t < r.e_hv ? r.pen : 0;
@@ -271,7 +275,7 @@ template <int PD, int PR>
 __device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t n, int T, int32_t slot,
                                               int32_t mslot, bool multi, int64_t tmin, int64_t tmax, double wsum,
                                               int32_t noprio, const StepTables& st, int64_t blk, Step1* s1b,
-                                              int64_t kst) {
+                                              int64_t kst, double winv = 0.0) {
     constexpr int NB = PR + 2;
     int64_t c[NB];
 #pragma unroll
@@ -288,7 +292,7 @@ __device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t 
         mn = min(mn, c[j]);
     }
     auto key = [&](int64_t t) {  // key_of for the run-time kind, at the first instant of a step
-        const int32_t f = score_at<PD, PR>(t, r, wsum, noprio);
+        const int32_t f = score_at<PD, PR>(t, r, wsum, noprio, winv);
         return (T == 1 || !(t < r.e_fail)) ? pack_key(f, n) : -1;
     };
     Step1* s1 = s1b + T * kst;
@@ -342,11 +346,12 @@ __device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t 
 template <int PD, int PR>
 __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
                                           double wsum, int32_t noprio, const StepSlots& o,
-                                          const StepTables& st, int64_t blk, Step1* s1b, int64_t kst) {
+                                          const StepTables& st, int64_t blk, Step1* s1b, int64_t kst,
+                                          double winv = 0.0) {
     if (o.slot0 >= 0)
-        step_emit_one<PD, PR>(r, n, 0, o.slot0, o.mslot0, o.multi0, tmin, tmax, wsum, noprio, st, blk, s1b, kst);
+        step_emit_one<PD, PR>(r, n, 0, o.slot0, o.mslot0, o.multi0, tmin, tmax, wsum, noprio, st, blk, s1b, kst, winv);
     if (o.slot1 >= 0)
-        step_emit_one<PD, PR>(r, n, 1, o.slot1, o.mslot1, o.multi1, tmin, tmax, wsum, noprio, st, blk, s1b, kst);
+        step_emit_one<PD, PR>(r, n, 1, o.slot1, o.mslot1, o.multi1, tmin, tmax, wsum, noprio, st, blk, s1b, kst, winv);
 }
 
 // Work item of the compacted emit: owner thread | kind << 12 | multi << 13 | slot << 14 | rs << 24,
@@ -375,11 +380,11 @@ __device__ __forceinline__ void step_queue(const StepSlots& o, int32_t* nq, uint
 // are marked ~0u).
 template <int PD, int PR, int CAP>
 __device__ __forceinline__ void step_count_queue(const NodeRec<PD, PR>& r, bool valid, int64_t n, int64_t tmin,
-                                                 int64_t tmax, double wsum, int32_t noprio, bool keep,
-                                                 StepShared& sh, int32_t* nrec, int32_t* nq, uint32_t* q,
-                                                 int32_t* qm, NodeRec<PD, PR>* lrec, StepSlots& o,
+                                                 int64_t tmax, double wsum, double winv, int32_t noprio,
+                                                 bool keep, StepShared& sh, int32_t* nrec, int32_t* nq,
+                                                 uint32_t* q, int32_t* qm, NodeRec<PD, PR>* lrec, StepSlots& o,
                                                  bool& self_emit) {
-    const int32_t s0 = score_at<PD, PR>(tmin, r, wsum, noprio);
+    const int32_t s0 = score_at<PD, PR>(tmin, r, wsum, noprio, winv);
     int cnt1 = 0;
     int64_t mn1 = INT64_MAX, mx1 = INT64_MIN;
     auto add = [&](int64_t e, int& c, int64_t& mn, int64_t& mx) {
