@@ -47,8 +47,9 @@ PMC_DIR = os.path.join(ROOT, "profiles", "pmc")
 DROPIN = os.path.join(ROOT, "crane-scheduler_amd", "lib", "dropin_bench")
 # kernel timer name -> rocprofv3 kernel name (prefix, suffix) for the PMC lookup
 KERNEL_PMC = {
-    "k1_node_pass+k3a_steps": ("crane::k1_node_pass<", "true>"),
-    "k1_node_pass": ("crane::k1_node_pass<", "false>"),
+    "k1_node_pass+k3a_steps": ("crane::k1_node_pass<", "true, false>"),
+    "k1_node_pass+k3a_count": ("crane::k1_node_pass<", "true, true>"),
+    "k1_node_pass": ("crane::k1_node_pass<", "false, false>"),
     "k2x_dedupe+k3p_pods": ("crane::k2x_dedupe_pods", ""),
     "k2x_dedupe": ("crane::k2x_dedupe", ""),
     "k3p_pods": ("crane::k3p_pods", ""),
@@ -530,6 +531,10 @@ def main():
         "k2x_dedupe+k3p_pods": (k2d_b + k3p_b, "bindings read + distinct entries + count/offset written; pod now + "
                                                "flag read, partition + keys written"),
         "k1_node_pass+k3a_steps": (N * (16 * M + 8) + E * 4 + co_b,
+                                   "SoA (value, ts) read + hot value written + K2 entries and count/offset read"),
+        # split form (past one round of resident workgroups): the same streams; k3a_emit then
+        # re-reads the L2-resident stepped records (not HBM-priced, like K3s)
+        "k1_node_pass+k3a_count": (N * (16 * M + 8) + E * 4 + co_b,
                                    "SoA (value, ts) read + hot value written + K2 entries and count/offset read"),
         "k3p_pods": (k3p_b, "pod now + flag read, partition + keys written"),
     }

@@ -117,7 +117,10 @@ __global__ __launch_bounds__(kK2Threads) void k2_hot_count(const int32_t* __rest
 constexpr int kK1RecCap = 112;
 constexpr int kK1S1Cap = 256;
 
-template <int PD, int PR, int kK1Threads, bool STEP>
+// SPLIT (with STEP; large N): classify and count only — the stepped records and queue items
+// go to HBM for k3a_emit, so no LDS staging and no epilogue (short-lived workgroups, more of
+// them per CU, the SoA stream is what bounds the launch).
+template <int PD, int PR, int kK1Threads, bool STEP, bool SPLIT = false>
 // 4x6 shape: registers for 5 waves per SIMD (with the ~30 KB of LDS, 5 workgroups per CU)
 __global__ __launch_bounds__(kK1Threads) __attribute__((amdgpu_waves_per_eu(PD * PR <= 24 ? 5 : 1)))
 void k1_node_pass(K1Args a, K1Step step) {
@@ -141,15 +144,15 @@ void k1_node_pass(K1Args a, K1Step step) {
     __shared__ StepShared ssh;
     int64_t tmin = 0, tmax = 0;
     __shared__ int32_t nq;                      // stepped (node, kind) items queued for the emit
-    __shared__ uint32_t q[STEP ? 2 * kK1Threads : 1];
-    __shared__ int32_t qm[STEP ? 2 * kK1Threads : 1];  // first middle-piece slot of queued items
+    __shared__ uint32_t q[STEP && !SPLIT ? 2 * kK1Threads : 1];
+    __shared__ int32_t qm[STEP && !SPLIT ? 2 * kK1Threads : 1];  // first middle-piece slot of queued items
     // one-step records per kind (2 per node at most, CAP staged in LDS): staging; sorted
     // copy over the records' LDS once the emit has read them (or past them when the
     // records are written out) (one buffer with the dedupe-form K2 buckets hxh below:
     // those are read before the step epilogue's first barrier, the staging is written after it)
     constexpr int CAP = kK1S1Cap < 2 * kK1Threads ? kK1S1Cap : 2 * kK1Threads;
     constexpr int kHxWords = kMaxWin * kK1Threads;
-    constexpr int kUnion = (STEP ? 2 * CAP * (int)sizeof(Step1) : 0) > 4 * kHxWords
+    constexpr int kUnion = (STEP && !SPLIT ? 2 * CAP * (int)sizeof(Step1) : 0) > 4 * kHxWords
                                ? 2 * CAP * (int)sizeof(Step1)
                                : 4 * kHxWords;
     __shared__ __attribute__((aligned(16))) unsigned char ush[kUnion];
@@ -197,19 +200,24 @@ void k1_node_pass(K1Args a, K1Step step) {
 #pragma unroll
             for (int k = 0; k < PD; ++k) {
                 const int64_t row = k < pol.npd ? pol.pred_slot[k] : 0;
-                pt[k] = ts[row * N + n];
-                pv[k] = val[row * N + n];
+                // uniform row base + lane offset (the SGPR-base load form)
+                const int64_t* __restrict__ tr = ts + (row * N + first);
+                const double* __restrict__ vr = val + (row * N + first);
+                pt[k] = tr[threadIdx.x];
+                pv[k] = vr[threadIdx.x];
             }
 #pragma unroll
             for (int k = 0; k < PR; ++k) {
                 const int64_t row = k < pol.npr ? pol.prio_slot[k] : 0;
-                qt[k] = ts[row * N + n];
-                qv[k] = val[row * N + n];
+                const int64_t* __restrict__ tr = ts + (row * N + first);
+                const double* __restrict__ vr = val + (row * N + first);
+                qt[k] = tr[threadIdx.x];
+                qv[k] = vr[threadIdx.x];
             }
         }
         if (buckets) {
 #pragma unroll
-            for (int b = 0; b < kMaxWin; ++b) bc[b] = b < pol.n_win ? buckets[(int64_t)b * N + n] : 0u;
+            for (int b = 0; b < kMaxWin; ++b) bc[b] = b < pol.n_win ? (buckets + first)[(int64_t)b * N + threadIdx.x] : 0u;
         }
         if (!buckets && !hx && hv) {
             hvl = hv[n];
@@ -304,7 +312,7 @@ void k1_node_pass(K1Args a, K1Step step) {
             if (buckets) {
 #pragma unroll
                 for (int b = 0; b < kMaxWin; ++b)  // consumed: leaves the buckets zeroed for the next K2
-                    if (b < pol.n_win) buckets[(int64_t)b * N + n] = 0;
+                    if (b < pol.n_win) (buckets + first)[(int64_t)b * N + threadIdx.x] = 0;
             }
             // window of cutoff rank r counts the buckets >= r: one running suffix sum
             int64_t v = 0;
@@ -349,6 +357,20 @@ void k1_node_pass(K1Args a, K1Step step) {
         // stepped (a few %): keys-only, the records are compacted into kK1RecCap LDS slots
         // (a node past them builds its own); the (node, kind) items go to the queue
         bool self_emit;
+        if constexpr (SPLIT) {
+            // every stepped node's record to HBM, every item queued in HBM; k3a_emit does the rest
+            const int64_t qo = blk * 2 * kK1Threads;
+            step_count_queue<PD, PR, kK1RecCap>(r, n < N, n, tmin, tmax, step.wsum, step.winv, step.noprio, true,
+                                                ssh, &nrec, &nq, step.qg + qo, step.qmg + qo, lrec, so, self_emit);
+            if (so.slot0 >= 0 || so.slot1 >= 0) static_cast<Rec*>(step.srec)[n] = r;
+            step_publish<kK1Threads>(so, ssh, step.st, blk);  // (its barrier: nq is final)
+            if (threadIdx.x == 0) step.nqg[blk] = nq;
+            CRANE_TSTAMP(a.trace, blockIdx.x, 3);
+            CRANE_TSTAMP(a.trace, blockIdx.x, 5);
+            CRANE_TSTAMP(a.trace, blockIdx.x, 6);
+            CRANE_TSTAMP(a.trace, blockIdx.x, 4);
+            return;
+        }
         step_count_queue<PD, PR, kK1RecCap>(r, n < N, n, tmin, tmax, step.wsum, step.winv, step.noprio,
                                             out != nullptr, ssh, &nrec, &nq, q, qm, lrec, so, self_emit);
         step_publish<kK1Threads>(so, ssh, step.st, blk);  // (its barrier also orders lrec and the queue)
@@ -390,6 +412,72 @@ void k1_node_pass(K1Args a, K1Step step) {
     for (int64_t i = threadIdx.x; i < nvec; i += kK1Threads) dst[i] = src[i];
 }
 
+// ---------------------------------------------------------------- K3a emit (split form)
+// One workgroup per producer block of the split node pass: the block's queued (node, kind)
+// items are built from the stepped records in HBM (L2-resident: written by the node pass on
+// the same XCD), then sorted, published and the tile rows written — the fused K1 epilogue.
+template <int PD, int PR, int BS>
+__global__ __launch_bounds__(BS) void k3a_emit(K1Step step, int64_t N) {
+    using Rec = NodeRec<PD, PR>;
+    constexpr int CAP = kK1S1Cap < 2 * BS ? kK1S1Cap : 2 * BS;
+    __shared__ StepShared ssh;
+    __shared__ __attribute__((aligned(16))) Step1 s1l[2 * CAP];
+    __shared__ __attribute__((aligned(16))) Step1 s1s[2 * CAP];
+    __shared__ int32_t nq;
+    const int64_t nb = (N + BS - 1) / BS;
+    const int64_t blk = xcd_block(blockIdx.x, nb);  // the node pass's mapping: same XCD
+    const int64_t first = blk * BS;
+    const StepTables& st = step.st;
+    if (threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = st.cnt[blk * 4 + threadIdx.x];
+    if (threadIdx.x < 2) {
+        // the block's flat maxima (step_tile_rows folds sh.fm over the waves)
+        ssh.fm[threadIdx.x][0] = st.flat[blk * 2 + threadIdx.x];
+        for (int i = 1; i < BS / 64; ++i) ssh.fm[threadIdx.x][i] = -1;
+    }
+    if (threadIdx.x == 0) nq = step.nqg[blk];
+    int64_t tpre = 0;
+    if (st.rows) tile_prefetch(st, &tpre);
+    const int64_t tmin = step.batch[0], tmax = step.batch[1];
+    __syncthreads();
+    const bool g1 = max(ssh.lc[0][0], ssh.lc[1][0]) > min(CAP, st.lds_cap);
+    Step1* s1b = g1 ? st.stage + blk * 2 * st.bs : s1l;
+    const int64_t kst = g1 ? st.s1pad : (int64_t)CAP;
+    const uint32_t* q = step.qg + blk * 2 * BS;
+    const int32_t* qm = step.qmg + blk * 2 * BS;
+    const Rec* rec = static_cast<const Rec*>(step.srec);
+    for (int w = threadIdx.x; w < nq; w += BS) {
+        const uint32_t it = q[w];
+        const int o = (int)(it & 0xFFF);
+        step_emit_one<PD, PR>(rec[first + o], first + o, (int)((it >> 12) & 1), (int32_t)((it >> 14) & 0x3FF), qm[w],
+                              ((it >> 13) & 1) != 0, tmin, tmax, step.wsum, step.noprio, st, blk, s1b, kst,
+                              step.winv);
+    }
+    __syncthreads();
+    if (g1) step_sort_publish_global<BS>(ssh, st, blk);
+    else step_sort_publish<BS, CAP>(s1l, s1s, ssh, st, blk);
+    if (st.rows) {
+        if (g1) step_tile_rows<BS, CAP, true>(s1l, s1s, ssh, st, blk, &tpre);
+        else step_tile_rows<BS, CAP, false>(s1l, s1s, ssh, st, blk, &tpre);
+    }
+}
+
+template <int PD, int PR>
+static hipError_t launch_emit_t(const K1Step& step, int64_t N, int32_t bs, hipStream_t st) {
+    const int64_t nb = (N + bs - 1) / bs;
+    if (nb <= 0) return hipSuccess;
+    if (bs == 256) return klaunch("k3a_emit", k3a_emit<PD, PR, 256>, dim3((unsigned)nb), dim3(256), 0, st, step, N);
+    if (bs == 128) return klaunch("k3a_emit", k3a_emit<PD, PR, 128>, dim3((unsigned)nb), dim3(128), 0, st, step, N);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs, hipStream_t st) {
+    switch (shape) {
+        case kShape4x6: return launch_emit_t<4, 6>(step, N, bs, st);
+        case kShape8x8: return launch_emit_t<8, 8>(step, N, bs, st);
+        default: return launch_emit_t<16, 16>(step, N, bs, st);
+    }
+}
+
 // ---------------------------------------------------------------- launchers
 template <int PD, int PR>
 static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t st) {
@@ -406,6 +494,13 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
     if (step && !step->st.stage) return hipErrorInvalidValue;
     const size_t ldsx = lds + (size_t)a.lds_extra;
     const K1Step sa = step ? *step : K1Step{};
+    if (step && step->srec) {  // split form: no LDS staging, the epilogue is k3a_emit's
+        if (a.out || !step->qg || !step->qmg || !step->nqg) return hipErrorInvalidValue;
+        const char* nm = "k1_node_pass+k3a_count";
+        if (T == 256)
+            return klaunch(nm, k1_node_pass<PD, PR, 256, true, true>, dim3(grid), dim3(256), 0, st, a, sa);
+        return klaunch(nm, k1_node_pass<PD, PR, 128, true, true>, dim3(grid), dim3(128), 0, st, a, sa);
+    }
     const char* nm = step ? "k1_node_pass+k3a_steps" : "k1_node_pass";
     if (T == 256)
         return step ? klaunch(nm, k1_node_pass<PD, PR, 256, true>, dim3(grid), dim3(256), ldsx, st, a, sa)

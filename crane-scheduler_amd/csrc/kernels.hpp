@@ -260,6 +260,13 @@ struct K1Step {
     double wsum;
     double winv;             // 1 / wsum when |wsum| is a power of two, else 0 (score_at)
     StepTables st;
+    // split form (large N): the node pass only classifies and counts; the stepped nodes'
+    // records (srec[node]), the queued (node, kind) items per block (qg / qmg [nblk][2 * bs])
+    // and their count (nqg [nblk]) go to HBM, and k3a_emit builds the block's tables
+    void* srec;
+    uint32_t* qg;
+    int32_t* qmg;
+    int32_t* nqg;
 };
 
 size_t node_rec_bytes(int shape);
@@ -292,5 +299,7 @@ struct K1Args {
 };
 // step (optional): also build the K3 step tables of a pod batch (K3a fused).
 hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr);
+// split form's second kernel: one workgroup per producer block of the node pass (bs nodes)
+hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs, hipStream_t st);
 
 }  // namespace crane

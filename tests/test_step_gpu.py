@@ -24,14 +24,16 @@ def _check(spec, c, now, ds):
     off, osc, och = oracle_soa(spec, c, now=now, ds=ds)
     # K3s from the producers' per-tile rows, and searching the records itself; K1's
     # one-step records through its LDS staging, through st.stage always (cap 0), or
-    # per block as its counts exceed a small cap
-    for rows, cap in ((1, 1 << 30), (0, 1 << 30), (1, 0), (0, 6), (1, 6)):
-        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap})
+    # per block as its counts exceed a small cap; the node pass fused with the step
+    # tables (split 0) or as the split form (count pass + k3a_emit, split 1)
+    for rows, cap, split in ((1, 1 << 30, 0), (0, 1 << 30, 0), (1, 0, 0), (0, 6, 0), (1, 6, 0),
+                             (1, 1 << 30, 1), (0, 6, 1), (1, 0, 1)):
+        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap, "k1_split": split})
         _, _, ch, cs = eng.eval(now, ds)
-        assert np.array_equal(ch, och), (rows, cap)
+        assert np.array_equal(ch, och), (rows, cap, split)
         for p in range(len(now)):
             ok = (off[p] < 0) | bool(ds[p])
-            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, p)
+            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, split, p)
         eng.close()
 
 
@@ -103,6 +105,25 @@ def test_step_policy_shapes():
     for i, spec in enumerate(specs):
         c = synth.make_cluster(spec, 777, 90, seed=200 + i, pod_step_ns=20_000_000_000, ds_frac=0.1)
         _check(spec, c, c.now, c.ds)
+
+
+def test_step_split_auto_at_large_n():
+    """Past one round of resident workgroups the node pass splits by itself (auto): 400k
+    nodes, the split form's keys equal the fused form's and the per-pair kernel's."""
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 400_000, 1500, seed=30, pod_step_ns=4_000_000, ds_frac=0.02)
+    out = []
+    for opts in ({"k1_split": 2}, {"k1_split": 0}, {"keys_path": 1}):
+        eng = engine_for(spec, c, opts=opts)
+        eng.set_profiling(True)
+        _, _, ch, cs = eng.eval(c.now, c.ds)
+        names = [n for n, _ in eng.stage_times()]
+        if opts.get("k1_split") == 2:
+            assert "k3a_emit" in names, names
+        out.append((ch, cs))
+        eng.close()
+    for ch, cs in out[1:]:
+        assert np.array_equal(ch, out[0][0]) and np.array_equal(cs, out[0][1])
 
 
 def test_step_matches_pair_keys():
@@ -209,14 +230,16 @@ def test_step_keys_async_matches_oracle(ride, pods):
     assert all(0 < t < 50 for _, t in times), times
 
 
+@pytest.mark.parametrize("split", [0, 1], ids=["fused", "split"])
 @pytest.mark.parametrize("k2", [0, 1, 2], ids=["dedupe", "binned", "hash"])
-def test_step_keys_async_k2_forms(k2):
+def test_step_keys_async_k2_forms(k2, split):
     """The combined step with each K2 form (dedupe: counts consumed by the fused node
-    pass from per-block entries; binned / hash: buckets) equals the oracle, replayed."""
+    pass from per-block entries; binned / hash: buckets) equals the oracle, replayed,
+    with the node pass fused with the step tables or split (count pass + k3a_emit)."""
     import torch
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 20000, 3000, n_bindings=400_000, seed=29, pod_step_ns=2_000_000, ds_frac=0.03)
-    eng = engine_for(spec, c, opts={"k2_form": k2})
+    eng = engine_for(spec, c, opts={"k2_form": k2, "k1_split": split})
     eng.upload_bindings(c.b_node, c.b_ts)
     now = int(synth.NOW0_NS)
     dev = torch.device("cuda", 0)
@@ -227,10 +250,13 @@ def test_step_keys_async_k2_forms(k2):
     _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=_oracle_hv(spec, c, now))
     with torch.cuda.stream(st):
         for rep in range(3):
+            eng.set_profiling(rep == 2)
             eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
             st.synchronize()
             ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
             assert np.array_equal(ch, och), rep
+    names = [n for n, _ in eng.stage_times()]
+    assert ("k1_node_pass+k3a_count" in names and "k3a_emit" in names) == bool(split), names
 
 
 @pytest.mark.parametrize("keep", [0, 1])

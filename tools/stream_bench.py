@@ -3,7 +3,8 @@
     python tools/stream_bench.py [--nodes 4000000] [--bindings 16000000] [--pods 10000] [--reps 5]
 
 One step = K2 refresh (the binned form at this size, or the hash form) then a
-keys-only eval (k3p_pods, k1_node_pass+k3a_steps, k3s_eval).  Kernel times come
+keys-only eval (k3p_pods, k1_node_pass+k3a_steps or its split form k1_node_pass+k3a_count +
+k3a_emit, k3s_eval).  Kernel times come
 from the engine's dispatch-stamped events (crane_dyn_set_profiling).  Before
 the refresh and before the eval a 1 GiB scratch buffer is written (--flush write:
 the Infinity Cache is then full of dirty lines that are written back while the
@@ -69,6 +70,8 @@ b_in = int((c.b_ts > now // 10**9 - max_tr).sum())
 alg = {
     "k2 (all K2 kernels)": B * 12 + 4 * W * N,
     "k1_node_pass+k3a_steps": N * (16 * M + 8 * W + 8 + (REC if args.keep_records else 0)),
+    "k1_node_pass+k3a_count": N * (16 * M + 8 * W + 8),  # split form (k3a_emit builds the tables after it)
+    "k1 split total (count + emit)": N * (16 * M + 8 * W + 8),
 }
 sink = torch.empty(1, dtype=torch.int64, device=dev)
 
@@ -98,6 +101,9 @@ for k2 in args.k2.split(","):
             for name, t in t_k2 + t_ev:
                 acc.setdefault(name, []).append(t)
             acc.setdefault("k2 (all K2 kernels)", []).append(sum(t for _, t in t_k2))
+            split = [t for name, t in t_ev if name in ("k1_node_pass+k3a_count", "k3a_emit")]
+            if len(split) == 2:  # the split form's two kernels together build what the fused one does
+                acc.setdefault("k1 split total (count + emit)", []).append(sum(split))
     eng.set_profiling(False)
     keys = d_keys.cpu().numpy()
     if keys_ref is None:
