@@ -168,6 +168,9 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     __shared__ int64_t tt[kK3sPods];         // the tile's pod times (sorted per kind)
     __shared__ int32_t tree[2 * kK3sPods];   // range maxima: node i covers its leaves' slots
     __shared__ int32_t umax[2];
+    __shared__ int32_t wcnt[4 * kK3sMaxBlk];     // work items per (block, category)
+    __shared__ int32_t wpre[4 * kK3sMaxBlk + 1];  // their exclusive prefix (+ the total)
+    __shared__ int32_t wjl[2 * kK3sMaxBlk];      // first record stepping inside, per block and kind
     const int64_t b = blockIdx.x;
     CRANE_TSTAMP(st.trace, b, 0);
     const int32_t r = (int32_t)(b % R);
@@ -178,19 +181,21 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     const int64_t tlo[2] = {ts[0], ts[2]}, thi[2] = {ts[1], ts[3]};
     const int32_t cn = (int32_t)ts[4], cd = (int32_t)ts[5];
     const int32_t klo[2] = {0, cn}, khi[2] = {cn, cn + cd};
-    // the slice's producer blocks: with R a multiple of 8, workgroup label r % 8 (= its XCD
-    // group, blockIdx % 8) takes the blocks K1 ran in the same group, b = c + 8 k, so their
-    // step tables are read from this XCD's L2; sub-slice r / 8 takes a range of k.  LPB lanes
-    // per block (a power of two <= 64).  (Placement only changes speed: the blocks covered
-    // depend on blockIdx alone.)
+    // the slice's producer blocks: with R a multiple of 8, workgroup label g = r % 8 (= its
+    // XCD group, blockIdx % 8) takes the blocks the node pass ran in the same group — its
+    // workgroup w built block xcd_block(w) (step_node.hpp), the contiguous run of XCD w % 8 —
+    // so their step tables are read from this XCD's L2; sub-slice s = r / 8 takes every S-th
+    // of them (neighbouring blocks — hot nodes cluster, and with them the step records —
+    // spread over the group's workgroups).  LPB lanes per block (a power of two <= 64).
+    // (Placement only changes speed: the blocks covered depend on blockIdx alone.)
     int32_t xc = 0, stride = 1, k0 = 0, m = 0;
     if (R % 8 == 0) {
-        xc = r & 7;
-        stride = 8;
-        const int32_t S = R >> 3, s = r >> 3;
-        const int32_t nc = (st.nblk - xc + 7) >> 3, per = ((st.nblk + 7) / 8 + S - 1) / S;
-        k0 = min(nc, s * per);
-        m = min(nc, k0 + per) - k0;
+        const int32_t g = r & 7, S = R >> 3, s = r >> 3;
+        const int32_t per = st.nblk >> 3, rem = st.nblk & 7;
+        const int32_t nc = per + (g < rem ? 1 : 0);  // the group's blocks: base + k, k < nc
+        xc = g * per + min(g, rem) + s;              // this sub-slice's: base + s + S j
+        stride = S;
+        m = nc > s ? (nc - s + S - 1) / S : 0;
     } else {
         const int32_t per = (st.nblk + R - 1) / R;
         k0 = min(st.nblk, r * per);
@@ -257,56 +262,68 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
             }
         }
     }
-    __syncthreads();  // tt, tree, umax initialised
+    // the slice's work as one list over the workgroup's lanes: per block j, category q
+    // (0/1: kind 0/1 one-step records stepping inside, 2/3: kind 0/1 middle pieces), so a
+    // block with many records (hot nodes) is spread over every lane instead of its team's
+    if (own && sub == 0) {
+        wcnt[4 * j + 0] = max(0, jj[1] - jj[0]);
+        wcnt[4 * j + 1] = max(0, jj[3] - jj[2]);
+        wcnt[4 * j + 2] = nm[0];
+        wcnt[4 * j + 3] = nm[1];
+        wjl[2 * j] = jj[0];
+        wjl[2 * j + 1] = jj[2];
+    }
+    __syncthreads();  // tt, tree, umax initialised; the work counts in
     CRANE_TSTAMP(st.trace, b, 1);
+    const int32_t E = 4 * m;  // work entries
+    if (threadIdx.x < 64) {  // wave 0: exclusive prefix over the entries (wpre[E] = total)
+        int32_t carry = 0;
+        for (int32_t e0 = 0; e0 < E; e0 += 64) {
+            const int32_t e = e0 + lane;
+            const int32_t v = e < E ? wcnt[e] : 0;
+            const int32_t inc = (int32_t)wave_scan_add((uint32_t)v) + carry;
+            if (e < E) wpre[e] = inc - v;
+            carry = __builtin_amdgcn_readlane(inc, 63);
+        }
+        if (lane == 0) wpre[E] = carry;
+    }
+    __syncthreads();
+    const int32_t total = wpre[E];
     bool upd = false;  // this lane wrote the tree
-    if (own) {
-#pragma unroll
-        for (int T = 0; T < 2; ++T) {
-            // one-step records stepping inside (lo, hi]: split the kind's slots
-            for (int32_t i = jj[2 * T] + sub; i < jj[2 * T + 1]; i += lpb) {
-                const Step1 q = base[T][i];
-                const int32_t sp = slot_lower(tt, klo[T], khi[T], q.bp);
-                if (q.k0 >= 0) tree_max(tree, klo[T], sp, q.k0);
-                if (q.k1 >= 0) tree_max(tree, sp, khi[T], q.k1);
+    for (int32_t it = threadIdx.x; it < total; it += kK3sThreads) {
+        // the entry holding item it: the last e with wpre[e] <= it
+        int32_t lo = 0, hi = E - 1;
+        while (lo < hi) {
+            const int32_t mid = (lo + hi + 1) >> 1;
+            if (wpre[mid] <= it) lo = mid;
+            else hi = mid - 1;
+        }
+        const int32_t e = lo, jb = e >> 2, q = e & 3, T = q & 1, idx = it - wpre[e];
+        const int64_t obj = xc + (int64_t)stride * (k0 + jb);
+        if (q < 2) {
+            // a one-step record stepping inside (lo, hi]: split the kind's slots
+            const Step1 r1 = (st.single + s1_at(st, T, obj))[wjl[2 * jb + T] + idx];
+            const int32_t sp = slot_lower(tt, klo[T], khi[T], r1.bp);
+            if (r1.k0 >= 0) tree_max(tree, klo[T], sp, r1.k0);
+            if (r1.k1 >= 0) tree_max(tree, sp, khi[T], r1.k1);
+            upd = true;
+        } else {
+            // a middle piece: covering -> uniform, overlapping partly -> range maximum over
+            // the slots with s <= now < e
+            const Mid pm = st.mid[(int64_t)T * st.mpad + obj * st.mstride + idx];
+            if (pm.s <= tlo[T] && pm.e > thi[T]) um[T] = max(um[T], pm.key);
+            else if (pm.s <= thi[T] && pm.e > tlo[T]) {
+                tree_max(tree, slot_lower(tt, klo[T], khi[T], pm.s), slot_lower(tt, klo[T], khi[T], pm.e), pm.key);
                 upd = true;
             }
         }
     }
-    CRANE_TSTAMP(st.trace, b, 6);  // (thread 0's records done)
-    if (own) {
-#pragma unroll
-        for (int T = 0; T < 2; ++T) {
-            // middle pieces, 4 loads in flight per lane: covering -> uniform, overlapping partly ->
-            // range maximum over the slots with s <= now < e
-            const Mid* mp = st.mid + (int64_t)T * st.mpad + ob * st.mstride;
-            for (int32_t i0 = sub; i0 < nm[T]; i0 += 4 * lpb) {
-                Mid q[4];
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const int32_t i = i0 + v * lpb;
-                    if (i < nm[T]) q[v] = mp[i];
-                    else q[v].s = INT64_MAX;  // (matches nothing)
-                }
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const Mid& p = q[v];
-                    if (p.s <= tlo[T] && p.e > thi[T]) um[T] = max(um[T], p.key);
-                    else if (p.s <= thi[T] && p.e > tlo[T]) {
-                        tree_max(tree, slot_lower(tt, klo[T], khi[T], p.s), slot_lower(tt, klo[T], khi[T], p.e),
-                                 p.key);
-                        upd = true;
-                    }
-                }
-            }
-        }
-    }
+    CRANE_TSTAMP(st.trace, b, 6);
     CRANE_TSTAMP(st.trace, b, 2);
     // uniform maxima: wave reduce, one LDS atomic per wave
 #pragma unroll
     for (int T = 0; T < 2; ++T) {
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) um[T] = max(um[T], __shfl_xor(um[T], o));
+        um[T] = wave_max(um[T]);
         if (lane == 0 && um[T] >= 0) atomicMax(&umax[T], um[T]);
     }
     const bool tree_used = __syncthreads_or(upd);
