@@ -266,6 +266,7 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
         const int32_t kl = __shfl(key, lead);
         const uint64_t m = __ballot(ok && key == kl);
         // (kl, count) rides on the lead lane; every other lane adds its own key once
+        // (more leader rounds for the next repeated keys measured slower: 9.6 -> 10.0 us at config 3)
         const bool mine = lane == lead || (ok && key != kl);
         const int32_t slot =
             mine ? hash_add(hkey, hcnt, hist, g.bb, lane == lead ? kl : key, lane == lead ? (uint32_t)__popcll(m) : 1u)
