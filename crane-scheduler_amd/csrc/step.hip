@@ -104,6 +104,14 @@ constexpr int kK3sThreads = kK3sWaves * 64;
 constexpr int kK3sPPL = 4;                          // pods per lane
 constexpr int kK3sPods = kK3sThreads * kK3sPPL;     // pods per workgroup (= kPodTile)
 constexpr int kK3sBlkPerWg = 16;                    // producer blocks per workgroup, aimed for
+// Work lists (k3s_eval) for slices of at most kK3sListBlk blocks, holding at most this many
+// straddling records / middle pieces (more: the blocks' teams).  Same-box A/B at configs 3 / 4
+// (one GPU) / 4 shard against the team loops alone: K3s 0.0397 -> 0.0364 ms per batch,
+// 0.122 -> 0.118 ms, 28.7 -> 24.8 us; every record and piece listed (and 4x the LDS):
+// 0.0362, 0.270 ms, 52 us (tools/gpu_lib_ab.sh)
+constexpr int kK3sListBlk = 64;
+constexpr int kK3sRecList = 512;
+constexpr int kK3sPieceList = 512;
 static_assert(kK3sMaxBlk <= kK3sThreads, "at least one lane per producer block");
 static_assert(kK3sPods == kPodTile, "a workgroup resolves one K3p tile");
 
@@ -168,9 +176,12 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     __shared__ int64_t tt[kK3sPods];         // the tile's pod times (sorted per kind)
     __shared__ int32_t tree[2 * kK3sPods];   // range maxima: node i covers its leaves' slots
     __shared__ int32_t umax[2];
-    __shared__ int32_t wcnt[4 * kK3sMaxBlk];     // work items per (block, category)
-    __shared__ int32_t wpre[4 * kK3sMaxBlk + 1];  // their exclusive prefix (+ the total)
-    __shared__ int32_t wjl[2 * kK3sMaxBlk];      // first record stepping inside, per block and kind
+    // work lists (slices of <= kK3sListBlk blocks): records stepping inside / middle pieces per
+    // (block, kind), turned in place into their exclusive prefix (+ the total); the first record
+    // stepping inside per (block, kind).  Small: K3s runs several rounds of workgroups at config 4
+    // and its LDS sets how many share a CU
+    __shared__ int32_t wpre[4 * kK3sListBlk + 1];
+    __shared__ int32_t wjl[2 * kK3sListBlk];
     const int64_t b = blockIdx.x;
     CRANE_TSTAMP(st.trace, b, 0);
     const int32_t r = (int32_t)(b % R);
@@ -262,45 +273,56 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
             }
         }
     }
-    // the slice's work as one list over the workgroup's lanes: per block j, category q
-    // (0/1: kind 0/1 one-step records stepping inside, 2/3: kind 0/1 middle pieces), so a
-    // block with many records (hot nodes) is spread over every lane instead of its team's
-    if (own && sub == 0) {
-        wcnt[4 * j + 0] = max(0, jj[1] - jj[0]);
-        wcnt[4 * j + 1] = max(0, jj[3] - jj[2]);
-        wcnt[4 * j + 2] = nm[0];
-        wcnt[4 * j + 3] = nm[1];
+    // the slice's work as lists over the workgroup's lanes, so a block with many records
+    // (hot nodes) is spread over every lane instead of its team's: entries e < 2m are
+    // (block, kind) one-step records stepping inside, e >= 2m (block, kind) middle pieces
+    const bool lists = m <= kK3sListBlk;  // (workgroup-uniform)
+    if (lists && own && sub == 0) {
+        wpre[2 * j + 0] = max(0, jj[1] - jj[0]);
+        wpre[2 * j + 1] = max(0, jj[3] - jj[2]);
+        wpre[2 * m + 2 * j + 0] = nm[0];
+        wpre[2 * m + 2 * j + 1] = nm[1];
         wjl[2 * j] = jj[0];
         wjl[2 * j + 1] = jj[2];
     }
-    __syncthreads();  // tt, tree, umax initialised; the work counts in
+    __syncthreads();  // tt, tree, umax initialised; the counts in
     CRANE_TSTAMP(st.trace, b, 1);
-    const int32_t E = 4 * m;  // work entries
-    if (threadIdx.x < 64) {  // wave 0: exclusive prefix over the entries (wpre[E] = total)
-        int32_t carry = 0;
-        for (int32_t e0 = 0; e0 < E; e0 += 64) {
-            const int32_t e = e0 + lane;
-            const int32_t v = e < E ? wcnt[e] : 0;
-            const int32_t inc = (int32_t)wave_scan_add((uint32_t)v) + carry;
-            if (e < E) wpre[e] = inc - v;
-            carry = __builtin_amdgcn_readlane(inc, 63);
+    const int32_t E = 4 * m;
+    int32_t nrec = 0, total = 0;
+    if (lists) {
+        if (threadIdx.x < 64) {  // wave 0: exclusive prefix over the entries, in place (wpre[E] = total)
+            const int32_t v = lane < E ? wpre[lane] : 0;  // E <= 4 * kK3sListBlk = 256: four chunks
+            int32_t carry = (int32_t)wave_scan_add((uint32_t)v);
+            if (lane < E) wpre[lane] = carry - v;
+            carry = __builtin_amdgcn_readlane(carry, 63);
+            for (int32_t e0 = 64; e0 < E; e0 += 64) {
+                const int32_t e = e0 + lane;
+                const int32_t x = e < E ? wpre[e] : 0;
+                const int32_t inc = (int32_t)wave_scan_add((uint32_t)x) + carry;
+                if (e < E) wpre[e] = inc - x;
+                carry = __builtin_amdgcn_readlane(inc, 63);
+            }
+            if (lane == 0) wpre[E] = carry;
         }
-        if (lane == 0) wpre[E] = carry;
+        __syncthreads();
+        nrec = wpre[2 * m];
+        total = wpre[E];
     }
-    __syncthreads();
-    const int32_t total = wpre[E];
+    const bool piece_list = lists && total - nrec <= kK3sPieceList;
+    const bool rec_list = lists && nrec <= kK3sRecList;
     bool upd = false;  // this lane wrote the tree
-    for (int32_t it = threadIdx.x; it < total; it += kK3sThreads) {
-        // the entry holding item it: the last e with wpre[e] <= it
-        int32_t lo = 0, hi = E - 1;
+    for (int32_t it = threadIdx.x + (rec_list ? 0 : nrec); it < (piece_list ? total : nrec); it += kK3sThreads) {
+        // the entry holding item it: the last e with wpre[e] <= it, in its half
+        int32_t lo = it < nrec ? 0 : 2 * m, hi = it < nrec ? 2 * m - 1 : E - 1;
         while (lo < hi) {
             const int32_t mid = (lo + hi + 1) >> 1;
             if (wpre[mid] <= it) lo = mid;
             else hi = mid - 1;
         }
-        const int32_t e = lo, jb = e >> 2, q = e & 3, T = q & 1, idx = it - wpre[e];
+        const bool rec = lo < 2 * m;
+        const int32_t ej = rec ? lo : lo - 2 * m, jb = ej >> 1, T = ej & 1, idx = it - wpre[lo];
         const int64_t obj = xc + (int64_t)stride * (k0 + jb);
-        if (q < 2) {
+        if (rec) {
             // a one-step record stepping inside (lo, hi]: split the kind's slots
             const Step1 r1 = (st.single + s1_at(st, T, obj))[wjl[2 * jb + T] + idx];
             const int32_t sp = slot_lower(tt, klo[T], khi[T], r1.bp);
@@ -318,7 +340,45 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
             }
         }
     }
+    if (own && !rec_list) {
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+            // many records: by the block's team (consecutive records, a lane each)
+            for (int32_t i = jj[2 * T] + sub; i < jj[2 * T + 1]; i += lpb) {
+                const Step1 q = base[T][i];
+                const int32_t sp = slot_lower(tt, klo[T], khi[T], q.bp);
+                if (q.k0 >= 0) tree_max(tree, klo[T], sp, q.k0);
+                if (q.k1 >= 0) tree_max(tree, sp, khi[T], q.k1);
+                upd = true;
+            }
+        }
+    }
     CRANE_TSTAMP(st.trace, b, 6);
+    if (own && !piece_list) {
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+            const Mid* mp = st.mid + (int64_t)T * st.mpad + ob * st.mstride;
+            for (int32_t i0 = sub; i0 < nm[T]; i0 += 4 * lpb) {
+                Mid q[4];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int32_t i = i0 + v * lpb;
+                    if (i < nm[T]) q[v] = mp[i];
+                    else q[v].s = INT64_MAX;  // (matches nothing)
+                }
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const Mid& pm = q[v];
+                    if (pm.s <= tlo[T] && pm.e > thi[T]) um[T] = max(um[T], pm.key);
+                    else if (pm.s <= thi[T] && pm.e > tlo[T]) {
+                        tree_max(tree, slot_lower(tt, klo[T], khi[T], pm.s), slot_lower(tt, klo[T], khi[T], pm.e),
+                                 pm.key);
+                        upd = true;
+                    }
+                }
+            }
+        }
+    }
     CRANE_TSTAMP(st.trace, b, 2);
     // uniform maxima: wave reduce, one LDS atomic per wave
 #pragma unroll
