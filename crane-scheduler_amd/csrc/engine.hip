@@ -109,8 +109,6 @@ struct Options {
     int k3s_blocks = 0;       // K3s producer blocks per workgroup aimed for: 0 automatic
     int k2x_threads = 512;    // dedupe K2 workgroup size: 256, 512 or 1024
     int step_lds_cap = 1 << 30;  // K1: one-step records per kind staged in LDS at most (0: always st.stage)
-    int dbg_stop = 0;         // TEMP probe: 1 stop after K1, 2 stop after K2x
-    int dbg_k1_lds = 0;
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
@@ -426,7 +424,6 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
         a.hv_ts = h->hv_ts.p;
     }
     a.threads = k1_bs(h);
-    a.lds_extra = h->opt.dbg_k1_lds;
     a.trace = (h->N + a.threads - 1) / a.threads <= kTraceWgs ? h->trace_region(1) : nullptr;
     HIPTRY(h, launch_node_pass(h->shape, a, st, step));
     if (consume) {
@@ -529,7 +526,6 @@ static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_k
         }
         HIPTRY(h, launch_step_nodes(h->shape, h->rec.p, h->N, h->dp.wsum, h->dp.noprio, sp.stt, sp.g, h->stile.p, st));
     }
-    if (h->opt.dbg_stop == 1) return CRANE_OK;
     HIPTRY(h, launch_step_pairs(h->shape, h->N, h->node_offset, P, d_keys, sp.stt, sp.g, h->sperm.p, h->spnow.p, h->stile.p, st));
     return CRANE_OK;
 }
@@ -682,9 +678,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "step_rows" && range(0, 1)) o.step_rows = (int)value;
     else if (n == "k3s_blocks" && range(0, 256)) o.k3s_blocks = (int)value;
     else if (n == "k2x_threads" && (value == 256 || value == 512 || value == 1024)) o.k2x_threads = (int)value;
-    else if (n == "dbg_stop") o.dbg_stop = (int)value;
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
-    else if (n == "dbg_k1_lds") o.dbg_k1_lds = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
         if (o.trace) {
@@ -1006,7 +1000,6 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
     bool pods_done = false;
     rc = hot_values_locked(h, now_ns, hv_ts_ns, st, h->opt.k3p_in_k2 ? &pp : nullptr, &pods_done);
     if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, st);
-    if (h->opt.dbg_stop == 2) return rc;
     if (!rc) rc = step_rest(h, sp, P, keys, st);
     return rc;
 }

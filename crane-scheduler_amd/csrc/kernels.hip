@@ -492,7 +492,6 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
     const size_t lds = a.out ? sizeof(NodeRec<PD, PR>) * T + s1
                              : std::max(sizeof(NodeRec<PD, PR>) * (size_t)std::min(T, kK1RecCap), s1);
     if (step && !step->st.stage) return hipErrorInvalidValue;
-    const size_t ldsx = lds + (size_t)a.lds_extra;
     const K1Step sa = step ? *step : K1Step{};
     if (step && step->srec) {  // split form: no LDS staging, the epilogue is k3a_emit's
         if (a.out || !step->qg || !step->qmg || !step->nqg) return hipErrorInvalidValue;
@@ -503,7 +502,7 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
     }
     const char* nm = step ? "k1_node_pass+k3a_steps" : "k1_node_pass";
     if (T == 256)
-        return step ? klaunch(nm, k1_node_pass<PD, PR, 256, true>, dim3(grid), dim3(256), ldsx, st, a, sa)
+        return step ? klaunch(nm, k1_node_pass<PD, PR, 256, true>, dim3(grid), dim3(256), lds, st, a, sa)
                     : klaunch(nm, k1_node_pass<PD, PR, 256, false>, dim3(grid), dim3(256), lds, st, a, sa);
     return step ? klaunch(nm, k1_node_pass<PD, PR, 128, true>, dim3(grid), dim3(128), lds, st, a, sa)
                 : klaunch(nm, k1_node_pass<PD, PR, 128, false>, dim3(grid), dim3(128), lds, st, a, sa);

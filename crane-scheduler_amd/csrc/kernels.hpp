@@ -294,7 +294,6 @@ struct K1Args {
     const uint32_t* hx_CO;
     int32_t hx_nblk;
     int32_t threads;        // workgroup size: 128 or 256
-    int32_t lds_extra;      // TEMP probe
     unsigned long long* trace;  // phase trace or null
 };
 // step (optional): also build the K3 step tables of a pod batch (K3a fused).
