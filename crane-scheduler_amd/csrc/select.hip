@@ -101,7 +101,9 @@ __global__ __launch_bounds__(256) void k_sel_fth(SelArgs a, int64_t* __restrict_
 // pod's count from its window start, a wave prefix over the round's chunks, the
 // K-th set bit); a round holding more than kChQ pod ends repeats the ballots for
 // the next ones.
-constexpr int kChT = 1024, kChU = 8, kChW = kChT / 64, kChQ = 4;
+// kChQ pods' masks per ballot pass: at the config-3 queue (windows of ~5300 positions,
+// 8192 a round) 2 takes 36.2 ms, 4 49.5 ms, 1 38.3 ms (same-box A/B, tools/gpu_select_ab.sh)
+constexpr int kChT = 1024, kChU = 8, kChW = kChT / 64, kChQ = 2;
 
 // position of the r-th set bit (r >= 1) of m: halving popcount search
 __device__ __forceinline__ int nth_set_bit(unsigned long long m, int r) {
@@ -119,6 +121,7 @@ __device__ __forceinline__ int nth_set_bit(unsigned long long m, int r) {
 }
 constexpr int kChC = kChU * kChW;         // 64-position chunks per round (chunk c = u * kChW + wave)
 constexpr int64_t kChR = 64LL * kChC;     // positions per round
+static_assert(kChC == 128, "wave 0 resolves a round's chunks two per lane");
 constexpr int kChPB = 1024;               // pod times cached per block
 
 __global__ __launch_bounds__(kChT) void k_sel_chain(SelArgs a, const int64_t* __restrict__ fth, int64_t K,
@@ -196,12 +199,8 @@ __global__ __launch_bounds__(kChT) void k_sel_chain(SelArgs a, const int64_t* __
                         mm[h] = m;
                         cnt2[h] = __popcll(m);
                     }
-                    int32_t x = cnt2[0] + cnt2[1];
-#pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const int32_t y = __shfl_up(x, o);
-                        if (lane >= o) x += y;
-                    }
+                    // inclusive prefix over the lanes (DPP, no LDS round trips)
+                    const int32_t x = (int32_t)wave_scan_add((uint32_t)(cnt2[0] + cnt2[1]));
                     const int64_t need = K - fnd;
                     const int32_t before = x - cnt2[0] - cnt2[1];  // feasible in earlier chunks
                     // the lane whose chunks hold the need-th feasible position
@@ -230,7 +229,7 @@ __global__ __launch_bounds__(kChT) void k_sel_chain(SelArgs a, const int64_t* __
                         ps = end + 1;
                         fnd = 0;
                     } else {
-                        fnd += __shfl(x, 63);
+                        fnd += __builtin_amdgcn_readlane(x, 63);
                         cont = false;
                     }
                 }
