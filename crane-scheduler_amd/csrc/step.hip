@@ -388,12 +388,24 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     }
     const bool tree_used = __syncthreads_or(upd);
     CRANE_TSTAMP(st.trace, b, 3);
+    // a pod's key: the max over its leaf's ancestors (every level's load issued at once, for
+    // all of the lane's pods: one LDS round trip, not a dependent walk per pod)
+    constexpr int kLevels = 11;  // leaves at kK3sPods + slot, root at 1
+    static_assert(kK3sPods == 1 << (kLevels - 1), "a segment tree over the tile's 1024 slots");
+    int32_t anc[kK3sPPL][kLevels];
+    if (tree_used) {
+#pragma unroll
+        for (int u = 0; u < kK3sPPL; ++u)
+#pragma unroll
+            for (int l = 0; l < kLevels; ++l) anc[u][l] = tree[(u * kK3sThreads + threadIdx.x + kK3sPods) >> l];
+    }
 #pragma unroll
     for (int u = 0; u < kK3sPPL; ++u) {
-        const int32_t i = u * kK3sThreads + threadIdx.x;
         int32_t best = umax[ds[u] ? 1 : 0];
-        if (tree_used)
-            for (int32_t x = i + kK3sPods; x >= 1; x >>= 1) best = max(best, tree[x]);
+        if (tree_used) {
+#pragma unroll
+            for (int l = 0; l < kLevels; ++l) best = max(best, anc[u][l]);
+        }
         if (live[u] && best >= 0) {
             const int64_t sc = best >> 24;
             const int64_t n = 0xFFFFFF - (best & 0xFFFFFF);
