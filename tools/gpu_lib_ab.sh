@@ -8,6 +8,11 @@ L=crane-scheduler_amd/lib/libcrane_dyn.so
 cp $L $O/orig.so
 for v in "$@"; do
   cp crane-scheduler_amd/lib_ab/lib_$v.so $L || { cp $O/orig.so $L; exit 1; }
+  if [ -n "$AB_TESTS" ]; then  # parity of the variant first (e.g. AB_TESTS=tests/test_step_gpu.py)
+    timeout -k 10 300 python -u -m pytest $AB_TESTS -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_$v.log 2>&1 \
+      || { tail -20 $O/pytest_$v.log; cp $O/orig.so $L; exit 1; }
+    echo "$v: $(tail -1 $O/pytest_$v.log)"
+  fi
   timeout -k 10 200 python tools/inflight_probe.py --inflight 1,4 > $O/inf_$v.json 2>&1 || { tail $O/inf_$v.json; cp $O/orig.so $L; exit 1; }
   timeout -k 10 300 python bench.py --config 4 --no-cpu-baseline --no-greedy --no-extras > $O/b4_$v.log 2>&1 || { tail $O/b4_$v.log; cp $O/orig.so $L; exit 1; }
   timeout -k 10 200 python tools/trace_step.py --config 4 > $O/t4_$v.json 2> $O/t4_$v.err || { tail $O/t4_$v.err; cp $O/orig.so $L; exit 1; }
