@@ -327,10 +327,13 @@ __global__ __launch_bounds__(BT) void k2x_dedupe_pods(const int32_t* __restrict_
                                                       const int64_t* __restrict__ bts, int64_t B, int64_t N,
                                                       HotCutoffs cut, HotPart g, uint32_t* __restrict__ CO,
                                                       uint32_t* __restrict__ region, PodPrep pp) {
-    if ((int32_t)blockIdx.x < g.nblk) k2d_body<BT>((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
-    else {
+    // the pod tiles first: dispatched first, their sort overlaps the regions' aggregation
+    // instead of trailing the launch
+    if ((int64_t)blockIdx.x >= pp.ntiles) {
+        k2d_body<BT>((int32_t)(blockIdx.x - pp.ntiles), bnode, bts, B, N, cut, g, CO, region);
+    } else {
         extern __shared__ __attribute__((aligned(16))) unsigned char k3p_lds[];
-        k3p_tile<BT>((int64_t)blockIdx.x - g.nblk, pp, k3p_lds);
+        k3p_tile<BT>((int64_t)blockIdx.x, pp, k3p_lds);
     }
 }
 
