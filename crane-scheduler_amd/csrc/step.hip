@@ -103,7 +103,10 @@ constexpr int kK3sWaves = 4;
 constexpr int kK3sThreads = kK3sWaves * 64;
 constexpr int kK3sPPL = 4;                          // pods per lane
 constexpr int kK3sPods = kK3sThreads * kK3sPPL;     // pods per workgroup (= kPodTile)
-constexpr int kK3sBlkPerWg = 16;                    // producer blocks per workgroup, aimed for
+// producer blocks per workgroup aimed for (launches over kMaxWg workgroups are capped first):
+// config 3 (391 blocks) then takes 16 workgroups per tile; 32 per tile (16 blocks) measured
+// 0.0128 vs 0.0123 ms per batch with 4 in flight (engine option k3s_blocks, tools/gpu_opt_probe.sh)
+constexpr int kK3sBlkPerWg = 32;
 // Work lists (k3s_eval) for slices of at most kK3sListBlk blocks, holding at most this many
 // straddling records / middle pieces (more: the blocks' teams).  Same-box A/B at configs 3 / 4
 // (one GPU) / 4 shard against the team loops alone: K3s 0.0397 -> 0.0364 ms per batch,
