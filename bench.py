@@ -148,8 +148,9 @@ def parse():
     ap.add_argument("--rehearse-collective", action="store_true",
                     help="run the N>1 collective path on one rank (under torchrun)")
     ap.add_argument("--no-extras", action="store_true", help="headline step only (matrix / drop-in / controller legs off)")
-    ap.add_argument("--leg", default="all", choices=("all", "matrix2", "matrix3"),
-                    help="matrix2 / matrix3: only that per-pair leg (for per-kernel PMC passes)")
+    ap.add_argument("--leg", default="all", choices=("all", "matrix2", "matrix3", "cold"),
+                    help="matrix2 / matrix3 / cold: only that leg (for per-kernel PMC passes)")
+    ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache 4M-node K1/K2 roofline leg")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as a captured graph (measured slower than eager launches on ROCm 7.2)")
     return ap.parse_args()
@@ -245,6 +246,80 @@ def matrix_leg(cd, spec, dev, stream, label, val, ts, hv, hv_ts, now, ds, steps,
     return out
 
 
+COLD = dict(nodes=4_000_000, bindings=16_000_000, pods=10_000)
+
+
+def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None):
+    """HBM roofline of the two streaming stages at a size no cache holds (the
+    >= 60 % claim is on cold-cache K1 and K2): 4M nodes, a 16M-entry binding log.  Before
+    the hot-value refresh (K2) and before the node pass (K1 + the step tables) a 1 GiB
+    scratch buffer is READ, which evicts the 256 MiB Infinity Cache and the L2s without
+    leaving dirty lines to be written back during the timed kernels.  Times are the kernels'
+    dispatch-stamped durations (crane_dyn_set_profiling), median over `reps`.
+    Algorithmic bytes:
+      K2 = 12 per binding (node i32 + ts i64 read) + 4 per node and window (counts written)
+      K1 = 16 per node and metric (value + ts read) + 4 per node and window (counts read)
+           + 8 per node (hot value written)"""
+    N, B, P = COLD["nodes"], COLD["bindings"], COLD["pods"]
+    c = synth.make_cluster(spec, N, P, n_bindings=B, seed=7)
+    c.now, c.ds = synth.make_pods(P, seed=8)
+    eng = cd.Engine(cd.Policy(spec), dev.index)
+    val, ts, _ = c.rows(eng.metric_names)
+    eng.upload_nodes(val, ts, c.hv, c.hv_ts)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    del val, ts
+    st = torch.cuda.Stream(dev)
+    sh = st.cuda_stream
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    d_keys = torch.empty(P, dtype=torch.int64, device=dev)
+    scratch = torch.empty(1 << 27, dtype=torch.int64, device=dev).fill_(1)
+    sink = torch.empty(1, dtype=torch.int64, device=dev)
+    M, W = len(eng.metric_names), len(spec["hotValue"])
+    now = int(synth.NOW0_NS)
+
+    def flush():
+        with torch.cuda.stream(st):
+            torch.sum(scratch, dim=0, keepdim=True, out=sink)
+
+    k2, k1, k2_parts = [], [], {}
+    for r in range(reps + 1):
+        flush()
+        eng.set_profiling(True)
+        eng.refresh_hot_values_async(now, now, sh)
+        t_k2 = eng.stage_times()
+        flush()
+        eng.set_profiling(True)
+        eng.eval_keys_async(d_now, d_flags, d_keys, sh)
+        t_ev = eng.stage_times()
+        if r:  # rep 0 warms the code paths
+            k2.append(sum(t for _, t in t_k2))
+            for name, t in t_k2:
+                k2_parts.setdefault(name, []).append(t)
+            k1.append(sum(t for name, t in t_ev if name.startswith("k1_node_pass")))
+    eng.set_profiling(False)
+    eng.close()
+    del scratch
+    k2_ms, k1_ms = float(np.median(k2)), float(np.median(k1))
+    tr_k2 = tr_k1 = None
+    if pmc:
+        ks = pmc.get("kernels", {})
+        k2t = [v.get("traffic_bytes") for k, v in ks.items() if k.startswith("crane::k2")]
+        if k2t and all(t is not None for t in k2t):
+            tr_k2 = int(sum(k2t))
+        k1t = [v.get("traffic_bytes") for k, v in ks.items() if k.startswith("crane::k1_node_pass<")]
+        if len(k1t) == 1 and k1t[0] is not None:
+            tr_k1 = int(k1t[0])
+    alg_k2 = B * 12 + 4 * W * N
+    alg_k1 = N * (16 * M + 4 * W + 8)
+    return {"workload": f"{N} nodes x {B}-entry binding log ({P}-pod batch), default policy",
+            "cache": "cold: 1 GiB read between the stages (Infinity Cache + L2 evicted, no dirty lines)",
+            "k2": roof(alg_k2, k2_ms, "bindings read (12 B) + per-node window counts written (4 B x W)", tr_k2,
+                       {"kernels": {k: round(float(np.median(v)), 4) for k, v in k2_parts.items()}}),
+            "k1": roof(alg_k1, k1_ms, "SoA (value, ts) read + window counts read + hot value written", tr_k1),
+            "traffic_source": pmc_src if (tr_k1 is not None or tr_k2 is not None) else None}
+
+
 def dropin_leg(cd, spec, ann, now, ds, ref_chosen, threads):
     """Per-pod cycle of the C++ plugin mirror as the framework drives it (tools/dropin_bench.cpp)."""
     if not os.path.exists(DROPIN):
@@ -338,11 +413,79 @@ def controller_leg(cd, O, synth, spec, dev, c, N, B):
             "matches_oracle": ok}
 
 
+def launch_ranks(args):
+    """`--gpus N > 1` without a launcher: start N ranks (one process per GPU) under
+    torch.distributed.run as a CHILD process and return its exit code.  Runs before anything
+    touches the GPU (torch.cuda.device_count() does not initialise it on this image)."""
+    have = torch.cuda.device_count()
+    if have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, this host has {have}", file=sys.stderr)
+        return 2
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def build_shard(synth, spec, args, world, rank):
+    """This rank's node shard, as a deterministic slice of ONE global cluster.
+    Config 3 (weak scaling): the global cluster is `world` cells of 100k nodes, each with
+    its own 1M-entry binding log; cell r (seed + r) is rank r's shard, so rank r's nodes
+    are global [r*100k, (r+1)*100k) for every N.  Config 4 (strong scaling): one 1M-node
+    cluster with one 1M-entry binding log (the same arrays at every N); rank r keeps
+    shard_range(1M, N, r) and the bindings of its nodes.  Returns (shard, global offset,
+    global node count, a function that builds the whole global cluster)."""
+    from crane_dyn.shard import shard_range
+    cfg = synth.CONFIGS[args.config]
+    P, B = cfg["pods"], cfg["bindings"]
+    if args.config == 4:
+        def whole():
+            return synth.make_cluster(spec, cfg["nodes"], P, n_bindings=B, seed=20250215 + 4000)
+        full = whole()
+        lo, hi = shard_range(cfg["nodes"], world, rank)
+        c = full.node_slice(lo, hi) if world > 1 else full
+        n_total = cfg["nodes"]
+    else:
+        def cell(r):
+            return synth.make_cluster(spec, cfg["nodes"], P, n_bindings=B, seed=20250215 + args.config * 1000 + r)
+
+        def whole():
+            return synth.concat([cell(r) for r in range(world)])
+        c = cell(rank)
+        lo, n_total = rank * cfg["nodes"], world * cfg["nodes"]
+    # the pod batch is the same on every shard (only nodes and bindings are per rank)
+    c.now, c.ds = synth.make_pods(P, seed=20250215 + args.config)
+    return c, lo, n_total, whole
+
+
+def keys_one_engine(cd, synth, spec, dev, whole, d_now, d_flags, now_sync):
+    """The keys of the batch from ONE engine holding the whole global cluster (its nodes
+    and its binding log) on this GPU: what the all-reduced shard keys must equal."""
+    g = whole()
+    e = cd.Engine(cd.Policy(spec), dev.index)
+    gv, gt, _ = g.rows(e.metric_names)
+    e.upload_nodes(gv, gt, g.hv, g.hv_ts)
+    e.upload_bindings(g.b_node, g.b_ts)
+    k = torch.empty(d_now.numel(), dtype=torch.int64, device=dev)
+    st = torch.cuda.Stream(dev)
+    e.step_keys_async(now_sync, now_sync, d_now, d_flags, k, st.cuda_stream)
+    st.synchronize()
+    e.close()
+    return k, g.n_nodes
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     # the collective path (RCCL all-reduce of the keys); --rehearse-collective runs it on a
     # single rank (torchrun --nproc-per-node 1) to exercise it on a one-GPU box
     coll = world > 1 or args.rehearse_collective
@@ -357,6 +500,11 @@ def main():
 
     shash = src_hash()
     spec = cd.default_policy_spec()
+    if args.leg == "cold":
+        pmc_c, pmc_cs = pmc_summary("cold", shash)
+        out = cold_leg(cd, synth, spec, dev, reps=max(2, args.steps), pmc=pmc_c, pmc_src=pmc_cs)
+        print(json.dumps({"leg": "cold", "src_hash": shash, **out}), flush=True)
+        return
     if args.leg != "all":
         stream = torch.cuda.Stream(dev)
         torch.cuda.set_stream(stream)
@@ -370,14 +518,9 @@ def main():
         print(json.dumps({"leg": args.leg, "src_hash": shash, **out}), flush=True)
         return
 
-    cfg = synth.CONFIGS[args.config]
-    N, P, B = cfg["nodes"], cfg["pods"], cfg["bindings"]
     strong = args.config == 4  # 1M nodes x 100k pods split over the ranks
-    if strong:
-        N = N // world
-    c = synth.make_cluster(spec, N, P, n_bindings=B, seed=20250215 + args.config * 1000 + rank)
-    # the pod batch is the same on every shard (only nodes and bindings are per rank)
-    c.now, c.ds = synth.make_pods(P, seed=20250215 + args.config)
+    c, node_lo, n_total, whole = build_shard(synth, spec, args, world, rank)
+    N, P, B = c.n_nodes, len(c.now), len(c.b_node)
     # K independent pod batches in flight (--inflight): K engines, each with its own copy of
     # the shard's nodes and binding log and its own scratch, on K streams; batch i runs the
     # whole step on engine i % K, so one batch's latency-bound kernels overlap another's
@@ -386,7 +529,7 @@ def main():
     eng = engs[0]
     val, ts, _ = c.rows(eng.metric_names)
     for e in engs:
-        e.upload_nodes(val, ts, c.hv, c.hv_ts, node_offset=rank * N)
+        e.upload_nodes(val, ts, c.hv, c.hv_ts, node_offset=node_lo)
         e.upload_bindings(c.b_node, c.b_ts)
     d_now = torch.from_numpy(c.now).to(dev)
     d_flags = torch.from_numpy(c.ds).to(dev)
@@ -486,6 +629,14 @@ def main():
     else:
         keys_agree = all(torch.equal(d_keys, k) for k in d_keys_k)
     keys = d_keys.cpu().numpy()
+    # the all-reduced keys of the last batch vs one engine holding the whole global cluster
+    keys_match = None
+    if coll and graph is None:
+        if rank == 0:
+            ref_k, n_glob = keys_one_engine(cd, synth, spec, dev, whole, d_now, d_flags, now_sync)
+            assert n_glob == n_total
+            keys_match = bool(torch.equal(ref_k, d_keys))
+        dist.barrier()
     # one batch's latency: the same step with nothing else in flight (outside the timed region)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
@@ -508,7 +659,7 @@ def main():
         torch.cuda.synchronize(dev)
         ar_ms = e0.elapsed_time(e1) / 10
 
-    evals = P * (N * world if not strong else N * world)
+    evals = P * n_total
     value = evals / (ms_step / 1e3)
     placements = P / (ms_step / 1e3)
 
@@ -567,6 +718,11 @@ def main():
                 cd, spec, dev, stream, "config3 nodes/pods (100000 x 10000), node_hot_value annotations: full "
                 "first-fail + score matrices (2 x 1 GB int8) + chosen node", val, ts, c.hv, c.hv_ts, c.now, c.ds, 10,
                 pmc_summary("3m", shash)[0])
+
+    roofline_cold = None
+    if world == 1 and not args.no_extras and not args.no_cold:
+        pmc_c, pmc_cs = pmc_summary("cold", shash)
+        roofline_cold = cold_leg(cd, synth, spec, dev, pmc=pmc_c, pmc_src=pmc_cs)
 
     greedy = None
     if world == 1 and not args.no_greedy and not args.no_extras:
@@ -666,9 +822,13 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"config{args.config}: {N} nodes/GPU x {P} pods, 6 metrics, hot values from "
-                                   f"{B}-entry binding log per GPU, README default policy",
-                       "nodes_per_gpu": N, "pods": P, "bindings_per_gpu": B, "parallelism": f"node-shard x{world}",
+            "config": {"workload": (f"config{args.config}: {n_total} nodes ({N} per GPU) x {P} pods, 6 metrics, "
+                                    + (f"hot values from one {synth.CONFIGS[4]['bindings']}-entry binding log over "
+                                       "all nodes (each rank holds its nodes' entries)" if strong else
+                                       f"hot values from a {B}-entry binding log per 100k-node cell")
+                                    + ", README default policy"),
+                       "nodes_total": n_total, "nodes_per_gpu": N, "pods": P, "bindings_this_rank": B,
+                       "parallelism": f"node-shard x{world}",
                        "launch": ("eager" if graph is None else "hipGraph replay per batch"),
                        "batches_in_flight": K},
             "batches_in_flight": {"k": K, "how": "K engines (own copy of the shard's nodes, binding log, scratch) on "
@@ -680,8 +840,13 @@ def main():
             "placements_per_s": round(placements, 1),
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "allreduce_ms": None if ar_ms is None else round(ar_ms, 4),
+            "keys_match_1gpu": keys_match,
+            "keys_match_1gpu_how": ("the last batch's all-reduced keys [P] == one engine holding the whole "
+                                    f"{n_total}-node global cluster and its binding log, same pods" if coll else
+                                    "single rank: no combine step"),
             "roofline": roofline,
             "roofline_kernels": roofs,
+            "roofline_cold": roofline_cold,
             "src_hash": shash,
             "cpu_baseline": cpu,
             "greedy": greedy,

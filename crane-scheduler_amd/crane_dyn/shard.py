@@ -72,9 +72,25 @@ class ShardedEngine:
         self.engine.eval_keys_async(d_now, d_flags, d_keys, stream)
 
     def schedule(self, now_ns, hv_ts_ns, d_now, d_flags, d_keys, stream=None, group=None):
-        """One batch across all ranks: local step, then the MAX all-reduce (the global choice)."""
+        """One batch across all ranks: local step, then the MAX all-reduce (the global choice).
+        With RCCL ("nccl") the device keys are reduced in place on the current stream; a
+        CPU-only backend (gloo) reduces a host copy, written back into d_keys."""
+        import torch
+        import torch.distributed as dist
+
         self.step_keys(now_ns, hv_ts_ns, d_now, d_flags, d_keys, stream)
-        return allreduce_keys(d_keys, group)
+        if dist.get_backend(group) == "nccl":
+            if stream is not None:  # the keys are produced on `stream`
+                with torch.cuda.stream(torch.cuda.ExternalStream(stream)):
+                    return allreduce_keys(d_keys, group)
+            return allreduce_keys(d_keys, group)
+        if stream is not None:
+            torch.cuda.ExternalStream(stream).synchronize()
+        else:
+            torch.cuda.synchronize(d_keys.device)
+        h = allreduce_keys(d_keys.cpu(), group)
+        d_keys.copy_(h)
+        return d_keys
 
     def close(self):
         self.engine.close()

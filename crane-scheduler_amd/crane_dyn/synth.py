@@ -90,6 +90,21 @@ class Cluster:
         return int(t // 10**9) if t != TS_INVALID else int(self._raw_ts_s[m, n])
 
 
+def concat(cells):
+    """One cluster from node cells laid end to end (cell k's nodes follow cell k-1's; its
+    bindings are re-indexed by the cell's offset).  Pods are the first cell's."""
+    c = dataclasses.replace(cells[0])
+    c.val, c.ts, c.ok, c.malformed = (np.concatenate([getattr(x, f) for x in cells], axis=1)
+                                      for f in ("val", "ts", "ok", "malformed"))
+    c.hv = np.concatenate([x.hv for x in cells])
+    c.hv_ts = np.concatenate([x.hv_ts for x in cells])
+    offs = np.cumsum([0] + [x.n_nodes for x in cells[:-1]])
+    c.b_node = np.concatenate([x.b_node.astype(np.int64) + o for x, o in zip(cells, offs)]).astype(np.int32)
+    c.b_ts = np.concatenate([x.b_ts for x in cells])
+    c._raw_ts_s = np.concatenate([x._raw_ts_s for x in cells], axis=1)
+    return c
+
+
 def _fmt(unix_s, off):
     return (_dt.datetime(1970, 1, 1) + _dt.timedelta(seconds=int(unix_s) + off)).strftime("%Y-%m-%dT%H:%M:%SZ")
 

@@ -188,6 +188,9 @@ struct crane_dyn {
     DevBuf<Step1> sstage;  // K1's one-step staging past its LDS (StepTables::stage)
     DevBuf<int32_t> spm1, ssm0;   // prefix / suffix key maxima of the sorted Step1 records
     DevBuf<int4> srows;           // per (pod tile, producer block): uniform keys + record ranges
+    // asynchronous work enqueued on caller streams: one completion event per stream,
+    // re-recorded by each *_async call; calls that replace engine state wait for all of them
+    std::vector<std::pair<hipStream_t, hipEvent_t>> busy;
     // kernel timing (crane_dyn_set_profiling)
     bool prof = false;
     EngineTimer timer;
@@ -587,6 +590,28 @@ static int flush_heap_slots(crane_dyn* h) {
     return CRANE_OK;
 }
 
+// After enqueueing work that reads engine buffers on a caller stream: mark the stream busy.
+static int mark_busy(crane_dyn* h, hipStream_t st) {
+    if (st == h->stream) return CRANE_OK;  // engine-stream work is ordered by the stream itself
+    for (auto& b : h->busy)
+        if (b.first == st) {
+            HIPTRY(h, hipEventRecord(b.second, st));
+            return CRANE_OK;
+        }
+    hipEvent_t e;
+    HIPTRY(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    h->busy.emplace_back(st, e);
+    HIPTRY(h, hipEventRecord(e, st));
+    return CRANE_OK;
+}
+
+// Before changing or reallocating buffers that asynchronous calls read (node SoA, binding
+// log, scratch): wait until every caller stream's work on this engine has finished.
+static int quiesce(crane_dyn* h) {
+    for (auto& b : h->busy) HIPTRY(h, hipEventSynchronize(b.second));
+    return CRANE_OK;
+}
+
 extern "C" {
 
 const char* crane_dyn_version(void) { return "crane_dyn 0.2 gfx950"; }
@@ -631,6 +656,11 @@ int crane_dyn_destroy(crane_dyn* h) {
         (void)hipSetDevice(h->device);
         (void)hipStreamSynchronize(h->stream);
     }
+    for (auto& b : h->busy) {
+        (void)hipEventSynchronize(b.second);
+        (void)hipEventDestroy(b.second);
+    }
+    h->busy.clear();
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->ev.clear();
     h->val.release(); h->hv.release(); h->ts.release(); h->hv_ts.release(); h->rec.release();
@@ -717,6 +747,7 @@ int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const d
     if (n > 0 && M > 0 && (!val || !ts)) return h->fail(CRANE_E_INVALID, "val/ts must not be NULL");
     if ((hv == nullptr) != (hv_ts == nullptr)) return h->fail(CRANE_E_INVALID, "hv and hv_ts must both be set or NULL");
     HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
     HIPTRY(h, h->val.reserve((size_t)(M * n)));
     HIPTRY(h, h->ts.reserve((size_t)(M * n)));
     HIPTRY(h, h->hv.reserve((size_t)n));
@@ -748,6 +779,7 @@ int crane_dyn_upload_bindings(crane_dyn* h, int64_t n, const int32_t* node, cons
     if (h->N == -2) return h->fail(CRANE_E_STATE, "engine was not created successfully");
     if (n < 0 || (n > 0 && (!node || !ts_s))) return h->fail(CRANE_E_INVALID, "bad binding arrays");
     HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
     HIPTRY(h, h->bnode.reserve((size_t)n));
     HIPTRY(h, h->bts.reserve((size_t)n));
     if (n > 0) {
@@ -768,6 +800,7 @@ int crane_dyn_binding_records(crane_dyn* h, int64_t size, int64_t gc_time_range_
     // size 0 would pop an empty heap in AddBinding (binding.go:73-75); size < 0 never evicts
     if (size <= 0 || size > 0x7FFFFFFF) return h->fail(CRANE_E_INVALID, "binding heap size must be in [1, 2^31)");
     HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
     HIPTRY(h, h->hnode.reserve((size_t)size));
     HIPTRY(h, h->hts.reserve((size_t)size));
     HIPTRY(h, h->bnode.reserve((size_t)size));
@@ -792,6 +825,7 @@ int crane_dyn_add_bindings(crane_dyn* h, int64_t n, const int32_t* node, const i
     if (!h->heap_mode) return h->fail(CRANE_E_STATE, "crane_dyn_binding_records first");
     if (n < 0 || (n > 0 && (!node || !ts_s))) return h->fail(CRANE_E_INVALID, "bad binding arrays");
     HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
     for (int64_t i = 0; i < n; ++i) h->heap.add(node[i], ts_s[i]);
     return flush_heap_slots(h);
 }
@@ -801,12 +835,14 @@ int crane_dyn_gc_bindings(crane_dyn* h, int64_t now_ns) {
     Locked lk(h);
     if (!h->heap_mode) return h->fail(CRANE_E_STATE, "crane_dyn_binding_records first");
     HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
     h->heap.gc(floor_div(now_ns, 1000000000LL));
     return flush_heap_slots(h);
 }
 
 int64_t crane_dyn_binding_count(const crane_dyn* h) {
     if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(const_cast<crane_dyn*>(h)->mu);
     return h->heap_mode ? h->heap.len() : h->B;
 }
 
@@ -850,14 +886,18 @@ int crane_dyn_refresh_hot_values_async(crane_dyn* h, int64_t now_ns, int64_t hv_
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
     HIPTRY(h, hipSetDevice(h->device));
-    return hot_values_locked(h, now_ns, hv_ts_ns, stream ? (hipStream_t)stream : h->stream);
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    int rc = hot_values_locked(h, now_ns, hv_ts_ns, st);
+    return rc ? rc : mark_busy(h, st);
 }
 
 int crane_dyn_node_pass_async(crane_dyn* h, void* stream) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
     HIPTRY(h, hipSetDevice(h->device));
-    return node_pass_locked(h, stream ? (hipStream_t)stream : h->stream);
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    int rc = node_pass_locked(h, st);
+    return rc ? rc : mark_busy(h, st);
 }
 
 int crane_dyn_eval_keys_async(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags,
@@ -866,8 +906,9 @@ int crane_dyn_eval_keys_async(crane_dyn* h, int64_t P, const int64_t* d_now, con
     Locked lk(h);
     if (P < 0 || (P > 0 && (!d_now || !d_keys))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
     HIPTRY(h, hipSetDevice(h->device));
-    return keys_locked(h, P, d_now, d_flags, reinterpret_cast<long long*>(d_keys),
-                       stream ? (hipStream_t)stream : h->stream);
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    int rc = keys_locked(h, P, d_now, d_flags, reinterpret_cast<long long*>(d_keys), st);
+    return rc ? rc : mark_busy(h, st);
 }
 
 int crane_dyn_eval_matrix_async(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags,
@@ -878,8 +919,10 @@ int crane_dyn_eval_matrix_async(crane_dyn* h, int64_t P, const int64_t* d_now, c
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
     if ((d_first_fail || d_score) && ld < h->N) return h->fail(CRANE_E_INVALID, "ld must be >= the node count");
     HIPTRY(h, hipSetDevice(h->device));
-    return matrix_locked(h, P, d_now, d_flags, reinterpret_cast<long long*>(d_keys), d_first_fail, d_score, false, ld,
-                         stream ? (hipStream_t)stream : h->stream);
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    int rc = matrix_locked(h, P, d_now, d_flags, reinterpret_cast<long long*>(d_keys), d_first_fail, d_score, false,
+                           ld, st);
+    return rc ? rc : mark_busy(h, st);
 }
 
 // kube-scheduler v1.23.3 numFeasibleNodesToFind (pkg/scheduler/core/generic_scheduler.go,
@@ -988,7 +1031,7 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
     if (!step_path_ok(h, P) || P == 0) {
         int rc = hot_values_locked(h, now_ns, hv_ts_ns, st);
         if (!rc) rc = keys_locked(h, P, d_now, d_flags, keys, st);
-        return rc;
+        return rc ? rc : mark_busy(h, st);
     }
     // the refresh leaves the records stale: plan for the fused node pass; K3p rides in
     // K2x's launch when the dedupe K2 runs
@@ -1001,7 +1044,7 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
     rc = hot_values_locked(h, now_ns, hv_ts_ns, st, h->opt.k3p_in_k2 ? &pp : nullptr, &pods_done);
     if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, st);
     if (!rc) rc = step_rest(h, sp, P, keys, st);
-    return rc;
+    return rc ? rc : mark_busy(h, st);
 }
 
 // Host-pointer evaluation: the matrices go through device scratch in pod slices of

@@ -20,7 +20,13 @@
  * Conventions: every function returns 0 on success and a negative CRANE_E_*
  * code on failure; crane_dyn_last_error() then describes it.  Callers own all
  * host arrays; the engine copies them during the call and keeps no pointer.
- * Calls on one engine are serialised by an internal mutex.  Nothing in the
+ * Calls on one engine are serialised by an internal mutex.  Asynchronous calls
+ * (*_async) enqueue work that reads the engine's buffers on the caller's stream;
+ * the calls that replace engine state (upload_nodes, upload_bindings,
+ * binding_records, add_bindings, gc_bindings, destroy) first wait for all such
+ * work, so they never change a buffer a kernel is still reading.  Asynchronous
+ * calls on ONE engine from several streams must be ordered by the caller (they
+ * share the engine's scratch): use one stream per engine.  Nothing in the
  * engine reads the environment; crane_dyn_set_option (tests / A-B tools only)
  * selects alternative kernel forms of the same results.
  */

@@ -203,3 +203,53 @@ def test_engine_heap_config3_syncs():
         eng.refresh_hot_values(now_ns, now_ns)
         _, hv = O.hot_values(spec, on, ot, N, synth.NOW0 + s)
         assert np.array_equal(eng.hot_values(), hv.astype(np.float64)), s
+
+
+@pytest.mark.gpu
+def test_heap_change_waits_for_async_step():
+    """A step enqueued on a caller stream reads the binding log; add_bindings / gc_bindings
+    issued right after (no host sync) must not change the slots under it: each step's keys
+    equal a fresh engine's keys for the log as it stood when the step was enqueued."""
+    import torch
+    spec = cd.default_policy_spec()
+    N, P = 20_000, 2_000
+    c = synth.make_cluster(spec, N, P, n_bindings=200_000, seed=31)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    eng = cd.Engine(cd.Policy(spec), 0)
+    val, ts, _ = c.rows(eng.metric_names)
+    eng.upload_nodes(val, ts, c.hv, c.hv_ts)
+    gc = 5 * M_NS
+    eng.binding_records(150_000, gc)
+    eng.add_bindings(c.b_node, c.b_ts)  # the heap evicts the oldest 50k
+    now = int(synth.NOW0_NS)
+    rng = np.random.default_rng(3)
+    keys = []
+    for rep in range(4):
+        k = torch.empty(P, dtype=torch.int64, device=dev)
+        eng.step_keys_async(now, now, d_now, d_flags, k, st.cuda_stream)
+        keys.append(k)
+        hot = rng.integers(0, 50, 40_000).astype(np.int32)  # hammer the hottest nodes' slots
+        eng.add_bindings(hot, np.full(len(hot), synth.NOW0 - rep, np.int64))
+        eng.gc_bindings(now + rep * 10**9)
+    st.synchronize()
+    # replay the same history through the oracle heap and a fresh engine per step
+    ops, nodes, args = [np.zeros(len(c.b_node), np.uint8)], [c.b_node], [c.b_ts]
+    rng = np.random.default_rng(3)
+    for rep in range(4):
+        on, ot = O.binding_heap(150_000, gc, np.concatenate(ops), np.concatenate(nodes), np.concatenate(args))
+        ref = cd.Engine(cd.Policy(spec), 0)
+        ref.upload_nodes(val, ts, c.hv, c.hv_ts)
+        ref.upload_bindings(on, ot)
+        rk = torch.empty(P, dtype=torch.int64, device=dev)
+        ref.step_keys_async(now, now, d_now, d_flags, rk, st.cuda_stream)
+        st.synchronize()
+        ref.close()
+        assert torch.equal(keys[rep], rk), rep
+        hot = rng.integers(0, 50, 40_000).astype(np.int32)
+        ops += [np.zeros(len(hot), np.uint8), np.ones(1, np.uint8)]
+        nodes += [hot, np.zeros(1, np.int32)]
+        args += [np.full(len(hot), synth.NOW0 - rep, np.int64), np.array([(now + rep * 10**9) // 10**9], np.int64)]
+    eng.close()

@@ -153,3 +153,6 @@ def test_greedy_config5_merge_equals_sequential(greedy_mode):
     b = eng.greedy(50_000, now, c.ds)
     assert np.array_equal(a, b)
     assert (a >= 0).all()
+    # placement i depends only on placements < i: the first 2,000 of the full run equal the
+    # oracle's sequential loop over the same cluster cut at 2,000 pods
+    assert np.array_equal(a[:2000], _oracle(spec, c, 2000, now))

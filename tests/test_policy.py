@@ -21,6 +21,21 @@ def test_default_policy_file():
     assert p.spec == {k: [tuple(x) for x in v] for k, v in cd.default_policy_spec().items()}
 
 
+REF_POLICY = "/root/reference/deploy/manifests/dynamic/policy.yaml"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_POLICY), reason="reference checkout absent (build container only)")
+def test_reference_policy_file():
+    """The reference's own shipped policy (deploy/manifests/dynamic/policy.yaml:1-52), read in
+    place with its '##' comment lines and blank lines, decodes to the default policy — the one
+    datum on this path the reference itself holds.  The fixture copy must decode the same."""
+    p = cd.Policy.load_file(REF_POLICY)
+    assert p.spec == {k: [tuple(x) for x in v] for k, v in cd.default_policy_spec().items()}
+    assert p.spec == cd.Policy.load_file(DEFAULT).spec
+    with open(REF_POLICY, "rb") as f:
+        assert cd.Policy.load_bytes(f.read()).spec == p.spec
+
+
 def test_json_equivalent():
     spec = cd.default_policy_spec()
     m = 60 * 10**9

@@ -92,6 +92,48 @@ def test_sharded_choice_matches_unsharded(tmp_path, world):
     assert score.tolist() == ref_score.tolist()
 
 
+def test_bench_gpus_needs_that_many_gpus():
+    """bench.py --gpus N launches N ranks itself, and refuses (instead of timing one rank and
+    reporting n_gpus 1) when fewer GPUs are visible — here, none."""
+    import subprocess
+    import sys
+    if torch.cuda.device_count() >= 4:
+        pytest.skip("host has >= 4 GPUs")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2
+    assert "--gpus 4 needs 4 visible GPUs" in r.stderr
+
+
+def test_bench_global_cluster_slices():
+    """Config-4 shards are slices of ONE global cluster (same arrays at every N), config-3
+    cells are the weak-scaling global cluster's node ranges."""
+    import argparse
+    import bench
+    spec = _spec()
+    saved = dict(synth.CONFIGS)
+    try:
+        synth.CONFIGS[4] = dict(nodes=1000, pods=8, bindings=5000)
+        synth.CONFIGS[3] = dict(nodes=300, pods=8, bindings=2000)
+        for cfg in (3, 4):
+            a = argparse.Namespace(config=cfg)
+            whole = bench.build_shard(synth, spec, a, 3, 0)[3]()
+            for world in (1, 2, 3) if cfg == 4 else (3,):  # (config 3's global cluster grows with N)
+                parts = [bench.build_shard(synth, spec, a, world, r) for r in range(world)]
+                assert sum(p[0].n_nodes for p in parts) == whole.n_nodes
+                for c, lo, n_total, _ in parts:
+                    assert n_total == whole.n_nodes
+                    hi = lo + c.n_nodes
+                    assert np.array_equal(c.val, whole.val[:, lo:hi]) and np.array_equal(c.ts, whole.ts[:, lo:hi])
+                    assert np.array_equal(c.hv, whole.hv[lo:hi]) and np.array_equal(c.hv_ts, whole.hv_ts[lo:hi])
+                    m = (whole.b_node >= lo) & (whole.b_node < hi)
+                    assert np.array_equal(c.b_node, whole.b_node[m] - lo) and np.array_equal(c.b_ts, whole.b_ts[m])
+                    assert np.array_equal(c.now, parts[0][0].now)
+    finally:
+        synth.CONFIGS.clear()
+        synth.CONFIGS.update(saved)
+
+
 def test_shard_ranges_cover():
     for n in (0, 1, 7, 100, 1_000_001):
         for w in (1, 2, 3, 8):

@@ -5,6 +5,8 @@ equal the unsharded engine and the oracle — with forced equal-score ties acros
 shard boundaries, whose winner must be the lowest GLOBAL index (key packing
 (score << 32) | (0xFFFFFFFF - global node), step.hip / matrix.hip).
 Reference: plugins.go:39-98 + upstream selectHost; binding.go:81-97."""
+import os
+
 import numpy as np
 import pytest
 
@@ -101,3 +103,70 @@ def test_sharded_step_with_binding_logs():
     assert np.array_equal(node, och)
     for se in shards:
         se.close()
+
+
+_TWO_PROC = dict(n_nodes=30_011, n_pods=3_000, seed=901, n_bind=300_000)
+
+
+def _two_proc_worker(rank, world, port, out):
+    """One rank: a ShardedEngine on GPU 0 holding its node range and those nodes' bindings,
+    then ShardedEngine.schedule (local step + MAX all-reduce over gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    spec, c = _tied_cluster(_TWO_PROC["n_nodes"], _TWO_PROC["n_pods"], _TWO_PROC["seed"], _TWO_PROC["n_bind"])
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    se = shard.ShardedEngine(cd.Policy(spec), c.n_nodes, world, rank, 0)
+    val, ts, _ = c.rows(se.engine.metric_names)
+    se.upload(val, ts, c.hv, c.hv_ts, c.b_node, c.b_ts)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
+    now = int(synth.NOW0_NS)
+    for rep in range(2):  # the second step re-runs K2 on the same log (idempotent)
+        se.schedule(now, now, d_now, d_flags, d_keys, st.cuda_stream)
+        if rank == 0:
+            np.save(f"{out}.{rep}.npy", d_keys.cpu().numpy())
+    dist.barrier()
+    se.close()
+    dist.destroy_process_group()
+
+
+def test_two_process_sharded_schedule(tmp_path):
+    """Two processes on GPU 0 (one per rank, as bench.py --gpus 2 runs them), each with a
+    ShardedEngine over half the nodes, combined by ShardedEngine.schedule's all-reduce: the
+    keys equal one engine over the whole cluster, and its chosen nodes equal the oracle's."""
+    import socket
+
+    import torch
+    import torch.multiprocessing as mp
+    from oracle import oracle as O
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "keys")
+    mp.start_processes(_two_proc_worker, args=(2, port, out), nprocs=2, start_method="spawn")
+    spec, c = _tied_cluster(_TWO_PROC["n_nodes"], _TWO_PROC["n_pods"], _TWO_PROC["seed"], _TWO_PROC["n_bind"])
+    dev = torch.device("cuda", 0)
+    full = cd.Engine(cd.Policy(spec), 0)
+    val, ts, _ = c.rows(full.metric_names)
+    full.upload_nodes(val, ts, c.hv, c.hv_ts)
+    full.upload_bindings(c.b_node, c.b_ts)
+    now = int(synth.NOW0_NS)
+    ref = torch.empty(len(c.now), dtype=torch.int64, device=dev)
+    full.step_keys_async(now, now, torch.from_numpy(c.now).to(dev), torch.from_numpy(c.ds).to(dev), ref)
+    torch.cuda.synchronize()
+    ref = ref.cpu().numpy()
+    full.close()
+    for rep in range(2):
+        assert np.array_equal(np.load(f"{out}.{rep}.npy"), ref), rep
+    _, hv = O.hot_values(spec, c.b_node, c.b_ts, c.n_nodes, now // 10**9)
+    _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=(hv.astype(np.float64),
+                                                                   np.full(c.n_nodes, now, np.int64)))
+    node, _ = shard.unpack_keys(ref)
+    assert np.array_equal(node, och)
+    assert (node == 3).sum() > 0
