@@ -151,6 +151,8 @@ def parse():
     ap.add_argument("--leg", default="all", choices=("all", "matrix2", "matrix3", "cold"),
                     help="matrix2 / matrix3 / cold: only that leg (for per-kernel PMC passes)")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache 4M-node K1/K2 roofline leg")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="engine option name=value for the --leg runs (A/B of kernel forms; repeatable)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as a captured graph (measured slower than eager launches on ROCm 7.2)")
     return ap.parse_args()
@@ -249,7 +251,7 @@ def matrix_leg(cd, spec, dev, stream, label, val, ts, hv, hv_ts, now, ds, steps,
 COLD = dict(nodes=4_000_000, bindings=16_000_000, pods=10_000)
 
 
-def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None):
+def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
     """HBM roofline of the two streaming stages at a size no cache holds (the
     >= 60 % claim is on cold-cache K1 and K2): 4M nodes, a 16M-entry binding log.  Before
     the hot-value refresh (K2) and before the node pass (K1 + the step tables) a 1 GiB
@@ -264,6 +266,9 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None):
     c = synth.make_cluster(spec, N, P, n_bindings=B, seed=7)
     c.now, c.ds = synth.make_pods(P, seed=8)
     eng = cd.Engine(cd.Policy(spec), dev.index)
+    for o in opts:
+        k, v = o.split("=")
+        eng.set_option(k, int(v))
     val, ts, _ = c.rows(eng.metric_names)
     eng.upload_nodes(val, ts, c.hv, c.hv_ts)
     eng.upload_bindings(c.b_node, c.b_ts)
@@ -502,7 +507,7 @@ def main():
     spec = cd.default_policy_spec()
     if args.leg == "cold":
         pmc_c, pmc_cs = pmc_summary("cold", shash)
-        out = cold_leg(cd, synth, spec, dev, reps=max(2, args.steps), pmc=pmc_c, pmc_src=pmc_cs)
+        out = cold_leg(cd, synth, spec, dev, reps=max(2, args.steps), pmc=pmc_c, pmc_src=pmc_cs, opts=args.opt)
         print(json.dumps({"leg": "cold", "src_hash": shash, **out}), flush=True)
         return
     if args.leg != "all":

@@ -92,7 +92,8 @@ int64_t floor_div(int64_t a, int64_t b) {
 // Engine options: fixed defaults; crane_dyn_set_option changes them per engine
 // (tests and A/B tools only — nothing reads the environment).
 struct Options {
-    int k2_form = 0;          // 0: dedupe (binned / hash when it does not fit), 1: binned, 2: hash
+    int k2_form = 0;          // 0: dedupe (large / binned / hash when it does not fit), 1: binned, 2: hash,
+                              // 3: large (region pass with coarse bins + dense per-bin histograms)
     int k1_threads = 256;     // K1 workgroup size (the dedupe K2 bins nodes by it): 128 or 256
     bool k1_keep_rec = false; // the fused keys-only step also writes the node records
     int k1_split = 0;         // K1+K3a as two kernels (count, then k3a_emit): 0 never, 1 always,
@@ -144,6 +145,7 @@ struct crane_dyn {
     int64_t hv_ts_counts = 0;
     bool rec_dirty = true;
     bool buckets_zero = false;    // K1 consumes (zeroes) the buckets K2 filled
+    bool buckets_dense = false;   // ... unless the large form wrote them whole (K1 leaves them)
     bool counts_pending = false;  // buckets hold K2 counts no node pass has consumed yet
     bool hx_pending = false;      // ... in the dedupe form: per-block entries in k2_sorted (hx_g)
     HotPart hx_g{};
@@ -371,6 +373,18 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     const size_t nb = (size_t)std::max(1, dp.n_win) * (size_t)std::max<int64_t>(h->N, 1);
     if (nb > h->buckets.n) h->buckets_zero = false;
     HIPTRY(h, h->buckets.reserve(nb));
+    const HotPart gl = hot_large_geometry(h->B, h->N, dp.n_win);
+    if ((h->opt.k2_form == 0 || h->opt.k2_form == 3) && gl.ok) {
+        // the region pass with coarse bins + the dense per-bin histogram: every bucket row
+        // is rewritten, so nothing is zeroed before and K1 leaves them
+        HIPTRY(h, h->k2_sorted.reserve(hot_dedupe_scratch(gl)));
+        HIPTRY(h, launch_hot_count_large(h->bnode.p, h->bts.p, h->B, h->N, cut, gl, h->k2_sorted.p, h->buckets.p, st,
+                                         h->opt.k2x_threads));
+        h->buckets_zero = false;
+        h->buckets_dense = true;
+        return CRANE_OK;
+    }
+    h->buckets_dense = false;
     if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
     const HotBins g = hot_bins_geometry(h->B, h->N, dp.n_win);
     if (g.ok && h->opt.k2_form != 2) {
@@ -417,6 +431,7 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
             a.hx_nblk = g.nblk;
         } else {
             a.buckets = h->buckets.p;
+            a.buckets_keep = h->buckets_dense ? 1 : 0;
         }
         a.cnt_out = cnt_out;
         a.hvc_out = h->hvc.p;
@@ -430,7 +445,7 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
     a.trace = (h->N + a.threads - 1) / a.threads <= kTraceWgs ? h->trace_region(1) : nullptr;
     HIPTRY(h, launch_node_pass(h->shape, a, st, step));
     if (consume) {
-        if (!h->hx_pending) h->buckets_zero = true;  // K1 zeroed what it read
+        if (!h->hx_pending) h->buckets_zero = !h->buckets_dense;  // K1 zeroed what it read
         h->counts_pending = false;
         h->hx_pending = false;
     }
@@ -695,7 +710,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     const std::string n = name;
     Options& o = h->opt;
     auto range = [&](int64_t lo, int64_t hi) { return value >= lo && value <= hi; };
-    if (n == "k2_form" && range(0, 2)) o.k2_form = (int)value;
+    if (n == "k2_form" && range(0, 3)) o.k2_form = (int)value;
     else if (n == "k1_threads" && (value == 128 || value == 256)) o.k1_threads = (int)value;
     else if (n == "k1_split" && range(0, 2)) o.k1_split = (int)value;
     else if (n == "k1_keep_records" && range(0, 1)) o.k1_keep_rec = value != 0;

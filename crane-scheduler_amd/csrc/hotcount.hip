@@ -27,6 +27,7 @@
 #include "dyn_types.hpp"
 #include "kernels.hpp"
 #include "pods.hpp"
+#include "step_node.hpp"
 
 namespace crane {
 
@@ -240,10 +241,11 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     int32_t nd[kPer];
     int64_t ts[kPer];
 #pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-        const int64_t b = b0 + u * BT;
-        nd[u] = b < B ? bnode[b] : -1;
-        ts[u] = b < B ? bts[b] : INT64_MIN;
+    for (int u = 0; u < kPer; ++u) {  // unconditional loads (clamped index): all in flight at once
+        const int64_t b = b0 + u * BT, bc = min(b, B - 1);
+        nd[u] = bnode[bc];
+        ts[u] = bts[bc];
+        if (b >= B) nd[u] = -1;
     }
     for (int i = threadIdx.x; i < kDSlots; i += BT) {
         hkey[i] = -1;
@@ -294,8 +296,10 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
         run += c;
     }
     __syncthreads();
-    // this region's row of (count | offset << 16) per node block: coalesced
-    for (int i = threadIdx.x; i < g.nbins; i += BT) CO[(int64_t)blk * g.nbins + i] = hist[i] | (off[i] << 16);
+    // this region's (count | offset << 16) per bin, column blk of CO [nbins][nblk]: the readers
+    // (K1 per node block, Y per coarse bin) read their bin's row contiguously; the regions of
+    // one XCD are consecutive (xcd_block), so a CO line is written whole in one L2
+    for (int i = threadIdx.x; i < g.nbins; i += BT) CO[(int64_t)i * g.nblk + blk] = hist[i] | (off[i] << 16);
     __syncthreads();
     CRANE_TSTAMP(g.trace, blk, 3);
     uint32_t* reg = region + (int64_t)blk * kXChunk;
@@ -319,7 +323,7 @@ template <int BT>
 __global__ __launch_bounds__(BT) void k2x_dedupe(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
                                                  int64_t B, int64_t N, HotCutoffs cut, HotPart g,
                                                  uint32_t* __restrict__ CO, uint32_t* __restrict__ region) {
-    k2d_body<BT>((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
+    k2d_body<BT>((int32_t)xcd_block(blockIdx.x, gridDim.x), bnode, bts, B, N, cut, g, CO, region);
 }
 
 template <int BT>
@@ -329,11 +333,12 @@ __global__ __launch_bounds__(BT) void k2x_dedupe_pods(const int32_t* __restrict_
                                                       uint32_t* __restrict__ region, PodPrep pp) {
     // the pod tiles first: dispatched first, their sort overlaps the regions' aggregation
     // instead of trailing the launch
-    if ((int64_t)blockIdx.x >= pp.ntiles) {
-        k2d_body<BT>((int32_t)(blockIdx.x - pp.ntiles), bnode, bts, B, N, cut, g, CO, region);
+    const int64_t m = xcd_block(blockIdx.x, gridDim.x);  // (pod tiles: blocks 0, 8, 16, ...)
+    if (m >= pp.ntiles) {
+        k2d_body<BT>((int32_t)(m - pp.ntiles), bnode, bts, B, N, cut, g, CO, region);
     } else {
         extern __shared__ __attribute__((aligned(16))) unsigned char k3p_lds[];
-        k3p_tile<BT>((int64_t)blockIdx.x, pp, k3p_lds);
+        k3p_tile<BT>(m, pp, k3p_lds);
     }
 }
 
@@ -386,6 +391,127 @@ hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int
 }
 
 size_t hot_dedupe_scratch(const HotPart& g) { return (size_t)g.cap + (size_t)g.nbins * (size_t)g.nblk; }
+
+// ---------------------------------------------------------------- large form
+// When the dedupe form's count/offset matrix (K1 blocks x regions) would pass its cap
+// (e.g. 4M nodes x 16M bindings: 15,625 x 7,813 words), the same region pass runs with
+// COARSE bins of 2^bb nodes (16K at two windows: 245 bins at 4M nodes), and a second
+// kernel turns each coarse bin into dense window-rank buckets:
+//   X  k2x_dedupe (above) with the coarse geometry: one pass over the log, entries
+//      aggregated per (region, node, bucket) — a Zipf-hot node costs one entry per region;
+//   Y  k2y_bin_hist: one workgroup per coarse bin gathers the bin's entries from every
+//      region (count/offset column, then the runs) into an LDS histogram [W][2^bb] and
+//      writes the bin's rows of buckets [W][N] whole — no global atomics, nothing to zero
+//      (K1 reads them and leaves them, K1Args::buckets_keep).
+// Consecutive bins run on one XCD (xcd_block), so the count/offset lines and region runs
+// that neighbouring bins share are fetched into that XCD's L2 once.
+constexpr int kYThreads = 1024;
+constexpr int kYPer = 8;     // regions per lane per round (16M bindings: 7,813 regions, one round)
+constexpr int kYFirst = 4;   // entries per run loaded with the count/offset words' round
+constexpr int kYQ = 2048;    // LDS queue of the longer runs' tails
+
+// Every load is unconditional (clamped index, result masked): conditional loads made the
+// compiler wait for each one before issuing the next.
+__global__ __launch_bounds__(kYThreads) void k2y_bin_hist(const uint32_t* __restrict__ region,
+                                                          const uint32_t* __restrict__ CO, HotPart g, int32_t W,
+                                                          int64_t N, uint32_t* __restrict__ buckets) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // [W][2^bb]
+    __shared__ uint2 q[kYQ];  // tail of a run: {first entry index, entries left}
+    __shared__ uint32_t qn;
+    const int bb = g.bb, binw = 1 << bb;
+    const int64_t bin = xcd_block(blockIdx.x, gridDim.x);
+    const uint32_t lmask = (uint32_t)binw - 1;
+    auto add = [&](uint32_t v) { atomicAdd(&hist[((v >> 16) & 7) * binw + (v & lmask)], v >> 19); };
+    for (int i0 = 0; i0 < g.nblk; i0 += kYThreads * kYPer) {
+        // this bin's (count, offset) word of kYPer regions per lane, then their runs' first entries
+        uint32_t c[kYPer], o[kYPer];
+#pragma unroll
+        for (int u = 0; u < kYPer; ++u) {
+            const int i = i0 + u * kYThreads + threadIdx.x;
+            const uint32_t co = CO[bin * g.nblk + min(i, g.nblk - 1)];  // the bin's row: coalesced
+            c[u] = i < g.nblk ? co & 0xFFFF : 0u;
+            o[u] = co >> 16;
+        }
+        // lanes past a run's end all load entry 0 (one shared line), so a load instruction
+        // costs the lines of the runs it reads
+        uint32_t v[kYPer][kYFirst];
+#pragma unroll
+        for (int u = 0; u < kYPer; ++u) {
+            const int64_t e0 = (int64_t)(i0 + u * kYThreads + threadIdx.x) * kHxRegion + o[u];
+#pragma unroll
+            for (int k = 0; k < kYFirst; ++k) v[u][k] = region[(uint32_t)k < c[u] ? e0 + k : 0];
+        }
+        if (i0 == 0) {
+            uint4* h4 = reinterpret_cast<uint4*>(hist);
+            const int n4 = (W * binw) >> 2;
+            for (int i = threadIdx.x; i < n4; i += kYThreads) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        if (threadIdx.x == 0) qn = 0;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kYPer; ++u) {
+#pragma unroll
+            for (int k = 0; k < kYFirst; ++k)
+                if ((uint32_t)k < c[u]) add(v[u][k]);
+            if (c[u] > (uint32_t)kYFirst) {  // the rest of a longer run: queued for the whole workgroup
+                const uint32_t e0 = (uint32_t)(i0 + u * kYThreads + threadIdx.x) * kHxRegion + o[u] + kYFirst;
+                const uint32_t p = atomicAdd(&qn, 1u);
+                if (p < (uint32_t)kYQ) {
+                    q[p] = make_uint2(e0, c[u] - kYFirst);
+                } else {  // queue full: this lane walks it
+                    for (uint32_t k = 0; k < c[u] - kYFirst; ++k) add(region[e0 + k]);
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t nq = min(qn, (uint32_t)kYQ);
+        for (uint32_t j = threadIdx.x; j < nq; j += kYThreads) {
+            const uint2 it = q[j];
+            for (uint32_t k0 = 0; k0 < it.y; k0 += 8) {
+                uint32_t w[8];
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) w[jj] = region[k0 + jj < it.y ? (int64_t)it.x + k0 + jj : 0];
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj)
+                    if (k0 + jj < it.y) add(w[jj]);
+            }
+        }
+        __syncthreads();  // (qn / q reused by the next round; hist complete after the last)
+    }
+    // the bin's rows, whole: lane i -> node n0 + i
+    const int64_t n0 = bin << bb;
+    const int nn = (int)min((int64_t)binw, N - n0);
+    for (int w = 0; w < W; ++w)
+        for (int i = threadIdx.x; i < nn; i += kYThreads) buckets[(int64_t)w * N + n0 + i] = hist[w * binw + i];
+}
+
+HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W) {
+    HotPart g{};
+    int bb = 16;  // entry format: local node in 16 bits
+    while (bb > 8 && (int64_t)std::max(W, 1) * (4LL << bb) > kK2LargeHistBytes) --bb;  // Y's LDS histogram
+    g.bb = bb;
+    g.nbins = (int32_t)((N + (1LL << bb) - 1) >> bb);
+    g.nblk = (int32_t)((B + kXChunk - 1) / kXChunk);
+    g.cap = (int64_t)g.nblk * kXChunk;
+    g.ok = N > 0 && B > 0 && W >= 1 && W <= kMaxWin && N < (1LL << 27) && B < (1LL << 31) && g.nbins <= 4096 &&
+           (double)g.nbins * (double)g.nblk <= (double)(1LL << 27);
+    return g;
+}
+
+hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
+                                  const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, uint32_t* buckets,
+                                  hipStream_t st, int threads) {
+    // (dynamic + the static tail queue stay within the CU's 160 KiB)
+    static const hipError_t attr = hipFuncSetAttribute((const void*)k2y_bin_hist,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)kK2LargeHistBytes);
+    if (attr != hipSuccess) return attr;
+    hipError_t e = launch_hot_count_dedupe(bnode, bts, B, N, cut, g, scratch, st, nullptr, threads);
+    if (e != hipSuccess) return e;
+    const size_t lds = sizeof(uint32_t) * (size_t)cut.n_win * ((size_t)1 << g.bb);
+    return klaunch("k2y_bin_hist", k2y_bin_hist, dim3((unsigned)g.nbins), dim3(kYThreads), lds, st,
+                   (const uint32_t*)scratch, (const uint32_t*)(scratch + g.cap), g, cut.n_win, N, buckets);
+}
 
 HotBins hot_bins_geometry(int64_t B, int64_t N, int32_t W) {
     HotBins g{};

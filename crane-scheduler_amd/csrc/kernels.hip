@@ -175,54 +175,55 @@ void k1_node_pass(K1Args a, K1Step step) {
     // wait on them, not on the whole SoA batch
     constexpr int kHxPer = 3, kHxFirst = 4, kHxRun = 8;
     uint32_t co0[kHxPer];
+    // Every load is unconditional, with a clamped index (lanes past N re-read node N-1, rows
+    // past npd/npr read row 0; both ignored): a load inside a branch makes the compiler wait
+    // for all loads at the join (s_waitcnt vmcnt(0)), which serialised the dedupe-form chain
+    // below behind the whole SoA stream.
+    const int lo = (int)min((int64_t)threadIdx.x, N - 1 - first);  // lane offset, clamped
     if (hx) {
+        const uint32_t* __restrict__ corow = a.hx_CO + blk * (int64_t)a.hx_nblk;  // this block's row
 #pragma unroll
-        for (int u = 0; u < kHxPer; ++u) {
-            const int i = u * kK1Threads + threadIdx.x;
-            co0[u] = i < a.hx_nblk ? a.hx_CO[(int64_t)i * gridDim.x + blk] : 0u;
-        }
+        for (int u = 0; u < kHxPer; ++u)  // (masked where used: a use here would wait for them)
+            co0[u] = corow[min(u * kK1Threads + (int)threadIdx.x, a.hx_nblk - 1)];
         for (int b = 0; b < kMaxWin; ++b) hxh[b][threadIdx.x] = 0;
     }
-    if (n < N) {
-        // every load first, unconditionally (rows past npd/npr read row 0 and are
-        // ignored), so a wave has them all in flight at once; compute after
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+        pt[k] = kTsInvalid;
+        pv[k] = 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+        qt[k] = kTsInvalid;
+        qv[k] = 0.0;
+    }
+    if (pol.n_slots > 0) {  // (val/ts are null without metrics; uniform branch)
 #pragma unroll
         for (int k = 0; k < PD; ++k) {
-            pt[k] = kTsInvalid;
-            pv[k] = 0.0;
+            const int64_t row = k < pol.npd ? pol.pred_slot[k] : 0;
+            // uniform row base + lane offset (the SGPR-base load form)
+            const int64_t* __restrict__ tr = ts + (row * N + first);
+            const double* __restrict__ vr = val + (row * N + first);
+            pt[k] = tr[lo];
+            pv[k] = vr[lo];
         }
 #pragma unroll
         for (int k = 0; k < PR; ++k) {
-            qt[k] = kTsInvalid;
-            qv[k] = 0.0;
+            const int64_t row = k < pol.npr ? pol.prio_slot[k] : 0;
+            const int64_t* __restrict__ tr = ts + (row * N + first);
+            const double* __restrict__ vr = val + (row * N + first);
+            qt[k] = tr[lo];
+            qv[k] = vr[lo];
         }
-        if (pol.n_slots > 0) {  // (val/ts are null without metrics)
+    }
+    if (buckets) {
 #pragma unroll
-            for (int k = 0; k < PD; ++k) {
-                const int64_t row = k < pol.npd ? pol.pred_slot[k] : 0;
-                // uniform row base + lane offset (the SGPR-base load form)
-                const int64_t* __restrict__ tr = ts + (row * N + first);
-                const double* __restrict__ vr = val + (row * N + first);
-                pt[k] = tr[threadIdx.x];
-                pv[k] = vr[threadIdx.x];
-            }
-#pragma unroll
-            for (int k = 0; k < PR; ++k) {
-                const int64_t row = k < pol.npr ? pol.prio_slot[k] : 0;
-                const int64_t* __restrict__ tr = ts + (row * N + first);
-                const double* __restrict__ vr = val + (row * N + first);
-                qt[k] = tr[threadIdx.x];
-                qv[k] = vr[threadIdx.x];
-            }
-        }
-        if (buckets) {
-#pragma unroll
-            for (int b = 0; b < kMaxWin; ++b) bc[b] = b < pol.n_win ? (buckets + first)[(int64_t)b * N + threadIdx.x] : 0u;
-        }
-        if (!buckets && !hx && hv) {
-            hvl = hv[n];
-            hvt = hv_ts ? hv_ts[n] : hv_ts_counts;  // null: the binding-log value of an earlier pass
-        }
+        for (int b = 0; b < kMaxWin; ++b)
+            bc[b] = b < pol.n_win ? (buckets + first)[(int64_t)b * N + lo] : 0u;
+    }
+    if (!buckets && !hx && hv) {
+        hvl = hv[first + lo];
+        hvt = hv_ts ? hv_ts[first + lo] : hv_ts_counts;  // null: the binding-log value of an earlier pass
     }
     if (hx) {
         // this block's (node, bucket, count) entries from every K2 source region
@@ -233,16 +234,17 @@ void k1_node_pass(K1Args a, K1Step step) {
 #pragma unroll
             for (int u = 0; u < kHxPer; ++u) {
                 const int i = i0 + u * kK1Threads + threadIdx.x;
-                const uint32_t co = i0 == 0 ? co0[u] : i < a.hx_nblk ? a.hx_CO[(int64_t)i * gridDim.x + blk] : 0u;
-                c[u] = co & 0xFFFF;
+                const uint32_t co = i0 == 0 ? co0[u] : a.hx_CO[blk * (int64_t)a.hx_nblk + min(i, a.hx_nblk - 1)];
+                c[u] = i < a.hx_nblk ? co & 0xFFFF : 0u;
                 o[u] = co >> 16;
             }
+            // lanes past a run's end load entry 0 of the region array (one shared line)
             uint32_t v[kHxPer][kHxFirst];
 #pragma unroll
             for (int u = 0; u < kHxPer; ++u) {
-                const uint32_t* src = a.hx_region + (int64_t)(i0 + u * kK1Threads + threadIdx.x) * kHxRegion + o[u];
+                const int64_t e0 = (int64_t)(i0 + u * kK1Threads + threadIdx.x) * kHxRegion + o[u];
 #pragma unroll
-                for (int k = 0; k < kHxFirst; ++k) v[u][k] = (uint32_t)k < c[u] ? src[k] : 0u;
+                for (int k = 0; k < kHxFirst; ++k) v[u][k] = a.hx_region[(uint32_t)k < c[u] ? e0 + k : 0];
             }
             if (i0 == 0) __syncthreads();  // hxh zeroed by every thread (uniform trip count)
 #pragma unroll
@@ -256,7 +258,7 @@ void k1_node_pass(K1Args a, K1Step step) {
                 for (uint32_t k0 = kHxFirst; k0 < c[u]; k0 += kHxRun) {
                     uint32_t w[kHxRun];
 #pragma unroll
-                    for (int j = 0; j < kHxRun; ++j) w[j] = k0 + j < c[u] ? src[k0 + j] : 0u;
+                    for (int j = 0; j < kHxRun; ++j) w[j] = src[k0 + j < c[u] ? k0 + j : 0];
 #pragma unroll
                     for (int j = 0; j < kHxRun; ++j)
                         if (k0 + j < c[u]) atomicAdd(&hxh[(w[j] >> 16) & 7][w[j] & 0xFFFF], w[j] >> 19);
@@ -309,7 +311,7 @@ void k1_node_pass(K1Args a, K1Step step) {
         if (buckets || hx) {
             // annotateNodeHotValue (node.go:113-121): value += count / p.Count (Go int division)
             // window w counts the bindings of buckets >= its cutoff rank (K2)
-            if (buckets) {
+            if (buckets && !a.buckets_keep) {
 #pragma unroll
                 for (int b = 0; b < kMaxWin; ++b)  // consumed: leaves the buckets zeroed for the next K2
                     if (b < pol.n_win) (buckets + first)[(int64_t)b * N + threadIdx.x] = 0;

@@ -185,6 +185,15 @@ size_t hot_dedupe_scratch(const HotPart& g);  // uint32 entries: regions + count
 hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                    const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
                                    const PodPrep* pods = nullptr, int threads = 1024);
+// Large form (past the dedupe form's cap): the same region pass with coarse bins of 2^bb
+// nodes (Y's LDS histogram [W][2^bb] <= kK2LargeHistBytes), then k2y_bin_hist writes the
+// dense window-rank buckets [W][N] (every row of every bin: K1 reads them, nothing to zero).
+// scratch: hot_dedupe_scratch(g) words.
+constexpr int64_t kK2LargeHistBytes = 128 * 1024;
+HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W);
+hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
+                                  const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, uint32_t* buckets,
+                                  hipStream_t st, int threads);
 
 // ---------------------------------------------------------------- K3 step path (step.hip)
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
@@ -283,6 +292,7 @@ struct K1Args {
     const double* hv;       // [N] or null
     const int64_t* hv_ts;   // [N] or null
     uint32_t* buckets;      // [W][N] K2 window-rank buckets or null
+    int32_t buckets_keep;   // 1: leave them (the large form rewrites every row), 0: zero what was read
     int64_t hv_ts_counts;   // stamp of binding-log hot values
     void* out;              // NodeRec [N], or null (keys-only step: records not kept)
     uint32_t* cnt_out;      // [W][N] per-window counts (greedy) or null

@@ -266,7 +266,7 @@ int64_t crane_dyn_key_node(int64_t key, int64_t *score);
 const char *crane_dyn_version(void);
 
 /* Alternative kernel forms of the same results, for tests and A/B tools:
- *   "k2_form" 0 dedupe (default) | 1 binned | 2 hash   "k1_threads" 256 | 128
+ *   "k2_form" 0 dedupe (default; large past its cap) | 1 binned | 2 hash | 3 large   "k1_threads" 256 | 128
  *   "k1_keep_records" 0 | 1   "k1_fuse_steps" 1 | 0   "k3p_in_k2" 1 | 0
  *   "k1_split" 0 fused node pass | 1 count pass + k3a_emit | 2 split past one round of workgroups
  *   "keys_path" 0 step path | 1 per-pair kernel   "greedy_form" 0 merge | 1 sequential

@@ -142,9 +142,9 @@ def test_hot_values_vs_oracle(kats):
     assert sc[0, 0] == 50  # hv = 5 (SURVEY KAT-11)
 
 
-@pytest.mark.parametrize("k2", [0, 1, 2], ids=["dedupe", "binned", "hash"])
+@pytest.mark.parametrize("k2", [0, 1, 2, 3], ids=["dedupe", "binned", "hash", "large"])
 @pytest.mark.parametrize("n_nodes,n_bind,seed", [(1000, 50_000, 1), (20_000, 300_000, 2), (100, 10, 3),
-                                                 (70_000, 2_000_000, 4)])
+                                                 (70_000, 2_000_000, 4), (40_000, 5_000_000, 5)])
 def test_hot_values_random(n_nodes, n_bind, seed, k2):
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, n_nodes, 16, n_bindings=n_bind, seed=seed, pod_step_ns=10_000_000_000)
@@ -162,9 +162,10 @@ def test_hot_values_random(n_nodes, n_bind, seed, k2):
     assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch, och)
 
 
-@pytest.mark.parametrize("threads,k2x", [(128, 512), (256, 512), (256, 1024), (256, 256)])
+@pytest.mark.parametrize("threads,k2x,k2", [(128, 512, 0), (256, 512, 0), (256, 1024, 0), (256, 256, 0),
+                                            (256, 512, 3), (256, 1024, 3)])
 @pytest.mark.parametrize("case", ["one_hot_node", "eight_windows", "last_node", "odd_counts"])
-def test_hot_values_dedupe_edges(case, threads, k2x):
+def test_hot_values_dedupe_edges(case, threads, k2x, k2):
     """Dedupe-form K2 (per-workgroup (node, bucket) aggregation, counts read by the
     node pass) at its packing limits: a region whose 2048 bindings all hit one node
     (count field), eight windows (bucket field), the shard's last node and bindings
@@ -187,7 +188,7 @@ def test_hot_values_dedupe_edges(case, threads, k2x):
         bn[::3] = n_nodes - 1
         bn[1::7] = n_nodes  # past the shard: ignored
         bn[2::11] = -3
-    eng = engine_for(spec, c, opts={"k2_form": 0, "k1_threads": threads, "k2x_threads": k2x})
+    eng = engine_for(spec, c, opts={"k2_form": k2, "k1_threads": threads, "k2x_threads": k2x})
     eng.upload_bindings(bn, c.b_ts)
     now = int(c.now[0])
     for rep in range(2):  # a second refresh after the first was consumed
@@ -199,6 +200,41 @@ def test_hot_values_dedupe_edges(case, threads, k2x):
         assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch, och), rep
     eng.refresh_hot_values(now, now)  # read back before any node pass consumed it
     assert np.array_equal(eng.hot_values(), cnt_hv.astype(np.float64))
+
+
+@pytest.mark.slow
+def test_hot_values_large_form_16m():
+    """The cold-leg size (4M nodes x 16M bindings), where the dedupe form's count/offset
+    matrix passes its cap and the large form runs by default: hot values equal the oracle's
+    (binding.go:81-97, node.go:113-121) and the binned form's, before and after a K1 pass
+    consumed them; a pod sample's Filter/Score/argmax equals the oracle over all 4M nodes."""
+    spec = cd.default_policy_spec()
+    N, B = 4_000_000, 16_000_000
+    c = synth.make_cluster(spec, N, 8, n_bindings=B, seed=7, pod_step_ns=20_000_000_000)
+    bn = c.b_node.copy()
+    bn[::1009] = -1
+    bn[1::1013] = N + 3
+    eng = engine_for(spec, c)
+    eng.upload_bindings(bn, c.b_ts)
+    now = int(synth.NOW0_NS)
+    _, cnt_hv = O.hot_values(spec, bn, c.b_ts, N, now // 10**9)
+    ref = cnt_hv.astype(np.float64)
+    eng.set_profiling(True)
+    eng.refresh_hot_values(now, now)
+    assert [n for n, _ in eng.stage_times()] == ["k2x_dedupe", "k2y_bin_hist"]
+    eng.set_profiling(False)
+    assert np.array_equal(eng.hot_values(), ref)
+    _, _, ch, _ = eng.eval(c.now, c.ds)
+    _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=(ref, np.full(N, now, np.int64)))
+    assert np.array_equal(ch, och)
+    eng.refresh_hot_values(now, now)  # again: the buckets are rewritten whole, nothing left to zero
+    assert np.array_equal(eng.hot_values(), ref)
+    eng.set_option("k2_form", 1)
+    eng.refresh_hot_values(now, now)
+    assert np.array_equal(eng.hot_values(), ref)
+    eng.set_option("k2_form", 0)
+    eng.refresh_hot_values(now, now)
+    assert np.array_equal(eng.hot_values(), ref)
 
 
 def test_division_exactness_sweep(kp):
