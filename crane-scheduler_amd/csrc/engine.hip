@@ -109,6 +109,9 @@ struct Options {
     int step_rows = 1;        // 1: producers write per-tile record ranges for K3s, 0: K3s searches
     int k3s_blocks = 0;       // K3s producer blocks per workgroup aimed for: 0 automatic
     int k2x_threads = 512;    // dedupe K2 workgroup size: 256, 512 or 1024
+    int k2l_region = 4096;    // large K2: bindings per region (2048 or 4096)
+    int k2l_co_t = 0;         // large K2: count/offset words [bin][region] (1) or [region][bin] (0)
+    int k2l_threads = 512;    // large K2: partition workgroup size at 4096-binding regions (512 or 1024)
     int step_lds_cap = 1 << 30;  // K1: one-step records per kind staged in LDS at most (0: always st.stage)
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
 };
@@ -373,13 +376,14 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     const size_t nb = (size_t)std::max(1, dp.n_win) * (size_t)std::max<int64_t>(h->N, 1);
     if (nb > h->buckets.n) h->buckets_zero = false;
     HIPTRY(h, h->buckets.reserve(nb));
-    const HotPart gl = hot_large_geometry(h->B, h->N, dp.n_win);
+    HotPart gl = hot_large_geometry(h->B, h->N, dp.n_win, h->opt.k2l_region, h->opt.k2l_co_t);
+    gl.trace = gl.nblk <= kTraceWgs ? h->trace_region(0) : nullptr;  // (stamps per region)
     if ((h->opt.k2_form == 0 || h->opt.k2_form == 3) && gl.ok) {
         // the region pass with coarse bins + the dense per-bin histogram: every bucket row
         // is rewritten, so nothing is zeroed before and K1 leaves them
         HIPTRY(h, h->k2_sorted.reserve(hot_dedupe_scratch(gl)));
-        HIPTRY(h, launch_hot_count_large(h->bnode.p, h->bts.p, h->B, h->N, cut, gl, h->k2_sorted.p, h->buckets.p, st,
-                                         h->opt.k2x_threads));
+        HIPTRY(h, launch_hot_count_large(h->bnode.p, h->bts.p, h->B, h->N, cut, gl, h->k2_sorted.p, h->buckets.p,
+                                         h->n_cu, st, h->opt.k2l_threads));
         h->buckets_zero = false;
         h->buckets_dense = true;
         return CRANE_OK;
@@ -723,6 +727,9 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "step_rows" && range(0, 1)) o.step_rows = (int)value;
     else if (n == "k3s_blocks" && range(0, 256)) o.k3s_blocks = (int)value;
     else if (n == "k2x_threads" && (value == 256 || value == 512 || value == 1024)) o.k2x_threads = (int)value;
+    else if (n == "k2l_region" && (value == 2048 || value == 4096)) o.k2l_region = (int)value;
+    else if (n == "k2l_co_t" && range(0, 1)) o.k2l_co_t = (int)value;
+    else if (n == "k2l_threads" && (value == 512 || value == 1024)) o.k2l_threads = (int)value;
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;

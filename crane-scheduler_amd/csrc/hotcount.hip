@@ -199,27 +199,54 @@ __device__ __forceinline__ uint32_t wg_excl_scan_u32(uint32_t v, uint32_t* part)
 constexpr int kDSlots = 4096;  // 2 slots per binding: an empty or matching slot always exists
 
 // Adds `add` to key's count; a lane that inserts a new key also counts it in its
-// bin and returns its slot (else -1).
+// bin and returns its slot (else -1).  One returning LDS atomic per probe (the CAS
+// itself tells an empty, a matching and a foreign slot apart).
+template <int SLOTS = kDSlots>
 __device__ __forceinline__ int32_t hash_add(int32_t* hkey, uint32_t* hcnt, uint32_t* hist, int bb, int32_t key,
                                             uint32_t add) {
-    uint32_t h = ((uint32_t)key * 2654435761u) >> (32 - 12);
-    for (;;) {  // ends: <= 2048 distinct keys in 4096 slots
-        int32_t k = __hip_atomic_load(&hkey[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (k == -1) {
-            const int32_t old = atomicCAS(&hkey[h], -1, key);
+    constexpr int kBits = __builtin_ctz(SLOTS);
+    uint32_t h = ((uint32_t)key * 2654435761u) >> (32 - kBits);
+    for (;;) {  // ends: at most SLOTS / 2 distinct keys
+        const int32_t old = atomicCAS(&hkey[h], -1, key);
+        if (old == -1 || old == key) {
+            atomicAdd(&hcnt[h], add);
             if (old == -1) {
-                atomicAdd(&hcnt[h], add);
                 atomicAdd(&hist[(key >> 3) >> bb], 1u);
                 return (int32_t)h;
             }
-            k = old;
-        }
-        if (k == key) {
-            atomicAdd(&hcnt[h], add);
             return -1;
         }
-        h = (h + 1) & (kDSlots - 1);
+        h = (h + 1) & (SLOTS - 1);
     }
+}
+
+// A thread's KPER keys (node * 8 + bucket, -1 = none) into the LDS hash, one wave-
+// instruction per key slot: the lanes sharing the first active lane's key add once
+// (the Zipf-hot node), every other lane adds its own key.  The slots of new keys go to
+// the wave's own segment of uniq (KPER * 64 entries: no shared counter); returns how many
+// (uniform).  (More leader rounds for the next repeated keys measured slower at config 3.)
+template <int SLOTS, int KPER>
+__device__ __forceinline__ uint32_t wave_aggregate(const int32_t* key, int32_t* hkey, uint32_t* hcnt, uint32_t* hist,
+                                                   int bb, uint16_t* useg) {
+    const int lane = threadIdx.x & 63;
+    uint32_t nw = 0;
+#pragma unroll
+    for (int u = 0; u < KPER; ++u) {
+        const bool ok = key[u] >= 0;
+        const uint64_t am = __ballot(ok);
+        if (am == 0) continue;
+        const int lead = __ffsll((long long)am) - 1;
+        const int32_t kl = __builtin_amdgcn_readlane(key[u], lead);
+        const uint64_t m = __ballot(ok && key[u] == kl);
+        const bool mine = lane == lead || (ok && key[u] != kl);
+        const int32_t slot = mine ? hash_add<SLOTS>(hkey, hcnt, hist, bb, lane == lead ? kl : key[u],
+                                                    lane == lead ? (uint32_t)__popcll(m) : 1u)
+                                  : -1;
+        const uint64_t nm = __ballot(slot >= 0);
+        if (slot >= 0) useg[nw + __popcll(nm & ((1ull << lane) - 1ull))] = (uint16_t)slot;
+        nw += __popcll(nm);
+    }
+    return nw;
 }
 
 template <int BT>
@@ -230,7 +257,6 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     constexpr int kPer = kXChunk / BT;  // bindings per thread
     __shared__ uint32_t part[BT];
-    __shared__ uint32_t nuniq;
     int32_t* hkey = reinterpret_cast<int32_t*>(sh);
     uint32_t* hcnt = sh + kDSlots;
     uint32_t* hist = hcnt + kDSlots;
@@ -252,37 +278,17 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
         hcnt[i] = 0;
     }
     for (int i = threadIdx.x; i < g.nbins; i += BT) hist[i] = 0;
-    if (threadIdx.x == 0) nuniq = 0;
     __syncthreads();
     CRANE_TSTAMP(g.trace, blk, 1);
-    const int lane = threadIdx.x & 63;
+    int32_t key[kPer];
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
         const int j = window_rank(ts[u], cut);
         const bool ok = nd[u] >= 0 && (int64_t)nd[u] < N && j > 0;  // binding.go:85-91
-        const int32_t key = ok ? nd[u] * 8 + (j - 1) : -1;
-        // the lanes sharing the first active lane's key add once
-        const uint64_t am = __ballot(ok);
-        if (am == 0) continue;
-        const int lead = __ffsll((long long)am) - 1;
-        const int32_t kl = __shfl(key, lead);
-        const uint64_t m = __ballot(ok && key == kl);
-        // (kl, count) rides on the lead lane; every other lane adds its own key once
-        // (more leader rounds for the next repeated keys measured slower: 9.6 -> 10.0 us at config 3)
-        const bool mine = lane == lead || (ok && key != kl);
-        const int32_t slot =
-            mine ? hash_add(hkey, hcnt, hist, g.bb, lane == lead ? kl : key, lane == lead ? (uint32_t)__popcll(m) : 1u)
-                 : -1;
-        // new keys: one append per wave to the distinct-key list
-        const uint64_t nm = __ballot(slot >= 0);
-        if (nm) {
-            const int l0 = __ffsll((long long)nm) - 1;
-            uint32_t base = 0;
-            if (lane == l0) base = atomicAdd(&nuniq, (uint32_t)__popcll(nm));
-            base = __shfl(base, l0);
-            if (slot >= 0) uniq[base + __popcll(nm & ((1ull << lane) - 1ull))] = (uint16_t)slot;
-        }
+        key[u] = ok ? nd[u] * 8 + (j - 1) : -1;
     }
+    uint16_t* useg = uniq + (threadIdx.x >> 6) * (kPer * 64);
+    const uint32_t nw = wave_aggregate<kDSlots, kPer>(key, hkey, hcnt, hist, g.bb, useg);
     __syncthreads();
     CRANE_TSTAMP(g.trace, blk, 2);
     const int per = (g.nbins + BT - 1) / BT;
@@ -296,17 +302,16 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
         run += c;
     }
     __syncthreads();
-    // this region's (count | offset << 16) per bin, column blk of CO [nbins][nblk]: the readers
-    // (K1 per node block, Y per coarse bin) read their bin's row contiguously; the regions of
-    // one XCD are consecutive (xcd_block), so a CO line is written whole in one L2
-    for (int i = threadIdx.x; i < g.nbins; i += BT) CO[(int64_t)i * g.nblk + blk] = hist[i] | (off[i] << 16);
+    // this region's row of (count | offset << 16) per node block: coalesced (CO [nblk][nbins];
+    // the column-major layout, contiguous for the readers, made this launch 10 % slower at
+    // config 3 and cost K1 as much as it saved)
+    for (int i = threadIdx.x; i < g.nbins; i += BT) CO[(int64_t)blk * g.nbins + i] = hist[i] | (off[i] << 16);
     __syncthreads();
     CRANE_TSTAMP(g.trace, blk, 3);
     uint32_t* reg = region + (int64_t)blk * kXChunk;
     const uint32_t mask = (1u << g.bb) - 1;
-    const uint32_t nu = nuniq;
-    for (uint32_t i = threadIdx.x; i < nu; i += BT) {
-        const int s = uniq[i];
+    for (uint32_t i = threadIdx.x & 63; i < nw; i += 64) {  // this wave's new keys
+        const int s = useg[i];
         const int32_t k = hkey[s];
         const uint32_t p = atomicAdd(&off[(k >> 3) >> g.bb], 1u);
         reg[p] = ((uint32_t)(k >> 3) & mask) | ((uint32_t)(k & 7) << 16) | (hcnt[s] << 19);
@@ -323,7 +328,7 @@ template <int BT>
 __global__ __launch_bounds__(BT) void k2x_dedupe(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
                                                  int64_t B, int64_t N, HotCutoffs cut, HotPart g,
                                                  uint32_t* __restrict__ CO, uint32_t* __restrict__ region) {
-    k2d_body<BT>((int32_t)xcd_block(blockIdx.x, gridDim.x), bnode, bts, B, N, cut, g, CO, region);
+    k2d_body<BT>((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
 }
 
 template <int BT>
@@ -333,12 +338,11 @@ __global__ __launch_bounds__(BT) void k2x_dedupe_pods(const int32_t* __restrict_
                                                       uint32_t* __restrict__ region, PodPrep pp) {
     // the pod tiles first: dispatched first, their sort overlaps the regions' aggregation
     // instead of trailing the launch
-    const int64_t m = xcd_block(blockIdx.x, gridDim.x);  // (pod tiles: blocks 0, 8, 16, ...)
-    if (m >= pp.ntiles) {
-        k2d_body<BT>((int32_t)(m - pp.ntiles), bnode, bts, B, N, cut, g, CO, region);
+    if ((int64_t)blockIdx.x >= pp.ntiles) {
+        k2d_body<BT>((int32_t)(blockIdx.x - pp.ntiles), bnode, bts, B, N, cut, g, CO, region);
     } else {
         extern __shared__ __attribute__((aligned(16))) unsigned char k3p_lds[];
-        k3p_tile<BT>(m, pp, k3p_lds);
+        k3p_tile<BT>((int64_t)blockIdx.x, pp, k3p_lds);
     }
 }
 
@@ -349,6 +353,7 @@ HotPart hot_dedupe_geometry(int64_t B, int64_t N, int32_t W, int32_t bs) {
     g.bb = bb;
     g.nbins = (int32_t)((N + bs - 1) / bs);
     g.nblk = (int32_t)((B + kXChunk - 1) / kXChunk);
+    g.reg = kXChunk;
     g.cap = (int64_t)g.nblk * kXChunk;
     // key nd*8+bucket in int32; hash + bin LDS <= 96 KiB; count/offset matrices <= 2^22 entries
     g.ok = N > 0 && B > 0 && (1 << bb) == bs && bb <= 16 && W >= 1 && W <= kMaxWin && N < (1LL << 27) &&
@@ -394,24 +399,116 @@ size_t hot_dedupe_scratch(const HotPart& g) { return (size_t)g.cap + (size_t)g.n
 
 // ---------------------------------------------------------------- large form
 // When the dedupe form's count/offset matrix (K1 blocks x regions) would pass its cap
-// (e.g. 4M nodes x 16M bindings: 15,625 x 7,813 words), the same region pass runs with
-// COARSE bins of 2^bb nodes (16K at two windows: 245 bins at 4M nodes), and a second
-// kernel turns each coarse bin into dense window-rank buckets:
-//   X  k2x_dedupe (above) with the coarse geometry: one pass over the log, entries
-//      aggregated per (region, node, bucket) — a Zipf-hot node costs one entry per region;
+// (e.g. 4M nodes x 16M bindings: 15,625 x 7,813 words), the log goes through two kernels:
+//   X  k2l_partition: the dedupe form's region pass (per region of REG bindings: LDS hash
+//      aggregation per (node, bucket) — a Zipf-hot node costs one entry per region — then
+//      the distinct entries binned) with COARSE bins of 2^bb nodes (16K at two windows:
+//      245 bins at 4M nodes); persistent: each workgroup walks regions blockIdx, + grid, ...
+//      and loads the next region's bindings while it aggregates the current one, and
+//      clears only the hash slots it used;
 //   Y  k2y_bin_hist: one workgroup per coarse bin gathers the bin's entries from every
-//      region (count/offset column, then the runs) into an LDS histogram [W][2^bb] and
+//      region (the count/offset words, then the runs) into an LDS histogram [W][2^bb] and
 //      writes the bin's rows of buckets [W][N] whole — no global atomics, nothing to zero
 //      (K1 reads them and leaves them, K1Args::buckets_keep).
-// Consecutive bins run on one XCD (xcd_block), so the count/offset lines and region runs
-// that neighbouring bins share are fetched into that XCD's L2 once.
+// Count/offset words: CO [nblk][nbins] (g.co_t = 0: X writes its row coalesced, Y reads a
+// column) or [nbins][nblk] (co_t = 1: Y reads its row coalesced, X writes a column).
+template <int BT, int REG>
+__global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(BT == 1024 ? 8 : 1)))
+void k2l_partition(const int32_t* __restrict__ bnode,
+                                                    const int64_t* __restrict__ bts, int64_t B, int64_t N,
+                                                    HotCutoffs cut, HotPart g, uint32_t* __restrict__ CO,
+                                                    uint32_t* __restrict__ region) {
+    constexpr int kPer = REG / BT;   // bindings per thread per region
+    constexpr int kSlots = 2 * REG;  // an empty or matching slot always exists
+    // hkey, hcnt [kSlots], hist, off [nbins], uniq u16 [REG]
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+    __shared__ uint32_t part[BT];
+    int32_t* hkey = reinterpret_cast<int32_t*>(sh);
+    uint32_t* hcnt = sh + kSlots;
+    uint32_t* hist = hcnt + kSlots;
+    uint32_t* off = hist + g.nbins;
+    uint16_t* useg = reinterpret_cast<uint16_t*>(off + g.nbins) + (threadIdx.x >> 6) * (kPer * 64);
+    for (int i = threadIdx.x; i < kSlots; i += BT) {
+        hkey[i] = -1;
+        hcnt[i] = 0;
+    }
+    for (int i = threadIdx.x; i < g.nbins; i += BT) hist[i] = 0;
+    auto load = [&](int64_t r, int32_t* nd, int64_t* ts) {  // unconditional loads, clamped index
+        const int64_t b0 = r * REG + threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int64_t b = b0 + u * BT, bc = min(b, B - 1);
+            nd[u] = bnode[bc];
+            ts[u] = bts[bc];
+            if (b >= B) nd[u] = -1;
+        }
+    };
+    int32_t nd[kPer];
+    int64_t ts[kPer];
+    int64_t r = blockIdx.x;  // (grid <= nblk)
+    load(r, nd, ts);
+    __syncthreads();
+    const uint32_t mask = (1u << g.bb) - 1;
+    const int per = (g.nbins + BT - 1) / BT;
+    const int lo = min(g.nbins, (int)threadIdx.x * per), hi = min(g.nbins, lo + per);
+    for (;;) {
+        const int64_t r2 = r + gridDim.x;
+        int32_t nd2[kPer];
+        int64_t ts2[kPer];
+        load(min(r2, (int64_t)g.nblk - 1), nd2, ts2);  // the next region, in flight meanwhile
+        CRANE_TSTAMP(g.trace, r, 0);
+        int32_t key[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int j = window_rank(ts[u], cut);
+            const bool ok = nd[u] >= 0 && (int64_t)nd[u] < N && j > 0;  // binding.go:85-91
+            key[u] = ok ? nd[u] * 8 + (j - 1) : -1;
+        }
+        const uint32_t nw = wave_aggregate<kSlots, kPer>(key, hkey, hcnt, hist, g.bb, useg);
+        __syncthreads();
+        CRANE_TSTAMP(g.trace, r, 1);
+        uint32_t sum = 0;
+        for (int i = lo; i < hi; ++i) sum += hist[i];
+        uint32_t run = wg_excl_scan_u32<BT>(sum, part);
+        for (int i = lo; i < hi; ++i) {  // offsets + this region's count/offset words; hist cleared
+            const uint32_t c = hist[i];
+            off[i] = run;
+            CO[g.co_t ? (int64_t)i * g.nblk + r : r * g.nbins + i] = c | (run << 16);
+            hist[i] = 0;
+            run += c;
+        }
+        __syncthreads();
+        CRANE_TSTAMP(g.trace, r, 2);
+        uint32_t* reg = region + r * REG;
+        for (uint32_t i = threadIdx.x & 63; i < nw; i += 64) {  // this wave's entries; its slots cleared
+            const int s = useg[i];
+            const int32_t k = hkey[s];
+            const uint32_t cnt = hcnt[s];
+            hkey[s] = -1;
+            hcnt[s] = 0;
+            const uint32_t p = atomicAdd(&off[(k >> 3) >> g.bb], 1u);
+            reg[p] = ((uint32_t)(k >> 3) & mask) | ((uint32_t)(k & 7) << 16) | (cnt << 19);
+        }
+        __syncthreads();
+        CRANE_TSTAMP(g.trace, r, 3);
+        r = r2;
+        if (r >= g.nblk) break;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            nd[u] = nd2[u];
+            ts[u] = ts2[u];
+        }
+    }
+}
+
 constexpr int kYThreads = 1024;
-constexpr int kYPer = 8;     // regions per lane per round (16M bindings: 7,813 regions, one round)
-constexpr int kYFirst = 4;   // entries per run loaded with the count/offset words' round
+// YPER regions per lane per round (4,096-binding regions at 16M bindings: 3,907, one round of
+// 4), YFIRST entries of each run loaded in the count/offset words' round, the rest queued
 constexpr int kYQ = 2048;    // LDS queue of the longer runs' tails
 
 // Every load is unconditional (clamped index, result masked): conditional loads made the
 // compiler wait for each one before issuing the next.
+template <int kYPer, int kYFirst>
 __global__ __launch_bounds__(kYThreads) void k2y_bin_hist(const uint32_t* __restrict__ region,
                                                           const uint32_t* __restrict__ CO, HotPart g, int32_t W,
                                                           int64_t N, uint32_t* __restrict__ buckets) {
@@ -422,13 +519,15 @@ __global__ __launch_bounds__(kYThreads) void k2y_bin_hist(const uint32_t* __rest
     const int64_t bin = xcd_block(blockIdx.x, gridDim.x);
     const uint32_t lmask = (uint32_t)binw - 1;
     auto add = [&](uint32_t v) { atomicAdd(&hist[((v >> 16) & 7) * binw + (v & lmask)], v >> 19); };
+    CRANE_TSTAMP(g.trace, bin, 4);  // (trace row = bin; the partition's rows use slots 0-3)
     for (int i0 = 0; i0 < g.nblk; i0 += kYThreads * kYPer) {
         // this bin's (count, offset) word of kYPer regions per lane, then their runs' first entries
         uint32_t c[kYPer], o[kYPer];
 #pragma unroll
         for (int u = 0; u < kYPer; ++u) {
             const int i = i0 + u * kYThreads + threadIdx.x;
-            const uint32_t co = CO[bin * g.nblk + min(i, g.nblk - 1)];  // the bin's row: coalesced
+            const int ic = min(i, g.nblk - 1);
+            const uint32_t co = CO[g.co_t ? bin * g.nblk + ic : (int64_t)ic * g.nbins + bin];
             c[u] = i < g.nblk ? co & 0xFFFF : 0u;
             o[u] = co >> 16;
         }
@@ -437,7 +536,7 @@ __global__ __launch_bounds__(kYThreads) void k2y_bin_hist(const uint32_t* __rest
         uint32_t v[kYPer][kYFirst];
 #pragma unroll
         for (int u = 0; u < kYPer; ++u) {
-            const int64_t e0 = (int64_t)(i0 + u * kYThreads + threadIdx.x) * kHxRegion + o[u];
+            const int64_t e0 = (int64_t)(i0 + u * kYThreads + threadIdx.x) * g.reg + o[u];
 #pragma unroll
             for (int k = 0; k < kYFirst; ++k) v[u][k] = region[(uint32_t)k < c[u] ? e0 + k : 0];
         }
@@ -454,7 +553,7 @@ __global__ __launch_bounds__(kYThreads) void k2y_bin_hist(const uint32_t* __rest
             for (int k = 0; k < kYFirst; ++k)
                 if ((uint32_t)k < c[u]) add(v[u][k]);
             if (c[u] > (uint32_t)kYFirst) {  // the rest of a longer run: queued for the whole workgroup
-                const uint32_t e0 = (uint32_t)(i0 + u * kYThreads + threadIdx.x) * kHxRegion + o[u] + kYFirst;
+                const uint32_t e0 = (uint32_t)(i0 + u * kYThreads + threadIdx.x) * (uint32_t)g.reg + o[u] + kYFirst;
                 const uint32_t p = atomicAdd(&qn, 1u);
                 if (p < (uint32_t)kYQ) {
                     q[p] = make_uint2(e0, c[u] - kYFirst);
@@ -478,39 +577,74 @@ __global__ __launch_bounds__(kYThreads) void k2y_bin_hist(const uint32_t* __rest
         }
         __syncthreads();  // (qn / q reused by the next round; hist complete after the last)
     }
+    CRANE_TSTAMP(g.trace, bin, 5);
     // the bin's rows, whole: lane i -> node n0 + i
     const int64_t n0 = bin << bb;
     const int nn = (int)min((int64_t)binw, N - n0);
     for (int w = 0; w < W; ++w)
         for (int i = threadIdx.x; i < nn; i += kYThreads) buckets[(int64_t)w * N + n0 + i] = hist[w * binw + i];
+    CRANE_TSTAMP(g.trace, bin, 6);
 }
 
-HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W) {
+HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W, int32_t reg, int32_t co_t) {
     HotPart g{};
     int bb = 16;  // entry format: local node in 16 bits
     while (bb > 8 && (int64_t)std::max(W, 1) * (4LL << bb) > kK2LargeHistBytes) --bb;  // Y's LDS histogram
     g.bb = bb;
+    g.reg = reg == 2048 ? 2048 : 4096;
+    g.co_t = co_t ? 1 : 0;
     g.nbins = (int32_t)((N + (1LL << bb) - 1) >> bb);
-    g.nblk = (int32_t)((B + kXChunk - 1) / kXChunk);
-    g.cap = (int64_t)g.nblk * kXChunk;
+    g.nblk = (int32_t)((B + g.reg - 1) / g.reg);
+    g.cap = (int64_t)g.nblk * g.reg;
+    // (count <= reg < 2^13 in an entry's top bits and in a count/offset half-word)
     g.ok = N > 0 && B > 0 && W >= 1 && W <= kMaxWin && N < (1LL << 27) && B < (1LL << 31) && g.nbins <= 4096 &&
            (double)g.nbins * (double)g.nblk <= (double)(1LL << 27);
     return g;
 }
 
+template <int BT, int REG>
+static hipError_t launch_large_x(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
+                                 const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, int n_cu,
+                                 hipStream_t st) {
+    const size_t lds = sizeof(uint32_t) * (4 * (size_t)REG + 2 * (size_t)g.nbins) + sizeof(uint16_t) * REG;
+    static const hipError_t attr =
+        hipFuncSetAttribute((const void*)k2l_partition<BT, REG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            100 * 1024);
+    if (attr != hipSuccess) return attr;
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k2l_partition<BT, REG>, BT,
+                                                               lds);
+    if (e != hipSuccess) return e;
+    const int64_t grid = std::min<int64_t>(g.nblk, (int64_t)std::max(1, per_cu) * std::max(1, n_cu));
+    return klaunch("k2l_partition", k2l_partition<BT, REG>, dim3((unsigned)grid), dim3(BT), lds, st, bnode, bts, B,
+                   N, cut, g, scratch + g.cap, scratch);
+}
+
 hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, uint32_t* buckets,
-                                  hipStream_t st, int threads) {
+                                  int n_cu, hipStream_t st, int threads) {
     // (dynamic + the static tail queue stay within the CU's 160 KiB)
-    static const hipError_t attr = hipFuncSetAttribute((const void*)k2y_bin_hist,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)kK2LargeHistBytes);
+    static const hipError_t attr = [] {
+        hipError_t e = hipFuncSetAttribute((const void*)k2y_bin_hist<4, 8>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kK2LargeHistBytes);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)k2y_bin_hist<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kK2LargeHistBytes);
+        return e;
+    }();
     if (attr != hipSuccess) return attr;
-    hipError_t e = launch_hot_count_dedupe(bnode, bts, B, N, cut, g, scratch, st, nullptr, threads);
+    hipError_t e;
+    if (g.reg == 2048) e = launch_large_x<512, 2048>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
+    else if (threads == 1024) e = launch_large_x<1024, 4096>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
+    else e = launch_large_x<512, 4096>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
     if (e != hipSuccess) return e;
     const size_t lds = sizeof(uint32_t) * (size_t)cut.n_win * ((size_t)1 << g.bb);
-    return klaunch("k2y_bin_hist", k2y_bin_hist, dim3((unsigned)g.nbins), dim3(kYThreads), lds, st,
-                   (const uint32_t*)scratch, (const uint32_t*)(scratch + g.cap), g, cut.n_win, N, buckets);
+    const uint32_t* co = scratch + g.cap;
+    if (g.nblk <= 4 * kYThreads)
+        return klaunch("k2y_bin_hist", k2y_bin_hist<4, 8>, dim3((unsigned)g.nbins), dim3(kYThreads), lds, st,
+                       (const uint32_t*)scratch, co, g, cut.n_win, N, buckets);
+    return klaunch("k2y_bin_hist", k2y_bin_hist<8, 4>, dim3((unsigned)g.nbins), dim3(kYThreads), lds, st,
+                   (const uint32_t*)scratch, co, g, cut.n_win, N, buckets);
 }
 
 HotBins hot_bins_geometry(int64_t B, int64_t N, int32_t W) {

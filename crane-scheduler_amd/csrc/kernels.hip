@@ -181,10 +181,9 @@ void k1_node_pass(K1Args a, K1Step step) {
     // below behind the whole SoA stream.
     const int lo = (int)min((int64_t)threadIdx.x, N - 1 - first);  // lane offset, clamped
     if (hx) {
-        const uint32_t* __restrict__ corow = a.hx_CO + blk * (int64_t)a.hx_nblk;  // this block's row
 #pragma unroll
         for (int u = 0; u < kHxPer; ++u)  // (masked where used: a use here would wait for them)
-            co0[u] = corow[min(u * kK1Threads + (int)threadIdx.x, a.hx_nblk - 1)];
+            co0[u] = a.hx_CO[(int64_t)min(u * kK1Threads + (int)threadIdx.x, a.hx_nblk - 1) * gridDim.x + blk];
         for (int b = 0; b < kMaxWin; ++b) hxh[b][threadIdx.x] = 0;
     }
 #pragma unroll
@@ -234,7 +233,7 @@ void k1_node_pass(K1Args a, K1Step step) {
 #pragma unroll
             for (int u = 0; u < kHxPer; ++u) {
                 const int i = i0 + u * kK1Threads + threadIdx.x;
-                const uint32_t co = i0 == 0 ? co0[u] : a.hx_CO[blk * (int64_t)a.hx_nblk + min(i, a.hx_nblk - 1)];
+                const uint32_t co = i0 == 0 ? co0[u] : a.hx_CO[(int64_t)min(i, a.hx_nblk - 1) * gridDim.x + blk];
                 c[u] = i < a.hx_nblk ? co & 0xFFFF : 0u;
                 o[u] = co >> 16;
             }

@@ -160,8 +160,10 @@ hipError_t launch_hot_count(const int32_t* bnode, const int64_t* bts, int64_t B,
 // (bs nodes), consumed by K1 through K1Args::hx_*.  Region stride kHxRegion entries.
 struct HotPart {
     int32_t bb, nbins;  // 2^bb nodes per bin
-    int64_t cap;        // region entries (nblk * 2048)
-    int32_t nblk;       // partition workgroups
+    int64_t cap;        // region entries (nblk * reg)
+    int32_t nblk;       // regions
+    int32_t reg;        // bindings per region (the dedupe form: kHxRegion)
+    int32_t co_t;       // count/offset words [nbins][nblk] (large form option), else [nblk][nbins]
     bool ok;
     unsigned long long* trace;  // phase trace or null
 };
@@ -190,10 +192,10 @@ hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int
 // dense window-rank buckets [W][N] (every row of every bin: K1 reads them, nothing to zero).
 // scratch: hot_dedupe_scratch(g) words.
 constexpr int64_t kK2LargeHistBytes = 128 * 1024;
-HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W);
+HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W, int32_t reg, int32_t co_t);
 hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, uint32_t* buckets,
-                                  hipStream_t st, int threads);
+                                  int n_cu, hipStream_t st, int threads = 512);
 
 // ---------------------------------------------------------------- K3 step path (step.hip)
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)

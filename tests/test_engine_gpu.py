@@ -163,7 +163,7 @@ def test_hot_values_random(n_nodes, n_bind, seed, k2):
 
 
 @pytest.mark.parametrize("threads,k2x,k2", [(128, 512, 0), (256, 512, 0), (256, 1024, 0), (256, 256, 0),
-                                            (256, 512, 3), (256, 1024, 3)])
+                                            (256, 4096, 3), (256, 2048, 3), (256, -4096, 3)])
 @pytest.mark.parametrize("case", ["one_hot_node", "eight_windows", "last_node", "odd_counts"])
 def test_hot_values_dedupe_edges(case, threads, k2x, k2):
     """Dedupe-form K2 (per-workgroup (node, bucket) aggregation, counts read by the
@@ -188,7 +188,10 @@ def test_hot_values_dedupe_edges(case, threads, k2x, k2):
         bn[::3] = n_nodes - 1
         bn[1::7] = n_nodes  # past the shard: ignored
         bn[2::11] = -3
-    eng = engine_for(spec, c, opts={"k2_form": k2, "k1_threads": threads, "k2x_threads": k2x})
+    # (k2 = 3: the large form; k2x = its region size, negative = count/offset words [bin][region])
+    opts = {"k2_form": k2, "k1_threads": threads}
+    opts.update({"k2l_region": abs(k2x), "k2l_co_t": int(k2x < 0)} if k2 == 3 else {"k2x_threads": k2x})
+    eng = engine_for(spec, c, opts=opts)
     eng.upload_bindings(bn, c.b_ts)
     now = int(c.now[0])
     for rep in range(2):  # a second refresh after the first was consumed
@@ -221,7 +224,7 @@ def test_hot_values_large_form_16m():
     ref = cnt_hv.astype(np.float64)
     eng.set_profiling(True)
     eng.refresh_hot_values(now, now)
-    assert [n for n, _ in eng.stage_times()] == ["k2x_dedupe", "k2y_bin_hist"]
+    assert [n for n, _ in eng.stage_times()] == ["k2l_partition", "k2y_bin_hist"]
     eng.set_profiling(False)
     assert np.array_equal(eng.hot_values(), ref)
     _, _, ch, _ = eng.eval(c.now, c.ds)

@@ -6,6 +6,7 @@
 #   profiles/pmc/config2_<hash>.json   per-pair matrix leg, config 2
 #   profiles/pmc/config3m_<hash>.json  per-pair matrix leg at config 3 size
 #   profiles/pmc/config4m_<hash>.json  cold-cache 4M-node pass (tools/stream_bench.py)
+#   profiles/pmc/configcold_<hash>.json  bench.py's cold-cache K1/K2 leg (roofline_cold)
 # Stops on any fault/timeout exit code.  Usage: bash tools/gpu_pmc.sh <tag> [workloads]
 cd "$GRAFT_REPO_ROOT"
 TAG=${1:-pmc}
@@ -18,9 +19,10 @@ for w in $WL; do
         2) CMD="python3 $GRAFT_REPO_ROOT/bench.py --leg matrix2 --steps 5";;
         3m) CMD="python3 $GRAFT_REPO_ROOT/bench.py --leg matrix3 --steps 3";;
         4m) CMD="python3 $GRAFT_REPO_ROOT/tools/stream_bench.py --k2 auto --reps 2";;
+        cold) CMD="python3 $GRAFT_REPO_ROOT/bench.py --leg cold --steps 2";;
         *) CMD="python3 $GRAFT_REPO_ROOT/bench.py --config $w --steps 5 --warmup 1 --inflight 1 --no-cpu-baseline --no-greedy --no-extras";;
     esac
-    for pass in "fetch FETCH_SIZE" "write WRITE_SIZE" "valu SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY" "l2 TCC_HIT_sum TCC_MISS_sum"; do
+    for pass in "fetch FETCH_SIZE" "write WRITE_SIZE" "valu SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY" "l2 TCC_HIT_sum TCC_MISS_sum" "lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
         set -- $pass
         name=$1; shift
         timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d $OUT -o $name -- $CMD > $OUT/$name.log 2>&1
