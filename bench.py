@@ -159,13 +159,16 @@ def parse():
 
 
 # ------------------------------------------------------------------ legs
-def select_leg(cd, spec, dev, stream, val, ts, hv, hv_ts, now, ds, reps=3):
+def select_leg(cd, spec, dev, stream, val, ts, hv, hv_ts, now, ds, reps=3, opts=()):
     """Framework-level selection for the config-3 queue with the shipped profile (SURVEY §8f
     row 4): Dynamic weight 3 + synthetic other plugins (95 % pass their filters, weighted
     sum in [0, 700]), percentageOfNodesToScore default (adaptive: 5 % of 100k = 5000
     feasible nodes per pod from a rotating start) and every node scored (100)."""
     N, P = val.shape[1], len(now)
     eng = cd.Engine(cd.Policy(spec), dev.index)
+    for o in opts:
+        k, v = o.split("=")
+        eng.set_option(k, int(v))
     eng.upload_nodes(val, ts, hv, hv_ts)
     rng = np.random.default_rng(77)
     d_now = torch.from_numpy(now).to(dev)

@@ -112,6 +112,7 @@ struct Options {
     int k2l_region = 4096;    // large K2: bindings per region (2048 or 4096)
     int k2l_co_t = 0;         // large K2: count/offset words [bin][region] (1) or [region][bin] (0)
     int k2l_threads = 512;    // large K2: partition workgroup size at 4096-binding regions (512 or 1024)
+    int sel_chain = 0;        // selection windows: 0 LDS rank/select walk when it fits, 1 streaming kernel
     int step_lds_cap = 1 << 30;  // K1: one-step records per kind staged in LDS at most (0: always st.stage)
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
 };
@@ -730,6 +731,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "k2l_region" && (value == 2048 || value == 4096)) o.k2l_region = (int)value;
     else if (n == "k2l_co_t" && range(0, 1)) o.k2l_co_t = (int)value;
     else if (n == "k2l_threads" && (value == 512 || value == 1024)) o.k2l_threads = (int)value;
+    else if (n == "sel_chain" && range(0, 1)) o.sel_chain = (int)value;
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
@@ -1005,7 +1007,7 @@ int crane_dyn_select(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_
     a.seed = tie_seed;
     a.kb = (uint32_t)(tie_seed * 0x9E3779B97F4A7C15ull >> 32);
     HIPTRY(h, h->sel_keys.reserve((size_t)P));
-    HIPTRY(h, h->sel_state.reserve(1));
+    HIPTRY(h, h->sel_state.reserve(2));  // next start, chain-form flag
     a.keys = h->sel_keys.p;
     int64_t* ws = d_wstart;
     int64_t* wl = d_wlen;
@@ -1017,7 +1019,8 @@ int crane_dyn_select(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_
             if (!wl) wl = h->sel_win.p + P;
         }
         HIPTRY(h, launch_select_fth(a, h->shape, h->sel_fth.p, st));
-        HIPTRY(h, launch_select_chain(a, h->sel_fth.p, K, start, ws, wl, h->sel_state.p, st));
+        HIPTRY(h, launch_select_chain(a, h->sel_fth.p, K, start, ws, wl, h->sel_state.p,
+                                      reinterpret_cast<int32_t*>(h->sel_state.p + 1), h->opt.sel_chain, st));
         a.wstart = ws;
         a.wlen = wl;
     }

@@ -167,25 +167,6 @@ __global__ __launch_bounds__(kHT) void k2d_bin_hist(const uint32_t* __restrict__
 
 constexpr int kXChunk = kHxRegion;  // bindings per dedupe-form workgroup (K1 reads the regions with this stride)
 
-// exclusive workgroup scan (BT threads): wave scans + a scan of the wave totals
-template <int BT = kHT>
-__device__ __forceinline__ uint32_t wg_excl_scan_u32(uint32_t v, uint32_t* part) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) part[w] = x;
-    __syncthreads();
-    uint32_t pre = 0;
-#pragma unroll
-    for (int i = 0; i < BT / 64; ++i) pre += i < w ? part[i] : 0u;
-    __syncthreads();
-    return pre + x - v;
-}
-
 // ---------------------------------------------------------------- dedupe form
 // X' partition_dedupe : as X, but each workgroup first aggregates its 2048
 //                bindings per (node, bucket) in an LDS hash table and writes one
@@ -503,7 +484,8 @@ void k2l_partition(const int32_t* __restrict__ bnode,
 
 constexpr int kYThreads = 1024;
 // YPER regions per lane per round (4,096-binding regions at 16M bindings: 3,907, one round of
-// 4), YFIRST entries of each run loaded in the count/offset words' round, the rest queued
+// 4), YFIRST aligned 16-byte blocks of each run loaded in the count/offset words' round, the
+// rest queued
 constexpr int kYQ = 2048;    // LDS queue of the longer runs' tails
 
 // Every load is unconditional (clamped index, result masked): conditional loads made the
@@ -531,14 +513,20 @@ __global__ __launch_bounds__(kYThreads) void k2y_bin_hist(const uint32_t* __rest
             c[u] = i < g.nblk ? co & 0xFFFF : 0u;
             o[u] = co >> 16;
         }
-        // lanes past a run's end all load entry 0 (one shared line), so a load instruction
-        // costs the lines of the runs it reads
-        uint32_t v[kYPer][kYFirst];
+        // each run as aligned 16-byte blocks: a run of up to 4 * YFIRST - 3 entries costs its
+        // one or two lines in YFIRST load instructions (per-entry loads cost a line per
+        // instruction: the gather was bound by the lines the loads touch); blocks past a
+        // run's end load block 0 (one line shared by the wave)
+        const uint4* __restrict__ region4 = reinterpret_cast<const uint4*>(region);
+        uint4 v[kYPer][kYFirst];
+        uint32_t a0[kYPer];
 #pragma unroll
         for (int u = 0; u < kYPer; ++u) {
-            const int64_t e0 = (int64_t)(i0 + u * kYThreads + threadIdx.x) * g.reg + o[u];
+            const uint32_t e0 = (uint32_t)(i0 + u * kYThreads + threadIdx.x) * (uint32_t)g.reg + o[u];
+            a0[u] = e0 & ~3u;
+            const uint32_t nb = c[u] ? ((e0 & 3u) + c[u] + 3u) >> 2 : 0u;
 #pragma unroll
-            for (int k = 0; k < kYFirst; ++k) v[u][k] = region[(uint32_t)k < c[u] ? e0 + k : 0];
+            for (int k = 0; k < kYFirst; ++k) v[u][k] = region4[(uint32_t)k < nb ? (a0[u] >> 2) + k : 0u];
         }
         if (i0 == 0) {
             uint4* h4 = reinterpret_cast<uint4*>(hist);
@@ -549,16 +537,22 @@ __global__ __launch_bounds__(kYThreads) void k2y_bin_hist(const uint32_t* __rest
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kYPer; ++u) {
+            const uint32_t e0 = a0[u] + (o[u] & 3u), e1 = e0 + c[u];  // the run: [e0, e1)
 #pragma unroll
-            for (int k = 0; k < kYFirst; ++k)
-                if ((uint32_t)k < c[u]) add(v[u][k]);
-            if (c[u] > (uint32_t)kYFirst) {  // the rest of a longer run: queued for the whole workgroup
-                const uint32_t e0 = (uint32_t)(i0 + u * kYThreads + threadIdx.x) * (uint32_t)g.reg + o[u] + kYFirst;
+            for (int k = 0; k < kYFirst; ++k) {
+                const uint32_t b = a0[u] + 4u * k;
+                if (b + 0 >= e0 && b + 0 < e1) add(v[u][k].x);
+                if (b + 1 >= e0 && b + 1 < e1) add(v[u][k].y);
+                if (b + 2 >= e0 && b + 2 < e1) add(v[u][k].z);
+                if (b + 3 >= e0 && b + 3 < e1) add(v[u][k].w);
+            }
+            const uint32_t done = a0[u] + 4u * kYFirst;
+            if (e1 > done) {  // the rest of a longer run: queued for the whole workgroup
                 const uint32_t p = atomicAdd(&qn, 1u);
                 if (p < (uint32_t)kYQ) {
-                    q[p] = make_uint2(e0, c[u] - kYFirst);
+                    q[p] = make_uint2(done, e1 - done);
                 } else {  // queue full: this lane walks it
-                    for (uint32_t k = 0; k < c[u] - kYFirst; ++k) add(region[e0 + k]);
+                    for (uint32_t e = done; e < e1; ++e) add(region[e]);
                 }
             }
         }
@@ -625,10 +619,10 @@ hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int6
                                   int n_cu, hipStream_t st, int threads) {
     // (dynamic + the static tail queue stay within the CU's 160 KiB)
     static const hipError_t attr = [] {
-        hipError_t e = hipFuncSetAttribute((const void*)k2y_bin_hist<4, 8>,
+        hipError_t e = hipFuncSetAttribute((const void*)k2y_bin_hist<4, 3>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kK2LargeHistBytes);
         if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k2y_bin_hist<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+            e = hipFuncSetAttribute((const void*)k2y_bin_hist<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kK2LargeHistBytes);
         return e;
     }();
@@ -641,9 +635,9 @@ hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int6
     const size_t lds = sizeof(uint32_t) * (size_t)cut.n_win * ((size_t)1 << g.bb);
     const uint32_t* co = scratch + g.cap;
     if (g.nblk <= 4 * kYThreads)
-        return klaunch("k2y_bin_hist", k2y_bin_hist<4, 8>, dim3((unsigned)g.nbins), dim3(kYThreads), lds, st,
+        return klaunch("k2y_bin_hist", k2y_bin_hist<4, 3>, dim3((unsigned)g.nbins), dim3(kYThreads), lds, st,
                        (const uint32_t*)scratch, co, g, cut.n_win, N, buckets);
-    return klaunch("k2y_bin_hist", k2y_bin_hist<8, 4>, dim3((unsigned)g.nbins), dim3(kYThreads), lds, st,
+    return klaunch("k2y_bin_hist", k2y_bin_hist<8, 2>, dim3((unsigned)g.nbins), dim3(kYThreads), lds, st,
                    (const uint32_t*)scratch, co, g, cut.n_win, N, buckets);
 }
 

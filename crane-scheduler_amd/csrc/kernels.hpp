@@ -95,8 +95,10 @@ struct SelArgs {
     long long* keys;           // [P]: (total << 32) | tie, -1 = no feasible node (initialised to -1)
 };
 hipError_t launch_select_fth(const SelArgs& a, int shape, int64_t* fth, hipStream_t st);
+// form: 0 the LDS rank/select walk when it fits (else / on overflow the streaming kernel), 1 streaming only;
+// done: device flag the two forms share
 hipError_t launch_select_chain(const SelArgs& a, const int64_t* fth, int64_t K, int64_t start, int64_t* wstart,
-                               int64_t* wlen, int64_t* next_start, hipStream_t st);
+                               int64_t* wlen, int64_t* next_start, int32_t* done, int form, hipStream_t st);
 hipError_t launch_select_pairs(int shape, const SelArgs& a, hipStream_t st);
 hipError_t launch_select_decode(const SelArgs& a, int64_t* chosen, int64_t* total, hipStream_t st);
 

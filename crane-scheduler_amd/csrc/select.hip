@@ -126,7 +126,9 @@ constexpr int kChPB = 1024;               // pod times cached per block
 
 __global__ __launch_bounds__(kChT) void k_sel_chain(SelArgs a, const int64_t* __restrict__ fth, int64_t K,
                                                     int64_t start, int64_t* __restrict__ wstart,
-                                                    int64_t* __restrict__ wlen, int64_t* __restrict__ next_start) {
+                                                    int64_t* __restrict__ wlen, int64_t* __restrict__ next_start,
+                                                    const int32_t* __restrict__ skip) {
+    if (skip && *skip) return;  // k_sel_chain_rs placed the windows
     __shared__ unsigned long long msk[kChQ][kChC];
     __shared__ int64_t ptime[kChPB];
     __shared__ int8_t pds[kChPB];
@@ -254,6 +256,247 @@ __global__ __launch_bounds__(kChT) void k_sel_chain(SelArgs a, const int64_t* __
     if (threadIdx.x == 0) {
         int64_t s0 = start + pstart % N;
         *next_start = s0 >= N ? s0 - N : s0;
+    }
+}
+
+// ---------------------------------------------------------------- k_sel_chain_rs
+// The same windows without streaming the rotation: for the pods of the queue (times in
+// [tmin, tmax] for the non-DaemonSet ones) a node is
+//   A  feasible for every non-DaemonSet pod      (fth <= tmin),
+//   I  feasible from some time inside the queue  (tmin < fth <= tmax),
+//   -  feasible for no non-DaemonSet pod         (fth > tmax),
+//   D  feasible for a DaemonSet pod              (fth != INT64_MAX).
+// The workgroup builds bit masks of A, I and D per 64-node word with prefix ranks and
+// select samples (every 64th set bit's word) in LDS, plus the I nodes as a sorted list
+// (node, fth).  Then one wave walks the queue: a pod's window ends at its K-th feasible
+// node from its start s, i.e. at the A node of rank rank_A(s) + K - 1 unless I nodes with
+// fth <= now lie before it; those candidates (the I list from rank_I(s), a few per
+// window) are ranked among the A nodes (merged rank = A nodes before it + candidates
+// before it), and the end is the candidate of merged rank K - 1 or else the A node of
+// rank rank_A(s) + K - 1 - (candidates before it).  About ten dependent LDS round trips
+// per pod instead of a stream over its ~N/20 positions.  Positions are unrolled: a window
+// [s, s + N) wraps past node N - 1 to node 0.
+// Applies while the LDS holds it (N <= 64 * kRsMaxW, |I| <= kRsIMax); else it flags the
+// streaming kernel (k_sel_chain, launched behind it) to run.
+constexpr int kRsT = 1024;
+constexpr int kRsMaxW = 2048;  // 64-node words: N <= 131,072
+constexpr int kRsIMax = 4096;  // in-range nodes
+
+__host__ __device__ inline size_t rs_lds_bytes(int64_t W) {
+    const size_t Wp = (size_t)W + 1;
+    return 8 * (3 * Wp + kRsIMax) + 4 * (5 * Wp + kRsIMax);
+}
+
+struct RsView {
+    const uint64_t *mA, *mI, *mD;
+    const uint32_t *bA, *bI, *bD, *sA, *sD;
+    int32_t W;
+};
+
+__device__ __forceinline__ int64_t rs_rank(const uint64_t* m, const uint32_t* b, int64_t n) {
+    const int64_t w = n >> 6;
+    const int k = (int)(n & 63);
+    return (int64_t)b[w] + __popcll(m[w] & ((1ull << k) - 1ull));
+}
+
+// node of the r-th (0-based) set bit; whole wave, uniform r < total
+__device__ __forceinline__ int64_t rs_select(const uint64_t* m, const uint32_t* b, const uint32_t* smp, int32_t W,
+                                             int64_t r) {
+    const int lane = threadIdx.x & 63;
+    int64_t w = smp[r >> 6];  // the word holding rank 64 * (r / 64) (r's word is at or after it)
+    for (;;) {
+        const int64_t wl = min(w + lane + 1, (int64_t)W);
+        const uint64_t hb = __ballot((int64_t)b[wl] > r);
+        if (hb) {
+            const int64_t ww = w + __ffsll((long long)hb) - 1;
+            return ww * 64 + nth_set_bit(m[ww], (int)(r - (int64_t)b[ww]) + 1);
+        }
+        w += 64;
+    }
+}
+
+__global__ __launch_bounds__(kRsT) void k_sel_chain_rs(SelArgs a, const int64_t* __restrict__ fth, int64_t K,
+                                                       int64_t start, int64_t* __restrict__ wstart,
+                                                       int64_t* __restrict__ wlen, int64_t* __restrict__ next_start,
+                                                       int32_t* __restrict__ done) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t rs[];
+    __shared__ int64_t red[2][kRsT / 64];
+    __shared__ uint32_t part[kRsT];
+    const int64_t N = a.N, P = a.P;
+    const int32_t W = (int32_t)((N + 63) >> 6);
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t Wp = W + 1;
+    uint64_t* mA = rs;
+    uint64_t* mI = mA + Wp;
+    uint64_t* mD = mI + Wp;
+    int64_t* iFth = reinterpret_cast<int64_t*>(mD + Wp);
+    uint32_t* bA = reinterpret_cast<uint32_t*>(iFth + kRsIMax);
+    uint32_t* bI = bA + Wp;
+    uint32_t* bD = bI + Wp;
+    uint32_t* sA = bD + Wp;
+    uint32_t* sD = sA + Wp;
+    uint32_t* iPos = sD + Wp;
+    // the non-DaemonSet pods' time range
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (int64_t p = threadIdx.x; p < P; p += kRsT) {
+        if (a.flags && (a.flags[p] & 1u)) continue;
+        const int64_t t = a.now[p];
+        lo = min(lo, t);
+        hi = max(hi, t);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        lo = min(lo, (int64_t)__shfl_xor((long long)lo, o));
+        hi = max(hi, (int64_t)__shfl_xor((long long)hi, o));
+    }
+    if (lane == 0) {
+        red[0][wv] = lo;
+        red[1][wv] = hi;
+    }
+    __syncthreads();
+    int64_t tmin = INT64_MAX, tmax = INT64_MIN;
+#pragma unroll
+    for (int i = 0; i < kRsT / 64; ++i) {
+        tmin = min(tmin, red[0][i]);
+        tmax = max(tmax, red[1][i]);
+    }
+    for (int32_t w = wv; w < Wp; w += kRsT / 64) {
+        const int64_t n = (int64_t)w * 64 + lane;
+        const bool v = n < N;
+        const int64_t f = fth[min(n, N - 1)];
+        const uint64_t ma = __ballot(v && f <= tmin);
+        const uint64_t mi = __ballot(v && f > tmin && f <= tmax);
+        const uint64_t md = __ballot(v && f != INT64_MAX);
+        if (lane == 0) {
+            mA[w] = ma;
+            mI[w] = mi;
+            mD[w] = md;
+        }
+    }
+    __syncthreads();
+    // exclusive prefix ranks over the words (W + 1 entries: the last is the total)
+    {
+        const int per = (int)((Wp + kRsT - 1) / kRsT);
+        const int w0 = min((int)Wp, (int)threadIdx.x * per), w1 = min((int)Wp, w0 + per);
+        uint64_t* ms[3] = {mA, mI, mD};
+        uint32_t* bs[3] = {bA, bI, bD};
+        for (int x = 0; x < 3; ++x) {
+            uint32_t sum = 0;
+            for (int w = w0; w < w1; ++w) sum += __popcll(ms[x][w]);
+            uint32_t run = wg_excl_scan_u32<kRsT>(sum, part);
+            for (int w = w0; w < w1; ++w) {
+                bs[x][w] = run;
+                run += __popcll(ms[x][w]);
+            }
+            __syncthreads();
+        }
+    }
+    const int64_t TA = bA[W], TI = bI[W], TD = bD[W];
+    if (TI > kRsIMax) {  // more in-range nodes than the list holds: the streaming kernel runs
+        if (threadIdx.x == 0) *done = 0;
+        return;
+    }
+    // the in-range list and the select samples
+    for (int32_t w = threadIdx.x; w < W; w += kRsT) {
+        uint64_t m = mI[w];
+        uint32_t b = bI[w];
+        while (m) {
+            const int j = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const int64_t n = (int64_t)w * 64 + j;
+            iPos[b] = (uint32_t)n;
+            iFth[b] = fth[n];
+            ++b;
+        }
+        for (uint32_t k = (bA[w] + 63) >> 6; (k << 6) < bA[w + 1]; ++k) sA[k] = (uint32_t)w;
+        for (uint32_t k = (bD[w] + 63) >> 6; (k << 6) < bD[w + 1]; ++k) sD[k] = (uint32_t)w;
+    }
+    __syncthreads();
+    if (wv != 0) return;  // one wave walks the queue
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int64_t s = start;
+    for (int64_t p0 = 0; p0 < P; p0 += 64) {
+        const int nv = (int)min((int64_t)64, P - p0);
+        const int64_t tn = a.now[p0 + min(lane, nv - 1)];
+        const int32_t dn = a.flags ? (int32_t)(a.flags[p0 + min(lane, nv - 1)] & 1u) : 0;
+        int64_t my_ws = 0, my_wl = 0;
+        for (int j = 0; j < nv; ++j) {
+            const int64_t t = readlane64(tn, j);
+            const bool d = __builtin_amdgcn_readlane(dn, j) != 0;
+            int64_t end;  // unrolled position of the window's last node, in [s, s + N)
+            if (d) {
+                if (TD < K) {
+                    end = s + N - 1;
+                } else {
+                    const int64_t r = rs_rank(mD, bD, s) + K - 1;
+                    end = r < TD ? rs_select(mD, bD, sD, W, r) : N + rs_select(mD, bD, sD, W, r - TD);
+                }
+            } else {
+                const int64_t rA0 = rs_rank(mA, bA, s), rI0 = rs_rank(mI, bI, s);
+                bool full = false;  // fewer than K feasible nodes in the whole rotation
+                if (TA < K) {
+                    int64_t cnt = 0;
+                    for (int64_t q0 = 0; q0 < TI; q0 += 64) {
+                        const int64_t q = q0 + lane;
+                        cnt += __popcll(__ballot(q < TI && iFth[min(q, TI - 1)] <= t));
+                    }
+                    full = TA + cnt < K;
+                }
+                if (full) {
+                    end = s + N - 1;
+                } else {
+                    const int64_t rT = rA0 + K - 1;
+                    const int64_t xA = TA < K ? s + N - 1
+                                              : (rT < TA ? rs_select(mA, bA, sA, W, rT)
+                                                         : N + rs_select(mA, bA, sA, W, rT - TA));
+                    // candidates: I nodes in [s, xA] with fth <= t, in position order
+                    int64_t c_lt = 0, cbase = 0, hitpos = -1;
+                    for (int64_t q0 = 0; q0 < TI; q0 += 64) {
+                        const int64_t q = q0 + lane;
+                        int64_t idx = rI0 + q;
+                        const bool wrap = idx >= TI;
+                        idx -= wrap ? TI : 0;
+                        const int64_t ic = min(idx, TI - 1);
+                        const int64_t y = (int64_t)iPos[ic] + (wrap ? N : 0);
+                        const bool inr = q < TI && y <= xA;
+                        const uint64_t rm = __ballot(inr);
+                        if (!rm) break;
+                        const bool cand = inr && iFth[ic] <= t;
+                        const uint64_t cm = __ballot(cand);
+                        const int64_t ra = y < N ? rs_rank(mA, bA, y) : TA + rs_rank(mA, bA, y - N);
+                        const int64_t mr = ra - rA0 + cbase + __popcll(cm & lt);
+                        c_lt += __popcll(__ballot(cand && mr < K - 1));
+                        const uint64_t eq = __ballot(cand && mr == K - 1);
+                        if (eq) {
+                            hitpos = readlane64(y, __ffsll((long long)eq) - 1);
+                            break;
+                        }
+                        cbase += __popcll(cm);
+                        if (rm != ~0ull) break;  // the window's last in-range node was in this chunk
+                    }
+                    if (hitpos >= 0) {
+                        end = hitpos;
+                    } else {
+                        const int64_t r = rA0 + K - 1 - c_lt;
+                        end = r < TA ? rs_select(mA, bA, sA, W, r) : N + rs_select(mA, bA, sA, W, r - TA);
+                    }
+                }
+            }
+            if (lane == j) {
+                my_ws = s;
+                my_wl = end - s + 1;
+            }
+            s = end + 1 >= N ? end + 1 - N : end + 1;
+            s = s >= N ? s - N : s;
+        }
+        if (lane < nv) {
+            wstart[p0 + lane] = my_ws;
+            wlen[p0 + lane] = my_wl;
+        }
+    }
+    if (lane == 0) {
+        *next_start = s;
+        *done = 1;
     }
 }
 
@@ -389,10 +632,22 @@ hipError_t launch_select_fth(const SelArgs& a, int shape, int64_t* fth, hipStrea
 }
 
 hipError_t launch_select_chain(const SelArgs& a, const int64_t* fth, int64_t K, int64_t start, int64_t* wstart,
-                               int64_t* wlen, int64_t* next_start, hipStream_t st) {
+                               int64_t* wlen, int64_t* next_start, int32_t* done, int form, hipStream_t st) {
     if (a.P <= 0 || a.N <= 0) return hipSuccess;
+    const int64_t W = (a.N + 63) >> 6;
+    const bool rs = form != 1 && W <= kRsMaxW && done;
+    if (rs) {
+        static const hipError_t attr = hipFuncSetAttribute(
+            (const void*)k_sel_chain_rs, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rs_lds_bytes(kRsMaxW));
+        if (attr != hipSuccess) return attr;
+        hipError_t e = klaunch("k_sel_chain_rs", k_sel_chain_rs, dim3(1), dim3(kRsT), rs_lds_bytes(W), st, a, fth, K,
+                               start, wstart, wlen, next_start, done);
+        if (e != hipSuccess) return e;
+    }
+    // the streaming form: the only one past the LDS form's size, else behind it (it exits at once
+    // unless the LDS form found more in-range nodes than it holds)
     return klaunch("k_sel_chain", k_sel_chain, dim3(1), dim3(kChT), 0, st, a, fth, K, start, wstart, wlen,
-                   next_start);
+                   next_start, rs ? (const int32_t*)done : nullptr);
 }
 
 template <int PD, int PR>

@@ -197,6 +197,25 @@ __device__ __forceinline__ void bracket(const NodeRec<PD, PR>& r, int64_t t, int
     upd(r.e_hv);
 }
 
+// exclusive workgroup scan (BT threads): wave scans + a scan of the wave totals
+template <int BT = 256>
+__device__ __forceinline__ uint32_t wg_excl_scan_u32(uint32_t v, uint32_t* part) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) part[w] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+#pragma unroll
+    for (int i = 0; i < BT / 64; ++i) pre += i < w ? part[i] : 0u;
+    __syncthreads();
+    return pre + x - v;
+}
+
 __device__ __forceinline__ int64_t readlane64(int64_t v, int j) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), j);

@@ -275,6 +275,7 @@ const char *crane_dyn_version(void);
  *   "k3s_blocks" 0 auto | producer blocks per K3s workgroup aimed for (1..256)
  *   "k2x_threads" 512 | 1024 | 256: dedupe K2 workgroup size
  *   "k2l_region" 4096 | 2048: large K2 bindings per region   "k2l_co_t" 0 | 1: its count/offset layout
+ *   "sel_chain" 0 LDS rank/select walk of the selection windows (N <= 131072) | 1 streaming kernel
  *   "trace" 0 | 1: phase stamps of the step kernels (crane_dyn_debug_trace) */
 int crane_dyn_set_option(crane_dyn *h, const char *name, int64_t value);
 /* Phase stamps of the last K2x (which = 0), K1 (1) or K3s (2) launch with option

@@ -125,3 +125,59 @@ def test_select_nothing_feasible_and_daemonsets():
     for g, w in zip(got[:4], want[:4]):
         assert np.array_equal(g, w)
     assert got[4] == want[4]
+
+
+def _bench_queue_ext(N):
+    """The bench's config-3 selection leg's other-plugin verdicts (bench.py select_leg)."""
+    rng = np.random.default_rng(77)
+    return rng.random(N) < 0.95, rng.integers(0, 8, N).astype(np.int64) * 100
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_select_config3_queue_prefix():
+    """The bench's config-3 queue (100k nodes x 10k pods, shipped profile, adaptive 5 %
+    windows): the first 64 pods' windows, chosen nodes and totals equal the oracle's (a
+    window chain's prefix depends on the queue's prefix only), and every pod's window
+    equals the streaming chain kernel's (sel_chain 1)."""
+    spec = cd.default_policy_spec()
+    cfg = synth.CONFIGS[3]
+    c = synth.make_cluster(spec, cfg["nodes"], cfg["pods"], n_bindings=0, seed=20250215 + 3000)
+    c.now, c.ds = synth.make_pods(cfg["pods"], seed=20250215 + 3)
+    ok, ext = _bench_queue_ext(c.n_nodes)
+    eng = engine_for(spec, c)
+    got = _run(eng, c, ok, ext, 3, 0, 0, 0)
+    eng.set_option("sel_chain", 1)
+    ref = _run(eng, c, ok, ext, 3, 0, 0, 0)
+    eng.close()
+    for name, g, r in zip(("chosen", "total", "wstart", "wlen"), got[:4], ref[:4]):
+        assert np.array_equal(g, r), (name, np.nonzero(g != r)[0][:5])
+    assert got[4] == ref[4]
+    n = 64
+    off, osc, _ = oracle_soa(spec, c, now=c.now[:n], ds=c.ds[:n])
+    want = S.framework_select(off, osc, c.ds[:n], ok, ext, 3, 0, 0, 0)
+    for name, g, w in zip(("chosen", "total", "wstart", "wlen"), got[:4], want[:4]):
+        assert np.array_equal(g[:n], w), (name, np.nonzero(g[:n] != w)[0][:5])
+    assert want[4] == (got[2][n] if len(got[2]) > n else got[4])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,P,step_ns,pct", [(3000, 400, 1_000_000_000, 0), (20_000, 600, 60_000_000_000, 0),
+                                             (131_072, 300, 1_000_000_000, 0), (131_073, 100, 1_000_000_000, 0),
+                                             (5000, 700, 10_000_000, 2)])
+def test_select_chain_forms_agree(N, P, step_ns, pct):
+    """The LDS rank/select walk equals the streaming chain kernel pod for pod: few and many
+    in-range nodes (pods minutes apart put more than its list holds in range: the streaming
+    kernel then runs behind it), the size limit (131,072 nodes) and one past it, tiny
+    windows."""
+    spec, c = _cluster(N, P, seed=N + P, step_ns=step_ns)
+    rng = np.random.default_rng(N)
+    ok = rng.random(N) < 0.9
+    eng = engine_for(spec, c)
+    got = _run(eng, c, ok, None, 3, pct, 7, 0)
+    eng.set_option("sel_chain", 1)
+    ref = _run(eng, c, ok, None, 3, pct, 7, 0)
+    eng.close()
+    for name, g, r in zip(("chosen", "total", "wstart", "wlen"), got[:4], ref[:4]):
+        assert np.array_equal(g, r), (name, np.nonzero(g != r)[0][:5])
+    assert got[4] == ref[4]

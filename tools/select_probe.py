@@ -1,4 +1,7 @@
-"""Timing of framework-level selection (bench.select_leg) at the config-3 shape."""
+"""Timing of framework-level selection (bench.select_leg) at the config-3 shape.
+
+    python tools/select_probe.py [option=value ...]   (engine options, e.g. sel_chain=1)
+"""
 import json
 import os
 import sys
@@ -21,4 +24,4 @@ val, ts, _ = c.rows(names)
 dev = torch.device("cuda", 0)
 st = torch.cuda.Stream(dev)
 torch.cuda.set_stream(st)
-print(json.dumps(bench.select_leg(cd, spec, dev, st, val, ts, c.hv, c.hv_ts, c.now, c.ds)))
+print(json.dumps(bench.select_leg(cd, spec, dev, st, val, ts, c.hv, c.hv_ts, c.now, c.ds, opts=sys.argv[1:])))
