@@ -328,30 +328,45 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
             "traffic_source": pmc_src if (tr_k1 is not None or tr_k2 is not None) else None}
 
 
-def dropin_leg(cd, spec, ann, now, ds, ref_chosen, threads):
-    """Per-pod cycle of the C++ plugin mirror as the framework drives it (tools/dropin_bench.cpp)."""
+DROPIN_CPU = os.path.join(ROOT, "oracle", "_build", "dropin_cpu")
+
+
+def _dropin_files(d, spec, ann, now, ds):
+    pol = {"apiVersion": "scheduler.policy.crane.io/v1alpha1", "kind": "DynamicSchedulerPolicy",
+           "spec": {"syncPolicy": [{"name": n, "period": f"{p // 10**9}s"} for n, p in spec["syncPolicy"]],
+                    "predicate": [{"name": n, "maxLimitPecent": v} for n, v in spec["predicate"]],
+                    "priority": [{"name": n, "weight": v} for n, v in spec["priority"]],
+                    "hotValue": [{"timeRange": f"{t // 10**9}s", "count": c} for t, c in spec["hotValue"]]}}
+    pp = os.path.join(d, "policy.json")
+    json.dump(pol, open(pp, "w"))
+    sp = os.path.join(d, "snap.tsv")
+    with open(sp, "w") as f:
+        for i, a in enumerate(ann):
+            f.write(f"N\tnode-{i}\n")
+            for k, v in a.items():
+                f.write(f"A\t{k}\t{v}\n")
+    pd = os.path.join(d, "pods.tsv")
+    with open(pd, "w") as f:
+        for p in range(len(now)):
+            f.write(f"P\tpod-{p}\t{int(now[p])}\t{int(ds[p])}\n")
+    return pp, sp, pd
+
+
+def dropin_leg(cd, spec, ann, now, ds, ref_chosen, threads, cpu_pods=0):
+    """Per-pod cycle of the C++ plugin mirror as the framework drives it (tools/dropin_bench.cpp),
+    with its parts, and (cpu_pods > 0, the CPU-baseline leg) the same harness driving a CPU
+    plugin that re-parses annotations per call (oracle string mode) on the first cpu_pods pods."""
     if not os.path.exists(DROPIN):
         return {"error": f"{DROPIN} not built"}
+    env = dict(os.environ, TZ="Asia/Shanghai")
     with tempfile.TemporaryDirectory() as d:
-        pol = {"apiVersion": "scheduler.policy.crane.io/v1alpha1", "kind": "DynamicSchedulerPolicy",
-               "spec": {"syncPolicy": [{"name": n, "period": f"{p // 10**9}s"} for n, p in spec["syncPolicy"]],
-                        "predicate": [{"name": n, "maxLimitPecent": v} for n, v in spec["predicate"]],
-                        "priority": [{"name": n, "weight": v} for n, v in spec["priority"]],
-                        "hotValue": [{"timeRange": f"{t // 10**9}s", "count": c} for t, c in spec["hotValue"]]}}
-        pp = os.path.join(d, "policy.json")
-        json.dump(pol, open(pp, "w"))
-        sp = os.path.join(d, "snap.tsv")
-        with open(sp, "w") as f:
-            for i, a in enumerate(ann):
-                f.write(f"N\tnode-{i}\n")
-                for k, v in a.items():
-                    f.write(f"A\t{k}\t{v}\n")
-        pd = os.path.join(d, "pods.tsv")
-        with open(pd, "w") as f:
-            for p in range(len(now)):
-                f.write(f"P\tpod-{p}\t{int(now[p])}\t{int(ds[p])}\n")
-        env = dict(os.environ, TZ="Asia/Shanghai")
+        pp, sp, pd = _dropin_files(d, spec, ann, now, ds)
         r = subprocess.run([DROPIN, pp, sp, pd, str(threads)], capture_output=True, text=True, timeout=600, env=env)
+        rc = None
+        if cpu_pods and os.path.exists(DROPIN_CPU):
+            pp, sp, pd = _dropin_files(d, spec, ann, now[:cpu_pods], ds[:cpu_pods])
+            rc = subprocess.run([DROPIN_CPU, pp, sp, pd, str(threads), "cpu"], capture_output=True, text=True,
+                                timeout=600, env=env)
     if r.returncode != 0:
         return {"error": r.stderr[-500:]}
     o = json.loads(r.stdout.strip().splitlines()[-1])
@@ -360,7 +375,27 @@ def dropin_leg(cd, spec, ann, now, ds, ref_chosen, threads):
     o["dropin_ms_per_pod"] = o["cycle_ms_median"]
     o["workload"] = (f"{o['nodes']} nodes x {o['pods']} pods, one scheduling cycle per pod: Filter on every node + "
                      f"Score on every feasible node from {o['threads']} threads + selectHost, through "
-                     "include/crane_dyn_plugin.hpp (per-cycle int8 rows from crane_dyn_eval_compact)")
+                     "include/crane_dyn_plugin.hpp (per-node answers looked up in the engine's step tables, "
+                     "crane_dyn_node_steps, one table per 60 s of pod time)")
+    o["breakdown"] = {"sync_ms": o.pop("sync_ms"), "filter_fanout_ms": o.pop("filter_fanout_ms_median"),
+                      "score_fanout_ms": o.pop("score_fanout_ms_median"), "select_ms": o.pop("select_ms_median"),
+                      "tables_built": o.pop("tables_built"),
+                      "note": "sync = bulk parse + upload of the snapshot, once per generation; the first cycle "
+                              "also builds the answer table (cycle_ms_max)"}
+    if rc is not None:
+        if rc.returncode != 0:
+            o["cpu_same_harness_error"] = rc.stderr[-300:]
+        else:
+            oc = json.loads(rc.stdout.strip().splitlines()[-1])
+            chc = oc.pop("chosen")
+            o["cpu_same_harness_ms_per_pod"] = oc["cycle_ms_median"]
+            o["cpu_same_harness"] = {
+                "pods": oc["pods"], "threads": oc["threads"], "cycle_ms_median": oc["cycle_ms_median"],
+                "filter_fanout_ms": oc["filter_fanout_ms_median"], "score_fanout_ms": oc["score_fanout_ms_median"],
+                "matches_engine_chosen": bool(np.array_equal(np.array(chc), np.asarray(ref_chosen)[:cpu_pods])),
+                "how": "same harness and thread pool; Filter / Score re-parse the node's annotations per call "
+                       "like stats.go:51-76 (oracle string mode, oracle/_build/dropin_cpu)"}
+            o["speedup_vs_cpu_same_harness"] = round(oc["cycle_ms_median"] / o["cycle_ms_median"], 1)
     return o
 
 
@@ -811,7 +846,7 @@ def main():
             ae = _annot_engine(cd, spec, local, val, ts, c)
             _, _, ref_ch, _ = ae.eval(c.now[:64], c.ds[:64])
             ae.close()
-            extras["dropin"] = dropin_leg(cd, spec, ann, c.now[:64], c.ds[:64], ref_ch, args.cpu_threads)
+            extras["dropin"] = dropin_leg(cd, spec, ann, c.now[:64], c.ds[:64], ref_ch, args.cpu_threads, cpu_pods=4)
             extras["controller_hot_values"] = controller_leg(cd, O, synth, spec, dev, c, N, B)
 
     if rank == 0:

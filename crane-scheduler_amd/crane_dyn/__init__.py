@@ -94,6 +94,8 @@ def _load():
         "crane_dyn_set_profiling": (C.c_int, [vp, C.c_int]),
         "crane_dyn_stage_times": (C.c_int, [vp, C.c_int32, P(C.c_char_p), P(C.c_double)]),
         "crane_dyn_key_node": (C.c_int64, [C.c_int64, P(C.c_int64)]),
+        "crane_dyn_step_slots": (C.c_int32, [vp]),
+        "crane_dyn_node_steps": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp, vp]),
         "crane_dyn_version": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
@@ -117,7 +119,7 @@ ABI_SYMBOLS = (
     "crane_dyn_binding_count", "crane_dyn_eval_compact", "crane_dyn_eval_matrix_async", "crane_dyn_set_option",
     "crane_translate_event", "crane_dyn_debug_trace", "crane_num_feasible_nodes_to_find", "crane_dyn_select",
     "crane_tz_load", "crane_tz_load_bytes", "crane_tz_free", "crane_tz_lookup", "crane_tz_date",
-    "crane_parse_annotation_tz", "crane_parse_annotations_tz",
+    "crane_parse_annotation_tz", "crane_parse_annotations_tz", "crane_dyn_step_slots", "crane_dyn_node_steps",
 )
 
 
@@ -507,6 +509,26 @@ class Engine:
                 check(rc)
 
         return step
+
+    def node_steps(self, t0_ns, t1_ns):
+        """Every node's Filter / Score over [t0, t1) as step functions (crane_dyn_node_steps):
+        (n_steps[N] u8, bp[N][S] i64, first_fail[N][S+1] i8, score[N][S+1] i8)."""
+        S, N = lib.crane_dyn_step_slots(self.h), self.n_nodes
+        ns = np.zeros(N, np.uint8)
+        bp = np.zeros((N, S), np.int64)
+        ff = np.zeros((N, S + 1), np.int8)
+        sc = np.zeros((N, S + 1), np.int8)
+        self._check(lib.crane_dyn_node_steps(self.h, int(t0_ns), int(t1_ns), N, _ptr(ns), _ptr(bp), _ptr(ff),
+                                             _ptr(sc)))
+        return ns, bp, ff, sc
+
+    @staticmethod
+    def table_lookup(tables, now_ns):
+        """first_fail[N], score[N] at now_ns from node_steps tables (what the plugin does per call)."""
+        ns, bp, ff, sc = tables
+        j = ((bp <= now_ns) & (np.arange(bp.shape[1])[None, :] < ns[:, None])).sum(1)
+        r = np.arange(len(ns))
+        return ff[r, j], sc[r, j]
 
     def greedy(self, n_pods, now_ns, pod_flags=None):
         fl = None if pod_flags is None else np.ascontiguousarray(pod_flags, np.uint8)

@@ -189,6 +189,8 @@ struct crane_dyn {
     DevBuf<int32_t> sqm, snq;     // their middle-piece slots, and the count per block
     DevBuf<int64_t> sel_fth, sel_win, sel_state;  // framework selection (select.hip)
     DevBuf<long long> sel_keys;
+    DevBuf<unsigned char> stp_dev;  // node answer tables (crane_dyn_node_steps): bp, ns, ff, score
+    HostBuf<unsigned char> stp_host;
     DevBuf<Mid> smid;
     DevBuf<Step1> sstep1;
     DevBuf<Step1> sstage;  // K1's one-step staging past its LDS (StepTables::stage)
@@ -695,6 +697,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->sperm.release(); h->scnt.release(); h->stile.release(); h->sbatch.release(); h->sq.release(); h->sqm.release(); h->snq.release(); h->spnow.release(); h->smid.release(); h->sstep1.release(); h->sstage.release();
     h->spm1.release(); h->ssm0.release(); h->srows.release();
     h->sel_fth.release(); h->sel_win.release(); h->sel_state.release(); h->sel_keys.release();
+    h->stp_dev.release(); h->stp_host.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -1145,6 +1148,47 @@ int crane_dyn_eval_compact(crane_dyn* h, int64_t P, const int64_t* now_ns, const
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
     return eval_host(h, P, now_ns, pod_flags, first_fail, score, false, chosen, chosen_score);
+}
+
+int32_t crane_dyn_step_slots(const crane_dyn* h) { return h && h->N != -2 ? node_step_slots(h->shape) : 0; }
+
+int crane_dyn_node_steps(crane_dyn* h, int64_t t0_ns, int64_t t1_ns, int64_t n, uint8_t* n_steps, int64_t* bp,
+                         int8_t* first_fail, int8_t* score) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before building node tables");
+    if (n != h->N) return h->fail(CRANE_E_INVALID, "the tables hold one entry per node of the shard");
+    if (n > 0 && (!n_steps || !bp || !first_fail || !score)) return h->fail(CRANE_E_INVALID, "NULL output");
+    if (!(t0_ns < t1_ns)) return h->fail(CRANE_E_INVALID, "t0 must be before t1");
+    if (n == 0) return CRANE_OK;
+    HIPTRY(h, hipSetDevice(h->device));
+    hipStream_t st = h->stream;
+    if (h->rec_dirty) {
+        int rc = node_pass_locked(h, st);
+        if (rc) return rc;
+    }
+    const size_t S = (size_t)node_step_slots(h->shape), N = (size_t)n;
+    const size_t o_ns = 8 * N * S, o_ff = o_ns + N, o_sc = o_ff + N * (S + 1), total = o_sc + N * (S + 1);
+    HIPTRY(h, h->stp_dev.reserve(total));
+    HIPTRY(h, h->stp_host.reserve(total));
+    MatrixArgs a{};
+    a.rec = h->rec.p;
+    a.N = h->N;
+    a.node_offset = h->node_offset;
+    a.wsum = h->dp.wsum;
+    a.noprio = h->dp.noprio;
+    std::memcpy(a.pred_orig, h->pred_orig, sizeof a.pred_orig);
+    unsigned char* d = h->stp_dev.p;
+    HIPTRY(h, launch_node_steps(h->shape, a, t0_ns, t1_ns, d + o_ns, reinterpret_cast<int64_t*>(d),
+                                reinterpret_cast<int8_t*>(d + o_ff), reinterpret_cast<int8_t*>(d + o_sc), st));
+    HIPTRY(h, hipMemcpyAsync(h->stp_host.p, d, total, hipMemcpyDeviceToHost, st));
+    HIPTRY(h, hipStreamSynchronize(st));
+    const unsigned char* p = h->stp_host.p;
+    std::memcpy(bp, p, 8 * N * S);
+    std::memcpy(n_steps, p + o_ns, N);
+    std::memcpy(first_fail, p + o_ff, N * (S + 1));
+    std::memcpy(score, p + o_sc, N * (S + 1));
+    return CRANE_OK;
 }
 
 int crane_dyn_set_profiling(crane_dyn* h, int on) {

@@ -73,6 +73,11 @@ struct MatrixArgs {
     int8_t pred_orig[kMaxPred];  // device predicate -> policy predicate index
 };
 hipError_t launch_matrix(int shape, const MatrixArgs& a, hipStream_t st);
+// Filter / Score of every node as step functions over [t0, t1) (crane_dyn_node_steps):
+// ns[n] breakpoints bp[n * S + j], values ff / sc[n * (S + 1) + j]; S = node_step_slots(shape)
+int node_step_slots(int shape);
+hipError_t launch_node_steps(int shape, const MatrixArgs& a, int64_t t0, int64_t t1, uint8_t* ns, int64_t* bp,
+                             int8_t* ff, int8_t* sc, hipStream_t st);
 
 // Framework-level selection (select.hip): upstream kube-scheduler's percentageOfNodesToScore
 // window with a rotating start, the weighted sum of Dynamic's score and the other score

@@ -312,4 +312,74 @@ hipError_t launch_matrix(int shape, const MatrixArgs& a, hipStream_t st) {
     }
 }
 
+// ---------------------------------------------------------------- node answer tables
+// The drop-in plugin's per-cycle answers as step functions of time (crane_dyn_node_steps):
+// a node's Filter (first failing predicate) and Score change only where `now` crosses one
+// of its expiries, so over [t0, t1) they are constant between the expiries inside it.  One
+// thread per node: the expiries in (t0, t1), sorted and deduplicated, and the values at t0
+// and at each of them (the same ff_at / score_at as every other path).
+template <int PD, int PR>
+__global__ __launch_bounds__(256) void k_node_steps(MatrixArgs a, int64_t t0, int64_t t1, uint8_t* __restrict__ ns,
+                                                    int64_t* __restrict__ bp, int8_t* __restrict__ ffv,
+                                                    int8_t* __restrict__ scv) {
+    constexpr int S = PD + PR + 1;
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (n >= a.N) return;
+    const NodeRec<PD, PR> r = static_cast<const NodeRec<PD, PR>*>(a.rec)[n];
+    int64_t e[S];
+    int c = 0;
+    auto put = [&](int64_t x) {
+        if (x > t0 && x < t1) e[c++] = x;
+    };
+#pragma unroll
+    for (int k = 0; k < PD; ++k) put(r.e_pred[k]);
+#pragma unroll
+    for (int k = 0; k < PR; ++k) put(r.e_prio[k]);
+    put(r.e_hv);
+    for (int i = 1; i < c; ++i) {  // insertion sort (at most S values)
+        const int64_t x = e[i];
+        int j = i - 1;
+        while (j >= 0 && e[j] > x) {
+            e[j + 1] = e[j];
+            --j;
+        }
+        e[j + 1] = x;
+    }
+    int m = 0;
+    for (int i = 0; i < c; ++i)
+        if (m == 0 || e[i] != e[m - 1]) e[m++] = e[i];
+    ns[n] = (uint8_t)m;
+    ffv[n * (S + 1)] = (int8_t)ff_at<PD, PR>(t0, r, a);
+    scv[n * (S + 1)] = (int8_t)score_at<PD, PR>(t0, r, a.wsum, a.noprio);
+    for (int i = 0; i < m; ++i) {
+        bp[n * S + i] = e[i];
+        ffv[n * (S + 1) + i + 1] = (int8_t)ff_at<PD, PR>(e[i], r, a);
+        scv[n * (S + 1) + i + 1] = (int8_t)score_at<PD, PR>(e[i], r, a.wsum, a.noprio);
+    }
+}
+
+int node_step_slots(int shape) {
+    switch (shape) {
+        case kShape4x6: return 4 + 6 + 1;
+        case kShape8x8: return 8 + 8 + 1;
+        default: return 16 + 16 + 1;
+    }
+}
+
+template <int PD, int PR>
+static hipError_t steps_t(const MatrixArgs& a, int64_t t0, int64_t t1, uint8_t* ns, int64_t* bp, int8_t* ff,
+                          int8_t* sc, hipStream_t st) {
+    return klaunch("k_node_steps", k_node_steps<PD, PR>, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, st, a, t0,
+                   t1, ns, bp, ff, sc);
+}
+hipError_t launch_node_steps(int shape, const MatrixArgs& a, int64_t t0, int64_t t1, uint8_t* ns, int64_t* bp,
+                             int8_t* ff, int8_t* sc, hipStream_t st) {
+    if (a.N <= 0) return hipSuccess;
+    switch (shape) {
+        case kShape4x6: return steps_t<4, 6>(a, t0, t1, ns, bp, ff, sc, st);
+        case kShape8x8: return steps_t<8, 8>(a, t0, t1, ns, bp, ff, sc, st);
+        default: return steps_t<16, 16>(a, t0, t1, ns, bp, ff, sc, st);
+    }
+}
+
 }  // namespace crane

@@ -299,9 +299,9 @@ __device__ __forceinline__ int64_t rs_rank(const uint64_t* m, const uint32_t* b,
     return (int64_t)b[w] + __popcll(m[w] & ((1ull << k) - 1ull));
 }
 
-// node of the r-th (0-based) set bit; whole wave, uniform r < total
+// node of the r-th (0-based) set bit; whole wave, uniform r < total; *word = its mask word
 __device__ __forceinline__ int64_t rs_select(const uint64_t* m, const uint32_t* b, const uint32_t* smp, int32_t W,
-                                             int64_t r) {
+                                             int64_t r, uint64_t* word = nullptr) {
     const int lane = threadIdx.x & 63;
     int64_t w = smp[r >> 6];  // the word holding rank 64 * (r / 64) (r's word is at or after it)
     for (;;) {
@@ -309,7 +309,9 @@ __device__ __forceinline__ int64_t rs_select(const uint64_t* m, const uint32_t* 
         const uint64_t hb = __ballot((int64_t)b[wl] > r);
         if (hb) {
             const int64_t ww = w + __ffsll((long long)hb) - 1;
-            return ww * 64 + nth_set_bit(m[ww], (int)(r - (int64_t)b[ww]) + 1);
+            const uint64_t mw = m[ww];
+            if (word) *word = mw;
+            return ww * 64 + nth_set_bit(mw, (int)(r - (int64_t)b[ww]) + 1);
         }
         w += 64;
     }
@@ -446,9 +448,10 @@ __global__ __launch_bounds__(kRsT) void k_sel_chain_rs(SelArgs a, const int64_t*
                     end = s + N - 1;
                 } else {
                     const int64_t rT = rA0 + K - 1;
+                    uint64_t wA = 0;  // the mask word holding xA (TA >= K)
                     const int64_t xA = TA < K ? s + N - 1
-                                              : (rT < TA ? rs_select(mA, bA, sA, W, rT)
-                                                         : N + rs_select(mA, bA, sA, W, rT - TA));
+                                              : (rT < TA ? rs_select(mA, bA, sA, W, rT, &wA)
+                                                         : N + rs_select(mA, bA, sA, W, rT - TA, &wA));
                     // candidates: I nodes in [s, xA] with fth <= t, in position order
                     int64_t c_lt = 0, cbase = 0, hitpos = -1;
                     for (int64_t q0 = 0; q0 < TI; q0 += 64) {
@@ -476,9 +479,18 @@ __global__ __launch_bounds__(kRsT) void k_sel_chain_rs(SelArgs a, const int64_t*
                     }
                     if (hitpos >= 0) {
                         end = hitpos;
+                    } else if (TA >= K && c_lt == 0) {
+                        end = xA;
                     } else {
-                        const int64_t r = rA0 + K - 1 - c_lt;
-                        end = r < TA ? rs_select(mA, bA, sA, W, r) : N + rs_select(mA, bA, sA, W, r - TA);
+                        // the A node c_lt before xA: inside xA's word when it holds that many below it
+                        const int xb = (int)((xA >= N ? xA - N : xA) & 63);  // xA's bit in its word
+                        const int below = TA >= K ? __popcll(wA & ((1ull << xb) - 1ull)) : -1;
+                        if (c_lt <= below) {
+                            end = xA - xb + nth_set_bit(wA, below - (int)c_lt + 1);
+                        } else {
+                            const int64_t r = rA0 + K - 1 - c_lt;
+                            end = r < TA ? rs_select(mA, bA, sA, W, r) : N + rs_select(mA, bA, sA, W, r - TA);
+                        }
                     }
                 }
             }

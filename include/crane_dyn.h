@@ -190,6 +190,17 @@ int crane_dyn_eval(crane_dyn *h, int64_t n_pods, const int64_t *now_ns, const ui
  * (pod, node) instead of 9 cross PCIe — the form the plugin shim uses per pod. */
 int crane_dyn_eval_compact(crane_dyn *h, int64_t n_pods, const int64_t *now_ns, const uint8_t *pod_flags,
                            int8_t *first_fail, int8_t *score, int64_t *chosen, int64_t *chosen_score);
+/* Answer tables for the drop-in plugin: a node's Filter and Score depend on `now` only
+ * through `now < expiry` against its expiries, so over [t0_ns, t1_ns) each is a step
+ * function.  For node i: n_steps[i] (<= S = crane_dyn_step_slots) breakpoints
+ * bp[i*S + j] ascending inside (t0, t1), and first_fail / score[i*(S+1) + j] (as in
+ * crane_dyn_eval, int8) on [bp[j-1], bp[j]) with bp[-1] = t0, bp[n_steps] = t1.  The
+ * engine computes every value (the same kernels' arithmetic); the plugin answers a pod's
+ * per-node calls at its `now` by a lookup, with no device call per pod.  Synchronous;
+ * n = the shard's node count; host arrays. */
+int32_t crane_dyn_step_slots(const crane_dyn *h);
+int crane_dyn_node_steps(crane_dyn *h, int64_t t0_ns, int64_t t1_ns, int64_t n, uint8_t *n_steps, int64_t *bp,
+                         int8_t *first_fail, int8_t *score);
 /* Device-resident matrix form, asynchronous on `stream`: d_first_fail[p*ld + i]
  * and d_score[p*ld + i] (int8) as crane_dyn_eval, any may be NULL; d_keys (NULL
  * = none) as crane_dyn_eval_keys_async. */

@@ -13,16 +13,20 @@
 // The k8s framework types are reduced to what the plugin touches.  Instead of
 // re-parsing annotations per call (stats.go:51-76), the plugin parses a node
 // snapshot once per generation (Sync: one bulk, threaded crane_parse_annotations
-// call) and answers a pod's Filter/Score calls from one engine evaluation of
-// that pod against every node (crane_dyn_eval_compact: int8 first-fail and
-// score rows), made once per scheduling cycle and kept in the CycleState.
+// call).  A node's Filter and Score depend on `now` only through its expiries, so
+// the engine returns every node's answers as step functions of time over a horizon
+// (crane_dyn_node_steps: int8 first-fail and score per piece, computed by the
+// engine's kernels); a pod's per-node calls are then lookups at its `now` — no
+// device call per pod, a new table only when a pod's time leaves the horizon or the
+// snapshot generation changes.
 //
 // Threading: the framework calls Filter/Score for one pod from 16 goroutines.
-// The first call of a cycle computes the cycle's row under std::call_once; every
-// call after that reads the immutable row (and the immutable name -> index map
-// of the snapshot generation it was computed against) without taking a lock.
+// The first call of a cycle fetches the table under std::call_once; every call
+// after that reads the immutable table (and the immutable node -> index maps of
+// the snapshot generation it was built from) without taking a lock.
 #pragma once
 
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -30,7 +34,9 @@
 #include <memory>
 #include <mutex>
 #include <stdexcept>
+#include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <thread>
 #include <typeinfo>
@@ -90,8 +96,8 @@ class NodeInfo {
 
 // One scheduling cycle of one pod (framework.CycleState).  time.Now() for the
 // whole cycle (the reference calls it per Filter/Score call; declared deviation).
-// The Dynamic plugin's per-cycle row lives here (as plugins keep cycle data in
-// the framework's CycleState); Clone() (preemption dry runs) shares it.
+// The Dynamic plugin's answer table of the cycle lives here (as plugins keep cycle
+// data in the framework's CycleState); Clone() (preemption dry runs) shares it.
 struct CycleState {
     int64_t now_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
                          std::chrono::system_clock::now().time_since_epoch())
@@ -172,28 +178,34 @@ class DynamicScheduler {
         if (IsDaemonsetPod(pod)) return NewStatus(Code::Success, "");
         const Node* node = nodeInfo.node();
         if (!node) return NewStatus(Code::Error, "node not found");
-        const Row* row;
+        const Table* t;
         int64_t idx;
         std::string err;
-        if (!row_for(state, pod, node->Name, &row, &idx, &err)) return NewStatus(Code::Error, err);
-        const int k = row->first_fail[(size_t)idx];
-        if (k >= 0)
-            return NewStatus(Code::Unschedulable,
-                             "Load[" + std::string(policy().pred_name[k]) + "] of node[" + node->Name + "] is too high");
+        if (!table_for(state, node, &t, &idx, &err)) return NewStatus(Code::Error, err);
+        const int k = t->first_fail[t->piece(idx, state.now_ns)];
+        if (k >= 0) {  // "Load[%s] of node[%s] is too high", one allocation
+            const char* pn = policy().pred_name[k];
+            const size_t pl = std::strlen(pn);
+            std::string m;
+            m.reserve(5 + pl + 9 + node->Name.size() + 13);
+            m.append("Load[", 5).append(pn, pl).append("] of node[", 10).append(node->Name).append("] is too high", 13);
+            return NewStatus(Code::Unschedulable, std::move(m));
+        }
         return NewStatus(Code::Success, "");
     }
 
     // Score (plugins.go:73-98)
     std::pair<int64_t, Status> Score(CycleState& state, const Pod& pod, const std::string& nodeName) {
+        (void)pod;
         std::string err;
         const Node* node = handle_.snapshot ? handle_.snapshot->Get(nodeName, &err) : nullptr;
         if (!err.empty() || !handle_.snapshot)
             return {0, NewStatus(Code::Error, "getting node \"" + nodeName + "\" from Snapshot: " + err)};
         if (!node) return {0, NewStatus(Code::Error, "node not found")};
-        const Row* row;
+        const Table* t;
         int64_t idx;
-        if (!row_for(state, pod, node->Name, &row, &idx, &err)) return {0, NewStatus(Code::Error, err)};
-        return {(int64_t)row->score[(size_t)idx], Status()};
+        if (!table_for(state, node, &t, &idx, &err)) return {0, NewStatus(Code::Error, err)};
+        return {(int64_t)t->score[t->piece(idx, state.now_ns)], Status()};
     }
 
     // Re-parse the snapshot's annotations into the engine (once per generation).
@@ -204,21 +216,80 @@ class DynamicScheduler {
 
     // host threads of the once-per-sync annotation parse (<= 0: all hardware threads)
     void SetParseThreads(int32_t n) { parse_threads_ = n; }
+    // time span one answer table covers (a pod later than it gets a new table)
+    void SetHorizon(int64_t ns) { horizon_ns_ = ns > 0 ? ns : 1; }
+    // answer tables built so far (one per horizon and snapshot generation)
+    uint64_t TablesBuilt() const { return tables_built_.load(); }
 
     friend std::pair<std::unique_ptr<DynamicScheduler>, std::string> NewDynamicScheduler(const Object& plArgs,
                                                                                          const Handle& h);
 
    private:
-    // one synced snapshot generation: node name -> engine index (immutable once published)
+    // one synced snapshot generation: node -> engine index (immutable once published).  The
+    // framework hands Filter the snapshot's own Node objects, so their address is the key
+    // (a flat open-addressing table); a name lookup remains for any other Node object.
     struct Synced {
         uint64_t generation;
         std::unordered_map<std::string, int64_t> index;
+        std::vector<const Node*> ptrs;                       // List() order
+        std::vector<std::pair<const Node*, int64_t>> slots;  // power-of-two size, {nullptr, -1} empty
+        int shift = 64;
+        static uint64_t mix(const Node* p) { return ((uint64_t)(uintptr_t)p >> 4) * 0x9E3779B97F4A7C15ull; }
+        void build(const std::vector<const Node*>& nodes) {
+            ptrs = nodes;
+            size_t cap = 16;
+            while (cap < 2 * nodes.size()) cap <<= 1;
+            shift = 64 - __builtin_ctzll(cap);
+            slots.assign(cap, {nullptr, -1});
+            for (size_t i = 0; i < nodes.size(); ++i) {
+                size_t h = (size_t)(mix(nodes[i]) >> shift);
+                while (slots[h].first && slots[h].first != nodes[i]) h = (h + 1) & (cap - 1);
+                slots[h] = {nodes[i], (int64_t)i};
+            }
+        }
+        int64_t find(const Node* p) const {
+            // the framework walks the nodes in List() order in chunks per goroutine: the node
+            // after this thread's last one (or a few further, for the feasible list) first
+            thread_local const Synced* last_snap = nullptr;
+            thread_local int64_t last = -1;
+            if (last_snap == this) {
+                const int64_t n = (int64_t)ptrs.size();
+                for (int64_t i = last + 1; i < std::min(n, last + 5); ++i)
+                    if (ptrs[(size_t)i] == p) return last = i;
+            }
+            const int64_t i = find_slow(p);
+            last_snap = this;
+            last = i;
+            return i;
+        }
+        int64_t find_slow(const Node* p) const {
+            size_t h = (size_t)(mix(p) >> shift);
+            for (;;) {
+                const auto& s = slots[h];
+                if (s.first == p) return s.second;
+                if (!s.first) break;
+                h = (h + 1) & (slots.size() - 1);
+            }
+            auto it = index.find(p->Name);
+            return it == index.end() ? -1 : it->second;
+        }
     };
-    // one cycle's answers for every node of `snap` (immutable once published)
-    struct Row {
+    // every node's answers over [t0, t1) as step functions (immutable once published)
+    struct Table {
         std::shared_ptr<const Synced> snap;
-        std::vector<int8_t> first_fail;
-        std::vector<int8_t> score;
+        int64_t t0 = 0, t1 = 0;
+        size_t S = 0;
+        std::vector<uint8_t> n_steps;
+        std::vector<int64_t> bp;
+        std::vector<int8_t> first_fail, score;
+        // index of node i's value at time t (t0 <= t < t1)
+        size_t piece(int64_t i, int64_t t) const {
+            const size_t nb = n_steps[(size_t)i];
+            const int64_t* b = bp.data() + (size_t)i * S;
+            size_t j = 0;
+            while (j < nb && b[j] <= t) ++j;
+            return (size_t)i * (S + 1) + j;
+        }
     };
 
     DynamicScheduler() = default;
@@ -236,6 +307,7 @@ class DynamicScheduler {
         auto snap = std::make_shared<Synced>();
         snap->generation = gen;
         snap->index.reserve(N);
+        snap->build(nodes);
         // rows [metric slot 0..M-1, node_hot_value] x N of annotation strings (NULL = key missing)
         std::vector<const char*> strs((size_t)(M + 1) * N, nullptr);
         std::vector<size_t> lens((size_t)(M + 1) * N, 0);
@@ -269,52 +341,59 @@ class DynamicScheduler {
             return nullptr;
         }
         synced_ = std::move(snap);
+        table_.reset();
         return synced_;
     }
 
-    // The cycle's row (computed by the first caller of the cycle), and the node's index in it.
-    bool row_for(CycleState& state, const Pod& pod, const std::string& node_name, const Row** row, int64_t* idx,
-                 std::string* err) {
+    // The table covering the cycle's time (fetched by the first caller of the cycle), and
+    // the node's index in it.
+    bool table_for(CycleState& state, const Node* node, const Table** table, int64_t* idx, std::string* err) {
         std::call_once(state.dyn_once_, [&] {
             std::string e;
-            std::shared_ptr<Row> r = compute_row(state.now_ns, pod, &e);
+            std::shared_ptr<const Table> t = table_at(state.now_ns, &e);
             std::lock_guard<std::mutex> g(state.clone_mu_);
-            state.dyn_row_ = r;
+            state.dyn_row_ = t;
             state.dyn_err_ = e;
             state.dyn_done_ = true;
         });
-        const Row* r = static_cast<const Row*>(state.dyn_row_.get());
-        if (!r) {
+        const Table* t = static_cast<const Table*>(state.dyn_row_.get());
+        if (!t) {
             *err = state.dyn_err_;
             return false;
         }
-        auto ni = r->snap->index.find(node_name);
-        if (ni == r->snap->index.end()) {
-            *err = "node \"" + node_name + "\" not in the synced snapshot";
+        const int64_t i = t->snap->find(node);
+        if (i < 0) {
+            *err = "node \"" + node->Name + "\" not in the synced snapshot";
             return false;
         }
-        *row = r;
-        *idx = ni->second;
+        *table = t;
+        *idx = i;
         return true;
     }
 
-    std::shared_ptr<Row> compute_row(int64_t now_ns, const Pod& pod, std::string* err) {
-        std::lock_guard<std::mutex> g(mu_);  // one engine: the sync and the evaluation are serial
+    std::shared_ptr<const Table> table_at(int64_t now_ns, std::string* err) {
+        std::lock_guard<std::mutex> g(mu_);  // one engine: the sync and the table build are serial
         std::shared_ptr<const Synced> snap = sync_locked(err);
         if (!snap) return nullptr;
-        auto r = std::make_shared<Row>();
-        r->snap = snap;
+        if (table_ && table_->snap == snap && table_->t0 <= now_ns && now_ns < table_->t1) return table_;
+        auto t = std::make_shared<Table>();
+        t->snap = snap;
+        t->t0 = now_ns;
+        t->t1 = now_ns > INT64_MAX - horizon_ns_ ? INT64_MAX : now_ns + horizon_ns_;
+        t->S = (size_t)crane_dyn_step_slots(eng_);
         const size_t N = snap->index.size();
-        r->first_fail.assign(N, -1);
-        r->score.assign(N, 0);
-        const uint8_t flag = IsDaemonsetPod(pod) ? CRANE_POD_DAEMONSET : 0;
-        int64_t chosen, chosen_score;
-        if (crane_dyn_eval_compact(eng_, 1, &now_ns, &flag, r->first_fail.data(), r->score.data(), &chosen,
-                                   &chosen_score)) {
+        t->n_steps.resize(N);
+        t->bp.resize(N * t->S);
+        t->first_fail.resize(N * (t->S + 1));
+        t->score.resize(N * (t->S + 1));
+        if (crane_dyn_node_steps(eng_, t->t0, t->t1, (int64_t)N, t->n_steps.data(), t->bp.data(),
+                                 t->first_fail.data(), t->score.data())) {
             *err = crane_dyn_last_error(eng_);
             return nullptr;
         }
-        return r;
+        ++tables_built_;
+        table_ = t;
+        return table_;
     }
 
     Handle handle_;
@@ -323,8 +402,11 @@ class DynamicScheduler {
     crane_tz* zone_ = nullptr;  // the IANA zone of $TZ, or null: the fixed offset tz_
     int64_t tz_ = 8 * 3600;
     int32_t parse_threads_ = 16;  // the framework's parallelism (upstream default)
+    int64_t horizon_ns_ = 60LL * 1000000000LL;
+    std::atomic<uint64_t> tables_built_{0};
     std::mutex mu_;
     std::shared_ptr<const Synced> synced_;
+    std::shared_ptr<const Table> table_;
 };
 
 // NewDynamicScheduler (plugins.go:105-120): the same error strings.

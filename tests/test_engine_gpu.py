@@ -413,3 +413,28 @@ def test_config4_shard_parity():
         feas = (offm[i] < 0) | bool(c.ds[p])
         assert score[p] == (osc[i][feas].max() if feas.any() else -1)
     assert ((score >= 0) & (score <= 100)).all()
+
+
+@pytest.mark.parametrize("N,horizon_s,seed", [(3000, 60, 71), (20_000, 600, 72), (5, 3600, 73)])
+def test_node_steps_tables(N, horizon_s, seed):
+    """crane_dyn_node_steps (the drop-in plugin's answer tables): at pod times across the
+    horizon — on breakpoints, one ns either side, both ends — the looked-up first-fail and
+    score equal the oracle's per-call answers for every node (plugins.go:39-98)."""
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, N, 4, seed=seed)
+    eng = engine_for(spec, c)
+    t0 = int(synth.NOW0_NS) - 7 * 10**9
+    t1 = t0 + horizon_s * 10**9
+    tab = eng.node_steps(t0, t1)
+    ns, bp = tab[0], tab[1]
+    assert (ns <= bp.shape[1]).all()
+    bps = np.unique(np.concatenate([bp[i, :ns[i]] for i in range(N)] + [np.array([t0], np.int64)]))
+    rng = np.random.default_rng(seed)
+    pick = rng.choice(bps, min(12, len(bps)), replace=False)
+    times = np.unique(np.concatenate([pick, pick - 1, pick + 1, [t0, t1 - 1]]))
+    times = times[(times >= t0) & (times < t1)]
+    off, osc, _ = oracle_soa(spec, c, now=times.astype(np.int64), ds=np.zeros(len(times), np.uint8))
+    for k, t in enumerate(times):
+        ff, sc = cd.Engine.table_lookup(tab, int(t))
+        assert np.array_equal(ff, off[k]) and np.array_equal(sc, osc[k]), int(t)
+    eng.close()
