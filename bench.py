@@ -144,7 +144,7 @@ def parse():
     ap.add_argument("--inflight", type=int, default=4,
                     help="independent pod batches in flight (engines x HIP streams); 1 = one batch at a time")
     ap.add_argument("--ar-group", type=int, default=0,
-                    help="N>1: batches per keys all-reduce (a multiple of --inflight; 0 = 8 x inflight)")
+                    help="N>1: batches per keys all-reduce (a multiple of --inflight; 0 = 16 x inflight)")
     ap.add_argument("--rehearse-collective", action="store_true",
                     help="run the N>1 collective path on one rank (under torchrun)")
     ap.add_argument("--no-extras", action="store_true", help="headline step only (matrix / drop-in / controller legs off)")
@@ -589,10 +589,10 @@ def main():
     sh_k = [s_.cuda_stream for s_ in streams]
     # N > 1: one RCCL max all-reduce per group of G batches over their keys [G][P], on its
     # own stream after the group's K streams (the collective's latency and host cost are
-    # per call; rehearsed on one rank: G = 4 / 8 / 16 / 32 -> 0.0272 / 0.0249 / 0.0175 /
-    # 0.0164 ms per batch against 0.0144 without the collective); two key buffers
+    # per call; rehearsed on one rank with the bound step calls: G = 32 / 64 / 128 -> 0.0175 /
+    # 0.0148 / 0.0148 ms per batch against 0.0130 without the collective); two key buffers
     # alternate so a group's batches never overwrite keys a collective still reads
-    G = max(K, args.ar_group or 8 * K) // K * K  # batches per collective, a multiple of K
+    G = max(K, args.ar_group or 16 * K) // K * K  # batches per collective, a multiple of K
     if coll:
         kbufs = [torch.empty((G, P), dtype=torch.int64, device=dev) for _ in range(2)]
         cstream = torch.cuda.Stream(dev)
@@ -609,17 +609,23 @@ def main():
         ev_ar[b].record(cstream)
         ar_done[b] = ev_ar[b]
 
+    # the step calls bound once to their engine, stream and key buffer (step_keys_fn: the
+    # pointer conversions happen here, a step in the timed loop pays only the C call)
+    step_own = [engs[j].step_keys_fn(d_now, d_flags, d_keys_k[j], sh_k[j]) for j in range(K)]
+    step_grp = ([[engs[r % K].step_keys_fn(d_now, d_flags, kbufs[b][r], sh_k[r % K]) for r in range(G)]
+                 for b in range(2)] if coll else None)
+
     def step(collective=True, i=0):
         j = i % K
         if coll and collective:
             b, row = (i // G) % 2, i % G
             if row < K and ar_done[b] is not None:  # this buffer's previous collective has read it
                 streams[j].wait_event(ar_done[b])
-            engs[j].step_keys_async(now_sync, now_sync, d_now, d_flags, kbufs[b][row], sh_k[j])
+            step_grp[b][row](now_sync, now_sync)
             if row == G - 1:
                 collect(b, G)
         else:
-            engs[j].step_keys_async(now_sync, now_sync, d_now, d_flags, d_keys_k[j], sh_k[j])
+            step_own[j](now_sync, now_sync)
 
     def flush(n_steps):  # the last, partial group's collective
         if coll and n_steps % G:

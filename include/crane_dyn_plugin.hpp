@@ -158,6 +158,15 @@ inline bool IsDaemonsetPod(const Pod& pod) {
     return false;
 }
 
+// FNV-1a over a node name (names are short; std::hash's murmur costs more per call)
+struct NameHash {
+    size_t operator()(const std::string& s) const {
+        uint64_t h = 1469598103934665603ull;
+        for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+        return (size_t)h;
+    }
+};
+
 // ---------------------------------------------------------------- plugin
 class DynamicScheduler {
    public:
@@ -194,17 +203,22 @@ class DynamicScheduler {
         return NewStatus(Code::Success, "");
     }
 
-    // Score (plugins.go:73-98)
+    // Score (plugins.go:73-98).  The node is looked up in the synced generation's index, which
+    // is the snapshot's node set; only a name outside it goes to the snapshot's own Get, for
+    // the reference's error (plugins.go:74-77).
     std::pair<int64_t, Status> Score(CycleState& state, const Pod& pod, const std::string& nodeName) {
         (void)pod;
         std::string err;
-        const Node* node = handle_.snapshot ? handle_.snapshot->Get(nodeName, &err) : nullptr;
-        if (!err.empty() || !handle_.snapshot)
-            return {0, NewStatus(Code::Error, "getting node \"" + nodeName + "\" from Snapshot: " + err)};
-        if (!node) return {0, NewStatus(Code::Error, "node not found")};
-        const Table* t;
-        int64_t idx;
-        if (!table_for(state, node, &t, &idx, &err)) return {0, NewStatus(Code::Error, err)};
+        const Table* t = table_of(state, &err);
+        const int64_t idx = t ? t->snap->find_name(nodeName) : -1;
+        if (idx < 0) {
+            const Node* node = handle_.snapshot ? handle_.snapshot->Get(nodeName, &err) : nullptr;
+            if (!err.empty() || !handle_.snapshot)
+                return {0, NewStatus(Code::Error, "getting node \"" + nodeName + "\" from Snapshot: " + err)};
+            if (!node) return {0, NewStatus(Code::Error, "node not found")};
+            if (!t) return {0, NewStatus(Code::Error, err)};
+            return {0, NewStatus(Code::Error, "node \"" + nodeName + "\" not in the synced snapshot")};
+        }
         return {(int64_t)t->score[t->piece(idx, state.now_ns)], Status()};
     }
 
@@ -230,7 +244,7 @@ class DynamicScheduler {
     // (a flat open-addressing table); a name lookup remains for any other Node object.
     struct Synced {
         uint64_t generation;
-        std::unordered_map<std::string, int64_t> index;
+        std::unordered_map<std::string, int64_t, NameHash> index;
         std::vector<const Node*> ptrs;                       // List() order
         std::vector<std::pair<const Node*, int64_t>> slots;  // power-of-two size, {nullptr, -1} empty
         int shift = 64;
@@ -258,6 +272,21 @@ class DynamicScheduler {
                     if (ptrs[(size_t)i] == p) return last = i;
             }
             const int64_t i = find_slow(p);
+            last_snap = this;
+            last = i;
+            return i;
+        }
+        // by name: the node after this thread's last one (or a few further) first, then the hash
+        int64_t find_name(const std::string& name) const {
+            thread_local const Synced* last_snap = nullptr;
+            thread_local int64_t last = -1;
+            if (last_snap == this) {
+                const int64_t n = (int64_t)ptrs.size();
+                for (int64_t i = last + 1; i < std::min(n, last + 5); ++i)
+                    if (ptrs[(size_t)i]->Name == name) return last = i;
+            }
+            auto it = index.find(name);
+            const int64_t i = it == index.end() ? -1 : it->second;
             last_snap = this;
             last = i;
             return i;
@@ -345,9 +374,8 @@ class DynamicScheduler {
         return synced_;
     }
 
-    // The table covering the cycle's time (fetched by the first caller of the cycle), and
-    // the node's index in it.
-    bool table_for(CycleState& state, const Node* node, const Table** table, int64_t* idx, std::string* err) {
+    // The table covering the cycle's time (fetched by the first caller of the cycle).
+    const Table* table_of(CycleState& state, std::string* err) {
         std::call_once(state.dyn_once_, [&] {
             std::string e;
             std::shared_ptr<const Table> t = table_at(state.now_ns, &e);
@@ -357,10 +385,14 @@ class DynamicScheduler {
             state.dyn_done_ = true;
         });
         const Table* t = static_cast<const Table*>(state.dyn_row_.get());
-        if (!t) {
-            *err = state.dyn_err_;
-            return false;
-        }
+        if (!t) *err = state.dyn_err_;
+        return t;
+    }
+
+    // ... and the node's index in it.
+    bool table_for(CycleState& state, const Node* node, const Table** table, int64_t* idx, std::string* err) {
+        const Table* t = table_of(state, err);
+        if (!t) return false;
         const int64_t i = t->snap->find(node);
         if (i < 0) {
             *err = "node \"" + node->Name + "\" not in the synced snapshot";

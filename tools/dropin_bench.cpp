@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <fstream>
 #include <functional>
@@ -34,14 +35,6 @@
 
 using namespace crane::dynamic;
 using Clock = std::chrono::steady_clock;
-
-struct NameHash {  // FNV-1a: node names are short
-    size_t operator()(const std::string& s) const {
-        uint64_t h = 1469598103934665603ull;
-        for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
-        return (size_t)h;
-    }
-};
 
 struct BenchSnap : Snapshot {
     std::vector<Node> nodes;
@@ -63,56 +56,67 @@ struct BenchSnap : Snapshot {
     uint64_t Generation() const override { return 1; }
 };
 
-// framework.Parallelizer().Until(ctx, n, f) on a fixed pool of workers that spin between
-// calls (goroutines wake in about a microsecond; a condition variable takes tens)
+// framework.Parallelizer().Until(ctx, n, f) on a fixed pool of workers
 class Pool {
    public:
     explicit Pool(int n) {
-        for (int i = 0; i < n - 1; ++i) th_.emplace_back([this] { loop(); });
+        for (int i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
     }
     ~Pool() {
-        stop_.store(true);
-        epoch_.fetch_add(1);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+            ++epoch_;
+        }
+        cv_.notify_all();
         for (auto& t : th_) t.join();
     }
     void until(int64_t n, const std::function<void(int64_t)>& f) {
-        f_ = &f;
-        n_ = n;
-        next_.store(0);
-        busy_.store((int)th_.size());
-        epoch_.fetch_add(1, std::memory_order_release);
-        work();  // the caller is one of the workers
-        while (busy_.load(std::memory_order_acquire) != 0) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            f_ = &f;
+            n_ = n;
+            next_ = 0;
+            busy_ = (int)th_.size();
+            ++epoch_;
         }
+        cv_.notify_all();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return busy_ == 0; });
     }
 
    private:
-    void work() {
-        for (;;) {  // chunks of 64 pieces, like the framework's chunked work queue
-            const int64_t i0 = next_.fetch_add(64);
-            if (i0 >= n_) break;
-            for (int64_t i = i0; i < std::min(n_, i0 + 64); ++i) (*f_)(i);
-        }
-    }
-    void loop() {
+    void loop(int) {
         uint64_t seen = 0;
         for (;;) {
-            uint64_t e;
-            while ((e = epoch_.load(std::memory_order_acquire)) == seen) {
+            const std::function<void(int64_t)>* f;
+            int64_t n;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return epoch_ != seen; });
+                seen = epoch_;
+                if (stop_) return;
+                f = f_;
+                n = n_;
             }
-            seen = e;
-            if (stop_.load()) return;
-            work();
-            busy_.fetch_sub(1, std::memory_order_acq_rel);
+            for (;;) {  // chunks of 64 pieces, like the framework's chunked work queue
+                const int64_t i0 = next_.fetch_add(64);
+                if (i0 >= n) break;
+                for (int64_t i = i0; i < std::min(n, i0 + 64); ++i) (*f)(i);
+            }
+            std::lock_guard<std::mutex> g(mu_);
+            if (--busy_ == 0) done_.notify_all();
         }
     }
     std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
     const std::function<void(int64_t)>* f_ = nullptr;
     int64_t n_ = 0;
     std::atomic<int64_t> next_{0};
-    std::atomic<int> busy_{0};
-    std::atomic<uint64_t> epoch_{0};
-    std::atomic<bool> stop_{false};
+    int busy_ = 0;
+    uint64_t epoch_ = 0;
+    bool stop_ = false;
 };
 
 #ifdef DROPIN_CPU
