@@ -379,9 +379,12 @@ def dropin_leg(cd, spec, ann, now, ds, ref_chosen, threads, cpu_pods=0):
                      "crane_dyn_node_steps, one table per 60 s of pod time)")
     o["breakdown"] = {"sync_ms": o.pop("sync_ms"), "filter_fanout_ms": o.pop("filter_fanout_ms_median"),
                       "score_fanout_ms": o.pop("score_fanout_ms_median"), "select_ms": o.pop("select_ms_median"),
+                      "harness_noop_fanouts_ms": o.pop("pool_noop_ms_median"),
                       "tables_built": o.pop("tables_built"),
                       "note": "sync = bulk parse + upload of the snapshot, once per generation; the first cycle "
-                              "also builds the answer table (cycle_ms_max)"}
+                              "also builds the answer table (cycle_ms_max); harness_noop_fanouts_ms = the same two "
+                              "fan-outs over no-op calls (the thread pool's own cost, measured before each cycle, "
+                              "not part of it)"}
     if rc is not None:
         if rc.returncode != 0:
             o["cpu_same_harness_error"] = rc.stderr[-300:]
@@ -392,6 +395,7 @@ def dropin_leg(cd, spec, ann, now, ds, ref_chosen, threads, cpu_pods=0):
             o["cpu_same_harness"] = {
                 "pods": oc["pods"], "threads": oc["threads"], "cycle_ms_median": oc["cycle_ms_median"],
                 "filter_fanout_ms": oc["filter_fanout_ms_median"], "score_fanout_ms": oc["score_fanout_ms_median"],
+                "harness_noop_fanouts_ms": oc["pool_noop_ms_median"],
                 "matches_engine_chosen": bool(np.array_equal(np.array(chc), np.asarray(ref_chosen)[:cpu_pods])),
                 "how": "same harness and thread pool; Filter / Score re-parse the node's annotations per call "
                        "like stats.go:51-76 (oracle string mode, oracle/_build/dropin_cpu)"}

@@ -201,12 +201,7 @@ __device__ __forceinline__ void bracket(const NodeRec<PD, PR>& r, int64_t t, int
 template <int BT = 256>
 __device__ __forceinline__ uint32_t wg_excl_scan_u32(uint32_t v, uint32_t* part) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
+    const uint32_t x = wave_scan_add(v);  // (DPP lane moves: every thread of the workgroup calls this)
     if (lane == 63) part[w] = x;
     __syncthreads();
     uint32_t pre = 0;

@@ -60,13 +60,26 @@ class Status {
    public:
     Status() = default;
     Status(Code c, std::string m) : code_(c), msg_(std::move(m)) {}
+    // the Filter's "Load[%s] of node[%s] is too high", formatted when read: a cycle's tens of
+    // thousands of Unschedulable answers are rarely read and need no allocation each
+    static Status Overloaded(const char* metric, const std::string* node) {
+        Status s(Code::Unschedulable, std::string());
+        s.metric_ = metric;
+        s.node_ = node;
+        return s;
+    }
     Code code() const { return code_; }
-    const std::string& message() const { return msg_; }
+    std::string message() const {
+        if (!metric_) return msg_;
+        return "Load[" + std::string(metric_) + "] of node[" + *node_ + "] is too high";
+    }
     bool IsSuccess() const { return code_ == Code::Success; }
 
    private:
     Code code_ = Code::Success;
     std::string msg_;
+    const char* metric_ = nullptr;     // (Overloaded: the policy's predicate name, lives with the plugin)
+    const std::string* node_ = nullptr;  // (the snapshot's node name, lives with the snapshot)
 };
 inline Status NewStatus(Code c, const std::string& m) { return Status(c, m); }
 
@@ -192,15 +205,8 @@ class DynamicScheduler {
         std::string err;
         if (!table_for(state, node, &t, &idx, &err)) return NewStatus(Code::Error, err);
         const int k = t->first_fail[t->piece(idx, state.now_ns)];
-        if (k >= 0) {  // "Load[%s] of node[%s] is too high", one allocation
-            const char* pn = policy().pred_name[k];
-            const size_t pl = std::strlen(pn);
-            std::string m;
-            m.reserve(5 + pl + 9 + node->Name.size() + 13);
-            m.append("Load[", 5).append(pn, pl).append("] of node[", 10).append(node->Name).append("] is too high", 13);
-            return NewStatus(Code::Unschedulable, std::move(m));
-        }
-        return NewStatus(Code::Success, "");
+        if (k >= 0) return Status::Overloaded(policy().pred_name[k], &node->Name);  // plugins.go:64
+        return Status();
     }
 
     // Score (plugins.go:73-98).  The node is looked up in the synced generation's index, which
