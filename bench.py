@@ -72,6 +72,12 @@ def src_hash():
     return h.hexdigest()[:12]
 
 
+def lib_hash():
+    """Hash of the engine library file this process loads (an A/B swap shows up here, not in src_hash)."""
+    p = os.path.join(ROOT, "crane-scheduler_amd", "lib", "libcrane_dyn.so")
+    return hashlib.sha256(open(p, "rb").read()).hexdigest()[:12] if os.path.exists(p) else None
+
+
 def pmc_summary(config, shash):
     """PMC summary of this config taken on these kernel sources (tools/gpu_pmc.sh), or None."""
     p = os.path.join(PMC_DIR, f"config{config}_{shash}.json")
@@ -550,7 +556,7 @@ def main():
     if args.leg == "cold":
         pmc_c, pmc_cs = pmc_summary("cold", shash)
         out = cold_leg(cd, synth, spec, dev, reps=max(2, args.steps), pmc=pmc_c, pmc_src=pmc_cs, opts=args.opt)
-        print(json.dumps({"leg": "cold", "src_hash": shash, **out}), flush=True)
+        print(json.dumps({"leg": "cold", "src_hash": shash, "lib_hash": lib_hash(), **out}), flush=True)
         return
     if args.leg != "all":
         stream = torch.cuda.Stream(dev)
@@ -562,7 +568,7 @@ def main():
         pmc_m, _ = pmc_summary("2" if cid == 2 else "3m", shash)
         out = matrix_leg(cd, spec, dev, stream, f"config{cid} full matrices", vm, tm, cm.hv, cm.hv_ts, cm.now, cm.ds,
                          args.steps, pmc_m)
-        print(json.dumps({"leg": args.leg, "src_hash": shash, **out}), flush=True)
+        print(json.dumps({"leg": args.leg, "src_hash": shash, "lib_hash": lib_hash(), **out}), flush=True)
         return
 
     strong = args.config == 4  # 1M nodes x 100k pods split over the ranks
@@ -901,6 +907,7 @@ def main():
             "roofline_kernels": roofs,
             "roofline_cold": roofline_cold,
             "src_hash": shash,
+            "lib_hash": lib_hash(),
             "cpu_baseline": cpu,
             "greedy": greedy,
             "host_parse": host_parse,

@@ -295,17 +295,19 @@ struct crane_tz {
         }
     }
 
-    // time.Date: the instant of the wall clock `local` (seconds, as if UTC) in this zone
+    // time.Date: the instant of the wall clock `local` (seconds, as if UTC) in this zone;
+    // go1.17 re-looks the zone up at start-1 (utc < start) or at end (utc >= end)
     int64_t date(int64_t local) const {
         int32_t off;
         int64_t start, end;
         lookup(local, &off, &start, &end);
         if (off != 0) {
             const int64_t utc = local - off;
-            if (utc < start || utc >= end) {
-                int64_t s2, e2;
-                lookup(utc, &off, &s2, &e2);
-            }
+            int64_t s2, e2;
+            if (utc < start)
+                lookup(start - 1, &off, &s2, &e2);
+            else if (utc >= end)
+                lookup(end, &off, &s2, &e2);
             local -= off;
         }
         return local;

@@ -291,12 +291,16 @@ class Location:
         return off, start, end
 
     def date(self, local):
-        """time.Date's instant (Unix seconds) of wall clock `local` (seconds, as if UTC)."""
+        """time.Date's instant (Unix seconds) of wall clock `local` (seconds, as if UTC):
+        go1.17 time.go Date re-looks the zone up at start-1 when utc < start, at end when
+        utc >= end (not at utc itself)."""
         off, start, end = self.lookup(local)
         if off != 0:
             utc = local - off
-            if utc < start or utc >= end:
-                off = self.lookup(utc)[0]
+            if utc < start:
+                off = self.lookup(start - 1)[0]
+            elif utc >= end:
+                off = self.lookup(end)[0]
             local -= off
         return local
 

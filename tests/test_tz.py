@@ -82,6 +82,35 @@ def test_transition_wall_times_as_go_chooses():
             assert z.date(local) == o.date(local)
 
 
+def _tzif(tx, idx, offs):
+    """A minimal version-2 TZif file (both data blocks, empty footer), abbreviation "ZZZ"."""
+    import struct
+
+    def block(tsize):
+        hdr = b"TZif2" + b"\0" * 15 + struct.pack(">6I", 0, 0, 0, len(tx), len(offs), 4)
+        body = b"".join(struct.pack(">q" if tsize == 8 else ">i", t) for t in tx) + bytes(idx)
+        body += b"".join(struct.pack(">iBB", o, 0, 0) for o in offs) + b"ZZZ\0"
+        return hdr + body
+    return block(4) + block(8) + b"\n\n"
+
+
+def test_date_close_transitions_looks_up_period_edge():
+    """go1.17 time.Date: when the wall time taken as UTC lands in a period whose offset puts
+    the instant before that period's start, the zone is looked up at start-1 (the period just
+    before), not at the instant itself.  Two transitions one hour apart make the two differ:
+    zones +0 (before 0), +1h on [0, 3600), +2h from 3600; wall 01:01:40 (3700 as UTC) ->
+    lookup(3700) = +2h, 3700 - 7200 < 3600 -> lookup(3599) = +1h -> 100 (lookup(-3500) would
+    give +0 -> 3700)."""
+    data = _tzif([0, 3600], [1, 2], [0, 3600, 7200])
+    z, o = cd.Zone(tzif=data), OT.Location(data)
+    assert o.date(3700) == z.date(3700) == 100
+    # and the symmetric edge: utc >= end -> lookup(end)
+    data = _tzif([0, 3600], [1, 2], [-7200, -3600, 0])
+    z, o = cd.Zone(tzif=data), OT.Location(data)
+    # lookup(-100) = -7200 (before 0), utc = 7100 >= end 0 -> lookup(0) = -3600 -> 3500
+    assert o.date(-100) == z.date(-100) == 3500
+
+
 def test_load_rules():
     """time.LoadLocation: "" and "UTC" are UTC, ".." and absolute names invalid, unknown
     names fail (the reference would then panic in ParseInLocation with a nil Location)."""

@@ -6,6 +6,8 @@ cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$1; shift; mkdir -p $O
 L=crane-scheduler_amd/lib/libcrane_dyn.so
 cp $L $O/orig.so
+# the product library comes back however the script ends (timeouts, signals, errors)
+trap 'cp $O/orig.so $L' EXIT
 for v in "$@"; do
   cp crane-scheduler_amd/lib_ab/lib_$v.so $L || { cp $O/orig.so $L; exit 1; }
   if [ -n "$AB_TESTS" ]; then  # parity of the variant first (e.g. AB_TESTS=tests/test_step_gpu.py)
