@@ -114,6 +114,11 @@ struct Options {
     int k2l_threads = 512;    // large K2: partition workgroup size at 4096-binding regions (512 or 1024)
     int sel_chain = 0;        // selection windows: 0 LDS rank/select walk when it fits, 1 streaming kernel
     int step_lds_cap = 1 << 30;  // K1: one-step records per kind staged in LDS at most (0: always st.stage)
+    int step_pieces = 0;      // middle pieces cut into elementary ones per block (step_pieces): 0 when the
+                              // producer blocks take more than 4 rounds of the CUs (there the producers'
+                              // extra latency overlaps other blocks'; in one round it is the kernel's
+                              // critical path: config 4 on one GPU K3s 0.118 -> 0.065 ms, K1 0.070 ->
+                              // 0.089; a config-4 shard, one round, got slower), 1 always, 2 never
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
@@ -196,6 +201,7 @@ struct crane_dyn {
     DevBuf<Step1> sstage;  // K1's one-step staging past its LDS (StepTables::stage)
     DevBuf<int32_t> spm1, ssm0;   // prefix / suffix key maxima of the sorted Step1 records
     DevBuf<int4> srows;           // per (pod tile, producer block): uniform keys + record ranges
+    DevBuf<int2> sprow;           // ... and middle-piece ranges
     // asynchronous work enqueued on caller streams: one completion event per stream,
     // re-recorded by each *_async call; calls that replace engine state wait for all of them
     std::vector<std::pair<hipStream_t, hipEvent_t>> busy;
@@ -500,6 +506,8 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     t.single = h->sstep1.p;
     t.stage = sp.fuse ? h->sstage.p : nullptr;
     t.lds_cap = h->opt.step_lds_cap;
+    const bool pieces = h->opt.step_pieces == 1 || (h->opt.step_pieces == 0 && nblk > 4 * h->n_cu);
+    t.piece_work = pieces ? 256 : INT32_MAX;
     t.pm1 = h->spm1.p;
     t.sm0 = h->ssm0.p;
     t.mid = h->smid.p;
@@ -513,7 +521,9 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     const int64_t nrows = g.ntiles * (int64_t)nblk;
     if (h->opt.step_rows && nrows <= kStepRowsMax) {
         HIPTRY(h, h->srows.reserve((size_t)std::max<int64_t>(nrows, 1)));
+        HIPTRY(h, h->sprow.reserve((size_t)std::max<int64_t>(nrows, 1)));
         t.rows = h->srows.p;
+        t.prow = h->sprow.p;
     }
     t.trace = g.ngroups * g.R <= kTraceWgs ? h->trace_region(2) : nullptr;
     return CRANE_OK;
@@ -695,7 +705,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->mFs.release(); h->mIs.release(); h->mgi.release();
     h->trace.release();
     h->sperm.release(); h->scnt.release(); h->stile.release(); h->sbatch.release(); h->sq.release(); h->sqm.release(); h->snq.release(); h->spnow.release(); h->smid.release(); h->sstep1.release(); h->sstage.release();
-    h->spm1.release(); h->ssm0.release(); h->srows.release();
+    h->spm1.release(); h->ssm0.release(); h->srows.release(); h->sprow.release();
     h->sel_fth.release(); h->sel_win.release(); h->sel_state.release(); h->sel_keys.release();
     h->stp_dev.release(); h->stp_host.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -735,6 +745,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "k2l_co_t" && range(0, 1)) o.k2l_co_t = (int)value;
     else if (n == "k2l_threads" && (value == 512 || value == 1024)) o.k2l_threads = (int)value;
     else if (n == "sel_chain" && range(0, 1)) o.sel_chain = (int)value;
+    else if (n == "step_pieces" && range(0, 2)) o.step_pieces = (int)value;
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
@@ -775,8 +786,9 @@ int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const d
     if ((hv == nullptr) != (hv_ts == nullptr)) return h->fail(CRANE_E_INVALID, "hv and hv_ts must both be set or NULL");
     HIPTRY(h, hipSetDevice(h->device));
     if (int rc = quiesce(h)) return rc;
-    HIPTRY(h, h->val.reserve((size_t)(M * n)));
-    HIPTRY(h, h->ts.reserve((size_t)(M * n)));
+    // (at least one row: the node pass issues its SoA loads unconditionally)
+    HIPTRY(h, h->val.reserve((size_t)(std::max<int64_t>(M, 1) * n)));
+    HIPTRY(h, h->ts.reserve((size_t)(std::max<int64_t>(M, 1) * n)));
     HIPTRY(h, h->hv.reserve((size_t)n));
     HIPTRY(h, h->hv_ts.reserve((size_t)n));
     HIPTRY(h, h->rec.reserve((size_t)n * h->rec_bytes));

@@ -43,6 +43,10 @@ inline hipError_t klaunch(const char* name, void (*kernel)(KArgs...), dim3 grid,
         }                                                                                            \
     } while (0)
 
+// Word 3 of a raw buffer resource on gfx9 (gfx950): 32-bit data format.  A resource with
+// num_records 0 makes every load through it return 0 (the branch-free optional source).
+constexpr int32_t kBufRsrcW3 = 0x00020000;
+
 struct HotCutoffs {
     int32_t n_win;
     int32_t pad;
@@ -242,11 +246,17 @@ struct StepTables {
     // {uniform key kind 0, kind 1, jl0 | jh0 << 16, jl1 | jh1 << 16}; [jl, jh) = the
     // block's sorted one-step records stepping inside the tile's range of that kind
     int4* rows;
+    // with rows, per (tile t, block b) at prow[t * nblk + b]: {pl0 | ph0 << 16, pl1 | ph1 << 16},
+    // the block's middle pieces [pl, ph) of that kind overlapping the tile's range (0: none)
+    int2* prow;
     unsigned long long* trace;  // K3s phase trace or null
     // K1's one-step staging for blocks with more records of a kind than its LDS holds
     // (or than lds_cap, 0 = always): same indexing as single
     Step1* stage;
     int32_t lds_cap;
+    // middle pieces x pod tiles from which a producer cuts a kind's pieces into elementary
+    // ones (step_pieces), INT32_MAX = never
+    int32_t piece_work;
 };
 constexpr int64_t kStepRowsMax = 1LL << 24;  // tile x block rows (256 MiB); larger batches: K3s searches
 __host__ __device__ inline int64_t s1_at(const StepTables& st, int T, int64_t b) {

@@ -74,7 +74,11 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
     if (st.rows) {
         int64_t pre;
         tile_prefetch(st, &pre);
-        step_tile_rows<kStepSeg>(s1l, s1s, sh, st, blockIdx.x, &pre);
+        // middle pieces' scratch: s1l past the prefix / suffix maxima ([2][2 * kStepSeg] int32 each)
+        const PieceScr ps{reinterpret_cast<unsigned char*>(s1l) + 32 * kStepSeg,
+                          ((int)sizeof(s1l) - 32 * kStepSeg) / PieceScr::bytes_per_piece & ~3};
+        step_pieces<kStepSeg>(sh, st, blockIdx.x, ps);
+        step_tile_rows<kStepSeg>(s1l, s1s, sh, st, blockIdx.x, &pre, ps);
     }
 }
 
@@ -185,6 +189,7 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     // and its LDS sets how many share a CU
     __shared__ int32_t wpre[4 * kK3sListBlk + 1];
     __shared__ int32_t wjl[2 * kK3sListBlk];
+    __shared__ int32_t wpl[2 * kK3sListBlk];  // the first middle piece per (block, kind)
     const int64_t b = blockIdx.x;
     CRANE_TSTAMP(st.trace, b, 0);
     const int32_t r = (int32_t)(b % R);
@@ -227,9 +232,13 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     // this slice's loads first (counts, the tile rows), then the pods, so they overlap
     int4 c = make_int4(0, 0, 0, 0);  // [records kind 0, pieces 0, records 1, pieces 1]
     int4 row = make_int4(-1, -1, 0, 0);
+    int2 prow = make_int2(0, 0);
     if (own) {
         c = reinterpret_cast<const int4*>(st.cnt)[ob];
-        if (st.rows) row = st.rows[grp * st.nblk + ob];
+        if (st.rows) {
+            row = st.rows[grp * st.nblk + ob];
+            prow = st.prow[grp * st.nblk + ob];
+        }
     }
     bool live[kK3sPPL], ds[kK3sPPL];
     int32_t pod[kK3sPPL];
@@ -246,7 +255,12 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     for (int i = threadIdx.x; i < 2 * kK3sPods; i += kK3sThreads) tree[i] = -1;
     if (threadIdx.x < 2) umax[threadIdx.x] = -1;
     CRANE_TSTAMP(st.trace, b, 5);  // (pods in: the LDS stores waited for them)
-    const int32_t n1[2] = {any[0] ? c.x : 0, any[1] ? c.z : 0}, nm[2] = {any[0] ? c.y : 0, any[1] ? c.w : 0};
+    const int32_t n1[2] = {any[0] ? c.x : 0, any[1] ? c.z : 0};
+    // middle pieces [pl, pl + nm) per kind: with rows, those overlapping the tile (the producer's
+    // elementary pieces, step_pieces), else all of them
+    const int32_t pl[2] = {st.rows ? prow.x & 0xFFFF : 0, st.rows ? prow.y & 0xFFFF : 0};
+    const int32_t nm[2] = {any[0] ? (st.rows ? (prow.x >> 16) - pl[0] : c.y) : 0,
+                           any[1] ? (st.rows ? (prow.y >> 16) - pl[1] : c.w) : 0};
     const Step1* base[2] = {st.single + s1_at(st, 0, ob), st.single + s1_at(st, 1, ob)};
     int32_t jj[4] = {0, 0, 0, 0};  // jl[0], jh[0], jl[1], jh[1]
     int32_t um[2] = {-1, -1};
@@ -287,6 +301,8 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         wpre[2 * m + 2 * j + 1] = nm[1];
         wjl[2 * j] = jj[0];
         wjl[2 * j + 1] = jj[2];
+        wpl[2 * j] = pl[0];
+        wpl[2 * j + 1] = pl[1];
     }
     __syncthreads();  // tt, tree, umax initialised; the counts in
     CRANE_TSTAMP(st.trace, b, 1);
@@ -335,7 +351,7 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
         } else {
             // a middle piece: covering -> uniform, overlapping partly -> range maximum over
             // the slots with s <= now < e
-            const Mid pm = st.mid[(int64_t)T * st.mpad + obj * st.mstride + idx];
+            const Mid pm = st.mid[(int64_t)T * st.mpad + obj * st.mstride + wpl[ej] + idx];
             if (pm.s <= tlo[T] && pm.e > thi[T]) um[T] = max(um[T], pm.key);
             else if (pm.s <= thi[T] && pm.e > tlo[T]) {
                 tree_max(tree, slot_lower(tt, klo[T], khi[T], pm.s), slot_lower(tt, klo[T], khi[T], pm.e), pm.key);
@@ -360,7 +376,7 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     if (own && !piece_list) {
 #pragma unroll
         for (int T = 0; T < 2; ++T) {
-            const Mid* mp = st.mid + (int64_t)T * st.mpad + ob * st.mstride;
+            const Mid* mp = st.mid + (int64_t)T * st.mpad + ob * st.mstride + pl[T];
             for (int32_t i0 = sub; i0 < nm[T]; i0 += 4 * lpb) {
                 Mid q[4];
 #pragma unroll

@@ -242,6 +242,7 @@ struct StepSlots {
 struct StepShared {
     int32_t lc[2][2];   // per kind: [one-step records, middle pieces]
     int32_t fm[2][16];  // per-wave flat maxima (<= 1024 threads)
+    int32_t pn[2];      // per kind: elementary pieces after step_pieces, -1 = raw pieces
 };
 
 // Phase 1.  A node with one distinct in-range expiry (a predicate's expiry
@@ -632,9 +633,114 @@ __device__ __forceinline__ void step_sort_publish_global(const StepShared& sh, c
     }
 }
 
+// ---- middle pieces -> disjoint elementary pieces (per block and kind, after the emit)
+// A kind's raw middle pieces [s, e) (every multi-step node's: they overlap across nodes)
+// are cut at every piece end into disjoint intervals, each carrying the max key of the
+// pieces covering it; intervals no feasible piece covers are dropped.  At any time the
+// max over the raw pieces containing it is the key of the one elementary piece containing
+// it, so a pod tile needs only the pieces its time range overlaps — a contiguous range
+// [pl, ph) of the sorted list (step_tile_rows writes it to st.prow; one covering the whole
+// range goes into the row's uniform key) — instead of every piece of the block once per
+// tile (config 4: ~32 pieces per kind and block, 98 tiles).  The list replaces the raw
+// one in st.mid (and its count in st.cnt).  Kinds with more than the scratch holds, or too
+// little work to pay for it (pieces x tiles < st.piece_work), stay raw: their row range is
+// all pieces.
+// LDS scratch per kind (pc pieces at most): sorted breakpoints bs[2pc] (i64), unsorted
+// bu[2pc] (i64: s, e of piece k at 2k, 2k + 1), maxima vm[2pc] (of the interval from each
+// sorted breakpoint to the next), compacted positions ix[2pc], raw keys rk[pc] (i32):
+// 52 * pc bytes.
+struct PieceScr {
+    unsigned char* p;
+    int32_t pc;  // pieces per kind the scratch holds (0: never decompose)
+    __device__ int64_t* bs(int T) const { return reinterpret_cast<int64_t*>(p + (int64_t)T * 52 * pc); }
+    __device__ int64_t* bu(int T) const { return reinterpret_cast<int64_t*>(p + (int64_t)T * 52 * pc + 16 * pc); }
+    __device__ int32_t* vm(int T) const { return reinterpret_cast<int32_t*>(p + (int64_t)T * 52 * pc + 32 * pc); }
+    __device__ int32_t* ix(int T) const { return reinterpret_cast<int32_t*>(p + (int64_t)T * 52 * pc + 40 * pc); }
+    __device__ int32_t* rk(int T) const { return reinterpret_cast<int32_t*>(p + (int64_t)T * 52 * pc + 48 * pc); }
+    static constexpr int bytes_per_piece = 2 * 52;  // both kinds
+};
+// Every thread calls it (barriers when a kind is decomposed); sh.lc final and the emit's
+// pieces in st.mid (a barrier after the emit).  Sets sh.pn (read after the next barrier).
+template <int BS>
+__device__ __forceinline__ void step_pieces(StepShared& sh, const StepTables& st, int64_t blk, const PieceScr& ps) {
+    static_assert(BS >= 128, "two waves compact the two kinds");
+    const int32_t nm0 = sh.lc[0][1], nm1 = sh.lc[1][1];
+    auto dec = [&](int32_t nm) { return nm >= 2 && nm <= ps.pc && (int64_t)nm * st.ntiles >= st.piece_work; };
+    const bool d0 = dec(nm0), d1 = dec(nm1);
+    if (!d0 && !d1) {  // (workgroup-uniform)
+        if (threadIdx.x < 2) sh.pn[threadIdx.x] = -1;
+        return;
+    }
+    const int32_t a0 = d0 ? nm0 : 0, a1 = d1 ? nm1 : 0;  // pieces taken per kind
+    // A: the raw pieces into LDS
+    for (int i = threadIdx.x; i < a0 + a1; i += BS) {
+        const int T = i >= a0, k = T ? i - a0 : i;
+        const Mid m = st.mid[(int64_t)T * st.mpad + blk * st.mstride + k];
+        ps.bu(T)[2 * k] = m.s;
+        ps.bu(T)[2 * k + 1] = m.e;
+        ps.rk(T)[k] = m.key;
+    }
+    __syncthreads();
+    // B: every breakpoint v (s or e of a piece) in one pass over its kind's pieces: its
+    // rank among the breakpoints (ties by index: its position in the sorted order) and the
+    // max key of the feasible pieces covering [v, next breakpoint), i.e. with s <= v < e
+    // (broadcast LDS reads, no atomics: equal breakpoints get equal maxima)
+    for (int i = threadIdx.x; i < 2 * (a0 + a1); i += BS) {
+        const int T = i >= 2 * a0, j = T ? i - 2 * a0 : i, n = T ? a1 : a0;
+        const int64_t* b = ps.bu(T);
+        const int32_t* rk = ps.rk(T);
+        const int64_t v = b[j];
+        int32_t r = 0, m = -1;
+        for (int k = 0; k < n; ++k) {
+            const int64_t s = b[2 * k], e = b[2 * k + 1];
+            r += (s < v) || (s == v && 2 * k < j);
+            r += (e < v) || (e == v && 2 * k + 1 < j);
+            if (s <= v && v < e) m = max(m, rk[k]);
+        }
+        ps.bs(T)[r] = v;
+        ps.vm(T)[r] = m;
+    }
+    __syncthreads();
+    // D: wave T compacts kind T's non-empty covered intervals (in order) and publishes them
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w < 2) {
+        const int T = w;
+        const int32_t n = 2 * (T ? a1 : a0);
+        if ((T ? d1 : d0)) {
+            const int64_t* bs = ps.bs(T);
+            const int32_t* vm = ps.vm(T);
+            Mid* out = st.mid + (int64_t)T * st.mpad + blk * st.mstride;
+            uint32_t carry = 0;
+            for (int32_t c0 = 0; c0 < n - 1; c0 += 64) {
+                const int32_t j = c0 + lane;
+                const bool f = j < n - 1 && bs[j] < bs[j + 1] && vm[j] >= 0;
+                const uint32_t inc = wave_scan_add(f ? 1u : 0u);
+                if (f) {
+                    const int32_t pos = (int32_t)(carry + inc - 1);
+                    ps.ix(T)[pos] = j;
+                    Mid m;
+                    m.s = bs[j];
+                    m.e = bs[j + 1];
+                    m.key = vm[j];
+                    m.pad = 0;
+                    out[pos] = m;
+                }
+                carry += __builtin_amdgcn_readlane(inc, 63);
+            }
+            if (lane == 0) {
+                sh.pn[T] = (int32_t)carry;
+                st.cnt[blk * 4 + 2 * T + 1] = (int32_t)carry;
+            }
+        } else if (lane == 0) {
+            sh.pn[T] = -1;
+        }
+    }
+}
+
 // The tile rows (st.rows set): per pod tile t, the block's uniform key per kind and
 // the range [jl, jh) of its sorted one-step records stepping inside the tile's range
-// (after step_sort_publish: srt sorted, s1l holding the prefix / suffix maxima).
+// (after step_sort_publish: srt sorted, s1l holding the prefix / suffix maxima), and
+// (st.prow) the range [pl, ph) of its middle pieces overlapping it (step_pieces).
 // pre: this thread's first item's bound (tile_prefetch, loaded early).  Every thread
 // calls it (barrier).
 __device__ __forceinline__ void tile_prefetch(const StepTables& st, int64_t* pre) {
@@ -645,7 +751,8 @@ __device__ __forceinline__ void tile_prefetch(const StepTables& st, int64_t* pre
 // searches read st.single / pm1 / sm0 instead of the LDS copies.
 template <int BS, int CAP = 2 * BS, bool G = false>
 __device__ __forceinline__ void step_tile_rows(const Step1* s1l, const Step1* srt, const StepShared& sh,
-                                               const StepTables& st, int64_t blk, const int64_t* pre) {
+                                               const StepTables& st, int64_t blk, const int64_t* pre,
+                                               const PieceScr& ps) {
     const int n0 = sh.lc[0][0], n1 = sh.lc[1][0];
     const int32_t* pmL = reinterpret_cast<const int32_t*>(s1l);
     const int32_t* smL = pmL + 2 * CAP;
@@ -663,9 +770,11 @@ __device__ __forceinline__ void step_tile_rows(const Step1* s1l, const Step1* sr
         const int i = i0 + threadIdx.x;
         const int t = i >> 2, T = (i >> 1) & 1, hi_b = i & 1;
         const int n = T ? n1 : n0;
-        int32_t c = 0, u = -1;
+        const int32_t pn = sh.pn[T];
+        int32_t c = 0, u = -1, pc = 0;
+        int64_t v = 0;
         if (t < st.ntiles) {
-            const int64_t v = i0 == 0 ? *pre : st.tiles[kTileStat * t + 2 * T + hi_b];
+            v = i0 == 0 ? *pre : st.tiles[kTileStat * t + 2 * T + hi_b];
             if (G) {
                 const int64_t base = s1_at(st, T, blk);
                 c = count_le(st.single + base, n, v);
@@ -676,13 +785,44 @@ __device__ __forceinline__ void step_tile_rows(const Step1* s1l, const Step1* sr
                 if (!hi_b && c > 0) u = pmL[T * CAP + c - 1];  // records stepped by lo: keys after
                 if (hi_b && c < n) u = smL[T * CAP + c];       // records stepping after hi: keys before
             }
+            // middle pieces: elementary ones ending by lo (pl) / starting by hi (ph); raw: all
+            if (pn >= 0) {
+                const int64_t* bs = ps.bs(T);
+                const int32_t* ix = ps.ix(T);
+                int32_t lo = 0, hi = pn;
+                while (lo < hi) {
+                    const int32_t mid = (lo + hi) >> 1;
+                    if (bs[ix[mid] + (hi_b ? 0 : 1)] <= v) lo = mid + 1;
+                    else hi = mid;
+                }
+                pc = lo;
+            } else {
+                pc = hi_b ? sh.lc[T][1] : 0;
+            }
         }
-        const int32_t co = quad_xor1(c), uo = quad_xor1(u);
+        const int32_t co = quad_xor1(c), uo = quad_xor1(u), pco = quad_xor1(pc);
+        const int64_t vo = (int64_t)(((uint64_t)(uint32_t)quad_xor1((int32_t)((uint64_t)v >> 32)) << 32) |
+                                     (uint32_t)quad_xor1((int32_t)(uint32_t)v));
         const int32_t jl = hi_b ? co : c, jh = hi_b ? c : co;
+        int32_t pl = hi_b ? pco : pc;
+        const int32_t ph = hi_b ? pc : pco;
+        int32_t ukey = -1;
+        if (pn >= 0 && ph - pl == 1 && t < st.ntiles) {  // one elementary piece: uniform if it covers [lo, hi]
+            const int64_t lo_v = hi_b ? vo : v, hi_v = hi_b ? v : vo;
+            const int32_t j = ps.ix(T)[pl];
+            if (ps.bs(T)[j] <= lo_v && ps.bs(T)[j + 1] > hi_v) {
+                ukey = ps.vm(T)[j];
+                pl = ph;
+            }
+        }
         // a kind without pods here (lo = INT64_MAX, hi = INT64_MIN) gives jl = n > jh = 0
-        const int32_t um = jl > jh ? -1 : max(fl[T], max(u, uo)), jp = jl > jh ? 0 : (jl | (jh << 16));
-        const int32_t um1 = quad_down2(um), jp1 = quad_down2(jp);
-        if ((i & 3) == 0 && t < st.ntiles) st.rows[(int64_t)t * st.nblk + blk] = make_int4(um, um1, jp, jp1);
+        const int32_t um = jl > jh ? -1 : max(max(fl[T], ukey), max(u, uo)), jp = jl > jh ? 0 : (jl | (jh << 16));
+        const int32_t pp = pl < ph ? (pl | (ph << 16)) : 0;
+        const int32_t um1 = quad_down2(um), jp1 = quad_down2(jp), pp1 = quad_down2(pp);
+        if ((i & 3) == 0 && t < st.ntiles) {
+            st.rows[(int64_t)t * st.nblk + blk] = make_int4(um, um1, jp, jp1);
+            st.prow[(int64_t)t * st.nblk + blk] = make_int2(pp, pp1);
+        }
     }
 }
 

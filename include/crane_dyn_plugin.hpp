@@ -246,15 +246,17 @@ class DynamicScheduler {
 
    private:
     // one synced snapshot generation: node -> engine index (immutable once published).  The
-    // framework hands Filter the snapshot's own Node objects, so their address is the key
-    // (a flat open-addressing table); a name lookup remains for any other Node object.
+    // framework hands Filter the snapshot's own Node objects and Score their Name strings, so
+    // the address of a node's Name field is the key of both (a flat open-addressing table: an
+    // address equal to a synced node's &Name is that node's name); a name lookup remains for
+    // any other object.
     struct Synced {
         uint64_t generation;
         std::unordered_map<std::string, int64_t, NameHash> index;
-        std::vector<const Node*> ptrs;                       // List() order
-        std::vector<std::pair<const Node*, int64_t>> slots;  // power-of-two size, {nullptr, -1} empty
+        std::vector<const Node*> ptrs;                              // List() order
+        std::vector<std::pair<const std::string*, int64_t>> slots;  // power-of-two size, {nullptr, -1} empty
         int shift = 64;
-        static uint64_t mix(const Node* p) { return ((uint64_t)(uintptr_t)p >> 4) * 0x9E3779B97F4A7C15ull; }
+        static uint64_t mix(const std::string* p) { return ((uint64_t)(uintptr_t)p >> 4) * 0x9E3779B97F4A7C15ull; }
         void build(const std::vector<const Node*>& nodes) {
             ptrs = nodes;
             size_t cap = 16;
@@ -262,50 +264,39 @@ class DynamicScheduler {
             shift = 64 - __builtin_ctzll(cap);
             slots.assign(cap, {nullptr, -1});
             for (size_t i = 0; i < nodes.size(); ++i) {
-                size_t h = (size_t)(mix(nodes[i]) >> shift);
-                while (slots[h].first && slots[h].first != nodes[i]) h = (h + 1) & (cap - 1);
-                slots[h] = {nodes[i], (int64_t)i};
+                const std::string* k = &nodes[i]->Name;
+                size_t h = (size_t)(mix(k) >> shift);
+                while (slots[h].first && slots[h].first != k) h = (h + 1) & (cap - 1);
+                slots[h] = {k, (int64_t)i};
             }
         }
-        int64_t find(const Node* p) const {
-            // the framework walks the nodes in List() order in chunks per goroutine: the node
-            // after this thread's last one (or a few further, for the feasible list) first
+        int64_t find(const Node* p) const { return find_key(&p->Name); }
+        int64_t find_name(const std::string& name) const { return find_key(&name); }
+        // the framework walks the nodes in List() order in chunks per goroutine: the node after
+        // this thread's last one (or a few further, for the feasible list) first — a pointer
+        // compare, no load of the node — then the table, then the name
+        int64_t find_key(const std::string* k) const {
             thread_local const Synced* last_snap = nullptr;
             thread_local int64_t last = -1;
             if (last_snap == this) {
                 const int64_t n = (int64_t)ptrs.size();
                 for (int64_t i = last + 1; i < std::min(n, last + 5); ++i)
-                    if (ptrs[(size_t)i] == p) return last = i;
+                    if (&ptrs[(size_t)i]->Name == k) return last = i;
             }
-            const int64_t i = find_slow(p);
+            const int64_t i = find_slow(k);
             last_snap = this;
             last = i;
             return i;
         }
-        // by name: the node after this thread's last one (or a few further) first, then the hash
-        int64_t find_name(const std::string& name) const {
-            thread_local const Synced* last_snap = nullptr;
-            thread_local int64_t last = -1;
-            if (last_snap == this) {
-                const int64_t n = (int64_t)ptrs.size();
-                for (int64_t i = last + 1; i < std::min(n, last + 5); ++i)
-                    if (ptrs[(size_t)i]->Name == name) return last = i;
-            }
-            auto it = index.find(name);
-            const int64_t i = it == index.end() ? -1 : it->second;
-            last_snap = this;
-            last = i;
-            return i;
-        }
-        int64_t find_slow(const Node* p) const {
-            size_t h = (size_t)(mix(p) >> shift);
+        int64_t find_slow(const std::string* k) const {
+            size_t h = (size_t)(mix(k) >> shift);
             for (;;) {
                 const auto& s = slots[h];
-                if (s.first == p) return s.second;
+                if (s.first == k) return s.second;
                 if (!s.first) break;
                 h = (h + 1) & (slots.size() - 1);
             }
-            auto it = index.find(p->Name);
+            auto it = index.find(*k);
             return it == index.end() ? -1 : it->second;
         }
     };

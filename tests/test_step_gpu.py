@@ -26,14 +26,15 @@ def _check(spec, c, now, ds):
     # one-step records through its LDS staging, through st.stage always (cap 0), or
     # per block as its counts exceed a small cap; the node pass fused with the step
     # tables (split 0) or as the split form (count pass + k3a_emit, split 1)
-    for rows, cap, split in ((1, 1 << 30, 0), (0, 1 << 30, 0), (1, 0, 0), (0, 6, 0), (1, 6, 0),
-                             (1, 1 << 30, 1), (0, 6, 1), (1, 0, 1)):
-        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap, "k1_split": split})
+    # the middle pieces raw or cut into elementary ones (step_pieces 1: whenever it pays)
+    for rows, cap, split, pc in ((1, 1 << 30, 0, 0), (0, 1 << 30, 0, 0), (1, 0, 0, 1), (0, 6, 0, 0), (1, 6, 0, 1),
+                                 (1, 1 << 30, 1, 1), (0, 6, 1, 0), (1, 0, 1, 2), (1, 1 << 30, 0, 1)):
+        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap, "k1_split": split, "step_pieces": pc})
         _, _, ch, cs = eng.eval(now, ds)
-        assert np.array_equal(ch, och), (rows, cap, split)
+        assert np.array_equal(ch, och), (rows, cap, split, pc)
         for p in range(len(now)):
             ok = (off[p] < 0) | bool(ds[p])
-            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, split, p)
+            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, split, pc, p)
         eng.close()
 
 
@@ -45,6 +46,8 @@ def _check(spec, c, now, ds):
     (3000, 700, 1_700_000_000, 0.05, 5),   # 20-minute batch: almost every node steps
     (20000, 2100, 0, 0.01, 6),             # one `now` for the whole batch: every node flat
     (1000, 300, 60_000_000_000, 1.0, 7),   # all DaemonSet pods
+    (6000, 9000, 20_000_000, 0.02, 8),     # 180 s over 9 tiles: middle pieces cut into elementary ones
+    (3000, 5000, 200_000_000, 0.3, 9),     # 1000 s: some blocks past the pieces' LDS scratch (raw)
 ])
 def test_step_random_vs_oracle(n_nodes, n_pods, step_ns, ds_frac, seed):
     spec = cd.default_policy_spec()
@@ -104,6 +107,10 @@ def test_step_policy_shapes():
     specs.append(s)
     for i, spec in enumerate(specs):
         c = synth.make_cluster(spec, 777, 90, seed=200 + i, pod_step_ns=20_000_000_000, ds_frac=0.1)
+        _check(spec, c, c.now, c.ds)
+    # many tiles and a wide batch: the shapes' middle pieces go through step_pieces
+    for i, spec in enumerate(specs[:2]):
+        c = synth.make_cluster(spec, 1500, 4100, seed=210 + i, pod_step_ns=60_000_000, ds_frac=0.1)
         _check(spec, c, c.now, c.ds)
 
 
