@@ -118,7 +118,9 @@ struct Options {
                               // producer blocks take more than 4 rounds of the CUs (there the producers'
                               // extra latency overlaps other blocks'; in one round it is the kernel's
                               // critical path: config 4 on one GPU K3s 0.118 -> 0.065 ms, K1 0.070 ->
-                              // 0.089; a config-4 shard, one round, got slower), 1 always, 2 never
+                              // 0.089; a config-4 shard, one round, got slower) and the batch has
+                              // >= kPieceMinTiles pod tiles (a piece is re-read once per tile), 1 always,
+                              // 2 never (then no per-tile piece ranges either: K3s reads all pieces)
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
@@ -506,7 +508,8 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     t.single = h->sstep1.p;
     t.stage = sp.fuse ? h->sstage.p : nullptr;
     t.lds_cap = h->opt.step_lds_cap;
-    const bool pieces = h->opt.step_pieces == 1 || (h->opt.step_pieces == 0 && nblk > 4 * h->n_cu);
+    const bool pieces = h->opt.step_pieces == 1 ||
+                        (h->opt.step_pieces == 0 && nblk > 4 * h->n_cu && g.ntiles >= kPieceMinTiles);
     t.piece_work = pieces ? 256 : INT32_MAX;
     t.pm1 = h->spm1.p;
     t.sm0 = h->ssm0.p;
@@ -521,9 +524,11 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     const int64_t nrows = g.ntiles * (int64_t)nblk;
     if (h->opt.step_rows && nrows <= kStepRowsMax) {
         HIPTRY(h, h->srows.reserve((size_t)std::max<int64_t>(nrows, 1)));
-        HIPTRY(h, h->sprow.reserve((size_t)std::max<int64_t>(nrows, 1)));
         t.rows = h->srows.p;
-        t.prow = h->sprow.p;
+        if (pieces) {
+            HIPTRY(h, h->sprow.reserve((size_t)std::max<int64_t>(nrows, 1)));
+            t.prow = h->sprow.p;
+        }
     }
     t.trace = g.ngroups * g.R <= kTraceWgs ? h->trace_region(2) : nullptr;
     return CRANE_OK;
@@ -786,9 +791,8 @@ int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const d
     if ((hv == nullptr) != (hv_ts == nullptr)) return h->fail(CRANE_E_INVALID, "hv and hv_ts must both be set or NULL");
     HIPTRY(h, hipSetDevice(h->device));
     if (int rc = quiesce(h)) return rc;
-    // (at least one row: the node pass issues its SoA loads unconditionally)
-    HIPTRY(h, h->val.reserve((size_t)(std::max<int64_t>(M, 1) * n)));
-    HIPTRY(h, h->ts.reserve((size_t)(std::max<int64_t>(M, 1) * n)));
+    HIPTRY(h, h->val.reserve((size_t)(M * n)));
+    HIPTRY(h, h->ts.reserve((size_t)(M * n)));
     HIPTRY(h, h->hv.reserve((size_t)n));
     HIPTRY(h, h->hv_ts.reserve((size_t)n));
     HIPTRY(h, h->rec.reserve((size_t)n * h->rec_bytes));

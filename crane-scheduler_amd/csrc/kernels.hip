@@ -170,60 +170,72 @@ void k1_node_pass(K1Args a, K1Step step) {
     uint32_t bc[kMaxWin];
     double hvl = 0.0;
     int64_t hvt = kTsInvalid;
-    // dedupe-form K2: the count/offset words of this block's first source regions go
-    // out first, so the dependent entry loads below wait on them and the SoA stream
+    // dedupe-form K2: the count/offset words of this block's first source
+    // regions go out before the SoA loads, so the dependent entry loads below
+    // wait on them, not on the whole SoA batch
     constexpr int kHxPer = 3, kHxFirst = 4, kHxRun = 8;
     uint32_t co0[kHxPer];
-    // The count/offset words and the SoA are issued in ONE straight-line block: the
-    // words through a buffer resource that holds no records outside the dedupe form
-    // (such a load returns 0, no branch), lanes past N re-read node N-1 and rows past
-    // npd / npr row 0 (ignored), and val / ts always hold a row (engine).  A branch
-    // between the loads makes the compiler's wait counts at the join conservative: the
-    // dedupe-form chain then waited for the whole SoA stream before it could issue its
-    // entry loads.  The other hot-value sources (K2 buckets, annotation values) are
-    // loaded in the branch that uses them, also through empty-able buffer resources.
+    // Every load is unconditional, with a clamped index (lanes past N re-read node N-1, rows
+    // past npd/npr read row 0; both ignored): a load inside a branch makes the compiler wait
+    // for all loads at the join (s_waitcnt vmcnt(0)), which serialised the dedupe-form chain
+    // below behind the whole SoA stream.
     const int lo = (int)min((int64_t)threadIdx.x, N - 1 - first);  // lane offset, clamped
-    const int32_t nrest = (int32_t)min(N - first, (int64_t)kK1Threads);  // this block's nodes
-    {
-        const __amdgpu_buffer_rsrc_t rco = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint32_t*>(a.hx_CO), 0, hx ? (int32_t)(4 * (int64_t)a.hx_nblk * gridDim.x) : 0, kBufRsrcW3);
+    if (hx) {
 #pragma unroll
         for (int u = 0; u < kHxPer; ++u)  // (masked where used: a use here would wait for them)
-            co0[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
-                rco, 4 * (int32_t)(max(min(u * kK1Threads + (int)threadIdx.x, a.hx_nblk - 1), 0) * gridDim.x + blk), 0, 0);
-        __builtin_amdgcn_sched_barrier(0);  // issued first: the scheduler would sink them past the SoA loads
+            co0[u] = a.hx_CO[(int64_t)min(u * kK1Threads + (int)threadIdx.x, a.hx_nblk - 1) * gridDim.x + blk];
+        for (int b = 0; b < kMaxWin; ++b) hxh[b][threadIdx.x] = 0;
     }
 #pragma unroll
     for (int k = 0; k < PD; ++k) {
-        const int64_t row = k < pol.npd ? pol.pred_slot[k] : 0;
-        // uniform row base + lane offset (the SGPR-base load form)
-        const int64_t* __restrict__ tr = ts + (row * N + first);
-        const double* __restrict__ vr = val + (row * N + first);
-        pt[k] = tr[lo];
-        pv[k] = vr[lo];
+        pt[k] = kTsInvalid;
+        pv[k] = 0.0;
     }
 #pragma unroll
     for (int k = 0; k < PR; ++k) {
-        const int64_t row = k < pol.npr ? pol.prio_slot[k] : 0;
-        const int64_t* __restrict__ tr = ts + (row * N + first);
-        const double* __restrict__ vr = val + (row * N + first);
-        qt[k] = tr[lo];
-        qv[k] = vr[lo];
+        qt[k] = kTsInvalid;
+        qv[k] = 0.0;
+    }
+    if (pol.n_slots > 0) {  // (val/ts are null without metrics; uniform branch)
+#pragma unroll
+        for (int k = 0; k < PD; ++k) {
+            const int64_t row = k < pol.npd ? pol.pred_slot[k] : 0;
+            // uniform row base + lane offset (the SGPR-base load form)
+            const int64_t* __restrict__ tr = ts + (row * N + first);
+            const double* __restrict__ vr = val + (row * N + first);
+            pt[k] = tr[lo];
+            pv[k] = vr[lo];
+        }
+#pragma unroll
+        for (int k = 0; k < PR; ++k) {
+            const int64_t row = k < pol.npr ? pol.prio_slot[k] : 0;
+            const int64_t* __restrict__ tr = ts + (row * N + first);
+            const double* __restrict__ vr = val + (row * N + first);
+            qt[k] = tr[lo];
+            qv[k] = vr[lo];
+        }
+    }
+    if (buckets) {
+#pragma unroll
+        for (int b = 0; b < kMaxWin; ++b)
+            bc[b] = b < pol.n_win ? (buckets + first)[(int64_t)b * N + lo] : 0u;
+    }
+    if (!buckets && !hx && hv) {
+        hvl = hv[first + lo];
+        hvt = hv_ts ? hv_ts[first + lo] : hv_ts_counts;  // null: the binding-log value of an earlier pass
     }
     if (hx) {
         // this block's (node, bucket, count) entries from every K2 source region
         // (dedupe form): C/O of up to kHxPer regions per lane, then their first
-        // kHxFirst entries, all loads in flight together; longer runs loop.  The first
-        // round (every region at configs 3 / 4: <= 768 regions) is peeled: its count /
-        // offset words were loaded above, ahead of the SoA stream
-        for (int b = 0; b < kMaxWin; ++b) hxh[b][threadIdx.x] = 0;
-        auto round = [&](int i0, const uint32_t (&co)[kHxPer]) {
+        // kHxFirst entries, all loads in flight together; longer runs loop
+        for (int i0 = 0; i0 < a.hx_nblk; i0 += kK1Threads * kHxPer) {
             uint32_t c[kHxPer], o[kHxPer];
 #pragma unroll
             for (int u = 0; u < kHxPer; ++u) {
                 const int i = i0 + u * kK1Threads + threadIdx.x;
-                c[u] = i < a.hx_nblk ? co[u] & 0xFFFF : 0u;
-                o[u] = co[u] >> 16;
+                const uint32_t co = i0 == 0 ? co0[u] : a.hx_CO[(int64_t)min(i, a.hx_nblk - 1) * gridDim.x + blk];
+                c[u] = i < a.hx_nblk ? co & 0xFFFF : 0u;
+                o[u] = co >> 16;
             }
             // lanes past a run's end load entry 0 of the region array (one shared line)
             uint32_t v[kHxPer][kHxFirst];
@@ -251,40 +263,10 @@ void k1_node_pass(K1Args a, K1Step step) {
                         if (k0 + j < c[u]) atomicAdd(&hxh[(w[j] >> 16) & 7][w[j] & 0xFFFF], w[j] >> 19);
                 }
             }
-        };
-        round(0, co0);
-        for (int i0 = kK1Threads * kHxPer; i0 < a.hx_nblk; i0 += kK1Threads * kHxPer) {
-            uint32_t co[kHxPer];
-#pragma unroll
-            for (int u = 0; u < kHxPer; ++u)
-                co[u] = a.hx_CO[(int64_t)min(i0 + u * kK1Threads + (int)threadIdx.x, a.hx_nblk - 1) * gridDim.x + blk];
-            round(i0, co);
         }
         __syncthreads();
 #pragma unroll
         for (int b = 0; b < kMaxWin; ++b) bc[b] = b < pol.n_win ? hxh[b][threadIdx.x] : 0u;
-    }
-    if (buckets || hv) {  // (never with hx)
-        // (after the dedupe-form block, not in it: there they would only be waited for as
-        // dead values; not an else branch of it either — nor a condition the compiler can
-        // fold into one: the structurizer gives that an edge into the block above, whose
-        // waits then cover these loads too)
-#pragma unroll
-        for (int b = 0; b < kMaxWin; ++b) {
-            const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-                buckets + (int64_t)b * N + first, 0, buckets && b < pol.n_win ? 4 * nrest : 0, kBufRsrcW3);
-            bc[b] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rb, 4 * lo, 0, 0);
-        }
-        {
-            const bool use_hv = !buckets && hv;
-            const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<double*>(hv) + first, 0, use_hv ? 8 * nrest : 0, kBufRsrcW3);
-            const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<int64_t*>(hv_ts) + first, 0, use_hv && hv_ts ? 8 * nrest : 0, kBufRsrcW3);
-            hvl = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, 8 * lo, 0, 0));
-            const int64_t t = __builtin_bit_cast(int64_t, __builtin_amdgcn_raw_buffer_load_b64(rt, 8 * lo, 0, 0));
-            hvt = hv_ts ? t : hv_ts_counts;  // null: the binding-log value of an earlier pass
-        }
     }
     CRANE_TSTAMP(a.trace, blockIdx.x, 1);
     // the batch time range partials: issued after the SoA loads, reduced after the compute

@@ -43,10 +43,6 @@ inline hipError_t klaunch(const char* name, void (*kernel)(KArgs...), dim3 grid,
         }                                                                                            \
     } while (0)
 
-// Word 3 of a raw buffer resource on gfx9 (gfx950): 32-bit data format.  A resource with
-// num_records 0 makes every load through it return 0 (the branch-free optional source).
-constexpr int32_t kBufRsrcW3 = 0x00020000;
-
 struct HotCutoffs {
     int32_t n_win;
     int32_t pad;
@@ -247,7 +243,8 @@ struct StepTables {
     // block's sorted one-step records stepping inside the tile's range of that kind
     int4* rows;
     // with rows, per (tile t, block b) at prow[t * nblk + b]: {pl0 | ph0 << 16, pl1 | ph1 << 16},
-    // the block's middle pieces [pl, ph) of that kind overlapping the tile's range (0: none)
+    // the block's middle pieces [pl, ph) of that kind overlapping the tile's range (0: none);
+    // null: no per-tile ranges (K3s reads every piece of the block, none is ever cut)
     int2* prow;
     unsigned long long* trace;  // K3s phase trace or null
     // K1's one-step staging for blocks with more records of a kind than its LDS holds
@@ -258,6 +255,7 @@ struct StepTables {
     // ones (step_pieces), INT32_MAX = never
     int32_t piece_work;
 };
+constexpr int64_t kPieceMinTiles = 32;  // pod tiles from which step_pieces runs (engine option step_pieces 0)
 constexpr int64_t kStepRowsMax = 1LL << 24;  // tile x block rows (256 MiB); larger batches: K3s searches
 __host__ __device__ inline int64_t s1_at(const StepTables& st, int T, int64_t b) {
     return T * st.s1pad + b * 2 * st.bs;

@@ -235,10 +235,8 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     int2 prow = make_int2(0, 0);
     if (own) {
         c = reinterpret_cast<const int4*>(st.cnt)[ob];
-        if (st.rows) {
-            row = st.rows[grp * st.nblk + ob];
-            prow = st.prow[grp * st.nblk + ob];
-        }
+        if (st.rows) row = st.rows[grp * st.nblk + ob];
+        if (st.prow) prow = st.prow[grp * st.nblk + ob];
     }
     bool live[kK3sPPL], ds[kK3sPPL];
     int32_t pod[kK3sPPL];
@@ -256,11 +254,11 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     if (threadIdx.x < 2) umax[threadIdx.x] = -1;
     CRANE_TSTAMP(st.trace, b, 5);  // (pods in: the LDS stores waited for them)
     const int32_t n1[2] = {any[0] ? c.x : 0, any[1] ? c.z : 0};
-    // middle pieces [pl, pl + nm) per kind: with rows, those overlapping the tile (the producer's
-    // elementary pieces, step_pieces), else all of them
-    const int32_t pl[2] = {st.rows ? prow.x & 0xFFFF : 0, st.rows ? prow.y & 0xFFFF : 0};
-    const int32_t nm[2] = {any[0] ? (st.rows ? (prow.x >> 16) - pl[0] : c.y) : 0,
-                           any[1] ? (st.rows ? (prow.y >> 16) - pl[1] : c.w) : 0};
+    // middle pieces [pl, pl + nm) per kind: with piece ranges, those overlapping the tile (the
+    // producer's elementary pieces, step_pieces), else all of them
+    const int32_t pl[2] = {st.prow ? prow.x & 0xFFFF : 0, st.prow ? prow.y & 0xFFFF : 0};
+    const int32_t nm[2] = {any[0] ? (st.prow ? (prow.x >> 16) - pl[0] : c.y) : 0,
+                           any[1] ? (st.prow ? (prow.y >> 16) - pl[1] : c.w) : 0};
     const Step1* base[2] = {st.single + s1_at(st, 0, ob), st.single + s1_at(st, 1, ob)};
     int32_t jj[4] = {0, 0, 0, 0};  // jl[0], jh[0], jl[1], jh[1]
     int32_t um[2] = {-1, -1};

@@ -665,7 +665,9 @@ template <int BS>
 __device__ __forceinline__ void step_pieces(StepShared& sh, const StepTables& st, int64_t blk, const PieceScr& ps) {
     static_assert(BS >= 128, "two waves compact the two kinds");
     const int32_t nm0 = sh.lc[0][1], nm1 = sh.lc[1][1];
-    auto dec = [&](int32_t nm) { return nm >= 2 && nm <= ps.pc && (int64_t)nm * st.ntiles >= st.piece_work; };
+    auto dec = [&](int32_t nm) {
+        return st.prow && nm >= 2 && nm <= ps.pc && (int64_t)nm * st.ntiles >= st.piece_work;
+    };
     const bool d0 = dec(nm0), d1 = dec(nm1);
     if (!d0 && !d1) {  // (workgroup-uniform)
         if (threadIdx.x < 2) sh.pn[threadIdx.x] = -1;
@@ -740,7 +742,7 @@ __device__ __forceinline__ void step_pieces(StepShared& sh, const StepTables& st
 // The tile rows (st.rows set): per pod tile t, the block's uniform key per kind and
 // the range [jl, jh) of its sorted one-step records stepping inside the tile's range
 // (after step_sort_publish: srt sorted, s1l holding the prefix / suffix maxima), and
-// (st.prow) the range [pl, ph) of its middle pieces overlapping it (step_pieces).
+// (st.prow set) the range [pl, ph) of its middle pieces overlapping it (step_pieces).
 // pre: this thread's first item's bound (tile_prefetch, loaded early).  Every thread
 // calls it (barrier).
 __device__ __forceinline__ void tile_prefetch(const StepTables& st, int64_t* pre) {
@@ -786,7 +788,8 @@ __device__ __forceinline__ void step_tile_rows(const Step1* s1l, const Step1* sr
                 if (hi_b && c < n) u = smL[T * CAP + c];       // records stepping after hi: keys before
             }
             // middle pieces: elementary ones ending by lo (pl) / starting by hi (ph); raw: all
-            if (pn >= 0) {
+            if (!st.prow) {
+            } else if (pn >= 0) {
                 const int64_t* bs = ps.bs(T);
                 const int32_t* ix = ps.ix(T);
                 int32_t lo = 0, hi = pn;
@@ -800,28 +803,32 @@ __device__ __forceinline__ void step_tile_rows(const Step1* s1l, const Step1* sr
                 pc = hi_b ? sh.lc[T][1] : 0;
             }
         }
-        const int32_t co = quad_xor1(c), uo = quad_xor1(u), pco = quad_xor1(pc);
-        const int64_t vo = (int64_t)(((uint64_t)(uint32_t)quad_xor1((int32_t)((uint64_t)v >> 32)) << 32) |
-                                     (uint32_t)quad_xor1((int32_t)(uint32_t)v));
+        const int32_t co = quad_xor1(c), uo = quad_xor1(u);
         const int32_t jl = hi_b ? co : c, jh = hi_b ? c : co;
-        int32_t pl = hi_b ? pco : pc;
-        const int32_t ph = hi_b ? pc : pco;
-        int32_t ukey = -1;
-        if (pn >= 0 && ph - pl == 1 && t < st.ntiles) {  // one elementary piece: uniform if it covers [lo, hi]
-            const int64_t lo_v = hi_b ? vo : v, hi_v = hi_b ? v : vo;
-            const int32_t j = ps.ix(T)[pl];
-            if (ps.bs(T)[j] <= lo_v && ps.bs(T)[j + 1] > hi_v) {
-                ukey = ps.vm(T)[j];
-                pl = ph;
+        int32_t ukey = -1, pp = 0;
+        if (st.prow) {  // (uniform)
+            const int32_t pco = quad_xor1(pc);
+            const int64_t vo = (int64_t)(((uint64_t)(uint32_t)quad_xor1((int32_t)((uint64_t)v >> 32)) << 32) |
+                                         (uint32_t)quad_xor1((int32_t)(uint32_t)v));
+            int32_t pl = hi_b ? pco : pc;
+            const int32_t ph = hi_b ? pc : pco;
+            if (pn >= 0 && ph - pl == 1 && t < st.ntiles) {  // one elementary piece: uniform if it covers [lo, hi]
+                const int64_t lo_v = hi_b ? vo : v, hi_v = hi_b ? v : vo;
+                const int32_t j = ps.ix(T)[pl];
+                if (ps.bs(T)[j] <= lo_v && ps.bs(T)[j + 1] > hi_v) {
+                    ukey = ps.vm(T)[j];
+                    pl = ph;
+                }
             }
+            pp = pl < ph ? (pl | (ph << 16)) : 0;
         }
         // a kind without pods here (lo = INT64_MAX, hi = INT64_MIN) gives jl = n > jh = 0
         const int32_t um = jl > jh ? -1 : max(max(fl[T], ukey), max(u, uo)), jp = jl > jh ? 0 : (jl | (jh << 16));
-        const int32_t pp = pl < ph ? (pl | (ph << 16)) : 0;
-        const int32_t um1 = quad_down2(um), jp1 = quad_down2(jp), pp1 = quad_down2(pp);
+        const int32_t um1 = quad_down2(um), jp1 = quad_down2(jp);
+        const int32_t pp1 = st.prow ? quad_down2(pp) : 0;
         if ((i & 3) == 0 && t < st.ntiles) {
             st.rows[(int64_t)t * st.nblk + blk] = make_int4(um, um1, jp, jp1);
-            st.prow[(int64_t)t * st.nblk + blk] = make_int2(pp, pp1);
+            if (st.prow) st.prow[(int64_t)t * st.nblk + blk] = make_int2(pp, pp1);
         }
     }
 }
