@@ -125,6 +125,13 @@ def roof(alg_bytes, ms, what, traffic=None, extra=None):
     return r
 
 
+def rec_bytes(spec):
+    """sizeof(NodeRec<PD, PR>) of the policy's record shape (dyn_types.hpp)."""
+    pd_, pr_ = len(spec["predicate"]), len(spec["priority"])
+    pd_, pr_ = (4, 6) if pd_ <= 4 and pr_ <= 6 else ((8, 8) if pd_ <= 8 and pr_ <= 8 else (16, 16))
+    return -(-(24 + 16 * pr_ + 8 * pd_) // 16) * 16
+
+
 def kernel_times(eng, fn, reps):
     """Mean dispatch-stamped duration per kernel name over `reps` calls of fn()."""
     acc = {}
@@ -237,9 +244,7 @@ def matrix_leg(cd, spec, dev, stream, label, val, ts, hv, hv_ts, now, ds, steps,
     eng.eval_keys_async(d_now, d_flags, d_k2, sh)
     stream.synchronize()
     same = bool(torch.equal(d_keys, d_k2))
-    pd_, pr_ = len(spec["predicate"]), len(spec["priority"])
-    pd_, pr_ = (4, 6) if pd_ <= 4 and pr_ <= 6 else ((8, 8) if pd_ <= 8 and pr_ <= 8 else (16, 16))
-    rec = -(-(24 + 16 * pr_ + 8 * pd_) // 16) * 16  # sizeof(NodeRec<PD, PR>)
+    rec = rec_bytes(spec)
     kname = "k3m_matrix+keys"
     kms = kt.get(kname, ms)
     alg = N * rec + P * (8 + 1 + 8) + 2 * P * N
@@ -267,10 +272,15 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
     scratch buffer is READ, which evicts the 256 MiB Infinity Cache and the L2s without
     leaving dirty lines to be written back during the timed kernels.  Times are the kernels'
     dispatch-stamped durations (crane_dyn_set_profiling), median over `reps`.
+    Two node passes over the same counts: `k1` the step path's (K1 fused with the step
+    tables of the pod batch, the headline step's kernel) and `k1_records` the node pass that
+    writes every node's record (what the matrix / greedy / selection / drop-in table paths
+    read; one per snapshot sync), each after its own K2 refresh and flush.
     Algorithmic bytes:
       K2 = 12 per binding (node i32 + ts i64 read) + 4 per node and window (counts written)
       K1 = 16 per node and metric (value + ts read) + 4 per node and window (counts read)
-           + 8 per node (hot value written)"""
+           + 8 per node (hot value written)
+      K1 records = K1 + the record written (sizeof(NodeRec), 160 B at the default policy)"""
     N, B, P = COLD["nodes"], COLD["bindings"], COLD["pods"]
     c = synth.make_cluster(spec, N, P, n_bindings=B, seed=7)
     c.now, c.ds = synth.make_pods(P, seed=8)
@@ -296,7 +306,7 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
         with torch.cuda.stream(st):
             torch.sum(scratch, dim=0, keepdim=True, out=sink)
 
-    k2, k1, k2_parts = [], [], {}
+    k2, k1, k1r, k2_parts = [], [], [], {}
     for r in range(reps + 1):
         flush()
         eng.set_profiling(True)
@@ -306,32 +316,41 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
         eng.set_profiling(True)
         eng.eval_keys_async(d_now, d_flags, d_keys, sh)
         t_ev = eng.stage_times()
+        eng.refresh_hot_values_async(now, now, sh)  # (counts pending again for the record pass)
+        flush()
+        eng.set_profiling(True)
+        eng.node_pass_async(sh)
+        t_np = eng.stage_times()
         if r:  # rep 0 warms the code paths
             k2.append(sum(t for _, t in t_k2))
             for name, t in t_k2:
                 k2_parts.setdefault(name, []).append(t)
             k1.append(sum(t for name, t in t_ev if name.startswith("k1_node_pass")))
+            k1r.append(sum(t for name, t in t_np if name == "k1_node_pass"))
     eng.set_profiling(False)
     eng.close()
     del scratch
-    k2_ms, k1_ms = float(np.median(k2)), float(np.median(k1))
-    tr_k2 = tr_k1 = None
+    k2_ms, k1_ms, k1r_ms = float(np.median(k2)), float(np.median(k1)), float(np.median(k1r))
+    tr_k2 = tr_k1 = tr_k1r = None
     if pmc:
         ks = pmc.get("kernels", {})
         k2t = [v.get("traffic_bytes") for k, v in ks.items() if k.startswith("crane::k2")]
         if k2t and all(t is not None for t in k2t):
             tr_k2 = int(sum(k2t))
-        k1t = [v.get("traffic_bytes") for k, v in ks.items() if k.startswith("crane::k1_node_pass<")]
-        if len(k1t) == 1 and k1t[0] is not None:
-            tr_k1 = int(k1t[0])
+        tr_k1 = pmc_traffic(pmc, "k1_node_pass+k3a_steps")
+        tr_k1r = pmc_traffic(pmc, "k1_node_pass")
     alg_k2 = B * 12 + 4 * W * N
     alg_k1 = N * (16 * M + 4 * W + 8)
+    rec_b = rec_bytes(spec)
     return {"workload": f"{N} nodes x {B}-entry binding log ({P}-pod batch), default policy",
             "cache": "cold: 1 GiB read between the stages (Infinity Cache + L2 evicted, no dirty lines)",
             "k2": roof(alg_k2, k2_ms, "bindings read (12 B) + per-node window counts written (4 B x W)", tr_k2,
                        {"kernels": {k: round(float(np.median(v)), 4) for k, v in k2_parts.items()}}),
-            "k1": roof(alg_k1, k1_ms, "SoA (value, ts) read + window counts read + hot value written", tr_k1),
-            "traffic_source": pmc_src if (tr_k1 is not None or tr_k2 is not None) else None}
+            "k1": roof(alg_k1, k1_ms, "SoA (value, ts) read + window counts read + hot value written", tr_k1,
+                       {"kernel": "k1_node_pass+k3a_steps (fused with the step tables)"}),
+            "k1_records": roof(alg_k1 + N * rec_b, k1r_ms, f"as k1 + the node record written ({rec_b} B)", tr_k1r,
+                               {"kernel": "k1_node_pass (records: matrix / greedy / selection / drop-in tables)"}),
+            "traffic_source": pmc_src if (tr_k1 is not None or tr_k2 is not None or tr_k1r is not None) else None}
 
 
 DROPIN_CPU = os.path.join(ROOT, "oracle", "_build", "dropin_cpu")

@@ -274,8 +274,9 @@ __global__ __launch_bounds__(kChT) void k_sel_chain(SelArgs a, const int64_t* __
 // window) are ranked among the A nodes (merged rank = A nodes before it + candidates
 // before it), and the end is the candidate of merged rank K - 1 or else the A node of
 // rank rank_A(s) + K - 1 - (candidates before it).  About ten dependent LDS round trips
-// per pod instead of a stream over its ~N/20 positions.  Positions are unrolled: a window
-// [s, s + N) wraps past node N - 1 to node 0.
+// per pod instead of a stream over its ~N/20 positions.  Each I node's A rank is kept
+// with the list, so a candidate chunk costs one LDS round trip (list entries), not two.
+// Positions are unrolled: a window [s, s + N) wraps past node N - 1 to node 0.
 // Applies while the LDS holds it (N <= 64 * kRsMaxW, |I| <= kRsIMax); else it flags the
 // streaming kernel (k_sel_chain, launched behind it) to run.
 constexpr int kRsT = 1024;
@@ -284,7 +285,7 @@ constexpr int kRsIMax = 4096;  // in-range nodes
 
 __host__ __device__ inline size_t rs_lds_bytes(int64_t W) {
     const size_t Wp = (size_t)W + 1;
-    return 8 * (3 * Wp + kRsIMax) + 4 * (5 * Wp + kRsIMax);
+    return 8 * (3 * Wp + kRsIMax) + 4 * (5 * Wp + 2 * kRsIMax);
 }
 
 struct RsView {
@@ -305,13 +306,17 @@ __device__ __forceinline__ int64_t rs_select(const uint64_t* m, const uint32_t* 
     const int lane = threadIdx.x & 63;
     int64_t w = smp[r >> 6];  // the word holding rank 64 * (r / 64) (r's word is at or after it)
     for (;;) {
-        const int64_t wl = min(w + lane + 1, (int64_t)W);
-        const uint64_t hb = __ballot((int64_t)b[wl] > r);
+        // lane l: word w + l's rank and mask and the next word's rank, one round trip
+        const int64_t wl = min(w + lane, (int64_t)W);
+        const uint32_t bl = b[wl], bn = b[min(wl + 1, (int64_t)W)];
+        const uint64_t ml = m[wl];
+        const uint64_t hb = __ballot((int64_t)bn > r);
         if (hb) {
-            const int64_t ww = w + __ffsll((long long)hb) - 1;
-            const uint64_t mw = m[ww];
+            const int j = __ffsll((long long)hb) - 1;
+            const uint64_t mw = (uint64_t)readlane64((int64_t)ml, j);
             if (word) *word = mw;
-            return ww * 64 + nth_set_bit(mw, (int)(r - (int64_t)b[ww]) + 1);
+            const int64_t bw = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)bl, j);
+            return (w + j) * 64 + nth_set_bit(mw, (int)(r - bw) + 1);
         }
         w += 64;
     }
@@ -338,6 +343,7 @@ __global__ __launch_bounds__(kRsT) void k_sel_chain_rs(SelArgs a, const int64_t*
     uint32_t* sA = bD + Wp;
     uint32_t* sD = sA + Wp;
     uint32_t* iPos = sD + Wp;
+    uint32_t* iRA = iPos + kRsIMax;  // an in-range node's rank among the A nodes (A nodes before it)
     // the non-DaemonSet pods' time range
     int64_t lo = INT64_MAX, hi = INT64_MIN;
     for (int64_t p = threadIdx.x; p < P; p += kRsT) {
@@ -408,6 +414,7 @@ __global__ __launch_bounds__(kRsT) void k_sel_chain_rs(SelArgs a, const int64_t*
             const int64_t n = (int64_t)w * 64 + j;
             iPos[b] = (uint32_t)n;
             iFth[b] = fth[n];
+            iRA[b] = (uint32_t)rs_rank(mA, bA, n);
             ++b;
         }
         for (uint32_t k = (bA[w] + 63) >> 6; (k << 6) < bA[w + 1]; ++k) sA[k] = (uint32_t)w;
@@ -466,7 +473,7 @@ __global__ __launch_bounds__(kRsT) void k_sel_chain_rs(SelArgs a, const int64_t*
                         if (!rm) break;
                         const bool cand = inr && iFth[ic] <= t;
                         const uint64_t cm = __ballot(cand);
-                        const int64_t ra = y < N ? rs_rank(mA, bA, y) : TA + rs_rank(mA, bA, y - N);
+                        const int64_t ra = (int64_t)iRA[ic] + (wrap ? TA : 0);  // (built with the list)
                         const int64_t mr = ra - rA0 + cbase + __popcll(cm & lt);
                         c_lt += __popcll(__ballot(cand && mr < K - 1));
                         const uint64_t eq = __ballot(cand && mr == K - 1);

@@ -283,9 +283,11 @@ int main(int argc, char** argv) {
             if (s.code() == Code::Error) errors++;
         });
         const auto t1 = Clock::now();
-        int64_t F = 0;
-        for (int64_t i = 0; i < N; ++i)
-            if (feas[(size_t)i]) fidx[(size_t)F++] = i;
+        int64_t F = 0;  // the feasible list in node order (branch-free: ~30 % of the nodes fail at random)
+        for (int64_t i = 0; i < N; ++i) {
+            fidx[(size_t)F] = i;
+            F += feas[(size_t)i];
+        }
         pool.until(F, [&](int64_t j) {  // prioritizeNodes -> RunScorePlugins
             std::pair<int64_t, Status> sr;
 #ifdef DROPIN_CPU
