@@ -111,7 +111,9 @@ struct Options {
     int k2x_threads = 512;    // dedupe K2 workgroup size: 256, 512 or 1024
     int k2l_region = 4096;    // large K2: bindings per region (2048 or 4096)
     int k2l_co_t = 0;         // large K2: count/offset words [bin][region] (1) or [region][bin] (0)
-    int k2l_threads = 512;    // large K2: partition workgroup size at 4096-binding regions (512 or 1024)
+    int k2l_threads = 1024;   // large K2: partition workgroup size at 4096-binding regions (512 or 1024;
+                              // cold 4M x 16M: 1024 0.084-0.085 ms vs 512 0.087-0.089, same-box sweeps
+                              // profiles/ab/r03_k2_cold_*.txt)
     int sel_chain = 0;        // selection windows: 0 LDS rank/select walk when it fits, 1 streaming kernel
     int step_lds_cap = 1 << 30;  // K1: one-step records per kind staged in LDS at most (0: always st.stage)
     int step_pieces = 0;      // middle pieces cut into elementary ones per block (step_pieces): 0 when the

@@ -306,17 +306,13 @@ __device__ __forceinline__ int64_t rs_select(const uint64_t* m, const uint32_t* 
     const int lane = threadIdx.x & 63;
     int64_t w = smp[r >> 6];  // the word holding rank 64 * (r / 64) (r's word is at or after it)
     for (;;) {
-        // lane l: word w + l's rank and mask and the next word's rank, one round trip
-        const int64_t wl = min(w + lane, (int64_t)W);
-        const uint32_t bl = b[wl], bn = b[min(wl + 1, (int64_t)W)];
-        const uint64_t ml = m[wl];
-        const uint64_t hb = __ballot((int64_t)bn > r);
+        const int64_t wl = min(w + lane + 1, (int64_t)W);
+        const uint64_t hb = __ballot((int64_t)b[wl] > r);
         if (hb) {
-            const int j = __ffsll((long long)hb) - 1;
-            const uint64_t mw = (uint64_t)readlane64((int64_t)ml, j);
+            const int64_t ww = w + __ffsll((long long)hb) - 1;
+            const uint64_t mw = m[ww];
             if (word) *word = mw;
-            const int64_t bw = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)bl, j);
-            return (w + j) * 64 + nth_set_bit(mw, (int)(r - bw) + 1);
+            return ww * 64 + nth_set_bit(mw, (int)(r - (int64_t)b[ww]) + 1);
         }
         w += 64;
     }
