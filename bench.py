@@ -852,7 +852,9 @@ def main():
                "sample": f"{legs['threads_16']['sample']}; string mode: every Filter/Score call re-parses its "
                          "annotations like stats.go:51-76 (oracle/crane_oracle.c)",
                "cpu_model": cpu_model(), "nproc": os.cpu_count(), "effective_cpus": ncpu,
-               "all_cores": legs["threads_all"],
+               "all_available_cpus": dict(legs["threads_all"], note=f"every CPU this process may use ({ncpu} of "
+                                                                     f"nproc {os.cpu_count()}: affinity mask / cgroup "
+                                                                     "quota)"),
                "note": "C restatement, not the Go plugin (no Go toolchain, SURVEY 8c); it resolves the fixed-offset "
                        "zone once instead of utils.GetLocation's time.LoadLocation on every call (utils.go:35-45), "
                        "so it is a stronger baseline than the reference",
