@@ -156,6 +156,9 @@ def parse():
     ap.add_argument("--no-greedy", action="store_true", help="skip the config-5 sequential-greedy measurement")
     ap.add_argument("--inflight", type=int, default=4,
                     help="independent pod batches in flight (engines x HIP streams); 1 = one batch at a time")
+    ap.add_argument("--ar-stream", default="own", choices=("own", "engine"),
+                    help="N>1: the keys all-reduce on its own stream, or on the stream of the group's last "
+                         "batch (no stream beyond the K engine streams: the box exposes 4 hardware queues)")
     ap.add_argument("--ar-group", type=int, default=0,
                     help="N>1: batches per keys all-reduce (a multiple of --inflight; 0 = 16 x inflight)")
     ap.add_argument("--rehearse-collective", action="store_true",
@@ -630,12 +633,15 @@ def main():
         ev_ar = [torch.cuda.Event(), torch.cuda.Event()]
 
     def collect(b, nb):
+        cs = cstream if args.ar_stream == "own" else streams[(nb - 1) % K]
         for jj in range(min(nb, K)):
+            if streams[jj] is cs:
+                continue
             ev_s[jj].record(streams[jj])
-            cstream.wait_event(ev_s[jj])
-        with torch.cuda.stream(cstream):
+            cs.wait_event(ev_s[jj])
+        with torch.cuda.stream(cs):
             dist.all_reduce(kbufs[b][:nb], op=dist.ReduceOp.MAX)  # RCCL over xGMI
-        ev_ar[b].record(cstream)
+        ev_ar[b].record(cs)
         ar_done[b] = ev_ar[b]
 
     # the step calls bound once to their engine, stream and key buffer (step_keys_fn: the
@@ -914,7 +920,9 @@ def main():
             "batches_in_flight": {"k": K, "how": "K engines (own copy of the shard's nodes, binding log, scratch) on "
                                                 "K HIP streams, batch i on engine i % K; every batch runs the whole "
                                                 "step" + (f"; one RCCL max all-reduce per group of {G} batches' keys "
-                                                          f"[{G}][P] on its own stream" if coll else ""),
+                                                          f"[{G}][P] on " + ("its own stream" if args.ar_stream == "own"
+                                                                             else "the group's last batch's stream")
+                                                          if coll else ""),
                                   "keys_agree": keys_agree,
                                   "batch_latency_ms": round(batch_latency_ms, 4)},
             "placements_per_s": round(placements, 1),
