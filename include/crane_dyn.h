@@ -24,7 +24,8 @@
  * (*_async) enqueue work that reads the engine's buffers on the caller's stream;
  * the calls that replace engine state (upload_nodes, upload_bindings,
  * binding_records, add_bindings, gc_bindings, destroy) first wait for all such
- * work, so they never change a buffer a kernel is still reading.  Asynchronous
+ * work (a device synchronize when asynchronous work was enqueued since the last
+ * one), so they never change a buffer a kernel is still reading.  Asynchronous
  * calls on ONE engine from several streams must be ordered by the caller (they
  * share the engine's scratch): use one stream per engine.  Nothing in the
  * engine reads the environment; crane_dyn_set_option (tests / A-B tools only)

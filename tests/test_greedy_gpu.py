@@ -83,7 +83,14 @@ def test_greedy_then_eval_consistent():
     eng.upload_nodes(*c.rows(eng.metric_names)[:2], c.hv, c.hv_ts)
     _, _, ch, _ = eng.eval(c.now, c.ds)
     from helpers import oracle_soa
-    assert np.array_equal(ch, oracle_soa(spec, c, want_matrix=False)[2])
+    want = oracle_soa(spec, c, want_matrix=False)[2]
+    if not np.array_equal(ch, want):
+        # diagnostics for a mismatch seen once in a full-suite run (not reproduced in 288
+        # repetitions, tools/repro_greedy_eval.py): does it persist, and in which path?
+        _, _, ch2, _ = eng.eval(c.now, c.ds)
+        eng.set_option("keys_path", 1)
+        _, _, ch3, _ = eng.eval(c.now, c.ds)
+        pytest.fail(f"eval after greedy: got {ch[:4]} want {want[:4]}; again {ch2[:4]}; matrix path {ch3[:4]}")
 
 
 @pytest.mark.parametrize("ds_frac,feas_all", [(0.0, False), (1.0, False), (0.3, False), (0.02, True)])
