@@ -491,7 +491,11 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     HIPTRY(h, h->stile.reserve((size_t)(kTileStat * g.ntiles)));
     if (!h->sbatch.p) {  // {tmin, tmax, tile counter}: the counter starts at 0, K3p re-arms it
         HIPTRY(h, h->sbatch.reserve(4));
-        HIPTRY(h, hipMemset(h->sbatch.p, 0, 4 * sizeof(int64_t)));
+        // on the engine stream and waited for: a null-stream hipMemset is not ordered with the
+        // non-blocking streams K3p runs on and may land after it (a batch then saw tmin = tmax
+        // = 0: every pod scored as at time 0, seen once in test_greedy_then_eval_consistent)
+        HIPTRY(h, hipMemsetAsync(h->sbatch.p, 0, 4 * sizeof(int64_t), h->stream));
+        HIPTRY(h, hipStreamSynchronize(h->stream));
     }
     HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
     HIPTRY(h, h->scnt.reserve((size_t)std::max<int32_t>(nblk, 1) * 6));  // cnt [nblk][4] + flat [nblk][2]
@@ -753,7 +757,8 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
         if (o.trace) {
             hipError_t e = hipSetDevice(h->device);
             if (e == hipSuccess) e = h->trace.reserve((size_t)3 * kTraceWgs * 8);
-            if (e == hipSuccess) e = hipMemset(h->trace.p, 0, sizeof(unsigned long long) * h->trace.n);
+            if (e == hipSuccess) e = hipMemsetAsync(h->trace.p, 0, sizeof(unsigned long long) * h->trace.n, h->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
             if (e != hipSuccess) return h->hipfail(e, "trace buffer");
         }
     }
@@ -1046,14 +1051,12 @@ int crane_dyn_select(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_
     if (window) HIPTRY(h, hipMemcpyAsync(&nxt, h->sel_state.p, sizeof nxt, hipMemcpyDeviceToHost, st));
     HIPTRY(h, hipStreamSynchronize(st));
     if (!window) {  // every pod checked all N nodes: the start advances by N, mod N
-        if (d_wstart) {
-            std::vector<int64_t> v((size_t)P, start);
-            HIPTRY(h, hipMemcpy(d_wstart, v.data(), sizeof(int64_t) * (size_t)P, hipMemcpyHostToDevice));
-        }
-        if (d_wlen) {
-            std::vector<int64_t> v((size_t)P, N);
-            HIPTRY(h, hipMemcpy(d_wlen, v.data(), sizeof(int64_t) * (size_t)P, hipMemcpyHostToDevice));
-        }
+        // on the caller's stream and waited for (a pageable hipMemcpy may return before the
+        // copy lands and is not ordered with non-blocking streams)
+        std::vector<int64_t> vs(d_wstart ? (size_t)P : 0, start), vl(d_wlen ? (size_t)P : 0, N);
+        if (d_wstart) HIPTRY(h, hipMemcpyAsync(d_wstart, vs.data(), sizeof(int64_t) * (size_t)P, hipMemcpyHostToDevice, st));
+        if (d_wlen) HIPTRY(h, hipMemcpyAsync(d_wlen, vl.data(), sizeof(int64_t) * (size_t)P, hipMemcpyHostToDevice, st));
+        if (d_wstart || d_wlen) HIPTRY(h, hipStreamSynchronize(st));
     }
     if (next_start) *next_start = nxt;
     return CRANE_OK;

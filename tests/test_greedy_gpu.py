@@ -85,8 +85,8 @@ def test_greedy_then_eval_consistent():
     from helpers import oracle_soa
     want = oracle_soa(spec, c, want_matrix=False)[2]
     if not np.array_equal(ch, want):
-        # diagnostics for a mismatch seen once in a full-suite run (not reproduced in 288
-        # repetitions, tools/repro_greedy_eval.py): does it persist, and in which path?
+        # diagnostics (a mismatch seen once was the first-batch state race that
+        # test_first_step_batch_of_fresh_engines covers): does it persist, in which path?
         _, _, ch2, _ = eng.eval(c.now, c.ds)
         eng.set_option("keys_path", 1)
         _, _, ch3, _ = eng.eval(c.now, c.ds)
@@ -163,3 +163,16 @@ def test_greedy_config5_merge_equals_sequential(greedy_mode):
     # placement i depends only on placements < i: the first 2,000 of the full run equal the
     # oracle's sequential loop over the same cluster cut at 2,000 pods
     assert np.array_equal(a[:2000], _oracle(spec, c, 2000, now))
+
+
+def test_first_step_batch_of_fresh_engines():
+    """The step path's batch state ({tmin, tmax, tile counter}) is zeroed on the engine stream
+    and waited for before the first K3p: a null-stream memset raced the first batch once (every
+    pod then scored as at time 0).  Forty fresh engines, each checked on its first batch."""
+    spec = cd.default_policy_spec()
+    for i in range(40):
+        c = synth.make_cluster(spec, 500, 50, n_bindings=0, seed=100 + i)
+        eng = _engine(spec, c)
+        _, _, ch, _ = eng.eval(c.now, c.ds)
+        from helpers import oracle_soa
+        assert np.array_equal(ch, oracle_soa(spec, c, want_matrix=False)[2]), i
