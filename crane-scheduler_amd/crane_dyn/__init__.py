@@ -348,6 +348,7 @@ class Engine:
             raise CraneError(rc, msg)
         self.metric_names = [lib.crane_dyn_metric_name(h, i).decode() for i in range(lib.crane_dyn_num_metrics(h))]
         self.n_nodes = 0
+        self.device = device
 
     def close(self):
         if getattr(self, "h", None) and self.h.value and lib is not None:
@@ -360,6 +361,15 @@ class Engine:
     def _check(self, rc):
         if rc:
             raise CraneError(rc, lib.crane_dyn_last_error(self.h).decode())
+
+    def _ready(self, stream):
+        """stream None = the engine's own stream, which is non-blocking: it is not ordered
+        after torch's current stream, so wait for that first (tensors torch just filled must
+        be written before the engine reads or overwrites them).  Results on the engine
+        stream still need a synchronize before torch reads them."""
+        if stream is None:
+            import torch
+            torch.cuda.current_stream(self.device).synchronize()
 
     def upload_nodes(self, val, ts, hv=None, hv_ts=None, node_offset=0):
         val = np.ascontiguousarray(val, np.float64)
@@ -441,6 +451,7 @@ class Engine:
         """Device matrices (torch int8 [P][ld], either may be None) and optional keys int64[P]."""
         P = d_now.numel()
         ld = self.n_nodes if ld is None else ld
+        self._ready(stream)
         vp = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
         self._check(lib.crane_dyn_eval_matrix_async(self.h, P, vp(d_now), vp(d_flags), vp(d_ff), vp(d_score), ld,
                                                     vp(d_keys), stream))
@@ -452,6 +463,7 @@ class Engine:
         P = d_now.numel()
         vp = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
         nxt = C.c_int64(0)
+        self._ready(stream)
         self._check(lib.crane_dyn_select(self.h, P, vp(d_now), vp(d_flags), vp(d_ext_ok), vp(d_ext_score),
                                          int(dyn_weight), int(percentage), int(start), int(tie_seed), vp(d_chosen),
                                          vp(d_total), vp(d_wstart), vp(d_wlen), C.byref(nxt), stream))
@@ -459,15 +471,18 @@ class Engine:
 
     # device-resident pipeline (torch tensors on the engine's device)
     def refresh_hot_values_async(self, now_ns, hv_ts_ns, stream=None):
+        self._ready(stream)
         self._check(lib.crane_dyn_refresh_hot_values_async(self.h, int(now_ns), int(hv_ts_ns), stream))
 
     def node_pass_async(self, stream=None):
+        self._ready(stream)
         self._check(lib.crane_dyn_node_pass_async(self.h, stream))
 
     def eval_keys_async(self, d_now, d_flags, d_keys, stream=None):
         """d_now int64[P], d_flags uint8[P] or None, d_keys int64[P]: torch CUDA tensors."""
         P = d_now.numel()
         assert d_keys.numel() == P and d_now.dtype.itemsize == 8 and d_keys.dtype.itemsize == 8
+        self._ready(stream)
         self._check(lib.crane_dyn_eval_keys_async(self.h, P, C.c_void_p(d_now.data_ptr()),
                                                   None if d_flags is None else C.c_void_p(d_flags.data_ptr()),
                                                   C.c_void_p(d_keys.data_ptr()), stream))
@@ -489,6 +504,7 @@ class Engine:
         """One scheduling step: hot-value refresh at now_ns + keys-only eval (torch CUDA tensors)."""
         P = d_now.numel()
         assert d_keys.numel() == P and d_now.dtype.itemsize == 8 and d_keys.dtype.itemsize == 8
+        self._ready(stream)
         self._check(lib.crane_dyn_step_keys_async(self.h, int(now_ns), int(hv_ts_ns), P, C.c_void_p(d_now.data_ptr()),
                                                   None if d_flags is None else C.c_void_p(d_flags.data_ptr()),
                                                   C.c_void_p(d_keys.data_ptr()), stream))
@@ -502,8 +518,11 @@ class Engine:
         pn, pk = C.c_void_p(d_now.data_ptr()), C.c_void_p(d_keys.data_ptr())
         pf = None if d_flags is None else C.c_void_p(d_flags.data_ptr())
         check = self._check
+        ready = self._ready if stream is None else None
 
         def step(now_ns, hv_ts_ns):
+            if ready:
+                ready(None)
             rc = fn(h, now_ns, hv_ts_ns, P, pn, pf, pk, stream)
             if rc:
                 check(rc)
