@@ -318,6 +318,21 @@ __device__ __forceinline__ int64_t rs_select(const uint64_t* m, const uint32_t* 
     }
 }
 
+// the same for one lane's own rank r < total: the sample words bracket r's word, a binary
+// search over the prefix ranks finds it
+__device__ __forceinline__ int64_t rs_select_lane(const uint64_t* m, const uint32_t* b, const uint32_t* smp,
+                                                  int32_t W, int64_t total, int64_t r) {
+    const int64_t k = r >> 6;
+    int32_t lo = (int32_t)smp[k];
+    int32_t hi = (k + 1) * 64 < total ? (int32_t)smp[k + 1] : W - 1;
+    while (lo < hi) {  // the last word with prefix rank <= r
+        const int32_t mid = (lo + hi + 1) >> 1;
+        if ((int64_t)b[mid] <= r) lo = mid;
+        else hi = mid - 1;
+    }
+    return (int64_t)lo * 64 + nth_set_bit(m[lo], (int)(r - (int64_t)b[lo]) + 1);
+}
+
 __global__ __launch_bounds__(kRsT) void k_sel_chain_rs(SelArgs a, const int64_t* __restrict__ fth, int64_t K,
                                                        int64_t start, int64_t* __restrict__ wstart,
                                                        int64_t* __restrict__ wlen, int64_t* __restrict__ next_start,
@@ -417,101 +432,251 @@ __global__ __launch_bounds__(kRsT) void k_sel_chain_rs(SelArgs a, const int64_t*
         for (uint32_t k = (bD[w] + 63) >> 6; (k << 6) < bD[w + 1]; ++k) sD[k] = (uint32_t)w;
     }
     __syncthreads();
-    if (wv != 0) return;  // one wave walks the queue
-    const uint64_t lt = (1ull << lane) - 1ull;
-    int64_t s = start;
-    for (int64_t p0 = 0; p0 < P; p0 += 64) {
-        const int nv = (int)min((int64_t)64, P - p0);
-        const int64_t tn = a.now[p0 + min(lane, nv - 1)];
-        const int32_t dn = a.flags ? (int32_t)(a.flags[p0 + min(lane, nv - 1)] & 1u) : 0;
-        int64_t my_ws = 0, my_wl = 0;
-        for (int j = 0; j < nv; ++j) {
-            const int64_t t = readlane64(tn, j);
-            const bool d = __builtin_amdgcn_readlane(dn, j) != 0;
-            int64_t end;  // unrolled position of the window's last node, in [s, s + N)
-            if (d) {
-                if (TD < K) {
-                    end = s + N - 1;
-                } else {
-                    const int64_t r = rs_rank(mD, bD, s) + K - 1;
-                    end = r < TD ? rs_select(mD, bD, sD, W, r) : N + rs_select(mD, bD, sD, W, r - TD);
-                }
-            } else {
-                const int64_t rA0 = rs_rank(mA, bA, s), rI0 = rs_rank(mI, bI, s);
-                bool full = false;  // fewer than K feasible nodes in the whole rotation
-                if (TA < K) {
-                    int64_t cnt = 0;
-                    for (int64_t q0 = 0; q0 < TI; q0 += 64) {
-                        const int64_t q = q0 + lane;
-                        cnt += __popcll(__ballot(q < TI && iFth[min(q, TI - 1)] <= t));
+    if (TA < K) {  // fewer nodes feasible for every pod than a window holds: position walk
+        if (wv != 0) return;  // one wave walks the queue
+        const uint64_t lt = (1ull << lane) - 1ull;
+        int64_t s = start;
+        for (int64_t p0 = 0; p0 < P; p0 += 64) {
+            const int nv = (int)min((int64_t)64, P - p0);
+            const int64_t tn = a.now[p0 + min(lane, nv - 1)];
+            const int32_t dn = a.flags ? (int32_t)(a.flags[p0 + min(lane, nv - 1)] & 1u) : 0;
+            int64_t my_ws = 0, my_wl = 0;
+            for (int j = 0; j < nv; ++j) {
+                const int64_t t = readlane64(tn, j);
+                const bool d = __builtin_amdgcn_readlane(dn, j) != 0;
+                int64_t end;  // unrolled position of the window's last node, in [s, s + N)
+                if (d) {
+                    if (TD < K) {
+                        end = s + N - 1;
+                    } else {
+                        const int64_t r = rs_rank(mD, bD, s) + K - 1;
+                        end = r < TD ? rs_select(mD, bD, sD, W, r) : N + rs_select(mD, bD, sD, W, r - TD);
                     }
-                    full = TA + cnt < K;
-                }
-                if (full) {
-                    end = s + N - 1;
                 } else {
-                    const int64_t rT = rA0 + K - 1;
-                    uint64_t wA = 0;  // the mask word holding xA (TA >= K)
-                    const int64_t xA = TA < K ? s + N - 1
-                                              : (rT < TA ? rs_select(mA, bA, sA, W, rT, &wA)
-                                                         : N + rs_select(mA, bA, sA, W, rT - TA, &wA));
-                    // candidates: I nodes in [s, xA] with fth <= t, in position order
-                    int64_t c_lt = 0, cbase = 0, hitpos = -1;
+                    const int64_t rA0 = rs_rank(mA, bA, s), rI0 = rs_rank(mI, bI, s);
+                    bool full = false;  // fewer than K feasible nodes in the whole rotation
+                    if (TA < K) {
+                        int64_t cnt = 0;
+                        for (int64_t q0 = 0; q0 < TI; q0 += 64) {
+                            const int64_t q = q0 + lane;
+                            cnt += __popcll(__ballot(q < TI && iFth[min(q, TI - 1)] <= t));
+                        }
+                        full = TA + cnt < K;
+                    }
+                    if (full) {
+                        end = s + N - 1;
+                    } else {
+                        const int64_t rT = rA0 + K - 1;
+                        uint64_t wA = 0;  // the mask word holding xA (TA >= K)
+                        const int64_t xA = TA < K ? s + N - 1
+                                                  : (rT < TA ? rs_select(mA, bA, sA, W, rT, &wA)
+                                                             : N + rs_select(mA, bA, sA, W, rT - TA, &wA));
+                        // candidates: I nodes in [s, xA] with fth <= t, in position order
+                        int64_t c_lt = 0, cbase = 0, hitpos = -1;
+                        for (int64_t q0 = 0; q0 < TI; q0 += 64) {
+                            const int64_t q = q0 + lane;
+                            int64_t idx = rI0 + q;
+                            const bool wrap = idx >= TI;
+                            idx -= wrap ? TI : 0;
+                            const int64_t ic = min(idx, TI - 1);
+                            const int64_t y = (int64_t)iPos[ic] + (wrap ? N : 0);
+                            const bool inr = q < TI && y <= xA;
+                            const uint64_t rm = __ballot(inr);
+                            if (!rm) break;
+                            const bool cand = inr && iFth[ic] <= t;
+                            const uint64_t cm = __ballot(cand);
+                            const int64_t ra = (int64_t)iRA[ic] + (wrap ? TA : 0);  // (built with the list)
+                            const int64_t mr = ra - rA0 + cbase + __popcll(cm & lt);
+                            c_lt += __popcll(__ballot(cand && mr < K - 1));
+                            const uint64_t eq = __ballot(cand && mr == K - 1);
+                            if (eq) {
+                                hitpos = readlane64(y, __ffsll((long long)eq) - 1);
+                                break;
+                            }
+                            cbase += __popcll(cm);
+                            if (rm != ~0ull) break;  // the window's last in-range node was in this chunk
+                        }
+                        if (hitpos >= 0) {
+                            end = hitpos;
+                        } else if (TA >= K && c_lt == 0) {
+                            end = xA;
+                        } else {
+                            // the A node c_lt before xA: inside xA's word when it holds that many below it
+                            const int xb = (int)((xA >= N ? xA - N : xA) & 63);  // xA's bit in its word
+                            const int below = TA >= K ? __popcll(wA & ((1ull << xb) - 1ull)) : -1;
+                            if (c_lt <= below) {
+                                end = xA - xb + nth_set_bit(wA, below - (int)c_lt + 1);
+                            } else {
+                                const int64_t r = rA0 + K - 1 - c_lt;
+                                end = r < TA ? rs_select(mA, bA, sA, W, r) : N + rs_select(mA, bA, sA, W, r - TA);
+                            }
+                        }
+                    }
+                }
+                if (lane == j) {
+                    my_ws = s;
+                    my_wl = end - s + 1;
+                }
+                s = end + 1 >= N ? end + 1 - N : end + 1;
+                s = s >= N ? s - N : s;
+            }
+            if (lane < nv) {
+                wstart[p0 + lane] = my_ws;
+                wlen[p0 + lane] = my_wl;
+            }
+        }
+        if (lane == 0) {
+            *next_start = s;
+            *done = 1;
+        }
+        return;
+    }
+    // Rank-space walk (TA >= K): the chain carries (rA, rI) = the A and I nodes before the
+    // pod's start, unrolled over rotations, instead of the start position.  A window that
+    // ends at an A node of rank e leaves (e + 1, the I nodes before that A node); one that
+    // ends at a candidate I node leaves (its A rank, its I index + 1) — no select and no
+    // rank lookup on the chain, about three dependent LDS round trips per pod.  Each pod's
+    // end goes out as a descriptor (A rank / I index / position, 2 tag bits) in wlen, and
+    // every wave turns the descriptors into windows afterwards.  DaemonSet pods walk the
+    // D nodes by position as before (their start from the previous descriptor).
+    __shared__ int64_t carry;
+    if (wv == 0) {
+        const uint64_t lt = (1ull << lane) - 1ull;
+        auto endpos = [&](int64_t dsc) -> int64_t {  // whole wave, uniform dsc
+            const int64_t v = dsc >> 2;
+            if ((dsc & 3) == 0) return rs_select(mA, bA, sA, W, v >= TA ? v - TA : v);
+            if ((dsc & 3) == 1) return (int64_t)iPos[v >= TI ? v - TI : v];
+            return v;
+        };
+        int64_t s = start;  // the start position, while spos
+        bool spos = true;
+        int64_t rA = rs_rank(mA, bA, start), rI = rs_rank(mI, bI, start);
+        int64_t dsc = 0;
+        for (int64_t p0 = 0; p0 < P; p0 += 64) {
+            const int nv = (int)min((int64_t)64, P - p0);
+            const int64_t tn = a.now[p0 + min(lane, nv - 1)];
+            const int32_t dn = a.flags ? (int32_t)(a.flags[p0 + min(lane, nv - 1)] & 1u) : 0;
+            int64_t my_d = 0;
+            for (int j = 0; j < nv; ++j) {
+                const int64_t t = readlane64(tn, j);
+                const bool d = __builtin_amdgcn_readlane(dn, j) != 0;
+                if (d) {
+                    if (!spos) {
+                        const int64_t e = endpos(dsc);
+                        s = e + 1 >= N ? e + 1 - N : e + 1;
+                    }
+                    int64_t end;
+                    if (TD < K) {
+                        end = s + N - 1;
+                    } else {
+                        const int64_t r = rs_rank(mD, bD, s) + K - 1;
+                        end = r < TD ? rs_select(mD, bD, sD, W, r) : N + rs_select(mD, bD, sD, W, r - TD);
+                    }
+                    const int64_t en = end >= N ? end - N : end;
+                    dsc = en * 4 + 2;
+                    s = en + 1 >= N ? en + 1 - N : en + 1;
+                    spos = true;
+                    rA = rs_rank(mA, bA, s);
+                    rI = rs_rank(mI, bI, s);
+                } else {
+                    const int64_t rT = rA + K - 1;  // the A-only window's last A node (unrolled rank)
+                    // candidates: I nodes from index rI before A node rT (A rank <= rT) with fth <= t
+                    int64_t c_lt = 0, cbase = 0, nin = 0, hit = -1, hra = 0;
                     for (int64_t q0 = 0; q0 < TI; q0 += 64) {
-                        const int64_t q = q0 + lane;
-                        int64_t idx = rI0 + q;
-                        const bool wrap = idx >= TI;
-                        idx -= wrap ? TI : 0;
-                        const int64_t ic = min(idx, TI - 1);
-                        const int64_t y = (int64_t)iPos[ic] + (wrap ? N : 0);
-                        const bool inr = q < TI && y <= xA;
+                        const int64_t q = q0 + lane, h = rI + q;
+                        const bool wrap = h >= TI;
+                        const int64_t ic = min(h - (wrap ? TI : 0), TI - 1);
+                        const int64_t ra = (int64_t)iRA[ic] + (wrap ? TA : 0);
+                        const bool inr = q < TI && ra <= rT;
                         const uint64_t rm = __ballot(inr);
                         if (!rm) break;
                         const bool cand = inr && iFth[ic] <= t;
                         const uint64_t cm = __ballot(cand);
-                        const int64_t ra = (int64_t)iRA[ic] + (wrap ? TA : 0);  // (built with the list)
-                        const int64_t mr = ra - rA0 + cbase + __popcll(cm & lt);
+                        const int64_t mr = ra - rA + cbase + __popcll(cm & lt);  // merged rank in the window
                         c_lt += __popcll(__ballot(cand && mr < K - 1));
                         const uint64_t eq = __ballot(cand && mr == K - 1);
                         if (eq) {
-                            hitpos = readlane64(y, __ffsll((long long)eq) - 1);
+                            const int l = __ffsll((long long)eq) - 1;
+                            hit = rI + q0 + l;
+                            hra = readlane64(ra, l);
                             break;
                         }
                         cbase += __popcll(cm);
+                        nin += __popcll(rm);
                         if (rm != ~0ull) break;  // the window's last in-range node was in this chunk
                     }
-                    if (hitpos >= 0) {
-                        end = hitpos;
-                    } else if (TA >= K && c_lt == 0) {
-                        end = xA;
-                    } else {
-                        // the A node c_lt before xA: inside xA's word when it holds that many below it
-                        const int xb = (int)((xA >= N ? xA - N : xA) & 63);  // xA's bit in its word
-                        const int below = TA >= K ? __popcll(wA & ((1ull << xb) - 1ull)) : -1;
-                        if (c_lt <= below) {
-                            end = xA - xb + nth_set_bit(wA, below - (int)c_lt + 1);
-                        } else {
-                            const int64_t r = rA0 + K - 1 - c_lt;
-                            end = r < TA ? rs_select(mA, bA, sA, W, r) : N + rs_select(mA, bA, sA, W, r - TA);
+                    if (hit >= 0) {  // the K-th feasible node is a candidate
+                        dsc = hit * 4 + 1;
+                        rA = hra;
+                        rI = hit + 1;
+                    } else {  // an A node: c_lt candidates took the places of the last A nodes
+                        const int64_t e = rT - c_lt;
+                        dsc = e * 4;
+                        rA = e + 1;
+                        if (c_lt == 0) {
+                            rI += nin;
+                        } else {  // the I nodes before A node e: a prefix of the list from rI
+                            int64_t cnt = 0;
+                            for (int64_t q0 = 0; q0 < TI; q0 += 64) {
+                                const int64_t q = q0 + lane, h = rI + q;
+                                const bool wrap = h >= TI;
+                                const int64_t ic = min(h - (wrap ? TI : 0), TI - 1);
+                                const int64_t ra = (int64_t)iRA[ic] + (wrap ? TA : 0);
+                                const uint64_t bm = __ballot(q < TI && ra <= e);
+                                cnt += __popcll(bm);
+                                if (bm != ~0ull) break;
+                            }
+                            rI += cnt;
                         }
                     }
+                    if (rA >= TA && rI >= TI) {  // past every A and I node of this rotation
+                        rA -= TA;
+                        rI -= TI;
+                    }
+                    spos = false;
                 }
+                if (lane == j) my_d = dsc;
             }
-            if (lane == j) {
-                my_ws = s;
-                my_wl = end - s + 1;
-            }
-            s = end + 1 >= N ? end + 1 - N : end + 1;
-            s = s >= N ? s - N : s;
+            if (lane < nv) wlen[p0 + lane] = my_d;
         }
-        if (lane < nv) {
-            wstart[p0 + lane] = my_ws;
-            wlen[p0 + lane] = my_wl;
+        if (!spos && P > 0) {
+            const int64_t e = endpos(dsc);
+            s = e + 1 >= N ? e + 1 - N : e + 1;
+        }
+        if (lane == 0) {
+            *next_start = s;
+            *done = 1;
         }
     }
-    if (lane == 0) {
-        *next_start = s;
-        *done = 1;
+    __syncthreads();  // the descriptors (global, wave 0's stores) in
+    // each pod's window end position -> wstart
+    for (int64_t p = threadIdx.x; p < P; p += kRsT) {
+        const int64_t dd = wlen[p], v = dd >> 2;
+        int64_t e;
+        if ((dd & 3) == 0) e = rs_select_lane(mA, bA, sA, W, TA, v >= TA ? v - TA : v);
+        else if ((dd & 3) == 1) e = (int64_t)iPos[v >= TI ? v - TI : v];
+        else e = v;
+        wstart[p] = e;
+    }
+    __syncthreads();
+    // windows: pod p starts after pod p - 1's end (the queue's first at `start`)
+    for (int64_t c0 = 0; c0 < P; c0 += kRsT) {
+        const int64_t p = c0 + threadIdx.x;
+        int64_t e = 0, ep = 0;
+        if (p < P) {
+            e = wstart[p];
+            ep = p == 0 ? start - 1 : (threadIdx.x == 0 ? carry : wstart[p - 1]);
+        }
+        __syncthreads();  // the chunk's ends read before they are overwritten
+        if (p < P) {
+            const int64_t s0 = ep + 1 >= N ? ep + 1 - N : ep + 1;
+            int64_t dl = e - s0;
+            if (dl < 0) dl += N;
+            wstart[p] = s0;
+            wlen[p] = dl + 1;
+        }
+        if (threadIdx.x == kRsT - 1) carry = e;
+        __syncthreads();
     }
 }
 

@@ -181,3 +181,35 @@ def test_select_chain_forms_agree(N, P, step_ns, pct):
     for name, g, r in zip(("chosen", "total", "wstart", "wlen"), got[:4], ref[:4]):
         assert np.array_equal(g, r), (name, np.nonzero(g != r)[0][:5])
     assert got[4] == ref[4]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,P,step_ns,pct,ds_frac,ok_frac,start", [
+    (2000, 1500, 1_000_000_000, 0, 0.0, 0.9, 0),          # many rotations, no DaemonSet pods
+    (2000, 1500, 1_000_000_000, 0, 0.3, 0.9, 1999),       # DaemonSet pods between rank-space runs
+    (5000, 800, 20_000_000_000, 1, 0.1, 0.95, 4321),      # tiny windows, many in-range nodes
+    (777, 900, 5_000_000_000, 40, 0.05, 0.6, 13),         # windows near the A count
+    (3000, 400, 1_000_000_000, 60, 0.2, 0.3, 5),          # fewer A nodes than a window: position walk
+    (64 * 300 + 17, 700, 2_000_000_000, 0, 1.0, 0.8, 9),  # every pod a DaemonSet pod
+])
+def test_select_rank_walk_agrees(N, P, step_ns, pct, ds_frac, ok_frac, start):
+    """The rank-space walk (window ends as A ranks / I indices, positions resolved after the
+    chain) equals the streaming chain kernel pod for pod, across DaemonSet mixes, window
+    sizes, wrap-arounds over many rotations and the position-walk fallback."""
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, N, P, seed=N * 7 + P, pod_step_ns=step_ns, ds_frac=ds_frac)
+    rng = np.random.default_rng(N + 1)
+    ok = rng.random(N) < ok_frac
+    eng = engine_for(spec, c)
+    got = _run(eng, c, ok, None, 3, pct, start, 0)
+    eng.set_option("sel_chain", 1)
+    ref = _run(eng, c, ok, None, 3, pct, start, 0)
+    eng.close()
+    for name, g, r in zip(("chosen", "total", "wstart", "wlen"), got[:4], ref[:4]):
+        assert np.array_equal(g, r), (name, np.nonzero(g != r)[0][:5])
+    assert got[4] == ref[4]
+    if N <= 3000 and P <= 900:
+        off, osc, _ = oracle_soa(spec, c)
+        want = S.framework_select(off, osc, c.ds, ok, None, 3, pct, start, 0)
+        for name, g, w in zip(("chosen", "total", "wstart", "wlen"), got[:4], want[:4]):
+            assert np.array_equal(g, w), (name, np.nonzero(g != w)[0][:5])
