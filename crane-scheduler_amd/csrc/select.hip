@@ -550,7 +550,8 @@ __global__ __launch_bounds__(kRsT) void k_sel_chain_rs(SelArgs a, const int64_t*
         };
         int64_t s = start;  // the start position, while spos
         bool spos = true;
-        int64_t rA = rs_rank(mA, bA, start), rI = rs_rank(mI, bI, start);
+        const int32_t TA32 = (int32_t)TA, TI32 = (int32_t)TI, K32 = (int32_t)K;
+        int32_t rA = (int32_t)rs_rank(mA, bA, start), rI = (int32_t)rs_rank(mI, bI, start);
         int64_t dsc = 0;
         for (int64_t p0 = 0; p0 < P; p0 += 64) {
             const int nv = (int)min((int64_t)64, P - p0);
@@ -576,62 +577,68 @@ __global__ __launch_bounds__(kRsT) void k_sel_chain_rs(SelArgs a, const int64_t*
                     dsc = en * 4 + 2;
                     s = en + 1 >= N ? en + 1 - N : en + 1;
                     spos = true;
-                    rA = rs_rank(mA, bA, s);
-                    rI = rs_rank(mI, bI, s);
+                    rA = (int32_t)rs_rank(mA, bA, s);
+                    rI = (int32_t)rs_rank(mI, bI, s);
                 } else {
-                    const int64_t rT = rA + K - 1;  // the A-only window's last A node (unrolled rank)
+                    // (32-bit ranks and indices: N <= 131,072, so unrolled ranks stay below 2^19)
+                    const int32_t rT = rA + K32 - 1;  // the A-only window's last A node (unrolled rank)
                     // candidates: I nodes from index rI before A node rT (A rank <= rT) with fth <= t
-                    int64_t c_lt = 0, cbase = 0, nin = 0, hit = -1, hra = 0;
-                    for (int64_t q0 = 0; q0 < TI; q0 += 64) {
-                        const int64_t q = q0 + lane, h = rI + q;
-                        const bool wrap = h >= TI;
-                        const int64_t ic = min(h - (wrap ? TI : 0), TI - 1);
-                        const int64_t ra = (int64_t)iRA[ic] + (wrap ? TA : 0);
-                        const bool inr = q < TI && ra <= rT;
+                    int32_t c_lt = 0, cbase = 0, nin = 0, hit = -1, hra = 0, ra0 = 0;
+                    bool one = true;  // the scan stopped in its first chunk (ra0 holds its A ranks)
+                    for (int32_t q0 = 0; q0 < TI32; q0 += 64) {
+                        const int32_t q = q0 + lane, h = rI + q;
+                        const bool wrap = h >= TI32;
+                        const int32_t ic = min(h - (wrap ? TI32 : 0), TI32 - 1);
+                        const int32_t ra = (int32_t)iRA[ic] + (wrap ? TA32 : 0);
+                        if (q0 == 0) ra0 = ra;
+                        const bool inr = q < TI32 && ra <= rT;
                         const uint64_t rm = __ballot(inr);
                         if (!rm) break;
                         const bool cand = inr && iFth[ic] <= t;
                         const uint64_t cm = __ballot(cand);
-                        const int64_t mr = ra - rA + cbase + __popcll(cm & lt);  // merged rank in the window
-                        c_lt += __popcll(__ballot(cand && mr < K - 1));
-                        const uint64_t eq = __ballot(cand && mr == K - 1);
+                        const int32_t mr = ra - rA + cbase + __popcll(cm & lt);  // merged rank in the window
+                        c_lt += __popcll(__ballot(cand && mr < K32 - 1));
+                        const uint64_t eq = __ballot(cand && mr == K32 - 1);
                         if (eq) {
                             const int l = __ffsll((long long)eq) - 1;
                             hit = rI + q0 + l;
-                            hra = readlane64(ra, l);
+                            hra = __builtin_amdgcn_readlane(ra, l);
                             break;
                         }
                         cbase += __popcll(cm);
                         nin += __popcll(rm);
                         if (rm != ~0ull) break;  // the window's last in-range node was in this chunk
+                        one = false;
                     }
                     if (hit >= 0) {  // the K-th feasible node is a candidate
-                        dsc = hit * 4 + 1;
+                        dsc = (int64_t)hit * 4 + 1;
                         rA = hra;
                         rI = hit + 1;
                     } else {  // an A node: c_lt candidates took the places of the last A nodes
-                        const int64_t e = rT - c_lt;
-                        dsc = e * 4;
+                        const int32_t e = rT - c_lt;
+                        dsc = (int64_t)e * 4;
                         rA = e + 1;
                         if (c_lt == 0) {
                             rI += nin;
-                        } else {  // the I nodes before A node e: a prefix of the list from rI
-                            int64_t cnt = 0;
-                            for (int64_t q0 = 0; q0 < TI; q0 += 64) {
-                                const int64_t q = q0 + lane, h = rI + q;
-                                const bool wrap = h >= TI;
-                                const int64_t ic = min(h - (wrap ? TI : 0), TI - 1);
-                                const int64_t ra = (int64_t)iRA[ic] + (wrap ? TA : 0);
-                                const uint64_t bm = __ballot(q < TI && ra <= e);
+                        } else if (one) {  // the I nodes before A node e: a prefix of the first chunk
+                            rI += __popcll(__ballot(lane < TI32 && ra0 <= e));
+                        } else {  // ... or of the chunks from rI
+                            int32_t cnt = 0;
+                            for (int32_t q0 = 0; q0 < TI32; q0 += 64) {
+                                const int32_t q = q0 + lane, h = rI + q;
+                                const bool wrap = h >= TI32;
+                                const int32_t ic = min(h - (wrap ? TI32 : 0), TI32 - 1);
+                                const int32_t ra = (int32_t)iRA[ic] + (wrap ? TA32 : 0);
+                                const uint64_t bm = __ballot(q < TI32 && ra <= e);
                                 cnt += __popcll(bm);
                                 if (bm != ~0ull) break;
                             }
                             rI += cnt;
                         }
                     }
-                    if (rA >= TA && rI >= TI) {  // past every A and I node of this rotation
-                        rA -= TA;
-                        rI -= TI;
+                    if (rA >= TA32 && rI >= TI32) {  // past every A and I node of this rotation
+                        rA -= TA32;
+                        rI -= TI32;
                     }
                     spos = false;
                 }
