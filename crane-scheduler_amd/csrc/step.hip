@@ -108,9 +108,11 @@ constexpr int kK3sThreads = kK3sWaves * 64;
 constexpr int kK3sPPL = 4;                          // pods per lane
 constexpr int kK3sPods = kK3sThreads * kK3sPPL;     // pods per workgroup (= kPodTile)
 // producer blocks per workgroup aimed for (launches over kMaxWg workgroups are capped first):
-// config 3 (391 blocks) then takes 16 workgroups per tile; 32 per tile (16 blocks) measured
-// 0.0128 vs 0.0123 ms per batch with 4 in flight (engine option k3s_blocks, tools/gpu_opt_probe.sh)
-constexpr int kK3sBlkPerWg = 32;
+// 64 -> config 3 (391 blocks) and the config-4 shard (489) take 8 workgroups per tile.  Round 3,
+// same box (option k3s_blocks, tools/gpu_r03k3.sh / gpu_r03k3b.sh): shard 0.0343 -> 0.0300 ms
+// per batch with 4 in flight (R 16 -> 8), config 3 unchanged (0.0120-0.0126); 32 per tile (16
+// blocks) had measured 0.0128 vs 0.0123 at config 3 in round 2
+constexpr int kK3sBlkPerWg = 64;
 // Work lists (k3s_eval) for slices of at most kK3sListBlk blocks, holding at most this many
 // straddling records / middle pieces (more: the blocks' teams).  Same-box A/B at configs 3 / 4
 // (one GPU) / 4 shard against the team loops alone: K3s 0.0397 -> 0.0364 ms per batch,
