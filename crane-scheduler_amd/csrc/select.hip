@@ -752,7 +752,20 @@ __global__ __launch_bounds__(kSelT) void k_sel_pairs(SelArgs a, int32_t chunk, i
                 multi = hi2 <= cmax;
             }
         }
-        for (int j = 0; j < nv; ++j) {
+        // the pods whose window meets this workgroup's node block (a few % of them with
+        // adaptive windows): the block's first node inside the window, or the window's first
+        // position inside the block (a position past N - 1 wrapping to the block: a spare pod)
+        uint64_t pm = __ballot(pv);
+        if (a.wstart) {
+            const int64_t nb0 = (int64_t)nb * kSelT;
+            int64_t r1 = nb0 - ws, r2 = ws - nb0;
+            if (r1 < 0) r1 += a.N;
+            if (r2 < 0) r2 += a.N;
+            pm = __ballot(pv && (r1 < wl || r2 < kSelT));
+        }
+        while (pm) {
+            const int j = __ffsll((long long)pm) - 1;
+            pm &= pm - 1;
             const int64_t t = readlane64(tn, j);
             const bool d = __builtin_amdgcn_readlane(fl, j) != 0;
             bool f = f0;
