@@ -73,23 +73,34 @@ class ShardedEngine:
 
     def schedule(self, now_ns, hv_ts_ns, d_now, d_flags, d_keys, stream=None, group=None):
         """One batch across all ranks: local step, then the MAX all-reduce (the global choice).
-        With RCCL ("nccl") the device keys are reduced in place on the current stream; a
-        CPU-only backend (gloo) reduces a host copy, written back into d_keys."""
+        The step and the all-reduce run on one stream: `stream`, or (None) a stream of this
+        shard that first waits for torch's current stream (the inputs) and that the current
+        stream then waits for (the reduced keys) — the engine's own stream is not ordered with
+        torch's, so the collective may not simply follow it.  RCCL ("nccl") reduces the device
+        keys in place on that stream; a CPU-only backend (gloo) reduces a host copy, written
+        back into d_keys."""
         import torch
         import torch.distributed as dist
 
+        cur = None
+        if stream is None:
+            cur = torch.cuda.current_stream(d_keys.device)
+            if getattr(self, "_stream", None) is None:
+                self._stream = torch.cuda.Stream(d_keys.device)
+            self._stream.wait_stream(cur)
+            stream = self._stream.cuda_stream
         self.step_keys(now_ns, hv_ts_ns, d_now, d_flags, d_keys, stream)
+        st = torch.cuda.ExternalStream(stream, device=d_keys.device)
         if dist.get_backend(group) == "nccl":
-            if stream is not None:  # the keys are produced on `stream`
-                with torch.cuda.stream(torch.cuda.ExternalStream(stream)):
-                    return allreduce_keys(d_keys, group)
-            return allreduce_keys(d_keys, group)
-        if stream is not None:
-            torch.cuda.ExternalStream(stream).synchronize()
+            with torch.cuda.stream(st):
+                allreduce_keys(d_keys, group)
         else:
-            torch.cuda.synchronize(d_keys.device)
-        h = allreduce_keys(d_keys.cpu(), group)
-        d_keys.copy_(h)
+            st.synchronize()
+            h = allreduce_keys(d_keys.cpu(), group)
+            with torch.cuda.stream(st):
+                d_keys.copy_(h)
+        if cur is not None:
+            cur.wait_stream(st)
         return d_keys
 
     def close(self):

@@ -206,9 +206,13 @@ struct crane_dyn {
     DevBuf<int32_t> spm1, ssm0;   // prefix / suffix key maxima of the sorted Step1 records
     DevBuf<int4> srows;           // per (pod tile, producer block): uniform keys + record ranges
     DevBuf<int2> sprow;           // ... and middle-piece ranges
-    // asynchronous work was enqueued on a caller stream since the last quiesce: calls that
-    // replace engine state first wait for the device
-    bool async_pending = false;
+    // caller streams that asynchronous work was enqueued on since the last quiesce: calls that
+    // replace engine state (and the synchronous calls on the engine stream) first wait for
+    // them — those streams only, not the device (another engine's batches and collectives
+    // keep running).  A handle is kept only until that wait.
+    std::vector<hipStream_t> busy;
+    DevBuf<unsigned char> upd_dev;   // crane_dyn_update_nodes / _node_steps_subset staging
+    HostBuf<unsigned char> upd_host;
     // kernel timing (crane_dyn_set_profiling)
     bool prof = false;
     EngineTimer timer;
@@ -633,23 +637,27 @@ static int flush_heap_slots(crane_dyn* h) {
     return CRANE_OK;
 }
 
-// After enqueueing work that reads engine buffers on a caller stream.  (Round 2 recorded a
-// completion event on the stream per call: its marker packet between two batches cost
-// 3 us of a config-3 batch's latency, 0.038 -> 0.035 ms, and 3 % of the in-flight rate.)
+// After enqueueing work that reads engine buffers on a caller stream: remember the stream
+// (no per-call HIP call: a completion event recorded per call, round 2, put a marker packet
+// between batches that cost 3 us of a config-3 batch's latency and 3 % of the in-flight rate).
 static int mark_busy(crane_dyn* h, hipStream_t st) {
-    if (st != h->stream) h->async_pending = true;  // engine-stream work is ordered by the stream itself
+    if (st == h->stream) return CRANE_OK;  // engine-stream work is ordered by the stream itself
+    for (hipStream_t s : h->busy)
+        if (s == st) return CRANE_OK;
+    h->busy.push_back(st);
     return CRANE_OK;
 }
 
 // Before changing or reallocating buffers that asynchronous calls read (node SoA, binding
-// log, scratch): wait for the device (every stream of the process: a superset of this
-// engine's caller-stream work, with no per-call cost and no stream handle kept past its
-// call).  State changes are per snapshot sync / controller tick, not per batch.
+// log, scratch), and before synchronous work on the engine stream: wait for the caller
+// streams this engine enqueued work on since the last wait — not the device, so other
+// engines' batches and collectives in flight are not drained.  State changes are per
+// snapshot sync / controller tick, not per batch.
 static int quiesce(crane_dyn* h) {
-    if (!h->async_pending) return CRANE_OK;
+    if (h->busy.empty()) return CRANE_OK;
     HIPTRY(h, hipSetDevice(h->device));
-    HIPTRY(h, hipDeviceSynchronize());
-    h->async_pending = false;
+    for (hipStream_t s : h->busy) HIPTRY(h, hipStreamSynchronize(s));
+    h->busy.clear();
     return CRANE_OK;
 }
 
@@ -697,7 +705,8 @@ int crane_dyn_destroy(crane_dyn* h) {
         (void)hipSetDevice(h->device);
         (void)hipStreamSynchronize(h->stream);
     }
-    if (h->async_pending) (void)hipDeviceSynchronize();
+    for (hipStream_t s : h->busy) (void)hipStreamSynchronize(s);
+    h->busy.clear();
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->ev.clear();
     h->val.release(); h->hv.release(); h->ts.release(); h->hv_ts.release(); h->rec.release();
@@ -712,7 +721,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->sperm.release(); h->scnt.release(); h->stile.release(); h->sbatch.release(); h->sq.release(); h->sqm.release(); h->snq.release(); h->spnow.release(); h->smid.release(); h->sstep1.release(); h->sstage.release();
     h->spm1.release(); h->ssm0.release(); h->srows.release(); h->sprow.release();
     h->sel_fth.release(); h->sel_win.release(); h->sel_state.release(); h->sel_keys.release();
-    h->stp_dev.release(); h->stp_host.release();
+    h->stp_dev.release(); h->stp_host.release(); h->upd_dev.release(); h->upd_host.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CRANE_OK;
@@ -894,6 +903,7 @@ int crane_dyn_refresh_hot_values(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns)
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
     HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
     int rc = hot_values_locked(h, now_ns, hv_ts_ns, h->stream);
     if (rc) return rc;
     HIPTRY(h, hipStreamSynchronize(h->stream));
@@ -907,6 +917,7 @@ int crane_dyn_hot_values(crane_dyn* h, int64_t n, double* hv_out) {
     if (n != h->N || (n > 0 && !hv_out)) return h->fail(CRANE_E_INVALID, "hv_out must hold one value per node");
     if (n == 0) return CRANE_OK;
     HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
     const double* src = nullptr;
     if (h->hv_from_counts) {
         if (h->counts_pending) {  // the node pass consumes the counts and keeps the values
@@ -998,6 +1009,7 @@ int crane_dyn_select(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_
     const int64_t N = h->N;
     if (start < 0 || (N > 0 && start >= N)) return h->fail(CRANE_E_INVALID, "start must be in [0, N)");
     HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     const int64_t K = crane_num_feasible_nodes_to_find(N, percentage);
     const bool window = K < N;  // otherwise every node is checked for every pod, the start stays
@@ -1097,6 +1109,7 @@ static int eval_host(crane_dyn* h, int64_t P, const int64_t* now_ns, const uint8
     if (P < 0 || (P > 0 && !now_ns)) return h->fail(CRANE_E_INVALID, "bad pod arrays");
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
     HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
     const int64_t N = h->N;
     const bool matrix = first_fail || score;
     int64_t pc = P;
@@ -1177,6 +1190,8 @@ int crane_dyn_node_steps(crane_dyn* h, int64_t t0_ns, int64_t t1_ns, int64_t n, 
     if (!(t0_ns < t1_ns)) return h->fail(CRANE_E_INVALID, "t0 must be before t1");
     if (n == 0) return CRANE_OK;
     HIPTRY(h, hipSetDevice(h->device));
+    // a fused step_keys_async on a caller stream may still be writing what the node pass reads
+    if (int rc = quiesce(h)) return rc;
     hipStream_t st = h->stream;
     if (h->rec_dirty) {
         int rc = node_pass_locked(h, st);
@@ -1203,6 +1218,128 @@ int crane_dyn_node_steps(crane_dyn* h, int64_t t0_ns, int64_t t1_ns, int64_t n, 
     std::memcpy(n_steps, p + o_ns, N);
     std::memcpy(first_fail, p + o_ff, N * (S + 1));
     std::memcpy(score, p + o_sc, N * (S + 1));
+    return CRANE_OK;
+}
+
+// k distinct local node indices in [0, N): CRANE_OK or the error
+static int check_subset(crane_dyn* h, int64_t k, const int64_t* idx) {
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes first");
+    if (k < 0 || (k > 0 && !idx)) return h->fail(CRANE_E_INVALID, "bad node index array");
+    if (k > h->N) return h->fail(CRANE_E_INVALID, "more indices than nodes");
+    std::vector<int64_t> sorted(idx, idx + k);
+    std::sort(sorted.begin(), sorted.end());
+    for (int64_t j = 0; j < k; ++j) {
+        if (sorted[j] < 0 || sorted[j] >= h->N) return h->fail(CRANE_E_INVALID, "node index out of range");
+        if (j > 0 && sorted[j] == sorted[j - 1]) return h->fail(CRANE_E_INVALID, "duplicate node index");
+    }
+    return CRANE_OK;
+}
+
+int crane_dyn_update_nodes(crane_dyn* h, int64_t k, const int64_t* idx, const double* val, const int64_t* ts,
+                           const double* hv, const int64_t* hv_ts) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    if (int rc = check_subset(h, k, idx)) return rc;
+    const int64_t M = h->dp.n_slots;
+    if (k > 0 && M > 0 && (!val || !ts)) return h->fail(CRANE_E_INVALID, "val/ts must not be NULL");
+    if ((hv == nullptr) != (hv_ts == nullptr)) return h->fail(CRANE_E_INVALID, "hv and hv_ts must both be set or NULL");
+    if (k == 0) return CRANE_OK;
+    HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
+    // the hot values come from the annotations again, as after crane_dyn_upload_nodes: records
+    // built from binding-log counts are stale as a whole
+    if (h->hv_from_counts) {
+        h->hv_from_counts = false;
+        h->counts_pending = false;
+        h->hx_pending = false;
+        h->rec_dirty = true;
+    }
+    if (hv && !h->have_hv) {  // the first hot-value annotations of the shard: the others have none
+        HIPTRY(h, h->hv.reserve((size_t)h->N));
+        HIPTRY(h, h->hv_ts.reserve((size_t)h->N));
+        HIPTRY(h, hipMemsetAsync(h->hv.p, 0, sizeof(double) * (size_t)h->N, h->stream));
+        HIPTRY(h, launch_fill_i64(h->hv_ts.p, h->N, kTsInvalid, h->stream));
+        h->have_hv = true;
+    }
+    // staging: idx [k] | val [M][k] | ts [M][k] | hv [k] | hv_ts [k]
+    const size_t K = (size_t)k, o_val = 8 * K, o_ts = o_val + 8 * (size_t)M * K, o_hv = o_ts + 8 * (size_t)M * K,
+                 o_hvt = o_hv + 8 * K, total = o_hvt + 8 * K;
+    HIPTRY(h, h->upd_host.reserve(total));
+    HIPTRY(h, h->upd_dev.reserve(total));
+    unsigned char* p = h->upd_host.p;
+    std::memcpy(p, idx, 8 * K);
+    if (M > 0) {
+        std::memcpy(p + o_val, val, 8 * (size_t)M * K);
+        std::memcpy(p + o_ts, ts, 8 * (size_t)M * K);
+    }
+    if (hv) {
+        std::memcpy(p + o_hv, hv, 8 * K);
+        std::memcpy(p + o_hvt, hv_ts, 8 * K);
+    }
+    HIPTRY(h, hipMemcpyAsync(h->upd_dev.p, p, hv ? total : o_hv, hipMemcpyHostToDevice, h->stream));
+    unsigned char* d = h->upd_dev.p;
+    UpdateArgs a{};
+    a.pol = h->dp;
+    a.N = h->N;
+    a.k = k;
+    a.idx = reinterpret_cast<const int64_t*>(d);
+    a.sval = reinterpret_cast<const double*>(d + o_val);
+    a.sts = reinterpret_cast<const int64_t*>(d + o_ts);
+    a.shv = hv ? reinterpret_cast<const double*>(d + o_hv) : nullptr;
+    a.shv_ts = hv ? reinterpret_cast<const int64_t*>(d + o_hvt) : nullptr;
+    a.val = h->val.p;
+    a.ts = h->ts.p;
+    a.hv = h->have_hv ? h->hv.p : nullptr;
+    a.hv_ts = h->have_hv ? h->hv_ts.p : nullptr;
+    a.rec = h->rec_dirty ? nullptr : h->rec.p;  // current records stay current
+    HIPTRY(h, launch_update_nodes(h->shape, a, h->stream));
+    // (waited for: the staging is reused, and work the caller enqueues next on its own
+    // streams must see the new columns)
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    return CRANE_OK;
+}
+
+int crane_dyn_node_steps_subset(crane_dyn* h, int64_t t0_ns, int64_t t1_ns, int64_t k, const int64_t* idx,
+                                uint8_t* n_steps, int64_t* bp, int8_t* first_fail, int8_t* score) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    if (int rc = check_subset(h, k, idx)) return rc;
+    if (k > 0 && (!n_steps || !bp || !first_fail || !score)) return h->fail(CRANE_E_INVALID, "NULL output");
+    if (!(t0_ns < t1_ns)) return h->fail(CRANE_E_INVALID, "t0 must be before t1");
+    if (k == 0) return CRANE_OK;
+    HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
+    hipStream_t st = h->stream;
+    if (h->rec_dirty) {
+        int rc = node_pass_locked(h, st);
+        if (rc) return rc;
+    }
+    // staging: out bp [k][S] | ns [k] | ff [k][S+1] | sc [k][S+1] | in idx [k]
+    const size_t S = (size_t)node_step_slots(h->shape), K = (size_t)k;
+    const size_t o_ns = 8 * K * S, o_ff = o_ns + K, o_sc = o_ff + K * (S + 1), o_out = o_sc + K * (S + 1);
+    const size_t o_idx = (o_out + 7) & ~(size_t)7, total = o_idx + 8 * K;
+    HIPTRY(h, h->upd_host.reserve(total));
+    HIPTRY(h, h->upd_dev.reserve(total));
+    std::memcpy(h->upd_host.p + o_idx, idx, 8 * K);
+    unsigned char* d = h->upd_dev.p;
+    HIPTRY(h, hipMemcpyAsync(d + o_idx, h->upd_host.p + o_idx, 8 * K, hipMemcpyHostToDevice, st));
+    MatrixArgs a{};
+    a.rec = h->rec.p;
+    a.N = k;
+    a.node_offset = h->node_offset;
+    a.wsum = h->dp.wsum;
+    a.noprio = h->dp.noprio;
+    std::memcpy(a.pred_orig, h->pred_orig, sizeof a.pred_orig);
+    HIPTRY(h, launch_node_steps(h->shape, a, t0_ns, t1_ns, d + o_ns, reinterpret_cast<int64_t*>(d),
+                                reinterpret_cast<int8_t*>(d + o_ff), reinterpret_cast<int8_t*>(d + o_sc), st,
+                                reinterpret_cast<const int64_t*>(d + o_idx)));
+    HIPTRY(h, hipMemcpyAsync(h->upd_host.p, d, o_out, hipMemcpyDeviceToHost, st));
+    HIPTRY(h, hipStreamSynchronize(st));
+    const unsigned char* p = h->upd_host.p;
+    std::memcpy(bp, p, 8 * K * S);
+    std::memcpy(n_steps, p + o_ns, K);
+    std::memcpy(first_fail, p + o_ff, K * (S + 1));
+    std::memcpy(score, p + o_sc, K * (S + 1));
     return CRANE_OK;
 }
 
@@ -1243,6 +1380,7 @@ int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before greedy placement");
     if (h->N > kGreedyMaxNodes) return h->fail(CRANE_E_INVALID, "greedy mode supports up to 64^4 nodes");
     HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
     hipStream_t st = h->stream;
     const int64_t N = h->N;
     // hot values from the binding log at `now`, annotation stamped `now` (fresh)

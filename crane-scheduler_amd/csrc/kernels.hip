@@ -12,24 +12,12 @@
 
 #include "dyn_types.hpp"
 #include "kernels.hpp"
+#include "node_rec.hpp"
 #include "step_node.hpp"
 
 namespace crane {
 
 thread_local KernelTimer* tl_ktimer = nullptr;
-
-// Go int(float64) on amd64 (CVTTSD2SQ): NaN and out-of-range -> INT64_MIN.
-// Used by stats.go:135 (int(score/weight)) and plugins.go:91 (int(hv*10)).
-__device__ __forceinline__ int64_t go_int(double x) {
-    if (!(x >= -9223372036854775808.0 && x < 9223372036854775808.0)) return INT64_MIN;
-    return (int64_t)x;
-}
-
-__device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {
-    int64_t r;
-    if (__builtin_add_overflow(a, b, &r)) return b > 0 ? INT64_MAX : INT64_MIN;
-    return r;
-}
 
 // ---------------------------------------------------------------- K2
 // Each binding b falls into the windows whose cutoff (now_unix -
@@ -277,36 +265,7 @@ void k1_node_pass(K1Args a, K1Step step) {
         if (step.st.rows) tile_prefetch(step.st, &tpre);
     }
     if (n < N) {
-#pragma unroll
-        for (int k = 0; k < PD; ++k) {
-            int64_t e = kTsInvalid;
-            if (k < pol.npd) {
-                const int64_t t = pt[k];
-                const double u = pv[k];
-                const double lim = pol.pred_limit[k];
-                // isOverLoad (stats.go:94-112): usable (stats.go:51-76), limit != 0, u > limit
-                const bool over = t != kTsInvalid && !(u < 0.0) && lim != 0.0 && u > lim;
-                if (over) e = sat_add(t, pol.pred_dur[k]);
-            }
-            r.e_pred[k] = e;
-        }
-#pragma unroll
-        for (int k = 0; k < PR; ++k) {
-            int64_t e = kTsInvalid;
-            double term = 0.0;
-            if (k < pol.npr) {
-                const int64_t t = qt[k];
-                const double u = qv[k];
-                if (t != kTsInvalid && !(u < 0.0)) {
-                    e = sat_add(t, pol.prio_dur[k]);
-                    // getScore (stats.go:89): (1. - usage) * Weight * float64(MaxNodeScore)
-                    term = (1.0 - u) * pol.prio_w[k];
-                    term = term * 100.0;
-                }
-            }
-            r.e_prio[k] = e;
-            r.t[k] = term;
-        }
+        rec_metrics<PD, PR>(pol, pt, pv, qt, qv, r);
         if (buckets || hx) {
             // annotateNodeHotValue (node.go:113-121): value += count / p.Count (Go int division)
             // window w counts the bindings of buckets >= its cutoff rank (K2)
@@ -337,18 +296,12 @@ void k1_node_pass(K1Args a, K1Step step) {
             r.pen = go_int(h * 10.0);
             r.e_hv = v >= 0 ? sat_add(hv_ts_counts, kHotActiveNs) : kTsInvalid;
         } else if (hv) {
-            const double h = hvl;
-            const int64_t t = hvt;
-            r.pen = go_int(h * 10.0);
-            r.e_hv = (t != kTsInvalid && !(h < 0.0)) ? sat_add(t, kHotActiveNs) : kTsInvalid;
+            rec_hot_annotation<PD, PR>(hvl, hvt, r);
         } else {
             r.pen = 0;
             r.e_hv = kTsInvalid;
         }
-        int64_t e_fail = kTsInvalid;
-#pragma unroll
-        for (int k = 0; k < PD; ++k) e_fail = max(e_fail, r.e_pred[k]);
-        r.e_fail = e_fail;
+        rec_fail<PD, PR>(r);
         if (out) lrec[threadIdx.x] = r;
     }
     CRANE_TSTAMP(a.trace, blockIdx.x, 2);

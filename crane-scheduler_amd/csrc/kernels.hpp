@@ -74,10 +74,32 @@ struct MatrixArgs {
 };
 hipError_t launch_matrix(int shape, const MatrixArgs& a, hipStream_t st);
 // Filter / Score of every node as step functions over [t0, t1) (crane_dyn_node_steps):
-// ns[n] breakpoints bp[n * S + j], values ff / sc[n * (S + 1) + j]; S = node_step_slots(shape)
+// ns[n] breakpoints bp[n * S + j], values ff / sc[n * (S + 1) + j]; S = node_step_slots(shape).
+// idx non-null: row n is node idx[n], for n < a.N (crane_dyn_node_steps_subset)
 int node_step_slots(int shape);
 hipError_t launch_node_steps(int shape, const MatrixArgs& a, int64_t t0, int64_t t1, uint8_t* ns, int64_t* bp,
-                             int8_t* ff, int8_t* sc, hipStream_t st);
+                             int8_t* ff, int8_t* sc, hipStream_t st, const int64_t* idx = nullptr);
+
+// Scatter update of k nodes' parsed annotations (crane_dyn_update_nodes, update.hip): the
+// staged columns go into the shard's SoA and, when the records are current, each changed
+// node's NodeRec is recomputed in place (the same rec_metrics / rec_hot_annotation as K1).
+struct UpdateArgs {
+    DevPolicy pol;
+    int64_t N, k;
+    const int64_t* idx;     // [k] local node indices, distinct
+    const double* sval;     // [M][k] staged values
+    const int64_t* sts;     // [M][k] staged timestamps
+    const double* shv;      // [k] staged node_hot_value or null (no annotation on these nodes)
+    const int64_t* shv_ts;  // [k]
+    double* val;            // [M][N] shard SoA
+    int64_t* ts;
+    double* hv;             // [N] or null (the shard holds no hot-value annotations)
+    int64_t* hv_ts;
+    void* rec;              // NodeRec [N] or null (records stale: the next node pass rebuilds them)
+};
+hipError_t launch_update_nodes(int shape, const UpdateArgs& a, hipStream_t st);
+// fill [n] int64 with v (hv_ts of a shard that had no hot-value annotations)
+hipError_t launch_fill_i64(int64_t* p, int64_t n, int64_t v, hipStream_t st);
 
 // Framework-level selection (select.hip): upstream kube-scheduler's percentageOfNodesToScore
 // window with a rotating start, the weighted sum of Dynamic's score and the other score

@@ -317,15 +317,16 @@ hipError_t launch_matrix(int shape, const MatrixArgs& a, hipStream_t st) {
 // a node's Filter (first failing predicate) and Score change only where `now` crosses one
 // of its expiries, so over [t0, t1) they are constant between the expiries inside it.  One
 // thread per node: the expiries in (t0, t1), sorted and deduplicated, and the values at t0
-// and at each of them (the same ff_at / score_at as every other path).
+// and at each of them (the same ff_at / score_at as every other path).  idx (subset form,
+// crane_dyn_node_steps_subset): output row n holds node idx[n] (a.N = the subset's size).
 template <int PD, int PR>
 __global__ __launch_bounds__(256) void k_node_steps(MatrixArgs a, int64_t t0, int64_t t1, uint8_t* __restrict__ ns,
                                                     int64_t* __restrict__ bp, int8_t* __restrict__ ffv,
-                                                    int8_t* __restrict__ scv) {
+                                                    int8_t* __restrict__ scv, const int64_t* __restrict__ idx) {
     constexpr int S = PD + PR + 1;
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (n >= a.N) return;
-    const NodeRec<PD, PR> r = static_cast<const NodeRec<PD, PR>*>(a.rec)[n];
+    const NodeRec<PD, PR> r = static_cast<const NodeRec<PD, PR>*>(a.rec)[idx ? idx[n] : n];
     int64_t e[S];
     int c = 0;
     auto put = [&](int64_t x) {
@@ -368,17 +369,17 @@ int node_step_slots(int shape) {
 
 template <int PD, int PR>
 static hipError_t steps_t(const MatrixArgs& a, int64_t t0, int64_t t1, uint8_t* ns, int64_t* bp, int8_t* ff,
-                          int8_t* sc, hipStream_t st) {
-    return klaunch("k_node_steps", k_node_steps<PD, PR>, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, st, a, t0,
-                   t1, ns, bp, ff, sc);
+                          int8_t* sc, const int64_t* idx, hipStream_t st) {
+    return klaunch(idx ? "k_node_steps_subset" : "k_node_steps", k_node_steps<PD, PR>,
+                   dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, st, a, t0, t1, ns, bp, ff, sc, idx);
 }
 hipError_t launch_node_steps(int shape, const MatrixArgs& a, int64_t t0, int64_t t1, uint8_t* ns, int64_t* bp,
-                             int8_t* ff, int8_t* sc, hipStream_t st) {
+                             int8_t* ff, int8_t* sc, hipStream_t st, const int64_t* idx) {
     if (a.N <= 0) return hipSuccess;
     switch (shape) {
-        case kShape4x6: return steps_t<4, 6>(a, t0, t1, ns, bp, ff, sc, st);
-        case kShape8x8: return steps_t<8, 8>(a, t0, t1, ns, bp, ff, sc, st);
-        default: return steps_t<16, 16>(a, t0, t1, ns, bp, ff, sc, st);
+        case kShape4x6: return steps_t<4, 6>(a, t0, t1, ns, bp, ff, sc, idx, st);
+        case kShape8x8: return steps_t<8, 8>(a, t0, t1, ns, bp, ff, sc, idx, st);
+        default: return steps_t<16, 16>(a, t0, t1, ns, bp, ff, sc, idx, st);
     }
 }
 

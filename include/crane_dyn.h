@@ -22,12 +22,17 @@
  * host arrays; the engine copies them during the call and keeps no pointer.
  * Calls on one engine are serialised by an internal mutex.  Asynchronous calls
  * (*_async) enqueue work that reads the engine's buffers on the caller's stream;
- * the calls that replace engine state (upload_nodes, upload_bindings,
- * binding_records, add_bindings, gc_bindings, destroy) first wait for all such
- * work (a device synchronize when asynchronous work was enqueued since the last
- * one), so they never change a buffer a kernel is still reading.  Asynchronous
- * calls on ONE engine from several streams must be ordered by the caller (they
- * share the engine's scratch): use one stream per engine.  Nothing in the
+ * the calls that replace engine state (upload_nodes, update_nodes,
+ * upload_bindings, binding_records, add_bindings, gc_bindings, destroy) and the
+ * synchronous calls that run on the engine's own stream (eval, eval_compact,
+ * node_steps, node_steps_subset, refresh_hot_values, hot_values, select, greedy)
+ * first wait for the caller streams this engine enqueued asynchronous work on
+ * since the last such wait — those streams only, not the device — so they never
+ * change a buffer a kernel is still reading.  The engine keeps a caller stream's
+ * handle until that wait: a stream passed to an *_async call must outlive the
+ * engine's next state change (or its destroy).  Asynchronous calls on ONE engine
+ * from several streams must be ordered by the caller (they share the engine's
+ * scratch): use one stream per engine.  Nothing in the
  * engine reads the environment; crane_dyn_set_option (tests / A-B tools only)
  * selects alternative kernel forms of the same results.
  */
@@ -143,6 +148,18 @@ int crane_dyn_upload_nodes(crane_dyn *h, int64_t n_nodes, int64_t node_offset,
                            const double *val, const int64_t *ts_ns,
                            const double *hv, const int64_t *hv_ts_ns);
 
+/* Replace the parsed annotations of k nodes of the shard, as the controller's patches change
+ * them (each (node, metric) sync patches the metric and node_hot_value, node.go:88-96,123-146,
+ * at every syncPolicy period, node.go:148-177) and the reference plugin reads them on its next
+ * call (stats.go:51-76).  idx[j] (distinct local node indices) gets val[m*k + j], ts_ns[m*k + j]
+ * for metric slot m and hv[j], hv_ts_ns[j] (hv NULL: those nodes carry no node_hot_value).
+ * The result equals crane_dyn_upload_nodes of the whole shard with those nodes' columns
+ * replaced (hot values come from the annotations again after a refresh from bindings); the
+ * node records of the changed nodes are recomputed in place, so crane_dyn_node_steps_subset
+ * of those nodes is all a table of answers needs.  Synchronous. */
+int crane_dyn_update_nodes(crane_dyn *h, int64_t k, const int64_t *idx, const double *val, const int64_t *ts_ns,
+                           const double *hv, const int64_t *hv_ts_ns);
+
 /* Upload the binding records (BindingRecords heap content, binding.go:14-19):
  * node = LOCAL node index of the shard (<0 or >= n_nodes: matches no node),
  * ts_s = Binding.Timestamp (Unix seconds).  Replaces the whole log (and ends
@@ -202,6 +219,11 @@ int crane_dyn_eval_compact(crane_dyn *h, int64_t n_pods, const int64_t *now_ns, 
 int32_t crane_dyn_step_slots(const crane_dyn *h);
 int crane_dyn_node_steps(crane_dyn *h, int64_t t0_ns, int64_t t1_ns, int64_t n, uint8_t *n_steps, int64_t *bp,
                          int8_t *first_fail, int8_t *score);
+/* The same answers for k distinct nodes idx[j] only, as compact rows j: n_steps[j], bp[j*S + ..],
+ * first_fail / score[j*(S+1) + ..] — equal to rows idx[j] of crane_dyn_node_steps over [t0, t1).
+ * What the drop-in plugin patches into its table for the nodes crane_dyn_update_nodes changed. */
+int crane_dyn_node_steps_subset(crane_dyn *h, int64_t t0_ns, int64_t t1_ns, int64_t k, const int64_t *idx,
+                                uint8_t *n_steps, int64_t *bp, int8_t *first_fail, int8_t *score);
 /* Device-resident matrix form, asynchronous on `stream`: d_first_fail[p*ld + i]
  * and d_score[p*ld + i] (int8) as crane_dyn_eval, any may be NULL; d_keys (NULL
  * = none) as crane_dyn_eval_keys_async. */

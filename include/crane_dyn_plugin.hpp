@@ -10,20 +10,27 @@
 //   DynamicArgs{PolicyConfigPath} + default           pkg/plugins/apis/config/types.go:10-14,
 //                                                     v1beta2/defaults.go:7-12
 //   IsDaemonsetPod                                    pkg/utils/utils.go:17-24
-// The k8s framework types are reduced to what the plugin touches.  Instead of
-// re-parsing annotations per call (stats.go:51-76), the plugin parses a node
-// snapshot once per generation (Sync: one bulk, threaded crane_parse_annotations
-// call).  A node's Filter and Score depend on `now` only through its expiries, so
-// the engine returns every node's answers as step functions of time over a horizon
-// (crane_dyn_node_steps: int8 first-fail and score per piece, computed by the
-// engine's kernels); a pod's per-node calls are then lookups at its `now` — no
-// device call per pod, a new table only when a pod's time leaves the horizon or the
-// snapshot generation changes.
+// The k8s framework types are reduced to what the plugin touches.  The reference
+// re-parses a node's annotations on every call (stats.go:51-76), so it always sees
+// the controller's latest patch (node.go:88-96,123-146).  Here the plugin keeps
+// every node's parsed annotations in the engine and every node's answers as step
+// functions of `now` over a time horizon (crane_dyn_node_steps: int8 first-fail and
+// score per piece, computed by the engine's kernels); a pod's per-node calls are
+// lookups at its `now`.  At the start of each scheduling cycle the plugin compares
+// every NodeInfo of the snapshot with the one it parsed (its Node object, which the
+// informer replaces on every update, and its Generation): only the changed nodes
+// are re-parsed, scattered into the engine (crane_dyn_update_nodes) and their table
+// rows rebuilt (crane_dyn_node_steps_subset).  The whole snapshot is parsed again
+// only when the node set changes, and the whole table only when a pod's time leaves
+// the horizon.
 //
 // Threading: the framework calls Filter/Score for one pod from 16 goroutines.
-// The first call of a cycle fetches the table under std::call_once; every call
-// after that reads the immutable table (and the immutable node -> index maps of
-// the snapshot generation it was built from) without taking a lock.
+// The first call of a cycle brings the plugin's state up to date under std::call_once;
+// every call after that reads it without taking a lock.  The state is patched in place
+// at the start of later cycles: the framework runs scheduling cycles one at a time, and
+// its binding cycles (which overlap the next scheduling cycle) call neither Filter nor
+// Score, so no call reads a row while it is patched.  A CycleState kept past its cycle
+// answers from the patched state.
 #pragma once
 
 #include <atomic>
@@ -61,25 +68,25 @@ class Status {
     Status() = default;
     Status(Code c, std::string m) : code_(c), msg_(std::move(m)) {}
     // the Filter's "Load[%s] of node[%s] is too high", formatted when read: a cycle's tens of
-    // thousands of Unschedulable answers are rarely read and need no allocation each
-    static Status Overloaded(const char* metric, const std::string* node) {
-        Status s(Code::Unschedulable, std::string());
+    // thousands of Unschedulable answers are rarely read.  The node name is copied (a Status
+    // may outlive the Node object, which the informer replaces on update); the metric name
+    // points into the plugin's policy, which lives as long as the plugin.
+    static Status Overloaded(const char* metric, const std::string& node) {
+        Status s(Code::Unschedulable, node);
         s.metric_ = metric;
-        s.node_ = node;
         return s;
     }
     Code code() const { return code_; }
     std::string message() const {
         if (!metric_) return msg_;
-        return "Load[" + std::string(metric_) + "] of node[" + *node_ + "] is too high";
+        return "Load[" + std::string(metric_) + "] of node[" + msg_ + "] is too high";
     }
     bool IsSuccess() const { return code_ == Code::Success; }
 
    private:
     Code code_ = Code::Success;
-    std::string msg_;
-    const char* metric_ = nullptr;     // (Overloaded: the policy's predicate name, lives with the plugin)
-    const std::string* node_ = nullptr;  // (the snapshot's node name, lives with the snapshot)
+    std::string msg_;               // (Overloaded: the node's name)
+    const char* metric_ = nullptr;  // (Overloaded: the policy's predicate name)
 };
 inline Status NewStatus(Code c, const std::string& m) { return Status(c, m); }
 
@@ -92,16 +99,22 @@ struct Pod {
     std::vector<OwnerReference> OwnerReferences;
 };
 
+// *v1.Node as the informer cache holds it: immutable once published — an update (such as the
+// controller's annotation patch) publishes a new object.
 struct Node {
     std::string Name;
     std::map<std::string, std::string> Annotations;
 };
 
-// framework.NodeInfo: Node() may be null.
+// framework.NodeInfo: node() may be null; the object is the snapshot's, stable for the node's
+// lifetime, and its Generation changes whenever the NodeInfo does (the framework's
+// nextGeneration()).
 class NodeInfo {
    public:
-    explicit NodeInfo(const Node* n = nullptr) : node_(n) {}
+    explicit NodeInfo(const Node* n = nullptr, int64_t generation = 0) : Generation(generation), node_(n) {}
     const Node* node() const { return node_; }
+    void SetNode(const Node* n) { node_ = n; }
+    int64_t Generation;
 
    private:
     const Node* node_;
@@ -109,8 +122,8 @@ class NodeInfo {
 
 // One scheduling cycle of one pod (framework.CycleState).  time.Now() for the
 // whole cycle (the reference calls it per Filter/Score call; declared deviation).
-// The Dynamic plugin's answer table of the cycle lives here (as plugins keep cycle
-// data in the framework's CycleState); Clone() (preemption dry runs) shares it.
+// The Dynamic plugin's answers of the cycle are referenced from here (as plugins keep
+// cycle data in the framework's CycleState); Clone() (preemption dry runs) shares them.
 struct CycleState {
     int64_t now_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
                          std::chrono::system_clock::now().time_since_epoch())
@@ -140,13 +153,13 @@ struct CycleState {
     std::string dyn_err_;
 };
 
-// The handle's snapshot lister (SnapshotSharedLister().NodeInfos()).
+// The handle's snapshot lister (SnapshotSharedLister().NodeInfos()), fixed for the length of
+// a scheduling cycle (the framework updates it before the cycle's first Filter).
 class Snapshot {
    public:
     virtual ~Snapshot() = default;
-    virtual std::vector<const Node*> List() const = 0;
-    virtual const Node* Get(const std::string& name, std::string* err) const = 0;
-    virtual uint64_t Generation() const = 0;  // changes when any node annotation changes
+    virtual const std::vector<const NodeInfo*>& List() const = 0;
+    virtual const NodeInfo* Get(const std::string& name, std::string* err) const = 0;
 };
 
 struct Handle {
@@ -180,6 +193,42 @@ struct NameHash {
     }
 };
 
+// Open-addressing map from an object address to a node index (power-of-two size, linear
+// probing, no deletion: a lookup is validated by the caller against the node's current
+// object, so an entry left behind by a replaced object is harmless).
+class AddrIndex {
+   public:
+    void reset(size_t n) {
+        size_t cap = 16;
+        while (cap < 2 * n + 16) cap <<= 1;
+        shift_ = 64 - __builtin_ctzll(cap);
+        slots_.assign(cap, {nullptr, -1});
+        used_ = 0;
+    }
+    void put(const void* k, int64_t i) {
+        size_t h = hash(k);
+        while (slots_[h].first && slots_[h].first != k) h = (h + 1) & (slots_.size() - 1);
+        if (!slots_[h].first) ++used_;
+        slots_[h] = {k, i};
+    }
+    int64_t get(const void* k) const {
+        size_t h = hash(k);
+        for (;;) {
+            const auto& s = slots_[h];
+            if (s.first == k) return s.second;
+            if (!s.first) return -1;
+            h = (h + 1) & (slots_.size() - 1);
+        }
+    }
+    bool crowded() const { return 2 * used_ > slots_.size(); }
+
+   private:
+    size_t hash(const void* k) const { return (size_t)((((uint64_t)(uintptr_t)k >> 4) * 0x9E3779B97F4A7C15ull) >> shift_); }
+    std::vector<std::pair<const void*, int64_t>> slots_;
+    int shift_ = 64;
+    size_t used_ = 0;
+};
+
 // ---------------------------------------------------------------- plugin
 class DynamicScheduler {
    public:
@@ -200,114 +249,83 @@ class DynamicScheduler {
         if (IsDaemonsetPod(pod)) return NewStatus(Code::Success, "");
         const Node* node = nodeInfo.node();
         if (!node) return NewStatus(Code::Error, "node not found");
-        const Table* t;
-        int64_t idx;
         std::string err;
-        if (!table_for(state, node, &t, &idx, &err)) return NewStatus(Code::Error, err);
-        const int k = t->first_fail[t->piece(idx, state.now_ns)];
-        if (k >= 0) return Status::Overloaded(policy().pred_name[k], &node->Name);  // plugins.go:64
+        const View* v = view_of(state, &err);
+        if (!v) return NewStatus(Code::Error, err);
+        const int64_t i = v->find_info(&nodeInfo, node);
+        if (i < 0) return NewStatus(Code::Error, "node \"" + node->Name + "\" not in the synced snapshot");
+        const int k = v->first_fail[v->piece(i, state.now_ns)];
+        if (k >= 0) return Status::Overloaded(policy().pred_name[k], node->Name);  // plugins.go:64
         return Status();
     }
 
-    // Score (plugins.go:73-98).  The node is looked up in the synced generation's index, which
-    // is the snapshot's node set; only a name outside it goes to the snapshot's own Get, for
-    // the reference's error (plugins.go:74-77).
+    // Score (plugins.go:73-98).  The node is looked up in the synced node set, which is the
+    // snapshot's; only a name outside it goes to the snapshot's own Get, for the reference's
+    // error (plugins.go:74-77).
     std::pair<int64_t, Status> Score(CycleState& state, const Pod& pod, const std::string& nodeName) {
         (void)pod;
         std::string err;
-        const Table* t = table_of(state, &err);
-        const int64_t idx = t ? t->snap->find_name(nodeName) : -1;
-        if (idx < 0) {
-            const Node* node = handle_.snapshot ? handle_.snapshot->Get(nodeName, &err) : nullptr;
+        const View* v = view_of(state, &err);
+        const int64_t i = v ? v->find_name(nodeName) : -1;
+        if (i < 0) {
+            const NodeInfo* ni = handle_.snapshot ? handle_.snapshot->Get(nodeName, &err) : nullptr;
             if (!err.empty() || !handle_.snapshot)
                 return {0, NewStatus(Code::Error, "getting node \"" + nodeName + "\" from Snapshot: " + err)};
-            if (!node) return {0, NewStatus(Code::Error, "node not found")};
-            if (!t) return {0, NewStatus(Code::Error, err)};
+            if (!ni || !ni->node()) return {0, NewStatus(Code::Error, "node not found")};
+            if (!v) return {0, NewStatus(Code::Error, err)};
             return {0, NewStatus(Code::Error, "node \"" + nodeName + "\" not in the synced snapshot")};
         }
-        return {(int64_t)t->score[t->piece(idx, state.now_ns)], Status()};
+        return {(int64_t)v->score[v->piece(i, state.now_ns)], Status()};
     }
 
-    // Re-parse the snapshot's annotations into the engine (once per generation).
+    // Bring the plugin's state up to date with the snapshot now (the first Filter / Score of a
+    // cycle does this itself).
     bool Sync(std::string* err) {
         std::lock_guard<std::mutex> g(mu_);
-        return sync_locked(err) != nullptr;
+        return sync_locked(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                               std::chrono::system_clock::now().time_since_epoch())
+                               .count(),
+                           err) != nullptr;
     }
 
-    // host threads of the once-per-sync annotation parse (<= 0: all hardware threads)
+    // host threads of the full-snapshot annotation parse (<= 0: all hardware threads)
     void SetParseThreads(int32_t n) { parse_threads_ = n; }
     // time span one answer table covers (a pod later than it gets a new table)
     void SetHorizon(int64_t ns) { horizon_ns_ = ns > 0 ? ns : 1; }
-    // answer tables built so far (one per horizon and snapshot generation)
-    uint64_t TablesBuilt() const { return tables_built_.load(); }
+    // work done so far: full tables built (a new node set or horizon), full snapshot parses,
+    // cycles that found changed nodes, and the changed nodes re-parsed over them
+    struct Counters {
+        uint64_t tables_built = 0, full_syncs = 0, incremental_syncs = 0, nodes_updated = 0;
+    };
+    Counters counters() const {
+        std::lock_guard<std::mutex> g(mu_);
+        return cnt_;
+    }
+    uint64_t TablesBuilt() const { return counters().tables_built; }
 
     friend std::pair<std::unique_ptr<DynamicScheduler>, std::string> NewDynamicScheduler(const Object& plArgs,
                                                                                          const Handle& h);
 
    private:
-    // one synced snapshot generation: node -> engine index (immutable once published).  The
-    // framework hands Filter the snapshot's own Node objects and Score their Name strings, so
-    // the address of a node's Name field is the key of both (a flat open-addressing table: an
-    // address equal to a synced node's &Name is that node's name); a name lookup remains for
-    // any other object.
-    struct Synced {
-        uint64_t generation;
-        std::unordered_map<std::string, int64_t, NameHash> index;
-        std::vector<const Node*> ptrs;                              // List() order
-        std::vector<std::pair<const std::string*, int64_t>> slots;  // power-of-two size, {nullptr, -1} empty
-        int shift = 64;
-        static uint64_t mix(const std::string* p) { return ((uint64_t)(uintptr_t)p >> 4) * 0x9E3779B97F4A7C15ull; }
-        void build(const std::vector<const Node*>& nodes) {
-            ptrs = nodes;
-            size_t cap = 16;
-            while (cap < 2 * nodes.size()) cap <<= 1;
-            shift = 64 - __builtin_ctzll(cap);
-            slots.assign(cap, {nullptr, -1});
-            for (size_t i = 0; i < nodes.size(); ++i) {
-                const std::string* k = &nodes[i]->Name;
-                size_t h = (size_t)(mix(k) >> shift);
-                while (slots[h].first && slots[h].first != k) h = (h + 1) & (cap - 1);
-                slots[h] = {k, (int64_t)i};
-            }
-        }
-        int64_t find(const Node* p) const { return find_key(&p->Name); }
-        int64_t find_name(const std::string& name) const { return find_key(&name); }
-        // the framework walks the nodes in List() order in chunks per goroutine: the node after
-        // this thread's last one (or a few further, for the feasible list) first — a pointer
-        // compare, no load of the node — then the table, then the name
-        int64_t find_key(const std::string* k) const {
-            thread_local const Synced* last_snap = nullptr;
-            thread_local int64_t last = -1;
-            if (last_snap == this) {
-                const int64_t n = (int64_t)ptrs.size();
-                for (int64_t i = last + 1; i < std::min(n, last + 5); ++i)
-                    if (&ptrs[(size_t)i]->Name == k) return last = i;
-            }
-            const int64_t i = find_slow(k);
-            last_snap = this;
-            last = i;
-            return i;
-        }
-        int64_t find_slow(const std::string* k) const {
-            size_t h = (size_t)(mix(k) >> shift);
-            for (;;) {
-                const auto& s = slots[h];
-                if (s.first == k) return s.second;
-                if (!s.first) break;
-                h = (h + 1) & (slots.size() - 1);
-            }
-            auto it = index.find(*k);
-            return it == index.end() ? -1 : it->second;
-        }
-    };
-    // every node's answers over [t0, t1) as step functions (immutable once published)
-    struct Table {
-        std::shared_ptr<const Synced> snap;
+    // The synced node set (List() order) and every node's answers over [t0, t1).
+    struct View {
+        std::vector<const NodeInfo*> infos;  // the snapshot's NodeInfo objects
+        std::vector<const Node*> nodes;      // the Node object each row was parsed from
+        std::vector<int64_t> gens;           // ... and its NodeInfo's Generation
+        std::unordered_map<std::string, int64_t, NameHash> by_name;
+        AddrIndex info_idx;  // NodeInfo address -> index (fixed for the node set)
+        AddrIndex name_idx;  // address of a node's Name -> index (entries added as Nodes are replaced)
         int64_t t0 = 0, t1 = 0;
         size_t S = 0;
         std::vector<uint8_t> n_steps;
         std::vector<int64_t> bp;
         std::vector<int8_t> first_fail, score;
+
+        void index_names() {
+            name_idx.reset(nodes.size());
+            for (size_t i = 0; i < nodes.size(); ++i)
+                if (nodes[i]) name_idx.put(&nodes[i]->Name, (int64_t)i);
+        }
         // index of node i's value at time t (t0 <= t < t1)
         size_t piece(int64_t i, int64_t t) const {
             const size_t nb = n_steps[(size_t)i];
@@ -316,113 +334,228 @@ class DynamicScheduler {
             while (j < nb && b[j] <= t) ++j;
             return (size_t)i * (S + 1) + j;
         }
+        // The framework walks the nodes in List() order in chunks per goroutine: the entry after
+        // this thread's last one (or a few further, for the feasible list) first — a pointer
+        // compare — then the address index, then the name.
+        int64_t find_info(const NodeInfo* ni, const Node* node) const {
+            thread_local const View* lv = nullptr;
+            thread_local int64_t last = -1;
+            const int64_t n = (int64_t)infos.size();
+            if (lv == this)
+                for (int64_t i = last + 1; i < std::min(n, last + 5); ++i)
+                    if (infos[(size_t)i] == ni) return last = i;
+            int64_t i = info_idx.get(ni);
+            if (i < 0) {  // a NodeInfo object that is not the snapshot's: by name
+                auto it = by_name.find(node->Name);
+                i = it == by_name.end() ? -1 : it->second;
+            }
+            lv = this;
+            last = i;
+            return i;
+        }
+        int64_t find_name(const std::string& name) const {
+            thread_local const View* lv = nullptr;
+            thread_local int64_t last = -1;
+            const int64_t n = (int64_t)nodes.size();
+            if (lv == this)
+                for (int64_t i = last + 1; i < std::min(n, last + 5); ++i)
+                    if (nodes[(size_t)i] && &nodes[(size_t)i]->Name == &name) return last = i;
+            int64_t i = name_idx.get(&name);
+            if (i >= 0 && !(nodes[(size_t)i] && &nodes[(size_t)i]->Name == &name)) i = -1;  // a replaced Node's
+            if (i < 0) {
+                auto it = by_name.find(name);
+                i = it == by_name.end() ? -1 : it->second;
+            }
+            lv = this;
+            last = i;
+            return i;
+        }
     };
 
     DynamicScheduler() = default;
 
-    std::shared_ptr<const Synced> sync_locked(std::string* err) {
+    const std::vector<std::string>& keys() {  // rows: metric slots 0..M-1, node_hot_value
+        if (keys_.empty()) {
+            const int32_t M = crane_dyn_num_metrics(eng_);
+            for (int32_t m = 0; m < M; ++m) keys_.emplace_back(crane_dyn_metric_name(eng_, m));
+            keys_.emplace_back(NodeHotValue);
+        }
+        return keys_;
+    }
+
+    // parse rows [key][n] of the nodes' annotation strings (NULL = key missing)
+    bool parse(const std::vector<const Node*>& nodes, int32_t threads, std::vector<double>* val,
+               std::vector<int64_t>* ts, std::string* err) {
+        const std::vector<std::string>& ks = keys();
+        const size_t R = ks.size(), n = nodes.size();
+        strs_.assign(R * n, nullptr);
+        lens_.assign(R * n, 0);
+        for (size_t i = 0; i < n; ++i) {
+            if (!nodes[i]) continue;
+            const auto& a = nodes[i]->Annotations;
+            for (size_t m = 0; m < R; ++m) {
+                auto it = a.find(ks[m]);
+                if (it == a.end()) continue;
+                strs_[m * n + i] = it->second.data();
+                lens_[m * n + i] = it->second.size();
+            }
+        }
+        val->resize(R * n);
+        ts->resize(R * n);
+        const int rc = zone_ ? crane_parse_annotations_tz((int64_t)(R * n), strs_.data(), lens_.data(), zone_,
+                                                         val->data(), ts->data(), threads)
+                             : crane_parse_annotations((int64_t)(R * n), strs_.data(), lens_.data(), tz_, val->data(),
+                                                       ts->data(), threads);
+        if (rc) *err = "annotation parse failed";
+        return rc == 0;
+    }
+
+    // every node's answers over [now, now + horizon) into v (sized for its node set)
+    bool build_table(View* v, int64_t now, std::string* err) {
+        const size_t N = v->infos.size();
+        v->t0 = now;
+        v->t1 = now > INT64_MAX - horizon_ns_ ? INT64_MAX : now + horizon_ns_;
+        v->S = (size_t)crane_dyn_step_slots(eng_);
+        v->n_steps.resize(N);
+        v->bp.resize(N * v->S);
+        v->first_fail.resize(N * (v->S + 1));
+        v->score.resize(N * (v->S + 1));
+        if (crane_dyn_node_steps(eng_, v->t0, v->t1, (int64_t)N, v->n_steps.data(), v->bp.data(),
+                                 v->first_fail.data(), v->score.data())) {
+            *err = crane_dyn_last_error(eng_);
+            return false;
+        }
+        ++cnt_.tables_built;
+        return true;
+    }
+
+    // a new node set: parse the whole snapshot, upload it, index it, build the table
+    std::shared_ptr<View> full_sync(const std::vector<const NodeInfo*>& L, int64_t now, std::string* err) {
+        auto v = std::make_shared<View>();
+        const size_t N = L.size();
+        v->infos = L;
+        v->nodes.resize(N);
+        v->gens.resize(N);
+        v->by_name.reserve(N);
+        v->info_idx.reset(N);
+        for (size_t i = 0; i < N; ++i) {
+            v->nodes[i] = L[i]->node();
+            v->gens[i] = L[i]->Generation;
+            v->info_idx.put(L[i], (int64_t)i);
+            if (v->nodes[i]) v->by_name.emplace(v->nodes[i]->Name, (int64_t)i);
+        }
+        v->index_names();
+        std::vector<double> val;
+        std::vector<int64_t> ts;
+        if (!parse(v->nodes, parse_threads_, &val, &ts, err)) return nullptr;
+        const size_t M = (size_t)crane_dyn_num_metrics(eng_);
+        if (crane_dyn_upload_nodes(eng_, (int64_t)N, 0, val.data(), ts.data(), val.data() + M * N,
+                                   ts.data() + M * N)) {
+            *err = crane_dyn_last_error(eng_);
+            return nullptr;
+        }
+        ++cnt_.full_syncs;
+        if (!build_table(v.get(), now, err)) return nullptr;
+        return v;
+    }
+
+    // the changed nodes: re-parse, scatter into the engine, rebuild their table rows
+    bool update(View* v, int64_t now, std::string* err) {
+        const std::vector<const NodeInfo*>& L = v->infos;
+        const size_t k = changed_.size();
+        cnodes_.resize(k);
+        for (size_t j = 0; j < k; ++j) cnodes_[j] = L[(size_t)changed_[j]]->node();
+        std::vector<double> val;
+        std::vector<int64_t> ts;
+        if (!parse(cnodes_, 1, &val, &ts, err)) return false;
+        const size_t M = (size_t)crane_dyn_num_metrics(eng_);
+        if (crane_dyn_update_nodes(eng_, (int64_t)k, changed_.data(), val.data(), ts.data(), val.data() + M * k,
+                                   ts.data() + M * k)) {
+            *err = crane_dyn_last_error(eng_);
+            return false;
+        }
+        for (size_t j = 0; j < k; ++j) {
+            const size_t i = (size_t)changed_[j];
+            v->nodes[i] = cnodes_[j];
+            v->gens[i] = L[i]->Generation;
+            if (cnodes_[j]) v->name_idx.put(&cnodes_[j]->Name, (int64_t)i);
+        }
+        if (v->name_idx.crowded()) v->index_names();  // entries of replaced Nodes pile up
+        ++cnt_.incremental_syncs;
+        cnt_.nodes_updated += k;
+        if (now < v->t0 || now >= v->t1) return true;  // the caller rebuilds the whole table
+        const size_t S = v->S;
+        rns_.resize(k);
+        rbp_.resize(k * S);
+        rff_.resize(k * (S + 1));
+        rsc_.resize(k * (S + 1));
+        if (crane_dyn_node_steps_subset(eng_, v->t0, v->t1, (int64_t)k, changed_.data(), rns_.data(), rbp_.data(),
+                                        rff_.data(), rsc_.data())) {
+            *err = crane_dyn_last_error(eng_);
+            return false;
+        }
+        for (size_t j = 0; j < k; ++j) {
+            const size_t i = (size_t)changed_[j];
+            v->n_steps[i] = rns_[j];
+            std::memcpy(&v->bp[i * S], &rbp_[j * S], 8 * S);
+            std::memcpy(&v->first_fail[i * (S + 1)], &rff_[j * (S + 1)], S + 1);
+            std::memcpy(&v->score[i * (S + 1)], &rsc_[j * (S + 1)], S + 1);
+        }
+        return true;
+    }
+
+    // The state for a cycle at `now`: compare the snapshot's NodeInfos with the synced ones.
+    std::shared_ptr<View> sync_locked(int64_t now, std::string* err) {
         if (!handle_.snapshot) {
             *err = "no snapshot";
             return nullptr;
         }
-        const uint64_t gen = handle_.snapshot->Generation();
-        if (synced_ && synced_->generation == gen) return synced_;
-        const auto nodes = handle_.snapshot->List();
-        const int32_t M = crane_dyn_num_metrics(eng_);
-        const size_t N = nodes.size();
-        auto snap = std::make_shared<Synced>();
-        snap->generation = gen;
-        snap->index.reserve(N);
-        snap->build(nodes);
-        // rows [metric slot 0..M-1, node_hot_value] x N of annotation strings (NULL = key missing)
-        std::vector<const char*> strs((size_t)(M + 1) * N, nullptr);
-        std::vector<size_t> lens((size_t)(M + 1) * N, 0);
-        std::vector<std::string> keys;
-        for (int32_t m = 0; m < M; ++m) keys.emplace_back(crane_dyn_metric_name(eng_, m));
-        keys.emplace_back(NodeHotValue);
-        for (size_t n = 0; n < N; ++n) {
-            snap->index.emplace(nodes[n]->Name, (int64_t)n);
-            const auto& a = nodes[n]->Annotations;
-            for (int32_t m = 0; m <= M; ++m) {
-                auto it = a.find(keys[(size_t)m]);
-                if (it == a.end()) continue;
-                strs[(size_t)m * N + n] = it->second.data();
-                lens[(size_t)m * N + n] = it->second.size();
+        const std::vector<const NodeInfo*>& L = handle_.snapshot->List();
+        std::shared_ptr<View> v = view_;
+        bool full = !v || L.size() != v->infos.size();
+        changed_.clear();
+        if (!full) {
+            const size_t n = L.size();
+            const NodeInfo* const* li = L.data();
+            const NodeInfo* const* vi = v->infos.data();
+            const Node* const* vn = v->nodes.data();
+            const int64_t* vg = v->gens.data();
+            for (size_t i = 0; i < n; ++i) {
+                const NodeInfo* x = li[i];
+                if (x != vi[i]) {
+                    full = true;
+                    break;
+                }
+                if (x->node() != vn[i] || x->Generation != vg[i]) changed_.push_back((int64_t)i);
             }
         }
-        std::vector<double> val((size_t)(M + 1) * N);
-        std::vector<int64_t> ts((size_t)(M + 1) * N);
-        const int prc = zone_ ? crane_parse_annotations_tz((int64_t)strs.size(), strs.data(), lens.data(), zone_,
-                                                           val.data(), ts.data(), parse_threads_)
-                              : crane_parse_annotations((int64_t)strs.size(), strs.data(), lens.data(), tz_,
-                                                        val.data(), ts.data(), parse_threads_);
-        if (prc) {
-            *err = "annotation parse failed";
-            return nullptr;
+        if (full) {
+            view_.reset();
+            view_ = full_sync(L, now, err);
+            return view_;
         }
-        const double* hv = val.data() + (size_t)M * N;
-        const int64_t* hv_ts = ts.data() + (size_t)M * N;
-        if (crane_dyn_upload_nodes(eng_, (int64_t)N, 0, val.data(), ts.data(), hv, hv_ts)) {
-            *err = crane_dyn_last_error(eng_);
-            return nullptr;
-        }
-        synced_ = std::move(snap);
-        table_.reset();
-        return synced_;
+        if (!changed_.empty() && !update(v.get(), now, err)) return nullptr;
+        if ((now < v->t0 || now >= v->t1) && !build_table(v.get(), now, err)) return nullptr;
+        return v;
     }
 
-    // The table covering the cycle's time (fetched by the first caller of the cycle).
-    const Table* table_of(CycleState& state, std::string* err) {
+    // The state of the cycle (brought up to date by the first caller of the cycle).
+    const View* view_of(CycleState& state, std::string* err) {
         std::call_once(state.dyn_once_, [&] {
             std::string e;
-            std::shared_ptr<const Table> t = table_at(state.now_ns, &e);
+            std::shared_ptr<const View> v;
+            {
+                std::lock_guard<std::mutex> g(mu_);  // one engine: syncs are serial
+                v = sync_locked(state.now_ns, &e);
+            }
             std::lock_guard<std::mutex> g(state.clone_mu_);
-            state.dyn_row_ = t;
+            state.dyn_row_ = v;
             state.dyn_err_ = e;
             state.dyn_done_ = true;
         });
-        const Table* t = static_cast<const Table*>(state.dyn_row_.get());
-        if (!t) *err = state.dyn_err_;
-        return t;
-    }
-
-    // ... and the node's index in it.
-    bool table_for(CycleState& state, const Node* node, const Table** table, int64_t* idx, std::string* err) {
-        const Table* t = table_of(state, err);
-        if (!t) return false;
-        const int64_t i = t->snap->find(node);
-        if (i < 0) {
-            *err = "node \"" + node->Name + "\" not in the synced snapshot";
-            return false;
-        }
-        *table = t;
-        *idx = i;
-        return true;
-    }
-
-    std::shared_ptr<const Table> table_at(int64_t now_ns, std::string* err) {
-        std::lock_guard<std::mutex> g(mu_);  // one engine: the sync and the table build are serial
-        std::shared_ptr<const Synced> snap = sync_locked(err);
-        if (!snap) return nullptr;
-        if (table_ && table_->snap == snap && table_->t0 <= now_ns && now_ns < table_->t1) return table_;
-        auto t = std::make_shared<Table>();
-        t->snap = snap;
-        t->t0 = now_ns;
-        t->t1 = now_ns > INT64_MAX - horizon_ns_ ? INT64_MAX : now_ns + horizon_ns_;
-        t->S = (size_t)crane_dyn_step_slots(eng_);
-        const size_t N = snap->index.size();
-        t->n_steps.resize(N);
-        t->bp.resize(N * t->S);
-        t->first_fail.resize(N * (t->S + 1));
-        t->score.resize(N * (t->S + 1));
-        if (crane_dyn_node_steps(eng_, t->t0, t->t1, (int64_t)N, t->n_steps.data(), t->bp.data(),
-                                 t->first_fail.data(), t->score.data())) {
-            *err = crane_dyn_last_error(eng_);
-            return nullptr;
-        }
-        ++tables_built_;
-        table_ = t;
-        return table_;
+        const View* v = static_cast<const View*>(state.dyn_row_.get());
+        if (!v) *err = state.dyn_err_;
+        return v;
     }
 
     Handle handle_;
@@ -432,10 +565,18 @@ class DynamicScheduler {
     int64_t tz_ = 8 * 3600;
     int32_t parse_threads_ = 16;  // the framework's parallelism (upstream default)
     int64_t horizon_ns_ = 60LL * 1000000000LL;
-    std::atomic<uint64_t> tables_built_{0};
-    std::mutex mu_;
-    std::shared_ptr<const Synced> synced_;
-    std::shared_ptr<const Table> table_;
+    mutable std::mutex mu_;
+    Counters cnt_;
+    std::shared_ptr<View> view_;
+    // scratch of the syncs (under mu_)
+    std::vector<std::string> keys_;
+    std::vector<int64_t> changed_;
+    std::vector<const Node*> cnodes_;
+    std::vector<const char*> strs_;
+    std::vector<size_t> lens_;
+    std::vector<uint8_t> rns_;
+    std::vector<int64_t> rbp_;
+    std::vector<int8_t> rff_, rsc_;
 };
 
 // NewDynamicScheduler (plugins.go:105-120): the same error strings.

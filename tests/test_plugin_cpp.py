@@ -116,3 +116,73 @@ def test_concurrent_filter_score_and_clones(driver, cluster_small, tmp_path):
         threaded = body[(2 * p + 1) * 2 * N:(2 * p + 2) * 2 * N]
         key = lambda r: (r[0], r[2])  # noqa: E731
         assert sorted(serial, key=key) == sorted(threaded, key=key), p
+
+
+def _stamp(unix_s):
+    import datetime as dt
+    return (dt.datetime(1970, 1, 1) + dt.timedelta(seconds=int(unix_s) + 8 * 3600)).strftime("%Y-%m-%dT%H:%M:%SZ")
+
+
+@pytest.mark.gpu
+def test_churn_through_plugin(driver, cluster_small, tmp_path):
+    """The controller keeps patching annotations between scheduling cycles (node.go:88-96,
+    123-146): each patch publishes a new Node object.  The plugin re-parses only the changed
+    nodes (crane_dyn_update_nodes + crane_dyn_node_steps_subset) and must answer every
+    Filter / Score exactly as the reference does on the CURRENT annotations (stats.go:51-76),
+    here the oracle's string mode on the patched annotation maps; a node added mid-way
+    changes the node set (a full sync)."""
+    import numpy as np
+    from oracle import oracle as O
+    c = cluster_small
+    pol = policy_from_json(c["policy"])
+    nodes = [dict(a) for a in c["nodes"]]
+    keys = [n for n, _ in pol["syncPolicy"]] + ["node_hot_value"]
+    rng = np.random.default_rng(5150)
+    lines = [f"policy\t{write_policy(tmp_path, pol)}"]
+    for i, a in enumerate(nodes):
+        lines.append(f"node\tnode-{i}")
+        lines += [f"anno\t{k}\t{v}" for k, v in a.items()]
+    expect = []
+    n_pat = 0
+    for p, pod in enumerate(c["pods"]):
+        now = pod["now_ns"]
+        if p == 7:  # a new node: the node set changes
+            nodes.append({"cpu_usage_avg_5m": f"0.10000,{_stamp(now // 10**9 - 5)}"})
+            lines.append(f"node\tnode-{len(nodes) - 1}")
+            lines += [f"anno\t{k}\t{v}" for k, v in nodes[-1].items()]
+        if p > 0:
+            for _ in range(int(rng.integers(1, 6))):
+                i = int(rng.integers(0, len(nodes)))
+                k = keys[int(rng.integers(0, len(keys)))]
+                r = rng.random()
+                n_pat += 1
+                if r < 0.1:
+                    nodes[i].pop(k, None)
+                    lines.append(f"unset\t{i}\t{k}")
+                    continue
+                st = _stamp(now // 10**9 - int(rng.integers(0, 700)))
+                v = (f"{int(rng.integers(0, 13))},{st}" if k == "node_hot_value" else
+                     "n/a" if r < 0.15 else f"{rng.random() * 1.2:.5f},{st}")
+                nodes[i][k] = v
+                lines.append(f"patch\t{i}\t{k}\t{v}")
+        lines.append(f"pod\tp{p}\t{now}\t{int(pod['daemonset'])}")
+        ff, sc, _ = O.eval_strings(pol, nodes, np.array([now], np.int64), np.array([pod["daemonset"]], np.uint8))
+        expect.append((ff[0].copy(), sc[0].copy(), len(nodes)))
+    lines.append("counters")
+    out = run(driver, "\n".join(lines) + "\n")
+    F = [o for o in out if o[0] == "F"]
+    S = [o for o in out if o[0] == "S"]
+    off = 0
+    for p, (ff, sc, N) in enumerate(expect):
+        for n in range(N):
+            f, s = F[off + n], S[off + n]
+            ds = c["pods"][p]["daemonset"]
+            assert f[3] == str(SUCCESS if (ds or ff[n] < 0) else UNSCHED), (p, n)
+            if not ds and ff[n] >= 0:
+                assert f[4] == f"Load[{pol['predicate'][ff[n]][0]}] of node[node-{n}] is too high", (p, n)
+            assert s[3] == str(sc[n]), (p, n)
+        off += N
+    C = [o for o in out if o[0] == "C"][0]
+    tables, full, incr, upd = (int(x) for x in C[1:5])
+    assert full == 2  # the first cycle and the one after the node was added
+    assert incr >= len(c["pods"]) - 3 and upd >= incr

@@ -108,14 +108,19 @@ def test_sharded_step_with_binding_logs():
 _TWO_PROC = dict(n_nodes=30_011, n_pods=3_000, seed=901, n_bind=300_000)
 
 
-def _two_proc_worker(rank, world, port, out):
+def _two_proc_worker(rank, world, port, out, own_stream=True, backend="gloo"):
     """One rank: a ShardedEngine on GPU 0 holding its node range and those nodes' bindings,
-    then ShardedEngine.schedule (local step + MAX all-reduce over gloo)."""
+    then ShardedEngine.schedule (local step + MAX all-reduce over gloo, or RCCL at world 1) on
+    a stream of the caller's or (own_stream False) with stream=None."""
     import torch
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     spec, c = _tied_cluster(_TWO_PROC["n_nodes"], _TWO_PROC["n_pods"], _TWO_PROC["seed"], _TWO_PROC["n_bind"])
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream(dev)
@@ -127,7 +132,11 @@ def _two_proc_worker(rank, world, port, out):
     d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
     now = int(synth.NOW0_NS)
     for rep in range(2):  # the second step re-runs K2 on the same log (idempotent)
-        se.schedule(now, now, d_now, d_flags, d_keys, st.cuda_stream)
+        if own_stream:
+            se.schedule(now, now, d_now, d_flags, d_keys, st.cuda_stream)
+        else:  # torch's current stream: the keys are read there right after
+            d_keys.fill_(-7)
+            se.schedule(now, now, d_now, d_flags, d_keys)
         if rank == 0:
             np.save(f"{out}.{rep}.npy", d_keys.cpu().numpy())
     dist.barrier()
@@ -135,10 +144,13 @@ def _two_proc_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_two_process_sharded_schedule(tmp_path):
+@pytest.mark.parametrize("world,own_stream,backend", [(2, True, "gloo"), (2, False, "gloo"), (1, False, "nccl")])
+def test_two_process_sharded_schedule(tmp_path, world, own_stream, backend):
     """Two processes on GPU 0 (one per rank, as bench.py --gpus 2 runs them), each with a
     ShardedEngine over half the nodes, combined by ShardedEngine.schedule's all-reduce: the
-    keys equal one engine over the whole cluster, and its chosen nodes equal the oracle's."""
+    keys equal one engine over the whole cluster, and its chosen nodes equal the oracle's.
+    stream=None orders the step and the collective after torch's current stream and before
+    its next read; RCCL runs at world size 1 (one GPU: two RCCL ranks cannot share it)."""
     import socket
 
     import torch
@@ -149,7 +161,8 @@ def test_two_process_sharded_schedule(tmp_path):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     out = str(tmp_path / "keys")
-    mp.start_processes(_two_proc_worker, args=(2, port, out), nprocs=2, start_method="spawn")
+    mp.start_processes(_two_proc_worker, args=(world, port, out, own_stream, backend), nprocs=world,
+                       start_method="spawn")
     spec, c = _tied_cluster(_TWO_PROC["n_nodes"], _TWO_PROC["n_pods"], _TWO_PROC["seed"], _TWO_PROC["n_bind"])
     dev = torch.device("cuda", 0)
     full = cd.Engine(cd.Policy(spec), 0)

@@ -1,17 +1,30 @@
 // dropin_bench.cpp — per-pod scheduling-cycle latency of the drop-in plugin
 // mirror (include/crane_dyn_plugin.hpp) the way the upstream framework drives
 // it: Filter on every node and Score on every feasible node from a pool of 16
-// threads (kube-scheduler's default parallelism), then selectHost.
+// threads (kube-scheduler's default parallelism), then selectHost — while the
+// controller keeps patching node annotations.
 //
-//   dropin_bench <policy file> <snapshot tsv> <pods tsv> [threads] [cpu]
+//   dropin_bench <policy file> <snapshot tsv> <pods tsv> [--threads N] [--cpu]
+//                [--churn X] [--churn-log path] [--seed S]
 //     snapshot tsv:  N<TAB>name   starts a node;  A<TAB>key<TAB>value  adds an annotation
 //     pods tsv:      P<TAB>uid<TAB>now_ns<TAB>daemonset(0/1)
-// Prints one JSON object: sync time (bulk parse + upload of the snapshot), the
-// per-pod cycle times with their parts (Filter fan-out, Score fan-out, selectHost),
-// and the chosen node of every pod (highest score, lowest index on ties: the
-// engine's declared tie-break, in place of upstream's random reservoir choice).
+// Prints one JSON object: the per-pod cycle times with their parts (the cycle's first
+// Filter call, which brings the plugin up to date; the Filter and Score fan-outs;
+// selectHost), the plugin's sync counters, and the chosen node of every pod (highest
+// score, lowest index on ties: the engine's declared tie-break, in place of upstream's
+// random reservoir choice).
 //
-// "cpu" (the dropin_cpu build, -DDROPIN_CPU, linked with the CPU oracle — bench.py's CPU
+// Churn (--churn X, X > 0): the controller's patch stream at X times its rate.  Every node
+// is re-synced for every syncPolicy metric at that metric's period / X (node.go:148-177,
+// each (node, metric) with its own phase); a sync patches the metric's annotation and then
+// node_hot_value (node.go:88-96,113-146), each stamped with the patch time in the local zone
+// (utils.GetLocalTime, Asia/Shanghai).  Pod p's cycle runs at its now_ns; the patches due in
+// (now_{p-1}, now_p] are published before it, as the informer would: each one a new Node
+// object and a new NodeInfo Generation.  --churn-log writes them (pod, node, key, value) so
+// the caller can recompute every pod's answer on the churned annotations.  At X = 1 and
+// 100k nodes with the shipped policy that is ~2,700 patches per simulated second.
+//
+// "--cpu" (the dropin_cpu build, -DDROPIN_CPU, linked with the CPU oracle — bench.py's CPU
 // baseline only): the same harness driving a CPU plugin whose Filter and Score re-parse
 // the node's annotations on every call, as the reference's getResourceUsage does
 // (stats.go:51-76), through the oracle's string mode (oracle/crane_oracle.c).
@@ -23,6 +36,9 @@
 #include <fstream>
 #include <functional>
 #include <iostream>
+#include <memory>
+#include <numeric>
+#include <queue>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -36,24 +52,121 @@
 using namespace crane::dynamic;
 using Clock = std::chrono::steady_clock;
 
+// The scheduler's snapshot as the informer keeps it: stable NodeInfo objects, each pointing
+// at the node's current (immutable) Node object; an update publishes a new Node object.
 struct BenchSnap : Snapshot {
-    std::vector<Node> nodes;
+    std::vector<std::unique_ptr<Node>> objs;
+    std::vector<std::unique_ptr<NodeInfo>> infos;
+    std::vector<const NodeInfo*> list;
     std::unordered_map<std::string, size_t, NameHash> by_name;
-    std::vector<const Node*> List() const override {
-        std::vector<const Node*> v;
-        v.reserve(nodes.size());
-        for (const auto& n : nodes) v.push_back(&n);
-        return v;
-    }
-    const Node* Get(const std::string& name, std::string* err) const override {
+    int64_t gen = 0;
+    const std::vector<const NodeInfo*>& List() const override { return list; }
+    const NodeInfo* Get(const std::string& name, std::string* err) const override {
         auto it = by_name.find(name);
         if (it == by_name.end()) {
             *err = "nodeinfo not found for node name \"" + name + "\"";
             return nullptr;
         }
-        return &nodes[it->second];
+        return infos[it->second].get();
     }
-    uint64_t Generation() const override { return 1; }
+    const Node& node(size_t i) const { return *objs[i]; }
+    void add(const std::string& name) {
+        by_name[name] = objs.size();
+        objs.emplace_back(new Node{name, {}});
+        infos.emplace_back(new NodeInfo(objs.back().get(), ++gen));
+        list.push_back(infos.back().get());
+    }
+    void patch(size_t i, const std::string& key, const std::string& value) {
+        std::unique_ptr<Node> n(new Node(*objs[i]));
+        n->Annotations[key] = value;
+        infos[i]->SetNode(n.get());
+        infos[i]->Generation = ++gen;
+        objs[i] = std::move(n);
+    }
+};
+
+// "YYYY-MM-DDTHH:MM:SSZ" of Unix second t in a fixed-offset zone (utils.TimeFormat, utils.go:11;
+// Asia/Shanghai has had no transition since 1991)
+static std::string local_stamp(int64_t t, int64_t off) {
+    int64_t s = t + off, days = s / 86400, sod = s % 86400;
+    if (sod < 0) {
+        sod += 86400;
+        --days;
+    }
+    // civil_from_days (Howard Hinnant)
+    days += 719468;
+    const int64_t era = (days >= 0 ? days : days - 146096) / 146097;
+    const int64_t doe = days - era * 146097;
+    const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    int64_t y = yoe + era * 400;
+    const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const int64_t mp = (5 * doy + 2) / 153;
+    const int64_t d = doy - (153 * mp + 2) / 5 + 1;
+    const int64_t m = mp < 10 ? mp + 3 : mp - 9;
+    if (m <= 2) ++y;
+    char buf[32];
+    std::snprintf(buf, sizeof buf, "%04lld-%02lld-%02lldT%02lld:%02lld:%02lldZ", (long long)y, (long long)m,
+                  (long long)d, (long long)(sod / 3600), (long long)(sod / 60 % 60), (long long)(sod % 60));
+    return buf;
+}
+
+static uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// The controller's patch stream (node.go:148-177): (node, syncPolicy entry) pairs due in time
+// order, each at its own phase within the entry's period.
+class Churn {
+   public:
+    struct Patch {
+        size_t node;
+        std::string key, value;
+    };
+    Churn(const crane_policy& pol, size_t n_nodes, int64_t t_start_ns, double scale, uint64_t seed) : seed_(seed) {
+        for (int32_t m = 0; m < pol.n_sync; ++m) {
+            if (pol.sync_period_ns[m] <= 0) continue;
+            names_.emplace_back(pol.sync_name[m]);
+            period_.push_back(std::max<int64_t>(1, (int64_t)((double)pol.sync_period_ns[m] / scale)));
+        }
+        std::vector<Ev> evs;
+        evs.reserve(n_nodes * names_.size());
+        for (size_t n = 0; n < n_nodes; ++n)
+            for (size_t m = 0; m < names_.size(); ++m) {
+                const int64_t ph = (int64_t)(mix64(seed_ ^ (n * 64 + m)) % (uint64_t)period_[m]);
+                evs.push_back({t_start_ns + ph, (uint32_t)n, (uint32_t)m});
+            }
+        q_ = std::priority_queue<Ev, std::vector<Ev>, std::greater<Ev>>(std::greater<Ev>(), std::move(evs));
+    }
+    // the patches due in (.., t_ns], in time order: metric m's value, then node_hot_value
+    void due(int64_t t_ns, std::vector<Patch>* out) {
+        while (!q_.empty() && q_.top().t <= t_ns) {
+            Ev e = q_.top();
+            q_.pop();
+            const uint64_t r = mix64(seed_ * 31 + (uint64_t)e.t * 1315423911ull + e.n * 7 + e.m);
+            const std::string st = local_stamp(e.t / 1000000000LL, 8 * 3600);
+            char v[64];
+            std::snprintf(v, sizeof v, "%.5f,%s", (double)(r % 120001) / 1e5, st.c_str());  // prometheus.go:124
+            out->push_back({e.n, names_[e.m], v});
+            std::snprintf(v, sizeof v, "%d,%s", (int)((r >> 20) % 13), st.c_str());  // strconv.Itoa, node.go:120
+            out->push_back({e.n, NodeHotValue, v});
+            e.t += period_[e.m];
+            q_.push(e);
+        }
+    }
+
+   private:
+    struct Ev {
+        int64_t t;
+        uint32_t n, m;
+        bool operator>(const Ev& o) const { return t != o.t ? t > o.t : (n != o.n ? n > o.n : m > o.m); }
+    };
+    uint64_t seed_;
+    std::vector<std::string> names_;
+    std::vector<int64_t> period_;
+    std::priority_queue<Ev, std::vector<Ev>, std::greater<Ev>> q_;
 };
 
 // framework.Parallelizer().Until(ctx, n, f) on a fixed pool: the caller and n - 1 workers
@@ -142,55 +255,50 @@ class Pool {
 
 #ifdef DROPIN_CPU
 // Filter / Score re-parsing the node's annotations on every call (stats.go:51-76): one
-// (pod, node) evaluation of the oracle's string mode per call.
+// (pod, node) evaluation of the oracle's string mode per call, on the node's current object.
 class CpuPlugin {
    public:
-    CpuPlugin(const crane_policy& p, const std::vector<Node>& nodes, int64_t tz) : tz_(tz) {
+    CpuPlugin(const crane_policy& p, const BenchSnap& snap, int64_t tz) : tz_(tz), snap_(&snap) {
         pol_ = or_policy{p.n_sync, p.sync_name, p.sync_period_ns, p.n_pred, p.pred_name, p.pred_limit,
                          p.n_prio, p.prio_name, p.prio_weight, p.n_hot, p.hot_tr_ns, p.hot_count};
-        for (const auto& n : nodes) {
-            off_.push_back((int64_t)keys_.size());
-            for (const auto& kv : n.Annotations) {
-                keys_.push_back(kv.first.c_str());
-                vals_.push_back(kv.second.c_str());
-            }
-        }
-        off_.push_back((int64_t)keys_.size());
-        for (size_t i = 0; i < nodes.size(); ++i) idx_[&nodes[i]] = (int64_t)i;
-        names_ = &nodes;
+        for (size_t i = 0; i < snap.infos.size(); ++i) idx_[snap.infos[i].get()] = (int64_t)i;
     }
     Status Filter(CycleState& st, const Pod& pod, const NodeInfo& ni) {
         if (IsDaemonsetPod(pod)) return NewStatus(Code::Success, "");
         const Node* n = ni.node();
         if (!n) return NewStatus(Code::Error, "node not found");
         int8_t ff = -1;
-        eval(idx_.at(n), st.now_ns, 0, &ff, nullptr);
+        eval(*n, st.now_ns, 0, &ff, nullptr);
         if (ff >= 0)
             return NewStatus(Code::Unschedulable,
                              "Load[" + std::string(pol_.pred_name[ff]) + "] of node[" + n->Name + "] is too high");
         return NewStatus(Code::Success, "");
     }
-    std::pair<int64_t, Status> Score(CycleState& st, const Pod&, const std::string& name, const Snapshot& snap) {
+    std::pair<int64_t, Status> Score(CycleState& st, const Pod&, const std::string& name) {
         std::string err;
-        const Node* n = snap.Get(name, &err);
-        if (!n) return {0, NewStatus(Code::Error, "getting node \"" + name + "\" from Snapshot: " + err)};
+        const NodeInfo* ni = snap_->Get(name, &err);
+        if (!ni) return {0, NewStatus(Code::Error, "getting node \"" + name + "\" from Snapshot: " + err)};
         int64_t s = 0;
-        eval(idx_.at(n), st.now_ns, 1, nullptr, &s);  // (flag 1: the Filter part is skipped)
+        eval(*ni->node(), st.now_ns, 1, nullptr, &s);  // (flag 1: the Filter part is skipped)
         return {s, Status()};
     }
 
    private:
-    void eval(int64_t i, int64_t now, uint8_t ds, int8_t* ff, int64_t* score) {
-        const int64_t off[2] = {0, off_[(size_t)i + 1] - off_[(size_t)i]};
-        or_eval_strings(&pol_, 1, off, keys_.data() + off_[(size_t)i], vals_.data() + off_[(size_t)i], 1, &now, &ds,
-                        tz_, 1, ff, score, nullptr);
+    void eval(const Node& n, int64_t now, uint8_t ds, int8_t* ff, int64_t* score) {
+        thread_local std::vector<const char*> keys, vals;
+        keys.clear();
+        vals.clear();
+        for (const auto& kv : n.Annotations) {
+            keys.push_back(kv.first.c_str());
+            vals.push_back(kv.second.c_str());
+        }
+        const int64_t off[2] = {0, (int64_t)keys.size()};
+        or_eval_strings(&pol_, 1, off, keys.data(), vals.data(), 1, &now, &ds, tz_, 1, ff, score, nullptr);
     }
     or_policy pol_;
     int64_t tz_;
-    std::vector<int64_t> off_;
-    std::vector<const char*> keys_, vals_;
-    std::unordered_map<const Node*, int64_t> idx_;
-    const std::vector<Node>* names_;
+    const BenchSnap* snap_;
+    std::unordered_map<const NodeInfo*, int64_t> idx_;
 };
 #endif
 
@@ -208,23 +316,49 @@ static std::vector<std::string> split_tab(const std::string& s) {
 
 int main(int argc, char** argv) {
     if (argc < 4) {
-        std::fprintf(stderr, "usage: dropin_bench <policy> <snapshot.tsv> <pods.tsv> [threads]\n");
+        std::fprintf(stderr, "usage: dropin_bench <policy> <snapshot.tsv> <pods.tsv> [--threads N] [--cpu] "
+                             "[--churn X] [--churn-log path] [--seed S]\n");
         return 2;
     }
-    const int threads = argc > 4 ? std::atoi(argv[4]) : 16;
+    int threads = 16;
+    bool cpu = false;
+    double churn_scale = 0.0;
+    std::string churn_log;
+    uint64_t seed = 1;
+    for (int a = 4; a < argc; ++a) {
+        const std::string k = argv[a];
+        auto next = [&]() -> std::string { return a + 1 < argc ? argv[++a] : ""; };
+        if (k == "--threads") threads = std::atoi(next().c_str());
+        else if (k == "--cpu") cpu = true;
+        else if (k == "--churn") churn_scale = std::atof(next().c_str());
+        else if (k == "--churn-log") churn_log = next();
+        else if (k == "--seed") seed = std::strtoull(next().c_str(), nullptr, 10);
+        else {
+            std::fprintf(stderr, "unknown argument %s\n", k.c_str());
+            return 2;
+        }
+    }
     BenchSnap snap;
     {
         std::ifstream f(argv[2]);
         std::string line;
+        std::vector<std::pair<std::string, std::string>> pend;
+        auto flush = [&] {
+            if (snap.objs.empty()) return;
+            Node& n = *snap.objs.back();  // (not yet published to any reader)
+            for (auto& kv : pend) n.Annotations[kv.first] = kv.second;
+            pend.clear();
+        };
         while (std::getline(f, line)) {
             auto t = split_tab(line);
             if (t[0] == "N") {
-                snap.by_name[t[1]] = snap.nodes.size();
-                snap.nodes.push_back(Node{t[1], {}});
+                flush();
+                snap.add(t[1]);
             } else if (t[0] == "A" && t.size() >= 3) {
-                snap.nodes.back().Annotations[t[1]] = t[2];
+                pend.emplace_back(t[1], t[2]);
             }
         }
+        flush();
     }
     struct PodIn {
         Pod pod;
@@ -249,7 +383,6 @@ int main(int argc, char** argv) {
     h.snapshot = &snap;
     DynamicArgs a;
     a.PolicyConfigPath = argv[1];
-    const bool cpu = argc > 5 && std::string(argv[5]) == "cpu";
 #ifndef DROPIN_CPU
     if (cpu) {
         std::fprintf(stderr, "the cpu mode is the dropin_cpu build\n");
@@ -265,41 +398,67 @@ int main(int argc, char** argv) {
     ds.SetParseThreads(threads);
     std::string err;
     double sync_ms = 0.0;
-    if (!cpu) {
+    if (!cpu) {  // the first full sync (parse + upload of the whole snapshot + table), before the pods
+        CycleState st;
+        st.now_ns = pods.empty() ? 0 : pods[0].now;
+        Pod none;
         const auto s0 = Clock::now();
-        if (!ds.Sync(&err)) {
-            std::fprintf(stderr, "Sync: %s\n", err.c_str());
+        if (!snap.list.empty() && ds.Filter(st, none, *snap.list[0]).code() == Code::Error) {
+            std::fprintf(stderr, "first sync failed\n");
             return 1;
         }
         sync_ms = std::chrono::duration<double, std::milli>(Clock::now() - s0).count();
     }
 #ifdef DROPIN_CPU
-    CpuPlugin cp(ds.policy(), snap.nodes, 8 * 3600);
+    CpuPlugin cp(ds.policy(), snap, 8 * 3600);
 #endif
+    std::unique_ptr<Churn> churn;
+    if (churn_scale > 0 && !pods.empty())
+        churn.reset(new Churn(ds.policy(), snap.objs.size(), pods[0].now, churn_scale, seed));
+    FILE* clog = churn_log.empty() ? nullptr : std::fopen(churn_log.c_str(), "w");
     Pool pool(threads);
-    const int64_t N = (int64_t)snap.nodes.size();
+    const int64_t N = (int64_t)snap.objs.size();
     std::vector<uint8_t> feas((size_t)N);
     std::vector<int64_t> fidx((size_t)N), fscore((size_t)N);
-    std::vector<double> cyc_ms, filt_ms, score_ms, sel_ms, pool_ms;
+    std::vector<double> cyc_ms, first_ms, filt_ms, score_ms, sel_ms, pool_ms, cyc_changed_ms;
     std::vector<int64_t> chosen;
+    std::vector<Churn::Patch> due;
+    int64_t n_patches = 0, changed_cycles = 0;
     std::atomic<int> errors{0};
-    for (auto& p : pods) {
+    for (size_t pi = 0; pi < pods.size(); ++pi) {
+        auto& p = pods[pi];
         {  // the harness's own cost: the two fan-outs over no-op calls
             const auto q0 = Clock::now();
             pool.until(N, [&](int64_t i) { feas[(size_t)i] = (uint8_t)(i & 1); });
             pool.until(N * 7 / 10, [&](int64_t j) { fscore[(size_t)j] = j; });
             pool_ms.push_back(std::chrono::duration<double, std::milli>(Clock::now() - q0).count());
         }
+        due.clear();
+        if (churn && pi > 0) churn->due(p.now, &due);  // published between the cycles (informer)
+        for (const auto& x : due) {
+            snap.patch(x.node, x.key, x.value);
+            if (clog) std::fprintf(clog, "%zu\t%zu\t%s\t%s\n", pi, x.node, x.key.c_str(), x.value.c_str());
+        }
+        n_patches += (int64_t)due.size();
         const auto t0 = Clock::now();
         CycleState st;
         st.now_ns = p.now;
+        // the cycle's first Filter call (on this thread): it brings the plugin up to date
+        Status s0;
+#ifdef DROPIN_CPU
+        if (cpu) s0 = cp.Filter(st, p.pod, *snap.list[0]);
+        else
+#endif
+            s0 = ds.Filter(st, p.pod, *snap.list[0]);
+        if (s0.code() == Code::Error) errors++;
+        const auto tf = Clock::now();
         pool.until(N, [&](int64_t i) {  // findNodesThatPassFilters
             Status s;
 #ifdef DROPIN_CPU
-            if (cpu) s = cp.Filter(st, p.pod, NodeInfo(&snap.nodes[(size_t)i]));
+            if (cpu) s = cp.Filter(st, p.pod, *snap.list[(size_t)i]);
             else
 #endif
-                s = ds.Filter(st, p.pod, NodeInfo(&snap.nodes[(size_t)i]));
+                s = ds.Filter(st, p.pod, *snap.list[(size_t)i]);
             feas[(size_t)i] = s.IsSuccess();
             if (s.code() == Code::Error) errors++;
         });
@@ -311,11 +470,12 @@ int main(int argc, char** argv) {
         }
         pool.until(F, [&](int64_t j) {  // prioritizeNodes -> RunScorePlugins
             std::pair<int64_t, Status> sr;
+            const std::string& name = snap.node((size_t)fidx[(size_t)j]).Name;
 #ifdef DROPIN_CPU
-            if (cpu) sr = cp.Score(st, p.pod, snap.nodes[(size_t)fidx[(size_t)j]].Name, snap);
+            if (cpu) sr = cp.Score(st, p.pod, name);
             else
 #endif
-                sr = ds.Score(st, p.pod, snap.nodes[(size_t)fidx[(size_t)j]].Name);
+                sr = ds.Score(st, p.pod, name);
             fscore[(size_t)j] = sr.first * 3;  // plugin weight (scheduler-config.yaml:16)
             if (!sr.second.IsSuccess()) errors++;
         });
@@ -331,11 +491,17 @@ int main(int argc, char** argv) {
             return std::chrono::duration<double, std::milli>(y - x).count();
         };
         cyc_ms.push_back(ms(t0, t3));
-        filt_ms.push_back(ms(t0, t1));
+        if (!due.empty()) {
+            cyc_changed_ms.push_back(ms(t0, t3));
+            ++changed_cycles;
+        }
+        first_ms.push_back(ms(t0, tf));
+        filt_ms.push_back(ms(tf, t1));
         score_ms.push_back(ms(t1, t2));
         sel_ms.push_back(ms(t2, t3));
         chosen.push_back(best);
     }
+    if (clog) std::fclose(clog);
     auto med = [](std::vector<double> v) {
         if (v.empty()) return 0.0;
         std::sort(v.begin(), v.end());
@@ -344,13 +510,22 @@ int main(int argc, char** argv) {
     std::vector<double> sorted = cyc_ms;
     std::sort(sorted.begin(), sorted.end());
     auto pct = [&](double q) { return sorted.empty() ? 0.0 : sorted[(size_t)(q * (double)(sorted.size() - 1))]; };
+    const auto c = ds.counters();
+    double sim_s = pods.size() > 1 ? (double)(pods.back().now - pods.front().now) / 1e9 : 0.0;
     std::printf("{\"nodes\": %lld, \"pods\": %zu, \"threads\": %d, \"mode\": \"%s\", \"sync_ms\": %.3f, "
                 "\"cycle_ms_median\": %.4f, \"cycle_ms_p90\": %.4f, \"cycle_ms_min\": %.4f, \"cycle_ms_max\": %.4f, "
-                "\"filter_fanout_ms_median\": %.4f, \"score_fanout_ms_median\": %.4f, \"select_ms_median\": %.4f, "
-                "\"pool_noop_ms_median\": %.4f, \"tables_built\": %llu, \"errors\": %d, \"chosen\": [",
+                "\"cycle_ms_mean\": %.4f, \"changed_cycle_ms_median\": %.4f, "
+                "\"first_call_ms_median\": %.4f, \"filter_fanout_ms_median\": %.4f, \"score_fanout_ms_median\": %.4f, "
+                "\"select_ms_median\": %.4f, \"pool_noop_ms_median\": %.4f, \"churn_scale\": %.3f, "
+                "\"patches\": %lld, \"simulated_s\": %.4f, \"cycles_with_patches\": %lld, \"tables_built\": %llu, "
+                "\"full_syncs\": %llu, \"incremental_syncs\": %llu, \"nodes_updated\": %llu, \"errors\": %d, "
+                "\"chosen\": [",
                 (long long)N, pods.size(), threads, cpu ? "cpu" : "engine", sync_ms, pct(0.5), pct(0.9), pct(0.0),
-                pct(1.0), med(filt_ms), med(score_ms), med(sel_ms), med(pool_ms), (unsigned long long)ds.TablesBuilt(),
-                errors.load());
+                pct(1.0), cyc_ms.empty() ? 0.0 : std::accumulate(cyc_ms.begin(), cyc_ms.end(), 0.0) / (double)cyc_ms.size(),
+                med(cyc_changed_ms), med(first_ms), med(filt_ms), med(score_ms), med(sel_ms), med(pool_ms), churn_scale,
+                (long long)n_patches, sim_s, (long long)changed_cycles, (unsigned long long)c.tables_built,
+                (unsigned long long)c.full_syncs, (unsigned long long)c.incremental_syncs,
+                (unsigned long long)c.nodes_updated, errors.load());
     for (size_t i = 0; i < chosen.size(); ++i) std::printf("%s%lld", i ? ", " : "", (long long)chosen[i]);
     std::printf("]}\n");
     return 0;
