@@ -183,3 +183,50 @@ def test_two_process_sharded_schedule(tmp_path, world, own_stream, backend):
     node, _ = shard.unpack_keys(ref)
     assert np.array_equal(node, och)
     assert (node == 3).sum() > 0
+
+
+def test_config4_global_combine_full_size():
+    """BASELINE config 4 at full size on one GPU: 1M nodes x 100k pods split into 8 node shards
+    (125k nodes each, node_offset, each with its own nodes' bindings from the one 1M-entry
+    log), every shard's step keys max-combined (the RCCL MAX all-reduce's operation) equal
+    one engine holding the whole 1M-node cluster, and a 64-pod sample equals the oracle with
+    the binding-log hot values.  Reference: plugins.go:39-98 + selectHost, binding.go:81-97;
+    SURVEY 8(e)."""
+    import torch
+    from oracle import oracle as O
+    cfg = synth.CONFIGS[4]
+    spec = cd.default_policy_spec()
+    N, P, S = cfg["nodes"], cfg["pods"], 8
+    c = synth.make_cluster(spec, N, P, n_bindings=cfg["bindings"], seed=20250215 + 4000)
+    c.now, c.ds = synth.make_pods(P, seed=20250215 + 4)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    pol = cd.Policy(spec)
+    now = int(synth.NOW0_NS)
+    full = cd.Engine(pol, 0)
+    val, ts, _ = c.rows(full.metric_names)
+    full.upload_nodes(val, ts, c.hv, c.hv_ts)
+    full.upload_bindings(c.b_node, c.b_ts)
+    ref = torch.empty(P, dtype=torch.int64, device=dev)
+    full.step_keys_async(now, now, d_now, d_flags, ref, st.cuda_stream)
+    st.synchronize()
+    full.close()
+    combined = torch.full((P,), -1, dtype=torch.int64, device=dev)
+    k = torch.empty(P, dtype=torch.int64, device=dev)
+    for r in range(S):
+        se = shard.ShardedEngine(pol, N, S, r, 0)
+        se.upload(val, ts, c.hv, c.hv_ts, c.b_node, c.b_ts)
+        se.step_keys(now, now, d_now, d_flags, k, st.cuda_stream)
+        st.synchronize()
+        combined = torch.maximum(combined, k)
+        se.close()
+    assert torch.equal(combined, ref)
+    node, score = shard.unpack_keys(combined.cpu().numpy())
+    sample = np.unique(np.concatenate([np.arange(8), np.linspace(0, P - 1, 48).astype(int),
+                                       np.flatnonzero(c.ds)[:8]]))[:64]
+    _, hv = O.hot_values(spec, c.b_node, c.b_ts, N, now // 10**9)
+    _, _, och = oracle_soa(spec, c, now=c.now[sample], ds=c.ds[sample], want_matrix=False, threads=16,
+                           hv_override=(hv.astype(np.float64), np.full(N, now, np.int64)))
+    assert np.array_equal(node[sample], och)
