@@ -124,6 +124,7 @@ struct Options {
                               // >= kPieceMinTiles pod tiles (a piece is re-read once per tile), 1 always,
                               // 2 never (then no per-tile piece ranges either: K3s reads all pieces)
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
+    int emit_threads = 0;     // split form's k3a_emit workgroup: 0 = the block's width, 64 = one wave per block
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
 
@@ -568,7 +569,7 @@ static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_k
         }
         int rc = node_pass_locked(h, st, nullptr, &ks);
         if (rc) return rc;
-        if (split) HIPTRY(h, launch_step_emit(h->shape, ks, h->N, bs, st));
+        if (split) HIPTRY(h, launch_step_emit(h->shape, ks, h->N, bs, st, h->opt.emit_threads ? h->opt.emit_threads : bs));
     } else {
         if (h->rec_dirty) {
             int rc = node_pass_locked(h, st);
@@ -761,6 +762,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "sel_chain" && range(0, 1)) o.sel_chain = (int)value;
     else if (n == "step_pieces" && range(0, 2)) o.step_pieces = (int)value;
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
+    else if (n == "emit_threads" && (value == 0 || value == 64)) o.emit_threads = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
         if (o.trace) {

@@ -374,28 +374,31 @@ void k1_node_pass(K1Args a, K1Step step) {
 }
 
 // ---------------------------------------------------------------- K3a emit (split form)
-// One workgroup per producer block of the split node pass: the block's queued (node, kind)
-// items are built from the stepped records in HBM (L2-resident: written by the node pass on
-// the same XCD), then sorted, published and the tile rows written — the fused K1 epilogue.
-template <int PD, int PR, int BS>
-__global__ __launch_bounds__(BS) void k3a_emit(K1Step step, int64_t N) {
+// One workgroup per producer block of the split node pass (NODES nodes): the block's queued
+// (node, kind) items are built from the stepped records in HBM (L2-resident: written by the
+// node pass on the same XCD), then sorted, published and the tile rows written — the fused
+// K1 epilogue.  BT threads: NODES (the block's own width), or one wave (BT = 64), whose
+// barriers are free and whose small LDS (CAP one-step records per kind staged; a block with
+// more goes through st.stage) lets many blocks' epilogues run on a CU at once.
+template <int PD, int PR, int NODES, int BT>
+__global__ __launch_bounds__(BT) void k3a_emit(K1Step step, int64_t N) {
     using Rec = NodeRec<PD, PR>;
-    constexpr int CAP = kK1S1Cap < 2 * BS ? kK1S1Cap : 2 * BS;
+    constexpr int CAP = BT == 64 ? 64 : (kK1S1Cap < 2 * NODES ? kK1S1Cap : 2 * NODES);
     __shared__ StepShared ssh;
     __shared__ __attribute__((aligned(16))) Step1 s1l[2 * CAP];
     __shared__ __attribute__((aligned(16))) Step1 s1s[2 * CAP];
-    constexpr int kPieceCap = 64;
+    constexpr int kPieceCap = BT == 64 ? 32 : 64;
     __shared__ __attribute__((aligned(16))) unsigned char pscr[kPieceCap * PieceScr::bytes_per_piece];
     __shared__ int32_t nq;
-    const int64_t nb = (N + BS - 1) / BS;
+    const int64_t nb = (N + NODES - 1) / NODES;
     const int64_t blk = xcd_block(blockIdx.x, nb);  // the node pass's mapping: same XCD
-    const int64_t first = blk * BS;
+    const int64_t first = blk * NODES;
     const StepTables& st = step.st;
     if (threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = st.cnt[blk * 4 + threadIdx.x];
     if (threadIdx.x < 2) {
         // the block's flat maxima (step_tile_rows folds sh.fm over the waves)
         ssh.fm[threadIdx.x][0] = st.flat[blk * 2 + threadIdx.x];
-        for (int i = 1; i < BS / 64; ++i) ssh.fm[threadIdx.x][i] = -1;
+        for (int i = 1; i < BT / 64; ++i) ssh.fm[threadIdx.x][i] = -1;
     }
     if (threadIdx.x == 0) nq = step.nqg[blk];
     int64_t tpre = 0;
@@ -405,10 +408,10 @@ __global__ __launch_bounds__(BS) void k3a_emit(K1Step step, int64_t N) {
     const bool g1 = max(ssh.lc[0][0], ssh.lc[1][0]) > min(CAP, st.lds_cap);
     Step1* s1b = g1 ? st.stage + blk * 2 * st.bs : s1l;
     const int64_t kst = g1 ? st.s1pad : (int64_t)CAP;
-    const uint32_t* q = step.qg + blk * 2 * BS;
-    const int32_t* qm = step.qmg + blk * 2 * BS;
+    const uint32_t* q = step.qg + blk * 2 * NODES;
+    const int32_t* qm = step.qmg + blk * 2 * NODES;
     const Rec* rec = static_cast<const Rec*>(step.srec);
-    for (int w = threadIdx.x; w < nq; w += BS) {
+    for (int w = threadIdx.x; w < nq; w += BT) {
         const uint32_t it = q[w];
         const int o = (int)(it & 0xFFF);
         step_emit_one<PD, PR>(rec[first + o], first + o, (int)((it >> 12) & 1), (int32_t)((it >> 14) & 0x3FF), qm[w],
@@ -416,30 +419,32 @@ __global__ __launch_bounds__(BS) void k3a_emit(K1Step step, int64_t N) {
                               step.winv);
     }
     __syncthreads();
-    if (g1) step_sort_publish_global<BS>(ssh, st, blk);
-    else step_sort_publish<BS, CAP>(s1l, s1s, ssh, st, blk);
+    if (g1) step_sort_publish_global<BT>(ssh, st, blk);
+    else step_sort_publish<BT, CAP>(s1l, s1s, ssh, st, blk);
     if (st.rows) {
         const PieceScr ps{pscr, kPieceCap};
-        step_pieces<BS>(ssh, st, blk, ps);
-        if (g1) step_tile_rows<BS, CAP, true>(s1l, s1s, ssh, st, blk, &tpre, ps);
-        else step_tile_rows<BS, CAP, false>(s1l, s1s, ssh, st, blk, &tpre, ps);
+        step_pieces<BT>(ssh, st, blk, ps);
+        if (g1) step_tile_rows<BT, CAP, true>(s1l, s1s, ssh, st, blk, &tpre, ps);
+        else step_tile_rows<BT, CAP, false>(s1l, s1s, ssh, st, blk, &tpre, ps);
     }
 }
 
 template <int PD, int PR>
-static hipError_t launch_emit_t(const K1Step& step, int64_t N, int32_t bs, hipStream_t st) {
+static hipError_t launch_emit_t(const K1Step& step, int64_t N, int32_t bs, int32_t bt, hipStream_t st) {
     const int64_t nb = (N + bs - 1) / bs;
     if (nb <= 0) return hipSuccess;
-    if (bs == 256) return klaunch("k3a_emit", k3a_emit<PD, PR, 256>, dim3((unsigned)nb), dim3(256), 0, st, step, N);
-    if (bs == 128) return klaunch("k3a_emit", k3a_emit<PD, PR, 128>, dim3((unsigned)nb), dim3(128), 0, st, step, N);
+    if (bs == 256 && bt == 64)
+        return klaunch("k3a_emit", k3a_emit<PD, PR, 256, 64>, dim3((unsigned)nb), dim3(64), 0, st, step, N);
+    if (bs == 256) return klaunch("k3a_emit", k3a_emit<PD, PR, 256, 256>, dim3((unsigned)nb), dim3(256), 0, st, step, N);
+    if (bs == 128) return klaunch("k3a_emit", k3a_emit<PD, PR, 128, 128>, dim3((unsigned)nb), dim3(128), 0, st, step, N);
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs, hipStream_t st) {
+hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs, hipStream_t st, int32_t bt) {
     switch (shape) {
-        case kShape4x6: return launch_emit_t<4, 6>(step, N, bs, st);
-        case kShape8x8: return launch_emit_t<8, 8>(step, N, bs, st);
-        default: return launch_emit_t<16, 16>(step, N, bs, st);
+        case kShape4x6: return launch_emit_t<4, 6>(step, N, bs, bt, st);
+        case kShape8x8: return launch_emit_t<8, 8>(step, N, bs, bt, st);
+        default: return launch_emit_t<16, 16>(step, N, bs, bt, st);
     }
 }
 

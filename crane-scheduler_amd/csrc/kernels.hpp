@@ -347,7 +347,8 @@ struct K1Args {
 };
 // step (optional): also build the K3 step tables of a pod batch (K3a fused).
 hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr);
-// split form's second kernel: one workgroup per producer block of the node pass (bs nodes)
-hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs, hipStream_t st);
+// split form's second kernel: one workgroup per producer block of the node pass (bs nodes) of
+// bt threads (bs, or 64: one wave per block)
+hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs, hipStream_t st, int32_t bt = 0);
 
 }  // namespace crane

@@ -564,8 +564,9 @@ __device__ __forceinline__ void step_sort_publish(Step1* s1l, Step1* srt, const 
     int32_t* pmL = reinterpret_cast<int32_t*>(s1l);  // [2][CAP]
     int32_t* smL = pmL + 2 * CAP;                     // [2][CAP]
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (w < 2) {
-        const int T = w, n = T ? n1 : n0;
+    // wave T takes kind T (a one-wave workgroup takes both in turn)
+    for (int T = w; T < 2; T += (BS >= 128 ? 2 : 1)) {
+        const int n = T ? n1 : n0;
         const Step1* a = srt + T * CAP;
         const int64_t base = s1_at(st, T, blk);
         int32_t carry = -1;
@@ -612,8 +613,8 @@ __device__ __forceinline__ void step_sort_publish_global(const StepShared& sh, c
     }
     __syncthreads();
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (w < 2) {
-        const int T = w, n = T ? n1 : n0;
+    for (int T = w; T < 2; T += (BS >= 128 ? 2 : 1)) {
+        const int n = T ? n1 : n0;
         const int64_t base = s1_at(st, T, blk);
         const Step1* a = st.single + base;
         int32_t carry = -1;
@@ -663,7 +664,6 @@ struct PieceScr {
 // pieces in st.mid (a barrier after the emit).  Sets sh.pn (read after the next barrier).
 template <int BS>
 __device__ __forceinline__ void step_pieces(StepShared& sh, const StepTables& st, int64_t blk, const PieceScr& ps) {
-    static_assert(BS >= 128, "two waves compact the two kinds");
     const int32_t nm0 = sh.lc[0][1], nm1 = sh.lc[1][1];
     auto dec = [&](int32_t nm) {
         return st.prow && nm >= 2 && nm <= ps.pc && (int64_t)nm * st.ntiles >= st.piece_work;
@@ -705,8 +705,7 @@ __device__ __forceinline__ void step_pieces(StepShared& sh, const StepTables& st
     __syncthreads();
     // D: wave T compacts kind T's non-empty covered intervals (in order) and publishes them
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (w < 2) {
-        const int T = w;
+    for (int T = w; T < 2; T += (BS >= 128 ? 2 : 1)) {  // wave T compacts kind T (one wave: both)
         const int32_t n = 2 * (T ? a1 : a0);
         if ((T ? d1 : d0)) {
             const int64_t* bs = ps.bs(T);

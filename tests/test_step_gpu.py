@@ -26,15 +26,19 @@ def _check(spec, c, now, ds):
     # one-step records through its LDS staging, through st.stage always (cap 0), or
     # per block as its counts exceed a small cap; the node pass fused with the step
     # tables (split 0) or as the split form (count pass + k3a_emit, split 1)
-    # the middle pieces raw or cut into elementary ones (step_pieces 1: whenever it pays)
-    for rows, cap, split, pc in ((1, 1 << 30, 0, 0), (0, 1 << 30, 0, 0), (1, 0, 0, 1), (0, 6, 0, 0), (1, 6, 0, 1),
-                                 (1, 1 << 30, 1, 1), (0, 6, 1, 0), (1, 0, 1, 2), (1, 1 << 30, 0, 1)):
-        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap, "k1_split": split, "step_pieces": pc})
+    # the middle pieces raw or cut into elementary ones (step_pieces 1: whenever it pays); the
+    # split form's k3a_emit as wide as the block (emit 0) or one wave per block (emit 64)
+    for rows, cap, split, pc, em in ((1, 1 << 30, 0, 0, 0), (0, 1 << 30, 0, 0, 0), (1, 0, 0, 1, 0), (0, 6, 0, 0, 0),
+                                     (1, 6, 0, 1, 0), (1, 1 << 30, 1, 1, 0), (0, 6, 1, 0, 0), (1, 0, 1, 2, 0),
+                                     (1, 1 << 30, 0, 1, 0), (1, 1 << 30, 1, 1, 64), (0, 6, 1, 0, 64),
+                                     (1, 1 << 30, 1, 0, 64)):
+        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap, "k1_split": split, "step_pieces": pc,
+                                        "emit_threads": em})
         _, _, ch, cs = eng.eval(now, ds)
-        assert np.array_equal(ch, och), (rows, cap, split, pc)
+        assert np.array_equal(ch, och), (rows, cap, split, pc, em)
         for p in range(len(now)):
             ok = (off[p] < 0) | bool(ds[p])
-            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, split, pc, p)
+            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, split, pc, em, p)
         eng.close()
 
 
