@@ -336,10 +336,24 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
                 if name.startswith(("k1_node_pass", "k3a_emit")):
                     k1_parts.setdefault(name, []).append(t)
             k1r.append(sum(t for name, t in t_np if name == "k1_node_pass"))
+    # the general form for a log in no particular order: every binding's node id and stamp read
+    eng.set_option("k2_sorted", 0)
+    k2ts, k2ts_parts = [], {}
+    for r in range(reps + 1):
+        flush()
+        eng.set_profiling(True)
+        eng.refresh_hot_values_async(now, now, sh)
+        t_k2 = eng.stage_times()
+        eng.node_pass_async(sh)  # (consume the counts)
+        if r:
+            k2ts.append(sum(t for _, t in t_k2))
+            for name, t in t_k2:
+                k2ts_parts.setdefault(name, []).append(t)
     eng.set_profiling(False)
     eng.close()
     del scratch
     k2_ms, k1_ms, k1r_ms = float(np.median(k2)), float(np.median(k1)), float(np.median(k1r))
+    k2ts_ms = float(np.median(k2ts))
     tr_k2 = tr_k1 = tr_k1r = None
     if pmc:
         ks = pmc.get("kernels", {})
@@ -348,13 +362,18 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
             tr_k2 = int(sum(k2t))
         tr_k1 = pmc_traffic(pmc, "k1_node_pass+k3a_steps")
         tr_k1r = pmc_traffic(pmc, "k1_node_pass")
-    alg_k2 = B * 12 + 4 * W * N
+    kb = k2_read(spec, c.b_ts, now)
+    alg_k2 = kb["bytes"] + 4 * W * N
     alg_k1 = N * (16 * M + 4 * W + 8)
     rec_b = rec_bytes(spec)
     return {"workload": f"{N} nodes x {B}-entry binding log ({P}-pod batch), default policy",
             "cache": "cold: 1 GiB read between the stages (Infinity Cache + L2 evicted, no dirty lines)",
-            "k2": roof(alg_k2, k2_ms, "bindings read (12 B) + per-node window counts written (4 B x W)", tr_k2,
+            "k2": roof(alg_k2, k2_ms, kb["what"] + " + per-node window counts written (4 B x W)", tr_k2,
                        {"kernels": {k: round(float(np.median(v)), 4) for k, v in k2_parts.items()}}),
+            "k2_timestamp_path": roof(12 * B + 4 * W * N, k2ts_ms, "every binding's node id + stamp read (12 B) "
+                                      "+ per-node window counts written (4 B x W): the form for a log in no "
+                                      "particular order (engine option k2_sorted 0)", None,
+                                      {"kernels": {k: round(float(np.median(v)), 4) for k, v in k2ts_parts.items()}}),
             "k1": roof(alg_k1, k1_ms, "SoA (value, ts) read + window counts read + hot value written", tr_k1,
                        {"kernel": "k1_node_pass+k3a_steps (fused with the step tables)",
                         "kernels": {k: round(float(np.median(v)), 4) for k, v in k1_parts.items()}}),
@@ -649,6 +668,20 @@ def keys_virtual_shards(cd, spec, dev, c, d_now, d_flags, now_sync, ref_keys, S)
     return bool(torch.equal(comb, ref_keys))
 
 
+def k2_read(spec, b_ts, now_ns):
+    """The bindings K2 reads, as the engine decides (engine option k2_sorted, default on): a
+    log in time order is read from the first binding inside the widest window on, node ids
+    only (4 B each: the window rank comes from the position); otherwise every binding's node
+    id and stamp (12 B)."""
+    B = len(b_ts)
+    if B and np.all(b_ts[1:] >= b_ts[:-1]) and spec["hotValue"]:
+        cmin = min(now_ns // 10**9 - tr // 10**9 for tr, _ in spec["hotValue"])
+        first = int(np.searchsorted(b_ts, cmin, side="right"))
+        return {"first": first, "read": B - first, "bytes": 4 * (B - first),
+                "what": f"node ids of the {B - first} bindings inside the widest window read (time-ordered log)"}
+    return {"first": 0, "read": B, "bytes": 12 * B, "what": "bindings read (node id + stamp)"}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -857,19 +890,21 @@ def main():
     # mean dispatch-stamped duration.  K3s re-reads L2-resident step records: not HBM-priced.
     M = len(eng.metric_names)
     W = len(spec["hotValue"])
+    kb = k2_read(spec, c.b_ts, now_sync)
     cut = np.sort(np.array([now_sync // 10**9 - tr // 10**9 for tr, _ in spec["hotValue"]], np.int64))
     jr = (c.b_ts[:, None] > cut[None, :]).sum(1)
     okb = (jr > 0) & (c.b_node >= 0) & (c.b_node < N)
-    reg = np.arange(B, dtype=np.int64) // 2048
     # dedupe-form K2: one 4-byte entry per distinct (2048-binding region, node, window rank),
-    # a (count, offset) word per (node block, region); the node pass reads both
+    # a (count, offset) word per (node block, region); the node pass reads both.  Regions
+    # start at the first binding K2 reads (a time-ordered log: the widest window's suffix)
+    reg = (np.arange(B, dtype=np.int64) - kb["first"]) // 2048
     E = int(np.unique((reg[okb] * (N + 1) + c.b_node[okb]) * 8 + jr[okb] - 1).size) if B else 0
-    co_b = 4 * (-(-N // 256)) * (-(-B // 2048))
+    co_b = 4 * (-(-N // 256)) * (-(-kb["read"] // 2048))
     k3p_b = P * (8 + 1 + 4 + 8 + 8)
-    k2d_b = B * 12 + E * 4 + co_b
+    k2d_b = kb["bytes"] + E * 4 + co_b
     alg = {
-        "k2x_dedupe": (k2d_b, "bindings read + distinct (region, node, bucket) entries + count/offset written"),
-        "k2x_dedupe+k3p_pods": (k2d_b + k3p_b, "bindings read + distinct entries + count/offset written; pod now + "
+        "k2x_dedupe": (k2d_b, kb["what"] + " + distinct (region, node, bucket) entries + count/offset written"),
+        "k2x_dedupe+k3p_pods": (k2d_b + k3p_b, kb["what"] + " + distinct entries + count/offset written; pod now + "
                                                "flag read, partition + keys written"),
         "k1_node_pass+k3a_steps": (N * (16 * M + 8) + E * 4 + co_b,
                                    "SoA (value, ts) read + hot value written + K2 entries and count/offset read"),

@@ -125,6 +125,7 @@ struct Options {
                               // 2 never (then no per-tile piece ranges either: K3s reads all pieces)
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
     int emit_threads = 0;     // split form's k3a_emit workgroup: 0 = the block's width, 64 = one wave per block
+    int k2_sorted = 1;        // a time-ordered log: K2 reads the widest window's suffix, ranks by position
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
 
@@ -167,6 +168,8 @@ struct crane_dyn {
     int64_t B = 0;
     BindingHeap heap;             // BindingRecords restatement (crane_dyn_binding_records mode)
     bool heap_mode = false;
+    bool log_sorted = false;            // uploaded log in non-decreasing time order (upload_bindings)
+    std::vector<int64_t> hts_copy;      // ... and its timestamps (the windows' suffixes are found here)
     HostBuf<int32_t> hnode;       // pinned mirror of the slots in heap mode
     HostBuf<int64_t> hts;
     DevBuf<double> val, hv;
@@ -379,12 +382,31 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     h->hv_from_counts = true;
     h->hv_ts_counts = hv_ts_ns;
     h->rec_dirty = true;
-    HotPart gx = hot_dedupe_geometry(h->B, h->N, dp.n_win, h->opt.k1_threads);
+    // A time-ordered log (a ring of bindings appended as they happen, checked at upload): the
+    // bindings inside window w are the suffix from s_w = the first with ts > cutoff_w
+    // (binding.go:85-91), found on the host copy of the timestamps.  The dedupe / large forms
+    // then read only the node ids of the widest window's suffix and rank a binding by its
+    // position — the same counts as the timestamp test, without the 8-byte stamps and without
+    // the bindings older than every window.
+    const int32_t* bn = h->bnode.p;
+    int64_t Bk = h->B;
+    HotCutoffs pcut = cut;
+    const bool by_pos = h->log_sorted && h->opt.k2_sorted && dp.n_win > 0 && (int64_t)h->hts_copy.size() == h->B;
+    if (by_pos) {
+        const int64_t* t0 = h->hts_copy.data();
+        const int64_t s0 = std::upper_bound(t0, t0 + h->B, cut.sorted[0]) - t0;
+        for (int r = 0; r < dp.n_win; ++r)
+            pcut.sorted[r] = (int64_t)(std::upper_bound(t0, t0 + h->B, cut.sorted[r]) - t0) - s0 - 1;
+        pcut.by_pos = 1;
+        bn = h->bnode.p + s0;
+        Bk = h->B - s0;
+    }
+    HotPart gx = hot_dedupe_geometry(Bk, h->N, dp.n_win, h->opt.k1_threads);
     gx.trace = gx.nblk <= kTraceWgs ? h->trace_region(0) : nullptr;
     if (h->opt.k2_form == 0 && gx.ok) {
         // one launch (+ K3p); the node pass counts its own block's entries (no buckets)
         HIPTRY(h, h->k2_sorted.reserve(hot_dedupe_scratch(gx)));
-        HIPTRY(h, launch_hot_count_dedupe(h->bnode.p, h->bts.p, h->B, h->N, cut, gx, h->k2_sorted.p, st, pods,
+        HIPTRY(h, launch_hot_count_dedupe(bn, h->bts.p, Bk, h->N, by_pos ? pcut : cut, gx, h->k2_sorted.p, st, pods,
                                           h->opt.k2x_threads));
         if (pods_done) *pods_done = pods != nullptr && pods->P > 0;
         h->hx_g = gx;
@@ -394,14 +416,14 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     const size_t nb = (size_t)std::max(1, dp.n_win) * (size_t)std::max<int64_t>(h->N, 1);
     if (nb > h->buckets.n) h->buckets_zero = false;
     HIPTRY(h, h->buckets.reserve(nb));
-    HotPart gl = hot_large_geometry(h->B, h->N, dp.n_win, h->opt.k2l_region, h->opt.k2l_co_t);
+    HotPart gl = hot_large_geometry(Bk, h->N, dp.n_win, h->opt.k2l_region, h->opt.k2l_co_t);
     gl.trace = gl.nblk <= kTraceWgs ? h->trace_region(0) : nullptr;  // (stamps per region)
     if ((h->opt.k2_form == 0 || h->opt.k2_form == 3) && gl.ok) {
         // the region pass with coarse bins + the dense per-bin histogram: every bucket row
         // is rewritten, so nothing is zeroed before and K1 leaves them
         HIPTRY(h, h->k2_sorted.reserve(hot_dedupe_scratch(gl)));
-        HIPTRY(h, launch_hot_count_large(h->bnode.p, h->bts.p, h->B, h->N, cut, gl, h->k2_sorted.p, h->buckets.p,
-                                         h->n_cu, st, h->opt.k2l_threads));
+        HIPTRY(h, launch_hot_count_large(bn, h->bts.p, Bk, h->N, by_pos ? pcut : cut, gl, h->k2_sorted.p,
+                                         h->buckets.p, h->n_cu, st, h->opt.k2l_threads));
         h->buckets_zero = false;
         h->buckets_dense = true;
         return CRANE_OK;
@@ -763,6 +785,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "step_pieces" && range(0, 2)) o.step_pieces = (int)value;
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
     else if (n == "emit_threads" && (value == 0 || value == 64)) o.emit_threads = (int)value;
+    else if (n == "k2_sorted" && range(0, 1)) o.k2_sorted = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
         if (o.trace) {
@@ -841,6 +864,11 @@ int crane_dyn_upload_bindings(crane_dyn* h, int64_t n, const int32_t* node, cons
         HIPTRY(h, hipMemcpyAsync(h->bnode.p, node, sizeof(int32_t) * n, hipMemcpyHostToDevice, h->stream));
         HIPTRY(h, hipMemcpyAsync(h->bts.p, ts_s, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
     }
+    // a ring of bindings appended in time order (the synthetic and the controller-shaped logs):
+    // kept for the suffix search of every refresh
+    h->log_sorted = n > 0 && std::is_sorted(ts_s, ts_s + n);
+    if (h->log_sorted) h->hts_copy.assign(ts_s, ts_s + n);
+    else h->hts_copy.clear();
     HIPTRY(h, hipStreamSynchronize(h->stream));
     h->B = n;
     h->heap_mode = false;
@@ -870,6 +898,8 @@ int crane_dyn_binding_records(crane_dyn* h, int64_t size, int64_t gc_time_range_
     h->heap.reset(size, gc_time_range_ns);
     h->heap.bind(h->hnode.p, h->hts.p);
     h->heap_mode = true;
+    h->log_sorted = false;  // heap order
+    h->hts_copy.clear();
     h->B = size;
     return CRANE_OK;
 }

@@ -247,12 +247,22 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     const int64_t b0 = (int64_t)blk * kXChunk + threadIdx.x;
     int32_t nd[kPer];
     int64_t ts[kPer];
+    if (cut.by_pos) {  // a time-ordered log: the window rank from the position, no timestamps read
 #pragma unroll
-    for (int u = 0; u < kPer; ++u) {  // unconditional loads (clamped index): all in flight at once
-        const int64_t b = b0 + u * BT, bc = min(b, B - 1);
-        nd[u] = bnode[bc];
-        ts[u] = bts[bc];
-        if (b >= B) nd[u] = -1;
+        for (int u = 0; u < kPer; ++u) {
+            const int64_t b = b0 + u * BT, bc = min(b, B - 1);
+            nd[u] = bnode[bc];
+            ts[u] = b;
+            if (b >= B) nd[u] = -1;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {  // unconditional loads (clamped index): all in flight at once
+            const int64_t b = b0 + u * BT, bc = min(b, B - 1);
+            nd[u] = bnode[bc];
+            ts[u] = bts[bc];
+            if (b >= B) nd[u] = -1;
+        }
     }
     for (int i = threadIdx.x; i < kDSlots; i += BT) {
         hkey[i] = -1;
@@ -416,12 +426,22 @@ void k2l_partition(const int32_t* __restrict__ bnode,
     for (int i = threadIdx.x; i < g.nbins; i += BT) hist[i] = 0;
     auto load = [&](int64_t r, int32_t* nd, int64_t* ts) {  // unconditional loads, clamped index
         const int64_t b0 = r * REG + threadIdx.x;
+        if (cut.by_pos) {  // a time-ordered log: ranks from positions, no timestamps read
 #pragma unroll
-        for (int u = 0; u < kPer; ++u) {
-            const int64_t b = b0 + u * BT, bc = min(b, B - 1);
-            nd[u] = bnode[bc];
-            ts[u] = bts[bc];
-            if (b >= B) nd[u] = -1;
+            for (int u = 0; u < kPer; ++u) {
+                const int64_t b = b0 + u * BT, bc = min(b, B - 1);
+                nd[u] = bnode[bc];
+                ts[u] = b;
+                if (b >= B) nd[u] = -1;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int64_t b = b0 + u * BT, bc = min(b, B - 1);
+                nd[u] = bnode[bc];
+                ts[u] = bts[bc];
+                if (b >= B) nd[u] = -1;
+            }
         }
     };
     int32_t nd[kPer];

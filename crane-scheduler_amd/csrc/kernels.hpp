@@ -45,8 +45,13 @@ inline hipError_t klaunch(const char* name, void (*kernel)(KArgs...), dim3 grid,
 
 struct HotCutoffs {
     int32_t n_win;
-    int32_t pad;
-    int64_t sorted[kMaxWin];  // ascending now_unix - int64(timeRange.Seconds())
+    // 0: sorted[] are the ascending cutoffs now_unix - int64(timeRange.Seconds()) and a
+    // binding's window rank is #{w : ts > sorted[w]};  1 (a time-ordered log, the binding
+    // array passed from its first binding inside the widest window on): sorted[w] = (the
+    // first binding inside window w) - 1, relative, and the rank is the same count over the
+    // binding's position — the timestamps are not read
+    int32_t by_pos;
+    int64_t sorted[kMaxWin];
 };
 
 // ---------------------------------------------------------------- K3m (matrix.hip)

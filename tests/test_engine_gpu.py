@@ -162,6 +162,54 @@ def test_hot_values_random(n_nodes, n_bind, seed, k2):
     assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch, och)
 
 
+@pytest.mark.parametrize("k2", [0, 3], ids=["dedupe", "large"])
+@pytest.mark.parametrize("order", ["sorted", "ties", "shuffled", "sorted_off", "all_old", "all_new", "one_out"])
+def test_hot_values_time_ordered_log(order, k2):
+    """A time-ordered log (a ring appended as bindings happen): K2 reads only the widest
+    window's suffix and ranks each binding by its position (engine option k2_sorted, checked
+    at upload).  Equal to the oracle's per-binding timestamp test (binding.go:85-91) with runs
+    of equal stamps on the cutoffs, a shuffled log (the timestamp path), the option off, every
+    binding older than the widest window, every binding inside the narrowest, one just out."""
+    spec = cd.default_policy_spec()
+    n_nodes, n_bind = 30_000, 400_000
+    c = synth.make_cluster(spec, n_nodes, 32, n_bindings=n_bind, seed=51, pod_step_ns=3_000_000_000)
+    now = int(c.now[0])
+    nu = now // 10**9
+    bn, bt = c.b_node.copy(), c.b_ts.copy()
+    bn[::89] = -1
+    bn[5::97] = n_nodes + 1
+    if order == "ties":  # stamps exactly on the cutoffs (now - 300 s, now - 60 s) and one second around
+        bt = np.sort(np.concatenate([bt[: n_bind // 2], np.repeat(np.array([nu - 301, nu - 300, nu - 299, nu - 61,
+                                                                            nu - 60, nu - 59]), n_bind // 12)]))
+        bt = bt[:n_bind]
+    if order == "all_old":
+        bt = np.sort(bt) - 10_000
+    if order == "all_new":
+        bt = np.full(n_bind, nu, np.int64)
+    if order == "one_out":
+        bt = np.full(n_bind, nu, np.int64)
+        bt[0] = nu - 300  # not > cutoff: outside every window
+    opts = {"k2_form": k2}
+    if order == "sorted_off":
+        opts["k2_sorted"] = 0
+    if order == "shuffled":
+        p = np.random.default_rng(51).permutation(n_bind)
+        bn, bt = bn[p], bt[p]
+    eng = engine_for(spec, c, opts=opts)
+    eng.upload_bindings(bn, bt)
+    for rep in range(2):
+        eng.refresh_hot_values(now + rep * 7 * 10**9, now)
+        _, cnt_hv = O.hot_values(spec, bn, bt, n_nodes, nu + rep * 7)
+        assert np.array_equal(eng.hot_values(), cnt_hv.astype(np.float64)), rep
+    eng.refresh_hot_values(now, now)
+    _, cnt_hv = O.hot_values(spec, bn, bt, n_nodes, nu)
+    _, _, ch, _ = eng.eval(c.now, c.ds)
+    _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=(cnt_hv.astype(np.float64),
+                                                                    np.full(n_nodes, now, np.int64)))
+    assert np.array_equal(ch, och)
+    eng.close()
+
+
 @pytest.mark.parametrize("threads,k2x,k2", [(128, 512, 0), (256, 512, 0), (256, 1024, 0), (256, 256, 0),
                                             (256, 4096, 3), (256, 2048, 3), (256, -4096, 3)])
 @pytest.mark.parametrize("case", ["one_hot_node", "eight_windows", "last_node", "odd_counts"])
