@@ -108,9 +108,12 @@ constexpr int kK1S1Cap = 256;
 // SPLIT (with STEP; large N): classify and count only — the stepped records and queue items
 // go to HBM for k3a_emit, so no LDS staging and no epilogue (short-lived workgroups, more of
 // them per CU, the SoA stream is what bounds the launch).
-template <int PD, int PR, int kK1Threads, bool STEP, bool SPLIT = false>
-// 4x6 shape: registers for 5 waves per SIMD (with the ~30 KB of LDS, 5 workgroups per CU)
-__global__ __launch_bounds__(kK1Threads) __attribute__((amdgpu_waves_per_eu(PD * PR <= 24 ? 5 : 1)))
+// WPE: waves per SIMD the 4x6 shape's registers are budgeted for (5: with the fused form's ~30 KB
+// of LDS, 5 workgroups per CU); HX 0: the dedupe-form K2 entries only when given, 1: never (the
+// buckets / annotation forms, fewer registers).  (The split count pass's variants are engine
+// option k1_count_form.)
+template <int PD, int PR, int kK1Threads, bool STEP, bool SPLIT = false, int WPE = 5, int HX = 0>
+__global__ __launch_bounds__(kK1Threads) __attribute__((amdgpu_waves_per_eu(PD * PR <= 24 ? WPE : 1)))
 void k1_node_pass(K1Args a, K1Step step) {
     const DevPolicy& pol = a.pol;
     const int64_t N = a.N;
@@ -150,7 +153,7 @@ void k1_node_pass(K1Args a, K1Step step) {
     __shared__ int32_t nrec;  // keys-only step: stepped records staged
     if (STEP && threadIdx.x == 0) nq = nrec = 0;
     auto hxh = reinterpret_cast<uint32_t(*)[kK1Threads]>(ush);  // dedupe-form K2: this block's window-rank buckets
-    const bool hx = a.hx_region != nullptr;
+    const bool hx = HX == 0 && a.hx_region != nullptr;
     StepSlots so;
     Rec r;
     int64_t pt[PD], qt[PR];
@@ -450,7 +453,7 @@ hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs
 
 // ---------------------------------------------------------------- launchers
 template <int PD, int PR>
-static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t st) {
+static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t st, int count_form) {
     if (a.N <= 0) return hipSuccess;
     const int T = a.threads;
     if (T != 128 && T != 256) return hipErrorInvalidValue;
@@ -466,6 +469,17 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
     if (step && step->srec) {  // split form: no LDS staging, the epilogue is k3a_emit's
         if (a.out || !step->qg || !step->qmg || !step->nqg) return hipErrorInvalidValue;
         const char* nm = "k1_node_pass+k3a_count";
+        if (T == 256 && PD * PR <= 24 && count_form != 0) {  // A/B forms of the count pass (4x6 shape)
+            const bool nohx = a.hx_region == nullptr;
+            switch (count_form) {
+                case 1: return nohx ? klaunch(nm, k1_node_pass<PD, PR, 256, true, true, 5, 1>, dim3(grid), dim3(256), 0, st, a, sa)
+                                    : klaunch(nm, k1_node_pass<PD, PR, 256, true, true, 5, 0>, dim3(grid), dim3(256), 0, st, a, sa);
+                case 2: return nohx ? klaunch(nm, k1_node_pass<PD, PR, 256, true, true, 6, 1>, dim3(grid), dim3(256), 0, st, a, sa)
+                                    : klaunch(nm, k1_node_pass<PD, PR, 256, true, true, 6, 0>, dim3(grid), dim3(256), 0, st, a, sa);
+                default: return nohx ? klaunch(nm, k1_node_pass<PD, PR, 256, true, true, 7, 1>, dim3(grid), dim3(256), 0, st, a, sa)
+                                     : klaunch(nm, k1_node_pass<PD, PR, 256, true, true, 7, 0>, dim3(grid), dim3(256), 0, st, a, sa);
+            }
+        }
         if (T == 256)
             return klaunch(nm, k1_node_pass<PD, PR, 256, true, true>, dim3(grid), dim3(256), 0, st, a, sa);
         return klaunch(nm, k1_node_pass<PD, PR, 128, true, true>, dim3(grid), dim3(128), 0, st, a, sa);
@@ -478,11 +492,11 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
                 : klaunch(nm, k1_node_pass<PD, PR, 128, false>, dim3(grid), dim3(128), lds, st, a, sa);
 }
 
-hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step) {
+hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step, int count_form) {
     switch (shape) {
-        case kShape4x6: return launch_k1_t<4, 6>(a, step, st);
-        case kShape8x8: return launch_k1_t<8, 8>(a, step, st);
-        default: return launch_k1_t<16, 16>(a, step, st);
+        case kShape4x6: return launch_k1_t<4, 6>(a, step, st, count_form);
+        case kShape8x8: return launch_k1_t<8, 8>(a, step, st, count_form);
+        default: return launch_k1_t<16, 16>(a, step, st, count_form);
     }
 }
 

@@ -351,7 +351,10 @@ struct K1Args {
     unsigned long long* trace;  // phase trace or null
 };
 // step (optional): also build the K3 step tables of a pod batch (K3a fused).
-hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr);
+// count_form (split form only): 0 the default kernel, 1 / 2 / 3 registers for 5 / 6 / 7 waves per
+// SIMD with the dedupe-form path compiled out when no K2 entries are given (A/B)
+hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr,
+                            int count_form = 0);
 // split form's second kernel: one workgroup per producer block of the node pass (bs nodes) of
 // bt threads (bs, or 64: one wave per block)
 hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs, hipStream_t st, int32_t bt = 0);

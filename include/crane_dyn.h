@@ -305,6 +305,7 @@ const char *crane_dyn_version(void);
  *   "k1_split" 0 fused node pass | 1 count pass + k3a_emit | 2 split past one round of workgroups
  *   "emit_threads" 0 k3a_emit workgroups as wide as the block | 64 one wave per block
  *   "k2_sorted" 1 a time-ordered log (checked at upload): K2 reads the widest window's suffix only | 0 never
+ *   "k1_count_form" 0 | 1 | 2 | 3: the split form's count pass budgeted for 5 / 6 / 7 waves per SIMD (A/B)
  *   "keys_path" 0 step path | 1 per-pair kernel   "greedy_form" 0 merge | 1 sequential
  *   "matrix_vec" 0 auto | 1 | 4 | 8 | 16 nodes per lane   "matrix_chunk" 0 auto | pods per workgroup (<= 1024)
  *   "step_rows" 1 producers index the records per pod tile | 0 K3s searches them
