@@ -10,10 +10,5 @@ tail -3 $OUT/pytest_new.log
 timeout -k 10 300 python -u tools/dropin_probe.py 5000 256 > $OUT/dropin_5k.json 2> $OUT/dropin_5k.err || { tail -30 $OUT/dropin_5k.err; exit 1; }
 timeout -k 10 400 python -u tools/dropin_probe.py 100000 256 > $OUT/dropin_100k.json 2> $OUT/dropin_100k.err || { tail -30 $OUT/dropin_100k.err; exit 1; }
 cut -c1-2500 $OUT/dropin_5k.json; echo; cut -c1-3500 $OUT/dropin_100k.json
-# cold 4M-node K1 / K2 legs: default vs 128-thread K1 workgroups (k1_threads)
-for o in "default" "k1_threads=128" "k1_split=1" "k1_split=1 emit_threads=64"; do
-  args=""; for x in $o; do [ "$x" != default ] && args="$args --opt $x"; done
-  f=$OUT/cold_$(echo $o | tr ' =' '__').json
-  timeout -k 10 300 python bench.py --leg cold --steps 5 $args > $f 2> $f.err || { tail -20 $f.err; exit 1; }
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], {k: (d[k]['ms'], d[k]['frac']) for k in ('k2','k1','k1_records')}, d['k1'].get('kernels'))" $f "$o"
-done
+# cold 4M-node K1 / K2 legs: the fused node pass and the split forms
+bash tools/gpu_r04c.sh ${1:-r04a} "default;k1_threads=128;k1_split=1;k1_split=1 emit_threads=64;k1_split=1 emit_threads=64 k1_count_form=1;k1_split=1 emit_threads=64 k1_count_form=2;k1_split=1 emit_threads=64 k1_count_form=3" || exit 1

@@ -12,3 +12,9 @@ for o in "${VARS[@]}"; do
   timeout -k 10 300 python bench.py --leg cold --steps 7 $args > $f 2> $f.err || { tail -20 $f.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], {k: (d[k]['ms'], d[k]['frac']) for k in ('k2','k2_timestamp_path','k1','k1_records')}, d['k1'].get('kernels'), d['k2'].get('kernels'))" $f "$o"
 done
+# phase traces of the node pass at 4M nodes: fused, and the split count pass
+for o in "" "--opt k1_split=1 --opt emit_threads=64"; do
+  f=$OUT/trace4M_$(echo "$o" | tr ' =-' '___').json
+  timeout -k 10 300 python tools/trace_step.py --nodes 4000000 --bindings 16000000 --reps 3 $o > $f 2> $f.err || { tail -20 $f.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], json.dumps(d.get('K1'))[:600])" $f "trace $o"
+done
