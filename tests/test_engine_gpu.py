@@ -179,9 +179,8 @@ def test_hot_values_time_ordered_log(order, k2):
     bn[::89] = -1
     bn[5::97] = n_nodes + 1
     if order == "ties":  # stamps exactly on the cutoffs (now - 300 s, now - 60 s) and one second around
-        bt = np.sort(np.concatenate([bt[: n_bind // 2], np.repeat(np.array([nu - 301, nu - 300, nu - 299, nu - 61,
-                                                                            nu - 60, nu - 59]), n_bind // 12)]))
-        bt = bt[:n_bind]
+        edge = np.array([nu - 301, nu - 300, nu - 299, nu - 61, nu - 60, nu - 59], np.int64)
+        bt = np.sort(np.concatenate([bt[: n_bind - 6 * (n_bind // 12)], np.repeat(edge, n_bind // 12)]))
     if order == "all_old":
         bt = np.sort(bt) - 10_000
     if order == "all_new":

@@ -4,7 +4,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${1:-r04a}
 mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest tests/test_dropin_gpu.py tests/test_plugin_cpp.py tests/test_shard_gpu.py tests/test_step_gpu.py tests/test_engine_gpu.py \
+timeout -k 10 900 python -u -m pytest tests -m gpu \
     -x -v --timeout 200 --timeout-method thread > $OUT/pytest_new.log 2>&1 || { echo "pytest failed"; tail -60 $OUT/pytest_new.log; exit 1; }
 tail -3 $OUT/pytest_new.log
 timeout -k 10 300 python -u tools/dropin_probe.py 5000 256 > $OUT/dropin_5k.json 2> $OUT/dropin_5k.err || { tail -30 $OUT/dropin_5k.err; exit 1; }
