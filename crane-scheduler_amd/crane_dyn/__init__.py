@@ -98,6 +98,8 @@ def _load():
         "crane_dyn_node_steps": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp, vp]),
         "crane_dyn_node_steps_subset": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp, vp, vp]),
         "crane_dyn_update_nodes": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp]),
+        "crane_dyn_update_node_steps": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, C.c_int64, C.c_int64, vp, vp, vp,
+                                                  vp]),
         "crane_dyn_version": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
@@ -122,7 +124,7 @@ ABI_SYMBOLS = (
     "crane_translate_event", "crane_dyn_debug_trace", "crane_num_feasible_nodes_to_find", "crane_dyn_select",
     "crane_tz_load", "crane_tz_load_bytes", "crane_tz_free", "crane_tz_lookup", "crane_tz_date",
     "crane_parse_annotation_tz", "crane_parse_annotations_tz", "crane_dyn_step_slots", "crane_dyn_node_steps",
-    "crane_dyn_node_steps_subset", "crane_dyn_update_nodes",
+    "crane_dyn_node_steps_subset", "crane_dyn_update_nodes", "crane_dyn_update_node_steps",
 )
 
 
@@ -567,6 +569,24 @@ class Engine:
             hv = np.ascontiguousarray(hv, np.float64).reshape(k)
             hv_ts = np.ascontiguousarray(hv_ts, np.int64).reshape(k)
         self._check(lib.crane_dyn_update_nodes(self.h, k, _ptr(idx), _ptr(val), _ptr(ts), _ptr(hv), _ptr(hv_ts)))
+
+    def update_node_steps(self, idx, val, ts, hv, hv_ts, t0_ns, t1_ns):
+        """update_nodes + node_steps_subset of the same nodes in one call (crane_dyn_update_node_steps)."""
+        idx = np.ascontiguousarray(idx, np.int64)
+        k, M = len(idx), len(self.metric_names)
+        val = np.ascontiguousarray(val, np.float64).reshape(M, k)
+        ts = np.ascontiguousarray(ts, np.int64).reshape(M, k)
+        if hv is not None:
+            hv = np.ascontiguousarray(hv, np.float64).reshape(k)
+            hv_ts = np.ascontiguousarray(hv_ts, np.int64).reshape(k)
+        S = lib.crane_dyn_step_slots(self.h)
+        ns = np.zeros(k, np.uint8)
+        bp = np.zeros((k, S), np.int64)
+        ff = np.zeros((k, S + 1), np.int8)
+        sc = np.zeros((k, S + 1), np.int8)
+        self._check(lib.crane_dyn_update_node_steps(self.h, k, _ptr(idx), _ptr(val), _ptr(ts), _ptr(hv), _ptr(hv_ts),
+                                                    int(t0_ns), int(t1_ns), _ptr(ns), _ptr(bp), _ptr(ff), _ptr(sc)))
+        return ns, bp, ff, sc
 
     @staticmethod
     def table_lookup(tables, now_ns):

@@ -1269,14 +1269,24 @@ static int check_subset(crane_dyn* h, int64_t k, const int64_t* idx) {
     return CRANE_OK;
 }
 
-int crane_dyn_update_nodes(crane_dyn* h, int64_t k, const int64_t* idx, const double* val, const int64_t* ts,
-                           const double* hv, const int64_t* hv_ts) {
-    if (!h) return CRANE_E_INVALID;
-    Locked lk(h);
+// Table rows the fused update writes (crane_dyn_update_node_steps): outputs of k rows.
+struct RowOut {
+    int64_t t0, t1;
+    uint8_t* n_steps;
+    int64_t* bp;
+    int8_t* first_fail;
+    int8_t* score;
+};
+
+static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const double* val, const int64_t* ts,
+                         const double* hv, const int64_t* hv_ts, const RowOut* rows) {
     if (int rc = check_subset(h, k, idx)) return rc;
     const int64_t M = h->dp.n_slots;
     if (k > 0 && M > 0 && (!val || !ts)) return h->fail(CRANE_E_INVALID, "val/ts must not be NULL");
     if ((hv == nullptr) != (hv_ts == nullptr)) return h->fail(CRANE_E_INVALID, "hv and hv_ts must both be set or NULL");
+    if (rows && k > 0 && (!rows->n_steps || !rows->bp || !rows->first_fail || !rows->score))
+        return h->fail(CRANE_E_INVALID, "NULL output");
+    if (rows && !(rows->t0 < rows->t1)) return h->fail(CRANE_E_INVALID, "t0 must be before t1");
     if (k == 0) return CRANE_OK;
     HIPTRY(h, hipSetDevice(h->device));
     if (int rc = quiesce(h)) return rc;
@@ -1295,9 +1305,13 @@ int crane_dyn_update_nodes(crane_dyn* h, int64_t k, const int64_t* idx, const do
         HIPTRY(h, launch_fill_i64(h->hv_ts.p, h->N, kTsInvalid, h->stream));
         h->have_hv = true;
     }
-    // staging: idx [k] | val [M][k] | ts [M][k] | hv [k] | hv_ts [k]
-    const size_t K = (size_t)k, o_val = 8 * K, o_ts = o_val + 8 * (size_t)M * K, o_hv = o_ts + 8 * (size_t)M * K,
-                 o_hvt = o_hv + 8 * K, total = o_hvt + 8 * K;
+    // staging: in idx [k] | val [M][k] | ts [M][k] | hv [k] | hv_ts [k];  out (rows) bp [k][S] | ns [k] |
+    // ff [k][S+1] | sc [k][S+1]
+    const size_t K = (size_t)k, S = (size_t)node_step_slots(h->shape);
+    const size_t o_val = 8 * K, o_ts = o_val + 8 * (size_t)M * K, o_hv = o_ts + 8 * (size_t)M * K,
+                 o_hvt = o_hv + 8 * K, o_out = o_hvt + 8 * K;
+    const size_t r_ns = o_out + 8 * K * S, r_ff = r_ns + K, r_sc = r_ff + K * (S + 1), r_end = r_sc + K * (S + 1);
+    const size_t total = rows ? r_end : o_out;
     HIPTRY(h, h->upd_host.reserve(total));
     HIPTRY(h, h->upd_dev.reserve(total));
     unsigned char* p = h->upd_host.p;
@@ -1310,7 +1324,7 @@ int crane_dyn_update_nodes(crane_dyn* h, int64_t k, const int64_t* idx, const do
         std::memcpy(p + o_hv, hv, 8 * K);
         std::memcpy(p + o_hvt, hv_ts, 8 * K);
     }
-    HIPTRY(h, hipMemcpyAsync(h->upd_dev.p, p, hv ? total : o_hv, hipMemcpyHostToDevice, h->stream));
+    HIPTRY(h, hipMemcpyAsync(h->upd_dev.p, p, hv ? o_out : o_hv, hipMemcpyHostToDevice, h->stream));
     unsigned char* d = h->upd_dev.p;
     UpdateArgs a{};
     a.pol = h->dp;
@@ -1326,11 +1340,45 @@ int crane_dyn_update_nodes(crane_dyn* h, int64_t k, const int64_t* idx, const do
     a.hv = h->have_hv ? h->hv.p : nullptr;
     a.hv_ts = h->have_hv ? h->hv_ts.p : nullptr;
     a.rec = h->rec_dirty ? nullptr : h->rec.p;  // current records stay current
+    if (rows) {
+        a.ma.wsum = h->dp.wsum;
+        a.ma.noprio = h->dp.noprio;
+        std::memcpy(a.ma.pred_orig, h->pred_orig, sizeof a.ma.pred_orig);
+        a.t0 = rows->t0;
+        a.t1 = rows->t1;
+        a.bp = reinterpret_cast<int64_t*>(d + o_out);
+        a.ns = d + r_ns;
+        a.ff = reinterpret_cast<int8_t*>(d + r_ff);
+        a.sc = reinterpret_cast<int8_t*>(d + r_sc);
+    }
     HIPTRY(h, launch_update_nodes(h->shape, a, h->stream));
+    if (rows) HIPTRY(h, hipMemcpyAsync(p + o_out, d + o_out, r_end - o_out, hipMemcpyDeviceToHost, h->stream));
     // (waited for: the staging is reused, and work the caller enqueues next on its own
     // streams must see the new columns)
     HIPTRY(h, hipStreamSynchronize(h->stream));
+    if (rows) {
+        std::memcpy(rows->bp, p + o_out, 8 * K * S);
+        std::memcpy(rows->n_steps, p + r_ns, K);
+        std::memcpy(rows->first_fail, p + r_ff, K * (S + 1));
+        std::memcpy(rows->score, p + r_sc, K * (S + 1));
+    }
     return CRANE_OK;
+}
+
+int crane_dyn_update_nodes(crane_dyn* h, int64_t k, const int64_t* idx, const double* val, const int64_t* ts,
+                           const double* hv, const int64_t* hv_ts) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    return update_locked(h, k, idx, val, ts, hv, hv_ts, nullptr);
+}
+
+int crane_dyn_update_node_steps(crane_dyn* h, int64_t k, const int64_t* idx, const double* val, const int64_t* ts,
+                                const double* hv, const int64_t* hv_ts, int64_t t0_ns, int64_t t1_ns,
+                                uint8_t* n_steps, int64_t* bp, int8_t* first_fail, int8_t* score) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    const RowOut rows{t0_ns, t1_ns, n_steps, bp, first_fail, score};
+    return update_locked(h, k, idx, val, ts, hv, hv_ts, &rows);
 }
 
 int crane_dyn_node_steps_subset(crane_dyn* h, int64_t t0_ns, int64_t t1_ns, int64_t k, const int64_t* idx,

@@ -230,7 +230,7 @@ __device__ __forceinline__ uint32_t wave_aggregate(const int32_t* key, int32_t* 
     return nw;
 }
 
-template <int BT>
+template <int BT, bool POS>
 __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __restrict__ bnode,
                                          const int64_t* __restrict__ bts, int64_t B, int64_t N, const HotCutoffs& cut,
                                          const HotPart& g, uint32_t* __restrict__ CO, uint32_t* __restrict__ region) {
@@ -247,22 +247,12 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     const int64_t b0 = (int64_t)blk * kXChunk + threadIdx.x;
     int32_t nd[kPer];
     int64_t ts[kPer];
-    if (cut.by_pos) {  // a time-ordered log: the window rank from the position, no timestamps read
 #pragma unroll
-        for (int u = 0; u < kPer; ++u) {
-            const int64_t b = b0 + u * BT, bc = min(b, B - 1);
-            nd[u] = bnode[bc];
-            ts[u] = b;
-            if (b >= B) nd[u] = -1;
-        }
-    } else {
-#pragma unroll
-        for (int u = 0; u < kPer; ++u) {  // unconditional loads (clamped index): all in flight at once
-            const int64_t b = b0 + u * BT, bc = min(b, B - 1);
-            nd[u] = bnode[bc];
-            ts[u] = bts[bc];
-            if (b >= B) nd[u] = -1;
-        }
+    for (int u = 0; u < kPer; ++u) {  // unconditional loads (clamped index): all in flight at once
+        const int64_t b = b0 + u * BT, bc = min(b, B - 1);
+        nd[u] = bnode[bc];
+        ts[u] = POS ? b : bts[bc];  // POS: the window rank from the position, no stamp loaded
+        if (b >= B) nd[u] = -1;
     }
     for (int i = threadIdx.x; i < kDSlots; i += BT) {
         hkey[i] = -1;
@@ -315,14 +305,14 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
 // in flight the idle waves of the widest cost throughput.  Engine option k2x_threads,
 // default 512 (config 3, one batch / 4 in flight: 1024 -> 0.0399 / 0.0168 ms per
 // step, 512 -> 0.0407 / 0.0141, 256 -> 0.0446 / 0.0147; tools/inflight_sweep.sh).
-template <int BT>
+template <int BT, bool POS>
 __global__ __launch_bounds__(BT) void k2x_dedupe(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
                                                  int64_t B, int64_t N, HotCutoffs cut, HotPart g,
                                                  uint32_t* __restrict__ CO, uint32_t* __restrict__ region) {
-    k2d_body<BT>((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
+    k2d_body<BT, POS>((int32_t)blockIdx.x, bnode, bts, B, N, cut, g, CO, region);
 }
 
-template <int BT>
+template <int BT, bool POS>
 __global__ __launch_bounds__(BT) void k2x_dedupe_pods(const int32_t* __restrict__ bnode,
                                                       const int64_t* __restrict__ bts, int64_t B, int64_t N,
                                                       HotCutoffs cut, HotPart g, uint32_t* __restrict__ CO,
@@ -330,7 +320,7 @@ __global__ __launch_bounds__(BT) void k2x_dedupe_pods(const int32_t* __restrict_
     // the pod tiles first: dispatched first, their sort overlaps the regions' aggregation
     // instead of trailing the launch
     if ((int64_t)blockIdx.x >= pp.ntiles) {
-        k2d_body<BT>((int32_t)(blockIdx.x - pp.ntiles), bnode, bts, B, N, cut, g, CO, region);
+        k2d_body<BT, POS>((int32_t)(blockIdx.x - pp.ntiles), bnode, bts, B, N, cut, g, CO, region);
     } else {
         extern __shared__ __attribute__((aligned(16))) unsigned char k3p_lds[];
         k3p_tile<BT>((int64_t)blockIdx.x, pp, k3p_lds);
@@ -352,15 +342,15 @@ HotPart hot_dedupe_geometry(int64_t B, int64_t N, int32_t W, int32_t bs) {
     return g;
 }
 
-template <int BT>
+template <int BT, bool POS>
 static hipError_t launch_dedupe_t(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
                                   const PodPrep* pods) {
     static const hipError_t attr = [] {
-        hipError_t e = hipFuncSetAttribute((const void*)k2x_dedupe<BT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           100 * 1024);
+        hipError_t e = hipFuncSetAttribute((const void*)k2x_dedupe<BT, POS>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
         if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k2x_dedupe_pods<BT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+            e = hipFuncSetAttribute((const void*)k2x_dedupe_pods<BT, POS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     100 * 1024);
         return e;
     }();
@@ -370,19 +360,27 @@ static hipError_t launch_dedupe_t(const int32_t* bnode, const int64_t* bts, int6
     size_t lds = sizeof(uint32_t) * (2 * (size_t)kDSlots + 2 * (size_t)g.nbins) + sizeof(uint16_t) * kXChunk;
     if (pods && pods->P > 0) lds = std::max(lds, kK3pLds);
     if (pods && pods->P > 0)
-        return klaunch("k2x_dedupe+k3p_pods", k2x_dedupe_pods<BT>, dim3((unsigned)(g.nblk + pods->ntiles)), dim3(BT),
-                       lds, st, bnode, bts, B, N, cut, g, CO, region, *pods);
-    return klaunch("k2x_dedupe", k2x_dedupe<BT>, dim3((unsigned)g.nblk), dim3(BT), lds, st, bnode, bts, B, N, cut, g,
-                   CO, region);
+        return klaunch("k2x_dedupe+k3p_pods", k2x_dedupe_pods<BT, POS>, dim3((unsigned)(g.nblk + pods->ntiles)),
+                       dim3(BT), lds, st, bnode, bts, B, N, cut, g, CO, region, *pods);
+    return klaunch("k2x_dedupe", k2x_dedupe<BT, POS>, dim3((unsigned)g.nblk), dim3(BT), lds, st, bnode, bts, B, N, cut,
+                   g, CO, region);
+}
+
+template <int BT>
+static hipError_t launch_dedupe_p(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
+                                  const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
+                                  const PodPrep* pods) {
+    return cut.by_pos ? launch_dedupe_t<BT, true>(bnode, bts, B, N, cut, g, scratch, st, pods)
+                      : launch_dedupe_t<BT, false>(bnode, bts, B, N, cut, g, scratch, st, pods);
 }
 
 hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                    const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
                                    const PodPrep* pods, int threads) {
     switch (threads) {
-        case 256: return launch_dedupe_t<256>(bnode, bts, B, N, cut, g, scratch, st, pods);
-        case 512: return launch_dedupe_t<512>(bnode, bts, B, N, cut, g, scratch, st, pods);
-        default: return launch_dedupe_t<1024>(bnode, bts, B, N, cut, g, scratch, st, pods);
+        case 256: return launch_dedupe_p<256>(bnode, bts, B, N, cut, g, scratch, st, pods);
+        case 512: return launch_dedupe_p<512>(bnode, bts, B, N, cut, g, scratch, st, pods);
+        default: return launch_dedupe_p<1024>(bnode, bts, B, N, cut, g, scratch, st, pods);
     }
 }
 
@@ -403,7 +401,10 @@ size_t hot_dedupe_scratch(const HotPart& g) { return (size_t)g.cap + (size_t)g.n
 //      (K1 reads them and leaves them, K1Args::buckets_keep).
 // Count/offset words: CO [nblk][nbins] (g.co_t = 0: X writes its row coalesced, Y reads a
 // column) or [nbins][nblk] (co_t = 1: Y reads its row coalesced, X writes a column).
-template <int BT, int REG>
+// POS: a time-ordered log ranked by position (HotCutoffs::by_pos): no timestamp loads (a
+// template parameter: a load inside a run-time branch makes the compiler wait for every load
+// at the join, which serialised the next region's prefetch)
+template <int BT, int REG, bool POS>
 __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(BT == 1024 ? 8 : 1)))
 void k2l_partition(const int32_t* __restrict__ bnode,
                                                     const int64_t* __restrict__ bts, int64_t B, int64_t N,
@@ -426,22 +427,12 @@ void k2l_partition(const int32_t* __restrict__ bnode,
     for (int i = threadIdx.x; i < g.nbins; i += BT) hist[i] = 0;
     auto load = [&](int64_t r, int32_t* nd, int64_t* ts) {  // unconditional loads, clamped index
         const int64_t b0 = r * REG + threadIdx.x;
-        if (cut.by_pos) {  // a time-ordered log: ranks from positions, no timestamps read
 #pragma unroll
-            for (int u = 0; u < kPer; ++u) {
-                const int64_t b = b0 + u * BT, bc = min(b, B - 1);
-                nd[u] = bnode[bc];
-                ts[u] = b;
-                if (b >= B) nd[u] = -1;
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < kPer; ++u) {
-                const int64_t b = b0 + u * BT, bc = min(b, B - 1);
-                nd[u] = bnode[bc];
-                ts[u] = bts[bc];
-                if (b >= B) nd[u] = -1;
-            }
+        for (int u = 0; u < kPer; ++u) {
+            const int64_t b = b0 + u * BT, bc = min(b, B - 1);
+            nd[u] = bnode[bc];
+            ts[u] = POS ? b : bts[bc];
+            if (b >= B) nd[u] = -1;
         }
     };
     int32_t nd[kPer];
@@ -616,22 +607,30 @@ HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W, int32_t reg, int32_t
     return g;
 }
 
+template <int BT, int REG, bool POS>
+static hipError_t launch_large_xp(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
+                                  const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, int n_cu,
+                                  hipStream_t st) {
+    const size_t lds = sizeof(uint32_t) * (4 * (size_t)REG + 2 * (size_t)g.nbins) + sizeof(uint16_t) * REG;
+    static const hipError_t attr =
+        hipFuncSetAttribute((const void*)k2l_partition<BT, REG, POS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            100 * 1024);
+    if (attr != hipSuccess) return attr;
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k2l_partition<BT, REG, POS>, BT,
+                                                               lds);
+    if (e != hipSuccess) return e;
+    const int64_t grid = std::min<int64_t>(g.nblk, (int64_t)std::max(1, per_cu) * std::max(1, n_cu));
+    return klaunch("k2l_partition", k2l_partition<BT, REG, POS>, dim3((unsigned)grid), dim3(BT), lds, st, bnode, bts,
+                   B, N, cut, g, scratch + g.cap, scratch);
+}
+
 template <int BT, int REG>
 static hipError_t launch_large_x(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                  const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, int n_cu,
                                  hipStream_t st) {
-    const size_t lds = sizeof(uint32_t) * (4 * (size_t)REG + 2 * (size_t)g.nbins) + sizeof(uint16_t) * REG;
-    static const hipError_t attr =
-        hipFuncSetAttribute((const void*)k2l_partition<BT, REG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            100 * 1024);
-    if (attr != hipSuccess) return attr;
-    int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k2l_partition<BT, REG>, BT,
-                                                               lds);
-    if (e != hipSuccess) return e;
-    const int64_t grid = std::min<int64_t>(g.nblk, (int64_t)std::max(1, per_cu) * std::max(1, n_cu));
-    return klaunch("k2l_partition", k2l_partition<BT, REG>, dim3((unsigned)grid), dim3(BT), lds, st, bnode, bts, B,
-                   N, cut, g, scratch + g.cap, scratch);
+    return cut.by_pos ? launch_large_xp<BT, REG, true>(bnode, bts, B, N, cut, g, scratch, n_cu, st)
+                      : launch_large_xp<BT, REG, false>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
 }
 
 hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,

@@ -101,6 +101,14 @@ struct UpdateArgs {
     double* hv;             // [N] or null (the shard holds no hot-value annotations)
     int64_t* hv_ts;
     void* rec;              // NodeRec [N] or null (records stale: the next node pass rebuilds them)
+    // optional: the changed nodes' answer-table rows over [t0, t1) (node_steps.hpp), row j for
+    // node idx[j] (ns null: none); ma carries wsum / noprio / pred_orig
+    MatrixArgs ma;
+    int64_t t0, t1;
+    uint8_t* ns;
+    int64_t* bp;
+    int8_t* ff;
+    int8_t* sc;
 };
 hipError_t launch_update_nodes(int shape, const UpdateArgs& a, hipStream_t st);
 // fill [n] int64 with v (hv_ts of a shard that had no hot-value annotations)

@@ -34,21 +34,13 @@
 #include "dyn_types.hpp"
 #include "kernels.hpp"
 #include "step_node.hpp"
+#include "node_steps.hpp"
 
 namespace crane {
 
 constexpr int kMxT = 256;       // threads per workgroup
 constexpr int kMxChunk = 1024;  // max pods per workgroup (LDS best keys)
 
-// first failing predicate at time t, in policy order (plugins.go:55-66); -1 = none
-template <int PD, int PR>
-__device__ __forceinline__ int32_t ff_at(int64_t t, const NodeRec<PD, PR>& r, const MatrixArgs& a) {
-    int32_t f = -1;
-#pragma unroll
-    for (int k = PD - 1; k >= 0; --k)
-        if (t < r.e_pred[k]) f = a.pred_orig[k];
-    return f;
-}
 
 __device__ __forceinline__ int32_t wave_max32(int32_t v) {
 #pragma unroll
@@ -323,40 +315,10 @@ template <int PD, int PR>
 __global__ __launch_bounds__(256) void k_node_steps(MatrixArgs a, int64_t t0, int64_t t1, uint8_t* __restrict__ ns,
                                                     int64_t* __restrict__ bp, int8_t* __restrict__ ffv,
                                                     int8_t* __restrict__ scv, const int64_t* __restrict__ idx) {
-    constexpr int S = PD + PR + 1;
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (n >= a.N) return;
     const NodeRec<PD, PR> r = static_cast<const NodeRec<PD, PR>*>(a.rec)[idx ? idx[n] : n];
-    int64_t e[S];
-    int c = 0;
-    auto put = [&](int64_t x) {
-        if (x > t0 && x < t1) e[c++] = x;
-    };
-#pragma unroll
-    for (int k = 0; k < PD; ++k) put(r.e_pred[k]);
-#pragma unroll
-    for (int k = 0; k < PR; ++k) put(r.e_prio[k]);
-    put(r.e_hv);
-    for (int i = 1; i < c; ++i) {  // insertion sort (at most S values)
-        const int64_t x = e[i];
-        int j = i - 1;
-        while (j >= 0 && e[j] > x) {
-            e[j + 1] = e[j];
-            --j;
-        }
-        e[j + 1] = x;
-    }
-    int m = 0;
-    for (int i = 0; i < c; ++i)
-        if (m == 0 || e[i] != e[m - 1]) e[m++] = e[i];
-    ns[n] = (uint8_t)m;
-    ffv[n * (S + 1)] = (int8_t)ff_at<PD, PR>(t0, r, a);
-    scv[n * (S + 1)] = (int8_t)score_at<PD, PR>(t0, r, a.wsum, a.noprio);
-    for (int i = 0; i < m; ++i) {
-        bp[n * S + i] = e[i];
-        ffv[n * (S + 1) + i + 1] = (int8_t)ff_at<PD, PR>(e[i], r, a);
-        scv[n * (S + 1) + i + 1] = (int8_t)score_at<PD, PR>(e[i], r, a.wsum, a.noprio);
-    }
+    node_steps_row<PD, PR>(r, a, t0, t1, n, ns, bp, ffv, scv);
 }
 
 int node_step_slots(int shape) {

@@ -8,7 +8,8 @@
 // changed node's parsed columns are staged (k entries) and scattered into the
 // shard's SoA here; when the node records are current, each changed node's
 // record is recomputed in place with the node pass's own arithmetic
-// (node_rec.hpp), so the answer tables of only those nodes need rebuilding.
+// (node_rec.hpp), so the answer tables of only those nodes need rebuilding — and the same
+// launch can write those rows (node_steps.hpp: crane_dyn_update_node_steps).
 //
 // One thread per changed node: k is a handful per scheduling cycle, so the
 // launch is latency-bound (one wave); nothing here is bandwidth-priced.
@@ -19,6 +20,7 @@
 #include "dyn_types.hpp"
 #include "kernels.hpp"
 #include "node_rec.hpp"
+#include "node_steps.hpp"
 
 namespace crane {
 
@@ -39,7 +41,7 @@ __global__ __launch_bounds__(256) void k_update_nodes(UpdateArgs a) {
         a.hv[i] = h;
         a.hv_ts[i] = ht;
     }
-    if (!a.rec) return;
+    if (!a.rec && !a.ns) return;
     int64_t pt[PD], qt[PR];
     double pv[PD], qv[PR];
 #pragma unroll
@@ -58,7 +60,8 @@ __global__ __launch_bounds__(256) void k_update_nodes(UpdateArgs a) {
     rec_metrics<PD, PR>(pol, pt, pv, qt, qv, r);
     rec_hot_annotation<PD, PR>(h, ht, r);
     rec_fail<PD, PR>(r);
-    static_cast<NodeRec<PD, PR>*>(a.rec)[i] = r;
+    if (a.rec) static_cast<NodeRec<PD, PR>*>(a.rec)[i] = r;
+    if (a.ns) node_steps_row<PD, PR>(r, a.ma, a.t0, a.t1, j, a.ns, a.bp, a.ff, a.sc);
 }
 
 __global__ __launch_bounds__(256) void k_fill_i64(int64_t* p, int64_t n, int64_t v) {

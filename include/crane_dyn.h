@@ -159,6 +159,11 @@ int crane_dyn_upload_nodes(crane_dyn *h, int64_t n_nodes, int64_t node_offset,
  * of those nodes is all a table of answers needs.  Synchronous. */
 int crane_dyn_update_nodes(crane_dyn *h, int64_t k, const int64_t *idx, const double *val, const int64_t *ts_ns,
                            const double *hv, const int64_t *hv_ts_ns);
+/* crane_dyn_update_nodes and crane_dyn_node_steps_subset of the same nodes over [t0, t1) in one
+ * call: one launch writes the columns, the records and the rows (one round trip to the device). */
+int crane_dyn_update_node_steps(crane_dyn *h, int64_t k, const int64_t *idx, const double *val, const int64_t *ts_ns,
+                                const double *hv, const int64_t *hv_ts_ns, int64_t t0_ns, int64_t t1_ns,
+                                uint8_t *n_steps, int64_t *bp, int8_t *first_fail, int8_t *score);
 
 /* Upload the binding records (BindingRecords heap content, binding.go:14-19):
  * node = LOCAL node index of the shard (<0 or >= n_nodes: matches no node),

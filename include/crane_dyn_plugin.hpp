@@ -19,8 +19,8 @@
 // lookups at its `now`.  At the start of each scheduling cycle the plugin compares
 // every NodeInfo of the snapshot with the one it parsed (its Node object, which the
 // informer replaces on every update, and its Generation): only the changed nodes
-// are re-parsed, scattered into the engine (crane_dyn_update_nodes) and their table
-// rows rebuilt (crane_dyn_node_steps_subset).  The whole snapshot is parsed again
+// are re-parsed, scattered into the engine and their table rows rebuilt in one call
+// (crane_dyn_update_node_steps).  The whole snapshot is parsed again
 // only when the node set changes, and the whole table only when a pod's time leaves
 // the horizon.
 //
@@ -140,6 +140,7 @@ struct CycleState {
             c->dyn_err_ = dyn_err_;
             std::call_once(c->dyn_once_, [] {});
             c->dyn_done_ = true;
+            c->dyn_ready_.store(true, std::memory_order_release);
         }
         return c;
     }
@@ -148,6 +149,7 @@ struct CycleState {
     friend class DynamicScheduler;
     mutable std::once_flag dyn_once_;
     mutable std::mutex clone_mu_;
+    std::atomic<bool> dyn_ready_{false};  // the cycle's answers are set (the lock-free fast path)
     bool dyn_done_ = false;
     std::shared_ptr<const void> dyn_row_;
     std::string dyn_err_;
@@ -469,11 +471,6 @@ class DynamicScheduler {
         std::vector<int64_t> ts;
         if (!parse(cnodes_, 1, &val, &ts, err)) return false;
         const size_t M = (size_t)crane_dyn_num_metrics(eng_);
-        if (crane_dyn_update_nodes(eng_, (int64_t)k, changed_.data(), val.data(), ts.data(), val.data() + M * k,
-                                   ts.data() + M * k)) {
-            *err = crane_dyn_last_error(eng_);
-            return false;
-        }
         for (size_t j = 0; j < k; ++j) {
             const size_t i = (size_t)changed_[j];
             v->nodes[i] = cnodes_[j];
@@ -483,14 +480,23 @@ class DynamicScheduler {
         if (v->name_idx.crowded()) v->index_names();  // entries of replaced Nodes pile up
         ++cnt_.incremental_syncs;
         cnt_.nodes_updated += k;
-        if (now < v->t0 || now >= v->t1) return true;  // the caller rebuilds the whole table
+        if (now < v->t0 || now >= v->t1) {  // the caller rebuilds the whole table: the columns only
+            if (crane_dyn_update_nodes(eng_, (int64_t)k, changed_.data(), val.data(), ts.data(), val.data() + M * k,
+                                       ts.data() + M * k)) {
+                *err = crane_dyn_last_error(eng_);
+                return false;
+            }
+            return true;
+        }
+        // the columns, the records and the changed nodes' rows in one launch (one round trip)
         const size_t S = v->S;
         rns_.resize(k);
         rbp_.resize(k * S);
         rff_.resize(k * (S + 1));
         rsc_.resize(k * (S + 1));
-        if (crane_dyn_node_steps_subset(eng_, v->t0, v->t1, (int64_t)k, changed_.data(), rns_.data(), rbp_.data(),
-                                        rff_.data(), rsc_.data())) {
+        if (crane_dyn_update_node_steps(eng_, (int64_t)k, changed_.data(), val.data(), ts.data(), val.data() + M * k,
+                                        ts.data() + M * k, v->t0, v->t1, rns_.data(), rbp_.data(), rff_.data(),
+                                        rsc_.data())) {
             *err = crane_dyn_last_error(eng_);
             return false;
         }
@@ -541,6 +547,11 @@ class DynamicScheduler {
 
     // The state of the cycle (brought up to date by the first caller of the cycle).
     const View* view_of(CycleState& state, std::string* err) {
+        if (state.dyn_ready_.load(std::memory_order_acquire)) {  // (every call after the first)
+            const View* v = static_cast<const View*>(state.dyn_row_.get());
+            if (!v) *err = state.dyn_err_;
+            return v;
+        }
         std::call_once(state.dyn_once_, [&] {
             std::string e;
             std::shared_ptr<const View> v;
@@ -552,6 +563,7 @@ class DynamicScheduler {
             state.dyn_row_ = v;
             state.dyn_err_ = e;
             state.dyn_done_ = true;
+            state.dyn_ready_.store(true, std::memory_order_release);
         });
         const View* v = static_cast<const View*>(state.dyn_row_.get());
         if (!v) *err = state.dyn_err_;

@@ -1,4 +1,5 @@
-"""Incremental drop-in updates (crane_dyn_update_nodes + crane_dyn_node_steps_subset).
+"""Incremental drop-in updates (crane_dyn_update_nodes + crane_dyn_node_steps_subset, and the
+fused crane_dyn_update_node_steps).
 
 The reference plugin reads the node's CURRENT annotations on every Filter / Score call
 (/root/reference/pkg/plugins/dynamic/stats.go:51-76) while the controller patches them
@@ -87,8 +88,13 @@ def test_incremental_tables_equal_rebuild_and_oracle(N, seed):
         hv_present = r != 6  # one round of patches without node_hot_value on those nodes
         now += int(rng.integers(1, 400)) * 10**6
         churn(c, spec, rng, idx, now, hv_present)
-        push(eng, c, idx, hv_present)
-        patch(tab, eng.node_steps_subset(t0, t1, idx), idx)
+        if r % 2:  # the fused form: columns, records and rows in one call
+            val, ts, _ = c.rows(eng.metric_names)
+            hv, hv_ts = (c.hv[idx], c.hv_ts[idx]) if hv_present else (None, None)
+            patch(tab, eng.update_node_steps(idx, val[:, idx], ts[:, idx], hv, hv_ts, t0, t1), idx)
+        else:
+            push(eng, c, idx, hv_present)
+            patch(tab, eng.node_steps_subset(t0, t1, idx), idx)
         if r in (0, 5, 11):  # the same engine's full table over its updated records
             assert same_tables(tab, eng.node_steps(t0, t1)), r
     fresh = engine_for(spec, c)  # one full upload of the final snapshot (K1's records)
