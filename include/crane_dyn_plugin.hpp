@@ -25,7 +25,8 @@
 // the horizon.
 //
 // Threading: the framework calls Filter/Score for one pod from 16 goroutines.
-// The first call of a cycle brings the plugin's state up to date under std::call_once;
+// The first call of a cycle brings the plugin's state up to date — the cycle's other
+// first calls, which must wait for it anyway, take chunks of its snapshot scan — and
 // every call after that reads it without taking a lock.  The state is patched in place
 // at the start of later cycles: the framework runs scheduling cycles one at a time, and
 // its binding cycles (which overlap the next scheduling cycle) call neither Filter nor
@@ -138,8 +139,8 @@ struct CycleState {
         if (dyn_done_) {
             c->dyn_row_ = dyn_row_;
             c->dyn_err_ = dyn_err_;
-            std::call_once(c->dyn_once_, [] {});
             c->dyn_done_ = true;
+            c->dyn_phase_.store(3, std::memory_order_relaxed);
             c->dyn_ready_.store(true, std::memory_order_release);
         }
         return c;
@@ -147,9 +148,12 @@ struct CycleState {
 
    private:
     friend class DynamicScheduler;
-    mutable std::once_flag dyn_once_;
     mutable std::mutex clone_mu_;
+    // the plugin's per-cycle sync: 0 not started, 1 the first caller brings the plugin up to
+    // date, 2 its scan of the snapshot is open to the cycle's other callers (dyn_job_), 3 done
+    std::atomic<int> dyn_phase_{0};
     std::atomic<bool> dyn_ready_{false};  // the cycle's answers are set (the lock-free fast path)
+    std::shared_ptr<void> dyn_job_;       // the open scan (set before phase 2, kept until the state dies)
     bool dyn_done_ = false;
     std::shared_ptr<const void> dyn_row_;
     std::string dyn_err_;
@@ -296,8 +300,9 @@ class DynamicScheduler {
     void SetHorizon(int64_t ns) { horizon_ns_ = ns > 0 ? ns : 1; }
     // work done so far: full tables built (a new node set or horizon), full snapshot parses,
     // cycles that found changed nodes, and the changed nodes re-parsed over them
+    // (sync_ns: wall time of the cycles' syncs, scan + update, as their leaders saw it)
     struct Counters {
-        uint64_t tables_built = 0, full_syncs = 0, incremental_syncs = 0, nodes_updated = 0;
+        uint64_t tables_built = 0, full_syncs = 0, incremental_syncs = 0, nodes_updated = 0, sync_ns = 0;
     };
     Counters counters() const {
         std::lock_guard<std::mutex> g(mu_);
@@ -510,8 +515,40 @@ class DynamicScheduler {
         return true;
     }
 
-    // The state for a cycle at `now`: compare the snapshot's NodeInfos with the synced ones.
-    std::shared_ptr<View> sync_locked(int64_t now, std::string* err) {
+    // The snapshot scan: every NodeInfo compared with the one its row was parsed from, in
+    // chunks any of the cycle's callers may take.
+    struct ScanJob {
+        const NodeInfo* const* L;
+        const NodeInfo* const* vi;
+        const Node* const* vn;
+        const int64_t* vg;
+        size_t n = 0, chunk = 0, nchunks = 0;
+        std::atomic<size_t> next{0}, done{0};
+        std::atomic<bool> full{false};  // a NodeInfo differs: the node set changed
+        std::vector<std::vector<int64_t>> changed;  // per chunk
+        void work() {
+            for (;;) {
+                const size_t c = next.fetch_add(1, std::memory_order_relaxed);
+                if (c >= nchunks) return;
+                const size_t hi = std::min(n, (c + 1) * chunk);
+                std::vector<int64_t>& out = changed[c];
+                for (size_t i = c * chunk; i < hi; ++i) {
+                    const NodeInfo* x = L[i];
+                    if (x != vi[i]) {
+                        full.store(true, std::memory_order_relaxed);
+                        break;
+                    }
+                    if (x->node() != vn[i] || x->Generation != vg[i]) out.push_back((int64_t)i);
+                }
+                done.fetch_add(1, std::memory_order_acq_rel);
+            }
+        }
+    };
+    static constexpr size_t kScanChunk = 4096;
+
+    // The state for a cycle at `now`: compare the snapshot's NodeInfos with the synced ones
+    // (with the cycle's other callers when `state` is given).
+    std::shared_ptr<View> sync_locked(int64_t now, std::string* err, CycleState* state = nullptr) {
         if (!handle_.snapshot) {
             *err = "no snapshot";
             return nullptr;
@@ -521,19 +558,24 @@ class DynamicScheduler {
         bool full = !v || L.size() != v->infos.size();
         changed_.clear();
         if (!full) {
-            const size_t n = L.size();
-            const NodeInfo* const* li = L.data();
-            const NodeInfo* const* vi = v->infos.data();
-            const Node* const* vn = v->nodes.data();
-            const int64_t* vg = v->gens.data();
-            for (size_t i = 0; i < n; ++i) {
-                const NodeInfo* x = li[i];
-                if (x != vi[i]) {
-                    full = true;
-                    break;
-                }
-                if (x->node() != vn[i] || x->Generation != vg[i]) changed_.push_back((int64_t)i);
+            auto job = std::make_shared<ScanJob>();
+            job->L = L.data();
+            job->vi = v->infos.data();
+            job->vn = v->nodes.data();
+            job->vg = v->gens.data();
+            job->n = L.size();
+            job->chunk = kScanChunk;
+            job->nchunks = (job->n + kScanChunk - 1) / kScanChunk;
+            job->changed.resize(job->nchunks);
+            if (state && job->nchunks > 1) {
+                state->dyn_job_ = job;
+                state->dyn_phase_.store(2, std::memory_order_release);
             }
+            job->work();
+            while (job->done.load(std::memory_order_acquire) < job->nchunks) relax();
+            full = job->full.load(std::memory_order_relaxed);
+            if (!full)
+                for (const auto& c : job->changed) changed_.insert(changed_.end(), c.begin(), c.end());
         }
         if (full) {
             view_.reset();
@@ -545,30 +587,47 @@ class DynamicScheduler {
         return v;
     }
 
-    // The state of the cycle (brought up to date by the first caller of the cycle).
+    // The state of the cycle.  Its first caller brings the plugin up to date; the cycle's other
+    // callers (the framework's 16 goroutines, all waiting for the same answers) take chunks of
+    // the snapshot scan meanwhile, then wait for the leader's update.
     const View* view_of(CycleState& state, std::string* err) {
-        if (state.dyn_ready_.load(std::memory_order_acquire)) {  // (every call after the first)
-            const View* v = static_cast<const View*>(state.dyn_row_.get());
-            if (!v) *err = state.dyn_err_;
-            return v;
-        }
-        std::call_once(state.dyn_once_, [&] {
-            std::string e;
-            std::shared_ptr<const View> v;
-            {
-                std::lock_guard<std::mutex> g(mu_);  // one engine: syncs are serial
-                v = sync_locked(state.now_ns, &e);
+        if (!state.dyn_ready_.load(std::memory_order_acquire)) {
+            int ph = 0;
+            if (state.dyn_phase_.compare_exchange_strong(ph, 1, std::memory_order_acq_rel)) {
+                std::string e;
+                std::shared_ptr<const View> v;
+                {
+                    std::lock_guard<std::mutex> g(mu_);  // one engine: syncs are serial
+                    const auto t0 = std::chrono::steady_clock::now();
+                    v = sync_locked(state.now_ns, &e, &state);
+                    cnt_.sync_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                        std::chrono::steady_clock::now() - t0)
+                                        .count();
+                }
+                std::lock_guard<std::mutex> g(state.clone_mu_);
+                state.dyn_row_ = v;
+                state.dyn_err_ = e;
+                state.dyn_done_ = true;
+                state.dyn_phase_.store(3, std::memory_order_relaxed);
+                state.dyn_ready_.store(true, std::memory_order_release);
+            } else {
+                bool helped = false;
+                for (uint32_t k = 0; !state.dyn_ready_.load(std::memory_order_acquire); ++k) {
+                    if (!helped && state.dyn_phase_.load(std::memory_order_acquire) == 2) {
+                        static_cast<ScanJob*>(state.dyn_job_.get())->work();
+                        helped = true;
+                    }
+                    if (k < 4096) relax();
+                    else std::this_thread::yield();
+                }
             }
-            std::lock_guard<std::mutex> g(state.clone_mu_);
-            state.dyn_row_ = v;
-            state.dyn_err_ = e;
-            state.dyn_done_ = true;
-            state.dyn_ready_.store(true, std::memory_order_release);
-        });
+        }
         const View* v = static_cast<const View*>(state.dyn_row_.get());
         if (!v) *err = state.dyn_err_;
         return v;
     }
+
+    static void relax() { __builtin_ia32_pause(); }
 
     Handle handle_;
     crane_policy_doc* doc_ = nullptr;
