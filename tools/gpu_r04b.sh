@@ -14,6 +14,17 @@ run() {  # label, env, args
   timeout -k 10 240 env "$@" > $OUT/$lab.json 2> $OUT/$lab.err || { tail -20 $OUT/$lab.err; return 1; }
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['ms_per_step'], d['batches_in_flight']['batch_latency_ms'], d.get('allreduce_ms'), d.get('keys_match_1gpu'))" $OUT/$lab.json $lab
 }
+# host enqueue: one thread vs one host thread per engine (ctypes drops the GIL in the call)
+for q in 4 8; do
+  timeout -k 10 240 env GPU_MAX_HW_QUEUES=$q python tools/inflight_probe.py --bound --steps 2000 --inflight 4,8 > $OUT/enq_q$q.json 2>$OUT/enq_q$q.err || { tail -5 $OUT/enq_q$q.err; exit 1; }
+  timeout -k 10 240 env GPU_MAX_HW_QUEUES=$q python tools/inflight_probe.py --bound --threads --steps 2000 --inflight 4,8 > $OUT/enq_thr_q$q.json 2>$OUT/enq_thr_q$q.err || { tail -5 $OUT/enq_thr_q$q.err; exit 1; }
+  echo "q$q one-thread $(cat $OUT/enq_q$q.json)"; echo "q$q threads $(cat $OUT/enq_thr_q$q.json)"
+done
+# batches in flight beyond the 4 hardware queues
+for k in 6 8; do
+  run plain_q8_k$k GPU_MAX_HW_QUEUES=8 python bench.py --no-extras --no-cpu-baseline --steps 512 --inflight $k || exit 1
+  run plain_q4_k$k GPU_MAX_HW_QUEUES=4 python bench.py --no-extras --no-cpu-baseline --steps 512 --inflight $k || exit 1
+done
 for q in 4 8; do
   for rep in 1 2; do
     run plain_q${q}_$rep GPU_MAX_HW_QUEUES=$q python bench.py --no-extras --no-cpu-baseline --steps 512 || exit 1
