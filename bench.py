@@ -994,7 +994,9 @@ def main():
         O.eval_soa(spec, eng.metric_names, okr, val, ts, np.ones(N, np.uint8), c.hv, c.hv_ts, c.now[:cp], c.ds[:cp],
                    threads=args.cpu_threads, want_matrix=False)
         dts = time.perf_counter() - t1
-        cpu = {"value": legs["threads_16"]["value"], "unit": "pod-node evals/s", "cores": args.cpu_threads,
+        # the headline's unit: a placement evaluates the pod against every node of the shard
+        cpu = {"value": round(legs["threads_16"]["value"] / N, 2), "unit": "placements/s",
+               "evals_per_s": legs["threads_16"]["value"], "cores": args.cpu_threads,
                "kind": "port",
                "sample": f"{legs['threads_16']['sample']}; string mode: every Filter/Score call re-parses its "
                          "annotations like stats.go:51-76 (oracle/crane_oracle.c)",
@@ -1002,7 +1004,8 @@ def main():
                "all_available_cpus": dict(legs["threads_all"], note=f"every CPU this process may use ({ncpu} of "
                                                                      f"nproc {os.cpu_count()}: affinity mask / cgroup "
                                                                      "quota)"),
-               "note": "C restatement, not the Go plugin (no Go toolchain, SURVEY 8c); it resolves the fixed-offset "
+               "note": f"placements/s = evals/s / {N} nodes (every node's Filter + Score per pod). "
+                       "C restatement, not the Go plugin (no Go toolchain, SURVEY 8c); it resolves the fixed-offset "
                        "zone once instead of utils.GetLocation's time.LoadLocation on every call (utils.go:35-45), "
                        "so it is a stronger baseline than the reference",
                "soa_mode": {"value": round(cp * N / dts, 1), "unit": "pod-node evals/s", "cores": args.cpu_threads,
