@@ -84,7 +84,10 @@ __device__ __forceinline__ int32_t score_at(int64_t t, const NodeRec<PD, PR>& r,
     int64_t base = 0;
     if (!noprio) {
         const double q = winv != 0.0 ? s * winv : s / wsum;  // stats.go:135 int(score / weight), Go CVTTSD2SQ
-        base = (q >= -9223372036854775808.0 && q < 9223372036854775808.0) ? (int64_t)q : INT64_MIN;
+        // |q| < 2^31 (every realistic score): one v_cvt_i32_f64 truncates toward zero exactly as
+        // the 64-bit conversion does; otherwise the full CVTTSD2SQ restatement (NaN, overflow)
+        if (__builtin_fabs(q) < 2147483648.0) base = (int64_t)(int32_t)q;
+        else base = (q >= -9223372036854775808.0 && q < 9223372036854775808.0) ? (int64_t)q : INT64_MIN;
     }
     const int64_t pen = t < r.e_hv ? r.pen : 0;
     const int64_t f = (int64_t)((uint64_t)base - (uint64_t)pen);  // plugins.go:91, wraps like Go
