@@ -171,6 +171,9 @@ struct crane_dyn {
     bool heap_mode = false;
     bool log_sorted = false;            // uploaded log in non-decreasing time order (upload_bindings)
     std::vector<int64_t> hts_copy;      // ... and its timestamps (the windows' suffixes are found here)
+    bool pos_valid = false;             // pos_s[r]: the suffix start of window rank r for cutoffs pos_cut
+    int64_t pos_cut[kMaxWin] = {};
+    int64_t pos_s[kMaxWin] = {};
     HostBuf<int32_t> hnode;       // pinned mirror of the slots in heap mode
     HostBuf<int64_t> hts;
     DevBuf<double> val, hv;
@@ -394,10 +397,15 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     HotCutoffs pcut = cut;
     const bool by_pos = h->log_sorted && h->opt.k2_sorted && dp.n_win > 0 && (int64_t)h->hts_copy.size() == h->B;
     if (by_pos) {
-        const int64_t* t0 = h->hts_copy.data();
-        const int64_t s0 = std::upper_bound(t0, t0 + h->B, cut.sorted[0]) - t0;
-        for (int r = 0; r < dp.n_win; ++r)
-            pcut.sorted[r] = (int64_t)(std::upper_bound(t0, t0 + h->B, cut.sorted[r]) - t0) - s0 - 1;
+        // (the cutoffs move once per second: the last search's suffixes are reused until they do)
+        if (!h->pos_valid || std::memcmp(h->pos_cut, cut.sorted, sizeof(int64_t) * dp.n_win) != 0) {
+            const int64_t* t0 = h->hts_copy.data();
+            for (int r = 0; r < dp.n_win; ++r) h->pos_s[r] = std::upper_bound(t0, t0 + h->B, cut.sorted[r]) - t0;
+            std::memcpy(h->pos_cut, cut.sorted, sizeof(int64_t) * dp.n_win);
+            h->pos_valid = true;
+        }
+        const int64_t s0 = h->pos_s[0];
+        for (int r = 0; r < dp.n_win; ++r) pcut.sorted[r] = h->pos_s[r] - s0 - 1;
         pcut.by_pos = 1;
         bn = h->bnode.p + s0;
         Bk = h->B - s0;
@@ -868,6 +876,7 @@ int crane_dyn_upload_bindings(crane_dyn* h, int64_t n, const int32_t* node, cons
     }
     // a ring of bindings appended in time order (the synthetic and the controller-shaped logs):
     // kept for the suffix search of every refresh
+    h->pos_valid = false;
     h->log_sorted = n > 0 && std::is_sorted(ts_s, ts_s + n);
     if (h->log_sorted) h->hts_copy.assign(ts_s, ts_s + n);
     else h->hts_copy.clear();
@@ -901,6 +910,7 @@ int crane_dyn_binding_records(crane_dyn* h, int64_t size, int64_t gc_time_range_
     h->heap.bind(h->hnode.p, h->hts.p);
     h->heap_mode = true;
     h->log_sorted = false;  // heap order
+    h->pos_valid = false;
     h->hts_copy.clear();
     h->B = size;
     return CRANE_OK;
