@@ -32,6 +32,7 @@ import os
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -104,6 +105,33 @@ def effective_cpus():
     except (OSError, ValueError):
         pass
     return n
+
+
+def task_cpu():
+    """{tid: (thread name, CPU seconds)} of this process's threads (/proc/self/task)."""
+    tick = os.sysconf("SC_CLK_TCK")
+    out = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            st = open(f"/proc/self/task/{tid}/stat").read()
+            name = st[st.index("(") + 1:st.rindex(")")]
+            f = st[st.rindex(")") + 2:].split()
+            out[int(tid)] = (name, (int(f[11]) + int(f[12])) / tick)  # utime + stime
+        except (OSError, ValueError, IndexError):
+            pass
+    return out
+
+
+def host_threads(c0, c1, t_enq, tc_enq, elapsed, steps):
+    """Host side of the timed loop: the enqueuing thread's wall and CPU time per step, and the
+    other threads of the process that used CPU meanwhile (e.g. a communicator's progress thread
+    beside the enqueuing thread; 10 ms tick resolution)."""
+    main = threading.get_native_id()
+    others = sorted(((c1[t][1] - c0.get(t, (None, 0.0))[1], c1[t][0]) for t in c1 if t != main), reverse=True)
+    return {"enqueue_us_per_step": round(t_enq * 1e6 / steps, 2),
+            "enqueue_cpu_us_per_step": round(tc_enq * 1e6 / steps, 2),
+            "other_threads_cpu_ms": [[n, round(s * 1e3, 1)] for s, n in others[:6] if s > 0],
+            "elapsed_ms": round(elapsed * 1e3, 3)}
 
 
 def cpu_model():
@@ -799,6 +827,13 @@ def main():
     for i in range(args.warmup):
         step(i=i)
     flush(args.warmup)
+    if coll:
+        # RCCL's first call at a given size sets that size up (a few hundred us at [64][10k]
+        # int64): untimed, call it once at every size the timed region reduces — both
+        # buffers' full groups and the last, partial group — so no setup lands in the timing
+        for b in range(2):
+            for nb in sorted({G, args.steps % G or G}):
+                collect(b, nb)
     torch.cuda.synchronize(dev)
     graph = None
     if args.graph:
@@ -822,15 +857,20 @@ def main():
     if coll:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    cpu0 = task_cpu()
     t0 = time.perf_counter()
+    tc0 = time.thread_time()
     for i in range(args.steps):
         timed_step(i)
     if graph is None:
         flush(args.steps)
+    t_enq = time.perf_counter() - t0
+    tc_enq = time.thread_time() - tc0
     torch.cuda.synchronize(dev)
     if coll:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    host = host_threads(cpu0, task_cpu(), t_enq, tc_enq, elapsed, args.steps)
     if coll:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1078,6 +1118,7 @@ def main():
             "placements_per_s": round(placements, 1),
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "allreduce_ms": None if ar_ms is None else round(ar_ms, 4),
+            "host": host,
             "keys_match_1gpu": keys_match,
             "keys_match_1gpu_how": keys_match_how,
             "roofline": roofline,
