@@ -40,7 +40,9 @@ struct DevBuf {
             n = 0;
             if (e != hipSuccess) return e;
         }
-        hipError_t e = hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T));
+        // + 64 B: a 16-byte vector load of a row's last element may run up to 12 B past it
+        // (the prefetching count pass's LDS-DMA of SoA / bucket rows, kernels.hip)
+        hipError_t e = hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T) + 64);
         if (e == hipSuccess) n = std::max<size_t>(want, 1);
         return e;
     }
@@ -126,7 +128,8 @@ struct Options {
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
     int emit_threads = 0;     // split form's k3a_emit workgroup: 0 = the block's width, 64 = one wave per block
     int k2_sorted = 1;        // a time-ordered log: K2 reads the widest window's suffix, ranks by position
-    int k1_count_form = 0;    // split form's count pass: 0 default, 1/2/3 registers for 5/6/7 waves (A/B)
+    int k1_count_form = 0;    // split form's count pass: 0 default, 1/2/3 registers for 5/6/7 waves (A/B),
+                              // 4 persistent with the next block's rows prefetched into LDS
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
 
@@ -495,6 +498,7 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
         a.hv_ts = h->hv_ts.p;
     }
     a.threads = k1_bs(h);
+    a.n_cu = h->n_cu;
     a.trace = (h->N + a.threads - 1) / a.threads <= kTraceWgs ? h->trace_region(1) : nullptr;
     HIPTRY(h, launch_node_pass(h->shape, a, st, step, h->opt.k1_count_form));
     if (consume) {
@@ -795,7 +799,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
     else if (n == "emit_threads" && (value == 0 || value == 64)) o.emit_threads = (int)value;
     else if (n == "k2_sorted" && range(0, 1)) o.k2_sorted = (int)value;
-    else if (n == "k1_count_form" && range(0, 3)) o.k1_count_form = (int)value;
+    else if (n == "k1_count_form" && range(0, 4)) o.k1_count_form = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
         if (o.trace) {

@@ -92,6 +92,36 @@ __global__ __launch_bounds__(kK2Threads) void k2_hot_count(const int32_t* __rest
 }
 
 // ---------------------------------------------------------------- K1
+// Hot-value part of the record from the node's K2 window-rank buckets bc[r]
+// (annotateNodeHotValue, node.go:113-121: value += count / p.Count, Go int division;
+// window w counts the bindings of buckets >= its cutoff rank): one running suffix sum.
+// cnt_out / hvc_out (null: not kept): the per-window counts and the value.
+template <int PD, int PR>
+__device__ __forceinline__ void rec_hot_counts(const DevPolicy& pol, const uint32_t (&bc)[kMaxWin], int64_t N, int64_t n,
+                                               uint32_t* __restrict__ cnt_out, double* __restrict__ hvc_out,
+                                               int64_t hv_ts_counts, NodeRec<PD, PR>& r) {
+    int64_t v = 0;
+    uint64_t suf = 0;
+#pragma unroll
+    for (int k = kMaxWin - 1; k >= 0; --k) {
+        if (k >= pol.n_win) continue;
+        suf += bc[k];
+        const int w = pol.win_of_rank[k];
+        if (cnt_out) cnt_out[(int64_t)w * N + n] = (uint32_t)suf;
+        // Go int division (truncates toward 0): exact multiply-high division when the
+        // count fits 32 bits and hotValue.count is in [1, 2^32)
+        if (pol.win_div_m[k] != 0 && suf <= 0xFFFFFFFFull)
+            v += (int64_t)div_magic((uint32_t)suf, pol.win_div_m[k], pol.win_div_sh[k]);
+        else
+            v += (int64_t)suf / pol.win_count[w];
+    }
+    // the plugin re-reads it via ParseFloat (exact) and rejects negatives (stats.go:71-73)
+    const double h = (double)v;
+    if (hvc_out) hvc_out[n] = h;  // kept for node passes after the buckets are consumed
+    r.pen = go_int(h * 10.0);
+    r.e_hv = v >= 0 ? sat_add(hv_ts_counts, kHotActiveNs) : kTsInvalid;
+}
+
 // One thread per node.  Reads the parsed SoA (and K2 buckets), writes the
 // node's NodeRec into LDS, then the workgroup streams its records out with
 // 16-byte coalesced stores.
@@ -270,34 +300,12 @@ void k1_node_pass(K1Args a, K1Step step) {
     if (n < N) {
         rec_metrics<PD, PR>(pol, pt, pv, qt, qv, r);
         if (buckets || hx) {
-            // annotateNodeHotValue (node.go:113-121): value += count / p.Count (Go int division)
-            // window w counts the bindings of buckets >= its cutoff rank (K2)
             if (buckets && !a.buckets_keep) {
 #pragma unroll
                 for (int b = 0; b < kMaxWin; ++b)  // consumed: leaves the buckets zeroed for the next K2
                     if (b < pol.n_win) (buckets + first)[(int64_t)b * N + threadIdx.x] = 0;
             }
-            // window of cutoff rank r counts the buckets >= r: one running suffix sum
-            int64_t v = 0;
-            uint64_t suf = 0;
-#pragma unroll
-            for (int r = kMaxWin - 1; r >= 0; --r) {
-                if (r >= pol.n_win) continue;
-                suf += bc[r];
-                const int w = pol.win_of_rank[r];
-                if (cnt_out) cnt_out[(int64_t)w * N + n] = (uint32_t)suf;
-                // Go int division (truncates toward 0): exact multiply-high division when the
-                // count fits 32 bits and hotValue.count is in [1, 2^32)
-                if (pol.win_div_m[r] != 0 && suf <= 0xFFFFFFFFull)
-                    v += (int64_t)div_magic((uint32_t)suf, pol.win_div_m[r], pol.win_div_sh[r]);
-                else
-                    v += (int64_t)suf / pol.win_count[w];
-            }
-            // the plugin re-reads it via ParseFloat (exact) and rejects negatives (stats.go:71-73)
-            const double h = (double)v;
-            if (a.hvc_out) a.hvc_out[n] = h;  // kept for node passes after the buckets are consumed
-            r.pen = go_int(h * 10.0);
-            r.e_hv = v >= 0 ? sat_add(hv_ts_counts, kHotActiveNs) : kTsInvalid;
+            rec_hot_counts<PD, PR>(pol, bc, N, n, cnt_out, a.hvc_out, hv_ts_counts, r);
         } else if (hv) {
             rec_hot_annotation<PD, PR>(hvl, hvt, r);
         } else {
@@ -374,6 +382,282 @@ void k1_node_pass(K1Args a, K1Step step) {
     const uint4* src = reinterpret_cast<const uint4*>(smem);
     uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(out) + first * (int64_t)sizeof(Rec));
     for (int64_t i = threadIdx.x; i < nvec; i += kK1Threads) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------- K1 count pass, prefetching (split form)
+// The split count pass as a persistent grid (the resident workgroups: 5 per CU at the default
+// policy, bound by the LDS staging): workgroup g takes the blocks g, g + grid, ... (their
+// xcd_block, so each XCD keeps its contiguous run and k3a_emit finds the records in its L2).
+// A block's rows — the SoA's value and stamp rows of every metric slot, the K2 bucket rows or
+// the hot-value annotation rows — are staged in LDS by LDS-DMA (global_load_lds_dwordx4: 1 KiB
+// per wave-instruction, no VGPR destination); each thread copies its node's values to registers,
+// then the NEXT block's DMA is issued and stays in flight through this block's record,
+// classification and publish.  The fused and the default count pass load a block and then work
+// on it, so a workgroup's loads are in flight only a quarter of its life (phase traces,
+// DESIGN 4.2); here they are in flight all the time.  All LDS is one dynamic array (a second
+// __shared__ object can make hipcc wait vmcnt(0) before an LDS access) and the barriers are raw
+// s_barrier after lgkmcnt(0): __syncthreads' fence would wait vmcnt(0) and drain the DMA.
+struct PfGeom {
+    int32_t ns;      // metric slots staged (pol.n_slots)
+    int32_t hvrow;   // chunk of the hot-value annotation rows (hv: 2 chunks, hv_ts: 2) or -1
+    int32_t bkrow;   // chunk of the first K2 bucket row (one chunk each) or -1
+    int32_t nchunk;  // 1 KiB chunks staged per block
+    int32_t grid;    // workgroups (a multiple of 8)
+};
+constexpr int kPfChunk = 1024;
+typedef __attribute__((address_space(3))) void* lds_void_t;
+typedef __attribute__((address_space(1))) void* glb_void_t;
+
+// Workgroup barriers of the prefetching pass, in asm with a memory clobber: the builtin s_barrier
+// does not order memory accesses (hipcc moved reads of the staging past it, after the next DMA),
+// and __syncthreads' fence waits vmcnt(0).  pf_barrier: this wave's LDS accesses done;
+// pf_barrier_dma: also its LDS-DMA and stores.
+__device__ __forceinline__ void pf_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void pf_barrier_dma() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Issue the LDS-DMA of block blk's rows into stage: chunk c (1 KiB) by wave c % 4.  8-byte rows
+// take two chunks per 256 nodes (2 nodes per lane), 4-byte bucket rows one (4 per lane); a lane
+// wholly past N reads the row's start instead (its bytes are never used), the one straddling N
+// reads up to 12 B past the row (the buffers carry 64 B of slack, engine.hip DevBuf).
+__device__ __forceinline__ void pf_issue(const K1Args& a, const PfGeom& pg, int64_t blk, unsigned char* stage) {
+    const int64_t N = a.N, first = blk * 256;
+    const int lane = threadIdx.x & 63;
+    for (int c = threadIdx.x >> 6; c < pg.nchunk; c += 4) {
+        const unsigned char* src;
+        if (pg.bkrow >= 0 && c >= pg.bkrow) {
+            const int64_t e = first + 4 * lane;
+            src = reinterpret_cast<const unsigned char*>(a.buckets + (int64_t)(c - pg.bkrow) * N + (e < N ? e : 0));
+        } else {
+            const int64_t e0 = first + 128 * (c & 1) + 2 * lane;
+            const int64_t e = e0 < N ? e0 : 0;
+            const int r = c >> 1;  // 8-byte row: val slots, ts slots, then hv, hv_ts
+            if (r < pg.ns) src = reinterpret_cast<const unsigned char*>(a.val + (int64_t)r * N + e);
+            else if (r < 2 * pg.ns) src = reinterpret_cast<const unsigned char*>(a.ts + (int64_t)(r - pg.ns) * N + e);
+            else if (r == 2 * pg.ns) src = reinterpret_cast<const unsigned char*>(a.hv + e);
+            else src = reinterpret_cast<const unsigned char*>(a.hv_ts + e);
+        }
+        __builtin_amdgcn_global_load_lds((glb_void_t)src, (lds_void_t)(stage + c * kPfChunk), 16, 0, 0);
+    }
+}
+
+// LDS traffic of the work between two blocks (the wave totals exchanged for the slot
+// assignment and the flat maxima) in inline asm: hipcc waits vmcnt(0) before every LDS access
+// it sees while an LDS-DMA is in flight (it cannot tell the targets apart), which would drain the
+// next block's prefetch; the asm carries its own lgkmcnt waits.
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+    return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+// (addr uniform: an SGPR moved into a VGPR here, so no address VGPR lives across the loop)
+__device__ __forceinline__ void asm_ds_write_b32(uint32_t addr, uint32_t v) {
+    uint32_t t;
+    asm volatile("v_mov_b32 %0, %1\n\tds_write_b32 %0, %2" : "=&v"(t) : "s"(addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint4 asm_ds_read_b128(uint32_t addr) {
+    uint4 v;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    return v;
+}
+
+template <int PD, int PR, int NCH>
+// 4 waves per SIMD (128 VGPRs): at 5 the loop spills ~100 VGPRs, and every reload's vmcnt wait
+// would drain the prefetch
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PD * PR <= 24 ? 4 : 1)))
+void k1_count_pf(K1Args a, K1Step step, PfGeom pg) {
+    using Rec = NodeRec<PD, PR>;
+    constexpr int BS = 256;
+    __shared__ __attribute__((aligned(16))) unsigned char stage[NCH * kPfChunk];
+    // per wave: one-step records | middle pieces << 16 of kind 0 and 1, queue items, flat maxima
+    __shared__ __attribute__((aligned(16))) uint32_t xch[5][4];
+    const int64_t N = a.N, nb = (N + BS - 1) / BS;
+    const int64_t tmin = step.batch[0], tmax = step.batch[1];  // K3p folded the batch range
+    int64_t b = blockIdx.x;
+    if (b < nb) pf_issue(a, pg, xcd_block(b, nb), stage);
+    for (; b < nb; b += pg.grid) {
+        // the thread index laundered per block: address arithmetic derived from it is redone
+        // each block instead of hoisted and kept live (spilled) across the loop
+        uint32_t tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63;
+        const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+        uint32_t xo = lds_off(&xch[0][0]);
+        asm volatile("" : "+s"(xo));
+        const int64_t blk = xcd_block(b, nb), first = blk * BS, n = first + tid;
+        // the policy re-read from the kernel arguments every block through a pointer the compiler
+        // cannot prove loop-invariant: hoisted out of the loop, its fields stayed live in SGPRs
+        // across it (222 SGPRs spilled, and 118 VGPRs with them)
+        const __attribute__((address_space(4))) K1Args* kp =
+            (const __attribute__((address_space(4))) K1Args*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kp));
+        const DevPolicy& pol = ((const K1Args*)kp)->pol;
+        pf_barrier_dma();  // this block's DMA (and the last block's stores) landed
+        CRANE_TSTAMP(a.trace, blk, 0);
+        // the node's values out of the staging (row r of 8-byte values at chunk 2r)
+        auto v8 = [&](int r) -> uint64_t {
+            return *reinterpret_cast<const uint64_t*>(stage + 2 * r * kPfChunk + 8 * tid);
+        };
+        int64_t pt[PD], qt[PR];
+        double pv[PD], qv[PR];
+#pragma unroll
+        for (int k = 0; k < PD; ++k) {
+            const int r = k < pol.npd ? pol.pred_slot[k] : 0;
+            pv[k] = __builtin_bit_cast(double, v8(r));
+            pt[k] = (int64_t)v8(pg.ns + r);
+        }
+#pragma unroll
+        for (int k = 0; k < PR; ++k) {
+            const int r = k < pol.npr ? pol.prio_slot[k] : 0;
+            qv[k] = __builtin_bit_cast(double, v8(r));
+            qt[k] = (int64_t)v8(pg.ns + r);
+        }
+        uint32_t bc[kMaxWin];
+        double hvl = 0.0;
+        int64_t hvt = kTsInvalid;
+        if (pg.bkrow >= 0) {
+#pragma unroll
+            for (int w = 0; w < kMaxWin; ++w)
+                bc[w] = w < pol.n_win
+                            ? *reinterpret_cast<const uint32_t*>(stage + (pg.bkrow + w) * kPfChunk + 4 * tid)
+                            : 0u;
+        } else if (pg.hvrow >= 0) {
+            hvl = __builtin_bit_cast(double, v8(pg.ns * 2));
+            hvt = a.hv_ts ? (int64_t)v8(pg.ns * 2 + 1) : a.hv_ts_counts;
+        }
+        pf_barrier();  // every value read: the staging is free
+        if (b + pg.grid < nb) pf_issue(a, pg, xcd_block(b + pg.grid, nb), stage);
+        CRANE_TSTAMP(a.trace, blk, 1);
+        Rec r;
+        const bool valid = n < N;
+        if (valid) {
+            rec_metrics<PD, PR>(pol, pt, pv, qt, qv, r);
+            if (pg.bkrow >= 0) {
+                if (!a.buckets_keep) {
+#pragma unroll
+                    for (int w = 0; w < kMaxWin; ++w)  // consumed: leaves the buckets zeroed for the next K2
+                        if (w < pol.n_win) a.buckets[(int64_t)w * N + n] = 0;
+                }
+                rec_hot_counts<PD, PR>(pol, bc, N, n, a.cnt_out, a.hvc_out, a.hv_ts_counts, r);
+            } else if (pg.hvrow >= 0) {
+                rec_hot_annotation<PD, PR>(hvl, hvt, r);
+            } else {
+                r.pen = 0;
+                r.e_hv = kTsInvalid;
+            }
+            rec_fail<PD, PR>(r);
+        }
+        CRANE_TSTAMP(a.trace, blk, 2);
+        // classify (step_count_queue's first half: in-range expiries per kind, the flat keys)
+        const int32_t s0 = score_at<PD, PR>(tmin, r, step.wsum, step.noprio, step.winv);
+        int cnt1 = 0;
+        int64_t mn1 = INT64_MAX, mx1 = INT64_MIN;
+        auto add = [&](int64_t e, int& c, int64_t& mn, int64_t& mx) {
+            const bool in = e > tmin && e <= tmax;
+            c += in;
+            mn = in ? min(mn, e) : mn;
+            mx = in ? max(mx, e) : mx;
+        };
+#pragma unroll
+        for (int k = 0; k < PR; ++k) add(r.e_prio[k], cnt1, mn1, mx1);
+        add(r.e_hv, cnt1, mn1, mx1);
+        int cnt0 = cnt1;
+        int64_t mn0 = mn1, mx0 = mx1;
+        add(r.e_fail, cnt0, mn0, mx0);  // DaemonSet pods bypass the Filter
+        if (!valid) cnt0 = cnt1 = 0;
+        const bool multi0 = cnt0 > 0 && mn0 != mx0, multi1 = cnt1 > 0 && mn1 != mx1;
+        const int32_t flat0 = valid && cnt0 == 0 ? key_of<PD, PR>(0, tmin, s0, r, n) : -1;
+        const int32_t flat1 = valid && cnt1 == 0 ? key_of<PD, PR>(1, tmin, s0, r, n) : -1;
+        // per lane: one-step records | middle pieces << 16 per kind; queue items << 16
+        const uint32_t w0 = (cnt0 ? (multi0 ? 2u : 1u) : 0u) | (multi0 ? (uint32_t)(cnt0 - 1) << 16 : 0u);
+        const uint32_t w1 = (cnt1 ? (multi1 ? 2u : 1u) : 0u) | (multi1 ? (uint32_t)(cnt1 - 1) << 16 : 0u);
+        const uint32_t w2 = ((cnt0 ? 1u : 0u) + (cnt1 ? 1u : 0u)) << 16;
+        uint32_t e0 = wave_scan_add(w0), e1 = wave_scan_add(w1), e2 = wave_scan_add(w2);
+        const int32_t f0 = wave_max(flat0), f1 = wave_max(flat1);
+        // the wave's totals and flat maxima to xch[.][wave], one exchange, one barrier: every lane
+        // then has the block's totals and the waves before its own (no LDS atomics)
+        if (lane == 63) {
+            asm_ds_write_b32(xo + 4 * (0 * 4 + wv), e0);
+            asm_ds_write_b32(xo + 4 * (1 * 4 + wv), e1);
+            asm_ds_write_b32(xo + 4 * (2 * 4 + wv), e2);
+            asm_ds_write_b32(xo + 4 * (3 * 4 + wv), (uint32_t)f0);
+            asm_ds_write_b32(xo + 4 * (4 * 4 + wv), (uint32_t)f1);
+        }
+        e0 -= w0;
+        e1 -= w1;
+        e2 -= w2;
+        pf_barrier();
+        uint32_t base[3], tot[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint4 x = asm_ds_read_b128(xo + 16 * k);
+            base[k] = (wv > 0 ? x.x : 0u) + (wv > 1 ? x.y : 0u) + (wv > 2 ? x.z : 0u);
+            tot[k] = x.x + x.y + x.z + x.w;
+        }
+        StepSlots so;
+        so.slot0 = cnt0 ? (int32_t)((base[0] + e0) & 0xFFFF) : -1;
+        so.mslot0 = multi0 ? (int32_t)((base[0] + e0) >> 16) : 0;
+        so.slot1 = cnt1 ? (int32_t)((base[1] + e1) & 0xFFFF) : -1;
+        so.mslot1 = multi1 ? (int32_t)((base[1] + e1) >> 16) : 0;
+        // queue items and the stepped record to HBM (k3a_emit builds the tables from them)
+        const int64_t qo = blk * 2 * BS;
+        if (cnt0 | cnt1) {
+            int qi = (int)((base[2] + e2) >> 16);
+            if (cnt0) {
+                step.qg[qo + qi] = tid | ((uint32_t)multi0 << 13) | ((uint32_t)so.slot0 << 14) |
+                                   ((uint32_t)tid << 24);
+                step.qmg[qo + qi] = so.mslot0;
+                ++qi;
+            }
+            if (cnt1) {
+                step.qg[qo + qi] = tid | (1u << 12) | ((uint32_t)multi1 << 13) | ((uint32_t)so.slot1 << 14) |
+                                   ((uint32_t)tid << 24);
+                step.qmg[qo + qi] = so.mslot1;
+            }
+            static_cast<Rec*>(step.srec)[n] = r;
+        }
+        if (tid < 6) {
+            // the block's flat maxima, record counts and queued items (step_publish's outputs)
+            const uint4 fx = asm_ds_read_b128(xo + 16 * (tid == 1 ? 4 : 3));
+            const int32_t fm = max(max((int32_t)fx.x, (int32_t)fx.y), max((int32_t)fx.z, (int32_t)fx.w));
+            if (tid < 2) {
+                step.st.flat[blk * 2 + tid] = fm;
+                if (tid == 0) step.nqg[blk] = (int32_t)(tot[2] >> 16);
+            } else {
+                const int L = tid - 2;  // [kind][one-step records, middle pieces]
+                const uint32_t t = tot[L >> 1];
+                step.st.cnt[blk * 4 + L] = (int32_t)((L & 1) ? t >> 16 : t & 0xFFFF);
+            }
+        }
+        CRANE_TSTAMP(a.trace, blk, 3);
+        if (a.trace && tid == 0) a.trace[8 * blk + 6] = blockIdx.x;  // (which workgroup: tools/trace_pf.py)
+    }
+}
+
+template <int PD, int PR>
+static hipError_t launch_count_pf(const K1Args& a, const K1Step& sa, hipStream_t st) {
+    PfGeom pg{};
+    pg.ns = a.pol.n_slots;
+    const int rows8 = 2 * pg.ns;
+    const bool bk = a.buckets != nullptr;
+    const bool hvr = !bk && a.hv != nullptr;
+    pg.hvrow = hvr ? 2 * rows8 : -1;
+    pg.bkrow = bk ? 2 * rows8 : -1;
+    pg.nchunk = 2 * rows8 + (hvr ? (a.hv_ts ? 4 : 2) : 0) + (bk ? a.pol.n_win : 0);
+    // the staging's size is a template parameter: a static array beside the other LDS
+    // objects, whose accesses the compiler then knows the DMA does not write (one array
+    // made it wait vmcnt(0) — drain the prefetch — before every LDS atomic of the block)
+    auto kern = pg.nchunk <= 16 ? k1_count_pf<PD, PR, 16> : (pg.nchunk <= 28 ? k1_count_pf<PD, PR, 28> : k1_count_pf<PD, PR, 44>);
+    if (pg.nchunk > 44) return hipErrorInvalidValue;
+    const size_t lds = 0;
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 256, lds);
+    if (e != hipSuccess) return e;
+    const int64_t nb = (a.N + 255) / 256;
+    int64_t grid = (int64_t)std::max(1, per_cu) * std::max(1, a.n_cu);
+    grid = std::min<int64_t>(grid, (nb + 7) / 8 * 8);
+    grid = std::max<int64_t>(8, grid / 8 * 8);
+    pg.grid = (int32_t)grid;
+    return klaunch("k1_node_pass+k3a_count", kern, dim3((unsigned)grid), dim3(256), lds, st, a, sa, pg);
 }
 
 // ---------------------------------------------------------------- K3a emit (split form)
@@ -469,7 +753,9 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
     if (step && step->srec) {  // split form: no LDS staging, the epilogue is k3a_emit's
         if (a.out || !step->qg || !step->qmg || !step->nqg) return hipErrorInvalidValue;
         const char* nm = "k1_node_pass+k3a_count";
-        if (T == 256 && PD * PR <= 24 && count_form != 0) {  // A/B forms of the count pass (4x6 shape)
+        if (count_form == 4 && T == 256 && a.hx_region == nullptr && a.pol.n_slots <= 8 && a.n_cu > 0)
+            return launch_count_pf<PD, PR>(a, sa, st);
+        if (T == 256 && PD * PR <= 24 && count_form != 0 && count_form != 4) {  // A/B forms of the count pass (4x6 shape)
             const bool nohx = a.hx_region == nullptr;
             switch (count_form) {
                 case 1: return nohx ? klaunch(nm, k1_node_pass<PD, PR, 256, true, true, 5, 1>, dim3(grid), dim3(256), 0, st, a, sa)

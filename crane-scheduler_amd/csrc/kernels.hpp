@@ -356,11 +356,14 @@ struct K1Args {
     const uint32_t* hx_CO;
     int32_t hx_nblk;
     int32_t threads;        // workgroup size: 128 or 256
+    int32_t n_cu;           // compute units (the prefetching count pass sizes its persistent grid by it)
     unsigned long long* trace;  // phase trace or null
 };
 // step (optional): also build the K3 step tables of a pod batch (K3a fused).
 // count_form (split form only): 0 the default kernel, 1 / 2 / 3 registers for 5 / 6 / 7 waves per
-// SIMD with the dedupe-form path compiled out when no K2 entries are given (A/B)
+// SIMD with the dedupe-form path compiled out when no K2 entries are given (A/B), 4 the persistent
+// count pass that prefetches the next block's rows into LDS (k1_count_pf; not with the dedupe-form
+// K2 entries, whose block runs it cannot stage: those take the default kernel)
 hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr,
                             int count_form = 0);
 // split form's second kernel: one workgroup per producer block of the node pass (bs nodes) of
