@@ -129,7 +129,10 @@ struct Options {
     int emit_threads = 0;     // split form's k3a_emit workgroup: 0 = the block's width, 64 = one wave per block
     int k2_sorted = 1;        // a time-ordered log: K2 reads the widest window's suffix, ranks by position
     int k1_count_form = 0;    // split form's count pass: 0 default, 1/2/3 registers for 5/6/7 waves (A/B),
-                              // 4 persistent with the next block's rows prefetched into LDS
+                              // 4 persistent with the next block's rows prefetched into LDS, 5/6/7 streamed
+                              // (no records; k3a_emit rebuilds the stepped ones) at 8/7/6 waves, 8/9
+                              // streamed writing the stepped records, 6/7 waves, 10/11 streamed emitting
+                              // them (k3a_emit sorts only), 6/5 waves
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
 
@@ -464,7 +467,8 @@ static int k1_bs(const crane_dyn* h) {
 // K1 (optionally with the K3 step tables fused in).  Hot values: pending K2
 // counts (consumed), else the values the last consuming pass kept, else the
 // uploaded annotation.
-static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nullptr, const K1Step* step = nullptr) {
+static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nullptr, const K1Step* step = nullptr,
+                            K1Args* used = nullptr) {
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before the node pass");
     K1Args a{};
     a.pol = h->dp;
@@ -501,6 +505,7 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
     a.n_cu = h->n_cu;
     a.trace = (h->N + a.threads - 1) / a.threads <= kTraceWgs ? h->trace_region(1) : nullptr;
     HIPTRY(h, launch_node_pass(h->shape, a, st, step, h->opt.k1_count_form));
+    if (used) *used = a;
     if (consume) {
         if (!h->hx_pending) h->buckets_zero = !h->buckets_dense;  // K1 zeroed what it read
         h->counts_pending = false;
@@ -602,9 +607,15 @@ static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_k
             ks.qmg = h->sqm.p;
             ks.nqg = h->snq.p;
         }
-        int rc = node_pass_locked(h, st, nullptr, &ks);
+        K1Args used{};
+        int rc = node_pass_locked(h, st, nullptr, &ks, &used);
         if (rc) return rc;
-        if (split) HIPTRY(h, launch_step_emit(h->shape, ks, h->N, bs, st, h->opt.emit_threads ? h->opt.emit_threads : bs));
+        // after the streamed count pass the emit rebuilds the stepped records from the SoA
+        const bool rebuild = split && count_stream_rebuild(h->opt.k1_count_form, used);
+        const bool emitted = split && count_stream_emits(h->opt.k1_count_form, used);
+        if (split)
+            HIPTRY(h, launch_step_emit(h->shape, ks, h->N, bs, st, h->opt.emit_threads ? h->opt.emit_threads : bs,
+                                       rebuild || emitted ? &used : nullptr, emitted));
     } else {
         if (h->rec_dirty) {
             int rc = node_pass_locked(h, st);
@@ -799,7 +810,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
     else if (n == "emit_threads" && (value == 0 || value == 64)) o.emit_threads = (int)value;
     else if (n == "k2_sorted" && range(0, 1)) o.k2_sorted = (int)value;
-    else if (n == "k1_count_form" && range(0, 4)) o.k1_count_form = (int)value;
+    else if (n == "k1_count_form" && range(0, 11)) o.k1_count_form = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
         if (o.trace) {

@@ -660,6 +660,266 @@ static hipError_t launch_count_pf(const K1Args& a, const K1Step& sa, hipStream_t
     return klaunch("k1_node_pass+k3a_count", kern, dim3((unsigned)grid), dim3(256), lds, st, a, sa, pg);
 }
 
+// ---------------------------------------------------------------- K1 count pass, streamed (split form)
+// The split count pass without the NodeRec: each node's expiries and terms are folded as its
+// rows arrive into what the count pass needs — e_fail, the ordered score sum at tmin, the
+// in-range count / min / max per pod kind, the hot value — so about 30 VGPRs of record never
+// live (64 VGPRs: eight waves per SIMD instead of five), no LDS atomics (the waves' totals are
+// exchanged once, one barrier), and no stepped records written: k3a_emit rebuilds the few
+// stepped nodes' records from the SoA (k3a_emit<..., RC = true>).  Not with the dedupe-form K2
+// entries (their block runs need the default pass's LDS counting).
+// KEEP: the stepped nodes' records are built here and written to step.srec like the default
+// count pass's, instead of rebuilt by k3a_emit: a stepped lane re-reads its node's rows (lines
+// this wave just read, still in L2) once its classification is known — keeping the row values
+// live to the end instead cost the occupancy the streamed form is for (83 VGPRs, five waves:
+// 0.118 ms vs 0.096 cold, profiles/r04/k1_prefetch_ab.txt), and rebuilding them in k3a_emit
+// after they have left the caches cost 0.022 ms of gathers.
+// KEEP 2: the stepped lanes go one step further and write their one-step records (into the
+// block's st.stage staging) and middle pieces themselves — step_emit, as a fused node pass's lane
+// past its LDS staging does — so k3a_emit (SORT_ONLY) only sorts, publishes and writes the rows.
+template <int PD, int PR, int WPE, int KEEP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k1_count_stream(K1Args a, K1Step step) {
+    constexpr int BS = 256;
+    __shared__ __attribute__((aligned(16))) uint32_t xch[5][4];
+    const DevPolicy& pol = a.pol;
+    const int64_t N = a.N;
+    const int64_t blk = xcd_block(blockIdx.x, gridDim.x), first = blk * BS, n = first + threadIdx.x;
+    CRANE_TSTAMP(a.trace, blockIdx.x, 0);
+    const int lo = (int)min((int64_t)threadIdx.x, N - 1 - first);  // lane offset, clamped (K1's loads)
+    int64_t pt[PD], qt[PR];
+    double pv[PD], qv[PR];
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+        pt[k] = kTsInvalid;
+        pv[k] = 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+        qt[k] = kTsInvalid;
+        qv[k] = 0.0;
+    }
+    if (pol.n_slots > 0) {
+#pragma unroll
+        for (int k = 0; k < PD; ++k) {
+            const int64_t row = k < pol.npd ? pol.pred_slot[k] : 0;
+            pt[k] = (a.ts + (row * N + first))[lo];
+            pv[k] = (a.val + (row * N + first))[lo];
+        }
+#pragma unroll
+        for (int k = 0; k < PR; ++k) {
+            const int64_t row = k < pol.npr ? pol.prio_slot[k] : 0;
+            qt[k] = (a.ts + (row * N + first))[lo];
+            qv[k] = (a.val + (row * N + first))[lo];
+        }
+    }
+    uint32_t bc[kMaxWin];
+    double hvl = 0.0;
+    int64_t hvt = kTsInvalid;
+    if (a.buckets) {
+#pragma unroll
+        for (int b = 0; b < kMaxWin; ++b) bc[b] = b < pol.n_win ? (a.buckets + first)[(int64_t)b * N + lo] : 0u;
+    } else if (a.hv) {
+        hvl = a.hv[first + lo];
+        hvt = a.hv_ts ? a.hv_ts[first + lo] : a.hv_ts_counts;
+    }
+    const int64_t tmin = step.batch[0], tmax = step.batch[1];  // K3p folded the batch range
+    CRANE_TSTAMP(a.trace, blockIdx.x, 1);
+    const bool valid = n < N;
+    // isOverLoad per predicate (stats.go:94-112): the Filter rejects iff now < e_fail
+    int64_t e_fail = kTsInvalid;
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+        if (k < pol.npd) {
+            const double u = pv[k], lim = pol.pred_limit[k];
+            const bool over = pt[k] != kTsInvalid && !(u < 0.0) && lim != 0.0 && u > lim;
+            if (over) e_fail = max(e_fail, sat_add(pt[k], pol.pred_dur[k]));
+        }
+    }
+    // hot value (getNodeHotValue / the binding-log counts) -> penalty and its expiry
+    NodeRec<PD, PR> hr;  // (only pen / e_hv are set and read)
+    if (a.buckets) {
+        if (valid && !a.buckets_keep) {
+#pragma unroll
+            for (int b = 0; b < kMaxWin; ++b)  // consumed: leaves the buckets zeroed for the next K2
+                if (b < pol.n_win) (a.buckets + first)[(int64_t)b * N + threadIdx.x] = 0;
+        }
+        rec_hot_counts<PD, PR>(pol, bc, N, n, valid ? a.cnt_out : nullptr, valid ? a.hvc_out : nullptr,
+                               a.hv_ts_counts, hr);
+    } else if (a.hv) {
+        rec_hot_annotation<PD, PR>(hvl, hvt, hr);
+    } else {
+        hr.pen = 0;
+        hr.e_hv = kTsInvalid;
+    }
+    // priorities in policy order: score_at(tmin)'s ordered sum, and the in-range expiries both
+    // pod kinds share (priorities, hot value); e_fail is kind 0's too (DaemonSet pods bypass the
+    // Filter) — step_count_queue's classification without the record
+    double s = 0.0;
+    int cnt1 = 0;
+    int64_t mn1 = INT64_MAX, mx1 = INT64_MIN;
+    auto add = [&](int64_t e, int& c, int64_t& mn, int64_t& mx) {
+        const bool in = e > tmin && e <= tmax;
+        c += in;
+        mn = in ? min(mn, e) : mn;
+        mx = in ? max(mx, e) : mx;
+    };
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+        int64_t e = kTsInvalid;
+        double term = 0.0;
+        if (k < pol.npr && qt[k] != kTsInvalid && !(qv[k] < 0.0)) {
+            e = sat_add(qt[k], pol.prio_dur[k]);
+            term = (1.0 - qv[k]) * pol.prio_w[k];  // getScore (stats.go:89), no FMA
+            term = term * 100.0;
+        }
+        if (tmin < e) s += term;  // stats.go:124-133
+        add(e, cnt1, mn1, mx1);
+    }
+    add(hr.e_hv, cnt1, mn1, mx1);
+    int cnt0 = cnt1;
+    int64_t mn0 = mn1, mx0 = mx1;
+    add(e_fail, cnt0, mn0, mx0);
+    if (!valid) cnt0 = cnt1 = 0;
+    const int32_t s0 = score_of_sum(s, tmin < hr.e_hv ? hr.pen : 0, step.wsum, step.noprio, step.winv);
+    const bool multi0 = cnt0 > 0 && mn0 != mx0, multi1 = cnt1 > 0 && mn1 != mx1;
+    const int32_t flat0 = valid && cnt0 == 0 && !(tmin < e_fail) ? pack_key(s0, n) : -1;
+    const int32_t flat1 = valid && cnt1 == 0 ? pack_key(s0, n) : -1;
+    CRANE_TSTAMP(a.trace, blockIdx.x, 2);
+    // slots: wave prefix sums, then the waves' totals exchanged once (one barrier, no LDS atomics)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t w0 = (cnt0 ? (multi0 ? 2u : 1u) : 0u) | (multi0 ? (uint32_t)(cnt0 - 1) << 16 : 0u);
+    const uint32_t w1 = (cnt1 ? (multi1 ? 2u : 1u) : 0u) | (multi1 ? (uint32_t)(cnt1 - 1) << 16 : 0u);
+    const uint32_t w2 = ((cnt0 ? 1u : 0u) + (cnt1 ? 1u : 0u)) << 16;
+    uint32_t e0 = wave_scan_add(w0), e1 = wave_scan_add(w1), e2 = wave_scan_add(w2);
+    const int32_t f0 = wave_max(flat0), f1 = wave_max(flat1);
+    if (lane == 63) {
+        xch[0][wv] = e0;
+        xch[1][wv] = e1;
+        xch[2][wv] = e2;
+        xch[3][wv] = (uint32_t)f0;
+        xch[4][wv] = (uint32_t)f1;
+    }
+    e0 -= w0;
+    e1 -= w1;
+    e2 -= w2;
+    pf_barrier();  // (not __syncthreads: its fence would wait for this block's hvc / bucket stores)
+    uint32_t base[3], tot[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint4 x = *reinterpret_cast<const uint4*>(xch[k]);
+        base[k] = (wv > 0 ? x.x : 0u) + (wv > 1 ? x.y : 0u) + (wv > 2 ? x.z : 0u);
+        tot[k] = x.x + x.y + x.z + x.w;
+    }
+    const int64_t qo = blk * 2 * BS;
+    if (cnt0 | cnt1) {
+        if constexpr (KEEP) {
+            int64_t rt[PD], rq[PR];
+            double rv[PD], rw[PR];
+#pragma unroll
+            for (int k = 0; k < PD; ++k) {
+                const int64_t row = k < pol.npd ? pol.pred_slot[k] : 0;
+                rt[k] = pol.n_slots > 0 ? a.ts[row * N + n] : kTsInvalid;
+                rv[k] = pol.n_slots > 0 ? a.val[row * N + n] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < PR; ++k) {
+                const int64_t row = k < pol.npr ? pol.prio_slot[k] : 0;
+                rq[k] = pol.n_slots > 0 ? a.ts[row * N + n] : kTsInvalid;
+                rw[k] = pol.n_slots > 0 ? a.val[row * N + n] : 0.0;
+            }
+            NodeRec<PD, PR> r;
+            rec_metrics<PD, PR>(pol, rt, rv, rq, rw, r);
+            r.pen = hr.pen;
+            r.e_hv = hr.e_hv;
+            rec_fail<PD, PR>(r);
+            if constexpr (KEEP == 2) {
+                StepSlots so;
+                so.slot0 = cnt0 ? (int32_t)((base[0] + e0) & 0xFFFF) : -1;
+                so.mslot0 = multi0 ? (int32_t)((base[0] + e0) >> 16) : 0;
+                so.multi0 = multi0;
+                so.slot1 = cnt1 ? (int32_t)((base[1] + e1) & 0xFFFF) : -1;
+                so.mslot1 = multi1 ? (int32_t)((base[1] + e1) >> 16) : 0;
+                so.multi1 = multi1;
+                step_emit<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, so, step.st, blk,
+                                  step.st.stage + blk * 2 * step.st.bs, step.st.s1pad, step.winv);
+            } else {
+                static_cast<NodeRec<PD, PR>*>(step.srec)[n] = r;
+            }
+        }
+        const int32_t slot0 = (int32_t)((base[0] + e0) & 0xFFFF), slot1 = (int32_t)((base[1] + e1) & 0xFFFF);
+        int qi = (int)((base[2] + e2) >> 16);
+        if (KEEP == 2) cnt0 = cnt1 = 0;  // (nothing queued: the records are out)
+        if (cnt0) {
+            step.qg[qo + qi] = threadIdx.x | ((uint32_t)multi0 << 13) | ((uint32_t)slot0 << 14);
+            step.qmg[qo + qi] = multi0 ? (int32_t)((base[0] + e0) >> 16) : 0;
+            ++qi;
+        }
+        if (cnt1) {
+            step.qg[qo + qi] = threadIdx.x | (1u << 12) | ((uint32_t)multi1 << 13) | ((uint32_t)slot1 << 14);
+            step.qmg[qo + qi] = multi1 ? (int32_t)((base[1] + e1) >> 16) : 0;
+        }
+    }
+    if (threadIdx.x < 6) {
+        // the block's flat maxima, record counts and queued items (step_publish's outputs)
+        const uint4 fx = *reinterpret_cast<const uint4*>(xch[threadIdx.x == 1 ? 4 : 3]);
+        const int32_t fm = max(max((int32_t)fx.x, (int32_t)fx.y), max((int32_t)fx.z, (int32_t)fx.w));
+        if (threadIdx.x < 2) {
+            step.st.flat[blk * 2 + threadIdx.x] = fm;
+            if (threadIdx.x == 0) step.nqg[blk] = KEEP == 2 ? 0 : (int32_t)(tot[2] >> 16);
+        } else {
+            const int L = threadIdx.x - 2;  // [kind][one-step records, middle pieces]
+            const uint32_t t = tot[L >> 1];
+            step.st.cnt[blk * 4 + L] = (int32_t)((L & 1) ? t >> 16 : t & 0xFFFF);
+        }
+    }
+    CRANE_TSTAMP(a.trace, blockIdx.x, 3);
+    CRANE_TSTAMP(a.trace, blockIdx.x, 4);
+}
+
+// A stepped node's record rebuilt from the SoA for k3a_emit after the streamed count pass
+// (K1's own rec_metrics / hot-value / rec_fail, so the same bits as the record K1 builds);
+// the binding-log hot value is the one the count pass kept in hvc_out.
+template <int PD, int PR>
+__device__ __forceinline__ NodeRec<PD, PR> rec_rebuild(const K1Args& a, int64_t n) {
+    const DevPolicy& pol = a.pol;
+    const int64_t N = a.N;
+    int64_t pt[PD], qt[PR];
+    double pv[PD], qv[PR];
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+        const int64_t row = k < pol.npd ? pol.pred_slot[k] : 0;
+        pt[k] = pol.n_slots > 0 ? a.ts[row * N + n] : kTsInvalid;
+        pv[k] = pol.n_slots > 0 ? a.val[row * N + n] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+        const int64_t row = k < pol.npr ? pol.prio_slot[k] : 0;
+        qt[k] = pol.n_slots > 0 ? a.ts[row * N + n] : kTsInvalid;
+        qv[k] = pol.n_slots > 0 ? a.val[row * N + n] : 0.0;
+    }
+    NodeRec<PD, PR> r;
+    rec_metrics<PD, PR>(pol, pt, pv, qt, qv, r);
+    if (a.buckets) {
+        const double h = a.hvc_out[n];  // (int64 v as double: v >= 0 iff h >= 0)
+        r.pen = go_int(h * 10.0);
+        r.e_hv = h >= 0.0 ? sat_add(a.hv_ts_counts, kHotActiveNs) : kTsInvalid;
+    } else if (a.hv) {
+        rec_hot_annotation<PD, PR>(a.hv[n], a.hv_ts ? a.hv_ts[n] : a.hv_ts_counts, r);
+    } else {
+        r.pen = 0;
+        r.e_hv = kTsInvalid;
+    }
+    rec_fail<PD, PR>(r);
+    return r;
+}
+
+template <int PD, int PR, int WPE, int KEEP>
+static hipError_t launch_count_stream_w(const K1Args& a, const K1Step& sa, hipStream_t st) {
+    const unsigned grid = (unsigned)((a.N + 255) / 256);
+    return klaunch("k1_node_pass+k3a_count", k1_count_stream<PD, PR, WPE, KEEP>, dim3(grid), dim3(256), 0, st, a, sa);
+}
+
 // ---------------------------------------------------------------- K3a emit (split form)
 // One workgroup per producer block of the split node pass (NODES nodes): the block's queued
 // (node, kind) items are built from the stepped records in HBM (L2-resident: written by the
@@ -667,8 +927,12 @@ static hipError_t launch_count_pf(const K1Args& a, const K1Step& sa, hipStream_t
 // K1 epilogue.  BT threads: NODES (the block's own width), or one wave (BT = 64), whose
 // barriers are free and whose small LDS (CAP one-step records per kind staged; a block with
 // more goes through st.stage) lets many blocks' epilogues run on a CU at once.
-template <int PD, int PR, int NODES, int BT>
-__global__ __launch_bounds__(BT) void k3a_emit(K1Step step, int64_t N) {
+// RC: the count pass was the streamed one (no stepped records written): each queued node's
+// record is rebuilt from the SoA (rec_rebuild) instead of read from step.srec.
+// SORT_ONLY: the count pass wrote the one-step records into st.stage and the middle pieces
+// itself (count_stream_emits): no items; the staging is read by the global sort path.
+template <int PD, int PR, int NODES, int BT, bool RC = false, bool SORT_ONLY = false>
+__global__ __launch_bounds__(BT) void k3a_emit(K1Step step, int64_t N, K1Args a) {
     using Rec = NodeRec<PD, PR>;
     constexpr int CAP = BT == 64 ? 64 : (kK1S1Cap < 2 * NODES ? kK1S1Cap : 2 * NODES);
     __shared__ StepShared ssh;
@@ -692,16 +956,17 @@ __global__ __launch_bounds__(BT) void k3a_emit(K1Step step, int64_t N) {
     if (st.rows) tile_prefetch(st, &tpre);
     const int64_t tmin = step.batch[0], tmax = step.batch[1];
     __syncthreads();
-    const bool g1 = max(ssh.lc[0][0], ssh.lc[1][0]) > min(CAP, st.lds_cap);
+    const bool g1 = SORT_ONLY || max(ssh.lc[0][0], ssh.lc[1][0]) > min(CAP, st.lds_cap);
     Step1* s1b = g1 ? st.stage + blk * 2 * st.bs : s1l;
     const int64_t kst = g1 ? st.s1pad : (int64_t)CAP;
     const uint32_t* q = step.qg + blk * 2 * NODES;
     const int32_t* qm = step.qmg + blk * 2 * NODES;
     const Rec* rec = static_cast<const Rec*>(step.srec);
-    for (int w = threadIdx.x; w < nq; w += BT) {
+    for (int w = threadIdx.x; w < (SORT_ONLY ? 0 : nq); w += BT) {
         const uint32_t it = q[w];
         const int o = (int)(it & 0xFFF);
-        step_emit_one<PD, PR>(rec[first + o], first + o, (int)((it >> 12) & 1), (int32_t)((it >> 14) & 0x3FF), qm[w],
+        const Rec r = RC ? rec_rebuild<PD, PR>(a, first + o) : rec[first + o];
+        step_emit_one<PD, PR>(r, first + o, (int)((it >> 12) & 1), (int32_t)((it >> 14) & 0x3FF), qm[w],
                               ((it >> 13) & 1) != 0, tmin, tmax, step.wsum, step.noprio, st, blk, s1b, kst,
                               step.winv);
     }
@@ -717,25 +982,47 @@ __global__ __launch_bounds__(BT) void k3a_emit(K1Step step, int64_t N) {
 }
 
 template <int PD, int PR>
-static hipError_t launch_emit_t(const K1Step& step, int64_t N, int32_t bs, int32_t bt, hipStream_t st) {
+static hipError_t launch_emit_t(const K1Step& step, int64_t N, int32_t bs, int32_t bt, hipStream_t st,
+                                const K1Args* rc, bool sort_only) {
     const int64_t nb = (N + bs - 1) / bs;
     if (nb <= 0) return hipSuccess;
+    const K1Args a = rc ? *rc : K1Args{};
+    if (rc) {  // after the streamed count pass (256-node blocks): rebuild, or sort only
+        if (bs != 256) return hipErrorInvalidValue;
+        if (sort_only) {
+            if (bt == 64)
+                return klaunch("k3a_emit", k3a_emit<PD, PR, 256, 64, false, true>, dim3((unsigned)nb), dim3(64), 0, st,
+                               step, N, a);
+            return klaunch("k3a_emit", k3a_emit<PD, PR, 256, 256, false, true>, dim3((unsigned)nb), dim3(256), 0, st,
+                           step, N, a);
+        }
+        if (bt == 64)
+            return klaunch("k3a_emit", k3a_emit<PD, PR, 256, 64, true>, dim3((unsigned)nb), dim3(64), 0, st, step, N, a);
+        return klaunch("k3a_emit", k3a_emit<PD, PR, 256, 256, true>, dim3((unsigned)nb), dim3(256), 0, st, step, N, a);
+    }
     if (bs == 256 && bt == 64)
-        return klaunch("k3a_emit", k3a_emit<PD, PR, 256, 64>, dim3((unsigned)nb), dim3(64), 0, st, step, N);
-    if (bs == 256) return klaunch("k3a_emit", k3a_emit<PD, PR, 256, 256>, dim3((unsigned)nb), dim3(256), 0, st, step, N);
-    if (bs == 128) return klaunch("k3a_emit", k3a_emit<PD, PR, 128, 128>, dim3((unsigned)nb), dim3(128), 0, st, step, N);
+        return klaunch("k3a_emit", k3a_emit<PD, PR, 256, 64>, dim3((unsigned)nb), dim3(64), 0, st, step, N, a);
+    if (bs == 256) return klaunch("k3a_emit", k3a_emit<PD, PR, 256, 256>, dim3((unsigned)nb), dim3(256), 0, st, step, N, a);
+    if (bs == 128) return klaunch("k3a_emit", k3a_emit<PD, PR, 128, 128>, dim3((unsigned)nb), dim3(128), 0, st, step, N, a);
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs, hipStream_t st, int32_t bt) {
+hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs, hipStream_t st, int32_t bt,
+                            const K1Args* rc, bool sort_only) {
     switch (shape) {
-        case kShape4x6: return launch_emit_t<4, 6>(step, N, bs, bt, st);
-        case kShape8x8: return launch_emit_t<8, 8>(step, N, bs, bt, st);
-        default: return launch_emit_t<16, 16>(step, N, bs, bt, st);
+        case kShape4x6: return launch_emit_t<4, 6>(step, N, bs, bt, st, rc, sort_only);
+        case kShape8x8: return launch_emit_t<8, 8>(step, N, bs, bt, st, rc, sort_only);
+        default: return launch_emit_t<16, 16>(step, N, bs, bt, st, rc, sort_only);
     }
 }
 
 // ---------------------------------------------------------------- launchers
+bool count_stream(int count_form, const K1Args& a) {
+    return count_form >= 5 && count_form <= 11 && a.threads == 256 && a.hx_region == nullptr && a.out == nullptr;
+}
+bool count_stream_rebuild(int count_form, const K1Args& a) { return count_stream(count_form, a) && count_form <= 7; }
+bool count_stream_emits(int count_form, const K1Args& a) { return count_stream(count_form, a) && count_form >= 10; }
+
 template <int PD, int PR>
 static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t st, int count_form) {
     if (a.N <= 0) return hipSuccess;
@@ -755,7 +1042,18 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
         const char* nm = "k1_node_pass+k3a_count";
         if (count_form == 4 && T == 256 && a.hx_region == nullptr && a.pol.n_slots <= 8 && a.n_cu > 0)
             return launch_count_pf<PD, PR>(a, sa, st);
-        if (T == 256 && PD * PR <= 24 && count_form != 0 && count_form != 4) {  // A/B forms of the count pass (4x6 shape)
+        if (count_stream(count_form, a)) {
+            switch (count_form) {
+                case 5: return launch_count_stream_w<PD, PR, 8, 0>(a, sa, st);
+                case 6: return launch_count_stream_w<PD, PR, 7, 0>(a, sa, st);
+                case 7: return launch_count_stream_w<PD, PR, 6, 0>(a, sa, st);
+                case 8: return launch_count_stream_w<PD, PR, 6, 1>(a, sa, st);
+                case 9: return launch_count_stream_w<PD, PR, 7, 1>(a, sa, st);
+                case 10: return launch_count_stream_w<PD, PR, 6, 2>(a, sa, st);
+                default: return launch_count_stream_w<PD, PR, 5, 2>(a, sa, st);
+            }
+        }
+        if (T == 256 && PD * PR <= 24 && count_form >= 1 && count_form <= 3) {  // A/B forms of the count pass (4x6 shape)
             const bool nohx = a.hx_region == nullptr;
             switch (count_form) {
                 case 1: return nohx ? klaunch(nm, k1_node_pass<PD, PR, 256, true, true, 5, 1>, dim3(grid), dim3(256), 0, st, a, sa)

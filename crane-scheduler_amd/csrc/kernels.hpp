@@ -363,11 +363,25 @@ struct K1Args {
 // count_form (split form only): 0 the default kernel, 1 / 2 / 3 registers for 5 / 6 / 7 waves per
 // SIMD with the dedupe-form path compiled out when no K2 entries are given (A/B), 4 the persistent
 // count pass that prefetches the next block's rows into LDS (k1_count_pf; not with the dedupe-form
-// K2 entries, whose block runs it cannot stage: those take the default kernel)
+// K2 entries, whose block runs it cannot stage: those take the default kernel), 5 / 6 / 7 the
+// streamed count pass (k1_count_stream, no records: k3a_emit rebuilds the stepped ones)
 hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr,
                             int count_form = 0);
 // split form's second kernel: one workgroup per producer block of the node pass (bs nodes) of
 // bt threads (bs, or 64: one wave per block)
-hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs, hipStream_t st, int32_t bt = 0);
+// rc: the node pass was the streamed count pass (count_stream true): the emit rebuilds the
+// stepped nodes' records from the SoA with these node-pass arguments
+// (sort_only, with rc: the count pass emitted the records itself, count_stream_emits)
+hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs, hipStream_t st, int32_t bt = 0,
+                            const K1Args* rc = nullptr, bool sort_only = false);
+// the split form's count pass for this count_form is the streamed one (k1_count_stream: 5 / 6 / 7
+// = registers for 8 / 7 / 6 waves per SIMD, the stepped records rebuilt by k3a_emit; 8 / 9 = the
+// stepped records written by the count pass, registers for 6 / 7 waves; not with the dedupe-form
+// K2 entries)
+// 10 / 11: the stepped lanes also emit their one-step records and middle pieces (registers for
+// 6 / 5 waves), k3a_emit only sorts and publishes
+bool count_stream(int count_form, const K1Args& a);
+bool count_stream_rebuild(int count_form, const K1Args& a);
+bool count_stream_emits(int count_form, const K1Args& a);
 
 }  // namespace crane

@@ -76,11 +76,11 @@ template <int PD, int PR>
 // 0: the reciprocal is then exact and s * winv the same correctly rounded quotient as s / wsum,
 // one multiply instead of the division sequence (a uniform branch).
 __device__ __forceinline__ int32_t score_at(int64_t t, const NodeRec<PD, PR>& r, double wsum, int32_t noprio,
-                                          double winv = 0.0) {
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < PR; ++k)
-        if (t < r.e_prio[k]) s += r.t[k];  // stats.go:124-133, policy order
+                                          double winv = 0.0);
+
+// The score from the ordered sum s of the active priority terms and the active hot-value
+// penalty pen (0 when inactive): score_at's tail, shared with the streamed count pass.
+__device__ __forceinline__ int32_t score_of_sum(double s, int64_t pen, double wsum, int32_t noprio, double winv) {
     int64_t base = 0;
     if (!noprio) {
         const double q = winv != 0.0 ? s * winv : s / wsum;  // stats.go:135 int(score / weight), Go CVTTSD2SQ
@@ -89,9 +89,18 @@ __device__ __forceinline__ int32_t score_at(int64_t t, const NodeRec<PD, PR>& r,
         if (__builtin_fabs(q) < 2147483648.0) base = (int64_t)(int32_t)q;
         else base = (q >= -9223372036854775808.0 && q < 9223372036854775808.0) ? (int64_t)q : INT64_MIN;
     }
-    const int64_t pen = t < r.e_hv ? r.pen : 0;
     const int64_t f = (int64_t)((uint64_t)base - (uint64_t)pen);  // plugins.go:91, wraps like Go
     return (int32_t)(f < 0 ? 0 : (f > 100 ? 100 : f));            // NormalizeScore (utils.go:58-68)
+}
+
+template <int PD, int PR>
+__device__ __forceinline__ int32_t score_at(int64_t t, const NodeRec<PD, PR>& r, double wsum, int32_t noprio,
+                                          double winv) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < PR; ++k)
+        if (t < r.e_prio[k]) s += r.t[k];  // stats.go:124-133, policy order
+    return score_of_sum(s, t < r.e_hv ? r.pen : 0, wsum, noprio, winv);
 }
 
 // Filter (plugins.go:41-43, 55-66) + packed key for pod kind T (0: Filter applies, 1: DaemonSet)

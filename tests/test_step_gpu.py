@@ -28,13 +28,18 @@ def _check(spec, c, now, ds):
     # tables (split 0) or as the split form (count pass + k3a_emit, split 1)
     # the middle pieces raw or cut into elementary ones (step_pieces 1: whenever it pays); the
     # split form's k3a_emit as wide as the block (emit 0) or one wave per block (emit 64); the
-    # split form's count pass the default kernel (cf 0) or the persistent one that prefetches the
-    # next block's rows into LDS (cf 4, k1_count_pf)
+    # split form's count pass the default kernel (cf 0), the persistent one that prefetches the
+    # next block's rows into LDS (cf 4, k1_count_pf) or the streamed one without records, whose
+    # stepped records k3a_emit rebuilds from the SoA (cf 5 / 6 / 7, k1_count_stream), writes itself
+    # (cf 8 / 9) or emits itself (cf 10 / 11: k3a_emit only sorts)
     for rows, cap, split, pc, em, cf in ((1, 1 << 30, 0, 0, 0, 0), (0, 1 << 30, 0, 0, 0, 0), (1, 0, 0, 1, 0, 0),
                                          (0, 6, 0, 0, 0, 0), (1, 6, 0, 1, 0, 0), (1, 1 << 30, 1, 1, 0, 0),
                                          (0, 6, 1, 0, 0, 0), (1, 0, 1, 2, 0, 0), (1, 1 << 30, 0, 1, 0, 0),
                                          (1, 1 << 30, 1, 1, 64, 0), (0, 6, 1, 0, 64, 0), (1, 1 << 30, 1, 0, 64, 0),
-                                         (1, 1 << 30, 1, 1, 64, 4), (0, 6, 1, 0, 0, 4), (1, 0, 1, 2, 64, 4)):
+                                         (1, 1 << 30, 1, 1, 64, 4), (0, 6, 1, 0, 0, 4), (1, 0, 1, 2, 64, 4),
+                                         (1, 1 << 30, 1, 1, 64, 6), (0, 6, 1, 0, 0, 5), (1, 0, 1, 2, 64, 7),
+                                         (1, 1 << 30, 1, 1, 64, 8), (0, 6, 1, 0, 0, 9), (1, 1 << 30, 1, 1, 64, 10),
+                                         (0, 6, 1, 0, 0, 11), (1, 0, 1, 2, 64, 10)):
         eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap, "k1_split": split, "step_pieces": pc,
                                         "emit_threads": em, "k1_count_form": cf})
         _, _, ch, cs = eng.eval(now, ds)
@@ -127,7 +132,10 @@ def test_step_split_auto_at_large_n():
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 400_000, 1500, seed=30, pod_step_ns=4_000_000, ds_frac=0.02)
     out = []
-    for opts in ({"k1_split": 2}, {"k1_split": 0}, {"keys_path": 1}, {"k1_split": 2, "k1_count_form": 4}):
+    for opts in ({"k1_split": 2}, {"k1_split": 0}, {"keys_path": 1}, {"k1_split": 2, "k1_count_form": 4},
+                 {"k1_split": 2, "k1_count_form": 6, "emit_threads": 64},
+                 {"k1_split": 2, "k1_count_form": 8, "emit_threads": 64},
+                 {"k1_split": 2, "k1_count_form": 10, "emit_threads": 64}):
         eng = engine_for(spec, c, opts=opts)
         eng.set_profiling(True)
         _, _, ch, cs = eng.eval(c.now, c.ds)
@@ -244,18 +252,19 @@ def test_step_keys_async_matches_oracle(ride, pods):
     assert all(0 < t < 50 for _, t in times), times
 
 
-@pytest.mark.parametrize("split", [0, 1, 4], ids=["fused", "split", "split-prefetch"])
+@pytest.mark.parametrize("split", [0, 1, 4, 6, 8, 10], ids=["fused", "split", "split-prefetch", "split-stream",
+                                                             "split-stream-rec", "split-stream-emit"])
 @pytest.mark.parametrize("k2", [0, 1, 2, 3], ids=["dedupe", "binned", "hash", "large"])
 def test_step_keys_async_k2_forms(k2, split):
     """The combined step with each K2 form (dedupe: counts consumed by the fused node
     pass from per-block entries; binned / hash / large: buckets) equals the oracle, replayed,
     with the node pass fused with the step tables or split (count pass + k3a_emit; the count
-    pass prefetching the next block's rows into LDS: k1_count_form 4, which the dedupe form's
-    entries route to the default count pass)."""
+    pass prefetching the next block's rows into LDS: k1_count_form 4, or streamed without records:
+    6; the dedupe form's entries route both to the default count pass)."""
     import torch
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 20000, 3000, n_bindings=400_000, seed=29, pod_step_ns=2_000_000, ds_frac=0.03)
-    eng = engine_for(spec, c, opts={"k2_form": k2, "k1_split": min(split, 1), "k1_count_form": 4 if split == 4 else 0})
+    eng = engine_for(spec, c, opts={"k2_form": k2, "k1_split": min(split, 1), "k1_count_form": split if split > 1 else 0})
     eng.upload_bindings(c.b_node, c.b_ts)
     now = int(synth.NOW0_NS)
     dev = torch.device("cuda", 0)
