@@ -48,17 +48,29 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 PMC_DIR = os.path.join(ROOT, "profiles", "pmc")
 DROPIN = os.path.join(ROOT, "crane-scheduler_amd", "lib", "dropin_bench")
 # kernel timer name -> rocprofv3 kernel name (prefix, suffix) for the PMC lookup
+# dispatch-stamp name -> (rocprof kernel name without its template arguments, {argument index:
+# value}) — the node pass's STEP / SPLIT flags are its 4th / 5th template arguments, K3m's keys /
+# matrices its last two
 KERNEL_PMC = {
-    "k1_node_pass+k3a_steps": ("crane::k1_node_pass<", "true, false>"),
-    "k1_node_pass+k3a_count": ("crane::k1_node_pass<", "true, true>"),
-    "k1_node_pass": ("crane::k1_node_pass<", "false, false>"),
-    "k2x_dedupe+k3p_pods": ("crane::k2x_dedupe_pods", ""),
-    "k2x_dedupe": ("crane::k2x_dedupe", ""),
-    "k3p_pods": ("crane::k3p_pods", ""),
-    "k3s_eval": ("crane::k3s_eval<", ">"),
-    "k3m_matrix+keys": ("crane::k3m_matrix<", "true, true>"),
-    "k3m_matrix": ("crane::k3m_matrix<", "true, false>"),
+    "k1_node_pass+k3a_steps": ("crane::k1_node_pass", {3: "true", 4: "false"}),
+    "k1_node_pass+k3a_count": ("crane::k1_node_pass", {3: "true", 4: "true"}),
+    "k1_node_pass": ("crane::k1_node_pass", {3: "false", 4: "false"}),
+    "k2x_dedupe+k3p_pods": ("crane::k2x_dedupe_pods", {}),
+    "k2x_dedupe": ("crane::k2x_dedupe", {}),
+    "k3p_pods": ("crane::k3p_pods", {}),
+    "k3s_eval": ("crane::k3s_eval", {}),
+    "k3m_matrix+keys": ("crane::k3m_matrix", {-2: "true", -1: "true"}),
+    "k3m_matrix": ("crane::k3m_matrix", {-2: "true", -1: "false"}),
 }
+
+
+def pmc_name_match(kname, base, args):
+    """rocprof's kernel name kname is `base` (with any template arguments) whose arguments at the
+    given positions have the given values."""
+    head = kname.split("(", 1)[0]
+    tmpl = head[head.index("<") + 1:head.rindex(">")].split(", ") if "<" in head else []
+    name = head.split("<", 1)[0]
+    return name == base and all(-len(tmpl) <= i < len(tmpl) and tmpl[i] == v for i, v in args.items())
 
 
 def src_hash():
@@ -89,9 +101,8 @@ def pmc_summary(config, shash):
 def pmc_traffic(pmc, name):
     if not pmc or name not in KERNEL_PMC:
         return None
-    pre, suf = KERNEL_PMC[name]
-    hits = [v for k, v in pmc.get("kernels", {}).items()
-            if k.startswith(pre) and k.endswith(suf) and (suf or k == pre) and "traffic_bytes" in v]
+    base, args = KERNEL_PMC[name]
+    hits = [v for k, v in pmc.get("kernels", {}).items() if pmc_name_match(k, base, args) and "traffic_bytes" in v]
     return int(hits[0]["traffic_bytes"]) if hits else None
 
 
@@ -382,12 +393,16 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
     del scratch
     k2_ms, k1_ms, k1r_ms = float(np.median(k2)), float(np.median(k1)), float(np.median(k1r))
     k2ts_ms = float(np.median(k2ts))
-    tr_k2 = tr_k1 = tr_k1r = None
+    tr_k2 = tr_k2ts = tr_k1 = tr_k1r = None
     if pmc:
         ks = pmc.get("kernels", {})
-        k2t = [v.get("traffic_bytes") for k, v in ks.items() if k.startswith("crane::k2")]
-        if k2t and all(t is not None for t in k2t):
-            tr_k2 = int(sum(k2t))
+
+        def k2_traffic(pos):  # k2l_partition of one path (its last template argument: ranks by position) + k2y
+            t = [v.get("traffic_bytes") for k, v in ks.items()
+                 if pmc_name_match(k, "crane::k2l_partition", {-1: pos}) or pmc_name_match(k, "crane::k2y_bin_hist", {})]
+            return int(sum(t)) if len(t) == 2 and all(x is not None for x in t) else None
+
+        tr_k2, tr_k2ts = k2_traffic("true"), k2_traffic("false")
         tr_k1 = pmc_traffic(pmc, "k1_node_pass+k3a_steps")
         tr_k1r = pmc_traffic(pmc, "k1_node_pass")
     kb = k2_read(spec, c.b_ts, now)
@@ -400,7 +415,7 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
                        {"kernels": {k: round(float(np.median(v)), 4) for k, v in k2_parts.items()}}),
             "k2_timestamp_path": roof(12 * B + 4 * W * N, k2ts_ms, "every binding's node id + stamp read (12 B) "
                                       "+ per-node window counts written (4 B x W): the form for a log in no "
-                                      "particular order (engine option k2_sorted 0)", None,
+                                      "particular order (engine option k2_sorted 0)", tr_k2ts,
                                       {"kernels": {k: round(float(np.median(v)), 4) for k, v in k2ts_parts.items()}}),
             "k1": roof(alg_k1, k1_ms, "SoA (value, ts) read + window counts read + hot value written", tr_k1,
                        {"kernel": "k1_node_pass+k3a_steps (fused with the step tables)",
