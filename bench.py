@@ -209,6 +209,9 @@ def parse():
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache 4M-node K1/K2 roofline leg")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option name=value for the --leg runs (A/B of kernel forms; repeatable)")
+    ap.add_argument("--enqueue-threads", type=int, default=1,
+                    help="host threads enqueuing the timed batches (thread t drives the engines j with "
+                         "j %% threads == t; one rank without the collective only)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as a captured graph (measured slower than eager launches on ROCm 7.2)")
     return ap.parse_args()
@@ -871,12 +874,33 @@ def main():
 
     if coll:
         dist.barrier()
+    # several enqueuing threads (--enqueue-threads): thread t issues the batches i with i % T == t,
+    # so each engine and its stream are driven by one thread (the C calls release the GIL)
+    TQ = max(1, args.enqueue_threads)
+    if TQ > 1:
+        if coll or graph is not None or K % TQ:
+            sys.exit("bench.py: --enqueue-threads needs one rank, no graph, and --inflight a multiple of it")
+        go = threading.Barrier(TQ + 1)
+
+        def enqueue(t):
+            go.wait()
+            for i in range(t, args.steps, TQ):
+                step(i=i)
+
+        workers = [threading.Thread(target=enqueue, args=(t,)) for t in range(TQ)]
+        for w_ in workers:
+            w_.start()
     torch.cuda.synchronize(dev)
     cpu0 = task_cpu()
     t0 = time.perf_counter()
     tc0 = time.thread_time()
-    for i in range(args.steps):
-        timed_step(i)
+    if TQ > 1:
+        go.wait()
+        for w_ in workers:
+            w_.join()
+    else:
+        for i in range(args.steps):
+            timed_step(i)
     if graph is None:
         flush(args.steps)
     t_enq = time.perf_counter() - t0
@@ -1121,6 +1145,7 @@ def main():
                        "nodes_total": n_total, "nodes_per_gpu": N, "pods": P, "bindings_this_rank": B,
                        "parallelism": f"node-shard x{world}",
                        "launch": ("eager" if graph is None else "hipGraph replay per batch"),
+                       "enqueue_threads": TQ,
                        "batches_in_flight": K},
             "batches_in_flight": {"k": K, "how": "K engines (own copy of the shard's nodes, binding log, scratch) on "
                                                 "K HIP streams, batch i on engine i % K; every batch runs the whole "
