@@ -46,6 +46,7 @@ __device__ __forceinline__ void k3p_tile(const int64_t t, const PodPrep& pp, uns
         if (p + 1 < pend) inorder &= tn[u] <= pp.now[p + 1];
         if (live[u]) pp.keys[p] = -1;
     }
+    int32_t e0, e1;  // kind boundaries: first slot of class >= 1 and of class 2 (pod counts per kind)
     if (__syncthreads_and(inorder)) {
         // times already ascending (a queue drained in order): a stable kind partition sorts the tile
         uint64_t mnm[kU], mdm[kU];
@@ -59,9 +60,14 @@ __device__ __forceinline__ void k3p_tile(const int64_t t, const PodPrep& pp, uns
             }
         }
         __syncthreads();
-        int32_t tot_n = 0;
+        int32_t tot_n = 0, tot_d = 0;
 #pragma unroll
-        for (int i = 0; i < kG; ++i) tot_n += gcn[i];
+        for (int i = 0; i < kG; ++i) {
+            tot_n += gcn[i];
+            tot_d += gcd[i];
+        }
+        e0 = tot_n;
+        e1 = tot_n + tot_d;
         const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -79,13 +85,16 @@ __device__ __forceinline__ void k3p_tile(const int64_t t, const PodPrep& pp, uns
         }
         __syncthreads();
     } else {
+        e0 = e1 = 0;
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const int i = u * kT + threadIdx.x;
             ku[i] = live[u] ? (uint64_t)tn[u] ^ kSign : ~0ull;
             kv[i] = ((live[u] ? (ds[u] ? 1u : 0u) : 2u) << 30) | (uint32_t)i;
+            e0 += __syncthreads_count(live[u] && !ds[u]);  // (barriers: the stores above are ordered too)
+            e1 += __syncthreads_count(ds[u]);
         }
-        __syncthreads();
+        e1 += e0;
         // bitonic sort of the 1024 (key, tag) pairs in LDS: 55 compare-exchange passes
         for (int k = 2; k <= 1024; k <<= 1) {
             for (int j = k >> 1; j > 0; j >>= 1) {
@@ -114,17 +123,8 @@ __device__ __forceinline__ void k3p_tile(const int64_t t, const PodPrep& pp, uns
         }
     }
     if (threadIdx.x == 0) {
-        // kind boundaries: first slot of class >= 1 and of class 2
-        auto first_class = [&](uint32_t c) {
-            int lo = 0, hi = 1024;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if ((kv[mid] >> 30) < c) lo = mid + 1;
-                else hi = mid;
-            }
-            return lo;
-        };
-        const int e0 = first_class(1), e1 = first_class(2);
+        // (e0 / e1 from the counts, not a binary search over the sorted classes: 20 dependent LDS
+        // reads on the launch's critical path)
         int64_t* ts = pp.tile_mm + kTileStat * t;
         ts[0] = e0 > 0 ? (int64_t)(ku[0] ^ kSign) : INT64_MAX;
         ts[1] = e0 > 0 ? (int64_t)(ku[e0 - 1] ^ kSign) : INT64_MIN;
