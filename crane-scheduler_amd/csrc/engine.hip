@@ -116,6 +116,9 @@ struct Options {
     int k2l_threads = 1024;   // large K2: partition workgroup size at 4096-binding regions (512 or 1024;
                               // cold 4M x 16M: 1024 0.084-0.085 ms vs 512 0.087-0.089, same-box sweeps
                               // profiles/ab/r03_k2_cold_*.txt)
+    int k2y_first = 6;        // large K2: 16-byte blocks of each region's run k2y loads up front (3..8;
+                              // cold 4M x 16M ordered log: k2y 0.019 ms at 3, 0.0165 at 6,
+                              // profiles/r04/k2y_first.txt)
     int sel_chain = 0;        // selection windows: 0 LDS rank/select walk when it fits, 1 streaming kernel
     int step_lds_cap = 1 << 30;  // K1: one-step records per kind staged in LDS at most (0: always st.stage)
     int step_pieces = 0;      // middle pieces cut into elementary ones per block (step_pieces): 0 when the
@@ -438,7 +441,8 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         // is rewritten, so nothing is zeroed before and K1 leaves them
         HIPTRY(h, h->k2_sorted.reserve(hot_dedupe_scratch(gl)));
         HIPTRY(h, launch_hot_count_large(bn, h->bts.p, Bk, h->N, by_pos ? pcut : cut, gl, h->k2_sorted.p,
-                                         h->buckets.p, h->n_cu, st, h->opt.k2l_threads));
+                                         h->buckets.p, h->n_cu, st, h->opt.k2l_threads,
+                                         h->opt.k2y_first));
         h->buckets_zero = false;
         h->buckets_dense = true;
         return CRANE_OK;
@@ -805,6 +809,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "k2l_region" && (value == 2048 || value == 4096)) o.k2l_region = (int)value;
     else if (n == "k2l_co_t" && range(0, 1)) o.k2l_co_t = (int)value;
     else if (n == "k2l_threads" && (value == 512 || value == 1024)) o.k2l_threads = (int)value;
+    else if (n == "k2y_first" && range(3, 8)) o.k2y_first = (int)value;
     else if (n == "sel_chain" && range(0, 1)) o.sel_chain = (int)value;
     else if (n == "step_pieces" && range(0, 2)) o.step_pieces = (int)value;
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);

@@ -633,31 +633,44 @@ static hipError_t launch_large_x(const int32_t* bnode, const int64_t* bts, int64
                       : launch_large_xp<BT, REG, false>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
 }
 
+template <int kYPer, int kYFirst>
+static hipError_t launch_y(const uint32_t* scratch, const HotPart& g, int32_t W, int64_t N, uint32_t* buckets,
+                           hipStream_t st) {
+    // (dynamic + the static tail queue stay within the CU's 160 KiB)
+    static const hipError_t attr = hipFuncSetAttribute((const void*)k2y_bin_hist<kYPer, kYFirst>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)kK2LargeHistBytes);
+    if (attr != hipSuccess) return attr;
+    const size_t lds = sizeof(uint32_t) * (size_t)W * ((size_t)1 << g.bb);
+    return klaunch("k2y_bin_hist", k2y_bin_hist<kYPer, kYFirst>, dim3((unsigned)g.nbins), dim3(kYThreads), lds, st,
+                   scratch, scratch + g.cap, g, W, N, buckets);
+}
+
 hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, uint32_t* buckets,
-                                  int n_cu, hipStream_t st, int threads) {
-    // (dynamic + the static tail queue stay within the CU's 160 KiB)
-    static const hipError_t attr = [] {
-        hipError_t e = hipFuncSetAttribute((const void*)k2y_bin_hist<4, 3>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kK2LargeHistBytes);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k2y_bin_hist<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kK2LargeHistBytes);
-        return e;
-    }();
-    if (attr != hipSuccess) return attr;
+                                  int n_cu, hipStream_t st, int threads, int yfirst) {
     hipError_t e;
     if (g.reg == 2048) e = launch_large_x<512, 2048>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
     else if (threads == 1024) e = launch_large_x<1024, 4096>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
     else e = launch_large_x<512, 4096>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
     if (e != hipSuccess) return e;
-    const size_t lds = sizeof(uint32_t) * (size_t)cut.n_win * ((size_t)1 << g.bb);
-    const uint32_t* co = scratch + g.cap;
-    if (g.nblk <= 4 * kYThreads)
-        return klaunch("k2y_bin_hist", k2y_bin_hist<4, 3>, dim3((unsigned)g.nbins), dim3(kYThreads), lds, st,
-                       (const uint32_t*)scratch, co, g, cut.n_win, N, buckets);
-    return klaunch("k2y_bin_hist", k2y_bin_hist<8, 2>, dim3((unsigned)g.nbins), dim3(kYThreads), lds, st,
-                   (const uint32_t*)scratch, co, g, cut.n_win, N, buckets);
+    // (k2y_first: 16-byte blocks of each run loaded in the count/offset words' round; kYPer = the
+    // fewest regions per lane that cover the log)
+    if (g.nblk > 4 * kYThreads) return launch_y<8, 2>(scratch, g, cut.n_win, N, buckets, st);
+    if (g.nblk > 2 * kYThreads) {
+        switch (yfirst) {
+            case 3: return launch_y<4, 3>(scratch, g, cut.n_win, N, buckets, st);
+            case 4: return launch_y<4, 4>(scratch, g, cut.n_win, N, buckets, st);
+            default: return launch_y<4, 5>(scratch, g, cut.n_win, N, buckets, st);
+        }
+    }
+    switch (yfirst) {
+        case 3: return launch_y<2, 3>(scratch, g, cut.n_win, N, buckets, st);
+        case 4: return launch_y<2, 4>(scratch, g, cut.n_win, N, buckets, st);
+        case 5: return launch_y<2, 5>(scratch, g, cut.n_win, N, buckets, st);
+        case 6: return launch_y<2, 6>(scratch, g, cut.n_win, N, buckets, st);
+        default: return launch_y<2, 8>(scratch, g, cut.n_win, N, buckets, st);
+    }
 }
 
 HotBins hot_bins_geometry(int64_t B, int64_t N, int32_t W) {

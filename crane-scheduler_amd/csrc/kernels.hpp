@@ -237,7 +237,7 @@ constexpr int64_t kK2LargeHistBytes = 128 * 1024;
 HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W, int32_t reg, int32_t co_t);
 hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, uint32_t* buckets,
-                                  int n_cu, hipStream_t st, int threads = 512);
+                                  int n_cu, hipStream_t st, int threads = 512, int yfirst = 3);
 
 // ---------------------------------------------------------------- K3 step path (step.hip)
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
