@@ -400,12 +400,19 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
     if pmc:
         ks = pmc.get("kernels", {})
 
-        def k2_traffic(pos):  # k2l_partition of one path (its last template argument: ranks by position) + k2y
+        def k2_traffic(pos, nread):
+            """k2l_partition of one path (its last template argument: ranks by position) + the k2y
+            instantiation that path launched (its first argument: regions per lane, the fewest of
+            2 / 4 / 8 that cover the path's 4096-binding regions, hotcount.hip launch_hot_count_large)."""
+            nblk = -(-nread // 4096)
+            per = "2" if nblk <= 2048 else "4" if nblk <= 4096 else "8"
             t = [v.get("traffic_bytes") for k, v in ks.items()
-                 if pmc_name_match(k, "crane::k2l_partition", {-1: pos}) or pmc_name_match(k, "crane::k2y_bin_hist", {})]
+                 if pmc_name_match(k, "crane::k2l_partition", {-1: pos})
+                 or pmc_name_match(k, "crane::k2y_bin_hist", {0: per})]
             return int(sum(t)) if len(t) == 2 and all(x is not None for x in t) else None
 
-        tr_k2, tr_k2ts = k2_traffic("true"), k2_traffic("false")
+        kr = k2_read(spec, c.b_ts, now)
+        tr_k2, tr_k2ts = k2_traffic("true", kr["read"]), k2_traffic("false", B)
         tr_k1 = pmc_traffic(pmc, "k1_node_pass+k3a_steps")
         tr_k1r = pmc_traffic(pmc, "k1_node_pass")
     kb = k2_read(spec, c.b_ts, now)
