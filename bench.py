@@ -98,6 +98,19 @@ def pmc_summary(config, shash):
     return (json.load(open(p)), os.path.relpath(p, ROOT)) if os.path.exists(p) else (None, None)
 
 
+def k2_path_traffic(ks, by_pos, nread):
+    """PMC traffic per launch of one large-form K2 path: k2l_partition of that path (its last
+    template argument: ranks by position) + the k2y instantiation the path launched (its first
+    argument: regions per lane, the fewest of 2 / 4 / 8 that cover the path's 4096-binding
+    regions, hotcount.hip launch_hot_count_large).  ks: a PMC summary's "kernels"."""
+    nblk = -(-nread // 4096)
+    per = "2" if nblk <= 2048 else "4" if nblk <= 4096 else "8"
+    t = [v.get("traffic_bytes") for k, v in ks.items()
+         if pmc_name_match(k, "crane::k2l_partition", {-1: "true" if by_pos else "false"})
+         or pmc_name_match(k, "crane::k2y_bin_hist", {0: per})]
+    return int(sum(t)) if len(t) == 2 and all(x is not None for x in t) else None
+
+
 def pmc_traffic(pmc, name):
     if not pmc or name not in KERNEL_PMC:
         return None
@@ -400,19 +413,8 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
     if pmc:
         ks = pmc.get("kernels", {})
 
-        def k2_traffic(pos, nread):
-            """k2l_partition of one path (its last template argument: ranks by position) + the k2y
-            instantiation that path launched (its first argument: regions per lane, the fewest of
-            2 / 4 / 8 that cover the path's 4096-binding regions, hotcount.hip launch_hot_count_large)."""
-            nblk = -(-nread // 4096)
-            per = "2" if nblk <= 2048 else "4" if nblk <= 4096 else "8"
-            t = [v.get("traffic_bytes") for k, v in ks.items()
-                 if pmc_name_match(k, "crane::k2l_partition", {-1: pos})
-                 or pmc_name_match(k, "crane::k2y_bin_hist", {0: per})]
-            return int(sum(t)) if len(t) == 2 and all(x is not None for x in t) else None
-
         kr = k2_read(spec, c.b_ts, now)
-        tr_k2, tr_k2ts = k2_traffic("true", kr["read"]), k2_traffic("false", B)
+        tr_k2, tr_k2ts = k2_path_traffic(ks, True, kr["read"]), k2_path_traffic(ks, False, B)
         tr_k1 = pmc_traffic(pmc, "k1_node_pass+k3a_steps")
         tr_k1r = pmc_traffic(pmc, "k1_node_pass")
     kb = k2_read(spec, c.b_ts, now)
