@@ -9,9 +9,13 @@ reference's hot path over one node shard, keys-only (chosen node per pod):
   K1 node pass over the shard's parsed annotations (stats.go:51-112 pod-invariant parts)
   K3 Filter + Score + argmax for every (pod, node) pair (plugins.go:39-98, selectHost)
   RCCL int64 max all-reduce of the per-pod packed keys across node shards (N > 1)
-Config 3 (default): each rank owns 100k nodes, all ranks score the same 10k pods
-(weak scaling).  Config 4: the 1M nodes are split over the ranks, 100k pods
-(strong scaling).  `value` is placements per second, measured: the pods of the
+Config 3 (default): each GPU owns 100k nodes, all GPUs score the same 10k pods
+(weak scaling).  Config 4: the 1M nodes are split over the GPUs, 100k pods
+(strong scaling).  `--engine group` (default): one process drives every GPU through
+the C ABI group (crane_dyn_group_*: per-device shard engines, in-library RCCL
+all-reduce); under a launcher the other ranks only wait.  `--engine ranks`: one
+process per GPU over torch.distributed (the comparison).  Batch i is scheduled at
+now0 + (i % 6) x 10 s (its pods shifted alike): the hot-value cutoffs move.  `value` is placements per second, measured: the pods of the
 timed steps over the timed region.  `pairs_decided_per_s` (P x nodes / step) is
 a full-rescan equivalent: every (pod, node) pair's Filter + Score is decided
 exactly, but the step path only evaluates a node per pod where one of its
@@ -49,12 +53,11 @@ PMC_DIR = os.path.join(ROOT, "profiles", "pmc")
 DROPIN = os.path.join(ROOT, "crane-scheduler_amd", "lib", "dropin_bench")
 # kernel timer name -> rocprofv3 kernel name (prefix, suffix) for the PMC lookup
 # dispatch-stamp name -> (rocprof kernel name without its template arguments, {argument index:
-# value}) — the node pass's STEP / SPLIT flags are its 4th / 5th template arguments, K3m's keys /
-# matrices its last two
+# value}) — the node pass's STEP flag is its 4th template argument, K3m's keys / matrices its
+# last two
 KERNEL_PMC = {
-    "k1_node_pass+k3a_steps": ("crane::k1_node_pass", {3: "true", 4: "false"}),
-    "k1_node_pass+k3a_count": ("crane::k1_node_pass", {3: "true", 4: "true"}),
-    "k1_node_pass": ("crane::k1_node_pass", {3: "false", 4: "false"}),
+    "k1_node_pass+k3a_steps": ("crane::k1_node_pass", {3: "true"}),
+    "k1_node_pass": ("crane::k1_node_pass", {3: "false"}),
     "k2x_dedupe+k3p_pods": ("crane::k2x_dedupe_pods", {}),
     "k2x_dedupe": ("crane::k2x_dedupe", {}),
     "k3p_pods": ("crane::k3p_pods", {}),
@@ -209,24 +212,21 @@ def parse():
     ap.add_argument("--no-greedy", action="store_true", help="skip the config-5 sequential-greedy measurement")
     ap.add_argument("--inflight", type=int, default=4,
                     help="independent pod batches in flight (engines x HIP streams); 1 = one batch at a time")
-    ap.add_argument("--ar-stream", default="own", choices=("own", "engine"),
-                    help="N>1: the keys all-reduce on its own stream, or on the stream of the group's last "
-                         "batch (no stream beyond the K engine streams: the box exposes 4 hardware queues)")
     ap.add_argument("--ar-group", type=int, default=0,
                     help="N>1: batches per keys all-reduce (a multiple of --inflight; 0 = 16 x inflight)")
     ap.add_argument("--rehearse-collective", action="store_true",
-                    help="run the N>1 collective path on one rank (under torchrun)")
+                    help="run the ranks path's N>1 collective on one rank (under torchrun)")
     ap.add_argument("--no-extras", action="store_true", help="headline step only (matrix / drop-in / controller legs off)")
     ap.add_argument("--leg", default="all", choices=("all", "matrix2", "matrix3", "cold"),
                     help="matrix2 / matrix3 / cold: only that leg (for per-kernel PMC passes)")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache 4M-node K1/K2 roofline leg")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option name=value for the --leg runs (A/B of kernel forms; repeatable)")
-    ap.add_argument("--enqueue-threads", type=int, default=1,
-                    help="host threads enqueuing the timed batches (thread t drives the engines j with "
-                         "j %% threads == t; one rank without the collective only)")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the step as a captured graph (measured slower than eager launches on ROCm 7.2)")
+    ap.add_argument("--engine", default="group", choices=("group", "ranks"),
+                    help="group: one process drives every GPU through the C ABI group (crane_dyn_group_*, "
+                         "in-library RCCL); ranks: one process per GPU under torch.distributed (comparison)")
+    ap.add_argument("--now-cycle", type=int, default=6,
+                    help="timed batch i is scheduled at now0 + (i %% C) x the batch's span (1 = every batch at now0)")
     return ap.parse_args()
 
 
@@ -384,11 +384,10 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
             k2.append(sum(t for _, t in t_k2))
             for name, t in t_k2:
                 k2_parts.setdefault(name, []).append(t)
-            # the node pass that builds the step tables: one fused kernel, or the split form's
-            # count pass + k3a_emit (engine option k1_split)
-            k1.append(sum(t for name, t in t_ev if name.startswith(("k1_node_pass", "k3a_emit"))))
+            # the node pass that builds the step tables (one fused kernel)
+            k1.append(sum(t for name, t in t_ev if name.startswith("k1_node_pass")))
             for name, t in t_ev:
-                if name.startswith(("k1_node_pass", "k3a_emit")):
+                if name.startswith("k1_node_pass"):
                     k1_parts.setdefault(name, []).append(t)
             k1r.append(sum(t for name, t in t_np if name == "k1_node_pass"))
     # the general form for a log in no particular order: every binding's node id and stamp read
@@ -737,22 +736,301 @@ def k2_read(spec, b_ts, now_ns):
     return {"first": 0, "read": B, "bytes": 12 * B, "what": "bindings read (node id + stamp)"}
 
 
+def batch_times(c, args):
+    """The timed batches' times (bench realism): batch i is scheduled at now_i = now0 + (i % C) x the
+    batch's span (the P pods' own spread, 10 s at config 3), its pods at their times shifted by the
+    same amount, so the hot-value cutoffs move every batch and the K2 suffix search reruns.  C
+    (--now-cycle, 6 = one minute of pod time) bounds the drift: the synthetic snapshot and binding
+    log are not re-synced between batches, and further out every 5-minute metric would go stale.
+    Returns (now_ns per cycle position, pod times per cycle position, span)."""
+    step = int(c.now[1] - c.now[0]) if len(c.now) > 1 else 10**9
+    span = int(c.now[-1] - c.now[0]) + step
+    C = max(1, args.now_cycle)
+    now0 = int(c.now[0])
+    return [now0 + j * span for j in range(C)], [c.now + j * span for j in range(C)], span
+
+
+def measure_ranks(cd, synth, spec, args, world, rank, local, dev):
+    """One rank per GPU (this process's GPU `local`): its node shard on K engines, batches in flight on
+    K streams; N > 1: one RCCL max all-reduce of a group of batches' keys (torch.distributed)."""
+    coll = world > 1 or args.rehearse_collective
+    strong = args.config == 4
+    c, node_lo, n_total, whole = build_shard(synth, spec, args, world, rank)
+    N, P = c.n_nodes, len(c.now)
+    K = max(1, args.inflight)
+    engs = [cd.Engine(cd.Policy(spec), local) for _ in range(K)]
+    eng = engs[0]
+    val, ts, _ = c.rows(eng.metric_names)
+    for e in engs:
+        e.upload_nodes(val, ts, c.hv, c.hv_ts, node_offset=node_lo)
+        e.upload_bindings(c.b_node, c.b_ts)
+    nows, pods, span = batch_times(c, args)
+    C = len(nows)
+    d_now = [torch.from_numpy(p).to(dev) for p in pods]
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    d_keys_k = [torch.empty(P, dtype=torch.int64, device=dev) for _ in range(K)]
+    # dedicated streams: the default stream's handle is 0, which the C ABI reads as "engine stream"
+    streams = [torch.cuda.Stream(dev) for _ in range(K)]
+    torch.cuda.set_stream(streams[0])
+    sh_k = [s_.cuda_stream for s_ in streams]
+    # N > 1: one RCCL max all-reduce per group of G batches over their keys [G][P], on its own
+    # stream after the group's K streams; two key buffers alternate so a group's batches never
+    # overwrite keys a collective still reads
+    G = max(K, args.ar_group or 16 * K) // K * K  # batches per collective, a multiple of K
+    if coll:
+        kbufs = [torch.empty((G, P), dtype=torch.int64, device=dev) for _ in range(2)]
+        cstream = torch.cuda.Stream(dev)
+        ar_done = [None, None]
+        ev_s = [torch.cuda.Event() for _ in range(K)]  # (reused: record() re-arms an event)
+        ev_ar = [torch.cuda.Event(), torch.cuda.Event()]
+
+    def collect(b, nb):
+        for jj in range(min(nb, K)):
+            ev_s[jj].record(streams[jj])
+            cstream.wait_event(ev_s[jj])
+        with torch.cuda.stream(cstream):
+            dist.all_reduce(kbufs[b][:nb], op=dist.ReduceOp.MAX)  # RCCL over xGMI
+        ev_ar[b].record(cstream)
+        ar_done[b] = ev_ar[b]
+
+    # the step calls bound once to their engine, stream, pod batch and key buffer
+    step_own = [[engs[j].step_keys_fn(d_now[t], d_flags, d_keys_k[j], sh_k[j]) for t in range(C)] for j in range(K)]
+    step_grp = ([[[engs[r % K].step_keys_fn(d_now[t], d_flags, kbufs[b][r], sh_k[r % K]) for t in range(C)]
+                  for r in range(G)] for b in range(2)] if coll else None)
+
+    def step(collective=True, i=0):
+        j, t = i % K, i % C
+        if coll and collective:
+            b, row = (i // G) % 2, i % G
+            if row < K and ar_done[b] is not None:  # this buffer's previous collective has read it
+                streams[j].wait_event(ar_done[b])
+            step_grp[b][row][t](nows[t], nows[t])
+            if row == G - 1:
+                collect(b, G)
+        else:
+            step_own[j][t](nows[t], nows[t])
+
+    def flush(n_steps):  # the last, partial group's collective
+        if coll and n_steps % G:
+            collect((n_steps // G) % 2, n_steps % G)
+
+    for i in range(args.warmup):
+        step(i=i)
+    flush(args.warmup)
+    if coll:
+        # RCCL's first call at a given size sets that size up: untimed, once at every size the
+        # timed region reduces, so no setup lands in the timing
+        for b in range(2):
+            for nb in sorted({G, args.steps % G or G}):
+                collect(b, nb)
+        ar_done[0] = ar_done[1] = None  # the timed groups start from fresh buffers
+    torch.cuda.synchronize(dev)
+    if coll:
+        dist.barrier()
+    cpu0 = task_cpu()
+    t0 = time.perf_counter()
+    tc0 = time.thread_time()
+    for i in range(args.steps):
+        step(i=i)
+    flush(args.steps)
+    t_enq = time.perf_counter() - t0
+    tc_enq = time.thread_time() - tc0
+    torch.cuda.synchronize(dev)
+    if coll:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    host = host_threads(cpu0, task_cpu(), t_enq, tc_enq, elapsed, args.steps)
+    if coll:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    t_last = (args.steps - 1) % C
+    if coll:  # the last group's keys (all-reduced over the ranks)
+        last = kbufs[((args.steps - 1) // G) % 2]
+        d_keys = last[(args.steps - 1) % G]
+        keys_agree = True
+    else:
+        d_keys = d_keys_k[(args.steps - 1) % K]
+        keys_agree = all(torch.equal(d_keys, k) for k in d_keys_k) if C == 1 else None
+    keys = d_keys.cpu().numpy()
+    keys_match, keys_match_how = None, "single rank: no combine step"
+    if coll:
+        if rank == 0:
+            ref_k, n_glob = keys_one_engine(cd, synth, spec, dev, whole, d_now[t_last], d_flags, nows[t_last])
+            assert n_glob == n_total
+            keys_match = bool(torch.equal(ref_k, d_keys))
+        dist.barrier()
+        keys_match_how = ("the last batch's all-reduced keys [P] == one engine holding the whole "
+                          f"{n_total}-node global cluster and its binding log, same pods")
+    elif world == 1 and strong:
+        # config 4 on one GPU: the 8-GPU layout's combine rehearsed on this GPU
+        keys_match = keys_virtual_shards(cd, spec, dev, c, d_now[t_last], d_flags, nows[t_last], d_keys, 8)
+        keys_match_how = ("8 node shards of the 1M-node cluster (125k nodes each, node_offset, each with its own "
+                          "nodes' bindings) on this GPU, their keys max-combined (the all-reduce's operation) == "
+                          "the one-engine keys of the last timed batch")
+    # one batch's latency: the same step with nothing else in flight (outside the timed region)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    nl = max(10, args.steps // 4)
+    for i in range(nl):
+        step(collective=False, i=i * K)  # (engine 0 only: each batch waits for the previous one on its stream)
+        if coll:
+            with torch.cuda.stream(streams[0]):
+                dist.all_reduce(d_keys_k[0], op=dist.ReduceOp.MAX)
+    torch.cuda.synchronize(dev)
+    batch_latency_ms = (time.perf_counter() - t1) * 1e3 / nl
+    kt = kernel_times(eng, lambda: step(collective=False), args.steps)
+    ar_ms = None
+    if coll:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(streams[0])
+        with torch.cuda.stream(streams[0]):
+            for _ in range(10):
+                dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)
+        e1.record(streams[0])
+        torch.cuda.synchronize(dev)
+        ar_ms = e0.elapsed_time(e1) / 10
+    m = dict(c=c, N=N, P=P, n_total=n_total, val=val, ts=ts, eng=eng, ms_step=elapsed * 1e3 / args.steps,
+             keys=keys, keys_agree=keys_agree, keys_match=keys_match, keys_match_how=keys_match_how, host=host,
+             batch_latency_ms=batch_latency_ms, kt=kt, ar_ms=ar_ms, K=K, nows=nows, span=span, stream=streams[0],
+             how=("K engines (own copy of the shard's nodes, binding log, scratch) on K HIP streams, batch i on "
+                  "engine i % K; every batch runs the whole step" +
+                  (f"; one RCCL max all-reduce (torch.distributed, one process per GPU) per group of {G} batches' "
+                   f"keys [{G}][P] on its own stream" if coll else "")),
+             engine_path="ranks" + (" (torch.distributed RCCL)" if coll else ""), n_gpus=world)
+    m["close"] = lambda: [e.close() for e in engs]
+    return m
+
+
+def measure_group(cd, synth, spec, args, n_dev, dev):
+    """One process driving n_dev GPUs through the C ABI group (crane_dyn_group_*, group.cpp): the
+    global cluster's node shards over the devices, K batches in flight (the group's slots), each
+    batch = every device's shard step + the in-library RCCL max all-reduce of the keys (n_dev > 1;
+    with one device there is nothing to combine)."""
+    from crane_dyn.shard import shard_range
+    strong = args.config == 4
+    cfg = synth.CONFIGS[args.config]
+    P, B = cfg["pods"], cfg["bindings"]
+    if strong:
+        g_all = synth.make_cluster(spec, cfg["nodes"], P, n_bindings=B, seed=20250215 + 4000)
+    else:
+        cells = [synth.make_cluster(spec, cfg["nodes"], P, n_bindings=B, seed=20250215 + args.config * 1000 + r)
+                 for r in range(n_dev)]
+        g_all = synth.concat(cells) if n_dev > 1 else cells[0]
+    g_all.now, g_all.ds = synth.make_pods(P, seed=20250215 + args.config)
+    n_total = g_all.n_nodes
+    lo0, hi0 = shard_range(n_total, n_dev, 0)
+    c = g_all if n_dev == 1 else g_all.node_slice(lo0, hi0)  # device 0's shard (per-kernel rooflines)
+    c.now, c.ds = g_all.now, g_all.ds
+    K = max(1, args.inflight)
+    grp = cd.Group(cd.Policy(spec), devices=list(range(n_dev)), depth=K)
+    val_all, ts_all, _ = g_all.rows(grp.metric_names)
+    grp.upload_nodes(val_all, ts_all, g_all.hv, g_all.hv_ts)
+    grp.upload_bindings(g_all.b_node, g_all.b_ts)
+    nows, pods, span = batch_times(g_all, args)
+    C = len(nows)
+    devs = [torch.device("cuda", d) for d in range(n_dev)]
+    d_now = [[torch.from_numpy(p).to(dv) for dv in devs] for p in pods]
+    d_flags = [torch.from_numpy(g_all.ds).to(dv) for dv in devs]
+    d_keys = [[torch.empty(P, dtype=torch.int64, device=dv) for dv in devs] for _ in range(K)]
+    fns = [[grp.step_keys_fn(d_now[t], d_flags, d_keys[s]) for t in range(C)] for s in range(K)]
+    seq = [0]  # batches enqueued on the group so far: batch b runs on slot b % K
+
+    def step(i):
+        t = i % C
+        fns[seq[0] % K][t](nows[t], nows[t])
+        seq[0] += 1
+
+    def sync_all():
+        grp.sync()
+        for dv in devs:
+            torch.cuda.synchronize(dv)
+
+    for i in range(args.warmup):
+        step(i)
+    sync_all()
+    cpu0 = task_cpu()
+    t0 = time.perf_counter()
+    tc0 = time.thread_time()
+    for i in range(args.steps):
+        step(i)
+    t_enq = time.perf_counter() - t0
+    tc_enq = time.thread_time() - tc0
+    grp.sync()
+    elapsed = time.perf_counter() - t0
+    host = host_threads(cpu0, task_cpu(), t_enq, tc_enq, elapsed, args.steps)
+    t_last, s_last = (args.steps - 1) % C, (seq[0] - 1) % K
+    last = d_keys[s_last]
+    keys = last[0].cpu().numpy()
+    keys_agree = all(torch.equal(last[0].cpu(), k.cpu()) for k in last[1:]) if n_dev > 1 else None
+    keys_match, keys_match_how = None, "one device: no combine step"
+    if n_dev > 1:
+        ref_k, _ = keys_one_engine(cd, synth, spec, devs[0], lambda: g_all, d_now[t_last][0], d_flags[0], nows[t_last])
+        keys_match = bool(torch.equal(ref_k.cpu(), last[0].cpu()))
+        keys_match_how = ("the last batch's all-reduced keys on every device == one engine holding the whole "
+                          f"{n_total}-node global cluster and its binding log, same pods")
+    elif strong:
+        keys_match = keys_virtual_shards(cd, spec, dev, c, d_now[t_last][0], d_flags[0], nows[t_last],
+                                         torch.from_numpy(keys).to(dev), 8)
+        keys_match_how = ("8 node shards of the 1M-node cluster (125k nodes each, node_offset, each with its own "
+                          "nodes' bindings) on this GPU, their keys max-combined (the all-reduce's operation) == "
+                          "the group's keys of the last timed batch")
+    sync_all()
+    nl = max(10, args.steps // 4)
+    t1 = time.perf_counter()
+    for i in range(nl):
+        step(i)
+        grp.sync()
+    batch_latency_ms = (time.perf_counter() - t1) * 1e3 / nl
+    # per-kernel durations: shard 0's engine of slot 0 stepping the same batch on its own stream
+    eng = grp.engine(0, 0)
+    st0 = torch.cuda.Stream(devs[0])
+    k0 = torch.empty(P, dtype=torch.int64, device=devs[0])
+    kt = kernel_times(eng, lambda: eng.step_keys_async(nows[0], nows[0], d_now[0][0], d_flags[0], k0,
+                                                       st0.cuda_stream), args.steps)
+    val, ts, _ = c.rows(grp.metric_names)
+    m = dict(c=c, N=c.n_nodes, P=P, n_total=n_total, val=val, ts=ts, eng=eng, ms_step=elapsed * 1e3 / args.steps,
+             keys=keys, keys_agree=keys_agree, keys_match=keys_match, keys_match_how=keys_match_how, host=host,
+             batch_latency_ms=batch_latency_ms, kt=kt, ar_ms=None, K=K, nows=nows, span=span, stream=st0,
+             how=(f"one process, crane_dyn_group over {n_dev} device(s) (C ABI, group.cpp): {K} batch slots, each "
+                  "with an engine per device (own copy of its shard) on its own HIP stream, batch i on slot i % K; "
+                  "every batch runs the whole shard step on every device" +
+                  ("; then an in-place RCCL ncclAllReduce(int64, max) of its keys on each device's stream "
+                   "(ncclCommInitAll communicators, one enqueueing worker thread per device)" if n_dev > 1 else "")),
+             engine_path="group (C ABI, in-library RCCL)" if n_dev > 1 else "group (C ABI, one device)",
+             n_gpus=n_dev)
+    m["close"] = lambda: grp.close()
+    return m
+
+
 def main():
     args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args))
+    launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
+    if launched and world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
-    # the collective path (RCCL all-reduce of the keys); --rehearse-collective runs it on a
-    # single rank (torchrun --nproc-per-node 1) to exercise it on a one-GPU box
-    coll = world > 1 or args.rehearse_collective
-    if coll:
+    if not launched and args.gpus > 1:
+        have = torch.cuda.device_count()  # (does not initialise the GPU on this image)
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, this host has {have}", file=sys.stderr)
+            sys.exit(2)
+        if args.engine == "ranks":
+            sys.exit(launch_ranks(args))
+    group = args.engine == "group" and not args.rehearse_collective
+    if group and launched and world > 1:
+        # the group drives every device from rank 0's process; the launcher's other ranks only
+        # wait (CPU barrier), touching no GPU
+        dist.init_process_group("gloo")
+        if rank != 0:
+            dist.barrier()
+            dist.destroy_process_group()
+            return
+    elif not group and (world > 1 or args.rehearse_collective):
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local if not group else 0)
     torch.cuda.set_device(dev)
 
     import crane_dyn as cd
@@ -778,206 +1056,35 @@ def main():
         print(json.dumps({"leg": args.leg, "src_hash": shash, "lib_hash": lib_hash(), **out}), flush=True)
         return
 
-    strong = args.config == 4  # 1M nodes x 100k pods split over the ranks
-    c, node_lo, n_total, whole = build_shard(synth, spec, args, world, rank)
-    N, P, B = c.n_nodes, len(c.now), len(c.b_node)
-    # K independent pod batches in flight (--inflight): K engines, each with its own copy of
-    # the shard's nodes and binding log and its own scratch, on K streams; batch i runs the
-    # whole step on engine i % K, so one batch's latency-bound kernels overlap another's
-    K = max(1, args.inflight)
-    engs = [cd.Engine(cd.Policy(spec), local) for _ in range(K)]
-    eng = engs[0]
-    val, ts, _ = c.rows(eng.metric_names)
-    for e in engs:
-        e.upload_nodes(val, ts, c.hv, c.hv_ts, node_offset=node_lo)
-        e.upload_bindings(c.b_node, c.b_ts)
-    d_now = torch.from_numpy(c.now).to(dev)
-    d_flags = torch.from_numpy(c.ds).to(dev)
-    d_keys_k = [torch.empty(P, dtype=torch.int64, device=dev) for _ in range(K)]
-    d_keys = d_keys_k[0]
-    now_sync = int(synth.NOW0_NS)
-
-    # dedicated streams: the default stream's handle is 0, which the C ABI reads as "engine stream"
-    streams = [torch.cuda.Stream(dev) for _ in range(K)]
-    stream = streams[0]
-    torch.cuda.set_stream(stream)
-    sh = stream.cuda_stream
-
-    sh_k = [s_.cuda_stream for s_ in streams]
-    # N > 1: one RCCL max all-reduce per group of G batches over their keys [G][P], on its
-    # own stream after the group's K streams (the collective's latency and host cost are
-    # per call; rehearsed on one rank with the bound step calls: G = 32 / 64 / 128 -> 0.0175 /
-    # 0.0148 / 0.0148 ms per batch against 0.0130 without the collective); two key buffers
-    # alternate so a group's batches never overwrite keys a collective still reads
-    G = max(K, args.ar_group or 16 * K) // K * K  # batches per collective, a multiple of K
-    if coll:
-        kbufs = [torch.empty((G, P), dtype=torch.int64, device=dev) for _ in range(2)]
-        cstream = torch.cuda.Stream(dev)
-        ar_done = [None, None]
-        ev_s = [torch.cuda.Event() for _ in range(K)]  # (reused: record() re-arms an event)
-        ev_ar = [torch.cuda.Event(), torch.cuda.Event()]
-
-    def collect(b, nb):
-        cs = cstream if args.ar_stream == "own" else streams[(nb - 1) % K]
-        for jj in range(min(nb, K)):
-            if streams[jj] is cs:
-                continue
-            ev_s[jj].record(streams[jj])
-            cs.wait_event(ev_s[jj])
-        with torch.cuda.stream(cs):
-            dist.all_reduce(kbufs[b][:nb], op=dist.ReduceOp.MAX)  # RCCL over xGMI
-        ev_ar[b].record(cs)
-        ar_done[b] = ev_ar[b]
-
-    # the step calls bound once to their engine, stream and key buffer (step_keys_fn: the
-    # pointer conversions happen here, a step in the timed loop pays only the C call)
-    step_own = [engs[j].step_keys_fn(d_now, d_flags, d_keys_k[j], sh_k[j]) for j in range(K)]
-    step_grp = ([[engs[r % K].step_keys_fn(d_now, d_flags, kbufs[b][r], sh_k[r % K]) for r in range(G)]
-                 for b in range(2)] if coll else None)
-
-    def step(collective=True, i=0):
-        j = i % K
-        if coll and collective:
-            b, row = (i // G) % 2, i % G
-            if row < K and ar_done[b] is not None:  # this buffer's previous collective has read it
-                streams[j].wait_event(ar_done[b])
-            step_grp[b][row](now_sync, now_sync)
-            if row == G - 1:
-                collect(b, G)
-        else:
-            step_own[j](now_sync, now_sync)
-
-    def flush(n_steps):  # the last, partial group's collective
-        if coll and n_steps % G:
-            collect((n_steps // G) % 2, n_steps % G)
-
-    for i in range(args.warmup):
-        step(i=i)
-    flush(args.warmup)
-    if coll:
-        # RCCL's first call at a given size sets that size up (a few hundred us at [64][10k]
-        # int64): untimed, call it once at every size the timed region reduces — both
-        # buffers' full groups and the last, partial group — so no setup lands in the timing
-        for b in range(2):
-            for nb in sorted({G, args.steps % G or G}):
-                collect(b, nb)
-    torch.cuda.synchronize(dev)
-    graph = None
-    if args.graph:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=stream):
-            step(collective=False)
-        graph.replay()
-        torch.cuda.synchronize(dev)
-
-    def timed_step(i):
-        if graph is None:
-            step(i=i)
-        else:
-            graph.replay()
-            if coll:
-                dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)
-
-    if coll:  # the timed groups start from fresh buffers
-        ar_done[0] = ar_done[1] = None
-
-    if coll:
-        dist.barrier()
-    # several enqueuing threads (--enqueue-threads): thread t issues the batches i with i % T == t,
-    # so each engine and its stream are driven by one thread (the C calls release the GIL)
-    TQ = max(1, args.enqueue_threads)
-    if TQ > 1:
-        if coll or graph is not None or K % TQ:
-            sys.exit("bench.py: --enqueue-threads needs one rank, no graph, and --inflight a multiple of it")
-        go = threading.Barrier(TQ + 1)
-
-        def enqueue(t):
-            go.wait()
-            for i in range(t, args.steps, TQ):
-                step(i=i)
-
-        workers = [threading.Thread(target=enqueue, args=(t,)) for t in range(TQ)]
-        for w_ in workers:
-            w_.start()
-    torch.cuda.synchronize(dev)
-    cpu0 = task_cpu()
-    t0 = time.perf_counter()
-    tc0 = time.thread_time()
-    if TQ > 1:
-        go.wait()
-        for w_ in workers:
-            w_.join()
+    if group:
+        m = measure_group(cd, synth, spec, args, args.gpus, dev)
+        n_gpus, solo = args.gpus, True
     else:
-        for i in range(args.steps):
-            timed_step(i)
-    if graph is None:
-        flush(args.steps)
-    t_enq = time.perf_counter() - t0
-    tc_enq = time.thread_time() - tc0
-    torch.cuda.synchronize(dev)
-    if coll:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    host = host_threads(cpu0, task_cpu(), t_enq, tc_enq, elapsed, args.steps)
-    if coll:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    ms_step = elapsed * 1e3 / args.steps
-    if coll and graph is None:  # the last group's keys (all-reduced over the ranks)
-        last = kbufs[((args.steps - 1) // G) % 2]
-        d_keys = last[0]
-        keys_agree = all(torch.equal(last[0], last[jj]) for jj in range((args.steps - 1) % G + 1))
-    else:
-        keys_agree = all(torch.equal(d_keys, k) for k in d_keys_k)
-    keys = d_keys.cpu().numpy()
-    # the all-reduced keys of the last batch vs one engine holding the whole global cluster
-    keys_match = None
-    keys_match_how = "single rank: no combine step"
-    if coll and graph is None:
-        if rank == 0:
-            ref_k, n_glob = keys_one_engine(cd, synth, spec, dev, whole, d_now, d_flags, now_sync)
-            assert n_glob == n_total
-            keys_match = bool(torch.equal(ref_k, d_keys))
-        dist.barrier()
-        keys_match_how = ("the last batch's all-reduced keys [P] == one engine holding the whole "
-                          f"{n_total}-node global cluster and its binding log, same pods")
-    elif world == 1 and strong and graph is None:
-        # config 4 on one GPU: the 8-GPU layout's combine rehearsed on this GPU
-        keys_match = keys_virtual_shards(cd, spec, dev, c, d_now, d_flags, now_sync, d_keys, 8)
-        keys_match_how = ("8 node shards of the 1M-node cluster (125k nodes each, node_offset, each with its own "
-                          "nodes' bindings) on this GPU, their keys max-combined (the all-reduce's operation) == "
-                          "the one-engine keys of the timed batch")
-    # one batch's latency: the same step with nothing else in flight (outside the timed region)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    for _ in range(max(10, args.steps // 4)):
-        step(collective=False)  # (engine 0 only: each batch waits for the previous one on its stream)
-        if coll:
-            with torch.cuda.stream(streams[0]):
-                dist.all_reduce(d_keys_k[0], op=dist.ReduceOp.MAX)
-    torch.cuda.synchronize(dev)
-    batch_latency_ms = (time.perf_counter() - t1) * 1e3 / max(10, args.steps // 4)
-    # per-kernel durations (dispatch-stamped) of the same step, outside the timed region
-    kt = kernel_times(eng, lambda: step(collective=False), args.steps)
-    ar_ms = None
-    if coll:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(10):
-            dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)
-        e1.record(stream)
-        torch.cuda.synchronize(dev)
-        ar_ms = e0.elapsed_time(e1) / 10
+        m = measure_ranks(cd, synth, spec, args, world, rank, local, dev)
+        n_gpus, solo = world, world == 1
+    finish(cd, synth, spec, args, m, n_gpus, rank, solo, dev, shash)
+    m["close"]()
+    if dist.is_initialized():
+        if group:
+            dist.barrier()  # (the other ranks are waiting here)
+        dist.destroy_process_group()
 
-    pairs = P * n_total
-    pairs_per_s = pairs / (ms_step / 1e3)
+
+def finish(cd, synth, spec, args, m, n_gpus, rank, solo, dev, shash):
+    """Rooflines, the extra legs (one GPU) and the JSON line (rank 0)."""
+    strong = args.config == 4
+    c, N, P, n_total, val, ts, eng, kt = m["c"], m["N"], m["P"], m["n_total"], m["val"], m["ts"], m["eng"], m["kt"]
+    B = len(c.b_node)
+    ms_step = m["ms_step"]
+    stream = m["stream"]
+    local = dev.index
+    pairs_per_s = P * n_total / (ms_step / 1e3)
     placements = P / (ms_step / 1e3)
+    now_sync = m["nows"][0]
 
     # Rooflines per kernel (DESIGN.md section 4): ALGORITHMIC bytes per launch / the kernel's
     # mean dispatch-stamped duration.  K3s re-reads L2-resident step records: not HBM-priced.
     M = len(eng.metric_names)
-    W = len(spec["hotValue"])
     kb = k2_read(spec, c.b_ts, now_sync)
     cut = np.sort(np.array([now_sync // 10**9 - tr // 10**9 for tr, _ in spec["hotValue"]], np.int64))
     jr = (c.b_ts[:, None] > cut[None, :]).sum(1)
@@ -996,10 +1103,6 @@ def main():
                                                "flag read, partition + keys written"),
         "k1_node_pass+k3a_steps": (N * (16 * M + 8) + E * 4 + co_b,
                                    "SoA (value, ts) read + hot value written + K2 entries and count/offset read"),
-        # split form (past one round of resident workgroups): the same streams; k3a_emit then
-        # re-reads the L2-resident stepped records (not HBM-priced, like K3s)
-        "k1_node_pass+k3a_count": (N * (16 * M + 8) + E * 4 + co_b,
-                                   "SoA (value, ts) read + hot value written + K2 entries and count/offset read"),
         "k3p_pods": (k3p_b, "pod now + flag read, partition + keys written"),
     }
     pmc, pmc_src = pmc_summary(args.config, shash)
@@ -1017,7 +1120,8 @@ def main():
                                 "per pod tile and has no HBM roofline; this is the longest HBM-priced kernel")
 
     extras = {}
-    if world == 1 and rank == 0 and not args.no_extras:
+    one = solo and n_gpus == 1 and rank == 0
+    if one and not args.no_extras:
         # BASELINE config 2 and the per-pair rate at config 3: every pair's result in HBM
         c2 = synth.make_cluster(spec, synth.CONFIGS[2]["nodes"], synth.CONFIGS[2]["pods"], seed=20250215 + 2)
         v2, t2, _ = c2.rows(eng.metric_names)
@@ -1033,12 +1137,12 @@ def main():
                 pmc_summary("3m", shash)[0])
 
     roofline_cold = None
-    if world == 1 and not args.no_extras and not args.no_cold:
+    if one and not args.no_extras and not args.no_cold:
         pmc_c, pmc_cs = pmc_summary("cold", shash)
         roofline_cold = cold_leg(cd, synth, spec, dev, pmc=pmc_c, pmc_src=pmc_cs)
 
     greedy = None
-    if world == 1 and not args.no_greedy and not args.no_extras:
+    if one and not args.no_greedy and not args.no_extras:
         # BASELINE config 5: 100k nodes x 50k pods placed sequentially, each binding
         # raising the chosen node's hot value before the next pod (one GPU).
         g5 = synth.CONFIGS[5]
@@ -1063,7 +1167,7 @@ def main():
 
     cpu = None
     host_parse = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 3:
+    if one and not args.no_cpu_baseline and args.config == 3:
         # (the headline configuration only: config 4's 1M-node annotation strings alone take minutes to build)
         from oracle import oracle as O
         ann = c.annotations()
@@ -1124,6 +1228,7 @@ def main():
             extras["controller_hot_values"] = controller_leg(cd, O, synth, spec, dev, c, N, B)
 
     if rank == 0:
+        keys = m["keys"]
         line = {
             "metric": "placements/sec",
             "value": round(placements, 1),
@@ -1137,7 +1242,7 @@ def main():
                                    "but the step path evaluates a node per pod only where one of its expiries falls "
                                    "inside the batch (DESIGN.md 4.4): a full-rescan equivalent, not an evaluation "
                                    "count; with node shards over N GPUs (weak scaling) it grows with the cluster"),
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
@@ -1148,28 +1253,26 @@ def main():
             "data": "synthetic",
             "config": {"workload": (f"config{args.config}: {n_total} nodes ({N} per GPU) x {P} pods, 6 metrics, "
                                     + (f"hot values from one {synth.CONFIGS[4]['bindings']}-entry binding log over "
-                                       "all nodes (each rank holds its nodes' entries)" if strong else
-                                       f"hot values from a {B}-entry binding log per 100k-node cell")
+                                       "all nodes (each GPU holds its nodes' entries)" if strong else
+                                       f"hot values from a {synth.CONFIGS[3]['bindings']}-entry binding log per "
+                                       "100k-node cell")
                                     + ", README default policy"),
-                       "nodes_total": n_total, "nodes_per_gpu": N, "pods": P, "bindings_this_rank": B,
-                       "parallelism": f"node-shard x{world}",
-                       "launch": ("eager" if graph is None else "hipGraph replay per batch"),
-                       "enqueue_threads": TQ,
-                       "batches_in_flight": K},
-            "batches_in_flight": {"k": K, "how": "K engines (own copy of the shard's nodes, binding log, scratch) on "
-                                                "K HIP streams, batch i on engine i % K; every batch runs the whole "
-                                                "step" + (f"; one RCCL max all-reduce per group of {G} batches' keys "
-                                                          f"[{G}][P] on " + ("its own stream" if args.ar_stream == "own"
-                                                                             else "the group's last batch's stream")
-                                                          if coll else ""),
-                                  "keys_agree": keys_agree,
-                                  "batch_latency_ms": round(batch_latency_ms, 4)},
+                       "nodes_total": n_total, "nodes_per_gpu": N, "pods": P, "bindings_gpu0": B,
+                       "parallelism": f"node-shard x{n_gpus}",
+                       "engine": m["engine_path"],
+                       "batches_in_flight": m["K"],
+                       "batch_times": (f"batch i at now0 + (i % {len(m['nows'])}) x {m['span'] / 1e9:g} s (its pods "
+                                       "shifted alike): the hot-value cutoffs move every batch and K2's suffix "
+                                       "search reruns; the cycle bounds the drift of the un-resynced synthetic "
+                                       "snapshot and log")},
+            "batches_in_flight": {"k": m["K"], "how": m["how"], "keys_agree": m["keys_agree"],
+                                  "batch_latency_ms": round(m["batch_latency_ms"], 4)},
             "placements_per_s": round(placements, 1),
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
-            "allreduce_ms": None if ar_ms is None else round(ar_ms, 4),
-            "host": host,
-            "keys_match_1gpu": keys_match,
-            "keys_match_1gpu_how": keys_match_how,
+            "allreduce_ms": None if m["ar_ms"] is None else round(m["ar_ms"], 4),
+            "host": m["host"],
+            "keys_match_1gpu": m["keys_match"],
+            "keys_match_1gpu_how": m["keys_match_how"],
             "roofline": roofline,
             "roofline_kernels": roofs,
             "roofline_cold": roofline_cold,
@@ -1182,10 +1285,6 @@ def main():
         }
         line.update(extras)
         print(json.dumps(line), flush=True)
-    for e in engs:
-        e.close()
-    if coll:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -101,6 +101,20 @@ def _load():
         "crane_dyn_update_node_steps": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, C.c_int64, C.c_int64, vp, vp, vp,
                                                   vp]),
         "crane_dyn_version": (C.c_char_p, []),
+        "crane_dyn_forget_stream": (C.c_int, [vp, vp]),
+        "crane_shard_range": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, P(C.c_int64), P(C.c_int64)]),
+        "crane_dyn_group_create": (C.c_int, [P(_CPolicy), C.c_int32, vp, C.c_int32, P(vp)]),
+        "crane_dyn_group_destroy": (C.c_int, [vp]),
+        "crane_dyn_group_last_error": (C.c_char_p, [vp]),
+        "crane_dyn_group_set_option": (C.c_int, [vp, C.c_char_p, C.c_int64]),
+        "crane_dyn_group_size": (C.c_int32, [vp]),
+        "crane_dyn_group_shard": (C.c_int, [vp, C.c_int32, P(C.c_int32), P(C.c_int64), P(C.c_int64)]),
+        "crane_dyn_group_engine": (vp, [vp, C.c_int32, C.c_int32]),
+        "crane_dyn_group_upload_nodes": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp]),
+        "crane_dyn_group_upload_bindings": (C.c_int, [vp, C.c_int64, vp, vp]),
+        "crane_dyn_group_step_keys_async": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp]),
+        "crane_dyn_group_sync": (C.c_int, [vp]),
+        "crane_dyn_group_schedule": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -125,6 +139,10 @@ ABI_SYMBOLS = (
     "crane_tz_load", "crane_tz_load_bytes", "crane_tz_free", "crane_tz_lookup", "crane_tz_date",
     "crane_parse_annotation_tz", "crane_parse_annotations_tz", "crane_dyn_step_slots", "crane_dyn_node_steps",
     "crane_dyn_node_steps_subset", "crane_dyn_update_nodes", "crane_dyn_update_node_steps",
+    "crane_dyn_forget_stream", "crane_shard_range", "crane_dyn_group_create", "crane_dyn_group_destroy",
+    "crane_dyn_group_last_error", "crane_dyn_group_set_option", "crane_dyn_group_size", "crane_dyn_group_shard",
+    "crane_dyn_group_engine", "crane_dyn_group_upload_nodes", "crane_dyn_group_upload_bindings",
+    "crane_dyn_group_step_keys_async", "crane_dyn_group_sync", "crane_dyn_group_schedule",
 )
 
 
@@ -492,6 +510,11 @@ class Engine:
                                                   None if d_flags is None else C.c_void_p(d_flags.data_ptr()),
                                                   C.c_void_p(d_keys.data_ptr()), stream))
 
+    def forget_stream(self, stream):
+        """The caller is about to destroy `stream` (a raw hipStream_t handle): wait for it and drop
+        the engine's handle of it (crane_dyn_forget_stream)."""
+        self._check(lib.crane_dyn_forget_stream(self.h, stream))
+
     # stage timing: HIP events the engine records after each kernel stage
     def set_profiling(self, on=True):
         self._check(lib.crane_dyn_set_profiling(self.h, 1 if on else 0))
@@ -601,6 +624,130 @@ class Engine:
         ch = np.empty(n_pods, np.int64)
         self._check(lib.crane_dyn_greedy(self.h, n_pods, int(now_ns), _ptr(fl), _ptr(ch)))
         return ch
+
+
+def shard_range(n_nodes, n_shards, shard):
+    """Contiguous balanced node range [lo, hi) of one shard (crane_shard_range)."""
+    lo, hi = C.c_int64(), C.c_int64()
+    rc = lib.crane_shard_range(int(n_nodes), int(n_shards), int(shard), C.byref(lo), C.byref(hi))
+    if rc:
+        raise CraneError(rc, "bad shard arguments")
+    return lo.value, hi.value
+
+
+class _BorrowedEngine(Engine):
+    """A group's engine (crane_dyn_group_engine): the group owns and destroys it."""
+
+    def __init__(self, h, policy, device):
+        self.policy, self.h, self.device, self.n_nodes = policy, C.c_void_p(h), device, 0
+        self.metric_names = [lib.crane_dyn_metric_name(self.h, i).decode()
+                             for i in range(lib.crane_dyn_num_metrics(self.h))]
+
+    def close(self):
+        self.h = C.c_void_p()
+
+
+class Group:
+    """One process, N devices (crane_dyn_group_*): node shards over the devices, `depth` batches in
+    flight, the shards' keys max-combined by an in-library RCCL all-reduce (ncclCommInitAll)."""
+
+    def __init__(self, policy: Policy, devices=(0,), depth: int = 1):
+        self.policy = policy
+        self.devices = [int(d) for d in devices]
+        self.depth = int(depth)
+        dv = (C.c_int32 * len(self.devices))(*self.devices)
+        h = C.c_void_p()
+        rc = lib.crane_dyn_group_create(C.byref(policy.c), len(self.devices), C.cast(dv, C.c_void_p), self.depth,
+                                        C.byref(h))
+        self.h = h
+        if rc:
+            msg = lib.crane_dyn_group_last_error(h).decode() if h.value else ""
+            self.close()
+            raise CraneError(rc, msg)
+        self.n_nodes = 0
+        self.metric_names = self.engine(0).metric_names
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value and lib is not None:
+            lib.crane_dyn_group_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc):
+        if rc:
+            raise CraneError(rc, lib.crane_dyn_group_last_error(self.h).decode())
+
+    def engine(self, i, slot=0):
+        """Shard i's engine for batch slot `slot` (borrowed: the group destroys it)."""
+        p = lib.crane_dyn_group_engine(self.h, int(i), int(slot))
+        if not p:
+            raise CraneError(-1, "no such shard / slot")
+        return _BorrowedEngine(p, self.policy, self.devices[i])
+
+    def set_option(self, name, value):
+        self._check(lib.crane_dyn_group_set_option(self.h, name.encode(), int(value)))
+
+    def shard(self, i):
+        """(device, lo, hi) of shard i."""
+        d, lo, hi = C.c_int32(), C.c_int64(), C.c_int64()
+        self._check(lib.crane_dyn_group_shard(self.h, int(i), C.byref(d), C.byref(lo), C.byref(hi)))
+        return d.value, lo.value, hi.value
+
+    def upload_nodes(self, val, ts, hv=None, hv_ts=None):
+        val = np.ascontiguousarray(val, np.float64)
+        ts = np.ascontiguousarray(ts, np.int64)
+        N = val.shape[1]
+        if hv is not None:
+            hv = np.ascontiguousarray(hv, np.float64)
+            hv_ts = np.ascontiguousarray(hv_ts, np.int64)
+        self._check(lib.crane_dyn_group_upload_nodes(self.h, N, _ptr(val), _ptr(ts), _ptr(hv), _ptr(hv_ts)))
+        self.n_nodes = N
+
+    def upload_bindings(self, node, ts_s):
+        node = np.ascontiguousarray(node, np.int32)
+        ts_s = np.ascontiguousarray(ts_s, np.int64)
+        self._check(lib.crane_dyn_group_upload_bindings(self.h, len(node), _ptr(node), _ptr(ts_s)))
+
+    @staticmethod
+    def _ptrs(ts, ctype=C.c_void_p):
+        return (ctype * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
+
+    def step_keys_fn(self, d_now, d_flags, d_keys):
+        """crane_dyn_group_step_keys_async bound to per-device torch tensors (lists, one per device):
+        returns f(now_ns, hv_ts_ns)."""
+        P = d_now[0].numel()
+        pn, pk = self._ptrs(d_now), self._ptrs(d_keys)
+        pf = None if d_flags is None else self._ptrs(d_flags)
+        fn, h, check = lib.crane_dyn_group_step_keys_async, self.h, self._check
+        an, ak = C.cast(pn, C.c_void_p), C.cast(pk, C.c_void_p)
+        af = None if pf is None else C.cast(pf, C.c_void_p)
+        keep = (pn, pk, pf)
+
+        def step(now_ns, hv_ts_ns):
+            _ = keep
+            rc = fn(h, now_ns, hv_ts_ns, P, an, af, ak)
+            if rc:
+                check(rc)
+
+        return step
+
+    def step_keys_async(self, now_ns, hv_ts_ns, d_now, d_flags, d_keys):
+        self.step_keys_fn(d_now, d_flags, d_keys)(int(now_ns), int(hv_ts_ns))
+
+    def sync(self):
+        self._check(lib.crane_dyn_group_sync(self.h))
+
+    def schedule(self, now_ns, hv_ts_ns, pods_now, pod_flags=None):
+        """One batch from host arrays: (chosen global node [P], chosen score [P])."""
+        now = np.ascontiguousarray(pods_now, np.int64).reshape(-1)
+        fl = None if pod_flags is None else np.ascontiguousarray(pod_flags, np.uint8).reshape(-1)
+        ch = np.empty(len(now), np.int64)
+        cs = np.empty(len(now), np.int64)
+        self._check(lib.crane_dyn_group_schedule(self.h, int(now_ns), int(hv_ts_ns), len(now), _ptr(now), _ptr(fl),
+                                                 _ptr(ch), _ptr(cs)))
+        return ch, cs
 
 
 def version() -> str:

@@ -98,10 +98,6 @@ struct Options {
                               // 3: large (region pass with coarse bins + dense per-bin histograms)
     int k1_threads = 256;     // K1 workgroup size (the dedupe K2 bins nodes by it): 128 or 256
     bool k1_keep_rec = false; // the fused keys-only step also writes the node records
-    int k1_split = 0;         // K1+K3a as two kernels (count, then k3a_emit): 0 never, 1 always,
-                              // 2 when the node blocks exceed one round of resident workgroups.
-                              // Off: at 4M nodes (cold) the count pass takes 0.115 ms (52 % of
-                              // HBM) but k3a_emit 0.066 ms more, vs 0.135 ms fused
     bool k1_fuse = true;      // K3a (step tables) fused into the node pass
     bool k3p_in_k2 = true;    // K3p rides as extra workgroups of the K2x launch
     int keys_path = 0;        // 0: step path when it applies, 1: the per-pair kernel (K3m keys)
@@ -116,9 +112,6 @@ struct Options {
     int k2l_threads = 1024;   // large K2: partition workgroup size at 4096-binding regions (512 or 1024;
                               // cold 4M x 16M: 1024 0.084-0.085 ms vs 512 0.087-0.089, same-box sweeps
                               // profiles/ab/r03_k2_cold_*.txt)
-    int k2y_first = 6;        // large K2: 16-byte blocks of each region's run k2y loads up front (3..8;
-                              // cold 4M x 16M ordered log: k2y 0.019 ms at 3, 0.0165 at 6,
-                              // profiles/r04/k2y_first.txt)
     int sel_chain = 0;        // selection windows: 0 LDS rank/select walk when it fits, 1 streaming kernel
     int step_lds_cap = 1 << 30;  // K1: one-step records per kind staged in LDS at most (0: always st.stage)
     int step_pieces = 0;      // middle pieces cut into elementary ones per block (step_pieces): 0 when the
@@ -129,13 +122,7 @@ struct Options {
                               // >= kPieceMinTiles pod tiles (a piece is re-read once per tile), 1 always,
                               // 2 never (then no per-tile piece ranges either: K3s reads all pieces)
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
-    int emit_threads = 0;     // split form's k3a_emit workgroup: 0 = the block's width, 64 = one wave per block
     int k2_sorted = 1;        // a time-ordered log: K2 reads the widest window's suffix, ranks by position
-    int k1_count_form = 0;    // split form's count pass: 0 default, 1/2/3 registers for 5/6/7 waves (A/B),
-                              // 4 persistent with the next block's rows prefetched into LDS, 5/6/7 streamed
-                              // (no records; k3a_emit rebuilds the stepped ones) at 8/7/6 waves, 8/9
-                              // streamed writing the stepped records, 6/7 waves, 10/11 streamed emitting
-                              // them (k3a_emit sorts only), 6/5 waves
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
 
@@ -152,7 +139,7 @@ struct crane_dyn {
     std::mutex mu;
     std::string err;
     int device = 0;
-    int n_cu = 0;  // compute units of the device (the split node pass's threshold)
+    int n_cu = 0;  // compute units of the device
     hipStream_t stream = nullptr;
     Options opt;
     // policy
@@ -211,8 +198,6 @@ struct crane_dyn {
     DevBuf<unsigned long long> trace;  // [3][kTraceWgs][8] phase stamps (option "trace")
     DevBuf<int32_t> sperm, scnt;  // K3 step path scratch (step.hip)
     DevBuf<int64_t> stile, spnow, sbatch;
-    DevBuf<uint32_t> sq;          // split form: queued items [nblk][2 * bs]
-    DevBuf<int32_t> sqm, snq;     // their middle-piece slots, and the count per block
     DevBuf<int64_t> sel_fth, sel_win, sel_state;  // framework selection (select.hip)
     DevBuf<long long> sel_keys;
     DevBuf<unsigned char> stp_dev;  // node answer tables (crane_dyn_node_steps): bp, ns, ff, score
@@ -441,8 +426,7 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         // is rewritten, so nothing is zeroed before and K1 leaves them
         HIPTRY(h, h->k2_sorted.reserve(hot_dedupe_scratch(gl)));
         HIPTRY(h, launch_hot_count_large(bn, h->bts.p, Bk, h->N, by_pos ? pcut : cut, gl, h->k2_sorted.p,
-                                         h->buckets.p, h->n_cu, st, h->opt.k2l_threads,
-                                         h->opt.k2y_first));
+                                         h->buckets.p, h->n_cu, st, h->opt.k2l_threads));
         h->buckets_zero = false;
         h->buckets_dense = true;
         return CRANE_OK;
@@ -471,8 +455,7 @@ static int k1_bs(const crane_dyn* h) {
 // K1 (optionally with the K3 step tables fused in).  Hot values: pending K2
 // counts (consumed), else the values the last consuming pass kept, else the
 // uploaded annotation.
-static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nullptr, const K1Step* step = nullptr,
-                            K1Args* used = nullptr) {
+static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nullptr, const K1Step* step = nullptr) {
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before the node pass");
     K1Args a{};
     a.pol = h->dp;
@@ -506,10 +489,8 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
         a.hv_ts = h->hv_ts.p;
     }
     a.threads = k1_bs(h);
-    a.n_cu = h->n_cu;
     a.trace = (h->N + a.threads - 1) / a.threads <= kTraceWgs ? h->trace_region(1) : nullptr;
-    HIPTRY(h, launch_node_pass(h->shape, a, st, step, h->opt.k1_count_form));
-    if (used) *used = a;
+    HIPTRY(h, launch_node_pass(h->shape, a, st, step));
     if (consume) {
         if (!h->hx_pending) h->buckets_zero = !h->buckets_dense;  // K1 zeroed what it read
         h->counts_pending = false;
@@ -598,28 +579,9 @@ static int step_pods(crane_dyn* h, const StepPlan& sp, int64_t P, const int64_t*
 static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_keys, hipStream_t st) {
     if (P == 0) return CRANE_OK;
     if (sp.fuse) {
-        K1Step ks{h->stile.p, h->sbatch.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, h->dp.winv, sp.stt};
-        const int32_t bs = sp.stt.bs, nblk = sp.stt.nblk;
-        const bool split = !h->opt.k1_keep_rec &&
-                           (h->opt.k1_split == 1 || (h->opt.k1_split == 2 && nblk > 5 * h->n_cu));
-        if (split) {
-            HIPTRY(h, h->sq.reserve((size_t)nblk * 2 * bs));
-            HIPTRY(h, h->sqm.reserve((size_t)nblk * 2 * bs));
-            HIPTRY(h, h->snq.reserve((size_t)nblk));
-            ks.srec = h->rec.p;
-            ks.qg = h->sq.p;
-            ks.qmg = h->sqm.p;
-            ks.nqg = h->snq.p;
-        }
-        K1Args used{};
-        int rc = node_pass_locked(h, st, nullptr, &ks, &used);
+        const K1Step ks{h->stile.p, h->sbatch.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, h->dp.winv, sp.stt};
+        int rc = node_pass_locked(h, st, nullptr, &ks);
         if (rc) return rc;
-        // after the streamed count pass the emit rebuilds the stepped records from the SoA
-        const bool rebuild = split && count_stream_rebuild(h->opt.k1_count_form, used);
-        const bool emitted = split && count_stream_emits(h->opt.k1_count_form, used);
-        if (split)
-            HIPTRY(h, launch_step_emit(h->shape, ks, h->N, bs, st, h->opt.emit_threads ? h->opt.emit_threads : bs,
-                                       rebuild || emitted ? &used : nullptr, emitted));
     } else {
         if (h->rec_dirty) {
             int rc = node_pass_locked(h, st);
@@ -706,9 +668,12 @@ static int mark_busy(crane_dyn* h, hipStream_t st) {
 // snapshot sync / controller tick, not per batch.
 static int quiesce(crane_dyn* h) {
     if (h->busy.empty()) return CRANE_OK;
+    // the list is cleared even when a wait fails (a stream the caller destroyed without
+    // crane_dyn_forget_stream): the error is reported once, not by every later state change
+    std::vector<hipStream_t> busy;
+    busy.swap(h->busy);
     HIPTRY(h, hipSetDevice(h->device));
-    for (hipStream_t s : h->busy) HIPTRY(h, hipStreamSynchronize(s));
-    h->busy.clear();
+    for (hipStream_t s : busy) HIPTRY(h, hipStreamSynchronize(s));
     return CRANE_OK;
 }
 
@@ -752,11 +717,12 @@ int crane_dyn_create(const crane_policy* pol, int32_t device, crane_dyn** out) {
 
 int crane_dyn_destroy(crane_dyn* h) {
     if (!h) return CRANE_OK;
+    // the whole device, not the remembered caller streams: a caller may have destroyed one of
+    // them already (its handle is then dangling), and nothing may still read the buffers freed here
     if (h->stream) {
         (void)hipSetDevice(h->device);
-        (void)hipStreamSynchronize(h->stream);
+        (void)hipDeviceSynchronize();
     }
-    for (hipStream_t s : h->busy) (void)hipStreamSynchronize(s);
     h->busy.clear();
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->ev.clear();
@@ -769,7 +735,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
     h->mFs.release(); h->mIs.release(); h->mgi.release();
     h->trace.release();
-    h->sperm.release(); h->scnt.release(); h->stile.release(); h->sbatch.release(); h->sq.release(); h->sqm.release(); h->snq.release(); h->spnow.release(); h->smid.release(); h->sstep1.release(); h->sstage.release();
+    h->sperm.release(); h->scnt.release(); h->stile.release(); h->sbatch.release(); h->spnow.release(); h->smid.release(); h->sstep1.release(); h->sstage.release();
     h->spm1.release(); h->ssm0.release(); h->srows.release(); h->sprow.release();
     h->sel_fth.release(); h->sel_win.release(); h->sel_state.release(); h->sel_keys.release();
     h->stp_dev.release(); h->stp_host.release(); h->upd_dev.release(); h->upd_host.release();
@@ -779,6 +745,17 @@ int crane_dyn_destroy(crane_dyn* h) {
 }
 
 const char* crane_dyn_last_error(const crane_dyn* h) { return h ? h->err.c_str() : "null engine"; }
+
+int crane_dyn_forget_stream(crane_dyn* h, void* stream) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    auto it = std::find(h->busy.begin(), h->busy.end(), (hipStream_t)stream);
+    if (it == h->busy.end()) return CRANE_OK;
+    h->busy.erase(it);
+    HIPTRY(h, hipSetDevice(h->device));
+    HIPTRY(h, hipStreamSynchronize((hipStream_t)stream));
+    return CRANE_OK;
+}
 
 int32_t crane_dyn_num_metrics(const crane_dyn* h) { return h ? (int32_t)h->slot_names.size() : 0; }
 
@@ -795,7 +772,6 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     auto range = [&](int64_t lo, int64_t hi) { return value >= lo && value <= hi; };
     if (n == "k2_form" && range(0, 3)) o.k2_form = (int)value;
     else if (n == "k1_threads" && (value == 128 || value == 256)) o.k1_threads = (int)value;
-    else if (n == "k1_split" && range(0, 2)) o.k1_split = (int)value;
     else if (n == "k1_keep_records" && range(0, 1)) o.k1_keep_rec = value != 0;
     else if (n == "k1_fuse_steps" && range(0, 1)) o.k1_fuse = value != 0;
     else if (n == "k3p_in_k2" && range(0, 1)) o.k3p_in_k2 = value != 0;
@@ -809,13 +785,10 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "k2l_region" && (value == 2048 || value == 4096)) o.k2l_region = (int)value;
     else if (n == "k2l_co_t" && range(0, 1)) o.k2l_co_t = (int)value;
     else if (n == "k2l_threads" && (value == 512 || value == 1024)) o.k2l_threads = (int)value;
-    else if (n == "k2y_first" && range(3, 8)) o.k2y_first = (int)value;
     else if (n == "sel_chain" && range(0, 1)) o.sel_chain = (int)value;
     else if (n == "step_pieces" && range(0, 2)) o.step_pieces = (int)value;
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
-    else if (n == "emit_threads" && (value == 0 || value == 64)) o.emit_threads = (int)value;
     else if (n == "k2_sorted" && range(0, 1)) o.k2_sorted = (int)value;
-    else if (n == "k1_count_form" && range(0, 11)) o.k1_count_form = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
         if (o.trace) {

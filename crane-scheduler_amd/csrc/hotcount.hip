@@ -648,29 +648,19 @@ static hipError_t launch_y(const uint32_t* scratch, const HotPart& g, int32_t W,
 
 hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, uint32_t* buckets,
-                                  int n_cu, hipStream_t st, int threads, int yfirst) {
+                                  int n_cu, hipStream_t st, int threads) {
     hipError_t e;
     if (g.reg == 2048) e = launch_large_x<512, 2048>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
     else if (threads == 1024) e = launch_large_x<1024, 4096>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
     else e = launch_large_x<512, 4096>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
     if (e != hipSuccess) return e;
-    // (k2y_first: 16-byte blocks of each run loaded in the count/offset words' round; kYPer = the
-    // fewest regions per lane that cover the log)
+    // kYPer = the fewest regions per lane that cover the log; kYFirst = the 16-byte blocks of each
+    // run loaded in the count/offset words' round (round 4's sweep, profiles/r04/k2y_first.txt:
+    // cold 4M x 16M ordered log k2y 0.019 ms at 3, 0.0165 at 6, as many as registers allow at
+    // four and eight regions per lane)
     if (g.nblk > 4 * kYThreads) return launch_y<8, 2>(scratch, g, cut.n_win, N, buckets, st);
-    if (g.nblk > 2 * kYThreads) {
-        switch (yfirst) {
-            case 3: return launch_y<4, 3>(scratch, g, cut.n_win, N, buckets, st);
-            case 4: return launch_y<4, 4>(scratch, g, cut.n_win, N, buckets, st);
-            default: return launch_y<4, 5>(scratch, g, cut.n_win, N, buckets, st);
-        }
-    }
-    switch (yfirst) {
-        case 3: return launch_y<2, 3>(scratch, g, cut.n_win, N, buckets, st);
-        case 4: return launch_y<2, 4>(scratch, g, cut.n_win, N, buckets, st);
-        case 5: return launch_y<2, 5>(scratch, g, cut.n_win, N, buckets, st);
-        case 6: return launch_y<2, 6>(scratch, g, cut.n_win, N, buckets, st);
-        default: return launch_y<2, 8>(scratch, g, cut.n_win, N, buckets, st);
-    }
+    if (g.nblk > 2 * kYThreads) return launch_y<4, 5>(scratch, g, cut.n_win, N, buckets, st);
+    return launch_y<2, 6>(scratch, g, cut.n_win, N, buckets, st);
 }
 
 HotBins hot_bins_geometry(int64_t B, int64_t N, int32_t W) {

@@ -237,7 +237,7 @@ constexpr int64_t kK2LargeHistBytes = 128 * 1024;
 HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W, int32_t reg, int32_t co_t);
 hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, uint32_t* buckets,
-                                  int n_cu, hipStream_t st, int threads = 512, int yfirst = 3);
+                                  int n_cu, hipStream_t st, int threads = 512);
 
 // ---------------------------------------------------------------- K3 step path (step.hip)
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
@@ -321,13 +321,6 @@ struct K1Step {
     double wsum;
     double winv;             // 1 / wsum when |wsum| is a power of two, else 0 (score_at)
     StepTables st;
-    // split form (large N): the node pass only classifies and counts; the stepped nodes'
-    // records (srec[node]), the queued (node, kind) items per block (qg / qmg [nblk][2 * bs])
-    // and their count (nqg [nblk]) go to HBM, and k3a_emit builds the block's tables
-    void* srec;
-    uint32_t* qg;
-    int32_t* qmg;
-    int32_t* nqg;
 };
 
 size_t node_rec_bytes(int shape);
@@ -356,32 +349,9 @@ struct K1Args {
     const uint32_t* hx_CO;
     int32_t hx_nblk;
     int32_t threads;        // workgroup size: 128 or 256
-    int32_t n_cu;           // compute units (the prefetching count pass sizes its persistent grid by it)
     unsigned long long* trace;  // phase trace or null
 };
 // step (optional): also build the K3 step tables of a pod batch (K3a fused).
-// count_form (split form only): 0 the default kernel, 1 / 2 / 3 registers for 5 / 6 / 7 waves per
-// SIMD with the dedupe-form path compiled out when no K2 entries are given (A/B), 4 the persistent
-// count pass that prefetches the next block's rows into LDS (k1_count_pf; not with the dedupe-form
-// K2 entries, whose block runs it cannot stage: those take the default kernel), 5 / 6 / 7 the
-// streamed count pass (k1_count_stream, no records: k3a_emit rebuilds the stepped ones)
-hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr,
-                            int count_form = 0);
-// split form's second kernel: one workgroup per producer block of the node pass (bs nodes) of
-// bt threads (bs, or 64: one wave per block)
-// rc: the node pass was the streamed count pass (count_stream true): the emit rebuilds the
-// stepped nodes' records from the SoA with these node-pass arguments
-// (sort_only, with rc: the count pass emitted the records itself, count_stream_emits)
-hipError_t launch_step_emit(int shape, const K1Step& step, int64_t N, int32_t bs, hipStream_t st, int32_t bt = 0,
-                            const K1Args* rc = nullptr, bool sort_only = false);
-// the split form's count pass for this count_form is the streamed one (k1_count_stream: 5 / 6 / 7
-// = registers for 8 / 7 / 6 waves per SIMD, the stepped records rebuilt by k3a_emit; 8 / 9 = the
-// stepped records written by the count pass, registers for 6 / 7 waves; not with the dedupe-form
-// K2 entries)
-// 10 / 11: the stepped lanes also emit their one-step records and middle pieces (registers for
-// 6 / 5 waves), k3a_emit only sorts and publishes
-bool count_stream(int count_form, const K1Args& a);
-bool count_stream_rebuild(int count_form, const K1Args& a);
-bool count_stream_emits(int count_form, const K1Args& a);
+hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr);
 
 }  // namespace crane

@@ -30,7 +30,8 @@
  * since the last such wait — those streams only, not the device — so they never
  * change a buffer a kernel is still reading.  The engine keeps a caller stream's
  * handle until that wait: a stream passed to an *_async call must outlive the
- * engine's next state change (or its destroy).  Asynchronous calls on ONE engine
+ * engine's next state change, or be handed back first with crane_dyn_forget_stream (which waits
+ * for it); destroy waits for the whole device.  Asynchronous calls on ONE engine
  * from several streams must be ordered by the caller (they share the engine's
  * scratch): use one stream per engine.  Nothing in the
  * engine reads the environment; crane_dyn_set_option (tests / A-B tools only)
@@ -132,6 +133,10 @@ typedef struct crane_dyn crane_dyn;
 int crane_dyn_create(const crane_policy *pol, int32_t device, crane_dyn **out);
 int crane_dyn_destroy(crane_dyn *h);
 const char *crane_dyn_last_error(const crane_dyn *h);
+/* A caller stream that *_async calls enqueued work on is about to be destroyed: wait for it and
+ * drop the engine's handle of it (the next state change would otherwise wait on a dangling
+ * handle).  No-op for a stream the engine does not hold. */
+int crane_dyn_forget_stream(crane_dyn *h, void *stream);
 
 /* Metric slots: the distinct annotation keys the policy reads, in the order
  * the SoA rows of crane_dyn_upload_nodes must follow. */
@@ -307,11 +312,8 @@ const char *crane_dyn_version(void);
 /* Alternative kernel forms of the same results, for tests and A/B tools:
  *   "k2_form" 0 dedupe (default; large past its cap) | 1 binned | 2 hash | 3 large   "k1_threads" 256 | 128
  *   "k1_keep_records" 0 | 1   "k1_fuse_steps" 1 | 0   "k3p_in_k2" 1 | 0
- *   "k1_split" 0 fused node pass | 1 count pass + k3a_emit | 2 split past one round of workgroups
- *   "emit_threads" 0 k3a_emit workgroups as wide as the block | 64 one wave per block
- *   "k2_sorted" 1 a time-ordered log (checked at upload): K2 reads the widest window's suffix only | 0 never
- *   "k1_count_form" 0 | 1 | 2 | 3: the split form's count pass budgeted for 5 / 6 / 7 waves per SIMD (A/B)
- *   "keys_path" 0 step path | 1 per-pair kernel   "greedy_form" 0 merge | 1 sequential
+  *   "k2_sorted" 1 a time-ordered log (checked at upload): K2 reads the widest window's suffix only | 0 never
+  *   "keys_path" 0 step path | 1 per-pair kernel   "greedy_form" 0 merge | 1 sequential
  *   "matrix_vec" 0 auto | 1 | 4 | 8 | 16 nodes per lane   "matrix_chunk" 0 auto | pods per workgroup (<= 1024)
  *   "step_rows" 1 producers index the records per pod tile | 0 K3s searches them
  *   "k3s_blocks" 0 auto | producer blocks per K3s workgroup aimed for (1..256)
@@ -324,6 +326,59 @@ int crane_dyn_set_option(crane_dyn *h, const char *name, int64_t value);
  * "trace" on: out[8 * workgroup + k] = s_memrealtime (100 MHz) at phase k.
  * Returns the number of entries copied (<= max). */
 int64_t crane_dyn_debug_trace(crane_dyn *h, int32_t which, int64_t max, uint64_t *out);
+
+/* ------------------------------------------------------------------ groups
+ * One process, N devices (SURVEY §8(b) crane_dyn_create(..., device_count, ...), §8(e)): the
+ * scheduler is one Go process with one plugin instance (cmd/scheduler/main.go:18-32,
+ * plugins.go:105-120), so the node-shard path is reached through one handle.  A group holds per
+ * device `depth` engines (one per batch in flight) over the device's contiguous node range
+ * (crane_shard_range of the cluster over n_dev shards), their HIP streams and one RCCL
+ * communicator per device (ncclCommInitAll).  A batch = every device's shard step
+ * (crane_dyn_step_keys_async), then an in-place ncclAllReduce(int64, ncclMax) of the packed keys
+ * on the same streams: every device then holds the global choice per pod.  With n_dev > 1 each
+ * device has a worker thread enqueueing its part (the caller only hands over the batch).
+ * Options (crane_dyn_group_set_option): "collective" 0 never (crane_dyn_group_schedule max-combines
+ * on the host; the async form leaves per-shard keys) | 1 when n_dev > 1 (default) | 2 always (a
+ * one-rank communicator: tests); "threads" -1 auto | 0 the caller's thread (the collective in
+ * ncclGroupStart/End) | 1 worker threads; any other name goes to every engine. */
+typedef struct crane_dyn_group crane_dyn_group;
+/* Contiguous balanced node range of shard `shard` of n_shards (the first n % n_shards get one more). */
+int crane_shard_range(int64_t n_nodes, int32_t n_shards, int32_t shard, int64_t *lo, int64_t *hi);
+/* devices NULL = 0 .. n_dev-1 (a device may be listed more than once: several shards on one GPU,
+ * combined without the collective); depth in [1, 64].  The handle is returned on failure too: read
+ * its error, then destroy it. */
+int crane_dyn_group_create(const crane_policy *pol, int32_t n_dev, const int32_t *devices, int32_t depth,
+                           crane_dyn_group **out);
+int crane_dyn_group_destroy(crane_dyn_group *g);
+const char *crane_dyn_group_last_error(const crane_dyn_group *g);
+int crane_dyn_group_set_option(crane_dyn_group *g, const char *name, int64_t value);
+int32_t crane_dyn_group_size(const crane_dyn_group *g);
+/* device and node range [lo, hi) of shard i (after crane_dyn_group_upload_nodes) */
+int crane_dyn_group_shard(const crane_dyn_group *g, int32_t i, int32_t *device, int64_t *lo, int64_t *hi);
+/* the engine of shard i for batch slot `slot` (metric names, profiling, options) */
+crane_dyn *crane_dyn_group_engine(crane_dyn_group *g, int32_t i, int32_t slot);
+/* The whole cluster's SoA as crane_dyn_upload_nodes takes it ([M][n_nodes] rows, global order);
+ * each device keeps its shard's columns (node_offset = its lo). */
+int crane_dyn_group_upload_nodes(crane_dyn_group *g, int64_t n_nodes, const double *val, const int64_t *ts,
+                                 const double *hv, const int64_t *hv_ts);
+/* The whole binding log with GLOBAL node indices; each device keeps its nodes' bindings, local
+ * indices, in log order (a time-ordered log stays one). */
+int crane_dyn_group_upload_bindings(crane_dyn_group *g, int64_t n, const int32_t *node, const int64_t *ts_s);
+/* One batch, asynchronous: d_now[i] / d_flags[i] (NULL array or entry = no flags) / d_keys[i] are
+ * device pointers on device i.  Batch b (counted from the group's creation) runs on slot b % depth:
+ * its engines and streams; d_keys[i] then holds the global keys (the per-shard keys with
+ * "collective" 0).  A key buffer reused every `depth` batches is ordered by the slot's stream.
+ * Errors of the enqueued work are reported by crane_dyn_group_sync. */
+int crane_dyn_group_step_keys_async(crane_dyn_group *g, int64_t now_ns, int64_t hv_ts_ns, int64_t n_pods,
+                                    const int64_t *const *d_now, const uint8_t *const *d_flags,
+                                    int64_t *const *d_keys);
+/* wait for every batch enqueued on the group */
+int crane_dyn_group_sync(crane_dyn_group *g);
+/* One batch from host arrays, synchronous: chosen[p] = global node index or -1, chosen_score[p]
+ * (either may be NULL) — the scheduler's call per pod batch. */
+int crane_dyn_group_schedule(crane_dyn_group *g, int64_t now_ns, int64_t hv_ts_ns, int64_t n_pods,
+                             const int64_t *now_pods, const uint8_t *pod_flags, int64_t *chosen,
+                             int64_t *chosen_score);
 
 /* ------------------------------------------------------------------ events
  * translateEventToBinding (event.go:118-145): a Scheduled event's message

@@ -285,7 +285,8 @@ class DynamicScheduler {
     }
 
     // Bring the plugin's state up to date with the snapshot now (the first Filter / Score of a
-    // cycle does this itself).
+    // cycle does this itself).  Only between scheduling cycles: it patches the state the
+    // cycle's lock-free Filter / Score calls read.
     bool Sync(std::string* err) {
         std::lock_guard<std::mutex> g(mu_);
         return sync_locked(std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -418,20 +419,23 @@ class DynamicScheduler {
     }
 
     // every node's answers over [now, now + horizon) into v (sized for its node set)
+    // (the horizon [t0, t1) is recorded only once the rows hold it: on a failure the caller
+    // drops the View, so no later cycle answers from rows of another horizon)
     bool build_table(View* v, int64_t now, std::string* err) {
         const size_t N = v->infos.size();
-        v->t0 = now;
-        v->t1 = now > INT64_MAX - horizon_ns_ ? INT64_MAX : now + horizon_ns_;
+        const int64_t t0 = now, t1 = now > INT64_MAX - horizon_ns_ ? INT64_MAX : now + horizon_ns_;
         v->S = (size_t)crane_dyn_step_slots(eng_);
         v->n_steps.resize(N);
         v->bp.resize(N * v->S);
         v->first_fail.resize(N * (v->S + 1));
         v->score.resize(N * (v->S + 1));
-        if (crane_dyn_node_steps(eng_, v->t0, v->t1, (int64_t)N, v->n_steps.data(), v->bp.data(),
-                                 v->first_fail.data(), v->score.data())) {
+        if (crane_dyn_node_steps(eng_, t0, t1, (int64_t)N, v->n_steps.data(), v->bp.data(), v->first_fail.data(),
+                                 v->score.data())) {
             *err = crane_dyn_last_error(eng_);
             return false;
         }
+        v->t0 = t0;
+        v->t1 = t1;
         ++cnt_.tables_built;
         return true;
     }
@@ -466,7 +470,9 @@ class DynamicScheduler {
         return v;
     }
 
-    // the changed nodes: re-parse, scatter into the engine, rebuild their table rows
+    // the changed nodes: re-parse, scatter into the engine, rebuild their table rows.  The View
+    // records the new Node objects only once the engine holds them: a failed call leaves the
+    // nodes marked changed (and the caller drops the View: the next cycle resyncs in full).
     bool update(View* v, int64_t now, std::string* err) {
         const std::vector<const NodeInfo*>& L = v->infos;
         const size_t k = changed_.size();
@@ -476,21 +482,24 @@ class DynamicScheduler {
         std::vector<int64_t> ts;
         if (!parse(cnodes_, 1, &val, &ts, err)) return false;
         const size_t M = (size_t)crane_dyn_num_metrics(eng_);
-        for (size_t j = 0; j < k; ++j) {
-            const size_t i = (size_t)changed_[j];
-            v->nodes[i] = cnodes_[j];
-            v->gens[i] = L[i]->Generation;
-            if (cnodes_[j]) v->name_idx.put(&cnodes_[j]->Name, (int64_t)i);
-        }
-        if (v->name_idx.crowded()) v->index_names();  // entries of replaced Nodes pile up
-        ++cnt_.incremental_syncs;
-        cnt_.nodes_updated += k;
+        auto record = [&] {
+            for (size_t j = 0; j < k; ++j) {
+                const size_t i = (size_t)changed_[j];
+                v->nodes[i] = cnodes_[j];
+                v->gens[i] = L[i]->Generation;
+                if (cnodes_[j]) v->name_idx.put(&cnodes_[j]->Name, (int64_t)i);
+            }
+            if (v->name_idx.crowded()) v->index_names();  // entries of replaced Nodes pile up
+            ++cnt_.incremental_syncs;
+            cnt_.nodes_updated += k;
+        };
         if (now < v->t0 || now >= v->t1) {  // the caller rebuilds the whole table: the columns only
             if (crane_dyn_update_nodes(eng_, (int64_t)k, changed_.data(), val.data(), ts.data(), val.data() + M * k,
                                        ts.data() + M * k)) {
                 *err = crane_dyn_last_error(eng_);
                 return false;
             }
+            record();
             return true;
         }
         // the columns, the records and the changed nodes' rows in one launch (one round trip)
@@ -512,6 +521,7 @@ class DynamicScheduler {
             std::memcpy(&v->first_fail[i * (S + 1)], &rff_[j * (S + 1)], S + 1);
             std::memcpy(&v->score[i * (S + 1)], &rsc_[j * (S + 1)], S + 1);
         }
+        record();
         return true;
     }
 
@@ -582,8 +592,16 @@ class DynamicScheduler {
             view_ = full_sync(L, now, err);
             return view_;
         }
-        if (!changed_.empty() && !update(v.get(), now, err)) return nullptr;
-        if ((now < v->t0 || now >= v->t1) && !build_table(v.get(), now, err)) return nullptr;
+        // a failed engine call drops the View: the next cycle starts from a full sync instead of
+        // answering from rows the engine no longer matches
+        if (!changed_.empty() && !update(v.get(), now, err)) {
+            view_.reset();
+            return nullptr;
+        }
+        if ((now < v->t0 || now >= v->t1) && !build_table(v.get(), now, err)) {
+            view_.reset();
+            return nullptr;
+        }
         return v;
     }
 

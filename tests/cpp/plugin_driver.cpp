@@ -15,6 +15,16 @@
 //   mt <uid> <now_ns> <ds>   as pod, but Filter/Score called from 16 threads at once, half
 //                            of them on a Clone() of the cycle state (preemption dry runs)
 //   counters                 the plugin's sync counters
+// The node-shard group through the C ABI (crane_dyn_group_*), over the same snapshot and policy:
+//   group <devices> <depth> <collective> <threads>   crane_dyn_group_create over the comma-separated
+//                            device list, options set, the snapshot's annotations parsed (the plugin's
+//                            keys, $TZ) and uploaded whole (each device keeps its shard)
+//   gbind <node> <ts_s>      a binding of global node <node> (collected; gbinds uploads them)
+//   gbinds                   crane_dyn_group_upload_bindings of the collected log
+//   gpod <now_ns> <ds>       a pod of the next batch
+//   gsched <now_ns>          crane_dyn_group_schedule of the collected pods at <now_ns> (hot values
+//                            from the bindings stamped now): "G <pod> <node> <score>" per pod
+//   gshard <i>               "GS <i> <device> <lo> <hi>"
 #include <iostream>
 #include <memory>
 #include <thread>
@@ -23,6 +33,8 @@
 #include <vector>
 
 #include "crane_dyn_plugin.hpp"
+
+#include <cstdlib>
 
 using namespace crane::dynamic;
 
@@ -75,6 +87,14 @@ int main() {
     Handle h;
     h.snapshot = &snap;
     std::unique_ptr<DynamicScheduler> ds;
+    crane_dyn_group* grp = nullptr;
+    std::vector<int32_t> gbn;
+    std::vector<int64_t> gbt, gnow;
+    std::vector<uint8_t> gds;
+    auto gcheck = [&](int rc, const char* what) {
+        if (rc) std::cout << "GERR\t" << what << "\t" << crane_dyn_group_last_error(grp) << "\n";
+        return rc == 0;
+    };
     std::string line;
     while (std::getline(std::cin, line)) {
         auto f = split_tab(line);
@@ -102,6 +122,72 @@ int main() {
             snap.replace((size_t)std::stoll(f[1]), f[2], &v);
         } else if (f[0] == "unset") {
             snap.replace((size_t)std::stoll(f[1]), f[2], nullptr);
+        } else if (f[0] == "group") {
+            std::vector<int32_t> devs;
+            for (size_t a = 0, b; a <= f[1].size(); a = b + 1) {
+                b = f[1].find(',', a);
+                if (b == std::string::npos) b = f[1].size();
+                devs.push_back((int32_t)std::stoi(f[1].substr(a, b - a)));
+            }
+            if (grp) crane_dyn_group_destroy(grp);
+            grp = nullptr;
+            if (!gcheck(crane_dyn_group_create(&ds->policy(), (int32_t)devs.size(), devs.data(), std::stoi(f[2]), &grp),
+                        "create") ||
+                !gcheck(crane_dyn_group_set_option(grp, "collective", std::stoll(f[3])), "collective") ||
+                !gcheck(crane_dyn_group_set_option(grp, "threads", std::stoll(f[4])), "threads"))
+                continue;
+            // the snapshot's annotation strings, rows [metric slots..., node_hot_value][node]
+            crane_dyn* e0 = crane_dyn_group_engine(grp, 0, 0);
+            std::vector<std::string> keys;
+            for (int32_t m = 0; m < crane_dyn_num_metrics(e0); ++m) keys.emplace_back(crane_dyn_metric_name(e0, m));
+            keys.emplace_back(NodeHotValue);
+            const size_t R = keys.size(), N = snap.objs.size();
+            std::vector<const char*> strs(R * N, nullptr);
+            std::vector<size_t> lens(R * N, 0);
+            for (size_t i = 0; i < N; ++i)
+                for (size_t m = 0; m < R; ++m) {
+                    auto it = snap.node(i).Annotations.find(keys[m]);
+                    if (it == snap.node(i).Annotations.end()) continue;
+                    strs[m * N + i] = it->second.data();
+                    lens[m * N + i] = it->second.size();
+                }
+            std::vector<double> val(R * N);
+            std::vector<int64_t> ts(R * N);
+            crane_tz* zone = nullptr;
+            const char* tzenv = std::getenv("TZ");
+            if (crane_tz_load(tzenv && *tzenv ? tzenv : "Asia/Shanghai", nullptr, &zone)) {
+                std::cout << "GERR\tzone\n";
+                continue;
+            }
+            crane_parse_annotations_tz((int64_t)(R * N), strs.data(), lens.data(), zone, val.data(), ts.data(), 4);
+            crane_tz_free(zone);
+            const size_t M = R - 1;
+            if (gcheck(crane_dyn_group_upload_nodes(grp, (int64_t)N, val.data(), ts.data(), val.data() + M * N,
+                                                    ts.data() + M * N),
+                       "upload_nodes"))
+                std::cout << "GROUP\t" << crane_dyn_group_size(grp) << "\n";
+        } else if (f[0] == "gbind") {
+            gbn.push_back((int32_t)std::stoll(f[1]));
+            gbt.push_back(std::stoll(f[2]));
+        } else if (f[0] == "gbinds") {
+            gcheck(crane_dyn_group_upload_bindings(grp, (int64_t)gbn.size(), gbn.data(), gbt.data()), "upload_bindings");
+        } else if (f[0] == "gpod") {
+            gnow.push_back(std::stoll(f[1]));
+            gds.push_back((uint8_t)std::stoi(f[2]));
+        } else if (f[0] == "gshard") {
+            int32_t d = -1;
+            int64_t lo = -1, hi = -1;
+            crane_dyn_group_shard(grp, std::stoi(f[1]), &d, &lo, &hi);
+            std::cout << "GS\t" << f[1] << "\t" << d << "\t" << lo << "\t" << hi << "\n";
+        } else if (f[0] == "gsched") {
+            const int64_t now = std::stoll(f[1]);
+            std::vector<int64_t> ch(gnow.size()), sc(gnow.size());
+            if (gcheck(crane_dyn_group_schedule(grp, now, now, (int64_t)gnow.size(), gnow.data(), gds.data(), ch.data(),
+                                                sc.data()),
+                       "schedule"))
+                for (size_t p = 0; p < gnow.size(); ++p) std::cout << "G\t" << p << "\t" << ch[p] << "\t" << sc[p] << "\n";
+            gnow.clear();
+            gds.clear();
         } else if (f[0] == "counters") {
             const auto c = ds->counters();
             std::cout << "C\t" << c.tables_built << "\t" << c.full_syncs << "\t" << c.incremental_syncs << "\t"
@@ -170,5 +256,6 @@ int main() {
             }
         }
     }
+    if (grp) crane_dyn_group_destroy(grp);
     return 0;
 }

@@ -279,13 +279,10 @@ def test_hot_values_large_form_16m():
     assert np.array_equal(ch, och)
     eng.refresh_hot_values(now, now)  # again: the buckets are rewritten whole, nothing left to zero
     assert np.array_equal(eng.hot_values(), ref)
-    for first in (3, 4, 5, 6, 8):  # k2y's up-front blocks per run, both the ordered and the stamp path
-        for srt in (0, 1):
-            eng.set_option("k2y_first", first)
-            eng.set_option("k2_sorted", srt)
-            eng.refresh_hot_values(now, now)
-            assert np.array_equal(eng.hot_values(), ref), (first, srt)
-    eng.set_option("k2y_first", 6)
+    for srt in (0, 1):  # the ordered and the stamp path
+        eng.set_option("k2_sorted", srt)
+        eng.refresh_hot_values(now, now)
+        assert np.array_equal(eng.hot_values(), ref), srt
     eng.set_option("k2_form", 1)
     eng.refresh_hot_values(now, now)
     assert np.array_equal(eng.hot_values(), ref)

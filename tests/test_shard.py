@@ -149,3 +149,25 @@ def test_key_packing_tiebreak():
     assert k[2] == -1
     node, score = shard.unpack_keys(k)
     assert node.tolist() == [5, 3, -1, 4_000_000_000] and score.tolist() == [90, 90, -1, 100]
+
+
+def test_c_shard_range_matches():
+    """crane_shard_range (the group's split, group.cpp) equals shard.shard_range."""
+    cd = pytest.importorskip("crane_dyn")
+    for n in (0, 1, 7, 100, 1_000_001, 2**32 - 1):
+        for w in (1, 2, 3, 7, 8):
+            for r in range(w):
+                assert cd.shard_range(n, w, r) == shard.shard_range(n, w, r)
+    with pytest.raises(cd.CraneError):
+        cd.shard_range(10, 0, 0)
+    with pytest.raises(cd.CraneError):
+        cd.shard_range(10, 2, 2)
+
+
+def test_group_without_gpu_fails_cleanly():
+    cd = pytest.importorskip("crane_dyn")
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(cd.CraneError):
+        cd.Group(cd.Policy(cd.default_policy_spec()), devices=[0])

@@ -24,29 +24,16 @@ def _check(spec, c, now, ds):
     off, osc, och = oracle_soa(spec, c, now=now, ds=ds)
     # K3s from the producers' per-tile rows, and searching the records itself; K1's
     # one-step records through its LDS staging, through st.stage always (cap 0), or
-    # per block as its counts exceed a small cap; the node pass fused with the step
-    # tables (split 0) or as the split form (count pass + k3a_emit, split 1)
-    # the middle pieces raw or cut into elementary ones (step_pieces 1: whenever it pays); the
-    # split form's k3a_emit as wide as the block (emit 0) or one wave per block (emit 64); the
-    # split form's count pass the default kernel (cf 0), the persistent one that prefetches the
-    # next block's rows into LDS (cf 4, k1_count_pf) or the streamed one without records, whose
-    # stepped records k3a_emit rebuilds from the SoA (cf 5 / 6 / 7, k1_count_stream), writes itself
-    # (cf 8 / 9) or emits itself (cf 10 / 11: k3a_emit only sorts)
-    for rows, cap, split, pc, em, cf in ((1, 1 << 30, 0, 0, 0, 0), (0, 1 << 30, 0, 0, 0, 0), (1, 0, 0, 1, 0, 0),
-                                         (0, 6, 0, 0, 0, 0), (1, 6, 0, 1, 0, 0), (1, 1 << 30, 1, 1, 0, 0),
-                                         (0, 6, 1, 0, 0, 0), (1, 0, 1, 2, 0, 0), (1, 1 << 30, 0, 1, 0, 0),
-                                         (1, 1 << 30, 1, 1, 64, 0), (0, 6, 1, 0, 64, 0), (1, 1 << 30, 1, 0, 64, 0),
-                                         (1, 1 << 30, 1, 1, 64, 4), (0, 6, 1, 0, 0, 4), (1, 0, 1, 2, 64, 4),
-                                         (1, 1 << 30, 1, 1, 64, 6), (0, 6, 1, 0, 0, 5), (1, 0, 1, 2, 64, 7),
-                                         (1, 1 << 30, 1, 1, 64, 8), (0, 6, 1, 0, 0, 9), (1, 1 << 30, 1, 1, 64, 10),
-                                         (0, 6, 1, 0, 0, 11), (1, 0, 1, 2, 64, 10)):
-        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap, "k1_split": split, "step_pieces": pc,
-                                        "emit_threads": em, "k1_count_form": cf})
+    # per block as its counts exceed a small cap; the middle pieces raw or cut into elementary
+    # ones (step_pieces 1 always, 0 when it pays, 2 never)
+    for rows, cap, pc in ((1, 1 << 30, 0), (0, 1 << 30, 0), (1, 0, 1), (0, 6, 0), (1, 6, 1), (1, 1 << 30, 1),
+                          (1, 0, 2)):
+        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap, "step_pieces": pc})
         _, _, ch, cs = eng.eval(now, ds)
-        assert np.array_equal(ch, och), (rows, cap, split, pc, em, cf)
+        assert np.array_equal(ch, och), (rows, cap, pc)
         for p in range(len(now)):
             ok = (off[p] < 0) | bool(ds[p])
-            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, split, pc, em, cf, p)
+            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, pc, p)
         eng.close()
 
 
@@ -126,145 +113,28 @@ def test_step_policy_shapes():
         _check(spec, c, c.now, c.ds)
 
 
-def test_step_split_auto_at_large_n():
-    """Past one round of resident workgroups the node pass splits by itself (auto): 400k
-    nodes, the split form's keys equal the fused form's and the per-pair kernel's."""
+def test_step_at_large_n():
+    """Past one round of resident workgroups (400k nodes): the fused node pass's keys equal the
+    per-pair kernel's."""
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 400_000, 1500, seed=30, pod_step_ns=4_000_000, ds_frac=0.02)
     out = []
-    for opts in ({"k1_split": 2}, {"k1_split": 0}, {"keys_path": 1}, {"k1_split": 2, "k1_count_form": 4},
-                 {"k1_split": 2, "k1_count_form": 6, "emit_threads": 64},
-                 {"k1_split": 2, "k1_count_form": 8, "emit_threads": 64},
-                 {"k1_split": 2, "k1_count_form": 10, "emit_threads": 64}):
+    for opts in ({}, {"keys_path": 1}):
         eng = engine_for(spec, c, opts=opts)
-        eng.set_profiling(True)
         _, _, ch, cs = eng.eval(c.now, c.ds)
-        names = [n for n, _ in eng.stage_times()]
-        if opts.get("k1_split") == 2:
-            assert "k3a_emit" in names and "k1_node_pass+k3a_count" in names, names
         out.append((ch, cs))
         eng.close()
-    for ch, cs in out[1:]:
-        assert np.array_equal(ch, out[0][0]) and np.array_equal(cs, out[0][1])
+    assert np.array_equal(out[1][0], out[0][0]) and np.array_equal(out[1][1], out[0][1])
 
 
-def test_step_matches_pair_keys():
-    """Same keys from the step path and the per-pair kernel (matrix.hip)."""
-    spec = cd.default_policy_spec()
-    c = synth.make_cluster(spec, 30000, 3000, seed=23, pod_step_ns=5_000_000)
-    eng = engine_for(spec, c)
-    _, _, ch5, cs5 = eng.eval(c.now, c.ds)
-    eng.set_option("keys_path", 1)
-    _, _, ch4, cs4 = eng.eval(c.now, c.ds)
-    assert np.array_equal(ch5, ch4) and np.array_equal(cs5, cs4)
-
-
-def test_step_fused_and_standalone_agree():
-    """First eval after an upload fuses the node pass with the step tables (K1 STEP
-    form); a second eval rebuilds them from the stored records (K3a).  Both match."""
-    spec = cd.default_policy_spec()
-    c = synth.make_cluster(spec, 9000, 2000, seed=24, pod_step_ns=40_000_000, ds_frac=0.03)
-    eng = engine_for(spec, c)
-    _, _, ch1, cs1 = eng.eval(c.now, c.ds)      # K3p -> K1+K3a -> K3s
-    _, _, ch2, cs2 = eng.eval(c.now, c.ds)      # K3p -> K3a -> K3s
-    _, _, och = oracle_soa(spec, c, want_matrix=False)
-    assert np.array_equal(ch1, och) and np.array_equal(ch2, och) and np.array_equal(cs1, cs2)
-
-
-def _oracle_hv(spec, c, now_ns):
-    from oracle import oracle as O
-    _, hv = O.hot_values(spec, c.b_node, c.b_ts, c.n_nodes, now_ns // 10**9)
-    return hv.astype(np.float64), np.full(c.n_nodes, now_ns, np.int64)
-
-
-def test_step_replayed_batches_with_binding_log():
-    """The bench's step (K2 refresh -> keys-only eval) replayed on one stream: K1
-    consumes the K2 buckets and zeroes K2's bin cursors in-stream, so every
-    replay must give the oracle's choices with hot values from the log."""
-    import torch
-    spec = cd.default_policy_spec()
-    c = synth.make_cluster(spec, 20000, 3000, n_bindings=200_000, seed=25, pod_step_ns=3_000_000)
-    eng = engine_for(spec, c)
-    eng.upload_bindings(c.b_node, c.b_ts)
-    now = int(synth.NOW0_NS)
-    dev = torch.device("cuda", 0)
-    st = torch.cuda.Stream(dev)
-    d_now = torch.from_numpy(c.now).to(dev)
-    d_flags = torch.from_numpy(c.ds).to(dev)
-    d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
-    _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=_oracle_hv(spec, c, now))
-    with torch.cuda.stream(st):
-        for rep in range(4):
-            eng.refresh_hot_values_async(now, now, st.cuda_stream)
-            eng.eval_keys_async(d_now, d_flags, d_keys, st.cuda_stream)
-            st.synchronize()
-            ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
-            assert np.array_equal(ch, och), rep
-
-
-def test_hot_values_kept_after_consumption():
-    """After the node pass has consumed the K2 buckets, a later node pass (records
-    made stale by greedy) still sees the refreshed binding-log hot values."""
-    spec = cd.default_policy_spec()
-    c = synth.make_cluster(spec, 3000, 500, n_bindings=40_000, seed=26, pod_step_ns=0)
-    eng = engine_for(spec, c)
-    eng.upload_bindings(c.b_node, c.b_ts)
-    now = int(c.now[0])
-    eng.refresh_hot_values(now, now)
-    _, _, ch1, _ = eng.eval(c.now, c.ds)          # consumes the counts
-    eng.greedy(50, now, c.ds[:50])                # refreshes at the same now, leaves records stale
-    ff, sc, ch2, _ = eng.eval(c.now, c.ds, matrix=True)   # K1 again from the kept hot values (pair kernel)
-    off, osc, och = oracle_soa(spec, c, hv_override=_oracle_hv(spec, c, now))
-    assert np.array_equal(ch1, och) and np.array_equal(ch2, och)
-    assert np.array_equal(ff, off) and np.array_equal(sc, osc)
-
-
-@pytest.mark.parametrize("ride,pods", [(1, 5000), (0, 5000), (1, 1), (1, 300), (1, 2048)])
-def test_step_keys_async_matches_oracle(ride, pods):
-    """crane_dyn_step_keys_async replayed (K3p riding in K2x's launch or in its own):
-    each step equals the oracle with binding-log hot values; with kernel timing on
-    too (dispatch-stamped events name every kernel of the step)."""
-    import torch
-    spec = cd.default_policy_spec()
-    c = synth.make_cluster(spec, 30000, pods, n_bindings=300_000, seed=27, pod_step_ns=2_000_000, ds_frac=0.02)
-    eng = engine_for(spec, c, opts={"k3p_in_k2": ride})
-    eng.upload_bindings(c.b_node, c.b_ts)
-    now = int(synth.NOW0_NS)
-    dev = torch.device("cuda", 0)
-    st = torch.cuda.Stream(dev)
-    d_now = torch.from_numpy(c.now).to(dev)
-    d_flags = torch.from_numpy(c.ds).to(dev)
-    d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
-    _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=_oracle_hv(spec, c, now))
-    with torch.cuda.stream(st):
-        for rep in range(4):
-            eng.set_profiling(rep == 3)
-            eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
-            st.synchronize()
-            ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
-            assert np.array_equal(ch, och), rep
-    times = eng.stage_times()
-    names = [n for n, _ in times]
-    if ride:
-        assert names == ["k2x_dedupe+k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
-    else:
-        assert names == ["k2x_dedupe", "k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
-    assert all(0 < t < 50 for _, t in times), times
-
-
-@pytest.mark.parametrize("split", [0, 1, 4, 6, 8, 10], ids=["fused", "split", "split-prefetch", "split-stream",
-                                                             "split-stream-rec", "split-stream-emit"])
 @pytest.mark.parametrize("k2", [0, 1, 2, 3], ids=["dedupe", "binned", "hash", "large"])
-def test_step_keys_async_k2_forms(k2, split):
+def test_step_keys_async_k2_forms(k2):
     """The combined step with each K2 form (dedupe: counts consumed by the fused node
-    pass from per-block entries; binned / hash / large: buckets) equals the oracle, replayed,
-    with the node pass fused with the step tables or split (count pass + k3a_emit; the count
-    pass prefetching the next block's rows into LDS: k1_count_form 4, or streamed without records:
-    6; the dedupe form's entries route both to the default count pass)."""
+    pass from per-block entries; binned / hash / large: buckets) equals the oracle, replayed."""
     import torch
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 20000, 3000, n_bindings=400_000, seed=29, pod_step_ns=2_000_000, ds_frac=0.03)
-    eng = engine_for(spec, c, opts={"k2_form": k2, "k1_split": min(split, 1), "k1_count_form": split if split > 1 else 0})
+    eng = engine_for(spec, c, opts={"k2_form": k2})
     eng.upload_bindings(c.b_node, c.b_ts)
     now = int(synth.NOW0_NS)
     dev = torch.device("cuda", 0)
@@ -281,7 +151,7 @@ def test_step_keys_async_k2_forms(k2, split):
             ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
             assert np.array_equal(ch, och), rep
     names = [n for n, _ in eng.stage_times()]
-    assert ("k1_node_pass+k3a_count" in names and "k3a_emit" in names) == bool(split), names
+    assert "k1_node_pass+k3a_steps" in names, names
 
 
 @pytest.mark.parametrize("keep", [0, 1])
