@@ -465,10 +465,11 @@ def _dropin_files(d, spec, ann, now, ds):
 
 
 def _replay_chosen(cd, spec, c, dev_index, now, ds, log_path, oracle_pods=()):
-    """Every pod's chosen node recomputed on the churned annotations: the harness's patch log
-    applied to the snapshot's SoA pod by pod, then one engine holding the whole patched
-    snapshot (a full upload per pod, no incremental path) evaluates the pod; for the pods in
-    `oracle_pods` the CPU oracle too.  Returns (chosen [P], oracle agreement or None)."""
+    """Every pod's chosen node recomputed on the churned cluster: the harness's log (annotation
+    patches, nodes joining "J" and leaving "L", by creation index) applied to the snapshot's SoA pod
+    by pod, then one engine holding the live nodes in the snapshot's list order (a full upload per
+    pod, no incremental path) evaluates the pod; for the pods in `oracle_pods` the CPU oracle too.
+    Returns (chosen creation index [P], oracle agreement or None)."""
     from oracle import oracle as O
     eng = cd.Engine(cd.Policy(spec), dev_index)
     names = eng.metric_names
@@ -476,26 +477,43 @@ def _replay_chosen(cd, spec, c, dev_index, now, ds, log_path, oracle_pods=()):
     val, ts = val.copy(), ts.copy()
     hv, hv_ts = c.hv.copy(), c.hv_ts.copy()
     row = {n: i for i, n in enumerate(names)}
-    log = {}
+    events = {}
     with open(log_path) as f:
         for ln in f:
-            p, n, k, v = ln.rstrip("\n").split("\t")
-            log.setdefault(int(p), []).append((int(n), k, v))
+            t = ln.rstrip("\n").split("\t")
+            if t[0] in ("J", "L"):
+                events.setdefault(int(t[1]), []).append((t[0], int(t[2]), None, None))
+            else:
+                events.setdefault(int(t[0]), []).append(("P", int(t[1]), t[2], t[3]))
+    live = list(range(c.n_nodes))
     chosen, ok_oracle = [], []
     for p in range(len(now)):
-        for n, k, v in log.get(p, ()):
-            x, t = cd.parse_annotation(v, synth_shanghai())
-            if k == "node_hot_value":
-                hv[n], hv_ts[n] = x, t
-            elif k in row:
-                val[row[k], n], ts[row[k], n] = x, t
-        eng.upload_nodes(val, ts, hv, hv_ts)
+        for kind, n, k, v in events.get(p, ()):
+            if kind == "J":
+                if n >= val.shape[1]:  # room for the joining node: no annotations until its patches
+                    extra = n + 1 - val.shape[1]
+                    val = np.concatenate([val, np.zeros((len(names), extra))], axis=1)
+                    ts = np.concatenate([ts, np.full((len(names), extra), cd.CRANE_TS_INVALID, np.int64)], axis=1)
+                    hv = np.concatenate([hv, np.zeros(extra)])
+                    hv_ts = np.concatenate([hv_ts, np.full(extra, cd.CRANE_TS_INVALID, np.int64)])
+                live.append(n)
+            elif kind == "L":
+                live.remove(n)
+            else:
+                x, t = cd.parse_annotation(v, synth_shanghai())
+                if k == "node_hot_value":
+                    hv[n], hv_ts[n] = x, t
+                elif k in row:
+                    val[row[k], n], ts[row[k], n] = x, t
+        ids = np.array(live, np.int64)
+        lv, lt, lh, lht = val[:, ids], ts[:, ids], hv[ids], hv_ts[ids]
+        eng.upload_nodes(lv, lt, lh, lht)
         ch = int(eng.eval(now[p:p + 1], ds[p:p + 1])[2][0])
-        chosen.append(ch)
+        chosen.append(int(ids[ch]) if ch >= 0 else -1)
         if p in oracle_pods:
-            okm = (ts != cd.CRANE_TS_INVALID).astype(np.uint8)
-            _, _, och = O.eval_soa(spec, names, okm, val, np.where(okm == 1, ts, 0),
-                                   (hv_ts != cd.CRANE_TS_INVALID).astype(np.uint8), hv, hv_ts, now[p:p + 1],
+            okm = (lt != cd.CRANE_TS_INVALID).astype(np.uint8)
+            _, _, och = O.eval_soa(spec, names, okm, lv, np.where(okm == 1, lt, 0),
+                                   (lht != cd.CRANE_TS_INVALID).astype(np.uint8), lh, lht, now[p:p + 1],
                                    ds[p:p + 1], threads=16, want_matrix=False)
             ok_oracle.append(int(och[0]) == ch)
     eng.close()
@@ -522,15 +540,25 @@ def dropin_leg(cd, spec, c, ann, now, ds, threads, dev_index, cpu_pods=0):
     with tempfile.TemporaryDirectory() as d:
         pp, sp, pd = _dropin_files(d, spec, ann, now, ds)
         runs, chosen = {}, {}
-        for label, scale in (("churn_x1", 1.0), ("churn_x10", 10.0), ("frozen", 0.0)):
+        # nodes_and_time: pods 1 s apart (255 s of pod time: past any one-minute table span) at the
+        # controller's rate, a node joining every 8th cycle and one leaving in between
+        now_long = now[0] + np.arange(len(now), dtype=np.int64) * 10**9
+        pd_long = os.path.join(d, "pods_long.tsv")
+        with open(pd_long, "w") as f:
+            for p in range(len(now)):
+                f.write(f"P\tpod-{p}\t{int(now_long[p])}\t{int(ds[p])}\n")
+        for label, scale, ev, pods_f, pnow in (("churn_x1", 1.0, 0, pd, now), ("churn_x10", 10.0, 0, pd, now),
+                                               ("frozen", 0.0, 0, pd, now),
+                                               ("nodes_and_time", 1.0, 8, pd_long, now_long)):
             lp = os.path.join(d, f"{label}.log")
-            cmd = [DROPIN, pp, sp, pd, "--threads", str(threads), "--churn", str(scale), "--churn-log", lp]
+            cmd = [DROPIN, pp, sp, pods_f, "--threads", str(threads), "--churn", str(scale), "--churn-log", lp,
+                   "--node-events", str(ev)]
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
             if r.returncode != 0:
                 return {"error": f"{label}: {r.stderr[-500:]}"}
             o = json.loads(r.stdout.strip().splitlines()[-1])
             ch = chosen[label] = np.array(o.pop("chosen"))
-            ref, orc = _replay_chosen(cd, spec, c, dev_index, now, ds, lp,
+            ref, orc = _replay_chosen(cd, spec, c, dev_index, pnow, ds, lp,
                                       oracle_pods=(0, len(now) // 2, len(now) - 1))
             o["matches_engine_chosen"] = bool(np.array_equal(ch, ref))
             o["matches_oracle_sample"] = orc
@@ -554,6 +582,7 @@ def dropin_leg(cd, spec, c, ann, now, ds, threads, dev_index, cpu_pods=0):
                                         "filter_fanout_ms_median", "score_fanout_ms_median", "select_ms_median",
                                         "pool_noop_ms_median", "patches", "simulated_s", "cycles_with_patches",
                                         "tables_built", "full_syncs", "incremental_syncs", "nodes_updated",
+                                        "nodes_joined", "nodes_left", "shard_grows", "slowest",
                                         "errors", "sync_ms", "matches_engine_chosen", "matches_oracle_sample")}
     out["how"] = ("each patch publishes a new Node object (informer); the plugin compares every NodeInfo with the "
                   "one it parsed at the cycle's first call, re-parses only the changed nodes, scatters them into the "

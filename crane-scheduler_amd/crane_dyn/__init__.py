@@ -102,6 +102,7 @@ def _load():
                                                   vp]),
         "crane_dyn_version": (C.c_char_p, []),
         "crane_dyn_forget_stream": (C.c_int, [vp, vp]),
+        "crane_dyn_resize_nodes": (C.c_int, [vp, C.c_int64]),
         "crane_shard_range": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, P(C.c_int64), P(C.c_int64)]),
         "crane_dyn_group_create": (C.c_int, [P(_CPolicy), C.c_int32, vp, C.c_int32, P(vp)]),
         "crane_dyn_group_destroy": (C.c_int, [vp]),
@@ -139,7 +140,7 @@ ABI_SYMBOLS = (
     "crane_tz_load", "crane_tz_load_bytes", "crane_tz_free", "crane_tz_lookup", "crane_tz_date",
     "crane_parse_annotation_tz", "crane_parse_annotations_tz", "crane_dyn_step_slots", "crane_dyn_node_steps",
     "crane_dyn_node_steps_subset", "crane_dyn_update_nodes", "crane_dyn_update_node_steps",
-    "crane_dyn_forget_stream", "crane_shard_range", "crane_dyn_group_create", "crane_dyn_group_destroy",
+    "crane_dyn_forget_stream", "crane_dyn_resize_nodes", "crane_shard_range", "crane_dyn_group_create", "crane_dyn_group_destroy",
     "crane_dyn_group_last_error", "crane_dyn_group_set_option", "crane_dyn_group_size", "crane_dyn_group_shard",
     "crane_dyn_group_engine", "crane_dyn_group_upload_nodes", "crane_dyn_group_upload_bindings",
     "crane_dyn_group_step_keys_async", "crane_dyn_group_sync", "crane_dyn_group_schedule",
@@ -592,6 +593,11 @@ class Engine:
             hv = np.ascontiguousarray(hv, np.float64).reshape(k)
             hv_ts = np.ascontiguousarray(hv_ts, np.int64).reshape(k)
         self._check(lib.crane_dyn_update_nodes(self.h, k, _ptr(idx), _ptr(val), _ptr(ts), _ptr(hv), _ptr(hv_ts)))
+
+    def resize_nodes(self, n):
+        """Grow / shrink the shard to n nodes (crane_dyn_resize_nodes): new nodes have no annotations."""
+        self._check(lib.crane_dyn_resize_nodes(self.h, int(n)))
+        self.n_nodes = int(n)
 
     def update_node_steps(self, idx, val, ts, hv, hv_ts, t0_ns, t1_ns):
         """update_nodes + node_steps_subset of the same nodes in one call (crane_dyn_update_node_steps)."""

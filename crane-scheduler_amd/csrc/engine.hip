@@ -1368,6 +1368,69 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
     return CRANE_OK;
 }
 
+// Grow or shrink the shard to n nodes in place: nodes [0, min(N, n)) keep their parsed columns,
+// nodes past the old count start with no annotations (every metric and the hot value missing);
+// records are rebuilt by the next pass that needs them.  (The drop-in plugin adds joining nodes
+// this way and then writes their columns with crane_dyn_update_node_steps.)
+int crane_dyn_resize_nodes(crane_dyn* h, int64_t n) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before resizing the shard");
+    if (n < 0 || n > 0xFFFFFFFFLL || h->node_offset + n > 0xFFFFFFFFLL)
+        return h->fail(CRANE_E_INVALID, "node count out of range (global indices must fit 32 bits)");
+    if (n == h->N) return CRANE_OK;
+    HIPTRY(h, hipSetDevice(h->device));
+    if (int rc = quiesce(h)) return rc;
+    const int64_t M = h->dp.n_slots, keep = std::min(h->N, n), N0 = h->N;
+    DevBuf<double> val, hv;
+    DevBuf<int64_t> ts, hv_ts;
+    auto fail = [&](hipError_t e, const char* what) {
+        val.release(); ts.release(); hv.release(); hv_ts.release();
+        return h->hipfail(e, what);
+    };
+    hipError_t e = val.reserve((size_t)(M * n));
+    if (e == hipSuccess) e = ts.reserve((size_t)(M * n));
+    if (e == hipSuccess) e = hv.reserve((size_t)n);
+    if (e == hipSuccess) e = hv_ts.reserve((size_t)n);
+    if (e != hipSuccess) return fail(e, "resize: hipMalloc");
+    hipStream_t st = h->stream;
+    if (M > 0 && keep > 0) {
+        e = hipMemcpy2DAsync(val.p, sizeof(double) * n, h->val.p, sizeof(double) * N0, sizeof(double) * keep, M,
+                             hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess)
+            e = hipMemcpy2DAsync(ts.p, sizeof(int64_t) * n, h->ts.p, sizeof(int64_t) * N0, sizeof(int64_t) * keep, M,
+                                 hipMemcpyDeviceToDevice, st);
+    }
+    for (int64_t m = 0; m < M && n > keep && e == hipSuccess; ++m) {
+        e = hipMemsetAsync(val.p + m * n + keep, 0, sizeof(double) * (size_t)(n - keep), st);
+        if (e == hipSuccess) e = launch_fill_i64(ts.p + m * n + keep, n - keep, kTsInvalid, st);
+    }
+    if (h->have_hv && keep > 0 && e == hipSuccess) {
+        e = hipMemcpyAsync(hv.p, h->hv.p, sizeof(double) * (size_t)keep, hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(hv_ts.p, h->hv_ts.p, sizeof(int64_t) * (size_t)keep, hipMemcpyDeviceToDevice, st);
+    }
+    if (h->have_hv && n > keep && e == hipSuccess) {
+        e = hipMemsetAsync(hv.p + keep, 0, sizeof(double) * (size_t)(n - keep), st);
+        if (e == hipSuccess) e = launch_fill_i64(hv_ts.p + keep, n - keep, kTsInvalid, st);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return fail(e, "resize: copy");
+    std::swap(h->val, val);
+    std::swap(h->ts, ts);
+    std::swap(h->hv, hv);
+    std::swap(h->hv_ts, hv_ts);
+    val.release(); ts.release(); hv.release(); hv_ts.release();
+    HIPTRY(h, h->rec.reserve((size_t)n * h->rec_bytes));
+    h->N = n;
+    h->buckets_zero = false;
+    h->hv_from_counts = false;  // binding-log hot values were per old node index
+    h->counts_pending = false;
+    h->hx_pending = false;
+    h->rec_dirty = true;
+    return CRANE_OK;
+}
+
 int crane_dyn_update_nodes(crane_dyn* h, int64_t k, const int64_t* idx, const double* val, const int64_t* ts,
                            const double* hv, const int64_t* hv_ts) {
     if (!h) return CRANE_E_INVALID;

@@ -164,6 +164,13 @@ int crane_dyn_upload_nodes(crane_dyn *h, int64_t n_nodes, int64_t node_offset,
  * of those nodes is all a table of answers needs.  Synchronous. */
 int crane_dyn_update_nodes(crane_dyn *h, int64_t k, const int64_t *idx, const double *val, const int64_t *ts_ns,
                            const double *hv, const int64_t *hv_ts_ns);
+/* Grow or shrink the shard to n nodes in place (global indices node_offset + i as before): nodes
+ * [0, min(N, n)) keep their parsed annotations, new ones start with none (every metric and the hot
+ * value missing) until crane_dyn_update_nodes writes them; hot values from the binding log revert to
+ * the annotations, as after crane_dyn_upload_nodes.  The drop-in plugin grows its shard this way when
+ * nodes join the cluster (the reference looks a node up per call, plugins.go:45-50,74-84: a new node
+ * costs it nothing either). */
+int crane_dyn_resize_nodes(crane_dyn *h, int64_t n);
 /* crane_dyn_update_nodes and crane_dyn_node_steps_subset of the same nodes over [t0, t1) in one
  * call: one launch writes the columns, the records and the rows (one round trip to the device). */
 int crane_dyn_update_node_steps(crane_dyn *h, int64_t k, const int64_t *idx, const double *val, const int64_t *ts_ns,

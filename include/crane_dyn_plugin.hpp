@@ -297,13 +297,16 @@ class DynamicScheduler {
 
     // host threads of the full-snapshot annotation parse (<= 0: all hardware threads)
     void SetParseThreads(int32_t n) { parse_threads_ = n; }
-    // time span one answer table covers (a pod later than it gets a new table)
-    void SetHorizon(int64_t ns) { horizon_ns_ = ns > 0 ? ns : 1; }
-    // work done so far: full tables built (a new node set or horizon), full snapshot parses,
-    // cycles that found changed nodes, and the changed nodes re-parsed over them
-    // (sync_ns: wall time of the cycles' syncs, scan + update, as their leaders saw it)
+    // time span one answer table covers from the pod that builds it (a later pod gets a new
+    // table); by default (and ns <= 0) the whole time axis, which never needs a new table
+    void SetHorizon(int64_t ns) { horizon_ns_ = ns > 0 ? ns : kAllTime; }
+    // work done so far: full tables built (the first sync, a finite horizon passed), full snapshot
+    // parses, cycles that found changed or joining nodes and the rows re-parsed over them, nodes
+    // that joined / left, times the shard grew (sync_ns: wall time of the cycles' syncs, scan +
+    // update, as their leaders saw it)
     struct Counters {
-        uint64_t tables_built = 0, full_syncs = 0, incremental_syncs = 0, nodes_updated = 0, sync_ns = 0;
+        uint64_t tables_built = 0, full_syncs = 0, incremental_syncs = 0, nodes_updated = 0, sync_ns = 0,
+                 nodes_joined = 0, nodes_left = 0, grows = 0;
     };
     Counters counters() const {
         std::lock_guard<std::mutex> g(mu_);
@@ -315,24 +318,49 @@ class DynamicScheduler {
                                                                                          const Handle& h);
 
    private:
-    // The synced node set (List() order) and every node's answers over [t0, t1).
+    // The synced node set and every node's answers.  Rows are the engine's node indices: a node
+    // keeps its row while it stays in the snapshot; a node that leaves frees its row (never read
+    // again) and a joining node takes a free row, or the shard grows (crane_dyn_resize_nodes) —
+    // the reference looks a node up per call (plugins.go:45-50,74-84), so a node set change costs
+    // it nothing, and here it costs the joining nodes' rows.  The answers cover [t0, t1): by
+    // default the whole time axis (every expiry of a node fits its row), so no pod time ever
+    // needs a new table.
     struct View {
-        std::vector<const NodeInfo*> infos;  // the snapshot's NodeInfo objects
-        std::vector<const Node*> nodes;      // the Node object each row was parsed from
+        std::vector<const NodeInfo*> infos;  // row -> the snapshot's NodeInfo (null: a free row)
+        std::vector<const Node*> nodes;      // row -> the Node object the row was parsed from
         std::vector<int64_t> gens;           // ... and its NodeInfo's Generation
+        std::vector<uint32_t> seen;          // row -> the last snapshot scan that found its NodeInfo
+        std::vector<int64_t> free_rows;      // (popped from the back: lowest row first)
+        size_t live = 0;
         std::unordered_map<std::string, int64_t, NameHash> by_name;
-        AddrIndex info_idx;  // NodeInfo address -> index (fixed for the node set)
-        AddrIndex name_idx;  // address of a node's Name -> index (entries added as Nodes are replaced)
+        AddrIndex info_idx;  // NodeInfo address -> row (a stale entry is rejected against infos)
+        AddrIndex name_idx;  // address of a node's Name -> row (entries added as Nodes are replaced)
         int64_t t0 = 0, t1 = 0;
         size_t S = 0;
         std::vector<uint8_t> n_steps;
         std::vector<int64_t> bp;
         std::vector<int8_t> first_fail, score;
 
+        size_t rows() const { return infos.size(); }
+        void grow(size_t n) {
+            infos.resize(n, nullptr);
+            nodes.resize(n, nullptr);
+            gens.resize(n, 0);
+            seen.resize(n, 0);
+            n_steps.resize(n, 0);
+            bp.resize(n * S, 0);
+            first_fail.resize(n * (S + 1), 0);
+            score.resize(n * (S + 1), 0);
+        }
+        void index_infos() {
+            info_idx.reset(rows());
+            for (size_t i = 0; i < rows(); ++i)
+                if (infos[i]) info_idx.put(infos[i], (int64_t)i);
+        }
         void index_names() {
-            name_idx.reset(nodes.size());
-            for (size_t i = 0; i < nodes.size(); ++i)
-                if (nodes[i]) name_idx.put(&nodes[i]->Name, (int64_t)i);
+            name_idx.reset(rows());
+            for (size_t i = 0; i < rows(); ++i)
+                if (infos[i] && nodes[i]) name_idx.put(&nodes[i]->Name, (int64_t)i);
         }
         // index of node i's value at time t (t0 <= t < t1)
         size_t piece(int64_t i, int64_t t) const {
@@ -342,17 +370,19 @@ class DynamicScheduler {
             while (j < nb && b[j] <= t) ++j;
             return (size_t)i * (S + 1) + j;
         }
-        // The framework walks the nodes in List() order in chunks per goroutine: the entry after
+        // The framework walks the nodes in List() order in chunks per goroutine: the row after
         // this thread's last one (or a few further, for the feasible list) first — a pointer
-        // compare — then the address index, then the name.
+        // compare; rows follow List() order until nodes join or leave —, then the address index,
+        // then the name.
         int64_t find_info(const NodeInfo* ni, const Node* node) const {
             thread_local const View* lv = nullptr;
             thread_local int64_t last = -1;
-            const int64_t n = (int64_t)infos.size();
+            const int64_t n = (int64_t)rows();
             if (lv == this)
                 for (int64_t i = last + 1; i < std::min(n, last + 5); ++i)
                     if (infos[(size_t)i] == ni) return last = i;
             int64_t i = info_idx.get(ni);
+            if (i >= 0 && infos[(size_t)i] != ni) i = -1;  // a departed NodeInfo's entry
             if (i < 0) {  // a NodeInfo object that is not the snapshot's: by name
                 auto it = by_name.find(node->Name);
                 i = it == by_name.end() ? -1 : it->second;
@@ -364,12 +394,13 @@ class DynamicScheduler {
         int64_t find_name(const std::string& name) const {
             thread_local const View* lv = nullptr;
             thread_local int64_t last = -1;
-            const int64_t n = (int64_t)nodes.size();
+            const int64_t n = (int64_t)rows();
+            auto mine = [&](int64_t i) { return infos[(size_t)i] && nodes[(size_t)i] && &nodes[(size_t)i]->Name == &name; };
             if (lv == this)
                 for (int64_t i = last + 1; i < std::min(n, last + 5); ++i)
-                    if (nodes[(size_t)i] && &nodes[(size_t)i]->Name == &name) return last = i;
+                    if (mine(i)) return last = i;
             int64_t i = name_idx.get(&name);
-            if (i >= 0 && !(nodes[(size_t)i] && &nodes[(size_t)i]->Name == &name)) i = -1;  // a replaced Node's
+            if (i >= 0 && !mine(i)) i = -1;  // a replaced or departed Node's
             if (i < 0) {
                 auto it = by_name.find(name);
                 i = it == by_name.end() ? -1 : it->second;
@@ -418,17 +449,16 @@ class DynamicScheduler {
         return rc == 0;
     }
 
-    // every node's answers over [now, now + horizon) into v (sized for its node set)
-    // (the horizon [t0, t1) is recorded only once the rows hold it: on a failure the caller
-    // drops the View, so no later cycle answers from rows of another horizon)
+    // every row's answers over the table's span into v: the whole time axis by default, else
+    // [now, now + horizon).  (The span is recorded only once the rows hold it: on a failure the
+    // caller drops the View, so no later cycle answers from rows of another span.)
     bool build_table(View* v, int64_t now, std::string* err) {
-        const size_t N = v->infos.size();
-        const int64_t t0 = now, t1 = now > INT64_MAX - horizon_ns_ ? INT64_MAX : now + horizon_ns_;
-        v->S = (size_t)crane_dyn_step_slots(eng_);
-        v->n_steps.resize(N);
-        v->bp.resize(N * v->S);
-        v->first_fail.resize(N * (v->S + 1));
-        v->score.resize(N * (v->S + 1));
+        const size_t N = v->rows();
+        int64_t t0 = INT64_MIN, t1 = INT64_MAX;
+        if (horizon_ns_ != kAllTime) {
+            t0 = now;
+            t1 = now > INT64_MAX - horizon_ns_ ? INT64_MAX : now + horizon_ns_;
+        }
         if (crane_dyn_node_steps(eng_, t0, t1, (int64_t)N, v->n_steps.data(), v->bp.data(), v->first_fail.data(),
                                  v->score.data())) {
             *err = crane_dyn_last_error(eng_);
@@ -440,21 +470,22 @@ class DynamicScheduler {
         return true;
     }
 
-    // a new node set: parse the whole snapshot, upload it, index it, build the table
+    // the first sync (or a change of most of the node set): parse the whole snapshot, upload it,
+    // index it, build the table
     std::shared_ptr<View> full_sync(const std::vector<const NodeInfo*>& L, int64_t now, std::string* err) {
         auto v = std::make_shared<View>();
         const size_t N = L.size();
-        v->infos = L;
-        v->nodes.resize(N);
-        v->gens.resize(N);
+        v->S = (size_t)crane_dyn_step_slots(eng_);
+        v->grow(N);
         v->by_name.reserve(N);
-        v->info_idx.reset(N);
         for (size_t i = 0; i < N; ++i) {
+            v->infos[i] = L[i];
             v->nodes[i] = L[i]->node();
             v->gens[i] = L[i]->Generation;
-            v->info_idx.put(L[i], (int64_t)i);
             if (v->nodes[i]) v->by_name.emplace(v->nodes[i]->Name, (int64_t)i);
         }
+        v->live = N;
+        v->index_infos();
         v->index_names();
         std::vector<double> val;
         std::vector<int64_t> ts;
@@ -470,14 +501,60 @@ class DynamicScheduler {
         return v;
     }
 
-    // the changed nodes: re-parse, scatter into the engine, rebuild their table rows.  The View
-    // records the new Node objects only once the engine holds them: a failed call leaves the
-    // nodes marked changed (and the caller drops the View: the next cycle resyncs in full).
+    // Nodes that left give their rows back; joining nodes take free rows (the shard grows by an
+    // eighth when none is left) and join the changed rows, whose columns update() writes.
+    bool membership(View* v, const std::vector<const NodeInfo*>& L, std::string* err) {
+        for (int64_t r : removed_) {
+            const Node* n = v->nodes[(size_t)r];
+            if (n) {
+                auto it = v->by_name.find(n->Name);
+                if (it != v->by_name.end() && it->second == r) v->by_name.erase(it);
+            }
+            v->infos[(size_t)r] = nullptr;
+            v->nodes[(size_t)r] = nullptr;
+            v->free_rows.push_back(r);
+            --v->live;
+        }
+        std::sort(v->free_rows.begin(), v->free_rows.end(), std::greater<int64_t>());
+        if (added_.size() > v->free_rows.size()) {
+            const size_t rows = v->rows(), need = added_.size() - v->free_rows.size();
+            const size_t cap = rows + std::max(need, rows / 8 + 64);
+            if (crane_dyn_resize_nodes(eng_, (int64_t)cap)) {
+                *err = crane_dyn_last_error(eng_);
+                return false;
+            }
+            v->grow(cap);
+            std::vector<int64_t> fresh;
+            for (size_t r = cap; r-- > rows;) fresh.push_back((int64_t)r);
+            v->free_rows.insert(v->free_rows.begin(), fresh.begin(), fresh.end());  // (after the old ones)
+            ++cnt_.grows;
+        }
+        for (int64_t j : added_) {
+            const int64_t r = v->free_rows.back();
+            v->free_rows.pop_back();
+            const NodeInfo* ni = L[(size_t)j];
+            v->infos[(size_t)r] = ni;
+            v->nodes[(size_t)r] = nullptr;  // (parsed by update(), which records the Node)
+            v->gens[(size_t)r] = ni->Generation;
+            v->seen[(size_t)r] = epoch_;
+            v->info_idx.put(ni, r);
+            if (ni->node()) v->by_name[ni->node()->Name] = r;
+            ++v->live;
+            changed_.push_back(r);
+        }
+        if (v->info_idx.crowded()) v->index_infos();  // entries of departed NodeInfos pile up
+        cnt_.nodes_joined += added_.size();
+        cnt_.nodes_left += removed_.size();
+        return true;
+    }
+
+    // the changed rows: re-parse, scatter into the engine, rebuild their table rows.  The View
+    // records the new Node objects only once the engine holds them (a failed call makes the
+    // caller drop the View: the next cycle resyncs in full).
     bool update(View* v, int64_t now, std::string* err) {
-        const std::vector<const NodeInfo*>& L = v->infos;
         const size_t k = changed_.size();
         cnodes_.resize(k);
-        for (size_t j = 0; j < k; ++j) cnodes_[j] = L[(size_t)changed_[j]]->node();
+        for (size_t j = 0; j < k; ++j) cnodes_[j] = v->infos[(size_t)changed_[j]]->node();
         std::vector<double> val;
         std::vector<int64_t> ts;
         if (!parse(cnodes_, 1, &val, &ts, err)) return false;
@@ -486,7 +563,7 @@ class DynamicScheduler {
             for (size_t j = 0; j < k; ++j) {
                 const size_t i = (size_t)changed_[j];
                 v->nodes[i] = cnodes_[j];
-                v->gens[i] = L[i]->Generation;
+                v->gens[i] = v->infos[i]->Generation;
                 if (cnodes_[j]) v->name_idx.put(&cnodes_[j]->Name, (int64_t)i);
             }
             if (v->name_idx.crowded()) v->index_names();  // entries of replaced Nodes pile up
@@ -525,30 +602,39 @@ class DynamicScheduler {
         return true;
     }
 
-    // The snapshot scan: every NodeInfo compared with the one its row was parsed from, in
-    // chunks any of the cycle's callers may take.
+    // The snapshot scan: every NodeInfo looked up in the synced rows and compared with the one
+    // its row was parsed from, in chunks any of the cycle's callers may take.  A NodeInfo with no
+    // row is a joining node; the rows no NodeInfo claimed are the nodes that left.
     struct ScanJob {
         const NodeInfo* const* L;
-        const NodeInfo* const* vi;
-        const Node* const* vn;
-        const int64_t* vg;
+        const View* v;
+        uint32_t* seen;
+        uint32_t epoch = 0;
         size_t n = 0, chunk = 0, nchunks = 0;
         std::atomic<size_t> next{0}, done{0};
-        std::atomic<bool> full{false};  // a NodeInfo differs: the node set changed
-        std::vector<std::vector<int64_t>> changed;  // per chunk
+        std::vector<std::vector<int64_t>> changed;  // per chunk: rows
+        std::vector<std::vector<int64_t>> added;    // per chunk: List() positions
         void work() {
             for (;;) {
                 const size_t c = next.fetch_add(1, std::memory_order_relaxed);
                 if (c >= nchunks) return;
                 const size_t hi = std::min(n, (c + 1) * chunk);
-                std::vector<int64_t>& out = changed[c];
+                std::vector<int64_t>& ch = changed[c];
+                std::vector<int64_t>& ad = added[c];
+                const NodeInfo* const* vi = v->infos.data();
+                const Node* const* vn = v->nodes.data();
+                const int64_t* vg = v->gens.data();
+                const int64_t rows = (int64_t)v->rows();
                 for (size_t i = c * chunk; i < hi; ++i) {
                     const NodeInfo* x = L[i];
-                    if (x != vi[i]) {
-                        full.store(true, std::memory_order_relaxed);
-                        break;
+                    // rows follow List() order until the set changes: the same position first
+                    int64_t r = (int64_t)i < rows && vi[i] == x ? (int64_t)i : v->info_idx.get(x);
+                    if (r < 0 || vi[r] != x) {
+                        ad.push_back((int64_t)i);
+                        continue;
                     }
-                    if (x->node() != vn[i] || x->Generation != vg[i]) out.push_back((int64_t)i);
+                    seen[r] = epoch;
+                    if (x->node() != vn[r] || x->Generation != vg[r]) ch.push_back(r);
                 }
                 done.fetch_add(1, std::memory_order_acq_rel);
             }
@@ -556,8 +642,9 @@ class DynamicScheduler {
     };
     static constexpr size_t kScanChunk = 4096;
 
-    // The state for a cycle at `now`: compare the snapshot's NodeInfos with the synced ones
-    // (with the cycle's other callers when `state` is given).
+    // The state for a cycle at `now`: compare the snapshot's NodeInfos with the synced rows (with
+    // the cycle's other callers when `state` is given), then apply the joins, departures and
+    // changes.
     std::shared_ptr<View> sync_locked(int64_t now, std::string* err, CycleState* state = nullptr) {
         if (!handle_.snapshot) {
             *err = "no snapshot";
@@ -565,35 +652,49 @@ class DynamicScheduler {
         }
         const std::vector<const NodeInfo*>& L = handle_.snapshot->List();
         std::shared_ptr<View> v = view_;
-        bool full = !v || L.size() != v->infos.size();
+        if (!v) {
+            view_ = full_sync(L, now, err);
+            return view_;
+        }
         changed_.clear();
-        if (!full) {
+        added_.clear();
+        removed_.clear();
+        ++epoch_;
+        {
             auto job = std::make_shared<ScanJob>();
             job->L = L.data();
-            job->vi = v->infos.data();
-            job->vn = v->nodes.data();
-            job->vg = v->gens.data();
+            job->v = v.get();
+            job->seen = v->seen.data();
+            job->epoch = epoch_;
             job->n = L.size();
             job->chunk = kScanChunk;
             job->nchunks = (job->n + kScanChunk - 1) / kScanChunk;
             job->changed.resize(job->nchunks);
+            job->added.resize(job->nchunks);
             if (state && job->nchunks > 1) {
                 state->dyn_job_ = job;
                 state->dyn_phase_.store(2, std::memory_order_release);
             }
             job->work();
             while (job->done.load(std::memory_order_acquire) < job->nchunks) relax();
-            full = job->full.load(std::memory_order_relaxed);
-            if (!full)
-                for (const auto& c : job->changed) changed_.insert(changed_.end(), c.begin(), c.end());
+            for (const auto& c : job->changed) changed_.insert(changed_.end(), c.begin(), c.end());
+            for (const auto& c : job->added) added_.insert(added_.end(), c.begin(), c.end());
         }
-        if (full) {
+        // the live rows no NodeInfo of this snapshot claimed: the nodes that left
+        if (L.size() - added_.size() != v->live)
+            for (size_t r = 0; r < v->rows(); ++r)
+                if (v->infos[r] && v->seen[r] != epoch_) removed_.push_back((int64_t)r);
+        if (4 * (added_.size() + removed_.size()) > L.size() + 256) {  // most of the set: resync whole
             view_.reset();
             view_ = full_sync(L, now, err);
             return view_;
         }
         // a failed engine call drops the View: the next cycle starts from a full sync instead of
         // answering from rows the engine no longer matches
+        if ((!added_.empty() || !removed_.empty()) && !membership(v.get(), L, err)) {
+            view_.reset();
+            return nullptr;
+        }
         if (!changed_.empty() && !update(v.get(), now, err)) {
             view_.reset();
             return nullptr;
@@ -653,13 +754,15 @@ class DynamicScheduler {
     crane_tz* zone_ = nullptr;  // the IANA zone of $TZ, or null: the fixed offset tz_
     int64_t tz_ = 8 * 3600;
     int32_t parse_threads_ = 16;  // the framework's parallelism (upstream default)
-    int64_t horizon_ns_ = 60LL * 1000000000LL;
+    static constexpr int64_t kAllTime = INT64_MAX;
+    int64_t horizon_ns_ = kAllTime;  // the table's span: the whole time axis unless SetHorizon
+    uint32_t epoch_ = 0;             // snapshot scans so far
     mutable std::mutex mu_;
     Counters cnt_;
     std::shared_ptr<View> view_;
     // scratch of the syncs (under mu_)
     std::vector<std::string> keys_;
-    std::vector<int64_t> changed_;
+    std::vector<int64_t> changed_, added_, removed_;
     std::vector<const Node*> cnodes_;
     std::vector<const char*> strs_;
     std::vector<size_t> lens_;

@@ -9,12 +9,15 @@
 //                            new Node object and bumps the NodeInfo's Generation; the old object
 //                            is freed, so its address may be reused)
 //   unset <i> <key>          the same with the annotation removed
+//   remove <i>               node i leaves the cluster: dropped from the snapshot, its NodeInfo and
+//                            Node freed (their addresses may be reused by a later node)
 //   pod <uid> <now_ns> <ds>  run Filter + Score of this pod on every node
 //   nilnode <uid> <now_ns>   Filter with NodeInfo(nullptr)
 //   missing <uid> <now_ns> <name>  Score of a node absent from the snapshot
 //   mt <uid> <now_ns> <ds>   as pod, but Filter/Score called from 16 threads at once, half
 //                            of them on a Clone() of the cycle state (preemption dry runs)
 //   counters                 the plugin's sync counters
+//   horizon <ns>             SetHorizon (a finite table span; default: the whole time axis)
 // The node-shard group through the C ABI (crane_dyn_group_*), over the same snapshot and policy:
 //   group <devices> <depth> <collective> <threads>   crane_dyn_group_create over the comma-separated
 //                            device list, options set, the snapshot's annotations parsed (the plugin's
@@ -122,6 +125,11 @@ int main() {
             snap.replace((size_t)std::stoll(f[1]), f[2], &v);
         } else if (f[0] == "unset") {
             snap.replace((size_t)std::stoll(f[1]), f[2], nullptr);
+        } else if (f[0] == "remove") {
+            const size_t i = (size_t)std::stoll(f[1]);
+            snap.list.erase(snap.list.begin() + (long)i);
+            snap.infos.erase(snap.infos.begin() + (long)i);
+            snap.objs.erase(snap.objs.begin() + (long)i);
         } else if (f[0] == "group") {
             std::vector<int32_t> devs;
             for (size_t a = 0, b; a <= f[1].size(); a = b + 1) {
@@ -188,10 +196,12 @@ int main() {
                 for (size_t p = 0; p < gnow.size(); ++p) std::cout << "G\t" << p << "\t" << ch[p] << "\t" << sc[p] << "\n";
             gnow.clear();
             gds.clear();
+        } else if (f[0] == "horizon") {
+            ds->SetHorizon(std::stoll(f[1]));
         } else if (f[0] == "counters") {
             const auto c = ds->counters();
             std::cout << "C\t" << c.tables_built << "\t" << c.full_syncs << "\t" << c.incremental_syncs << "\t"
-                      << c.nodes_updated << "\n";
+                      << c.nodes_updated << "\t" << c.nodes_joined << "\t" << c.nodes_left << "\t" << c.grows << "\n";
         } else if (f[0] == "mt") {
             Pod pod;
             pod.UID = pod.Name = f[1];

@@ -231,3 +231,51 @@ def test_state_change_waits_only_for_its_own_streams():
     assert torch.equal(a_keys, ref)
     for e in (ea, ea2, eb):
         e.close()
+
+
+def test_resize_then_update_equals_fresh_engine_all_time():
+    """Nodes joining (crane_dyn_resize_nodes grows the shard: the new rows have no annotations until
+    crane_dyn_update_node_steps writes them) and a shrink that drops the last rows: the tables over
+    the whole time axis (t0 = INT64_MIN, t1 = INT64_MAX: every expiry fits a row) equal a fresh
+    engine holding the final nodes, and the oracle at pod times hours apart."""
+    spec = cd.default_policy_spec()
+    rng = np.random.default_rng(808)
+    c = synth.make_cluster(spec, 3000, 64, seed=808, pod_step_ns=1_800_000_000_000 // 64)
+    full = synth.make_cluster(spec, 3500, 64, seed=809)
+    keep = 2800  # the engine first holds 2800 nodes, then grows to 3500, then shrinks to 3300
+    eng = engine_for(spec)
+    val, ts, _ = full.rows(eng.metric_names)
+    eng.upload_nodes(val[:, :keep], ts[:, :keep], full.hv[:keep], full.hv_ts[:keep])
+    lo, hi = np.iinfo(np.int64).min, np.iinfo(np.int64).max
+    eng.resize_nodes(3500)
+    tab = list(eng.node_steps(lo, hi))
+    # the new rows: no annotations yet (every metric missing: Filter passes, Score from failed terms)
+    new = np.arange(keep, 3500)
+    rows = eng.update_node_steps(new, val[:, new], ts[:, new], full.hv[new], full.hv_ts[new], lo, hi)
+    patch(tab, rows, new)
+    churn(full, spec, rng, np.arange(0, 3500, 7), int(synth.NOW0_NS))
+    val, ts, _ = full.rows(eng.metric_names)
+    idx = np.arange(0, 3500, 7)
+    patch(tab, eng.update_node_steps(idx, val[:, idx], ts[:, idx], full.hv[idx], full.hv_ts[idx], lo, hi), idx)
+    fresh = engine_for(spec)
+    fresh.upload_nodes(val, ts, full.hv, full.hv_ts)
+    ref = fresh.node_steps(lo, hi)
+    for a, b in zip(tab, ref):
+        assert np.array_equal(a, b)
+    assert np.array_equal(eng.node_steps(lo, hi)[0], ref[0])  # (a full rebuild on the grown engine too)
+    from oracle import oracle as O
+    okm = (ts != TS_INVALID).astype(np.uint8)
+    for p in range(0, 64, 9):  # pods half an hour apart: one table answers them all
+        now = np.array([c.now[p]], np.int64)
+        ff, sc = cd.Engine.table_lookup(tab, now[0])
+        off, osc, _ = O.eval_soa(spec, eng.metric_names, okm, val, np.where(okm == 1, ts, 0),
+                                 (full.hv_ts != TS_INVALID).astype(np.uint8), full.hv, full.hv_ts, now,
+                                 np.zeros(1, np.uint8))
+        assert np.array_equal(ff, off[0]) and np.array_equal(sc, osc[0]), p
+    eng.resize_nodes(3300)
+    tab2 = eng.node_steps(lo, hi)
+    for a, b in zip(tab2, ref):
+        assert np.array_equal(a, b[:3300])
+    fresh.close()
+    eng.close()
+

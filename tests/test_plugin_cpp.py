@@ -124,38 +124,50 @@ def _stamp(unix_s):
 
 
 @pytest.mark.gpu
-def test_churn_through_plugin(driver, cluster_small, tmp_path):
+@pytest.mark.parametrize("horizon", ["all", "finite"])
+def test_churn_through_plugin(driver, cluster_small, tmp_path, horizon):
     """The controller keeps patching annotations between scheduling cycles (node.go:88-96,
     123-146): each patch publishes a new Node object.  The plugin re-parses only the changed
-    nodes (crane_dyn_update_nodes + crane_dyn_node_steps_subset) and must answer every
-    Filter / Score exactly as the reference does on the CURRENT annotations (stats.go:51-76),
-    here the oracle's string mode on the patched annotation maps; a node added mid-way
-    changes the node set (a full sync)."""
+    nodes (crane_dyn_update_node_steps) and must answer every Filter / Score exactly as the
+    reference does on the CURRENT annotations (stats.go:51-76), here the oracle's string mode on
+    the patched annotation maps.  Nodes join (a free row, or the shard grows:
+    crane_dyn_resize_nodes) and leave (their rows freed; the freed NodeInfo addresses may come
+    back for a new node) without a full resync.  Tables over the whole time axis (the default)
+    never need rebuilding; pods are hours apart here."""
     import numpy as np
     from oracle import oracle as O
     c = cluster_small
     pol = policy_from_json(c["policy"])
     nodes = [dict(a) for a in c["nodes"]]
+    names = [f"node-{i}" for i in range(len(nodes))]
     keys = [n for n, _ in pol["syncPolicy"]] + ["node_hot_value"]
     rng = np.random.default_rng(5150)
     lines = [f"policy\t{write_policy(tmp_path, pol)}"]
     for i, a in enumerate(nodes):
-        lines.append(f"node\tnode-{i}")
+        lines.append(f"node\t{names[i]}")
         lines += [f"anno\t{k}\t{v}" for k, v in a.items()]
     expect = []
-    n_pat = 0
-    for p, pod in enumerate(c["pods"]):
+    n_joined = n_left = 0
+    pods = [dict(p, now_ns=p["now_ns"] + (q // 3) * 3600 * 10**9) for q, p in enumerate(c["pods"])]
+    for p, pod in enumerate(pods):
         now = pod["now_ns"]
-        if p == 7:  # a new node: the node set changes
-            nodes.append({"cpu_usage_avg_5m": f"0.10000,{_stamp(now // 10**9 - 5)}"})
-            lines.append(f"node\tnode-{len(nodes) - 1}")
+        if p in (4, 7, 11):  # a node joins
+            nodes.append({"cpu_usage_avg_5m": f"0.10000,{_stamp(now // 10**9 - 5)}",
+                          "mem_usage_avg_5m": f"0.{p:02d}000,{_stamp(now // 10**9 - 9)}"})
+            names.append(f"joined-{p}")
+            lines.append(f"node\t{names[-1]}")
             lines += [f"anno\t{k}\t{v}" for k, v in nodes[-1].items()]
+            n_joined += 1
+        if p in (5, 9, 10):  # a node leaves
+            i = int(rng.integers(0, len(nodes)))
+            del nodes[i], names[i]
+            lines.append(f"remove\t{i}")
+            n_left += 1
         if p > 0:
             for _ in range(int(rng.integers(1, 6))):
                 i = int(rng.integers(0, len(nodes)))
                 k = keys[int(rng.integers(0, len(keys)))]
                 r = rng.random()
-                n_pat += 1
                 if r < 0.1:
                     nodes[i].pop(k, None)
                     lines.append(f"unset\t{i}\t{k}")
@@ -167,22 +179,31 @@ def test_churn_through_plugin(driver, cluster_small, tmp_path):
                 lines.append(f"patch\t{i}\t{k}\t{v}")
         lines.append(f"pod\tp{p}\t{now}\t{int(pod['daemonset'])}")
         ff, sc, _ = O.eval_strings(pol, nodes, np.array([now], np.int64), np.array([pod["daemonset"]], np.uint8))
-        expect.append((ff[0].copy(), sc[0].copy(), len(nodes)))
+        expect.append((ff[0].copy(), sc[0].copy(), list(names)))
     lines.append("counters")
+    if horizon == "finite":
+        lines.insert(1, "horizon\t60000000000")
     out = run(driver, "\n".join(lines) + "\n")
     F = [o for o in out if o[0] == "F"]
     S = [o for o in out if o[0] == "S"]
     off = 0
-    for p, (ff, sc, N) in enumerate(expect):
-        for n in range(N):
+    for p, (ff, sc, nm) in enumerate(expect):
+        for n, name in enumerate(nm):
             f, s = F[off + n], S[off + n]
-            ds = c["pods"][p]["daemonset"]
+            assert f[2] == name and s[2] == name, (p, n)
+            ds = pods[p]["daemonset"]
             assert f[3] == str(SUCCESS if (ds or ff[n] < 0) else UNSCHED), (p, n)
             if not ds and ff[n] >= 0:
-                assert f[4] == f"Load[{pol['predicate'][ff[n]][0]}] of node[node-{n}] is too high", (p, n)
+                assert f[4] == f"Load[{pol['predicate'][ff[n]][0]}] of node[{name}] is too high", (p, n)
             assert s[3] == str(sc[n]), (p, n)
-        off += N
+        off += len(nm)
     C = [o for o in out if o[0] == "C"][0]
-    tables, full, incr, upd = (int(x) for x in C[1:5])
-    assert full == 2  # the first cycle and the one after the node was added
-    assert incr >= len(c["pods"]) - 3 and upd >= incr
+    tables, full, incr, upd, joined, left, grows = (int(x) for x in C[1:8])
+    assert full == 1  # the first cycle only: joins and departures are incremental
+    assert joined == n_joined and left == n_left and grows >= 1
+    assert incr >= len(pods) - 3 and upd >= incr
+    want, t0, t1 = 0, None, None  # finite: a new table whenever a pod leaves the last one's span
+    for pod in pods:
+        if t0 is None or not (t0 <= pod["now_ns"] < t1):
+            want, t0, t1 = want + 1, pod["now_ns"], pod["now_ns"] + 60 * 10**9
+    assert tables == (1 if horizon == "all" else want)

@@ -25,6 +25,13 @@
 // the caller can recompute every pod's answer on the churned annotations.  At X = 1 and
 // 100k nodes with the shipped policy that is ~2,700 patches per simulated second.
 //
+// Node set changes (--node-events E, E > 0): every E-th cycle one node joins the cluster (a new
+// Node with every syncPolicy metric and node_hot_value, stamped at the cycle's time) and, in
+// between, one node leaves (a random live node; its NodeInfo and Node are freed).  Nodes are
+// identified by creation index (the snapshot's nodes 0..N-1, then the joining ones); the churn
+// log records joins ("J pod id name") and departures ("L pod id") and the chosen node of every
+// pod is a creation index.  The slowest cycles are reported with their parts (slowest).
+//
 // "--cpu" (the dropin_cpu build, -DDROPIN_CPU, linked with the CPU oracle — bench.py's CPU
 // baseline only): the same harness driving a CPU plugin whose Filter and Score re-parse
 // the node's annotations on every call, as the reference's getResourceUsage does
@@ -37,6 +44,7 @@
 #include <fstream>
 #include <functional>
 #include <iostream>
+#include <map>
 #include <memory>
 #include <numeric>
 #include <queue>
@@ -59,7 +67,9 @@ struct BenchSnap : Snapshot {
     std::vector<std::unique_ptr<Node>> objs;
     std::vector<std::unique_ptr<NodeInfo>> infos;
     std::vector<const NodeInfo*> list;
-    std::unordered_map<std::string, size_t, NameHash> by_name;
+    std::vector<int64_t> ids;          // list position -> creation index
+    std::vector<int64_t> pos_of;       // creation index -> list position (-1: left)
+    std::unordered_map<std::string, size_t, NameHash> by_name;  // name -> list position
     int64_t gen = 0;
     const std::vector<const NodeInfo*>& List() const override { return list; }
     const NodeInfo* Get(const std::string& name, std::string* err) const override {
@@ -73,9 +83,29 @@ struct BenchSnap : Snapshot {
     const Node& node(size_t i) const { return *objs[i]; }
     void add(const std::string& name) {
         by_name[name] = objs.size();
+        pos_of.push_back((int64_t)objs.size());
+        ids.push_back((int64_t)pos_of.size() - 1);
         objs.emplace_back(new Node{name, {}});
         infos.emplace_back(new NodeInfo(objs.back().get(), ++gen));
         list.push_back(infos.back().get());
+    }
+    // a joining node, published whole (its annotations set before any reader sees it)
+    void join(const std::string& name, std::map<std::string, std::string> ann) {
+        add(name);
+        objs.back()->Annotations = std::move(ann);
+    }
+    // node at list position i leaves: dropped from the list, its objects freed
+    void leave(size_t i) {
+        by_name.erase(objs[i]->Name);
+        pos_of[(size_t)ids[i]] = -1;
+        list.erase(list.begin() + (long)i);
+        infos.erase(infos.begin() + (long)i);
+        objs.erase(objs.begin() + (long)i);
+        ids.erase(ids.begin() + (long)i);
+        for (size_t j = i; j < ids.size(); ++j) {
+            pos_of[(size_t)ids[j]] = (int64_t)j;
+            by_name[objs[j]->Name] = j;
+        }
     }
     void patch(size_t i, const std::string& key, const std::string& value) {
         std::unique_ptr<Node> n(new Node(*objs[i]));
@@ -322,6 +352,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     int threads = 16;
+    int node_events = 0;
     bool cpu = false;
     double churn_scale = 0.0;
     std::string churn_log;
@@ -334,6 +365,7 @@ int main(int argc, char** argv) {
         else if (k == "--churn") churn_scale = std::atof(next().c_str());
         else if (k == "--churn-log") churn_log = next();
         else if (k == "--seed") seed = std::strtoull(next().c_str(), nullptr, 10);
+        else if (k == "--node-events") node_events = std::atoi(next().c_str());
         else {
             std::fprintf(stderr, "unknown argument %s\n", k.c_str());
             return 2;
@@ -418,29 +450,77 @@ int main(int argc, char** argv) {
         churn.reset(new Churn(ds.policy(), snap.objs.size(), pods[0].now, churn_scale, seed));
     FILE* clog = churn_log.empty() ? nullptr : std::fopen(churn_log.c_str(), "w");
     Pool pool(threads);
-    const int64_t N = (int64_t)snap.objs.size();
-    std::vector<uint8_t> feas((size_t)N);
-    std::vector<int64_t> fidx((size_t)N), fscore((size_t)N);
+    const int64_t N0 = (int64_t)snap.objs.size();
+    std::vector<uint8_t> feas((size_t)N0);
+    std::vector<int64_t> fidx((size_t)N0), fscore((size_t)N0);
+    int64_t n_joins = 0, n_leaves = 0;
     std::vector<double> cyc_ms, first_ms, filt_ms, score_ms, sel_ms, pool_ms, cyc_changed_ms;
     std::vector<int64_t> chosen;
     std::vector<Churn::Patch> due;
     int64_t n_patches = 0, changed_cycles = 0;
+    struct Slow {
+        double cyc, first, filt, score;
+        size_t pod;
+        int64_t patches;
+    };
+    std::vector<Slow> slow;
     std::atomic<int> errors{0};
     for (size_t pi = 0; pi < pods.size(); ++pi) {
         auto& p = pods[pi];
         {  // the harness's own cost: the two fan-outs over no-op calls
+            const int64_t Nn = (int64_t)snap.list.size();
             const auto q0 = Clock::now();
-            pool.until(N, [&](int64_t i) { feas[(size_t)i] = (uint8_t)(i & 1); });
-            pool.until(N * 7 / 10, [&](int64_t j) { fscore[(size_t)j] = j; });
+            pool.until(Nn, [&](int64_t i) { feas[(size_t)i] = (uint8_t)(i & 1); });
+            pool.until(Nn * 7 / 10, [&](int64_t j) { fscore[(size_t)j] = j; });
             pool_ms.push_back(std::chrono::duration<double, std::milli>(Clock::now() - q0).count());
         }
         due.clear();
+        const int64_t patches0 = n_patches;
         if (churn && pi > 0) churn->due(p.now, &due);  // published between the cycles (informer)
+        if (cpu && node_events > 0) {
+            std::fprintf(stderr, "--node-events needs the engine plugin\n");
+            return 2;
+        }
         for (const auto& x : due) {
-            snap.patch(x.node, x.key, x.value);
+            const int64_t at = snap.pos_of[x.node];
+            if (at < 0) continue;  // (a node that left)
+            snap.patch((size_t)at, x.key, x.value);
+            ++n_patches;
             if (clog) std::fprintf(clog, "%zu\t%zu\t%s\t%s\n", pi, x.node, x.key.c_str(), x.value.c_str());
         }
-        n_patches += (int64_t)due.size();
+        if (node_events > 0 && pi > 0 && pi % (size_t)node_events == 0) {  // a node joins
+            std::map<std::string, std::string> ann;
+            const std::string st = local_stamp(p.now / 1000000000LL, 8 * 3600);
+            uint64_t r = mix64(seed * 977 + pi);
+            char v[64];
+            for (int32_t m = 0; m < ds.policy().n_sync; ++m) {
+                r = mix64(r);
+                std::snprintf(v, sizeof v, "%.5f,%s", (double)(r % 120001) / 1e5, st.c_str());
+                ann[ds.policy().sync_name[m]] = v;
+            }
+            std::snprintf(v, sizeof v, "%d,%s", (int)((r >> 20) % 13), st.c_str());
+            ann[NodeHotValue] = v;
+            const std::string name = "joined-" + std::to_string(pi);
+            snap.join(name, ann);
+            ++n_joins;
+            if (clog) {
+                std::fprintf(clog, "J\t%zu\t%lld\t%s\n", pi, (long long)snap.ids.back(), name.c_str());
+                for (const auto& kv : ann)
+                    std::fprintf(clog, "%zu\t%lld\t%s\t%s\n", pi, (long long)snap.ids.back(), kv.first.c_str(),
+                                 kv.second.c_str());
+            }
+        } else if (node_events > 0 && pi > 0 && pi % (size_t)node_events == (size_t)node_events / 2) {  // one leaves
+            const size_t i = (size_t)(mix64(seed * 131 + pi) % snap.list.size());
+            if (clog) std::fprintf(clog, "L\t%zu\t%lld\n", pi, (long long)snap.ids[i]);
+            snap.leave(i);
+            ++n_leaves;
+        }
+        const int64_t N = (int64_t)snap.list.size();
+        if ((int64_t)feas.size() < N) {
+            feas.resize((size_t)N);
+            fidx.resize((size_t)N);
+            fscore.resize((size_t)N);
+        }
         const uint64_t sync0 = cpu ? 0 : ds.counters().sync_ns;
         const auto t0 = Clock::now();
         CycleState st;
@@ -494,8 +574,10 @@ int main(int argc, char** argv) {
         filt_ms.push_back(ms(t0, t1));
         score_ms.push_back(ms(t1, t2));
         sel_ms.push_back(ms(t2, t3));
-        chosen.push_back(best);
+        chosen.push_back(best < 0 ? -1 : snap.ids[(size_t)best]);
+        slow.push_back({ms(t0, t3), first_ms.back(), ms(t0, t1), ms(t1, t2), pi, n_patches - patches0});
     }
+    std::sort(slow.begin(), slow.end(), [](const Slow& a, const Slow& b) { return a.cyc > b.cyc; });
     if (clog) std::fclose(clog);
     auto med = [](std::vector<double> v) {
         if (v.empty()) return 0.0;
@@ -514,13 +596,22 @@ int main(int argc, char** argv) {
                 "\"select_ms_median\": %.4f, \"pool_noop_ms_median\": %.4f, \"churn_scale\": %.3f, "
                 "\"patches\": %lld, \"simulated_s\": %.4f, \"cycles_with_patches\": %lld, \"tables_built\": %llu, "
                 "\"full_syncs\": %llu, \"incremental_syncs\": %llu, \"nodes_updated\": %llu, \"errors\": %d, "
-                "\"chosen\": [",
-                (long long)N, pods.size(), threads, cpu ? "cpu" : "engine", sync_ms, pct(0.5), pct(0.9), pct(0.0),
+                "\"nodes_joined\": %lld, \"nodes_left\": %lld, \"plugin_joined\": %llu, \"plugin_left\": %llu, "
+                "\"shard_grows\": %llu, \"nodes_end\": %zu, \"slowest\": [",
+                (long long)N0, pods.size(), threads, cpu ? "cpu" : "engine", sync_ms, pct(0.5), pct(0.9), pct(0.0),
                 pct(1.0), cyc_ms.empty() ? 0.0 : std::accumulate(cyc_ms.begin(), cyc_ms.end(), 0.0) / (double)cyc_ms.size(),
                 med(cyc_changed_ms), med(first_ms), med(filt_ms), med(score_ms), med(sel_ms), med(pool_ms), churn_scale,
                 (long long)n_patches, sim_s, (long long)changed_cycles, (unsigned long long)c.tables_built,
                 (unsigned long long)c.full_syncs, (unsigned long long)c.incremental_syncs,
-                (unsigned long long)c.nodes_updated, errors.load());
+                (unsigned long long)c.nodes_updated, errors.load(), (long long)n_joins, (long long)n_leaves,
+                (unsigned long long)c.nodes_joined, (unsigned long long)c.nodes_left, (unsigned long long)c.grows,
+                snap.list.size());
+    for (size_t i = 0; i < std::min<size_t>(5, slow.size()); ++i)
+        std::printf("%s{\"pod\": %zu, \"cycle_ms\": %.4f, \"first_call_ms\": %.4f, \"filter_ms\": %.4f, "
+                    "\"score_ms\": %.4f, \"patches\": %lld}",
+                    i ? ", " : "", slow[i].pod, slow[i].cyc, slow[i].first, slow[i].filt, slow[i].score,
+                    (long long)slow[i].patches);
+    std::printf("], \"chosen\": [");
     for (size_t i = 0; i < chosen.size(); ++i) std::printf("%s%lld", i ? ", " : "", (long long)chosen[i]);
     std::printf("]}\n");
     return 0;
