@@ -167,6 +167,7 @@ struct crane_dyn {
     bool heap_mode = false;
     bool log_sorted = false;            // uploaded log in non-decreasing time order (upload_bindings)
     std::vector<int64_t> hts_copy;      // ... and its timestamps (the windows' suffixes are found here)
+    std::vector<int64_t> hts_sample;    // every 64th of them: the suffix search touches one 512-byte run
     bool pos_valid = false;             // pos_s[r]: the suffix start of window rank r for cutoffs pos_cut
     int64_t pos_cut[kMaxWin] = {};
     int64_t pos_s[kMaxWin] = {};
@@ -393,8 +394,15 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     if (by_pos) {
         // (the cutoffs move once per second: the last search's suffixes are reused until they do)
         if (!h->pos_valid || std::memcmp(h->pos_cut, cut.sorted, sizeof(int64_t) * dp.n_win) != 0) {
+            // (a batch whose time advanced moves them: the sampled stamps narrow each search to one
+            // 64-stamp run, ~7 + 6 probes, instead of 20 probes across the 8 MB stamp array)
+            const std::vector<int64_t>& smp = h->hts_sample;
             const int64_t* t0 = h->hts_copy.data();
-            for (int r = 0; r < dp.n_win; ++r) h->pos_s[r] = std::upper_bound(t0, t0 + h->B, cut.sorted[r]) - t0;
+            for (int r = 0; r < dp.n_win; ++r) {
+                const int64_t j = std::upper_bound(smp.begin(), smp.end(), cut.sorted[r]) - smp.begin();
+                const int64_t lo = j == 0 ? 0 : 64 * (j - 1), hi = std::min<int64_t>(h->B, 64 * j);
+                h->pos_s[r] = std::upper_bound(t0 + lo, t0 + hi, cut.sorted[r]) - t0;
+            }
             std::memcpy(h->pos_cut, cut.sorted, sizeof(int64_t) * dp.n_win);
             h->pos_valid = true;
         }
@@ -871,8 +879,13 @@ int crane_dyn_upload_bindings(crane_dyn* h, int64_t n, const int32_t* node, cons
     // kept for the suffix search of every refresh
     h->pos_valid = false;
     h->log_sorted = n > 0 && std::is_sorted(ts_s, ts_s + n);
-    if (h->log_sorted) h->hts_copy.assign(ts_s, ts_s + n);
-    else h->hts_copy.clear();
+    h->hts_sample.clear();
+    if (h->log_sorted) {
+        h->hts_copy.assign(ts_s, ts_s + n);
+        for (int64_t i = 0; i < n; i += 64) h->hts_sample.push_back(ts_s[i]);
+    } else {
+        h->hts_copy.clear();
+    }
     HIPTRY(h, hipStreamSynchronize(h->stream));
     h->B = n;
     h->heap_mode = false;
@@ -905,6 +918,7 @@ int crane_dyn_binding_records(crane_dyn* h, int64_t size, int64_t gc_time_range_
     h->log_sorted = false;  // heap order
     h->pos_valid = false;
     h->hts_copy.clear();
+    h->hts_sample.clear();
     h->B = size;
     return CRANE_OK;
 }

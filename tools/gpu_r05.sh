@@ -18,6 +18,8 @@ verify)
   tail -1 $O/smoke.log
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline > $O/bench20.log 2>&1 || { tail -30 $O/bench20.log; exit 1; }
   tail -1 $O/bench20.log | cut -c1-900
+  timeout -k 10 60 ./tools/bin_kernarg_probe > $O/kernarg.log 2>&1 || { cat $O/kernarg.log; exit 1; }
+  cat $O/kernarg.log
   ;;
 bench)
   timeout -k 10 600 python bench.py > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
