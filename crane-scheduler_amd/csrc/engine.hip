@@ -122,6 +122,8 @@ struct Options {
                               // >= kPieceMinTiles pod tiles (a piece is re-read once per tile), 1 always,
                               // 2 never (then no per-tile piece ranges either: K3s reads all pieces)
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
+    int k1_stream = 1;        // keys-only step without dedupe-form K2 entries: the streamed step pass
+                              // (k1_stream_steps, no record in registers) | 0 the fused record pass
     int k2_sorted = 1;        // a time-ordered log: K2 reads the widest window's suffix, ranks by position
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
@@ -498,7 +500,7 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
     }
     a.threads = k1_bs(h);
     a.trace = (h->N + a.threads - 1) / a.threads <= kTraceWgs ? h->trace_region(1) : nullptr;
-    HIPTRY(h, launch_node_pass(h->shape, a, st, step));
+    HIPTRY(h, launch_node_pass(h->shape, a, st, step, h->opt.k1_stream != 0));
     if (consume) {
         if (!h->hx_pending) h->buckets_zero = !h->buckets_dense;  // K1 zeroed what it read
         h->counts_pending = false;
@@ -587,7 +589,9 @@ static int step_pods(crane_dyn* h, const StepPlan& sp, int64_t P, const int64_t*
 static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_keys, hipStream_t st) {
     if (P == 0) return CRANE_OK;
     if (sp.fuse) {
-        const K1Step ks{h->stile.p, h->sbatch.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, h->dp.winv, sp.stt};
+        // (the records the fused step leaves stale serve as the streamed pass's scratch)
+        const K1Step ks{h->stile.p, h->sbatch.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, h->dp.winv, sp.stt,
+                        h->rec.p};
         int rc = node_pass_locked(h, st, nullptr, &ks);
         if (rc) return rc;
     } else {
@@ -797,6 +801,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "step_pieces" && range(0, 2)) o.step_pieces = (int)value;
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
     else if (n == "k2_sorted" && range(0, 1)) o.k2_sorted = (int)value;
+    else if (n == "k1_stream" && range(0, 1)) o.k1_stream = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
         if (o.trace) {

@@ -321,6 +321,7 @@ struct K1Step {
     double wsum;
     double winv;             // 1 / wsum when |wsum| is a power of two, else 0 (score_at)
     StepTables st;
+    void* srec;              // NodeRec [N] scratch (the streamed step pass's stepped nodes past its LDS)
 };
 
 size_t node_rec_bytes(int shape);
@@ -351,7 +352,10 @@ struct K1Args {
     int32_t threads;        // workgroup size: 128 or 256
     unsigned long long* trace;  // phase trace or null
 };
-// step (optional): also build the K3 step tables of a pod batch (K3a fused).
-hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr);
+// step (optional): also build the K3 step tables of a pod batch (K3a fused).  stream: with step,
+// no records written and no dedupe-form K2 entries, the streamed step pass (k1_stream_steps: no
+// record in registers, the stepped nodes' records built in LDS)
+hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr,
+                            bool stream = false);
 
 }  // namespace crane

@@ -26,14 +26,17 @@ def _check(spec, c, now, ds):
     # one-step records through its LDS staging, through st.stage always (cap 0), or
     # per block as its counts exceed a small cap; the middle pieces raw or cut into elementary
     # ones (step_pieces 1 always, 0 when it pays, 2 never)
-    for rows, cap, pc in ((1, 1 << 30, 0), (0, 1 << 30, 0), (1, 0, 1), (0, 6, 0), (1, 6, 1), (1, 1 << 30, 1),
-                          (1, 0, 2)):
-        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap, "step_pieces": pc})
+    # the node pass as the streamed step pass (k1_stream 1, the default without dedupe-form K2
+    # entries: no record in registers, the stepped records built in LDS in chunks of 64) or the
+    # record-holding fused pass (0)
+    for rows, cap, pc, sf in ((1, 1 << 30, 0, 1), (0, 1 << 30, 0, 1), (1, 0, 1, 1), (0, 6, 0, 1), (1, 6, 1, 1),
+                              (1, 1 << 30, 1, 1), (1, 0, 2, 1), (1, 1 << 30, 0, 0), (0, 6, 1, 0), (1, 0, 2, 0)):
+        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap, "step_pieces": pc, "k1_stream": sf})
         _, _, ch, cs = eng.eval(now, ds)
-        assert np.array_equal(ch, och), (rows, cap, pc)
+        assert np.array_equal(ch, och), (rows, cap, pc, sf)
         for p in range(len(now)):
             ok = (off[p] < 0) | bool(ds[p])
-            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, pc, p)
+            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, pc, sf, p)
         eng.close()
 
 
@@ -151,7 +154,8 @@ def test_step_keys_async_k2_forms(k2):
             ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
             assert np.array_equal(ch, och), rep
     names = [n for n, _ in eng.stage_times()]
-    assert "k1_node_pass+k3a_steps" in names, names
+    # the dedupe form's per-block entries need the record-holding fused pass; the others stream
+    assert ("k1_node_pass+k3a_steps" if k2 == 0 else "k1_stream_steps") in names, names
 
 
 @pytest.mark.parametrize("keep", [0, 1])
