@@ -1,0 +1,383 @@
+// k1stream.hip — the node pass fused with the step tables, streamed (K1 for large N).
+//
+// Numerics: the same per-term arithmetic as node_rec.hpp / step_node.hpp (stats.go:89-138,
+// plugins.go:39-98 bit for bit, -ffp-contract=off).
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+#include "dyn_types.hpp"
+#include "kernels.hpp"
+#include "node_rec.hpp"
+#include "step_node.hpp"
+
+namespace crane {
+
+// The node pass fused with the step tables, without a NodeRec in registers.  Round 4 found what
+// holds the fused pass at 0.41 of HBM cold: occupancy, which the 160 B record costs (96 VGPRs,
+// five waves per SIMD) — a count pass that folds each row into what classification needs as it
+// arrives runs at seven waves and 0.59 on its own — and every way of handing the ~3 % stepped
+// nodes' records to a separate emit kernel cost more than it saved.  Here the
+// hand-off stays inside the workgroup:
+//   A  each lane streams its node's rows and keeps only e_fail, the hot-value penalty and
+//      expiry, and per pod kind the in-range expiry count / min / max and the flat key;
+//   B  wave prefix sums + one exchange of the waves' totals give every stepped node its
+//      one-step / middle-piece slots and its rank among the block's stepped nodes;
+//   C  in chunks of kSRec stepped nodes: each stepped lane writes its e_fail / pen / e_hv and
+//      slots into an LDS record, the workgroup then gathers the chunk's priority rows from L2
+//      (one (node, term) per lane: the lines this workgroup streamed microseconds earlier) and
+//      writes e_prio / t with rec_metrics' arithmetic, and the first lanes emit the chunk's
+//      (node, kind) items from the LDS records (step_emit_one);
+//   D  the fused pass's tail: sort + publish, elementary pieces, tile rows.
+// Not with the dedupe-form K2 entries (their per-block counting needs the default pass's LDS).
+// step_emit_one for a record in LDS, register-light: every field is read from LDS where it is
+// used, in rolled loops (no copy of the record is kept in registers — a record held in registers
+// anywhere in the kernel would set the VGPR count of every wave), and the in-range expiries are
+// walked in ascending order, with multiplicity, by repeated minimum searches instead of being
+// sorted in registers.  The outputs are step_emit_one's, bit for bit.
+template <int PD, int PR>
+__device__ __forceinline__ int32_t score_at_lds(int64_t t, const NodeRec<PD, PR>* r, double wsum, int32_t noprio,
+                                                double winv) {
+    double s = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < PR; ++k)  // (rolled: one term's two fields in registers at a time)
+        if (t < r->e_prio[k]) s += r->t[k];  // stats.go:124-133, policy order
+    return score_of_sum(s, t < r->e_hv ? r->pen : 0, wsum, noprio, winv);
+}
+template <int PD, int PR>
+__device__ __forceinline__ void emit_lds(const NodeRec<PD, PR>* r, int64_t n, int T, int32_t slot, int32_t mslot,
+                                         bool multi, int64_t tmin, int64_t tmax, double wsum, int32_t noprio,
+                                         const StepTables& st, int64_t blk, Step1* s1b, int64_t kst, double winv) {
+    const volatile NodeRec<PD, PR>* v = r;
+    constexpr int NB = PR + 2;
+    auto field = [&](int j) -> int64_t {  // expiry j of the kind, INT64_MAX when outside (tmin, tmax]
+        const int64_t c = j < PR ? v->e_prio[j] : (j == PR ? v->e_hv : (T == 0 ? v->e_fail : INT64_MIN));
+        return c > tmin && c <= tmax ? c : INT64_MAX;
+    };
+    const int64_t e_fail = v->e_fail;
+    auto key = [&](int64_t t) {
+        const int32_t f = score_at_lds<PD, PR>(t, r, wsum, noprio, winv);
+        return (T == 1 || !(t < e_fail)) ? pack_key(f, n) : -1;
+    };
+    int cnt = 0;
+    int64_t mn = INT64_MAX;
+#pragma unroll 1
+    for (int j = 0; j < NB; ++j) {
+        const int64_t c = field(j);
+        cnt += c != INT64_MAX;
+        mn = min(mn, c);
+    }
+    Step1* s1 = s1b + T * kst;
+    const int32_t k0 = key(tmin);
+    if (!multi) {
+        Step1 o;
+        o.bp = mn;
+        o.k0 = k0;
+        o.k1 = key(mn);
+        s1[slot] = o;
+        return;
+    }
+    // the in-range expiries in ascending order with multiplicity: (value, copies left)
+    int64_t cur = mn;
+    int left = 0;
+#pragma unroll 1
+    for (int j = 0; j < NB; ++j) left += field(j) == mn;
+    auto next = [&]() {
+        if (--left > 0) return;
+        int64_t m = INT64_MAX;
+#pragma unroll 1
+        for (int j = 0; j < NB; ++j) {
+            const int64_t c = field(j);
+            m = c > cur && c < m ? c : m;
+        }
+        cur = m;
+#pragma unroll 1
+        for (int j = 0; j < NB; ++j) left += field(j) == m;
+    };
+    Mid* md = st.mid + (int64_t)T * st.mpad + blk * st.mstride + mslot;
+    int32_t kprev = k0;
+    int64_t last = mn;
+#pragma unroll 1
+    for (int j = 0; j < cnt; ++j) {
+        const int64_t cj = cur;
+        const int32_t kj = key(cj);  // the key from c[j] on
+        if (j + 1 < cnt) {
+            next();
+            Mid p;
+            p.s = cj;
+            p.e = cur;
+            p.key = kj;
+            p.pad = 0;
+            md[j] = p;
+        }
+        last = cj;
+        kprev = kj;
+    }
+    Step1 x, y;
+    x.bp = mn;
+    x.k0 = k0;
+    x.k1 = -1;
+    y.bp = last;
+    y.k0 = -1;
+    y.k1 = kprev;
+    s1[slot] = x;
+    s1[slot + 1] = y;
+}
+
+constexpr int kSRec = 64;   // stepped records staged per chunk
+constexpr int kSCap = 128;  // one-step records per kind staged in LDS (more: st.stage)
+template <int PD, int PR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PD * PR <= 24 ? 7 : 1)))
+void k1_stream_steps(K1Args a, K1Step step) {
+    using Rec = NodeRec<PD, PR>;
+    constexpr int BS = 256;
+    // a staged stepped node's record: e_fail, pen, e_hv, e_prio, t (what the emit reads), and in
+    // e_pred's first words its slots per kind (slot < 0: none) and multi flags
+    __shared__ __attribute__((aligned(16))) Rec lrec[kSRec];
+    __shared__ uint8_t rank_lane[BS];  // a stepped node's rank in the block -> its lane
+    __shared__ __attribute__((aligned(16))) Step1 s1l[2 * kSCap];  // one-step staging, then pm / sm maxima
+    __shared__ __attribute__((aligned(16))) Step1 srt[2 * kSCap];  // sorted copy
+    __shared__ __attribute__((aligned(16))) uint32_t xch[5][4];
+    __shared__ StepShared ssh;
+    const DevPolicy& pol = a.pol;
+    const int64_t N = a.N;
+    const int64_t blk = xcd_block(blockIdx.x, gridDim.x), first = blk * BS, n = first + threadIdx.x;
+    CRANE_TSTAMP(a.trace, blockIdx.x, 0);
+    const int lo = (int)min((int64_t)threadIdx.x, N - 1 - first);  // lane offset, clamped
+    // ---- A: stream the rows (every load unconditional, clamped index: all in flight at once)
+    int64_t pt[PD], qt[PR];
+    double pv[PD], qv[PR];
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+        pt[k] = kTsInvalid;
+        pv[k] = 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+        qt[k] = kTsInvalid;
+        qv[k] = 0.0;
+    }
+    if (pol.n_slots > 0) {
+#pragma unroll
+        for (int k = 0; k < PD; ++k) {
+            const int64_t row = k < pol.npd ? pol.pred_slot[k] : 0;
+            pt[k] = (a.ts + (row * N + first))[lo];
+            pv[k] = (a.val + (row * N + first))[lo];
+        }
+#pragma unroll
+        for (int k = 0; k < PR; ++k) {
+            const int64_t row = k < pol.npr ? pol.prio_slot[k] : 0;
+            qt[k] = (a.ts + (row * N + first))[lo];
+            qv[k] = (a.val + (row * N + first))[lo];
+        }
+    }
+    uint32_t bc[kMaxWin];
+    double hvl = 0.0;
+    int64_t hvt = kTsInvalid;
+    if (a.buckets) {
+#pragma unroll
+        for (int b = 0; b < kMaxWin; ++b) bc[b] = b < pol.n_win ? (a.buckets + first)[(int64_t)b * N + lo] : 0u;
+    } else if (a.hv) {
+        hvl = a.hv[first + lo];
+        hvt = a.hv_ts ? a.hv_ts[first + lo] : a.hv_ts_counts;
+    }
+    const int64_t tmin = step.batch[0], tmax = step.batch[1];  // K3p folded the batch range
+    int64_t tpre = 0;  // this thread's first tile-row bound (step_tile_rows)
+    if (step.st.rows) tile_prefetch(step.st, &tpre);
+    if (threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+    CRANE_TSTAMP(a.trace, blockIdx.x, 1);
+    const bool valid = n < N;
+    // isOverLoad per predicate (stats.go:94-112): the Filter rejects iff now < e_fail
+    int64_t e_fail = kTsInvalid;
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+        if (k < pol.npd) {
+            const double u = pv[k], lim = pol.pred_limit[k];
+            const bool over = pt[k] != kTsInvalid && !(u < 0.0) && lim != 0.0 && u > lim;
+            if (over) e_fail = max(e_fail, sat_add(pt[k], pol.pred_dur[k]));
+        }
+    }
+    // hot value (getNodeHotValue / the binding-log counts) -> penalty and its expiry
+    Rec hr;  // (only pen / e_hv are set and read)
+    if (a.buckets) {
+        if (valid && !a.buckets_keep) {
+#pragma unroll
+            for (int b = 0; b < kMaxWin; ++b)  // consumed: leaves the buckets zeroed for the next K2
+                if (b < pol.n_win) (a.buckets + first)[(int64_t)b * N + threadIdx.x] = 0;
+        }
+        rec_hot_counts<PD, PR>(pol, bc, N, n, valid ? a.cnt_out : nullptr, valid ? a.hvc_out : nullptr,
+                               a.hv_ts_counts, hr);
+    } else if (a.hv) {
+        rec_hot_annotation<PD, PR>(hvl, hvt, hr);
+    } else {
+        hr.pen = 0;
+        hr.e_hv = kTsInvalid;
+    }
+    // priorities in policy order: score_at(tmin)'s ordered sum and the in-range expiries both
+    // pod kinds share (priorities, hot value); e_fail is kind 0's too (DaemonSet pods bypass)
+    double s = 0.0;
+    int cnt1 = 0;
+    int64_t mn1 = INT64_MAX, mx1 = INT64_MIN;
+    auto add = [&](int64_t e, int& c, int64_t& mn, int64_t& mx) {
+        const bool in = e > tmin && e <= tmax;
+        c += in;
+        mn = in ? min(mn, e) : mn;
+        mx = in ? max(mx, e) : mx;
+    };
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+        int64_t e = kTsInvalid;
+        double term = 0.0;
+        if (k < pol.npr && qt[k] != kTsInvalid && !(qv[k] < 0.0)) {
+            e = sat_add(qt[k], pol.prio_dur[k]);
+            term = (1.0 - qv[k]) * pol.prio_w[k];  // getScore (stats.go:89), no FMA
+            term = term * 100.0;
+        }
+        if (tmin < e) s += term;  // stats.go:124-133
+        add(e, cnt1, mn1, mx1);
+    }
+    add(hr.e_hv, cnt1, mn1, mx1);
+    int cnt0 = cnt1;
+    int64_t mn0 = mn1, mx0 = mx1;
+    add(e_fail, cnt0, mn0, mx0);
+    if (!valid) cnt0 = cnt1 = 0;
+    const int32_t s0 = score_of_sum(s, tmin < hr.e_hv ? hr.pen : 0, step.wsum, step.noprio, step.winv);
+    const bool multi0 = cnt0 > 0 && mn0 != mx0, multi1 = cnt1 > 0 && mn1 != mx1;
+    StepSlots so;
+    so.flat0 = valid && cnt0 == 0 && !(tmin < e_fail) ? pack_key(s0, n) : -1;
+    so.flat1 = valid && cnt1 == 0 ? pack_key(s0, n) : -1;
+    CRANE_TSTAMP(a.trace, blockIdx.x, 2);
+    // ---- B: slots (wave prefix sums, the waves' totals exchanged once: one barrier)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t w0 = (cnt0 ? (multi0 ? 2u : 1u) : 0u) | (multi0 ? (uint32_t)(cnt0 - 1) << 16 : 0u);
+    const uint32_t w1 = (cnt1 ? (multi1 ? 2u : 1u) : 0u) | (multi1 ? (uint32_t)(cnt1 - 1) << 16 : 0u);
+    const uint32_t w2 = (cnt0 | cnt1) ? 1u : 0u;
+    uint32_t e0 = wave_scan_add(w0), e1 = wave_scan_add(w1), e2 = wave_scan_add(w2);
+    if (lane == 63) {
+        xch[0][wv] = e0;
+        xch[1][wv] = e1;
+        xch[2][wv] = e2;
+    }
+    e0 -= w0;
+    e1 -= w1;
+    e2 -= w2;
+    __syncthreads();
+    uint32_t base[3], tot[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint4 x = *reinterpret_cast<const uint4*>(xch[k]);
+        base[k] = (wv > 0 ? x.x : 0u) + (wv > 1 ? x.y : 0u) + (wv > 2 ? x.z : 0u);
+        tot[k] = x.x + x.y + x.z + x.w;
+    }
+    const int32_t slot0 = cnt0 ? (int32_t)((base[0] + e0) & 0xFFFF) : -1;
+    const int32_t mslot0 = multi0 ? (int32_t)((base[0] + e0) >> 16) : 0;
+    const int32_t slot1 = cnt1 ? (int32_t)((base[1] + e1) & 0xFFFF) : -1;
+    const int32_t mslot1 = multi1 ? (int32_t)((base[1] + e1) >> 16) : 0;
+    const int32_t rs = (int32_t)(base[2] + e2);  // rank among the block's stepped nodes
+    const int32_t nst = (int32_t)tot[2];
+    if (threadIdx.x == 0) {
+        ssh.lc[0][0] = (int32_t)(tot[0] & 0xFFFF);
+        ssh.lc[0][1] = (int32_t)(tot[0] >> 16);
+        ssh.lc[1][0] = (int32_t)(tot[1] & 0xFFFF);
+        ssh.lc[1][1] = (int32_t)(tot[1] >> 16);
+    }
+    step_publish<BS>(so, ssh, step.st, blk);  // flat maxima, counts (its barrier: ssh.lc final)
+    CRANE_TSTAMP(a.trace, blockIdx.x, 3);
+    // one-step records staged in LDS, or (more of a kind than it holds) in st.stage
+    const bool g1 = max(ssh.lc[0][0], ssh.lc[1][0]) > min(kSCap, step.st.lds_cap);
+    Step1* s1b = g1 ? step.st.stage + blk * 2 * step.st.bs : s1l;
+    const int64_t kst = g1 ? step.st.s1pad : (int64_t)kSCap;
+    // ---- C: the stepped nodes' records in LDS, chunk by chunk, and their (node, kind) items.
+    // The first kSRec stepped nodes write their part (e_fail, pen, e_hv, slots) into the LDS
+    // records now; any further ones into their node's record slot in HBM (step.srec, the node
+    // records the keys-only step leaves stale anyway: the slots go in e_pred, which the emit does
+    // not read), fetched chunk by chunk — no per-lane state lives across the chunks.
+    const bool stepped = (cnt0 | cnt1) != 0;
+    if (stepped) {
+        rank_lane[rs] = (uint8_t)threadIdx.x;
+        Rec* r = rs < kSRec ? &lrec[rs] : static_cast<Rec*>(step.srec) + n;
+        r->e_fail = e_fail;
+        r->pen = hr.pen;
+        r->e_hv = hr.e_hv;
+        int32_t* dw = reinterpret_cast<int32_t*>(r->e_pred);
+        dw[0] = slot0;
+        dw[1] = mslot0;
+        dw[2] = slot1;
+        dw[3] = mslot1;
+        dw[4] = (multi0 ? 1 : 0) | (multi1 ? 2 : 0);
+    }
+    __syncthreads();
+    for (int32_t c0 = 0; c0 < nst; c0 += kSRec) {  // (workgroup-uniform)
+        const int32_t m = min(kSRec, nst - c0);
+        if (c0 > 0) {  // this chunk's parts from HBM (L2: written by this workgroup)
+            for (int i = threadIdx.x; i < m * 8; i += BS) {
+                const int j = i >> 3, f = i & 7;
+                const int64_t* src = reinterpret_cast<const int64_t*>(static_cast<const Rec*>(step.srec) + first +
+                                                                      rank_lane[c0 + j]);
+                int64_t* dst = reinterpret_cast<int64_t*>(&lrec[j]);
+                // e_fail, e_hv, pen (words 0-2) and the slots (e_pred's first words)
+                const int w = f < 3 ? f : (int)(offsetof(Rec, e_pred) / 8) + (f - 3);
+                if (f < 6) dst[w] = src[w];
+            }
+            __syncthreads();
+        }
+        // the priority terms of the chunk's nodes, one (node, term) per lane, from L2 (rec_metrics)
+        for (int i = threadIdx.x; i < m * PR; i += BS) {
+            const int j = i / PR, k = i - j * PR;
+            const int64_t nd = first + rank_lane[c0 + j];
+            int64_t e = kTsInvalid;
+            double term = 0.0;
+            if (k < pol.npr && pol.n_slots > 0) {
+                const int64_t row = pol.prio_slot[k];
+                const int64_t t = a.ts[row * N + nd];
+                const double u = a.val[row * N + nd];
+                if (t != kTsInvalid && !(u < 0.0)) {
+                    e = sat_add(t, pol.prio_dur[k]);
+                    term = (1.0 - u) * pol.prio_w[k];
+                    term = term * 100.0;
+                }
+            }
+            lrec[j].e_prio[k] = e;
+            lrec[j].t[k] = term;
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < 2 * m; i += BS) {
+            const int j = i >> 1, T = i & 1;
+            const int32_t* dw = reinterpret_cast<const int32_t*>(lrec[j].e_pred);
+            const int32_t sl = dw[T ? 2 : 0];
+            if (sl < 0) continue;
+            emit_lds<PD, PR>(&lrec[j], first + rank_lane[c0 + j], T, sl, dw[T ? 3 : 1], ((dw[4] >> T) & 1) != 0, tmin,
+                             tmax, step.wsum, step.noprio, step.st, blk, s1b, kst, step.winv);
+        }
+        __syncthreads();  // (the chunk's records are reused by the next chunk)
+    }
+    CRANE_TSTAMP(a.trace, blockIdx.x, 5);
+    // ---- D: the fused pass's tail
+    if (g1) step_sort_publish_global<BS>(ssh, step.st, blk);
+    else step_sort_publish<BS, kSCap>(s1l, srt, ssh, step.st, blk);
+    CRANE_TSTAMP(a.trace, blockIdx.x, 6);
+    if (step.st.rows) {
+        // the middle pieces' scratch: the staged records' LDS (dead after the emit)
+        constexpr int kPc = ((int)sizeof(lrec) / PieceScr::bytes_per_piece) & ~3;
+        const PieceScr ps{reinterpret_cast<unsigned char*>(lrec), kPc < 128 ? kPc : 128};
+        step_pieces<BS>(ssh, step.st, blk, ps);
+        if (g1) step_tile_rows<BS, kSCap, true>(s1l, srt, ssh, step.st, blk, &tpre, ps);
+        else step_tile_rows<BS, kSCap, false>(s1l, srt, ssh, step.st, blk, &tpre, ps);
+    }
+    CRANE_TSTAMP(a.trace, blockIdx.x, 4);
+}
+
+template <int PD, int PR>
+static hipError_t launch_t(const K1Args& a, const K1Step& sa, hipStream_t st) {
+    const unsigned grid = (unsigned)((a.N + 255) / 256);
+    return klaunch("k1_stream_steps", k1_stream_steps<PD, PR>, dim3(grid), dim3(256), 0, st, a, sa);
+}
+
+hipError_t launch_stream_steps(int pd, int pr, const K1Args& a, const K1Step& sa, hipStream_t st) {
+    if (a.N <= 0) return hipSuccess;
+    if (pd <= 4 && pr <= 6) return launch_t<4, 6>(a, sa, st);
+    if (pd <= 8 && pr <= 8) return launch_t<8, 8>(a, sa, st);
+    return launch_t<16, 16>(a, sa, st);
+}
+
+}  // namespace crane

@@ -72,6 +72,36 @@ __device__ __forceinline__ void rec_hot_annotation(double h, int64_t t, NodeRec<
     r.e_hv = (t != kTsInvalid && !(h < 0.0)) ? sat_add(t, kHotActiveNs) : kTsInvalid;
 }
 
+// Hot-value part of the record from the node's K2 window-rank buckets bc[r]
+// (annotateNodeHotValue, node.go:113-121: value += count / p.Count, Go int division;
+// window w counts the bindings of buckets >= its cutoff rank): one running suffix sum.
+// cnt_out / hvc_out (null: not kept): the per-window counts and the value.
+template <int PD, int PR>
+__device__ __forceinline__ void rec_hot_counts(const DevPolicy& pol, const uint32_t (&bc)[kMaxWin], int64_t N, int64_t n,
+                                               uint32_t* __restrict__ cnt_out, double* __restrict__ hvc_out,
+                                               int64_t hv_ts_counts, NodeRec<PD, PR>& r) {
+    int64_t v = 0;
+    uint64_t suf = 0;
+#pragma unroll
+    for (int k = kMaxWin - 1; k >= 0; --k) {
+        if (k >= pol.n_win) continue;
+        suf += bc[k];
+        const int w = pol.win_of_rank[k];
+        if (cnt_out) cnt_out[(int64_t)w * N + n] = (uint32_t)suf;
+        // Go int division (truncates toward 0): exact multiply-high division when the
+        // count fits 32 bits and hotValue.count is in [1, 2^32)
+        if (pol.win_div_m[k] != 0 && suf <= 0xFFFFFFFFull)
+            v += (int64_t)div_magic((uint32_t)suf, pol.win_div_m[k], pol.win_div_sh[k]);
+        else
+            v += (int64_t)suf / pol.win_count[w];
+    }
+    // the plugin re-reads it via ParseFloat (exact) and rejects negatives (stats.go:71-73)
+    const double h = (double)v;
+    if (hvc_out) hvc_out[n] = h;  // kept for node passes after the buckets are consumed
+    r.pen = go_int(h * 10.0);
+    r.e_hv = v >= 0 ? sat_add(hv_ts_counts, kHotActiveNs) : kTsInvalid;
+}
+
 // The Filter rejects iff now < e_fail = max over the predicates' expiries.
 template <int PD, int PR>
 __device__ __forceinline__ void rec_fail(NodeRec<PD, PR>& r) {
