@@ -417,8 +417,12 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     HotPart gx = hot_dedupe_geometry(Bk, h->N, dp.n_win, h->opt.k1_threads);
     gx.trace = gx.nblk <= kTraceWgs ? h->trace_region(0) : nullptr;
     if (h->opt.k2_form == 0 && gx.ok) {
-        // one launch (+ K3p); the node pass counts its own block's entries (no buckets)
-        HIPTRY(h, h->k2_sorted.reserve(hot_dedupe_scratch(gx)));
+        // one launch (+ K3p); the node pass counts its own block's entries (no buckets).  The
+        // scratch is sized for the whole log, not this refresh's suffix: the suffix moves with
+        // `now`, and a reallocation (hipFree waits for the device) inside a pipeline of batches
+        // cost 30-55 us per batch when the batch times advanced
+        const HotPart gf = hot_dedupe_geometry(h->B, h->N, dp.n_win, h->opt.k1_threads);
+        HIPTRY(h, h->k2_sorted.reserve(std::max(hot_dedupe_scratch(gx), gf.ok ? hot_dedupe_scratch(gf) : 0)));
         HIPTRY(h, launch_hot_count_dedupe(bn, h->bts.p, Bk, h->N, by_pos ? pcut : cut, gx, h->k2_sorted.p, st, pods,
                                           h->opt.k2x_threads));
         if (pods_done) *pods_done = pods != nullptr && pods->P > 0;
@@ -434,7 +438,8 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     if ((h->opt.k2_form == 0 || h->opt.k2_form == 3) && gl.ok) {
         // the region pass with coarse bins + the dense per-bin histogram: every bucket row
         // is rewritten, so nothing is zeroed before and K1 leaves them
-        HIPTRY(h, h->k2_sorted.reserve(hot_dedupe_scratch(gl)));
+        const HotPart gf = hot_large_geometry(h->B, h->N, dp.n_win, h->opt.k2l_region, h->opt.k2l_co_t);
+        HIPTRY(h, h->k2_sorted.reserve(std::max(hot_dedupe_scratch(gl), gf.ok ? hot_dedupe_scratch(gf) : 0)));
         HIPTRY(h, launch_hot_count_large(bn, h->bts.p, Bk, h->N, by_pos ? pcut : cut, gl, h->k2_sorted.p,
                                          h->buckets.p, h->n_cu, st, h->opt.k2l_threads));
         h->buckets_zero = false;

@@ -328,6 +328,15 @@ int crane_dyn_group_create(const crane_policy* pol, int32_t n_dev, const int32_t
     g->b_now.assign((size_t)n_dev, nullptr);
     g->b_keys.assign((size_t)n_dev, nullptr);
     g->b_flags.assign((size_t)n_dev, nullptr);
+    // the slots' streams first, then the engines (each creates a stream of its own, idle here):
+    // the runtime deals a device's streams round-robin over its hardware queues (4 on the box),
+    // so the depth streams the batches run on get distinct queues
+    for (int s = 0; s < depth; ++s)
+        for (int i = 0; i < n_dev; ++i) {
+            e = hipSetDevice(dv[(size_t)i]);
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->st[(size_t)s][(size_t)i], hipStreamNonBlocking);
+            if (e != hipSuccess) return g->hipfail(e, "hipStreamCreate");
+        }
     for (int s = 0; s < depth; ++s)
         for (int i = 0; i < n_dev; ++i) {
             crane_dyn* eg = nullptr;
@@ -337,9 +346,6 @@ int crane_dyn_group_create(const crane_policy* pol, int32_t n_dev, const int32_t
                 g->err = eg ? crane_dyn_last_error(eg) : "engine creation failed";
                 return rc;
             }
-            e = hipSetDevice(dv[(size_t)i]);
-            if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->st[(size_t)s][(size_t)i], hipStreamNonBlocking);
-            if (e != hipSuccess) return g->hipfail(e, "hipStreamCreate");
         }
     g->n = n_dev;
     return CRANE_OK;

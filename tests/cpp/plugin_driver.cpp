@@ -161,14 +161,20 @@ int main() {
                 }
             std::vector<double> val(R * N);
             std::vector<int64_t> ts(R * N);
+            // (the plugin's zone: tzdata when present, else the fixed-offset table, as NewDynamicScheduler)
             crane_tz* zone = nullptr;
             const char* tzenv = std::getenv("TZ");
-            if (crane_tz_load(tzenv && *tzenv ? tzenv : "Asia/Shanghai", nullptr, &zone)) {
+            const char* zname = tzenv && *tzenv ? tzenv : "Asia/Shanghai";
+            int64_t off = 0;
+            if (crane_tz_load(zname, nullptr, &zone) == 0) {
+                crane_parse_annotations_tz((int64_t)(R * N), strs.data(), lens.data(), zone, val.data(), ts.data(), 4);
+                crane_tz_free(zone);
+            } else if (crane_tz_offset(zname, &off) == 0) {
+                crane_parse_annotations((int64_t)(R * N), strs.data(), lens.data(), off, val.data(), ts.data(), 4);
+            } else {
                 std::cout << "GERR\tzone\n";
                 continue;
             }
-            crane_parse_annotations_tz((int64_t)(R * N), strs.data(), lens.data(), zone, val.data(), ts.data(), 4);
-            crane_tz_free(zone);
             const size_t M = R - 1;
             if (gcheck(crane_dyn_group_upload_nodes(grp, (int64_t)N, val.data(), ts.data(), val.data() + M * N,
                                                     ts.data() + M * N),

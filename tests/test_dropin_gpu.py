@@ -260,9 +260,8 @@ def test_resize_then_update_equals_fresh_engine_all_time():
     fresh = engine_for(spec)
     fresh.upload_nodes(val, ts, full.hv, full.hv_ts)
     ref = fresh.node_steps(lo, hi)
-    for a, b in zip(tab, ref):
-        assert np.array_equal(a, b)
-    assert np.array_equal(eng.node_steps(lo, hi)[0], ref[0])  # (a full rebuild on the grown engine too)
+    assert same_tables(tab, ref)
+    assert same_tables(eng.node_steps(lo, hi), ref)  # (a full rebuild on the grown engine too)
     from oracle import oracle as O
     okm = (ts != TS_INVALID).astype(np.uint8)
     for p in range(0, 64, 9):  # pods half an hour apart: one table answers them all
@@ -273,9 +272,7 @@ def test_resize_then_update_equals_fresh_engine_all_time():
                                  np.zeros(1, np.uint8))
         assert np.array_equal(ff, off[0]) and np.array_equal(sc, osc[0]), p
     eng.resize_nodes(3300)
-    tab2 = eng.node_steps(lo, hi)
-    for a, b in zip(tab2, ref):
-        assert np.array_equal(a, b[:3300])
+    assert same_tables(eng.node_steps(lo, hi), [x[:3300] for x in ref])
     fresh.close()
     eng.close()
 

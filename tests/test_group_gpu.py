@@ -133,8 +133,11 @@ def test_group_errors_and_empty_shards():
         g.schedule(int(c.now[0]), int(c.now[0]), c.now, c.ds)  # "collective" 1 with n > 1: RCCL
     g.set_option("collective", 0)
     assert g.shard(3)[1:] == (3, 3)
-    ch, _ = g.schedule(int(c.now[0]), int(c.now[0]), c.now, c.ds)
-    _, _, och = oracle_soa(spec, c, want_matrix=False)
+    now = int(c.now[0])
+    ch, _ = g.schedule(now, now, c.now, c.ds)
+    # (a batch takes its hot values from the binding log at `now`: none uploaded, all 0)
+    _, _, och = oracle_soa(spec, c, want_matrix=False,
+                           hv_override=(np.zeros(c.n_nodes), np.full(c.n_nodes, now, np.int64)))
     assert np.array_equal(ch, och)
     g.close()
 

@@ -130,6 +130,87 @@ def test_step_at_large_n():
     assert np.array_equal(out[1][0], out[0][0]) and np.array_equal(out[1][1], out[0][1])
 
 
+def _oracle_hv(spec, c, now_ns):
+    from oracle import oracle as O
+    _, hv = O.hot_values(spec, c.b_node, c.b_ts, c.n_nodes, now_ns // 10**9)
+    return hv.astype(np.float64), np.full(c.n_nodes, now_ns, np.int64)
+
+
+def test_step_replayed_batches_with_binding_log():
+    """The bench's step (K2 refresh -> keys-only eval) replayed on one stream: K1
+    consumes the K2 buckets and zeroes K2's bin cursors in-stream, so every
+    replay must give the oracle's choices with hot values from the log."""
+    import torch
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 20000, 3000, n_bindings=200_000, seed=25, pod_step_ns=3_000_000)
+    eng = engine_for(spec, c)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    now = int(synth.NOW0_NS)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
+    _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=_oracle_hv(spec, c, now))
+    with torch.cuda.stream(st):
+        for rep in range(4):
+            eng.refresh_hot_values_async(now, now, st.cuda_stream)
+            eng.eval_keys_async(d_now, d_flags, d_keys, st.cuda_stream)
+            st.synchronize()
+            ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
+            assert np.array_equal(ch, och), rep
+
+
+def test_hot_values_kept_after_consumption():
+    """After the node pass has consumed the K2 buckets, a later node pass (records
+    made stale by greedy) still sees the refreshed binding-log hot values."""
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 3000, 500, n_bindings=40_000, seed=26, pod_step_ns=0)
+    eng = engine_for(spec, c)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    now = int(c.now[0])
+    eng.refresh_hot_values(now, now)
+    _, _, ch1, _ = eng.eval(c.now, c.ds)          # consumes the counts
+    eng.greedy(50, now, c.ds[:50])                # refreshes at the same now, leaves records stale
+    ff, sc, ch2, _ = eng.eval(c.now, c.ds, matrix=True)   # K1 again from the kept hot values (pair kernel)
+    off, osc, och = oracle_soa(spec, c, hv_override=_oracle_hv(spec, c, now))
+    assert np.array_equal(ch1, och) and np.array_equal(ch2, och)
+    assert np.array_equal(ff, off) and np.array_equal(sc, osc)
+
+
+@pytest.mark.parametrize("ride,pods", [(1, 5000), (0, 5000), (1, 1), (1, 300), (1, 2048)])
+def test_step_keys_async_matches_oracle(ride, pods):
+    """crane_dyn_step_keys_async replayed (K3p riding in K2x's launch or in its own):
+    each step equals the oracle with binding-log hot values; with kernel timing on
+    too (dispatch-stamped events name every kernel of the step)."""
+    import torch
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 30000, pods, n_bindings=300_000, seed=27, pod_step_ns=2_000_000, ds_frac=0.02)
+    eng = engine_for(spec, c, opts={"k3p_in_k2": ride})
+    eng.upload_bindings(c.b_node, c.b_ts)
+    now = int(synth.NOW0_NS)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
+    _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=_oracle_hv(spec, c, now))
+    with torch.cuda.stream(st):
+        for rep in range(4):
+            eng.set_profiling(rep == 3)
+            eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
+            st.synchronize()
+            ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
+            assert np.array_equal(ch, och), rep
+    times = eng.stage_times()
+    names = [n for n, _ in times]
+    if ride:
+        assert names == ["k2x_dedupe+k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
+    else:
+        assert names == ["k2x_dedupe", "k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
+    assert all(0 < t < 50 for _, t in times), times
+
+
 @pytest.mark.parametrize("k2", [0, 1, 2, 3], ids=["dedupe", "binned", "hash", "large"])
 def test_step_keys_async_k2_forms(k2):
     """The combined step with each K2 form (dedupe: counts consumed by the fused node
