@@ -179,35 +179,26 @@ constexpr int kXChunk = kHxRegion;  // bindings per dedupe-form workgroup (K1 re
 // bin for the hottest bins instead).
 constexpr int kDSlots = 4096;  // 2 slots per binding: an empty or matching slot always exists
 
-// One LDS hash slot packs (key << 32 | count): a probe is one 64-bit access, and a key already
-// present costs one plain read + one add (round 4's split key / count arrays took a returning
-// CAS on the key array and an add on the count array for every key).
-constexpr unsigned long long kSlotEmpty = 0xFFFFFFFF00000000ull;  // key -1, count 0
-
-// Adds `add` to key's count; a lane that inserts a new key also counts it in its bin and
-// returns its slot (else -1).  A slot, once holding a key, keeps it for the phase, so the plain
-// read first tells a matching and a foreign slot apart; only an empty slot takes the CAS.
+// (Round 5 measured one packed 64-bit (key << 32 | count) slot with a plain read before the CAS
+// against these split key / count arrays: k2l_partition 0.042 -> 0.048 ms on the ordered log,
+// 0.063 -> 0.071 on the stamp path, cold 4M x 16M: reverted.)
+// Adds `add` to key's count; a lane that inserts a new key also counts it in its
+// bin and returns its slot (else -1).  One returning LDS atomic per probe (the CAS
+// itself tells an empty, a matching and a foreign slot apart).
 template <int SLOTS = kDSlots>
-__device__ __forceinline__ int32_t hash_add(unsigned long long* hs, uint32_t* hist, int bb, int32_t key, uint32_t add) {
+__device__ __forceinline__ int32_t hash_add(int32_t* hkey, uint32_t* hcnt, uint32_t* hist, int bb, int32_t key,
+                                            uint32_t add) {
     constexpr int kBits = __builtin_ctz(SLOTS);
     uint32_t h = ((uint32_t)key * 2654435761u) >> (32 - kBits);
-    const unsigned long long mine = (unsigned long long)(uint32_t)key << 32;
     for (;;) {  // ends: at most SLOTS / 2 distinct keys
-        const unsigned long long cur = __hip_atomic_load(&hs[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if ((cur & 0xFFFFFFFF00000000ull) == mine) {
-            atomicAdd(&hs[h], (unsigned long long)add);
-            return -1;
-        }
-        if (cur == kSlotEmpty) {
-            const unsigned long long old = atomicCAS(&hs[h], kSlotEmpty, mine | add);
-            if (old == kSlotEmpty) {
+        const int32_t old = atomicCAS(&hkey[h], -1, key);
+        if (old == -1 || old == key) {
+            atomicAdd(&hcnt[h], add);
+            if (old == -1) {
                 atomicAdd(&hist[(key >> 3) >> bb], 1u);
                 return (int32_t)h;
             }
-            if ((old & 0xFFFFFFFF00000000ull) == mine) {
-                atomicAdd(&hs[h], (unsigned long long)add);
-                return -1;
-            }
+            return -1;
         }
         h = (h + 1) & (SLOTS - 1);
     }
@@ -219,8 +210,8 @@ __device__ __forceinline__ int32_t hash_add(unsigned long long* hs, uint32_t* hi
 // the wave's own segment of uniq (KPER * 64 entries: no shared counter); returns how many
 // (uniform).  (More leader rounds for the next repeated keys measured slower at config 3.)
 template <int SLOTS, int KPER>
-__device__ __forceinline__ uint32_t wave_aggregate(const int32_t* key, unsigned long long* hs, uint32_t* hist, int bb,
-                                                   uint16_t* useg) {
+__device__ __forceinline__ uint32_t wave_aggregate(const int32_t* key, int32_t* hkey, uint32_t* hcnt, uint32_t* hist,
+                                                   int bb, uint16_t* useg) {
     const int lane = threadIdx.x & 63;
     uint32_t nw = 0;
 #pragma unroll
@@ -232,7 +223,7 @@ __device__ __forceinline__ uint32_t wave_aggregate(const int32_t* key, unsigned 
         const int32_t kl = __builtin_amdgcn_readlane(key[u], lead);
         const uint64_t m = __ballot(ok && key[u] == kl);
         const bool mine = lane == lead || (ok && key[u] != kl);
-        const int32_t slot = mine ? hash_add<SLOTS>(hs, hist, bb, lane == lead ? kl : key[u],
+        const int32_t slot = mine ? hash_add<SLOTS>(hkey, hcnt, hist, bb, lane == lead ? kl : key[u],
                                                     lane == lead ? (uint32_t)__popcll(m) : 1u)
                                   : -1;
         const uint64_t nm = __ballot(slot >= 0);
@@ -246,12 +237,13 @@ template <int BT, bool POS>
 __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __restrict__ bnode,
                                          const int64_t* __restrict__ bts, int64_t B, int64_t N, const HotCutoffs& cut,
                                          const HotPart& g, uint32_t* __restrict__ CO, uint32_t* __restrict__ region) {
-    // hash slots u64 [kDSlots], hist, off [nbins], uniq u16 [kXChunk]
+    // hkey, hcnt [kDSlots], hist, off [nbins], uniq u16 [kXChunk]
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     constexpr int kPer = kXChunk / BT;  // bindings per thread
     __shared__ uint32_t part[BT];
-    unsigned long long* hs = reinterpret_cast<unsigned long long*>(sh);
-    uint32_t* hist = sh + 2 * kDSlots;
+    int32_t* hkey = reinterpret_cast<int32_t*>(sh);
+    uint32_t* hcnt = sh + kDSlots;
+    uint32_t* hist = hcnt + kDSlots;
     uint32_t* off = hist + g.nbins;
     uint16_t* uniq = reinterpret_cast<uint16_t*>(off + g.nbins);
     CRANE_TSTAMP(g.trace, blk, 0);
@@ -265,7 +257,10 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
         ts[u] = POS ? b : bts[bc];  // POS: the window rank from the position, no stamp loaded
         if (b >= B) nd[u] = -1;
     }
-    for (int i = threadIdx.x; i < kDSlots; i += BT) hs[i] = kSlotEmpty;
+    for (int i = threadIdx.x; i < kDSlots; i += BT) {
+        hkey[i] = -1;
+        hcnt[i] = 0;
+    }
     for (int i = threadIdx.x; i < g.nbins; i += BT) hist[i] = 0;
     __syncthreads();
     CRANE_TSTAMP(g.trace, blk, 1);
@@ -277,7 +272,7 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
         key[u] = ok ? nd[u] * 8 + (j - 1) : -1;
     }
     uint16_t* useg = uniq + (threadIdx.x >> 6) * (kPer * 64);
-    const uint32_t nw = wave_aggregate<kDSlots, kPer>(key, hs, hist, g.bb, useg);
+    const uint32_t nw = wave_aggregate<kDSlots, kPer>(key, hkey, hcnt, hist, g.bb, useg);
     __syncthreads();
     CRANE_TSTAMP(g.trace, blk, 2);
     const int per = (g.nbins + BT - 1) / BT;
@@ -300,10 +295,10 @@ __device__ __forceinline__ void k2d_body(const int32_t blk, const int32_t* __res
     uint32_t* reg = region + (int64_t)blk * kXChunk;
     const uint32_t mask = (1u << g.bb) - 1;
     for (uint32_t i = threadIdx.x & 63; i < nw; i += 64) {  // this wave's new keys
-        const unsigned long long v = hs[useg[i]];
-        const int32_t k = (int32_t)(v >> 32);
+        const int s = useg[i];
+        const int32_t k = hkey[s];
         const uint32_t p = atomicAdd(&off[(k >> 3) >> g.bb], 1u);
-        reg[p] = ((uint32_t)(k >> 3) & mask) | ((uint32_t)(k & 7) << 16) | ((uint32_t)v << 19);
+        reg[p] = ((uint32_t)(k >> 3) & mask) | ((uint32_t)(k & 7) << 16) | (hcnt[s] << 19);
     }
     CRANE_TSTAMP(g.trace, blk, 4);
 }
@@ -420,14 +415,18 @@ void k2l_partition(const int32_t* __restrict__ bnode,
                                                     uint32_t* __restrict__ region) {
     constexpr int kPer = REG / BT;   // bindings per thread per region
     constexpr int kSlots = 2 * REG;  // an empty or matching slot always exists
-    // hash slots u64 [kSlots], hist, off [nbins], uniq u16 [REG]
+    // hkey, hcnt [kSlots], hist, off [nbins], uniq u16 [REG]
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     __shared__ uint32_t part[BT];
-    unsigned long long* hs = reinterpret_cast<unsigned long long*>(sh);
-    uint32_t* hist = sh + 2 * kSlots;
+    int32_t* hkey = reinterpret_cast<int32_t*>(sh);
+    uint32_t* hcnt = sh + kSlots;
+    uint32_t* hist = hcnt + kSlots;
     uint32_t* off = hist + g.nbins;
     uint16_t* useg = reinterpret_cast<uint16_t*>(off + g.nbins) + (threadIdx.x >> 6) * (kPer * 64);
-    for (int i = threadIdx.x; i < kSlots; i += BT) hs[i] = kSlotEmpty;
+    for (int i = threadIdx.x; i < kSlots; i += BT) {
+        hkey[i] = -1;
+        hcnt[i] = 0;
+    }
     for (int i = threadIdx.x; i < g.nbins; i += BT) hist[i] = 0;
     auto load = [&](int64_t r, int32_t* nd, int64_t* ts) {  // unconditional loads, clamped index
         const int64_t b0 = r * REG + threadIdx.x;
@@ -460,7 +459,7 @@ void k2l_partition(const int32_t* __restrict__ bnode,
             const bool ok = nd[u] >= 0 && (int64_t)nd[u] < N && j > 0;  // binding.go:85-91
             key[u] = ok ? nd[u] * 8 + (j - 1) : -1;
         }
-        const uint32_t nw = wave_aggregate<kSlots, kPer>(key, hs, hist, g.bb, useg);
+        const uint32_t nw = wave_aggregate<kSlots, kPer>(key, hkey, hcnt, hist, g.bb, useg);
         __syncthreads();
         CRANE_TSTAMP(g.trace, r, 1);
         uint32_t sum = 0;
@@ -478,10 +477,10 @@ void k2l_partition(const int32_t* __restrict__ bnode,
         uint32_t* reg = region + r * REG;
         for (uint32_t i = threadIdx.x & 63; i < nw; i += 64) {  // this wave's entries; its slots cleared
             const int s = useg[i];
-            const unsigned long long v = hs[s];
-            const int32_t k = (int32_t)(v >> 32);
-            const uint32_t cnt = (uint32_t)v;
-            hs[s] = kSlotEmpty;
+            const int32_t k = hkey[s];
+            const uint32_t cnt = hcnt[s];
+            hkey[s] = -1;
+            hcnt[s] = 0;
             const uint32_t p = atomicAdd(&off[(k >> 3) >> g.bb], 1u);
             reg[p] = ((uint32_t)(k >> 3) & mask) | ((uint32_t)(k & 7) << 16) | (cnt << 19);
         }

@@ -30,98 +30,106 @@ namespace crane {
 //      (node, kind) items from the LDS records (step_emit_one);
 //   D  the fused pass's tail: sort + publish, elementary pieces, tile rows.
 // Not with the dedupe-form K2 entries (their per-block counting needs the default pass's LDS).
-// step_emit_one for a record in LDS, register-light: every field is read from LDS where it is
-// used, in rolled loops (no copy of the record is kept in registers — a record held in registers
-// anywhere in the kernel would set the VGPR count of every wave), and the in-range expiries are
-// walked in ascending order, with multiplicity, by repeated minimum searches instead of being
-// sorted in registers.  The outputs are step_emit_one's, bit for bit.
+// step_emit_one's outputs for the stepped (node, kind) items of a chunk, spread over the lanes:
+// item i takes lanes (tasks) i * NB + q, q = 0 .. NB - 1, and task q handles the q-th smallest
+// of the kind's in-range expiries c_q (with multiplicity, found by ranking the NB expiries in
+// registers): its key, its middle piece [c_q, c_{q+1}), and — q = 0 / q = cnt - 1 — the
+// half-line records.  A single (node, kind) item's keys are then computed side by side instead of
+// one after another (round 5's first form, one lane per item walking its expiries in order with
+// the record read from LDS term by term, spent 4.9 us per workgroup here: a chain of dependent
+// LDS reads).  The outputs are step_emit_one's, bit for bit.
+__device__ __forceinline__ int64_t readfirstlane64(int64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// score_at for a record in LDS with its terms read one at a time (a rolled loop: two fields in
+// registers at a time — the emit's keys are computed side by side, so each one's own latency
+// matters less than the registers a copy of the record would hold)
 template <int PD, int PR>
-__device__ __forceinline__ int32_t score_at_lds(int64_t t, const NodeRec<PD, PR>* r, double wsum, int32_t noprio,
+__device__ __forceinline__ int32_t score_at_lds(int64_t t, const NodeRec<PD, PR>& r, double wsum, int32_t noprio,
                                                 double winv) {
     double s = 0.0;
 #pragma unroll 1
-    for (int k = 0; k < PR; ++k)  // (rolled: one term's two fields in registers at a time)
-        if (t < r->e_prio[k]) s += r->t[k];  // stats.go:124-133, policy order
-    return score_of_sum(s, t < r->e_hv ? r->pen : 0, wsum, noprio, winv);
+    for (int k = 0; k < PR; ++k)
+        if (t < r.e_prio[k]) s += r.t[k];  // stats.go:124-133, policy order
+    return score_of_sum(s, t < r.e_hv ? r.pen : 0, wsum, noprio, winv);
 }
+
 template <int PD, int PR>
-__device__ __forceinline__ void emit_lds(const NodeRec<PD, PR>* r, int64_t n, int T, int32_t slot, int32_t mslot,
-                                         bool multi, int64_t tmin, int64_t tmax, double wsum, int32_t noprio,
-                                         const StepTables& st, int64_t blk, Step1* s1b, int64_t kst, double winv) {
-    const volatile NodeRec<PD, PR>* v = r;
+__device__ __forceinline__ void emit_task(const NodeRec<PD, PR>& r, int64_t n, int T, int q, int32_t slot,
+                                          int32_t mslot, bool multi, int64_t tmin, int64_t tmax, double wsum,
+                                          int32_t noprio, const StepTables& st, int64_t blk, Step1* s1b, int64_t kst,
+                                          double winv) {
     constexpr int NB = PR + 2;
-    auto field = [&](int j) -> int64_t {  // expiry j of the kind, INT64_MAX when outside (tmin, tmax]
-        const int64_t c = j < PR ? v->e_prio[j] : (j == PR ? v->e_hv : (T == 0 ? v->e_fail : INT64_MIN));
-        return c > tmin && c <= tmax ? c : INT64_MAX;
-    };
-    const int64_t e_fail = v->e_fail;
-    auto key = [&](int64_t t) {
-        const int32_t f = score_at_lds<PD, PR>(t, r, wsum, noprio, winv);
-        return (T == 1 || !(t < e_fail)) ? pack_key(f, n) : -1;
-    };
+    int64_t c[NB];
+#pragma unroll
+    for (int k = 0; k < PR; ++k) c[k] = r.e_prio[k];
+    c[PR] = r.e_hv;
+    c[PR + 1] = T == 0 ? r.e_fail : INT64_MIN;  // DaemonSet pods bypass the Filter
     int cnt = 0;
-    int64_t mn = INT64_MAX;
-#pragma unroll 1
-    for (int j = 0; j < NB; ++j) {
-        const int64_t c = field(j);
-        cnt += c != INT64_MAX;
-        mn = min(mn, c);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        const bool in = c[k] > tmin && c[k] <= tmax;
+        c[k] = in ? c[k] : INT64_MAX;
+        cnt += in;
     }
+    if (q >= cnt) return;  // (cnt >= 1: the item is stepped)
+    // ascending (odd-even transposition, static indices), then the values of ranks q and q + 1
+    // picked by selects (a dynamic index into a register array would go through scratch)
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = i & 1; j + 1 < NB; j += 2) {
+            const int64_t x = c[j], y = c[j + 1];
+            c[j] = min(x, y);
+            c[j + 1] = max(x, y);
+        }
+    int64_t cq = c[0], cn = c[1];
+#pragma unroll
+    for (int j = 1; j < NB; ++j) {
+        cq = q == j ? c[j] : cq;
+        cn = q + 1 == j ? c[j] : cn;
+    }
+    auto key = [&](int64_t t) {  // key_of for the run-time kind, at the first instant of a step
+        const int32_t f = score_at_lds<PD, PR>(t, r, wsum, noprio, winv);
+        return (T == 1 || !(t < r.e_fail)) ? pack_key(f, n) : -1;
+    };
     Step1* s1 = s1b + T * kst;
-    const int32_t k0 = key(tmin);
-    if (!multi) {
-        Step1 o;
-        o.bp = mn;
-        o.k0 = k0;
-        o.k1 = key(mn);
-        s1[slot] = o;
+    if (!multi) {  // one record: before / from the one distinct expiry
+        if (q == 0) {
+            Step1 v;
+            v.bp = cq;
+            v.k0 = key(tmin);
+            v.k1 = key(cq);
+            s1[slot] = v;
+        }
         return;
     }
-    // the in-range expiries in ascending order with multiplicity: (value, copies left)
-    int64_t cur = mn;
-    int left = 0;
-#pragma unroll 1
-    for (int j = 0; j < NB; ++j) left += field(j) == mn;
-    auto next = [&]() {
-        if (--left > 0) return;
-        int64_t m = INT64_MAX;
-#pragma unroll 1
-        for (int j = 0; j < NB; ++j) {
-            const int64_t c = field(j);
-            m = c > cur && c < m ? c : m;
-        }
-        cur = m;
-#pragma unroll 1
-        for (int j = 0; j < NB; ++j) left += field(j) == m;
-    };
-    Mid* md = st.mid + (int64_t)T * st.mpad + blk * st.mstride + mslot;
-    int32_t kprev = k0;
-    int64_t last = mn;
-#pragma unroll 1
-    for (int j = 0; j < cnt; ++j) {
-        const int64_t cj = cur;
-        const int32_t kj = key(cj);  // the key from c[j] on
-        if (j + 1 < cnt) {
-            next();
-            Mid p;
-            p.s = cj;
-            p.e = cur;
-            p.key = kj;
-            p.pad = 0;
-            md[j] = p;
-        }
-        last = cj;
-        kprev = kj;
+    const int32_t kq = key(cq);  // the key from c_q on
+    if (q + 1 < cnt) {
+        Mid p;
+        p.s = cq;
+        p.e = cn;
+        p.key = kq;
+        p.pad = 0;
+        (st.mid + (int64_t)T * st.mpad + blk * st.mstride + mslot)[q] = p;
     }
-    Step1 x, y;
-    x.bp = mn;
-    x.k0 = k0;
-    x.k1 = -1;
-    y.bp = last;
-    y.k0 = -1;
-    y.k1 = kprev;
-    s1[slot] = x;
-    s1[slot + 1] = y;
+    if (q == 0) {
+        Step1 x;
+        x.bp = cq;
+        x.k0 = key(tmin);
+        x.k1 = -1;
+        s1[slot] = x;
+    }
+    if (q == cnt - 1) {
+        Step1 y;
+        y.bp = cq;
+        y.k0 = -1;
+        y.k1 = kq;
+        s1[slot + 1] = y;
+    }
 }
 
 constexpr int kSRec = 64;   // stepped records staged per chunk
@@ -181,9 +189,8 @@ void k1_stream_steps(K1Args a, K1Step step) {
         hvl = a.hv[first + lo];
         hvt = a.hv_ts ? a.hv_ts[first + lo] : a.hv_ts_counts;
     }
-    const int64_t tmin = step.batch[0], tmax = step.batch[1];  // K3p folded the batch range
-    int64_t tpre = 0;  // this thread's first tile-row bound (step_tile_rows)
-    if (step.st.rows) tile_prefetch(step.st, &tpre);
+    // the batch range K3p folded, uniform: kept in SGPRs
+    const int64_t tmin = readfirstlane64(step.batch[0]), tmax = readfirstlane64(step.batch[1]);
     if (threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
     CRANE_TSTAMP(a.trace, blockIdx.x, 1);
     const bool valid = n < N;
@@ -341,13 +348,14 @@ void k1_stream_steps(K1Args a, K1Step step) {
             lrec[j].t[k] = term;
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < 2 * m; i += BS) {
-            const int j = i >> 1, T = i & 1;
+        constexpr int NB = PR + 2;
+        for (int tk = threadIdx.x; tk < 2 * m * NB; tk += BS) {
+            const int i = tk / NB, q = tk - i * NB, j = i >> 1, T = i & 1;
             const int32_t* dw = reinterpret_cast<const int32_t*>(lrec[j].e_pred);
             const int32_t sl = dw[T ? 2 : 0];
             if (sl < 0) continue;
-            emit_lds<PD, PR>(&lrec[j], first + rank_lane[c0 + j], T, sl, dw[T ? 3 : 1], ((dw[4] >> T) & 1) != 0, tmin,
-                             tmax, step.wsum, step.noprio, step.st, blk, s1b, kst, step.winv);
+            emit_task<PD, PR>(lrec[j], first + rank_lane[c0 + j], T, q, sl, dw[T ? 3 : 1], ((dw[4] >> T) & 1) != 0,
+                              tmin, tmax, step.wsum, step.noprio, step.st, blk, s1b, kst, step.winv);
         }
         __syncthreads();  // (the chunk's records are reused by the next chunk)
     }
@@ -357,6 +365,8 @@ void k1_stream_steps(K1Args a, K1Step step) {
     else step_sort_publish<BS, kSCap>(s1l, srt, ssh, step.st, blk);
     CRANE_TSTAMP(a.trace, blockIdx.x, 6);
     if (step.st.rows) {
+        int64_t tpre = 0;  // this thread's first tile-row bound (step_tile_rows)
+        tile_prefetch(step.st, &tpre);
         // the middle pieces' scratch: the staged records' LDS (dead after the emit)
         constexpr int kPc = ((int)sizeof(lrec) / PieceScr::bytes_per_piece) & ~3;
         const PieceScr ps{reinterpret_cast<unsigned char*>(lrec), kPc < 128 ? kPc : 128};

@@ -328,6 +328,7 @@ class DynamicScheduler {
     struct View {
         std::vector<const NodeInfo*> infos;  // row -> the snapshot's NodeInfo (null: a free row)
         std::vector<const Node*> nodes;      // row -> the Node object the row was parsed from
+        std::vector<std::string> names;      // ... its name (a departed node's objects may be freed)
         std::vector<int64_t> gens;           // ... and its NodeInfo's Generation
         std::vector<uint32_t> seen;          // row -> the last snapshot scan that found its NodeInfo
         std::vector<int64_t> free_rows;      // (popped from the back: lowest row first)
@@ -345,6 +346,7 @@ class DynamicScheduler {
         void grow(size_t n) {
             infos.resize(n, nullptr);
             nodes.resize(n, nullptr);
+            names.resize(n);
             gens.resize(n, 0);
             seen.resize(n, 0);
             n_steps.resize(n, 0);
@@ -482,7 +484,10 @@ class DynamicScheduler {
             v->infos[i] = L[i];
             v->nodes[i] = L[i]->node();
             v->gens[i] = L[i]->Generation;
-            if (v->nodes[i]) v->by_name.emplace(v->nodes[i]->Name, (int64_t)i);
+            if (v->nodes[i]) {
+                v->names[i] = v->nodes[i]->Name;
+                v->by_name.emplace(v->names[i], (int64_t)i);
+            }
         }
         v->live = N;
         v->index_infos();
@@ -505,13 +510,12 @@ class DynamicScheduler {
     // eighth when none is left) and join the changed rows, whose columns update() writes.
     bool membership(View* v, const std::vector<const NodeInfo*>& L, std::string* err) {
         for (int64_t r : removed_) {
-            const Node* n = v->nodes[(size_t)r];
-            if (n) {
-                auto it = v->by_name.find(n->Name);
-                if (it != v->by_name.end() && it->second == r) v->by_name.erase(it);
-            }
+            // (by the kept name: the snapshot may have freed the departed node's objects)
+            auto it = v->by_name.find(v->names[(size_t)r]);
+            if (it != v->by_name.end() && it->second == r) v->by_name.erase(it);
             v->infos[(size_t)r] = nullptr;
             v->nodes[(size_t)r] = nullptr;
+            v->names[(size_t)r].clear();
             v->free_rows.push_back(r);
             --v->live;
         }
@@ -538,7 +542,10 @@ class DynamicScheduler {
             v->gens[(size_t)r] = ni->Generation;
             v->seen[(size_t)r] = epoch_;
             v->info_idx.put(ni, r);
-            if (ni->node()) v->by_name[ni->node()->Name] = r;
+            if (ni->node()) {
+                v->names[(size_t)r] = ni->node()->Name;
+                v->by_name[v->names[(size_t)r]] = r;
+            }
             ++v->live;
             changed_.push_back(r);
         }
