@@ -505,7 +505,7 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
     }
     a.threads = k1_bs(h);
     a.trace = (h->N + a.threads - 1) / a.threads <= kTraceWgs ? h->trace_region(1) : nullptr;
-    HIPTRY(h, launch_node_pass(h->shape, a, st, step, h->opt.k1_stream != 0));
+    HIPTRY(h, launch_node_pass(h->shape, a, st, step, h->opt.k1_stream));
     if (consume) {
         if (!h->hx_pending) h->buckets_zero = !h->buckets_dense;  // K1 zeroed what it read
         h->counts_pending = false;

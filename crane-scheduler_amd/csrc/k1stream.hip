@@ -51,16 +51,19 @@ template <int PD, int PR>
 __device__ __forceinline__ int32_t score_at_lds(int64_t t, const NodeRec<PD, PR>& r, double wsum, int32_t noprio,
                                                 double winv) {
     double s = 0.0;
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < PR; ++k)
         if (t < r.e_prio[k]) s += r.t[k];  // stats.go:124-133, policy order
     return score_of_sum(s, t < r.e_hv ? r.pen : 0, wsum, noprio, winv);
 }
 
+constexpr int kSRec = 64;   // stepped records staged per chunk
+constexpr int kSCap = 128;  // one-step records per kind staged in LDS (more: st.stage)
+
 template <int PD, int PR>
 __device__ __forceinline__ void emit_task(const NodeRec<PD, PR>& r, int64_t n, int T, int q, int32_t slot,
                                           int32_t mslot, bool multi, int64_t tmin, int64_t tmax, double wsum,
-                                          int32_t noprio, const StepTables& st, int64_t blk, Step1* s1b, int64_t kst,
+                                          int32_t noprio, const StepTables& st, int64_t blk, const S1Out& s1o,
                                           double winv) {
     constexpr int NB = PR + 2;
     int64_t c[NB];
@@ -69,41 +72,42 @@ __device__ __forceinline__ void emit_task(const NodeRec<PD, PR>& r, int64_t n, i
     c[PR] = r.e_hv;
     c[PR + 1] = T == 0 ? r.e_fail : INT64_MIN;  // DaemonSet pods bypass the Filter
     int cnt = 0;
+    uint32_t inm = 0;  // in-range expiries
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
         const bool in = c[k] > tmin && c[k] <= tmax;
-        c[k] = in ? c[k] : INT64_MAX;
+        inm |= in ? 1u << k : 0u;
         cnt += in;
     }
-    if (q >= cnt) return;  // (cnt >= 1: the item is stepped)
-    // ascending (odd-even transposition, static indices), then the values of ranks q and q + 1
-    // picked by selects (a dynamic index into a register array would go through scratch)
+    // the task's expiry c[q] and its rank in the ascending order of (c, index), and the next one's
+    // value: a rank among NB registers (static indices) instead of a sort
+    if (!((inm >> q) & 1u)) return;  // out of range
+    int64_t cq = c[0];
 #pragma unroll
-    for (int i = 0; i < NB; ++i)
+    for (int j = 1; j < NB; ++j) cq = q == j ? c[j] : cq;
+    int rk = 0;
+    int64_t cn = INT64_MAX;
 #pragma unroll
-        for (int j = i & 1; j + 1 < NB; j += 2) {
-            const int64_t x = c[j], y = c[j + 1];
-            c[j] = min(x, y);
-            c[j + 1] = max(x, y);
-        }
-    int64_t cq = c[0], cn = c[1];
-#pragma unroll
-    for (int j = 1; j < NB; ++j) {
-        cq = q == j ? c[j] : cq;
-        cn = q + 1 == j ? c[j] : cn;
+    for (int j = 0; j < NB; ++j) {
+        const bool in = (inm >> j) & 1u;
+        const bool before = in && (c[j] < cq || (c[j] == cq && j < q));
+        const bool after = in && (c[j] > cq || (c[j] == cq && j > q));
+        rk += before;
+        cn = after ? min(cn, c[j]) : cn;
     }
+    q = rk;
     auto key = [&](int64_t t) {  // key_of for the run-time kind, at the first instant of a step
         const int32_t f = score_at_lds<PD, PR>(t, r, wsum, noprio, winv);
         return (T == 1 || !(t < r.e_fail)) ? pack_key(f, n) : -1;
     };
-    Step1* s1 = s1b + T * kst;
+    auto put = [&](int32_t i, const Step1& v) { s1o.put(T, i, v); };
     if (!multi) {  // one record: before / from the one distinct expiry
         if (q == 0) {
             Step1 v;
             v.bp = cq;
             v.k0 = key(tmin);
             v.k1 = key(cq);
-            s1[slot] = v;
+            put(slot, v);
         }
         return;
     }
@@ -121,19 +125,17 @@ __device__ __forceinline__ void emit_task(const NodeRec<PD, PR>& r, int64_t n, i
         x.bp = cq;
         x.k0 = key(tmin);
         x.k1 = -1;
-        s1[slot] = x;
+        put(slot, x);
     }
     if (q == cnt - 1) {
         Step1 y;
         y.bp = cq;
         y.k0 = -1;
         y.k1 = kq;
-        s1[slot + 1] = y;
+        put(slot + 1, y);
     }
 }
 
-constexpr int kSRec = 64;   // stepped records staged per chunk
-constexpr int kSCap = 128;  // one-step records per kind staged in LDS (more: st.stage)
 template <int PD, int PR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PD * PR <= 24 ? 7 : 1)))
 void k1_stream_steps(K1Args a, K1Step step) {
@@ -231,17 +233,21 @@ void k1_stream_steps(K1Args a, K1Step step) {
         mn = in ? min(mn, e) : mn;
         mx = in ? max(mx, e) : mx;
     };
+    // the terms stay in registers (they replace the rows' ts / usage) until a stepped lane has
+    // its record slot (after B): no second read of the rows
+    int64_t ep[PR];
+    double tp[PR];
 #pragma unroll
     for (int k = 0; k < PR; ++k) {
-        int64_t e = kTsInvalid;
-        double term = 0.0;
+        ep[k] = kTsInvalid;
+        tp[k] = 0.0;
         if (k < pol.npr && qt[k] != kTsInvalid && !(qv[k] < 0.0)) {
-            e = sat_add(qt[k], pol.prio_dur[k]);
-            term = (1.0 - qv[k]) * pol.prio_w[k];  // getScore (stats.go:89), no FMA
-            term = term * 100.0;
+            ep[k] = sat_add(qt[k], pol.prio_dur[k]);
+            tp[k] = (1.0 - qv[k]) * pol.prio_w[k];  // getScore (stats.go:89), no FMA
+            tp[k] = tp[k] * 100.0;
         }
-        if (tmin < e) s += term;  // stats.go:124-133
-        add(e, cnt1, mn1, mx1);
+        if (tmin < ep[k]) s += tp[k];  // stats.go:124-133
+        add(ep[k], cnt1, mn1, mx1);
     }
     add(hr.e_hv, cnt1, mn1, mx1);
     int cnt0 = cnt1;
@@ -292,70 +298,57 @@ void k1_stream_steps(K1Args a, K1Step step) {
     CRANE_TSTAMP(a.trace, blockIdx.x, 3);
     // one-step records staged in LDS, or (more of a kind than it holds) in st.stage
     const bool g1 = max(ssh.lc[0][0], ssh.lc[1][0]) > min(kSCap, step.st.lds_cap);
-    Step1* s1b = g1 ? step.st.stage + blk * 2 * step.st.bs : s1l;
-    const int64_t kst = g1 ? step.st.s1pad : (int64_t)kSCap;
+    const S1Out s1o{s1l, step.st.stage + blk * 2 * step.st.bs, g1, (int64_t)kSCap, step.st.s1pad};
     // ---- C: the stepped nodes' records in LDS, chunk by chunk, and their (node, kind) items.
     // The first kSRec stepped nodes write their part (e_fail, pen, e_hv, slots) into the LDS
     // records now; any further ones into their node's record slot in HBM (step.srec, the node
     // records the keys-only step leaves stale anyway: the slots go in e_pred, which the emit does
     // not read), fetched chunk by chunk — no per-lane state lives across the chunks.
     const bool stepped = (cnt0 | cnt1) != 0;
-    if (stepped) {
-        rank_lane[rs] = (uint8_t)threadIdx.x;
-        Rec* r = rs < kSRec ? &lrec[rs] : static_cast<Rec*>(step.srec) + n;
+    auto put = [&](Rec* r) {  // (called with an LDS and a global pointer: no flat stores)
         r->e_fail = e_fail;
         r->pen = hr.pen;
         r->e_hv = hr.e_hv;
+#pragma unroll
+        for (int k = 0; k < PR; ++k) {
+            r->e_prio[k] = ep[k];
+            r->t[k] = tp[k];
+        }
         int32_t* dw = reinterpret_cast<int32_t*>(r->e_pred);
         dw[0] = slot0;
         dw[1] = mslot0;
         dw[2] = slot1;
         dw[3] = mslot1;
         dw[4] = (multi0 ? 1 : 0) | (multi1 ? 2 : 0);
+    };
+    if (stepped) {
+        rank_lane[rs] = (uint8_t)threadIdx.x;
+        if (rs < kSRec) put(&lrec[rs]);
+        else put(static_cast<Rec*>(step.srec) + n);
     }
     __syncthreads();
     for (int32_t c0 = 0; c0 < nst; c0 += kSRec) {  // (workgroup-uniform)
         const int32_t m = min(kSRec, nst - c0);
-        if (c0 > 0) {  // this chunk's parts from HBM (L2: written by this workgroup)
-            for (int i = threadIdx.x; i < m * 8; i += BS) {
-                const int j = i >> 3, f = i & 7;
+        if (c0 > 0) {  // this chunk's records from HBM (L2: written by this workgroup)
+            constexpr int W = 3 + 2 * PR + 3;  // e_fail, e_hv, pen, e_prio, t, then the slot words
+            for (int i = threadIdx.x; i < m * W; i += BS) {
+                const int j = i / W, f = i - j * W;
                 const int64_t* src = reinterpret_cast<const int64_t*>(static_cast<const Rec*>(step.srec) + first +
                                                                       rank_lane[c0 + j]);
-                int64_t* dst = reinterpret_cast<int64_t*>(&lrec[j]);
-                // e_fail, e_hv, pen (words 0-2) and the slots (e_pred's first words)
-                const int w = f < 3 ? f : (int)(offsetof(Rec, e_pred) / 8) + (f - 3);
-                if (f < 6) dst[w] = src[w];
+                reinterpret_cast<int64_t*>(&lrec[j])[f] = src[f];
             }
             __syncthreads();
         }
-        // the priority terms of the chunk's nodes, one (node, term) per lane, from L2 (rec_metrics)
-        for (int i = threadIdx.x; i < m * PR; i += BS) {
-            const int j = i / PR, k = i - j * PR;
-            const int64_t nd = first + rank_lane[c0 + j];
-            int64_t e = kTsInvalid;
-            double term = 0.0;
-            if (k < pol.npr && pol.n_slots > 0) {
-                const int64_t row = pol.prio_slot[k];
-                const int64_t t = a.ts[row * N + nd];
-                const double u = a.val[row * N + nd];
-                if (t != kTsInvalid && !(u < 0.0)) {
-                    e = sat_add(t, pol.prio_dur[k]);
-                    term = (1.0 - u) * pol.prio_w[k];
-                    term = term * 100.0;
-                }
+        {
+            constexpr int NB = PR + 2;
+            for (int tk = threadIdx.x; tk < 2 * m * NB; tk += BS) {
+                const int i = tk / NB, q = tk - i * NB, j = i >> 1, T = i & 1;
+                const int32_t* dw = reinterpret_cast<const int32_t*>(lrec[j].e_pred);
+                const int32_t sl = dw[T ? 2 : 0];
+                if (sl < 0) continue;
+                emit_task<PD, PR>(lrec[j], first + rank_lane[c0 + j], T, q, sl, dw[T ? 3 : 1], ((dw[4] >> T) & 1) != 0,
+                                  tmin, tmax, step.wsum, step.noprio, step.st, blk, s1o, step.winv);
             }
-            lrec[j].e_prio[k] = e;
-            lrec[j].t[k] = term;
-        }
-        __syncthreads();
-        constexpr int NB = PR + 2;
-        for (int tk = threadIdx.x; tk < 2 * m * NB; tk += BS) {
-            const int i = tk / NB, q = tk - i * NB, j = i >> 1, T = i & 1;
-            const int32_t* dw = reinterpret_cast<const int32_t*>(lrec[j].e_pred);
-            const int32_t sl = dw[T ? 2 : 0];
-            if (sl < 0) continue;
-            emit_task<PD, PR>(lrec[j], first + rank_lane[c0 + j], T, q, sl, dw[T ? 3 : 1], ((dw[4] >> T) & 1) != 0,
-                              tmin, tmax, step.wsum, step.noprio, step.st, blk, s1b, kst, step.winv);
         }
         __syncthreads();  // (the chunk's records are reused by the next chunk)
     }

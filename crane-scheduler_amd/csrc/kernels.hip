@@ -295,11 +295,10 @@ void k1_node_pass(K1Args a, K1Step step) {
         CRANE_TSTAMP(a.trace, blockIdx.x, 3);
         // one-step records staged in LDS, or (more of a kind than it holds) in st.stage
         const bool g1 = max(ssh.lc[0][0], ssh.lc[1][0]) > min(CAP, step.st.lds_cap);
-        Step1* s1b = g1 ? step.st.stage + blk * 2 * step.st.bs : s1l;
-        const int64_t kst = g1 ? step.st.s1pad : (int64_t)CAP;
+        const S1Out s1o{s1l, step.st.stage + blk * 2 * step.st.bs, g1, (int64_t)CAP, step.st.s1pad};
         // (a node past the staging emits first: its record then dies before the queue's)
         if (self_emit)
-            step_emit<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, so, step.st, blk, s1b, kst, step.winv);
+            step_emit<PD, PR>(r, n, tmin, tmax, step.wsum, step.noprio, so, step.st, blk, s1o, step.winv);
         // the queued items are built densely by the first lanes of the workgroup
         for (int w = threadIdx.x; w < nq; w += kK1Threads) {
             const uint32_t it = q[w];
@@ -307,7 +306,7 @@ void k1_node_pass(K1Args a, K1Step step) {
             const int o = (int)(it & 0xFFF);
             step_emit_one<PD, PR>(lrec[it >> 24], first + o, (int)((it >> 12) & 1), (int32_t)((it >> 14) & 0x3FF),
                                   qm[w], ((it >> 13) & 1) != 0, tmin, tmax, step.wsum, step.noprio, step.st, blk,
-                                  s1b, kst, step.winv);
+                                  s1o, step.winv);
         }
         __syncthreads();
         CRANE_TSTAMP(a.trace, blockIdx.x, 5);
@@ -339,7 +338,7 @@ void k1_node_pass(K1Args a, K1Step step) {
 
 // ---------------------------------------------------------------- launchers
 template <int PD, int PR>
-static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t st, bool stream) {
+static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t st, int stream) {
     if (a.N <= 0) return hipSuccess;
     const int T = a.threads;
     if (T != 128 && T != 256) return hipErrorInvalidValue;
@@ -353,7 +352,8 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
     if (step && !step->st.stage) return hipErrorInvalidValue;
     const K1Step sa = step ? *step : K1Step{};
     const char* nm = step ? "k1_node_pass+k3a_steps" : "k1_node_pass";
-    if (step && stream && !a.out && a.hx_region == nullptr && T == 256) return launch_stream_steps(PD, PR, a, sa, st);
+    if (step && stream && !a.out && a.hx_region == nullptr && T == 256)
+        return launch_stream_steps(PD, PR, a, sa, st);
     if (T == 256)
         return step ? klaunch(nm, k1_node_pass<PD, PR, 256, true>, dim3(grid), dim3(256), lds, st, a, sa)
                     : klaunch(nm, k1_node_pass<PD, PR, 256, false>, dim3(grid), dim3(256), lds, st, a, sa);
@@ -361,7 +361,7 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
                 : klaunch(nm, k1_node_pass<PD, PR, 128, false>, dim3(grid), dim3(128), lds, st, a, sa);
 }
 
-hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step, bool stream) {
+hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step, int stream) {
     switch (shape) {
         case kShape4x6: return launch_k1_t<4, 6>(a, step, st, stream);
         case kShape8x8: return launch_k1_t<8, 8>(a, step, st, stream);

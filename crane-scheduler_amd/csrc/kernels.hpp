@@ -356,7 +356,7 @@ struct K1Args {
 // no records written and no dedupe-form K2 entries, the streamed step pass (k1_stream_steps: no
 // record in registers, the stepped nodes' records built in LDS)
 hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step = nullptr,
-                            bool stream = false);
+                            int stream = 0);
 // the streamed step pass (k1stream.hip) for the record shape PD x PR
 hipError_t launch_stream_steps(int pd, int pr, const K1Args& a, const K1Step& sa, hipStream_t st);
 

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
         step_count<PD, PR>(r, n, tmin, tmax, wsum, noprio, sh, o);
     }
     step_publish<kStepSeg>(o, sh, st, blockIdx.x);
-    if (n < N && (o.slot0 >= 0 || o.slot1 >= 0)) step_emit<PD, PR>(r, n, tmin, tmax, wsum, noprio, o, st, blockIdx.x, s1l, 2 * kStepSeg);
+    if (n < N && (o.slot0 >= 0 || o.slot1 >= 0)) step_emit<PD, PR>(r, n, tmin, tmax, wsum, noprio, o, st, blockIdx.x, S1Out{s1l, nullptr, false, 2 * kStepSeg, 0});
     __syncthreads();
     step_sort_publish<kStepSeg>(s1l, s1s, sh, st, blockIdx.x);
     if (st.rows) {

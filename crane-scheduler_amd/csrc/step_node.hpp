@@ -295,14 +295,30 @@ __device__ __forceinline__ void step_count(const NodeRec<PD, PR>& r, int64_t n, 
 }
 
 // Phase 2, one (node, kind): the node's one-step records go to the workgroup's
-// staging s1b[T * kst + slot] (LDS, or st.stage when the block's records exceed the
+// staging (S1Out) (LDS, or st.stage when the block's records exceed the
 // LDS staging; step_sort_publish writes them out sorted), its middle pieces
 // straight to st.mid.
+// Where a block's one-step records go: its LDS staging (lds, kind stride kl) or, when the block
+// holds more of a kind than that takes (g, workgroup-uniform), st.stage (glb, stride kg).  Two
+// stores with known address spaces: one store through a pointer selected between LDS and global
+// is a flat store, which goes down the vector memory path even for LDS (round 5: the streamed
+// pass's emit 2.6 -> 1.3 us per workgroup without them).
+struct S1Out {
+    Step1* lds;
+    Step1* glb;
+    bool g;
+    int64_t kl, kg;
+    __device__ __forceinline__ void put(int T, int32_t i, const Step1& v) const {
+        if (g) glb[T * kg + i] = v;
+        else lds[T * kl + i] = v;
+    }
+};
+
 template <int PD, int PR>
 __device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t n, int T, int32_t slot,
                                               int32_t mslot, bool multi, int64_t tmin, int64_t tmax, double wsum,
-                                              int32_t noprio, const StepTables& st, int64_t blk, Step1* s1b,
-                                              int64_t kst, double winv = 0.0) {
+                                              int32_t noprio, const StepTables& st, int64_t blk, const S1Out& s1o,
+                                              double winv = 0.0) {
     constexpr int NB = PR + 2;
     int64_t c[NB];
 #pragma unroll
@@ -322,14 +338,13 @@ __device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t 
         const int32_t f = score_at<PD, PR>(t, r, wsum, noprio, winv);
         return (T == 1 || !(t < r.e_fail)) ? pack_key(f, n) : -1;
     };
-    Step1* s1 = s1b + T * kst;
     const int32_t k0 = key(tmin);
     if (!multi) {
         Step1 v;
         v.bp = mn;
         v.k0 = k0;
         v.k1 = key(mn);
-        s1[slot] = v;
+        s1o.put(T, slot, v);
         return;
     }
 #pragma unroll
@@ -365,20 +380,20 @@ __device__ __forceinline__ void step_emit_one(const NodeRec<PD, PR>& r, int64_t 
     b.bp = last;
     b.k0 = -1;
     b.k1 = kprev;
-    s1[slot] = a;
-    s1[slot + 1] = b;
+    s1o.put(T, slot, a);
+    s1o.put(T, slot + 1, b);
 }
 
 // Phase 2 for every kind of a node (the stand-alone K3a).
 template <int PD, int PR>
 __device__ __forceinline__ void step_emit(const NodeRec<PD, PR>& r, int64_t n, int64_t tmin, int64_t tmax,
                                           double wsum, int32_t noprio, const StepSlots& o,
-                                          const StepTables& st, int64_t blk, Step1* s1b, int64_t kst,
+                                          const StepTables& st, int64_t blk, const S1Out& s1o,
                                           double winv = 0.0) {
     if (o.slot0 >= 0)
-        step_emit_one<PD, PR>(r, n, 0, o.slot0, o.mslot0, o.multi0, tmin, tmax, wsum, noprio, st, blk, s1b, kst, winv);
+        step_emit_one<PD, PR>(r, n, 0, o.slot0, o.mslot0, o.multi0, tmin, tmax, wsum, noprio, st, blk, s1o, winv);
     if (o.slot1 >= 0)
-        step_emit_one<PD, PR>(r, n, 1, o.slot1, o.mslot1, o.multi1, tmin, tmax, wsum, noprio, st, blk, s1b, kst, winv);
+        step_emit_one<PD, PR>(r, n, 1, o.slot1, o.mslot1, o.multi1, tmin, tmax, wsum, noprio, st, blk, s1o, winv);
 }
 
 // Work item of the compacted emit: owner thread | kind << 12 | multi << 13 | slot << 14 | rs << 24,
