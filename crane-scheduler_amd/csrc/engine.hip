@@ -46,6 +46,11 @@ struct DevBuf {
         if (e == hipSuccess) n = std::max<size_t>(want, 1);
         return e;
     }
+    // staging that follows a varying size: geometric growth (an allocation syncs the device)
+    hipError_t grow(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        return reserve(std::max({want, n + n / 2, (size_t)65536 / sizeof(T)}));
+    }
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;
@@ -69,6 +74,10 @@ struct HostBuf {
         hipError_t e = hipHostMalloc((void**)&p, std::max<size_t>(want, 1) * sizeof(T), hipHostMallocDefault);
         if (e == hipSuccess) n = std::max<size_t>(want, 1);
         return e;
+    }
+    hipError_t grow(size_t want) {  // (pinned allocations cost ~0.1-1 ms: geometric growth)
+        if (want <= n && p) return hipSuccess;
+        return reserve(std::max({want, n + n / 2, (size_t)65536 / sizeof(T)}));
     }
     void release() {
         if (p) (void)hipHostFree(p);
@@ -1339,8 +1348,8 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
                  o_hvt = o_hv + 8 * K, o_out = o_hvt + 8 * K;
     const size_t r_ns = o_out + 8 * K * S, r_ff = r_ns + K, r_sc = r_ff + K * (S + 1), r_end = r_sc + K * (S + 1);
     const size_t total = rows ? r_end : o_out;
-    HIPTRY(h, h->upd_host.reserve(total));
-    HIPTRY(h, h->upd_dev.reserve(total));
+    HIPTRY(h, h->upd_host.grow(total));
+    HIPTRY(h, h->upd_dev.grow(total));
     unsigned char* p = h->upd_host.p;
     std::memcpy(p, idx, 8 * K);
     if (M > 0) {
@@ -1490,8 +1499,8 @@ int crane_dyn_node_steps_subset(crane_dyn* h, int64_t t0_ns, int64_t t1_ns, int6
     const size_t S = (size_t)node_step_slots(h->shape), K = (size_t)k;
     const size_t o_ns = 8 * K * S, o_ff = o_ns + K, o_sc = o_ff + K * (S + 1), o_out = o_sc + K * (S + 1);
     const size_t o_idx = (o_out + 7) & ~(size_t)7, total = o_idx + 8 * K;
-    HIPTRY(h, h->upd_host.reserve(total));
-    HIPTRY(h, h->upd_dev.reserve(total));
+    HIPTRY(h, h->upd_host.grow(total));
+    HIPTRY(h, h->upd_dev.grow(total));
     std::memcpy(h->upd_host.p + o_idx, idx, 8 * K);
     unsigned char* d = h->upd_dev.p;
     HIPTRY(h, hipMemcpyAsync(d + o_idx, h->upd_host.p + o_idx, 8 * K, hipMemcpyHostToDevice, st));

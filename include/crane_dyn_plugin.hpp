@@ -150,10 +150,12 @@ struct CycleState {
     friend class DynamicScheduler;
     mutable std::mutex clone_mu_;
     // the plugin's per-cycle sync: 0 not started, 1 the first caller brings the plugin up to
-    // date, 2 its scan of the snapshot is open to the cycle's other callers (dyn_job_), 3 done
+    // date, 2 its scan of the snapshot is open to the cycle's other callers (dyn_job_), 4 its
+    // parse of the changed nodes' annotations is (dyn_parse_), 3 done
     std::atomic<int> dyn_phase_{0};
     std::atomic<bool> dyn_ready_{false};  // the cycle's answers are set (the lock-free fast path)
     std::shared_ptr<void> dyn_job_;       // the open scan (set before phase 2, kept until the state dies)
+    std::shared_ptr<void> dyn_parse_;     // the open parse (set before phase 4, likewise)
     bool dyn_done_ = false;
     std::shared_ptr<const void> dyn_row_;
     std::string dyn_err_;
@@ -307,6 +309,9 @@ class DynamicScheduler {
     struct Counters {
         uint64_t tables_built = 0, full_syncs = 0, incremental_syncs = 0, nodes_updated = 0, sync_ns = 0,
                  nodes_joined = 0, nodes_left = 0, grows = 0;
+        // the incremental syncs' parts: snapshot scan, joins / departures, the changed nodes'
+        // parse, the engine call
+        uint64_t scan_ns = 0, membership_ns = 0, parse_ns = 0, engine_ns = 0;
     };
     Counters counters() const {
         std::lock_guard<std::mutex> g(mu_);
@@ -424,11 +429,69 @@ class DynamicScheduler {
         return keys_;
     }
 
-    // parse rows [key][n] of the nodes' annotation strings (NULL = key missing)
+    // The changed nodes parsed in chunks of nodes by the cycle's callers — the annotation lookups
+    // and the parses (a cycle at the controller's rate at one pod per second re-parses ~1,400
+    // nodes, ~10k strings: 1-2 ms on one thread while the other callers wait).
+    struct ParseJob {
+        const Node* const* nodes;
+        const std::string* keys;
+        size_t R = 0, n = 0, nchunks = 0;
+        double* val;
+        int64_t* ts;
+        const crane_tz* zone;
+        int64_t tz;
+        std::atomic<size_t> next{0}, done{0};
+        void work() {
+            for (;;) {
+                const size_t c = next.fetch_add(1, std::memory_order_relaxed);
+                if (c >= nchunks) return;
+                const size_t hi = std::min(n, (c + 1) * kParseChunk);
+                for (size_t i = c * kParseChunk; i < hi; ++i)
+                    for (size_t m = 0; m < R; ++m) {
+                        double* v = val + m * n + i;
+                        int64_t* t = ts + m * n + i;
+                        const Node* nd = nodes[i];
+                        auto it = nd ? nd->Annotations.find(keys[m]) : decltype(nd->Annotations.end()){};
+                        if (!nd || it == nd->Annotations.end()) {
+                            *v = 0;  // key not found (stats.go:52-55)
+                            *t = CRANE_TS_INVALID;
+                        } else if (zone) {
+                            crane_parse_annotation_tz(it->second.data(), it->second.size(), zone, v, t);
+                        } else {
+                            crane_parse_annotation(it->second.data(), it->second.size(), tz, v, t);
+                        }
+                    }
+                done.fetch_add(1, std::memory_order_acq_rel);
+            }
+        }
+    };
+    static constexpr size_t kParseChunk = 64;  // nodes
+
+    // parse rows [key][n] of the nodes' annotation strings (NULL = key missing); with the cycle's
+    // state, a parse of more than a few chunks is shared with the cycle's other callers
     bool parse(const std::vector<const Node*>& nodes, int32_t threads, std::vector<double>* val,
-               std::vector<int64_t>* ts, std::string* err) {
+               std::vector<int64_t>* ts, std::string* err, CycleState* state = nullptr) {
         const std::vector<std::string>& ks = keys();
         const size_t R = ks.size(), n = nodes.size();
+        val->resize(R * n);
+        ts->resize(R * n);
+        if (state && n >= 4 * kParseChunk) {
+            auto job = std::make_shared<ParseJob>();
+            job->nodes = nodes.data();
+            job->keys = ks.data();
+            job->R = R;
+            job->n = n;
+            job->nchunks = (n + kParseChunk - 1) / kParseChunk;
+            job->val = val->data();
+            job->ts = ts->data();
+            job->zone = zone_;
+            job->tz = tz_;
+            state->dyn_parse_ = job;
+            state->dyn_phase_.store(4, std::memory_order_release);
+            job->work();
+            while (job->done.load(std::memory_order_acquire) < job->nchunks) relax();
+            return true;
+        }
         strs_.assign(R * n, nullptr);
         lens_.assign(R * n, 0);
         for (size_t i = 0; i < n; ++i) {
@@ -441,8 +504,6 @@ class DynamicScheduler {
                 lens_[m * n + i] = it->second.size();
             }
         }
-        val->resize(R * n);
-        ts->resize(R * n);
         const int rc = zone_ ? crane_parse_annotations_tz((int64_t)(R * n), strs_.data(), lens_.data(), zone_,
                                                          val->data(), ts->data(), threads)
                              : crane_parse_annotations((int64_t)(R * n), strs_.data(), lens_.data(), tz_, val->data(),
@@ -503,6 +564,24 @@ class DynamicScheduler {
         }
         ++cnt_.full_syncs;
         if (!build_table(v.get(), now, err)) return nullptr;
+        // warm the incremental path (its staging buffers, its kernel) with row 0's own columns,
+        // which rewrites row 0 unchanged: the first cycle that finds changed nodes then costs
+        // what the later ones do
+        if (N > 0) {
+            std::vector<double> cv(M + 1);
+            std::vector<int64_t> ct(M + 1);
+            for (size_t m = 0; m <= M; ++m) {
+                cv[m] = val[m * N];
+                ct[m] = ts[m * N];
+            }
+            const int64_t r0 = 0;
+            if (crane_dyn_update_node_steps(eng_, 1, &r0, cv.data(), ct.data(), cv.data() + M, ct.data() + M, v->t0,
+                                            v->t1, v->n_steps.data(), v->bp.data(), v->first_fail.data(),
+                                            v->score.data())) {
+                *err = crane_dyn_last_error(eng_);
+                return nullptr;
+            }
+        }
         return v;
     }
 
@@ -558,13 +637,25 @@ class DynamicScheduler {
     // the changed rows: re-parse, scatter into the engine, rebuild their table rows.  The View
     // records the new Node objects only once the engine holds them (a failed call makes the
     // caller drop the View: the next cycle resyncs in full).
-    bool update(View* v, int64_t now, std::string* err) {
+    bool update(View* v, int64_t now, std::string* err, CycleState* state) {
         const size_t k = changed_.size();
         cnodes_.resize(k);
         for (size_t j = 0; j < k; ++j) cnodes_[j] = v->infos[(size_t)changed_[j]]->node();
         std::vector<double> val;
         std::vector<int64_t> ts;
-        if (!parse(cnodes_, 1, &val, &ts, err)) return false;
+        const auto tp = std::chrono::steady_clock::now();
+        if (!parse(cnodes_, 1, &val, &ts, err, state)) return false;
+        const auto te = std::chrono::steady_clock::now();
+        cnt_.parse_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(te - tp).count();
+        struct EngineTime {  // (the engine call and the rows' copy, however update() returns)
+            Counters& c;
+            std::chrono::steady_clock::time_point t;
+            ~EngineTime() {
+                c.engine_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                   std::chrono::steady_clock::now() - t)
+                                   .count();
+            }
+        } et{cnt_, te};
         const size_t M = (size_t)crane_dyn_num_metrics(eng_);
         auto record = [&] {
             for (size_t j = 0; j < k; ++j) {
@@ -667,6 +758,7 @@ class DynamicScheduler {
         added_.clear();
         removed_.clear();
         ++epoch_;
+        const auto ts0 = std::chrono::steady_clock::now();
         {
             auto job = std::make_shared<ScanJob>();
             job->L = L.data();
@@ -691,6 +783,8 @@ class DynamicScheduler {
         if (L.size() - added_.size() != v->live)
             for (size_t r = 0; r < v->rows(); ++r)
                 if (v->infos[r] && v->seen[r] != epoch_) removed_.push_back((int64_t)r);
+        const auto ts1 = std::chrono::steady_clock::now();
+        cnt_.scan_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(ts1 - ts0).count();
         if (4 * (added_.size() + removed_.size()) > L.size() + 256) {  // most of the set: resync whole
             view_.reset();
             view_ = full_sync(L, now, err);
@@ -702,7 +796,10 @@ class DynamicScheduler {
             view_.reset();
             return nullptr;
         }
-        if (!changed_.empty() && !update(v.get(), now, err)) {
+        cnt_.membership_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                  std::chrono::steady_clock::now() - ts1)
+                                  .count();
+        if (!changed_.empty() && !update(v.get(), now, err, state)) {
             view_.reset();
             return nullptr;
         }
@@ -715,7 +812,8 @@ class DynamicScheduler {
 
     // The state of the cycle.  Its first caller brings the plugin up to date; the cycle's other
     // callers (the framework's 16 goroutines, all waiting for the same answers) take chunks of
-    // the snapshot scan meanwhile, then wait for the leader's update.
+    // the snapshot scan and of the changed nodes' parse meanwhile, then wait for the leader's
+    // engine update.
     const View* view_of(CycleState& state, std::string* err) {
         if (!state.dyn_ready_.load(std::memory_order_acquire)) {
             int ph = 0;
@@ -737,11 +835,17 @@ class DynamicScheduler {
                 state.dyn_phase_.store(3, std::memory_order_relaxed);
                 state.dyn_ready_.store(true, std::memory_order_release);
             } else {
-                bool helped = false;
+                bool scanned = false, parsed = false;
                 for (uint32_t k = 0; !state.dyn_ready_.load(std::memory_order_acquire); ++k) {
-                    if (!helped && state.dyn_phase_.load(std::memory_order_acquire) == 2) {
+                    const int ph = state.dyn_phase_.load(std::memory_order_acquire);
+                    if (ph == 2 && !scanned) {
                         static_cast<ScanJob*>(state.dyn_job_.get())->work();
-                        helped = true;
+                        scanned = true;
+                        k = 0;
+                    } else if (ph == 4 && !parsed) {
+                        static_cast<ParseJob*>(state.dyn_parse_.get())->work();
+                        parsed = true;
+                        k = 0;
                     }
                     if (k < 4096) relax();
                     else std::this_thread::yield();

@@ -462,6 +462,8 @@ int main(int argc, char** argv) {
         double cyc, first, filt, score;
         size_t pod;
         int64_t patches;
+        double scan, memb, parse, eng;  // the cycle's sync parts (plugin counters)
+        long long upd;
     };
     std::vector<Slow> slow;
     std::atomic<int> errors{0};
@@ -521,7 +523,8 @@ int main(int argc, char** argv) {
             fidx.resize((size_t)N);
             fscore.resize((size_t)N);
         }
-        const uint64_t sync0 = cpu ? 0 : ds.counters().sync_ns;
+        const auto c0 = cpu ? decltype(ds.counters()){} : ds.counters();
+        const uint64_t sync0 = c0.sync_ns;
         const auto t0 = Clock::now();
         CycleState st;
         st.now_ns = p.now;
@@ -575,7 +578,11 @@ int main(int argc, char** argv) {
         score_ms.push_back(ms(t1, t2));
         sel_ms.push_back(ms(t2, t3));
         chosen.push_back(best < 0 ? -1 : snap.ids[(size_t)best]);
-        slow.push_back({ms(t0, t3), first_ms.back(), ms(t0, t1), ms(t1, t2), pi, n_patches - patches0});
+        const auto c1 = cpu ? decltype(ds.counters()){} : ds.counters();
+        slow.push_back({ms(t0, t3), first_ms.back(), ms(t0, t1), ms(t1, t2), pi, n_patches - patches0,
+                        (double)(c1.scan_ns - c0.scan_ns) / 1e6, (double)(c1.membership_ns - c0.membership_ns) / 1e6,
+                        (double)(c1.parse_ns - c0.parse_ns) / 1e6, (double)(c1.engine_ns - c0.engine_ns) / 1e6,
+                        (long long)(c1.nodes_updated - c0.nodes_updated)});
     }
     std::sort(slow.begin(), slow.end(), [](const Slow& a, const Slow& b) { return a.cyc > b.cyc; });
     if (clog) std::fclose(clog);
@@ -608,9 +615,10 @@ int main(int argc, char** argv) {
                 snap.list.size());
     for (size_t i = 0; i < std::min<size_t>(5, slow.size()); ++i)
         std::printf("%s{\"pod\": %zu, \"cycle_ms\": %.4f, \"first_call_ms\": %.4f, \"filter_ms\": %.4f, "
-                    "\"score_ms\": %.4f, \"patches\": %lld}",
+                    "\"score_ms\": %.4f, \"patches\": %lld, \"scan_ms\": %.4f, \"membership_ms\": %.4f, "
+                    "\"parse_ms\": %.4f, \"engine_ms\": %.4f, \"nodes_updated\": %lld}",
                     i ? ", " : "", slow[i].pod, slow[i].cyc, slow[i].first, slow[i].filt, slow[i].score,
-                    (long long)slow[i].patches);
+                    (long long)slow[i].patches, slow[i].scan, slow[i].memb, slow[i].parse, slow[i].eng, slow[i].upd);
     std::printf("], \"chosen\": [");
     for (size_t i = 0; i < chosen.size(); ++i) std::printf("%s%lld", i ? ", " : "", (long long)chosen[i]);
     std::printf("]}\n");
