@@ -342,7 +342,11 @@ void k1_stream_steps(K1Args a, K1Step step) {
         {
             constexpr int NB = PR + 2;
             for (int tk = threadIdx.x; tk < 2 * m * NB; tk += BS) {
-                const int i = tk / NB, q = tk - i * NB, j = i >> 1, T = i & 1;
+                const int i = tk / NB, j = i >> 1, T = i & 1;
+                int q = tk - i * NB;
+                // (q = threadIdx.x % NB in every trip: without this the compiler hoists emit_task's
+                // per-q lane masks out of the loop and spills them, ~30 SGPRs for the whole kernel)
+                asm volatile("" : "+v"(q));
                 const int32_t* dw = reinterpret_cast<const int32_t*>(lrec[j].e_pred);
                 const int32_t sl = dw[T ? 2 : 0];
                 if (sl < 0) continue;
