@@ -57,6 +57,11 @@ __device__ __forceinline__ int32_t score_at_lds(int64_t t, const NodeRec<PD, PR>
     return score_of_sum(s, t < r.e_hv ? r.pen : 0, wsum, noprio, winv);
 }
 
+// K1S_SKIP (cost ablation builds only, tools/gpu_k1_ablate.sh; wrong tables): 1 no emit tasks,
+// 2 no tail (sort / pieces / tile rows), 4 no record staging
+#ifndef K1S_SKIP
+#define K1S_SKIP 0
+#endif
 constexpr int kSRec = 64;   // stepped records staged per chunk
 constexpr int kSCap = 128;  // one-step records per kind staged in LDS (more: st.stage)
 
@@ -321,13 +326,13 @@ void k1_stream_steps(K1Args a, K1Step step) {
         dw[3] = mslot1;
         dw[4] = (multi0 ? 1 : 0) | (multi1 ? 2 : 0);
     };
-    if (stepped) {
+    if (stepped && !(K1S_SKIP & 4)) {
         rank_lane[rs] = (uint8_t)threadIdx.x;
         if (rs < kSRec) put(&lrec[rs]);
         else put(static_cast<Rec*>(step.srec) + n);
     }
     __syncthreads();
-    for (int32_t c0 = 0; c0 < nst; c0 += kSRec) {  // (workgroup-uniform)
+    for (int32_t c0 = 0; c0 < ((K1S_SKIP & 1) ? 0 : nst); c0 += kSRec) {  // (workgroup-uniform)
         const int32_t m = min(kSRec, nst - c0);
         if (c0 > 0) {  // this chunk's records from HBM (L2: written by this workgroup)
             constexpr int W = 3 + 2 * PR + 3;  // e_fail, e_hv, pen, e_prio, t, then the slot words
@@ -358,6 +363,7 @@ void k1_stream_steps(K1Args a, K1Step step) {
     }
     CRANE_TSTAMP(a.trace, blockIdx.x, 5);
     // ---- D: the fused pass's tail
+    if (K1S_SKIP & 2) return;
     if (g1) step_sort_publish_global<BS>(ssh, step.st, blk);
     else step_sort_publish<BS, kSCap>(s1l, srt, ssh, step.st, blk);
     CRANE_TSTAMP(a.trace, blockIdx.x, 6);
