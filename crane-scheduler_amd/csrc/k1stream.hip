@@ -30,14 +30,16 @@ namespace crane {
 //      (node, kind) items from the LDS records (step_emit_one);
 //   D  the fused pass's tail: sort + publish, elementary pieces, tile rows.
 // Not with the dedupe-form K2 entries (their per-block counting needs the default pass's LDS).
-// step_emit_one's outputs for the stepped (node, kind) items of a chunk, spread over the lanes:
-// item i takes lanes (tasks) i * NB + q, q = 0 .. NB - 1, and task q handles the q-th smallest
-// of the kind's in-range expiries c_q (with multiplicity, found by ranking the NB expiries in
-// registers): its key, its middle piece [c_q, c_{q+1}), and — q = 0 / q = cnt - 1 — the
-// half-line records.  A single (node, kind) item's keys are then computed side by side instead of
-// one after another (round 5's first form, one lane per item walking its expiries in order with
-// the record read from LDS term by term, spent 4.9 us per workgroup here: a chain of dependent
-// LDS reads).  The outputs are step_emit_one's, bit for bit.
+// step_emit_one's outputs for the stepped nodes of a chunk, spread over the lanes: node j takes
+// lanes j * (PR + 2) + q, and lane q handles candidate expiry q (the priorities', the hot
+// value's, e_fail) for both pod kinds at once: if it is in the batch range, its rank r in the
+// kind's ascending order (with multiplicity, by ranking the candidates in registers), its key
+// (one score serves both kinds: the Filter only gates kind 0's), its middle piece
+// [c_r, c_{r+1}), and — r = 0 / r = cnt - 1 — the half-line records.  A node's keys are then
+// computed side by side instead of one after another (round 5's first form, one lane per item
+// walking its expiries in order with the record read from LDS term by term, spent 4.9 us per
+// workgroup here: a chain of dependent LDS reads; a lane per (node, kind, candidate) doubled the
+// emitting waves for 1 % more time).  The outputs are step_emit_one's, bit for bit.
 __device__ __forceinline__ int64_t readfirstlane64(int64_t v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
@@ -62,87 +64,99 @@ __device__ __forceinline__ int32_t score_at_lds(int64_t t, const NodeRec<PD, PR>
 #ifndef K1S_SKIP
 #define K1S_SKIP 0
 #endif
+#ifndef K1S_WAVES  // waves per SIMD the 4x6 form is built for (72 VGPRs: 7; 64: 8)
+#define K1S_WAVES 7
+#endif
 constexpr int kSRec = 64;   // stepped records staged per chunk
 constexpr int kSCap = 128;  // one-step records per kind staged in LDS (more: st.stage)
 
 template <int PD, int PR>
-__device__ __forceinline__ void emit_task(const NodeRec<PD, PR>& r, int64_t n, int T, int q, int32_t slot,
-                                          int32_t mslot, bool multi, int64_t tmin, int64_t tmax, double wsum,
-                                          int32_t noprio, const StepTables& st, int64_t blk, const S1Out& s1o,
-                                          double winv) {
-    constexpr int NB = PR + 2;
+__device__ __forceinline__ void emit_task(const NodeRec<PD, PR>& r, int64_t n, int q, const int32_t* dw, int64_t tmin,
+                                          int64_t tmax, double wsum, int32_t noprio, const StepTables& st,
+                                          int64_t blk, const S1Out& s1o, double winv) {
+    constexpr int NB = PR + 2, F = PR + 1;  // candidate F = e_fail: kind 0's only (DaemonSet pods bypass the Filter)
     int64_t c[NB];
 #pragma unroll
     for (int k = 0; k < PR; ++k) c[k] = r.e_prio[k];
     c[PR] = r.e_hv;
-    c[PR + 1] = T == 0 ? r.e_fail : INT64_MIN;  // DaemonSet pods bypass the Filter
-    int cnt = 0;
-    uint32_t inm = 0;  // in-range expiries
+    c[F] = r.e_fail;
+    uint32_t inm = 0;  // kind 0's in-range candidates; kind 1's are inm without F
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
-        const bool in = c[k] > tmin && c[k] <= tmax;
-        inm |= in ? 1u << k : 0u;
-        cnt += in;
-    }
-    // the task's expiry c[q] and its rank in the ascending order of (c, index), and the next one's
-    // value: a rank among NB registers (static indices) instead of a sort
+    for (int k = 0; k < NB; ++k) inm |= (c[k] > tmin && c[k] <= tmax) ? 1u << k : 0u;
     if (!((inm >> q) & 1u)) return;  // out of range
+    const int cnt0 = __builtin_popcount(inm), cnt1 = __builtin_popcount(inm & ~(1u << F));
+    // c[q], its rank in the ascending order of (c, index) and the next one's value, per kind:
+    // ranks among NB registers (static indices) instead of a sort
     int64_t cq = c[0];
 #pragma unroll
     for (int j = 1; j < NB; ++j) cq = q == j ? c[j] : cq;
-    int rk = 0;
-    int64_t cn = INT64_MAX;
+    int rk0 = 0;
+    bool fb = false;  // e_fail before c[q] (kind 0 only)
+    int64_t cn1 = INT64_MAX, cn0;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
         const bool in = (inm >> j) & 1u;
         const bool before = in && (c[j] < cq || (c[j] == cq && j < q));
         const bool after = in && (c[j] > cq || (c[j] == cq && j > q));
-        rk += before;
-        cn = after ? min(cn, c[j]) : cn;
-    }
-    q = rk;
-    auto key = [&](int64_t t) {  // key_of for the run-time kind, at the first instant of a step
-        const int32_t f = score_at_lds<PD, PR>(t, r, wsum, noprio, winv);
-        return (T == 1 || !(t < r.e_fail)) ? pack_key(f, n) : -1;
-    };
-    auto put = [&](int32_t i, const Step1& v) { s1o.put(T, i, v); };
-    if (!multi) {  // one record: before / from the one distinct expiry
-        if (q == 0) {
-            Step1 v;
-            v.bp = cq;
-            v.k0 = key(tmin);
-            v.k1 = key(cq);
-            put(slot, v);
+        rk0 += before;
+        if (j == F) {
+            fb = before;
+            cn0 = after ? min(cn1, c[j]) : cn1;
+        } else {
+            cn1 = after ? min(cn1, c[j]) : cn1;
         }
-        return;
     }
-    const int32_t kq = key(cq);  // the key from c_q on
-    if (q + 1 < cnt) {
-        Mid p;
-        p.s = cq;
-        p.e = cn;
-        p.key = kq;
-        p.pad = 0;
-        (st.mid + (int64_t)T * st.mpad + blk * st.mstride + mslot)[q] = p;
-    }
-    if (q == 0) {
-        Step1 x;
-        x.bp = cq;
-        x.k0 = key(tmin);
-        x.k1 = -1;
-        put(slot, x);
-    }
-    if (q == cnt - 1) {
-        Step1 y;
-        y.bp = cq;
-        y.k0 = -1;
-        y.k1 = kq;
-        put(slot + 1, y);
+    const int rk1 = rk0 - (fb ? 1 : 0);
+    // one score per instant serves both kinds (the Filter only gates kind 0's key)
+    const int64_t pk = pack_key(score_at_lds<PD, PR>(cq, r, wsum, noprio, winv), n);
+    const bool need0 = rk0 == 0 || (q != F && rk1 == 0);
+    const int64_t pk0 = need0 ? pack_key(score_at_lds<PD, PR>(tmin, r, wsum, noprio, winv), n) : 0;
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+        const int32_t slot = dw[T ? 2 : 0];
+        if (slot < 0 || (T == 1 && q == F)) continue;
+        const int rk = T ? rk1 : rk0, cnt = T ? cnt1 : cnt0;
+        const int64_t cn = T ? cn1 : cn0;
+        const int32_t kq = (int32_t)((T == 1 || !(cq < r.e_fail)) ? pk : -1);    // the key from c_rk on
+        const int32_t kt = (int32_t)((T == 1 || !(tmin < r.e_fail)) ? pk0 : -1); // ... before c_0
+        const bool multi = ((dw[4] >> T) & 1) != 0;
+        if (!multi) {  // one record: before / from the one distinct expiry
+            if (rk == 0) {
+                Step1 v;
+                v.bp = cq;
+                v.k0 = kt;
+                v.k1 = kq;
+                s1o.put(T, slot, v);
+            }
+            continue;
+        }
+        if (rk + 1 < cnt) {
+            Mid pc;
+            pc.s = cq;
+            pc.e = cn;
+            pc.key = kq;
+            pc.pad = 0;
+            (st.mid + (int64_t)T * st.mpad + blk * st.mstride + dw[T ? 3 : 1])[rk] = pc;
+        }
+        if (rk == 0) {
+            Step1 x;
+            x.bp = cq;
+            x.k0 = kt;
+            x.k1 = -1;
+            s1o.put(T, slot, x);
+        }
+        if (rk == cnt - 1) {
+            Step1 y;
+            y.bp = cq;
+            y.k0 = -1;
+            y.k1 = kq;
+            s1o.put(T, slot + 1, y);
+        }
     }
 }
 
 template <int PD, int PR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PD * PR <= 24 ? 7 : 1)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PD * PR <= 24 ? K1S_WAVES : 1)))
 void k1_stream_steps(K1Args a, K1Step step) {
     using Rec = NodeRec<PD, PR>;
     constexpr int BS = 256;
@@ -346,17 +360,15 @@ void k1_stream_steps(K1Args a, K1Step step) {
         }
         {
             constexpr int NB = PR + 2;
-            for (int tk = threadIdx.x; tk < 2 * m * NB; tk += BS) {
-                const int i = tk / NB, j = i >> 1, T = i & 1;
-                int q = tk - i * NB;
+            for (int tk = threadIdx.x; tk < m * NB; tk += BS) {  // (node, candidate): both kinds
+                const int j = tk / NB;
+                int q = tk - j * NB;
                 // (q = threadIdx.x % NB in every trip: without this the compiler hoists emit_task's
                 // per-q lane masks out of the loop and spills them, ~30 SGPRs for the whole kernel)
                 asm volatile("" : "+v"(q));
-                const int32_t* dw = reinterpret_cast<const int32_t*>(lrec[j].e_pred);
-                const int32_t sl = dw[T ? 2 : 0];
-                if (sl < 0) continue;
-                emit_task<PD, PR>(lrec[j], first + rank_lane[c0 + j], T, q, sl, dw[T ? 3 : 1], ((dw[4] >> T) & 1) != 0,
-                                  tmin, tmax, step.wsum, step.noprio, step.st, blk, s1o, step.winv);
+                emit_task<PD, PR>(lrec[j], first + rank_lane[c0 + j], q,
+                                  reinterpret_cast<const int32_t*>(lrec[j].e_pred), tmin, tmax, step.wsum, step.noprio,
+                                  step.st, blk, s1o, step.winv);
             }
         }
         __syncthreads();  // (the chunk's records are reused by the next chunk)
