@@ -133,6 +133,8 @@ struct Options {
     bool trace = false;       // phase stamps of K2x / K1 / K3s (crane_dyn_debug_trace)
     int k1_stream = 1;        // keys-only step without dedupe-form K2 entries: the streamed step pass
                               // (k1_stream_steps, no record in registers) | 0 the fused record pass
+    int k1_tail = 0;          // the streamed pass's tail: 0 on one wave when the grid has >= 4096 blocks
+                              // (the other waves leave), 1 always on one wave, 4 on all four
     int k2_sorted = 1;        // a time-ordered log: K2 reads the widest window's suffix, ranks by position
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
@@ -605,7 +607,7 @@ static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_k
     if (sp.fuse) {
         // (the records the fused step leaves stale serve as the streamed pass's scratch)
         const K1Step ks{h->stile.p, h->sbatch.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, h->dp.winv, sp.stt,
-                        h->rec.p};
+                        h->rec.p, h->opt.k1_tail};
         int rc = node_pass_locked(h, st, nullptr, &ks);
         if (rc) return rc;
     } else {
@@ -816,6 +818,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
     else if (n == "k2_sorted" && range(0, 1)) o.k2_sorted = (int)value;
     else if (n == "k1_stream" && range(0, 1)) o.k1_stream = (int)value;
+    else if (n == "k1_tail" && (value == 0 || value == 1 || value == 4)) o.k1_tail = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
         if (o.trace) {

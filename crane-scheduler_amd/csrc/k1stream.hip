@@ -64,6 +64,9 @@ __device__ __forceinline__ int32_t score_at_lds(int64_t t, const NodeRec<PD, PR>
 #ifndef K1S_SKIP
 #define K1S_SKIP 0
 #endif
+#ifndef K1S_TAIL1  // the single-wave tail for grids of many rounds (A/B: 0 off)
+#define K1S_TAIL1 1
+#endif
 #ifndef K1S_WAVES  // waves per SIMD the 4x6 form is built for (72 VGPRs: 7; 64: 8)
 #define K1S_WAVES 7
 #endif
@@ -153,6 +156,26 @@ __device__ __forceinline__ void emit_task(const NodeRec<PD, PR>& r, int64_t n, i
             s1o.put(T, slot + 1, y);
         }
     }
+}
+
+// the step epilogue after the emit: sort + publish, elementary pieces, tile rows, by the BS
+// threads still running (lrec: the staged records' LDS, dead now: the pieces' scratch)
+template <int BS, class Rec>
+__device__ __forceinline__ void tail(bool g1, Rec* lrec, Step1* s1l, Step1* srt, StepShared& ssh, const K1Step& step,
+                                     int64_t blk, unsigned long long* trace) {
+    if (g1) step_sort_publish_global<BS>(ssh, step.st, blk);
+    else step_sort_publish<BS, kSCap>(s1l, srt, ssh, step.st, blk);
+    CRANE_TSTAMP(trace, blockIdx.x, 6);
+    if (step.st.rows) {
+        int64_t tpre = 0;  // this thread's first tile-row bound (step_tile_rows)
+        tile_prefetch(step.st, &tpre);
+        constexpr int kPc = ((int)(kSRec * sizeof(Rec)) / PieceScr::bytes_per_piece) & ~3;
+        const PieceScr ps{reinterpret_cast<unsigned char*>(lrec), kPc < 128 ? kPc : 128};
+        step_pieces<BS>(ssh, step.st, blk, ps);
+        if (g1) step_tile_rows<BS, kSCap, true>(s1l, srt, ssh, step.st, blk, &tpre, ps);
+        else step_tile_rows<BS, kSCap, false>(s1l, srt, ssh, step.st, blk, &tpre, ps);
+    }
+    CRANE_TSTAMP(trace, blockIdx.x, 4);
 }
 
 template <int PD, int PR>
@@ -376,20 +399,19 @@ void k1_stream_steps(K1Args a, K1Step step) {
     CRANE_TSTAMP(a.trace, blockIdx.x, 5);
     // ---- D: the fused pass's tail
     if (K1S_SKIP & 2) return;
-    if (g1) step_sort_publish_global<BS>(ssh, step.st, blk);
-    else step_sort_publish<BS, kSCap>(s1l, srt, ssh, step.st, blk);
-    CRANE_TSTAMP(a.trace, blockIdx.x, 6);
-    if (step.st.rows) {
-        int64_t tpre = 0;  // this thread's first tile-row bound (step_tile_rows)
-        tile_prefetch(step.st, &tpre);
-        // the middle pieces' scratch: the staged records' LDS (dead after the emit)
-        constexpr int kPc = ((int)sizeof(lrec) / PieceScr::bytes_per_piece) & ~3;
-        const PieceScr ps{reinterpret_cast<unsigned char*>(lrec), kPc < 128 ? kPc : 128};
-        step_pieces<BS>(ssh, step.st, blk, ps);
-        if (g1) step_tile_rows<BS, kSCap, true>(s1l, srt, ssh, step.st, blk, &tpre, ps);
-        else step_tile_rows<BS, kSCap, false>(s1l, srt, ssh, step.st, blk, &tpre, ps);
+    // a grid of many rounds: wave 0 alone runs the tail and the other three waves leave, so their
+    // slots take the next workgroups' streams (the tail is a few single-wave phases between
+    // barriers); a grid of one or two rounds keeps all four (its time is one workgroup's chain)
+    if (K1S_TAIL1 && (step.tail1 == 1 || (step.tail1 == 0 && gridDim.x >= 4096))) {
+        if (threadIdx.x >= 64) return;
+        if (threadIdx.x < 2) {  // the block's flat maxima into wave 0's slot (tile rows read it)
+            const int T = threadIdx.x;
+            ssh.fm[T][0] = max(max(ssh.fm[T][0], ssh.fm[T][1]), max(ssh.fm[T][2], ssh.fm[T][3]));
+        }
+        tail<64>(g1, lrec, s1l, srt, ssh, step, blk, a.trace);
+        return;
     }
-    CRANE_TSTAMP(a.trace, blockIdx.x, 4);
+    tail<BS>(g1, lrec, s1l, srt, ssh, step, blk, a.trace);
 }
 
 template <int PD, int PR>

@@ -322,6 +322,7 @@ struct K1Step {
     double winv;             // 1 / wsum when |wsum| is a power of two, else 0 (score_at)
     StepTables st;
     void* srec;              // NodeRec [N] scratch (the streamed step pass's stepped nodes past its LDS)
+    int32_t tail1;           // the streamed pass's tail on one wave (0: when the grid has >= 4096 blocks)
 };
 
 size_t node_rec_bytes(int shape);

@@ -29,14 +29,18 @@ def _check(spec, c, now, ds):
     # the node pass as the streamed step pass (k1_stream 1, the default without dedupe-form K2
     # entries: no record in registers, the stepped records built in LDS in chunks of 64) or the
     # record-holding fused pass (0)
-    for rows, cap, pc, sf in ((1, 1 << 30, 0, 1), (0, 1 << 30, 0, 1), (1, 0, 1, 1), (0, 6, 0, 1), (1, 6, 1, 1),
-                              (1, 1 << 30, 1, 1), (1, 0, 2, 1), (1, 1 << 30, 0, 0), (0, 6, 1, 0), (1, 0, 2, 0)):
-        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap, "step_pieces": pc, "k1_stream": sf})
+    # (k1_tail: the streamed pass's tail on one wave, 1, or on all four, 4: auto picks by grid size)
+    for rows, cap, pc, sf, tl in ((1, 1 << 30, 0, 1, 0), (0, 1 << 30, 0, 1, 0), (1, 0, 1, 1, 0), (0, 6, 0, 1, 0),
+                                  (1, 6, 1, 1, 0), (1, 1 << 30, 1, 1, 0), (1, 0, 2, 1, 0), (1, 1 << 30, 0, 0, 0),
+                                  (0, 6, 1, 0, 0), (1, 0, 2, 0, 0), (1, 1 << 30, 1, 1, 1), (0, 6, 0, 1, 1),
+                                  (1, 0, 2, 1, 1)):
+        eng = engine_for(spec, c, opts={"step_rows": rows, "step_lds_cap": cap, "step_pieces": pc, "k1_stream": sf,
+                                        "k1_tail": tl})
         _, _, ch, cs = eng.eval(now, ds)
-        assert np.array_equal(ch, och), (rows, cap, pc, sf)
+        assert np.array_equal(ch, och), (rows, cap, pc, sf, tl)
         for p in range(len(now)):
             ok = (off[p] < 0) | bool(ds[p])
-            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, pc, sf, p)
+            assert cs[p] == (osc[p][ok].max() if ok.any() else -1), (rows, cap, pc, sf, tl, p)
         eng.close()
 
 
@@ -117,17 +121,18 @@ def test_step_policy_shapes():
 
 
 def test_step_at_large_n():
-    """Past one round of resident workgroups (400k nodes): the fused node pass's keys equal the
-    per-pair kernel's."""
+    """Past one round of resident workgroups (400k nodes): the step path's keys (streamed pass with
+    its tail on one wave or on four, the fused pass) equal the per-pair kernel's."""
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 400_000, 1500, seed=30, pod_step_ns=4_000_000, ds_frac=0.02)
     out = []
-    for opts in ({}, {"keys_path": 1}):
+    for opts in ({"keys_path": 1}, {}, {"k1_tail": 1}, {"k1_tail": 4}, {"k1_stream": 0}):
         eng = engine_for(spec, c, opts=opts)
         _, _, ch, cs = eng.eval(c.now, c.ds)
         out.append((ch, cs))
         eng.close()
-    assert np.array_equal(out[1][0], out[0][0]) and np.array_equal(out[1][1], out[0][1])
+    for i in range(1, len(out)):
+        assert np.array_equal(out[i][0], out[0][0]) and np.array_equal(out[i][1], out[0][1]), i
 
 
 def _oracle_hv(spec, c, now_ns):
