@@ -70,8 +70,14 @@ __device__ __forceinline__ int32_t score_at_lds(int64_t t, const NodeRec<PD, PR>
 #ifndef K1S_WAVES  // waves per SIMD the 4x6 form is built for (72 VGPRs: 7; 64: 8)
 #define K1S_WAVES 7
 #endif
-constexpr int kSRec = 64;   // stepped records staged per chunk
-constexpr int kSCap = 128;  // one-step records per kind staged in LDS (more: st.stage)
+#ifndef K1S_SREC
+#define K1S_SREC 64
+#endif
+#ifndef K1S_SCAP
+#define K1S_SCAP 128
+#endif
+constexpr int kSRec = K1S_SREC;  // stepped records staged per chunk
+constexpr int kSCap = K1S_SCAP;  // one-step records per kind staged in LDS (more: st.stage)
 
 template <int PD, int PR>
 __device__ __forceinline__ void emit_task(const NodeRec<PD, PR>& r, int64_t n, int q, const int32_t* dw, int64_t tmin,
@@ -369,6 +375,14 @@ void k1_stream_steps(K1Args a, K1Step step) {
         else put(static_cast<Rec*>(step.srec) + n);
     }
     __syncthreads();
+    // a grid of many rounds: the epilogue's single-wave phases run on wave 0 alone and the other
+    // waves leave, so their slots take the next workgroups' streams — before the emit when its
+    // tasks fit one wave, else before the tail; a grid of one or two rounds keeps all four waves
+    // (its time is one workgroup's chain)
+    const bool t1 = K1S_TAIL1 && (step.tail1 == 1 || (step.tail1 == 0 && gridDim.x >= 4096));
+    const bool emit1 = t1 && nst * (PR + 2) <= 64;  // (workgroup-uniform)
+    if (emit1 && threadIdx.x >= 64) return;
+    const int nthr = emit1 ? 64 : BS;
     for (int32_t c0 = 0; c0 < ((K1S_SKIP & 1) ? 0 : nst); c0 += kSRec) {  // (workgroup-uniform)
         const int32_t m = min(kSRec, nst - c0);
         if (c0 > 0) {  // this chunk's records from HBM (L2: written by this workgroup)
@@ -383,7 +397,7 @@ void k1_stream_steps(K1Args a, K1Step step) {
         }
         {
             constexpr int NB = PR + 2;
-            for (int tk = threadIdx.x; tk < m * NB; tk += BS) {  // (node, candidate): both kinds
+            for (int tk = threadIdx.x; tk < m * NB; tk += nthr) {  // (node, candidate): both kinds
                 const int j = tk / NB;
                 int q = tk - j * NB;
                 // (q = threadIdx.x % NB in every trip: without this the compiler hoists emit_task's
@@ -399,10 +413,7 @@ void k1_stream_steps(K1Args a, K1Step step) {
     CRANE_TSTAMP(a.trace, blockIdx.x, 5);
     // ---- D: the fused pass's tail
     if (K1S_SKIP & 2) return;
-    // a grid of many rounds: wave 0 alone runs the tail and the other three waves leave, so their
-    // slots take the next workgroups' streams (the tail is a few single-wave phases between
-    // barriers); a grid of one or two rounds keeps all four (its time is one workgroup's chain)
-    if (K1S_TAIL1 && (step.tail1 == 1 || (step.tail1 == 0 && gridDim.x >= 4096))) {
+    if (t1) {
         if (threadIdx.x >= 64) return;
         if (threadIdx.x < 2) {  // the block's flat maxima into wave 0's slot (tile rows read it)
             const int T = threadIdx.x;

@@ -8,10 +8,10 @@ cp $L $O/orig.so
 trap 'cp $O/orig.so $L' EXIT
 for rep in 1 2; do
   for m in "$@"; do
-    cp crane-scheduler_amd/lib_ab/lib_s$m.so $L || exit 1
+    cp crane-scheduler_amd/lib_ab/lib_$m.so $L || exit 1
     timeout -k 10 200 python -u bench.py --leg cold --steps 5 > $O/cold_${m}_$rep.log 2>&1 || { tail -20 $O/cold_${m}_$rep.log; exit 1; }
     python3 -c "
 import json; d=json.loads(open('$O/cold_${m}_$rep.log').read().strip().splitlines()[-1])
-print('skip=$m rep $rep', 'k1', d['k1']['ms'], d['k1']['frac'])"
+print('$m rep $rep', 'k1', d['k1']['ms'], d['k1']['frac'])"
   done
 done
