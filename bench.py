@@ -559,6 +559,9 @@ def dropin_leg(cd, spec, c, ann, now, ds, threads, dev_index, cpu_pods=0):
             cmd = [DROPIN, pp, sp, pods_f, "--threads", str(threads), "--churn", str(scale), "--churn-log", lp,
                    "--node-events", str(ev)]
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
+            if os.environ.get("CRANE_DROPIN_STDERR"):  # (diagnostics: the harness's stderr per run)
+                with open(f"{os.environ['CRANE_DROPIN_STDERR']}_{label}.txt", "w") as f:
+                    f.write(r.stderr)
             if r.returncode != 0:
                 return {"error": f"{label}: {r.stderr[-500:]}"}
             o = json.loads(r.stdout.strip().splitlines()[-1])

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -49,7 +50,7 @@ struct DevBuf {
     // staging that follows a varying size: geometric growth (an allocation syncs the device)
     hipError_t grow(size_t want) {
         if (want <= n && p) return hipSuccess;
-        return reserve(std::max({want, n + n / 2, (size_t)65536 / sizeof(T)}));
+        return reserve(std::max({want, n + n / 2, (size_t)(1 << 20) / sizeof(T)}));
     }
     void release() {
         if (p) (void)hipFree(p);
@@ -77,7 +78,7 @@ struct HostBuf {
     }
     hipError_t grow(size_t want) {  // (pinned allocations cost ~0.1-1 ms: geometric growth)
         if (want <= n && p) return hipSuccess;
-        return reserve(std::max({want, n + n / 2, (size_t)65536 / sizeof(T)}));
+        return reserve(std::max({want, n + n / 2, (size_t)(1 << 20) / sizeof(T)}));
     }
     void release() {
         if (p) (void)hipHostFree(p);
@@ -1327,8 +1328,13 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
         return h->fail(CRANE_E_INVALID, "NULL output");
     if (rows && !(rows->t0 < rows->t1)) return h->fail(CRANE_E_INVALID, "t0 must be before t1");
     if (k == 0) return CRANE_OK;
+    // CRANE_DYN_TRACE_UPD=1: each update's parts on stderr (the drop-in's slowest cycles)
+    static const bool trace_upd = std::getenv("CRANE_DYN_TRACE_UPD") != nullptr;
+    using TClock = std::chrono::steady_clock;
+    const TClock::time_point u0 = trace_upd ? TClock::now() : TClock::time_point{};
     HIPTRY(h, hipSetDevice(h->device));
     if (int rc = quiesce(h)) return rc;
+    const TClock::time_point u1 = trace_upd ? TClock::now() : TClock::time_point{};
     // the hot values come from the annotations again, as after crane_dyn_upload_nodes: records
     // built from binding-log counts are stale as a whole
     if (h->hv_from_counts) {
@@ -1352,7 +1358,6 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
     const size_t r_ns = o_out + 8 * K * S, r_ff = r_ns + K, r_sc = r_ff + K * (S + 1), r_end = r_sc + K * (S + 1);
     const size_t total = rows ? r_end : o_out;
     HIPTRY(h, h->upd_host.grow(total));
-    HIPTRY(h, h->upd_dev.grow(total));
     unsigned char* p = h->upd_host.p;
     std::memcpy(p, idx, 8 * K);
     if (M > 0) {
@@ -1363,8 +1368,12 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
         std::memcpy(p + o_hv, hv, 8 * K);
         std::memcpy(p + o_hvt, hv_ts, 8 * K);
     }
-    HIPTRY(h, hipMemcpyAsync(h->upd_dev.p, p, hv ? o_out : o_hv, hipMemcpyHostToDevice, h->stream));
-    unsigned char* d = h->upd_dev.p;
+    // The kernel reads the staged columns from and writes the rows to the pinned staging itself
+    // (a few KB to a few hundred): no copy-engine commands, whose first use after the device sat
+    // idle for a while cost the drop-in's first changed cycle 10-15 ms (the copy engines power
+    // down; a kernel's first launch after the same gap costs 0.3 ms, tools/idle_probe.py)
+    unsigned char* d = nullptr;
+    HIPTRY(h, hipHostGetDevicePointer(reinterpret_cast<void**>(&d), p, 0));
     UpdateArgs a{};
     a.pol = h->dp;
     a.N = h->N;
@@ -1390,11 +1399,20 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
         a.ff = reinterpret_cast<int8_t*>(d + r_ff);
         a.sc = reinterpret_cast<int8_t*>(d + r_sc);
     }
+    const TClock::time_point u2 = trace_upd ? TClock::now() : TClock::time_point{};
     HIPTRY(h, launch_update_nodes(h->shape, a, h->stream));
-    if (rows) HIPTRY(h, hipMemcpyAsync(p + o_out, d + o_out, r_end - o_out, hipMemcpyDeviceToHost, h->stream));
+    const TClock::time_point u3 = trace_upd ? TClock::now() : TClock::time_point{};
     // (waited for: the staging is reused, and work the caller enqueues next on its own
     // streams must see the new columns)
     HIPTRY(h, hipStreamSynchronize(h->stream));
+    if (trace_upd) {
+        auto us = [](TClock::time_point x, TClock::time_point y) {
+            return std::chrono::duration<double, std::micro>(y - x).count();
+        };
+        const TClock::time_point u4 = TClock::now();
+        std::fprintf(stderr, "crane_dyn update k=%lld: quiesce %.1f us, staging %.1f us, launch %.1f us, "
+                     "sync %.1f us\n", (long long)k, us(u0, u1), us(u1, u2), us(u2, u3), us(u3, u4));
+    }
     if (rows) {
         std::memcpy(rows->bp, p + o_out, 8 * K * S);
         std::memcpy(rows->n_steps, p + r_ns, K);
