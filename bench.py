@@ -586,6 +586,7 @@ def dropin_leg(cd, spec, c, ann, now, ds, threads, dev_index, cpu_pods=0):
                        "(churn_x1: its rate, each (node, metric) re-synced at the policy's periods; churn_x10: 10x)")
     for label, o in runs.items():
         out[label] = {k: o[k] for k in ("cycle_ms_median", "cycle_ms_p90", "cycle_ms_mean", "cycle_ms_max",
+                                        "cycle_ms_max_after_first_change",
                                         "changed_cycle_ms_median", "first_call_ms_median",
                                         "filter_fanout_ms_median", "score_fanout_ms_median", "select_ms_median",
                                         "pool_noop_ms_median", "patches", "simulated_s", "cycles_with_patches",
