@@ -223,6 +223,10 @@ def parse():
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache 4M-node K1/K2 roofline leg")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option name=value for the --leg runs (A/B of kernel forms; repeatable)")
+    ap.add_argument("--group-collective", type=int, default=1, choices=(0, 1, 2),
+                    help="group engine: 1 RCCL max all-reduce when n > 1, 2 always (rehearses it on one device), 0 never")
+    ap.add_argument("--group-threads", type=int, default=-1, choices=(-1, 0, 1),
+                    help="group engine: -1 auto (a worker per device when n > 1), 0 the caller's thread, 1 workers")
     ap.add_argument("--engine", default="group", choices=("group", "ranks"),
                     help="group: one process drives every GPU through the C ABI group (crane_dyn_group_*, "
                          "in-library RCCL); ranks: one process per GPU under torch.distributed (comparison)")
@@ -962,6 +966,8 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
     c.now, c.ds = g_all.now, g_all.ds
     K = max(1, args.inflight)
     grp = cd.Group(cd.Policy(spec), devices=list(range(n_dev)), depth=K)
+    grp.set_option("collective", args.group_collective)
+    grp.set_option("threads", args.group_threads)
     val_all, ts_all, _ = g_all.rows(grp.metric_names)
     grp.upload_nodes(val_all, ts_all, g_all.hv, g_all.hv_ts)
     grp.upload_bindings(g_all.b_node, g_all.b_ts)
@@ -1021,6 +1027,8 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
         grp.sync()
     batch_latency_ms = (time.perf_counter() - t1) * 1e3 / nl
     # per-kernel durations: shard 0's engine of slot 0 stepping the same batch on its own stream
+    coll = args.group_collective == 2 or (args.group_collective == 1 and n_dev > 1)
+    workers = args.group_threads == 1 or (args.group_threads == -1 and n_dev > 1)
     eng = grp.engine(0, 0)
     st0 = torch.cuda.Stream(devs[0])
     k0 = torch.empty(P, dtype=torch.int64, device=devs[0])
@@ -1034,8 +1042,10 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
                   "with an engine per device (own copy of its shard) on its own HIP stream, batch i on slot i % K; "
                   "every batch runs the whole shard step on every device" +
                   ("; then an in-place RCCL ncclAllReduce(int64, max) of its keys on each device's stream "
-                   "(ncclCommInitAll communicators, one enqueueing worker thread per device)" if n_dev > 1 else "")),
-             engine_path="group (C ABI, in-library RCCL)" if n_dev > 1 else "group (C ABI, one device)",
+                   "(ncclCommInitAll communicators)" if coll else "") +
+                  ("; enqueued by one worker thread per device" if workers else "; enqueued by the caller's thread")),
+             engine_path=("group (C ABI, in-library RCCL" + (", rehearsed on one device)" if n_dev == 1 else ")")
+                          if coll else "group (C ABI, one device)"),
              n_gpus=n_dev)
     m["close"] = lambda: grp.close()
     return m
