@@ -222,7 +222,7 @@ def parse():
                     help="matrix2 / matrix3 / cold: only that leg (for per-kernel PMC passes)")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache 4M-node K1/K2 roofline leg")
     ap.add_argument("--opt", action="append", default=[],
-                    help="engine option name=value for the --leg runs (A/B of kernel forms; repeatable)")
+                    help="engine option name=value (A/B of kernel forms; repeatable): the --leg runs and the group step")
     ap.add_argument("--group-collective", type=int, default=1, choices=(0, 1, 2),
                     help="group engine: 1 RCCL max all-reduce when n > 1, 2 always (rehearses it on one device), 0 never")
     ap.add_argument("--group-threads", type=int, default=-1, choices=(-1, 0, 1),
@@ -968,6 +968,9 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
     grp = cd.Group(cd.Policy(spec), devices=list(range(n_dev)), depth=K)
     grp.set_option("collective", args.group_collective)
     grp.set_option("threads", args.group_threads)
+    for o in args.opt:  # engine options (name=value) on every slot's engines
+        k, v = o.split("=")
+        grp.set_option(k, int(v))
     val_all, ts_all, _ = g_all.rows(grp.metric_names)
     grp.upload_nodes(val_all, ts_all, g_all.hv, g_all.hv_ts)
     grp.upload_bindings(g_all.b_node, g_all.b_ts)

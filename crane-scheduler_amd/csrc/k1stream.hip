@@ -60,7 +60,8 @@ __device__ __forceinline__ int32_t score_at_lds(int64_t t, const NodeRec<PD, PR>
 }
 
 // K1S_SKIP (cost ablation builds only, tools/gpu_k1_ablate.sh; wrong tables): 1 no emit tasks,
-// 2 no tail (sort / pieces / tile rows), 4 no record staging
+// 2 no tail (sort / pieces / tile rows), 4 no record staging, 8 middle pieces left raw (no
+// elementary pieces: the tables stay right, K3s reads every piece), 16 no tile rows
 #ifndef K1S_SKIP
 #define K1S_SKIP 0
 #endif
@@ -172,11 +173,11 @@ __device__ __forceinline__ void tail(bool g1, Rec* lrec, Step1* s1l, Step1* srt,
     if (g1) step_sort_publish_global<BS>(ssh, step.st, blk);
     else step_sort_publish<BS, kSCap>(s1l, srt, ssh, step.st, blk);
     CRANE_TSTAMP(trace, blockIdx.x, 6);
-    if (step.st.rows) {
+    if (step.st.rows && !(K1S_SKIP & 16)) {
         int64_t tpre = 0;  // this thread's first tile-row bound (step_tile_rows)
         tile_prefetch(step.st, &tpre);
         constexpr int kPc = ((int)(kSRec * sizeof(Rec)) / PieceScr::bytes_per_piece) & ~3;
-        const PieceScr ps{reinterpret_cast<unsigned char*>(lrec), kPc < 128 ? kPc : 128};
+        const PieceScr ps{reinterpret_cast<unsigned char*>(lrec), (K1S_SKIP & 8) ? 0 : (kPc < 128 ? kPc : 128)};
         step_pieces<BS>(ssh, step.st, blk, ps);
         if (g1) step_tile_rows<BS, kSCap, true>(s1l, srt, ssh, step.st, blk, &tpre, ps);
         else step_tile_rows<BS, kSCap, false>(s1l, srt, ssh, step.st, blk, &tpre, ps);
