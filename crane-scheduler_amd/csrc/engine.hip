@@ -1403,8 +1403,18 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
     HIPTRY(h, launch_update_nodes(h->shape, a, h->stream));
     const TClock::time_point u3 = trace_upd ? TClock::now() : TClock::time_point{};
     // (waited for: the staging is reused, and work the caller enqueues next on its own
-    // streams must see the new columns)
-    HIPTRY(h, hipStreamSynchronize(h->stream));
+    // streams must see the new columns).  Polled for the first 2 ms, then a blocking wait: the
+    // update is tens of microseconds of GPU work, and a blocking wait's wake-up is the host's
+    // interrupt path, slow when every core is busy (the framework's goroutines spin meanwhile)
+    {
+        const TClock::time_point w0 = TClock::now();
+        hipError_t q;
+        while ((q = hipStreamQuery(h->stream)) == hipErrorNotReady &&
+               TClock::now() - w0 < std::chrono::milliseconds(2))
+            __builtin_ia32_pause();
+        if (q == hipErrorNotReady) q = hipStreamSynchronize(h->stream);
+        HIPTRY(h, q);
+    }
     if (trace_upd) {
         auto us = [](TClock::time_point x, TClock::time_point y) {
             return std::chrono::duration<double, std::micro>(y - x).count();

@@ -179,9 +179,11 @@ constexpr int kXChunk = kHxRegion;  // bindings per dedupe-form workgroup (K1 re
 // bin for the hottest bins instead).
 constexpr int kDSlots = 4096;  // 2 slots per binding: an empty or matching slot always exists
 
-// (Round 5 measured one packed 64-bit (key << 32 | count) slot with a plain read before the CAS
-// against these split key / count arrays: k2l_partition 0.042 -> 0.048 ms on the ordered log,
-// 0.063 -> 0.071 on the stamp path, cold 4M x 16M: reverted.)
+// (Round 5 measured against these split key / count arrays, cold 4M x 16M, same boxes, reverted:
+// one packed 64-bit (key << 32 | count) slot with a plain read before the CAS — k2l_partition
+// 0.042 -> 0.048 ms on the ordered log, 0.063 -> 0.071 on the stamp path; a thread's four first
+// probes issued back to back and waited for together — 0.042 -> 0.044, 0.061 -> 0.066: the
+// hash phase is bound by the LDS atomics' throughput and bank conflicts, not their latency.)
 // Adds `add` to key's count; a lane that inserts a new key also counts it in its
 // bin and returns its slot (else -1).  One returning LDS atomic per probe (the CAS
 // itself tells an empty, a matching and a foreign slot apart).
