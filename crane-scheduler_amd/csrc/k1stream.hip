@@ -119,8 +119,8 @@ __device__ __forceinline__ void emit_task(const NodeRec<PD, PR>& r, int64_t n, i
     const int rk1 = rk0 - (fb ? 1 : 0);
     // one score per instant serves both kinds (the Filter only gates kind 0's key)
     const int64_t pk = pack_key(score_at_lds<PD, PR>(cq, r, wsum, noprio, winv), n);
-    const bool need0 = rk0 == 0 || (q != F && rk1 == 0);
-    const int64_t pk0 = need0 ? pack_key(score_at_lds<PD, PR>(tmin, r, wsum, noprio, winv), n) : 0;
+    // the score at tmin: phase A's, kept in the record's slot words (dw[5])
+    const int64_t pk0 = pack_key(dw[5], n);
 #pragma unroll
     for (int T = 0; T < 2; ++T) {
         const int32_t slot = dw[T ? 2 : 0];
@@ -191,7 +191,7 @@ void k1_stream_steps(K1Args a, K1Step step) {
     using Rec = NodeRec<PD, PR>;
     constexpr int BS = 256;
     // a staged stepped node's record: e_fail, pen, e_hv, e_prio, t (what the emit reads), and in
-    // e_pred's first words its slots per kind (slot < 0: none) and multi flags
+    // e_pred's first words its slots per kind (slot < 0: none), multi flags and the score at tmin
     __shared__ __attribute__((aligned(16))) Rec lrec[kSRec];
     __shared__ uint8_t rank_lane[BS];  // a stepped node's rank in the block -> its lane
     __shared__ __attribute__((aligned(16))) Step1 s1l[2 * kSCap];  // one-step staging, then pm / sm maxima
@@ -369,6 +369,7 @@ void k1_stream_steps(K1Args a, K1Step step) {
         dw[2] = slot1;
         dw[3] = mslot1;
         dw[4] = (multi0 ? 1 : 0) | (multi1 ? 2 : 0);
+        dw[5] = s0;  // score_at(tmin): the keys before a node's first step
     };
     if (stepped && !(K1S_SKIP & 4)) {
         rank_lane[rs] = (uint8_t)threadIdx.x;
