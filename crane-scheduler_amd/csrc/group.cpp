@@ -66,6 +66,7 @@ struct crane_dyn_group {
     int threads = -1;    // -1: worker threads when n > 1, 0: the caller's thread, 1: worker threads
     bool comm_broken = false;
     uint64_t batch = 0;
+    uint64_t synced = 0;  // batch at the last wait_all: the slots used since are the ones to wait for
     std::vector<std::unique_ptr<GroupWorker>> workers;
     // crane_dyn_group_schedule's device buffers per device, and its pinned key staging
     std::vector<int64_t*> b_now, b_keys;
@@ -219,12 +220,19 @@ int wait_all(crane_dyn_group* g) {
         g->comm.clear();
         g->comm_broken = true;
     }
-    for (int s = 0; s < g->depth; ++s)
+    // the slots that ran batches since the last wait, oldest first (by the time the oldest is
+    // done the others mostly are: a wait on every slot, idle or not, cost the short timed
+    // regions a few microseconds per slot)
+    const uint64_t used = std::min<uint64_t>(g->batch - g->synced, (uint64_t)g->depth);
+    for (uint64_t b = g->batch - used; b < g->batch; ++b) {
+        const size_t s = (size_t)(b % (uint64_t)g->depth);
         for (int i = 0; i < g->n; ++i) {
             hipError_t e = hipSetDevice(g->dev[(size_t)i]);
-            if (e == hipSuccess) e = hipStreamSynchronize(g->st[(size_t)s][(size_t)i]);
+            if (e == hipSuccess) e = hipStreamSynchronize(g->st[s][(size_t)i]);
             if (e != hipSuccess && !rc) rc = g->hipfail(e, "hipStreamSynchronize");
         }
+    }
+    g->synced = g->batch;
     return rc;
 }
 
