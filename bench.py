@@ -33,6 +33,7 @@ import glob
 import hashlib
 import json
 import os
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -534,7 +535,47 @@ def synth_shanghai():
     return synth.SHANGHAI
 
 
-def dropin_leg(cd, spec, c, ann, now, ds, threads, dev_index, cpu_pods=0):
+def dropin_runs(spec, ann, now, ds, threads, cpu_pods=0):
+    """The drop-in harness runs of dropin_leg (subprocesses only: call it before this process
+    touches the GPU, so the harness's queues are the only ones on the device, as in a scheduler
+    process — a parent holding a dozen idle queues made the harness's first update after its
+    initial sync wait 5-20 ms for the hardware scheduler).  Returns the runs' outputs and the
+    temporary directory holding their churn logs (removed by dropin_leg)."""
+    d = tempfile.mkdtemp(prefix="crane_dropin_")
+    env = dict(os.environ, TZ="Asia/Shanghai")
+    pp, sp, pd = _dropin_files(d, spec, ann, now, ds)
+    now_long = now[0] + np.arange(len(now), dtype=np.int64) * 10**9
+    pd_long = os.path.join(d, "pods_long.tsv")
+    with open(pd_long, "w") as f:
+        for p in range(len(now)):
+            f.write(f"P\tpod-{p}\t{int(now_long[p])}\t{int(ds[p])}\n")
+    runs = {"dir": d, "now_long": now_long, "out": {}, "err": None, "cpu": None}
+    if not os.path.exists(DROPIN):
+        runs["err"] = f"{DROPIN} not built"
+        return runs
+    for label, scale, ev, pods_f in (("churn_x1", 1.0, 0, pd), ("churn_x10", 10.0, 0, pd), ("frozen", 0.0, 0, pd),
+                                     ("nodes_and_time", 1.0, 8, pd_long)):
+        lp = os.path.join(d, f"{label}.log")
+        cmd = [DROPIN, pp, sp, pods_f, "--threads", str(threads), "--churn", str(scale), "--churn-log", lp,
+               "--node-events", str(ev)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
+        if os.environ.get("CRANE_DROPIN_STDERR"):  # (diagnostics: the harness's stderr per run)
+            with open(f"{os.environ['CRANE_DROPIN_STDERR']}_{label}.txt", "w") as f:
+                f.write(r.stderr)
+        if r.returncode != 0:
+            runs["err"] = f"{label}: {r.stderr[-500:]}"
+            return runs
+        runs["out"][label] = (json.loads(r.stdout.strip().splitlines()[-1]), lp)
+    if cpu_pods and os.path.exists(DROPIN_CPU):
+        d2 = os.path.join(d, "cpu")
+        os.makedirs(d2)
+        pp2, sp2, pd2 = _dropin_files(d2, spec, ann, now[:cpu_pods], ds[:cpu_pods])
+        runs["cpu"] = subprocess.run([DROPIN_CPU, pp2, sp2, pd2, "--threads", str(threads), "--cpu", "--churn", "1"],
+                                     capture_output=True, text=True, timeout=900, env=env)
+    return runs
+
+
+def dropin_leg(cd, spec, c, ann, now, ds, threads, dev_index, cpu_pods=0, runs=None):
     """Per-pod cycle of the C++ plugin mirror as the framework drives it (tools/dropin_bench.cpp),
     with its parts, while the controller patches annotations at its own rate (churn x1: every
     (node, metric) re-synced at the policy's periods, metric + node_hot_value per sync) and at 10x
@@ -542,44 +583,25 @@ def dropin_leg(cd, spec, c, ann, now, ds, threads, dev_index, cpu_pods=0):
     re-uploaded with the churned snapshot (and a pod sample against the oracle).  With cpu_pods > 0
     (the CPU-baseline leg) the same harness drives a CPU plugin that re-parses annotations per
     call (oracle string mode) on the first cpu_pods pods, under the same churn."""
-    if not os.path.exists(DROPIN):
-        return {"error": f"{DROPIN} not built"}
-    env = dict(os.environ, TZ="Asia/Shanghai")
-    out = {}
-    with tempfile.TemporaryDirectory() as d:
-        pp, sp, pd = _dropin_files(d, spec, ann, now, ds)
-        runs, chosen = {}, {}
-        # nodes_and_time: pods 1 s apart (255 s of pod time: past any one-minute table span) at the
-        # controller's rate, a node joining every 8th cycle and one leaving in between
-        now_long = now[0] + np.arange(len(now), dtype=np.int64) * 10**9
-        pd_long = os.path.join(d, "pods_long.tsv")
-        with open(pd_long, "w") as f:
-            for p in range(len(now)):
-                f.write(f"P\tpod-{p}\t{int(now_long[p])}\t{int(ds[p])}\n")
-        for label, scale, ev, pods_f, pnow in (("churn_x1", 1.0, 0, pd, now), ("churn_x10", 10.0, 0, pd, now),
-                                               ("frozen", 0.0, 0, pd, now),
-                                               ("nodes_and_time", 1.0, 8, pd_long, now_long)):
-            lp = os.path.join(d, f"{label}.log")
-            cmd = [DROPIN, pp, sp, pods_f, "--threads", str(threads), "--churn", str(scale), "--churn-log", lp,
-                   "--node-events", str(ev)]
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
-            if os.environ.get("CRANE_DROPIN_STDERR"):  # (diagnostics: the harness's stderr per run)
-                with open(f"{os.environ['CRANE_DROPIN_STDERR']}_{label}.txt", "w") as f:
-                    f.write(r.stderr)
-            if r.returncode != 0:
-                return {"error": f"{label}: {r.stderr[-500:]}"}
-            o = json.loads(r.stdout.strip().splitlines()[-1])
+    if runs is None:  # (the harness runs now: this process already holds GPU queues)
+        runs = dropin_runs(spec, ann, now, ds, threads, cpu_pods)
+    try:
+        if runs["err"]:
+            return {"error": runs["err"]}
+        res, chosen = {}, {}
+        for label, (o, lp) in runs["out"].items():
+            pnow = runs["now_long"] if label == "nodes_and_time" else now
             ch = chosen[label] = np.array(o.pop("chosen"))
             ref, orc = _replay_chosen(cd, spec, c, dev_index, pnow, ds, lp,
                                       oracle_pods=(0, len(now) // 2, len(now) - 1))
             o["matches_engine_chosen"] = bool(np.array_equal(ch, ref))
             o["matches_oracle_sample"] = orc
-            runs[label] = o
-        rc = None
-        if cpu_pods and os.path.exists(DROPIN_CPU):
-            pp2, sp2, pd2 = _dropin_files(d, spec, ann, now[:cpu_pods], ds[:cpu_pods])
-            rc = subprocess.run([DROPIN_CPU, pp2, sp2, pd2, "--threads", str(threads), "--cpu", "--churn", "1"],
-                                capture_output=True, text=True, timeout=900, env=env)
+            res[label] = o
+        rc = runs["cpu"]
+    finally:
+        shutil.rmtree(runs["dir"], ignore_errors=True)
+    runs = res
+    out = {}
     main = runs["churn_x1"]
     out["dropin_ms_per_pod"] = main["cycle_ms_median"]
     out["matches_engine_chosen"] = all(r["matches_engine_chosen"] for r in runs.values())
@@ -598,11 +620,13 @@ def dropin_leg(cd, spec, c, ann, now, ds, threads, dev_index, cpu_pods=0):
                                         "nodes_joined", "nodes_left", "shard_grows", "slowest",
                                         "errors", "sync_ms", "matches_engine_chosen", "matches_oracle_sample")}
     out["how"] = ("each patch publishes a new Node object (informer); the plugin compares every NodeInfo with the "
-                  "one it parsed at the cycle's first call, re-parses only the changed nodes, scatters them into the "
-                  "engine (crane_dyn_update_nodes) and rebuilds their table rows (crane_dyn_node_steps_subset); "
+                  "one it parsed at the cycle's first call, re-parses only the changed nodes (the cycle's callers "
+                  "share the parse), writes them into the engine and rebuilds their table rows in one call "
+                  "(crane_dyn_update_node_steps); joining nodes take free rows, leaving ones free theirs; "
                   "first_call = that first Filter call; sync_ms = the initial full parse + upload + table; "
-                  "pool_noop = the harness's two fan-outs over no-op calls (not part of the cycle); checks: every "
-                  "pod's chosen node vs one engine re-uploaded with the churned snapshot, 3 pods vs the oracle")
+                  "pool_noop = the harness's two fan-outs over no-op calls (not part of the cycle); the harness runs "
+                  "before the bench process touches the GPU (a scheduler process holds the device alone); checks: "
+                  "every pod's chosen node vs one engine re-uploaded with the churned snapshot, 3 pods vs the oracle")
     if rc is not None:
         if rc.returncode != 0:
             out["cpu_same_harness_error"] = rc.stderr[-300:]
@@ -1081,14 +1105,26 @@ def main():
     elif not group and (world > 1 or args.rehearse_collective):
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if not group else 0)
-    torch.cuda.set_device(dev)
-
     import crane_dyn as cd
     from crane_dyn import synth
 
-    shash = src_hash()
     spec = cd.default_policy_spec()
+    # the drop-in harness runs first, while this process holds no GPU queue (dropin_runs); its
+    # snapshot is the config-3 cell measure_group builds (same seeds), checked there
+    early = None
+    if (args.leg == "all" and group and args.gpus == 1 and not args.no_extras and not args.no_cpu_baseline
+            and args.config == 3 and rank == 0):
+        cfg = synth.CONFIGS[3]
+        c0 = synth.make_cluster(spec, cfg["nodes"], cfg["pods"], n_bindings=cfg["bindings"], seed=20250215 + 3000)
+        c0.now, c0.ds = synth.make_pods(cfg["pods"], seed=20250215 + 3)
+        ann0 = c0.annotations()
+        early = {"c": c0, "ann": ann0,
+                 "runs": dropin_runs(spec, ann0, c0.now[:256], c0.ds[:256], args.cpu_threads, cpu_pods=4)}
+    args.early = early
+
+    dev = torch.device("cuda", local if not group else 0)
+    torch.cuda.set_device(dev)
+    shash = src_hash()
     if args.leg == "cold":
         pmc_c, pmc_cs = pmc_summary("cold", shash)
         out = cold_leg(cd, synth, spec, dev, reps=max(2, args.steps), pmc=pmc_c, pmc_src=pmc_cs, opts=args.opt)
@@ -1222,7 +1258,12 @@ def finish(cd, synth, spec, args, m, n_gpus, rank, solo, dev, shash):
     if one and not args.no_cpu_baseline and args.config == 3:
         # (the headline configuration only: config 4's 1M-node annotation strings alone take minutes to build)
         from oracle import oracle as O
-        ann = c.annotations()
+        early = getattr(args, "early", None)
+        same = (early is not None and early["c"].n_nodes == c.n_nodes and np.array_equal(early["c"].hv, c.hv)
+                and np.array_equal(early["c"].now, c.now) and np.array_equal(early["c"].b_node, c.b_node))
+        ann = early["ann"] if same else c.annotations()
+        if early is not None and not same:
+            shutil.rmtree(early["runs"]["dir"], ignore_errors=True)
         ncpu = effective_cpus()
         legs = {}
         for label, th in (("threads_16", args.cpu_threads), ("threads_all", ncpu)):
@@ -1276,7 +1317,7 @@ def finish(cd, synth, spec, args, m, n_gpus, rank, solo, dev, shash):
             # the drop-in plugin cycle under annotation churn, and the
             # controller's hot-value sync
             extras["dropin"] = dropin_leg(cd, spec, c, ann, c.now[:256], c.ds[:256], args.cpu_threads, local,
-                                          cpu_pods=4)
+                                          cpu_pods=4, runs=early["runs"] if same else None)
             extras["controller_hot_values"] = controller_leg(cd, O, synth, spec, dev, c, N, B)
 
     if rank == 0:

@@ -1400,18 +1400,31 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
         a.sc = reinterpret_cast<int8_t*>(d + r_sc);
     }
     const TClock::time_point u2 = trace_upd ? TClock::now() : TClock::time_point{};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    if (trace_upd && hipEventCreate(&ev[0]) == hipSuccess && hipEventCreate(&ev[1]) == hipSuccess)
+        (void)hipEventRecord(ev[0], h->stream);
     HIPTRY(h, launch_update_nodes(h->shape, a, h->stream));
+    if (ev[1]) (void)hipEventRecord(ev[1], h->stream);
     const TClock::time_point u3 = trace_upd ? TClock::now() : TClock::time_point{};
     // (waited for: the staging is reused, and work the caller enqueues next on its own
     // streams must see the new columns).  Polled for the first 2 ms, then a blocking wait: the
     // update is tens of microseconds of GPU work, and a blocking wait's wake-up is the host's
     // interrupt path, slow when every core is busy (the framework's goroutines spin meanwhile)
+    long long nq = 0;
+    double qmax_us = 0.0;
     {
         const TClock::time_point w0 = TClock::now();
         hipError_t q;
-        while ((q = hipStreamQuery(h->stream)) == hipErrorNotReady &&
-               TClock::now() - w0 < std::chrono::milliseconds(2))
+        for (;;) {
+            const TClock::time_point a0 = trace_upd ? TClock::now() : TClock::time_point{};
+            q = hipStreamQuery(h->stream);
+            if (trace_upd) {
+                ++nq;
+                qmax_us = std::max(qmax_us, std::chrono::duration<double, std::micro>(TClock::now() - a0).count());
+            }
+            if (q != hipErrorNotReady || TClock::now() - w0 >= std::chrono::milliseconds(2)) break;
             __builtin_ia32_pause();
+        }
         if (q == hipErrorNotReady) q = hipStreamSynchronize(h->stream);
         HIPTRY(h, q);
     }
@@ -1420,8 +1433,13 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
             return std::chrono::duration<double, std::micro>(y - x).count();
         };
         const TClock::time_point u4 = TClock::now();
+        float gpu_ms = -1.f;
+        if (ev[1]) (void)hipEventElapsedTime(&gpu_ms, ev[0], ev[1]);
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
         std::fprintf(stderr, "crane_dyn update k=%lld: quiesce %.1f us, staging %.1f us, launch %.1f us, "
-                     "sync %.1f us\n", (long long)k, us(u0, u1), us(u1, u2), us(u2, u3), us(u3, u4));
+                     "sync %.1f us (kernel between events %.1f us; %lld queries, the longest %.1f us)\n",
+                     (long long)k, us(u0, u1), us(u1, u2), us(u2, u3), us(u3, u4), gpu_ms * 1000.f, nq, qmax_us);
     }
     if (rows) {
         std::memcpy(rows->bp, p + o_out, 8 * K * S);
