@@ -137,6 +137,8 @@ struct Options {
     int k1_tail = 0;          // the streamed pass's tail: 0 on one wave when the grid has >= 4096 blocks
                               // (the other waves leave), 1 always on one wave, 4 on all four
     int k2_sorted = 1;        // a time-ordered log: K2 reads the widest window's suffix, ranks by position
+    int k2_slide = 0;         // 1: ... and keeps dense window counts, moved by the bindings between the last
+                              // refresh's window starts and this one's | 0 recount every refresh
 };
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
 
@@ -183,6 +185,8 @@ struct crane_dyn {
     std::vector<int64_t> hts_copy;      // ... and its timestamps (the windows' suffixes are found here)
     std::vector<int64_t> hts_sample;    // every 64th of them: the suffix search touches one 512-byte run
     bool pos_valid = false;             // pos_s[r]: the suffix start of window rank r for cutoffs pos_cut
+    bool slide_valid = false;           // buckets hold the window-rank counts for suffix starts slide_s
+    int64_t slide_s[kMaxWin] = {};
     int64_t pos_cut[kMaxWin] = {};
     int64_t pos_s[kMaxWin] = {};
     HostBuf<int32_t> hnode;       // pinned mirror of the slots in heap mode
@@ -426,9 +430,49 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         bn = h->bnode.p + s0;
         Bk = h->B - s0;
     }
+    // Sliding windows: the last refresh's dense counts moved by the bindings between its window
+    // starts and this one's (a batch 10 s later: tens of thousands of bindings instead of the
+    // suffix's hundreds of thousands); a first refresh, or most of the log in between, recounts
+    // with the large form (dense counts), which the next refreshes then move
+    const bool slide = by_pos && h->opt.k2_slide != 0 && h->opt.k2_form == 0;
+    if (!slide) h->slide_valid = false;
+    if (slide && h->slide_valid) {
+        SlideArgs sa{};
+        sa.bnode = h->bnode.p;
+        sa.N = h->N;
+        sa.W = dp.n_win;
+        sa.buckets = h->buckets.p;
+        std::pair<int64_t, int64_t> iv[kMaxWin];
+        int ni = 0;
+        for (int r = 0; r < dp.n_win; ++r) {
+            sa.s_old[r] = h->slide_s[r];
+            sa.s_new[r] = h->pos_s[r];
+            const int64_t a = std::min(sa.s_old[r], sa.s_new[r]), b = std::max(sa.s_old[r], sa.s_new[r]);
+            if (a < b) iv[ni++] = {a, b};
+        }
+        std::sort(iv, iv + ni);
+        for (int i = 0; i < ni; ++i) {  // the disjoint union
+            if (sa.nr > 0 && iv[i].first <= sa.lo[sa.nr - 1] + sa.len[sa.nr - 1]) {
+                sa.len[sa.nr - 1] = std::max(sa.len[sa.nr - 1], iv[i].second - sa.lo[sa.nr - 1]);
+            } else {
+                sa.lo[sa.nr] = iv[i].first;
+                sa.len[sa.nr] = iv[i].second - iv[i].first;
+                ++sa.nr;
+            }
+        }
+        for (int i = 0; i < sa.nr; ++i) sa.total += sa.len[i];
+        if (sa.total <= Bk / 2) {
+            HIPTRY(h, launch_hot_slide(sa, st, pods));
+            if (pods_done) *pods_done = pods != nullptr && pods->P > 0;
+            std::memcpy(h->slide_s, h->pos_s, sizeof(int64_t) * dp.n_win);
+            h->buckets_zero = false;
+            h->buckets_dense = true;
+            return CRANE_OK;
+        }
+    }
     HotPart gx = hot_dedupe_geometry(Bk, h->N, dp.n_win, h->opt.k1_threads);
     gx.trace = gx.nblk <= kTraceWgs ? h->trace_region(0) : nullptr;
-    if (h->opt.k2_form == 0 && gx.ok) {
+    if (h->opt.k2_form == 0 && gx.ok && !slide) {
         // one launch (+ K3p); the node pass counts its own block's entries (no buckets).  The
         // scratch is sized for the whole log, not this refresh's suffix: the suffix moves with
         // `now`, and a reallocation (hipFree waits for the device) inside a pipeline of batches
@@ -456,9 +500,12 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
                                          h->buckets.p, h->n_cu, st, h->opt.k2l_threads));
         h->buckets_zero = false;
         h->buckets_dense = true;
+        h->slide_valid = slide;
+        if (slide) std::memcpy(h->slide_s, h->pos_s, sizeof(int64_t) * dp.n_win);
         return CRANE_OK;
     }
     h->buckets_dense = false;
+    h->slide_valid = false;
     if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
     const HotBins g = hot_bins_geometry(h->B, h->N, dp.n_win);
     if (g.ok && h->opt.k2_form != 2) {
@@ -819,6 +866,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
     else if (n == "k2_sorted" && range(0, 1)) o.k2_sorted = (int)value;
     else if (n == "k1_stream" && range(0, 1)) o.k1_stream = (int)value;
+    else if (n == "k2_slide" && range(0, 1)) o.k2_slide = (int)value;
     else if (n == "k1_tail" && (value == 0 || value == 1 || value == 4)) o.k1_tail = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
@@ -875,6 +923,7 @@ int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const d
     }
     HIPTRY(h, hipStreamSynchronize(h->stream));
     if (n != h->N) h->buckets_zero = false;
+    h->slide_valid = false;
     h->N = n;
     h->node_offset = node_offset;
     h->have_hv = hv != nullptr;
@@ -901,6 +950,7 @@ int crane_dyn_upload_bindings(crane_dyn* h, int64_t n, const int32_t* node, cons
     // a ring of bindings appended in time order (the synthetic and the controller-shaped logs):
     // kept for the suffix search of every refresh
     h->pos_valid = false;
+    h->slide_valid = false;
     h->log_sorted = n > 0 && std::is_sorted(ts_s, ts_s + n);
     h->hts_sample.clear();
     if (h->log_sorted) {
@@ -940,6 +990,7 @@ int crane_dyn_binding_records(crane_dyn* h, int64_t size, int64_t gc_time_range_
     h->heap_mode = true;
     h->log_sorted = false;  // heap order
     h->pos_valid = false;
+    h->slide_valid = false;
     h->hts_copy.clear();
     h->hts_sample.clear();
     h->B = size;
@@ -1506,6 +1557,7 @@ int crane_dyn_resize_nodes(crane_dyn* h, int64_t n) {
     HIPTRY(h, h->rec.reserve((size_t)n * h->rec_bytes));
     h->N = n;
     h->buckets_zero = false;
+    h->slide_valid = false;     // the dense counts' layout is [W][N]
     h->hv_from_counts = false;  // binding-log hot values were per old node index
     h->counts_pending = false;
     h->hx_pending = false;

@@ -708,4 +708,53 @@ hipError_t launch_hot_count_binned(const int32_t* bnode, const int64_t* bts, int
     return e;
 }
 
+
+// ---------------------------------------------------------------- sliding windows (kernels.hpp)
+constexpr int kSlideThreads = 512;
+__device__ __forceinline__ void slide_body(const SlideArgs& a, int64_t b, int64_t nb) {
+    for (int64_t i = b * kSlideThreads + threadIdx.x; i < a.total; i += nb * kSlideThreads) {
+        int64_t off = i, p = -1;
+        for (int r = 0; r < a.nr; ++r) {  // (nr <= kMaxWin: the range holding flat index i)
+            if (p < 0 && off < a.len[r]) p = a.lo[r] + off;
+            off -= a.len[r];
+        }
+        int ro = 0, rn = 0;
+        for (int r = 0; r < a.W; ++r) {
+            ro += p >= a.s_old[r];
+            rn += p >= a.s_new[r];
+        }
+        if (ro == rn) continue;
+        const int32_t nd = a.bnode[p];
+        if (nd < 0 || (int64_t)nd >= a.N) continue;  // binding.go:85-91 counts known nodes only
+        if (ro > 0) atomicSub(&a.buckets[(int64_t)(ro - 1) * a.N + nd], 1u);
+        if (rn > 0) atomicAdd(&a.buckets[(int64_t)(rn - 1) * a.N + nd], 1u);
+    }
+}
+
+__global__ __launch_bounds__(kSlideThreads) void k2s_slide(SlideArgs a) {
+    slide_body(a, blockIdx.x, gridDim.x);
+}
+
+__global__ __launch_bounds__(kSlideThreads) void k2s_slide_pods(SlideArgs a, PodPrep pp) {
+    if ((int64_t)blockIdx.x < pp.ntiles) {  // the pod tiles first (dispatched first)
+        extern __shared__ __attribute__((aligned(16))) unsigned char k3p_lds[];
+        k3p_tile<kSlideThreads>((int64_t)blockIdx.x, pp, k3p_lds);
+    } else {
+        slide_body(a, (int64_t)blockIdx.x - pp.ntiles, (int64_t)gridDim.x - pp.ntiles);
+    }
+}
+
+hipError_t launch_hot_slide(const SlideArgs& a, hipStream_t st, const PodPrep* pods) {
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((a.total + kSlideThreads - 1) / kSlideThreads, 1024));
+    if (pods && pods->P > 0) {
+        static const hipError_t attr = hipFuncSetAttribute((const void*)k2s_slide_pods,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kK3pLds);
+        if (attr != hipSuccess) return attr;
+        return klaunch("k2s_slide+k3p_pods", k2s_slide_pods, dim3((unsigned)(pods->ntiles + (a.total > 0 ? nb : 0))),
+                       dim3(kSlideThreads), kK3pLds, st, a, *pods);
+    }
+    if (a.total <= 0) return hipSuccess;
+    return klaunch("k2s_slide", k2s_slide, dim3((unsigned)nb), dim3(kSlideThreads), 0, st, a);
+}
+
 }  // namespace crane

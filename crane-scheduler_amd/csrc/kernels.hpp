@@ -239,6 +239,23 @@ hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int6
                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, uint32_t* buckets,
                                   int n_cu, hipStream_t st, int threads = 512);
 
+// Sliding windows on a time-ordered log (round 5): the dense window-rank buckets [W][N] of the
+// previous refresh, whose window suffixes started at positions s_old[r], moved to the cutoffs'
+// new starts s_new[r]: only the bindings between an old and a new start change rank — each
+// leaves its old bucket and joins its new one (rank = #{r : p >= s[r]}, bucket rank - 1, rank 0
+// counted nowhere).  ranges: the disjoint union of [min(s_old, s_new), max(s_old, s_new)) per
+// rank (nr <= kMaxWin).  With pods, K3p's tiles ride as the launch's first workgroups.
+struct SlideArgs {
+    const int32_t* bnode;
+    int64_t N;
+    int32_t W, nr;
+    int64_t s_old[kMaxWin], s_new[kMaxWin];
+    int64_t lo[kMaxWin], len[kMaxWin];  // the ranges
+    int64_t total;                      // their summed length
+    uint32_t* buckets;
+};
+hipError_t launch_hot_slide(const SlideArgs& a, hipStream_t st, const PodPrep* pods = nullptr);
+
 // ---------------------------------------------------------------- K3 step path (step.hip)
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
 constexpr int64_t kStepMaxNodes = 1LL << 24;  // packed key keeps 24 bits of node index

@@ -320,6 +320,8 @@ const char *crane_dyn_version(void);
  *   "k2_form" 0 dedupe (default; large past its cap) | 1 binned | 2 hash | 3 large   "k1_threads" 256 | 128
  *   "k1_keep_records" 0 | 1   "k1_fuse_steps" 1 | 0   "k3p_in_k2" 1 | 0
   *   "k2_sorted" 1 a time-ordered log (checked at upload): K2 reads the widest window's suffix only | 0 never
+  *   "k2_slide" 0 recount every refresh | 1 keep dense window counts and move them by the bindings between
+  *     the last refresh's window starts and this one's (time-ordered log; slower at large shifts)
   *   "k1_stream" 1 the streamed step pass without dedupe-form K2 entries | 0 the record-holding fused pass
   *   "k1_tail" 0 its tail on one wave when the grid has >= 4096 blocks | 1 always | 4 on all four waves
   *   "keys_path" 0 step path | 1 per-pair kernel   "greedy_form" 0 merge | 1 sequential

@@ -216,6 +216,42 @@ def test_step_keys_async_matches_oracle(ride, pods):
     assert all(0 < t < 50 for _, t in times), times
 
 
+@pytest.mark.parametrize("W,n_nodes,n_bind", [(2, 20000, 300_000), (3, 5000, 100_000)])
+def test_step_sliding_windows(W, n_nodes, n_bind):
+    """Option k2_slide: the dense window counts moved between refreshes (batches advancing,
+    retreating, jumping past half the log, repeated) equal the oracle's hot values at each
+    `now`, through the whole step; the first refresh and the big jump recount (large form)."""
+    import torch
+    spec = cd.default_policy_spec()
+    if W == 3:
+        spec = dict(spec, hotValue=list(spec["hotValue"]) + [(120_000_000_000, 3)])
+    c = synth.make_cluster(spec, n_nodes, 2000, n_bindings=n_bind, seed=31 + W, pod_step_ns=2_000_000, ds_frac=0.02)
+    eng = engine_for(spec, c, opts={"k2_slide": 1})
+    eng.upload_bindings(c.b_node, c.b_ts)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
+    t0 = int(synth.NOW0_NS)
+    names = []
+    with torch.cuda.stream(st):
+        for i, dt_s in enumerate((0, 10, 20, 5, 5, 400, 410, -30, 0)):
+            now = t0 + dt_s * 10**9
+            pods_now = c.now + dt_s * 10**9
+            d_now = torch.from_numpy(pods_now).to(dev)
+            eng.set_profiling(True)
+            eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
+            st.synchronize()
+            names.append([n for n, _ in eng.stage_times()][0])
+            ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
+            c.now, saved = pods_now, c.now  # (the oracle's pods at this batch's times)
+            _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=_oracle_hv(spec, c, now))
+            c.now = saved
+            assert np.array_equal(ch, och), (i, dt_s)
+    assert any(n.startswith("k2s_slide") for n in names), names
+    assert any(n.startswith("k2l_partition") for n in names), names
+
+
 @pytest.mark.parametrize("k2", [0, 1, 2, 3], ids=["dedupe", "binned", "hash", "large"])
 def test_step_keys_async_k2_forms(k2):
     """The combined step with each K2 form (dedupe: counts consumed by the fused node
