@@ -3,6 +3,9 @@
 // the time since the last GPU work?  Prints one line per gap: the update's wall time (three
 // updates per gap, each after the gap).  Usage: update_gap_probe <policy.yaml>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -13,6 +16,21 @@
 
 int main(int argc, char** argv) {
     if (argc < 2) return 2;
+    // a host thread started before the engine exists (a framework goroutine's thread), used at
+    // the end: its first update
+    std::mutex pm;
+    std::condition_variable pcv;
+    int ptask = 0;  // 1: run the update, 2: done
+    std::function<double(int64_t)> pupdate;
+    double pfirst = 0, psecond = 0;
+    std::thread pre([&] {
+        std::unique_lock<std::mutex> l(pm);
+        pcv.wait(l, [&] { return ptask == 1; });
+        pfirst = pupdate(40);
+        psecond = pupdate(41);
+        ptask = 2;
+        pcv.notify_all();
+    });
     crane_policy_doc* doc = nullptr;
     char err[512];
     if (crane_policy_load_file(argv[1], &doc, err, sizeof err)) {
@@ -118,6 +136,15 @@ int main(int argc, char** argv) {
         std::printf("new thread %d: first %.3f ms, second %.3f ms\n", t, first, second);
         std::fflush(stdout);
     }
+    pupdate = update;
+    {
+        std::unique_lock<std::mutex> l(pm);
+        ptask = 1;
+        pcv.notify_all();
+        pcv.wait(l, [&] { return ptask == 2; });
+    }
+    pre.join();
+    std::printf("thread started before the engine: first %.3f ms, second %.3f ms\n", pfirst, psecond);
     crane_dyn_destroy(h);
     crane_policy_free(doc);
     return 0;
