@@ -116,6 +116,12 @@ def _load():
         "crane_dyn_group_step_keys_async": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp]),
         "crane_dyn_group_sync": (C.c_int, [vp]),
         "crane_dyn_group_schedule": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp, vp]),
+        "crane_queue_create": (C.c_int, [C.c_int32, C.c_int32, P(vp)]),
+        "crane_queue_wait": (C.c_int, [vp]),
+        "crane_queue_last_error": (C.c_char_p, [vp]),
+        "crane_queue_destroy": (C.c_int, [vp]),
+        "crane_dyn_step_keys_queue": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp, vp]),
+        "crane_dyn_forget_queue": (C.c_int, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -144,6 +150,8 @@ ABI_SYMBOLS = (
     "crane_dyn_group_last_error", "crane_dyn_group_set_option", "crane_dyn_group_size", "crane_dyn_group_shard",
     "crane_dyn_group_engine", "crane_dyn_group_upload_nodes", "crane_dyn_group_upload_bindings",
     "crane_dyn_group_step_keys_async", "crane_dyn_group_sync", "crane_dyn_group_schedule",
+    "crane_queue_create", "crane_queue_wait", "crane_queue_last_error", "crane_queue_destroy",
+    "crane_dyn_step_keys_queue", "crane_dyn_forget_queue",
 )
 
 
@@ -538,6 +546,15 @@ class Engine:
                                                   None if d_flags is None else C.c_void_p(d_flags.data_ptr()),
                                                   C.c_void_p(d_keys.data_ptr()), stream))
 
+    def step_keys_queue(self, now_ns, hv_ts_ns, d_now, d_flags, d_keys, queue):
+        """step_keys_async with the kernels on a dispatch queue (Queue): the inputs must be complete
+        on the device (torch.cuda.synchronize() after writing them); keys after queue.wait()."""
+        P = d_now.numel()
+        assert d_keys.numel() == P and d_now.dtype.itemsize == 8 and d_keys.dtype.itemsize == 8
+        self._check(lib.crane_dyn_step_keys_queue(self.h, int(now_ns), int(hv_ts_ns), P, C.c_void_p(d_now.data_ptr()),
+                                                  None if d_flags is None else C.c_void_p(d_flags.data_ptr()),
+                                                  C.c_void_p(d_keys.data_ptr()), queue.h))
+
     def step_keys_fn(self, d_now, d_flags, d_keys, stream=None):
         """step_keys_async bound to fixed device buffers and stream: returns f(now_ns, hv_ts_ns).
         The pointer conversions happen once, so a loop of steps pays only the C call."""
@@ -651,6 +668,33 @@ class _BorrowedEngine(Engine):
 
     def close(self):
         self.h = C.c_void_p()
+
+
+class Queue:
+    """A dispatch queue (crane_queue_*): a user-mode AQL queue on one device that an engine's step
+    kernels are written to as packets (Engine.step_keys_queue).  ring_kind 0: kernel arguments in
+    device memory, 1: in pinned host memory."""
+
+    def __init__(self, device=0, ring_kind=0):
+        h = C.c_void_p()
+        rc = lib.crane_queue_create(int(device), int(ring_kind), C.byref(h))
+        self.h = h
+        if rc:
+            msg = lib.crane_queue_last_error(h).decode() if h.value else ""
+            self.close()
+            raise CraneError(rc, msg)
+
+    def wait(self):
+        if lib.crane_queue_wait(self.h):
+            raise CraneError(-2, lib.crane_queue_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value and lib is not None:
+            lib.crane_queue_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        self.close()
 
 
 class Group:

@@ -1,0 +1,47 @@
+// aql.hpp — the engine's kernels dispatched as AQL packets on a user-mode HSA queue
+// (crane_queue_*, crane_dyn_step_keys_queue in include/crane_dyn.h).
+//
+// A HIP launch costs the enqueuing thread 2.6-3.7 us on this image (the runtime's command
+// objects, locks and argument handling; profiles/r05/kernarg_probe.txt), so a config-3 batch
+// (three kernels) costs ~9-11 us of host time against ~11 us of GPU time per batch with four in
+// flight: the step is host-bound.  Writing the packet ourselves costs ~0.3 us
+// (profiles/r05/aql_probe.txt).  While a queue is installed on the calling thread (tl_aql),
+// klaunch (kernels.hpp) packs the kernel's arguments by the AMDGPU kernarg rules (each by-value
+// argument at its natural alignment, then the code-object-v5 implicit arguments the kernel
+// reads: block counts, group sizes, grid dimensions, dynamic LDS size) into the queue's
+// kernarg ring and writes a kernel-dispatch packet.  Every packet has the barrier bit (a
+// queue is in order, like a stream); a step's packets become visible to the packet processor
+// together (aql_commit: headers in order, one doorbell), the last one carrying the queue's
+// completion signal, which counts the committed steps still running.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstring>
+
+struct crane_queue;
+
+namespace crane {
+
+constexpr size_t kAqlMaxArgs = 3072;  // explicit argument bytes (K1's are ~1.3 KiB)
+
+// the queue this thread's klaunch calls go to (set for one step on a queue), else HIP
+extern thread_local crane_queue* tl_aql;
+
+hipError_t aql_launch(crane_queue* q, const void* host_fn, dim3 grid, dim3 block, uint32_t dyn_lds,
+                      const unsigned char* args, size_t explicit_bytes);
+// make the packets written since the last commit visible, the last one counted on the
+// queue's completion signal
+hipError_t aql_commit(crane_queue* q);
+// commit, then wait until every committed packet has completed
+hipError_t aql_wait(crane_queue* q);
+const char* aql_error(const crane_queue* q);
+
+template <typename T>
+inline void aql_pack(unsigned char* buf, size_t& off, const T& v) {
+    off = (off + alignof(T) - 1) & ~(alignof(T) - 1);
+    std::memcpy(buf + off, &v, sizeof(T));
+    off += sizeof(T);
+}
+
+}  // namespace crane

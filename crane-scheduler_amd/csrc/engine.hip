@@ -29,6 +29,11 @@ using namespace crane;
 
 namespace {
 
+// A buffer replaced during a step on a dispatch queue (a first batch sizing its scratch) may
+// still be read by the packets this thread put on that queue: wait for them first (hipFree
+// waits for HIP's own queues only)
+hipError_t before_free() { return crane::tl_aql ? crane::aql_wait(crane::tl_aql) : hipSuccess; }
+
 template <typename T>
 struct DevBuf {
     T* p = nullptr;
@@ -36,6 +41,7 @@ struct DevBuf {
     hipError_t reserve(size_t want) {
         if (want <= n && p) return hipSuccess;
         if (p) {
+            if (hipError_t e = before_free()) return e;
             hipError_t e = hipFree(p);
             p = nullptr;
             n = 0;
@@ -67,6 +73,7 @@ struct HostBuf {
     hipError_t reserve(size_t want) {
         if (want <= n && p) return hipSuccess;
         if (p) {
+            if (hipError_t e = before_free()) return e;
             hipError_t e = hipHostFree(p);
             p = nullptr;
             n = 0;
@@ -232,6 +239,7 @@ struct crane_dyn {
     // them — those streams only, not the device (another engine's batches and collectives
     // keep running).  A handle is kept only until that wait.
     std::vector<hipStream_t> busy;
+    std::vector<crane_queue*> busy_q;  // the same for dispatch queues (crane_dyn_step_keys_queue)
     DevBuf<unsigned char> upd_dev;   // crane_dyn_update_nodes / _node_steps_subset staging
     HostBuf<unsigned char> upd_host;
     // kernel timing (crane_dyn_set_profiling)
@@ -506,7 +514,15 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     }
     h->buckets_dense = false;
     h->slide_valid = false;
-    if (!h->buckets_zero) HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
+    if (!h->buckets_zero && tl_aql) {
+        // (on a dispatch queue: a fill is no kernel here — after the queue's packets, on the engine
+        // stream, waited for)
+        HIPTRY(h, aql_wait(tl_aql));
+        HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), h->stream));
+        HIPTRY(h, hipStreamSynchronize(h->stream));
+    } else if (!h->buckets_zero) {
+        HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
+    }
     const HotBins g = hot_bins_geometry(h->B, h->N, dp.n_win);
     if (g.ok && h->opt.k2_form != 2) {
         HIPTRY(h, h->k2_cnt.reserve((size_t)g.nbins * (size_t)g.nchunks));
@@ -743,6 +759,12 @@ static int mark_busy(crane_dyn* h, hipStream_t st) {
 // engines' batches and collectives in flight are not drained.  State changes are per
 // snapshot sync / controller tick, not per batch.
 static int quiesce(crane_dyn* h) {
+    if (!h->busy_q.empty()) {
+        std::vector<crane_queue*> qs;
+        qs.swap(h->busy_q);
+        for (crane_queue* q : qs)
+            if (aql_wait(q) != hipSuccess) return h->fail(CRANE_E_HIP, std::string("queue: ") + aql_error(q));
+    }
     if (h->busy.empty()) return CRANE_OK;
     // the list is cleared even when a wait fails (a stream the caller destroyed without
     // crane_dyn_forget_stream): the error is reported once, not by every later state change
@@ -800,6 +822,7 @@ int crane_dyn_destroy(crane_dyn* h) {
         (void)hipDeviceSynchronize();
     }
     h->busy.clear();
+    h->busy_q.clear();  // (not waited for: the caller waits for or destroys its queues first)
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->ev.clear();
     h->val.release(); h->hv.release(); h->ts.release(); h->hv_ts.release(); h->rec.release();
@@ -830,6 +853,16 @@ int crane_dyn_forget_stream(crane_dyn* h, void* stream) {
     h->busy.erase(it);
     HIPTRY(h, hipSetDevice(h->device));
     HIPTRY(h, hipStreamSynchronize((hipStream_t)stream));
+    return CRANE_OK;
+}
+
+int crane_dyn_forget_queue(crane_dyn* h, crane_queue* q) {
+    if (!h) return CRANE_E_INVALID;
+    std::lock_guard<std::mutex> g(h->mu);
+    auto it = std::find(h->busy_q.begin(), h->busy_q.end(), q);
+    if (it == h->busy_q.end()) return CRANE_OK;
+    h->busy_q.erase(it);
+    if (aql_wait(q) != hipSuccess) return h->fail(CRANE_E_HIP, std::string("queue: ") + aql_error(q));
     return CRANE_OK;
 }
 
@@ -1206,6 +1239,9 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
     if (P < 0 || (P > 0 && (!d_now || !d_keys))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
     HIPTRY(h, hipSetDevice(h->device));
+    if (!h->busy_q.empty()) {  // (steps on dispatch queues before: they are not ordered with streams)
+        if (int rc = quiesce(h)) return rc;
+    }
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     long long* keys = reinterpret_cast<long long*>(d_keys);
     if (!step_path_ok(h, P) || P == 0) {
@@ -1225,6 +1261,51 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
     if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, st);
     if (!rc) rc = step_rest(h, sp, P, keys, st);
     return rc ? rc : mark_busy(h, st);
+}
+
+int crane_dyn_step_keys_queue(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, int64_t P, const int64_t* d_now,
+                              const uint8_t* d_flags, int64_t* d_keys, crane_queue* q) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);
+    if (!q) return h->fail(CRANE_E_INVALID, "null queue");
+    if (P < 0 || (P > 0 && (!d_now || !d_keys))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
+    if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
+    HIPTRY(h, hipSetDevice(h->device));
+    // a queue is ordered with nothing else: this engine's work on HIP streams or other queues first
+    if (!h->busy.empty() || h->busy_q.size() > 1 || (h->busy_q.size() == 1 && h->busy_q[0] != q)) {
+        if (int rc = quiesce(h)) return rc;
+    }
+    long long* keys = reinterpret_cast<long long*>(d_keys);
+    if (!step_path_ok(h, P) || P == 0) {
+        // (the per-pair form has fills and copies: on the engine stream after the queue, waited for)
+        if (aql_wait(q) != hipSuccess) return h->fail(CRANE_E_HIP, std::string("queue: ") + aql_error(q));
+        int rc = hot_values_locked(h, now_ns, hv_ts_ns, h->stream);
+        if (!rc) rc = keys_locked(h, P, d_now, d_flags, keys, h->stream);
+        if (!rc) HIPTRY(h, hipStreamSynchronize(h->stream));
+        return rc;
+    }
+    struct OnQueue {  // this thread's launches go to q until the step is written
+        explicit OnQueue(crane_queue* x) { tl_aql = x; }
+        ~OnQueue() { tl_aql = nullptr; }
+    };
+    int rc;
+    {
+        OnQueue on(q);
+        h->rec_dirty = true;
+        StepPlan sp{};
+        rc = step_plan(h, P, sp);
+        const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys, h->sbatch.p};
+        bool pods_done = false;
+        if (!rc) rc = hot_values_locked(h, now_ns, hv_ts_ns, h->stream, h->opt.k3p_in_k2 ? &pp : nullptr, &pods_done);
+        if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, h->stream);
+        if (!rc) rc = step_rest(h, sp, P, keys, h->stream);
+    }
+    // (what was written runs even after an error: the packets before it are whole)
+    const hipError_t ce = aql_commit(q);
+    if (std::find(h->busy_q.begin(), h->busy_q.end(), q) == h->busy_q.end()) h->busy_q.push_back(q);
+    if (rc) return rc;
+    if (ce != hipSuccess) return h->fail(CRANE_E_HIP, std::string("queue: ") + aql_error(q));
+    return CRANE_OK;
 }
 
 // Host-pointer evaluation: the matrices go through device scratch in pod slices of

@@ -64,6 +64,11 @@ struct crane_dyn_group {
     int64_t N = -1;
     int collective = 1;  // 0: never (a host max combines), 1: when n > 1, 2: always (tests at n = 1)
     int threads = -1;    // -1: worker threads when n > 1, 0: the caller's thread, 1: worker threads
+    // 0: the steps' kernels on the slots' HIP streams; 1: on user-mode AQL queues (crane_queue, one
+    // per slot and device, created on first use; no collective); -1: queues unless the collective
+    // runs.  ring_kind of their kernargs
+    int dispatch = -1, ring_kind = 0;
+    std::vector<std::vector<crane_queue*>> q;  // [slot][device index]
     bool comm_broken = false;
     uint64_t batch = 0;
     uint64_t synced = 0;  // batch at the last wait_all: the slots used since are the ones to wait for
@@ -88,6 +93,8 @@ struct crane_dyn_group {
         return CRANE_E_HIP;
     }
     bool use_coll() const { return collective == 2 || (collective == 1 && n > 1); }
+    bool use_queues() const { return dispatch == 1 || (dispatch < 0 && !use_coll()); }
+    crane_queue* queue(int slot, int i) const { return use_queues() && !q.empty() ? q[(size_t)slot][(size_t)i] : nullptr; }
     bool use_workers() const { return threads == 1 || (threads < 0 && n > 1); }
 };
 
@@ -120,11 +127,14 @@ struct GroupWorker {
     void run_job(const Job& j) {
         crane_dyn* e = g->eng[j.slot][i];
         hipStream_t s = g->st[j.slot][i];
+        crane_queue* qq = g->queue(j.slot, i);
         if (g->hi[i] > g->lo[i]) {
-            if (crane_dyn_step_keys_async(e, j.now, j.hv_ts, j.P, j.d_now, j.d_flags, j.d_keys, s))
+            if (qq ? crane_dyn_step_keys_queue(e, j.now, j.hv_ts, j.P, j.d_now, j.d_flags, j.d_keys, qq)
+                   : crane_dyn_step_keys_async(e, j.now, j.hv_ts, j.P, j.d_now, j.d_flags, j.d_keys, s))
                 record(CRANE_E_HIP, std::string("device ") + std::to_string(g->dev[i]) + ": " + crane_dyn_last_error(e));
         } else if (j.P > 0) {  // an empty shard contributes "no node"
             hipError_t r = hipMemsetAsync(j.d_keys, 0xFF, sizeof(int64_t) * (size_t)j.P, s);
+            if (r == hipSuccess && qq) r = hipStreamSynchronize(s);  // (queues: wait_all waits for those only)
             if (r != hipSuccess) record(CRANE_E_HIP, hipGetErrorString(r));
         }
         if (g->use_coll() && j.P > 0) {
@@ -227,6 +237,10 @@ int wait_all(crane_dyn_group* g) {
     for (uint64_t b = g->batch - used; b < g->batch; ++b) {
         const size_t s = (size_t)(b % (uint64_t)g->depth);
         for (int i = 0; i < g->n; ++i) {
+            if (crane_queue* qq = g->queue((int)s, i)) {
+                if (crane_queue_wait(qq) && !rc) rc = g->fail(CRANE_E_HIP, std::string("queue: ") + crane_queue_last_error(qq));
+                continue;
+            }
             hipError_t e = hipSetDevice(g->dev[(size_t)i]);
             if (e == hipSuccess) e = hipStreamSynchronize(g->st[s][(size_t)i]);
             if (e != hipSuccess && !rc) rc = g->hipfail(e, "hipStreamSynchronize");
@@ -271,13 +285,16 @@ int step_here(crane_dyn_group* g, const Job& j, const int64_t* const* d_now, con
     for (int i = 0; i < g->n; ++i) {
         crane_dyn* e = g->eng[(size_t)j.slot][(size_t)i];
         hipStream_t s = g->st[(size_t)j.slot][(size_t)i];
+        crane_queue* qq = g->queue(j.slot, i);
         if (g->hi[(size_t)i] > g->lo[(size_t)i]) {
-            int rc = crane_dyn_step_keys_async(e, j.now, j.hv_ts, j.P, d_now[i], d_flags ? d_flags[i] : nullptr,
-                                               d_keys[i], s);
+            const uint8_t* fl = d_flags ? d_flags[i] : nullptr;
+            int rc = qq ? crane_dyn_step_keys_queue(e, j.now, j.hv_ts, j.P, d_now[i], fl, d_keys[i], qq)
+                        : crane_dyn_step_keys_async(e, j.now, j.hv_ts, j.P, d_now[i], fl, d_keys[i], s);
             if (rc) return engine_err(g, e, rc, i);
         } else if (j.P > 0) {
             hipError_t r = hipSetDevice(g->dev[(size_t)i]);
             if (r == hipSuccess) r = hipMemsetAsync(d_keys[i], 0xFF, sizeof(int64_t) * (size_t)j.P, s);
+            if (r == hipSuccess && qq) r = hipStreamSynchronize(s);
             if (r != hipSuccess) return g->hipfail(r, "hipMemsetAsync");
         }
     }
@@ -296,6 +313,38 @@ int step_here(crane_dyn_group* g, const Job& j, const int64_t* const* d_now, con
 int check_ready(crane_dyn_group* g) {
     if (g->n <= 0) return g->fail(CRANE_E_STATE, "group was not created successfully");
     if (g->N < 0) return g->fail(CRANE_E_STATE, "upload nodes before scheduling");
+    return 0;
+}
+
+// (after wait_all) the dispatch queues, waited for; the engines forget them first
+void free_queues(crane_dyn_group* g) {
+    for (size_t s = 0; s < g->q.size(); ++s)
+        for (size_t i = 0; i < g->q[s].size(); ++i)
+            if (crane_queue*& qq = g->q[s][i]) {
+                if (g->eng[s][i]) (void)crane_dyn_forget_queue(g->eng[s][i], qq);
+                (void)crane_queue_destroy(qq);
+                qq = nullptr;
+            }
+    g->q.clear();
+}
+
+// dispatch 1: one queue per slot and device, on first use
+int ensure_queues(crane_dyn_group* g) {
+    if (!g->use_queues() || !g->q.empty()) return 0;
+    if (g->use_coll())
+        return g->fail(CRANE_E_STATE, "dispatch 1 (queues) has no collective: set \"collective\" 0 or \"dispatch\" 0");
+    g->q.assign((size_t)g->depth, std::vector<crane_queue*>((size_t)g->n, nullptr));
+    for (int s = 0; s < g->depth; ++s)
+        for (int i = 0; i < g->n; ++i) {
+            crane_queue* qq = nullptr;
+            if (crane_queue_create(g->dev[(size_t)i], g->ring_kind, &qq)) {
+                const std::string m = std::string("crane_queue_create: ") + crane_queue_last_error(qq);
+                (void)crane_queue_destroy(qq);
+                free_queues(g);
+                return g->fail(CRANE_E_HIP, m);
+            }
+            g->q[(size_t)s][(size_t)i] = qq;
+        }
     return 0;
 }
 
@@ -364,6 +413,7 @@ int crane_dyn_group_destroy(crane_dyn_group* g) {
     {
         std::lock_guard<std::mutex> l(g->mu);
         stop_workers(g);
+        free_queues(g);  // (each waited for, and handed back by its engine, before the engines go)
         for (size_t i = 0; i < g->dev.size(); ++i) {
             if (hipSetDevice(g->dev[i]) == hipSuccess) (void)hipDeviceSynchronize();
         }
@@ -411,9 +461,18 @@ int crane_dyn_group_set_option(crane_dyn_group* g, const char* name, int64_t val
     GLock lk(g);
     if (g->n <= 0) return g->fail(CRANE_E_STATE, "group was not created successfully");
     const std::string nm = name;
+    if (nm == "dispatch" || nm == "dispatch_ring") {
+        if (value < (nm == "dispatch" ? -1 : 0) || value > 1)
+            return g->fail(CRANE_E_INVALID, nm + (nm == "dispatch" ? ": -1 | 0 | 1" : ": 0 | 1"));
+        if (int rc = wait_all(g)) return rc;
+        free_queues(g);  // (the engines wait for the queues they used at their next state change: none now)
+        (nm == "dispatch" ? g->dispatch : g->ring_kind) = (int)value;
+        return CRANE_OK;
+    }
     if (nm == "collective" || nm == "threads") {
         if (int rc = wait_all(g)) return rc;
         if (nm == "collective") {
+            free_queues(g);  // (dispatch -1 follows the collective)
             if (value < 0 || value > 2) return g->fail(CRANE_E_INVALID, "collective: 0 | 1 | 2");
             g->collective = (int)value;
         } else {
@@ -502,6 +561,7 @@ int crane_dyn_group_step_keys_async(crane_dyn_group* g, int64_t now_ns, int64_t 
     for (int i = 0; i < g->n && n_pods > 0; ++i)
         if (!d_now[i] || !d_keys[i]) return g->fail(CRANE_E_INVALID, "NULL device pointer");
     if (int rc = ensure_comms(g)) return rc;
+    if (int rc = ensure_queues(g)) return rc;
     const int slot = (int)(g->batch++ % (uint64_t)g->depth);
     Job j{now_ns, hv_ts_ns, n_pods, nullptr, nullptr, nullptr, slot};
     if (g->use_workers()) {
@@ -532,6 +592,7 @@ int crane_dyn_group_schedule(crane_dyn_group* g, int64_t now_ns, int64_t hv_ts_n
     if (n_pods == 0) return CRANE_OK;
     if (int rc = wait_all(g)) return rc;
     if (int rc = ensure_comms(g)) return rc;
+    if (int rc = ensure_queues(g)) return rc;
     const size_t P = (size_t)n_pods;
     if (P > g->b_cap) {
         for (int i = 0; i < g->n; ++i) {
@@ -567,6 +628,7 @@ int crane_dyn_group_schedule(crane_dyn_group* g, int64_t now_ns, int64_t hv_ts_n
         if (e == hipSuccess)
             e = pod_flags ? hipMemcpyAsync(g->b_flags[(size_t)i], pod_flags, P, hipMemcpyHostToDevice, s)
                           : hipMemsetAsync(g->b_flags[(size_t)i], 0, P, s);
+        if (e == hipSuccess && g->queue(0, i)) e = hipStreamSynchronize(s);  // (a queue orders with nothing)
         if (e != hipSuccess) return g->hipfail(e, "pod upload");
     }
     Job j{now_ns, hv_ts_ns, n_pods, nullptr, nullptr, nullptr, 0};
@@ -580,6 +642,8 @@ int crane_dyn_group_schedule(crane_dyn_group* g, int64_t now_ns, int64_t hv_ts_n
     const int nk = g->use_coll() ? 1 : g->n;
     for (int i = 0; i < nk; ++i) {
         hipStream_t s = g->st[0][(size_t)i];
+        if (crane_queue* qq = g->queue(0, i))
+            if (crane_queue_wait(qq)) return g->fail(CRANE_E_HIP, std::string("queue: ") + crane_queue_last_error(qq));
         hipError_t e = hipSetDevice(g->dev[(size_t)i]);
         if (e == hipSuccess)
             e = hipMemcpyAsync(g->h_keys + (size_t)i * P, g->b_keys[(size_t)i], sizeof(int64_t) * P,

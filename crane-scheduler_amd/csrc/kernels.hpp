@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "aql.hpp"
 #include "dyn_types.hpp"
 
 namespace crane {
@@ -22,9 +23,18 @@ struct KernelTimer {
 };
 extern thread_local KernelTimer* tl_ktimer;
 
+// On a thread with an AQL queue installed (aql.hpp: a step on a crane_queue) the launch is a
+// packet on that queue instead (no timing events there).
 template <typename... KArgs, typename... Args>
 inline hipError_t klaunch(const char* name, void (*kernel)(KArgs...), dim3 grid, dim3 block, size_t lds,
                           hipStream_t st, Args... args) {
+    if (tl_aql) {
+        static_assert((sizeof(KArgs) + ... + 0) + 16 * sizeof...(KArgs) <= kAqlMaxArgs, "kernel arguments too large");
+        alignas(16) unsigned char buf[kAqlMaxArgs];
+        size_t off = 0;
+        (aql_pack<KArgs>(buf, off, static_cast<KArgs>(args)), ...);
+        return aql_launch(tl_aql, reinterpret_cast<const void*>(kernel), grid, block, (uint32_t)lds, buf, off);
+    }
     hipEvent_t a = nullptr, b = nullptr;
     if (tl_ktimer) tl_ktimer->next(name, &a, &b);
     hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, st, a, b, 0u, static_cast<KArgs>(args)...);

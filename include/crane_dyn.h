@@ -289,6 +289,29 @@ int crane_dyn_eval_keys_async(crane_dyn *h, int64_t n_pods, const int64_t *d_now
  * evaluation of the pod batch (as crane_dyn_eval_keys_async). */
 int crane_dyn_step_keys_async(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns, int64_t n_pods,
                               const int64_t *d_now_ns, const uint8_t *d_pod_flags, int64_t *d_keys, void *stream);
+/* Dispatch queues: a user-mode AQL queue on one device (HSA, the layer under HIP) to which the
+ * step's kernels are written as packets by the calling thread — ~0.3 us per kernel instead of
+ * HIP's 2.6-3.7 us per launch, which made a batch's three launches cost the host about the GPU's
+ * time per batch.  A queue is in order (like a stream); it is not a HIP stream: work
+ * on it is ordered with HIP work only through crane_queue_wait (the engine does this itself
+ * around its own synchronous calls).  ring_kind 0 puts the kernel arguments in device memory
+ * the host writes through the PCIe BAR (default), 1 in pinned host memory.  The handle is
+ * returned on failure too (read its error, then destroy it). */
+typedef struct crane_queue crane_queue;
+int crane_queue_create(int32_t device, int32_t ring_kind, crane_queue **out);
+/* Wait until every step enqueued on the queue has completed. */
+int crane_queue_wait(crane_queue *q);
+const char *crane_queue_last_error(const crane_queue *q);
+/* Waits for the queue, then frees it. */
+int crane_queue_destroy(crane_queue *q);
+/* crane_dyn_step_keys_async with the step's kernels on `q`: d_now / d_flags must be complete on
+ * the device when called (written by finished work); d_keys is complete after crane_queue_wait.
+ * The engine's own state changes wait for the queues it used: a queue must outlive the engine's
+ * next state change, or be handed back first with crane_dyn_forget_queue. */
+int crane_dyn_step_keys_queue(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns, int64_t n_pods,
+                              const int64_t *d_now_ns, const uint8_t *d_pod_flags, int64_t *d_keys, crane_queue *q);
+/* Hand a queue back (waits for it): the engine no longer waits for it at its state changes. */
+int crane_dyn_forget_queue(crane_dyn *h, crane_queue *q);
 /* Asynchronous pieces of one scheduling step on `stream`:
  * hot values from bindings (K2) and the node pass (K1). */
 int crane_dyn_refresh_hot_values_async(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns, void *stream);
@@ -351,7 +374,11 @@ int64_t crane_dyn_debug_trace(crane_dyn *h, int32_t which, int64_t max, uint64_t
  * Options (crane_dyn_group_set_option): "collective" 0 never (crane_dyn_group_schedule max-combines
  * on the host; the async form leaves per-shard keys) | 1 when n_dev > 1 (default) | 2 always (a
  * one-rank communicator: tests); "threads" -1 auto | 0 the caller's thread (the collective in
- * ncclGroupStart/End) | 1 worker threads; any other name goes to every engine. */
+ * ncclGroupStart/End) | 1 worker threads; "dispatch" -1 (default) dispatch queues unless the
+ * collective runs | 0 the steps' kernels launched through HIP on the slots' streams | 1 on dispatch
+ * queues (crane_queue, one per slot and device; no collective); "dispatch_ring" 0 | 1 their
+ * ring_kind; any other name goes to every engine.  Either way the batch's d_now / d_flags must be
+ * complete on the devices when it is handed over (the group's streams and queues are its own). */
 typedef struct crane_dyn_group crane_dyn_group;
 /* Contiguous balanced node range of shard `shard` of n_shards (the first n % n_shards get one more). */
 int crane_shard_range(int64_t n_nodes, int32_t n_shards, int32_t shard, int64_t *lo, int64_t *hi);

@@ -27,6 +27,8 @@ ap.add_argument("--inflight", default="1,2,3,4")
 ap.add_argument("--bound", action="store_true", help="pre-bound step functions (Engine.step_keys_fn)")
 ap.add_argument("--threads", action="store_true", help="one host thread per engine enqueues its batches")
 ap.add_argument("--opt", action="append", default=[], help="engine option name=value (repeatable)")
+ap.add_argument("--start-at", type=float, default=0.0,
+                help="time.time() at which the timed loop starts (several processes on one GPU timed together)")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 spec = cd.default_policy_spec()
@@ -66,7 +68,10 @@ for K in [int(x) for x in args.inflight.split(",")]:
     for i in range(10):
         step(i)
     torch.cuda.synchronize()
+    if args.start_at:
+        time.sleep(max(0.0, args.start_at - time.time()))
     t0 = time.perf_counter()
+    w0 = time.time()
     if args.threads:
         def run(j):
             f = fns[j]
@@ -85,7 +90,7 @@ for K in [int(x) for x in args.inflight.split(",")]:
     ms = (time.perf_counter() - t0) * 1e3 / args.steps
     same = all(torch.equal(keys[0], k) for k in keys)
     out[f"inflight{K}"] = {"ms_per_step": round(ms, 4), "host_enqueue_ms_per_step": round(t_host * 1e3 / args.steps, 4),
-                           "keys_equal": same}
+                           "keys_equal": same, "wall": [round(w0, 6), round(w0 + ms * args.steps / 1e3, 6)]}
     for e in engs:
         e.close()
 print(json.dumps(out))
