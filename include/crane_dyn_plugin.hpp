@@ -299,6 +299,8 @@ class DynamicScheduler {
 
     // host threads of the full-snapshot annotation parse (<= 0: all hardware threads)
     void SetParseThreads(int32_t n) { parse_threads_ = n; }
+    // an engine option (crane_dyn_set_option: alternative kernel forms, tests and A/B tools)
+    bool SetEngineOption(const char* name, int64_t value) { return crane_dyn_set_option(eng_, name, value) == 0; }
     // time span one answer table covers from the pod that builds it (a later pod gets a new
     // table); by default (and ns <= 0) the whole time axis, which never needs a new table
     void SetHorizon(int64_t ns) { horizon_ns_ = ns > 0 ? ns : kAllTime; }

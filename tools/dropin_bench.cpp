@@ -348,7 +348,7 @@ static std::vector<std::string> split_tab(const std::string& s) {
 int main(int argc, char** argv) {
     if (argc < 4) {
         std::fprintf(stderr, "usage: dropin_bench <policy> <snapshot.tsv> <pods.tsv> [--threads N] [--cpu] "
-                             "[--churn X] [--churn-log path] [--seed S]\n");
+                             "[--churn X] [--churn-log path] [--seed S] [--engine-opt name=value]\n");
         return 2;
     }
     int threads = 16;
@@ -357,6 +357,7 @@ int main(int argc, char** argv) {
     double churn_scale = 0.0;
     std::string churn_log;
     uint64_t seed = 1;
+    std::vector<std::string> engine_opts;  // name=value
     for (int a = 4; a < argc; ++a) {
         const std::string k = argv[a];
         auto next = [&]() -> std::string { return a + 1 < argc ? argv[++a] : ""; };
@@ -366,6 +367,7 @@ int main(int argc, char** argv) {
         else if (k == "--churn-log") churn_log = next();
         else if (k == "--seed") seed = std::strtoull(next().c_str(), nullptr, 10);
         else if (k == "--node-events") node_events = std::atoi(next().c_str());
+        else if (k == "--engine-opt") engine_opts.push_back(next());
         else {
             std::fprintf(stderr, "unknown argument %s\n", k.c_str());
             return 2;
@@ -429,6 +431,15 @@ int main(int argc, char** argv) {
     }
     DynamicScheduler& ds = *r.first;
     ds.SetParseThreads(threads);
+#ifndef DROPIN_CPU
+    for (const std::string& o : engine_opts) {
+        const size_t eq = o.find('=');
+        if (eq == std::string::npos || !ds.SetEngineOption(o.substr(0, eq).c_str(), std::atoll(o.c_str() + eq + 1))) {
+            std::fprintf(stderr, "bad --engine-opt %s\n", o.c_str());
+            return 2;
+        }
+    }
+#endif
     std::string err;
     double sync_ms = 0.0;
     if (!cpu) {  // the first full sync (parse + upload of the whole snapshot + table), before the pods
