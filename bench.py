@@ -1023,7 +1023,18 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
         for dv in devs:
             torch.cuda.synchronize(dv)
 
-    for i in range(args.warmup):
+    dispatch_note = None
+    try:
+        step(0)  # (the first batch makes the dispatch queues)
+    except cd.CraneError as e:
+        if args.group_dispatch >= 0:
+            raise
+        # auto: a box whose runtime refuses the queues keeps HIP launches, and the line says so
+        dispatch_note = f"dispatch queues unavailable ({e}); HIP launches on the slots' streams"
+        dispatch = 0
+        grp.set_option("dispatch", 0)
+        step(0)
+    for i in range(1, args.warmup):
         step(i)
     sync_all()
     cpu0 = task_cpu()
@@ -1082,7 +1093,7 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
                    "; the step's kernels launched through HIP on the slots' streams")),
              engine_path=("group (C ABI, in-library RCCL" + (", rehearsed on one device)" if n_dev == 1 else ")")
                           if coll else "group (C ABI, one device)") + (", dispatch queues" if dispatch else ""),
-             n_gpus=n_dev)
+             dispatch_note=dispatch_note, n_gpus=n_dev)
     m["close"] = lambda: grp.close()
     return m
 
@@ -1361,7 +1372,7 @@ def finish(cd, synth, spec, args, m, n_gpus, rank, solo, dev, shash):
                                     + ", README default policy"),
                        "nodes_total": n_total, "nodes_per_gpu": N, "pods": P, "bindings_gpu0": B,
                        "parallelism": f"node-shard x{n_gpus}",
-                       "engine": m["engine_path"],
+                       "engine": m["engine_path"] + (f" ({m['dispatch_note']})" if m.get("dispatch_note") else ""),
                        "batches_in_flight": m["K"],
                        "batch_times": (f"batch i at now0 + (i % {len(m['nows'])}) x {m['span'] / 1e9:g} s (its pods "
                                        "shifted alike): the hot-value cutoffs move every batch and K2's suffix "
