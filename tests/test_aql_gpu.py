@@ -165,3 +165,29 @@ def test_forget_queue_then_state_change():
     assert torch.equal(ka, kb)
     for e in engs:
         e.close()
+
+
+def test_queue_runs_ahead_past_its_ring():
+    """700 steps written to one queue with no wait between them (2,100 packets through a
+    1,024-packet ring and its kernarg slots: the writer waits for the packet processor to move on,
+    committing its partial step first), then one wait: the last batch's keys equal the stream's."""
+    import torch
+    _, c, engs, dev = _setup(2000, 300, 5000, 20250308)
+    t0 = int(synth.NOW0_NS)
+    q = cd.Queue(0)
+    d_now = torch.from_numpy(c.now).to(dev)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    torch.cuda.synchronize()
+    kq = torch.empty(len(c.now), dtype=torch.int64, device=dev)
+    times = [t0 + (k % 5) * 4_000_000_000 for k in range(700)]
+    for t in times:
+        engs[1].step_keys_queue(t, t, d_now, d_flags, kq, q)
+    q.wait()
+    st = torch.cuda.Stream(dev)
+    ks = torch.empty_like(kq)
+    engs[0].step_keys_async(times[-1], times[-1], d_now, d_flags, ks, st.cuda_stream)
+    st.synchronize()
+    assert torch.equal(kq, ks)
+    for e in engs:
+        e.close()
+    q.close()
