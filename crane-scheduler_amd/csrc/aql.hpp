@@ -1,11 +1,11 @@
 // aql.hpp — the engine's kernels dispatched as AQL packets on a user-mode HSA queue
 // (crane_queue_*, crane_dyn_step_keys_queue in include/crane_dyn.h).
 //
-// A HIP launch costs the enqueuing thread 2.6-3.7 us on this image (the runtime's command
-// objects, locks and argument handling; profiles/r05/kernarg_probe.txt), so a config-3 batch
-// (three kernels) costs ~9-11 us of host time against ~11 us of GPU time per batch with four in
-// flight: the step is host-bound.  Writing the packet ourselves costs ~0.3 us
-// (profiles/r05/aql_probe.txt).  While a queue is installed on the calling thread (tl_aql),
+// A HIP launch costs the enqueuing thread 2.1-5.2 us on this image, box to box (the runtime's
+// command objects, locks and argument handling; profiles/r05/kernarg_probe.txt), so a config-3
+// batch (three kernels) costs ~9-15 us of host time, about the GPU's ~11 us per batch with four
+// in flight.  Writing the packet ourselves costs 0.2-0.6 us (profiles/r05/aql_probe.txt): the
+// host stays under the GPU's rate on every box.  While a queue is installed on the calling thread (tl_aql),
 // klaunch (kernels.hpp) packs the kernel's arguments by the AMDGPU kernarg rules (each by-value
 // argument at its natural alignment, then the code-object-v5 implicit arguments the kernel
 // reads: block counts, group sizes, grid dimensions, dynamic LDS size) into the queue's

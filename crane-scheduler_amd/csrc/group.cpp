@@ -12,8 +12,10 @@
 // device, then an in-place ncclAllReduce(int64, ncclMax) of the per-pod keys on the same
 // stream: afterwards every device holds the global choice.
 //
-// Enqueueing: a step costs the host ~9 us of kernel launches per device, so one thread
-// feeding eight devices would leave them idle.  With more than one device each device has
+// Enqueueing: a step costs the host ~9 us of HIP kernel launches per device (~4 us on the
+// dispatch queues, aql.cpp, which the group uses unless the collective runs: RCCL's kernels are
+// on HIP streams, which a queue is not ordered with), so one thread feeding eight devices would
+// leave them idle.  With more than one device each device has
 // a worker thread (spinning briefly, then sleeping) that takes the batch descriptors the
 // caller pushes and enqueues its device's step and its part of the all-reduce on its own
 // communicator (RCCL's one-thread-per-device usage); the caller only pushes descriptors.
@@ -341,6 +343,10 @@ int ensure_queues(crane_dyn_group* g) {
                 const std::string m = std::string("crane_queue_create: ") + crane_queue_last_error(qq);
                 (void)crane_queue_destroy(qq);
                 free_queues(g);
+                if (g->dispatch < 0) {  // (auto: a runtime that refuses the queues keeps HIP launches)
+                    g->dispatch = 0;
+                    return 0;
+                }
                 return g->fail(CRANE_E_HIP, m);
             }
             g->q[(size_t)s][(size_t)i] = qq;
