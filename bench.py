@@ -791,6 +791,31 @@ def keys_virtual_shards(cd, spec, dev, c, d_now, d_flags, now_sync, ref_keys, S)
     return bool(torch.equal(comb, ref_keys))
 
 
+def oracle_sample(spec, g, names, pod_now, now, keys, n=64):
+    """The batch's keys against the CPU oracle (oracle/crane_oracle.c, a checker: after the timed
+    region) on an n-pod sample — evenly spread pods plus the first DaemonSet ones — with the hot
+    values the controller computes from the binding log at `now` (O.hot_values, binding.go:81-97)
+    stamped `now`, as the step stamps them: chosen node and score per sampled pod."""
+    from oracle import oracle as O
+    P = len(pod_now)
+    smp = np.unique(np.concatenate([np.linspace(0, P - 1, n - 8).astype(np.int64), np.flatnonzero(g.ds)[:8]]))
+    _, hv = O.hot_values(spec, g.b_node, g.b_ts, g.n_nodes, int(now) // 10**9)
+    val, ts, ok = g.rows(names)
+    ff, sc, och = O.eval_soa(spec, names, ok, val, np.where(ok == 1, ts, 0), np.ones(g.n_nodes, np.uint8),
+                             hv.astype(np.float64), np.full(g.n_nodes, int(now), np.int64), pod_now[smp], g.ds[smp],
+                             threads=16, want_matrix=g.n_nodes * len(smp) <= (1 << 24))
+    knode = np.where(keys[smp] < 0, -1, 0xFFFFFFFF - (keys[smp] & 0xFFFFFFFF))
+    kscore = np.where(keys[smp] < 0, -1, keys[smp] >> 32)
+    ok_node = bool(np.array_equal(knode, och))
+    ok_score = None
+    if sc is not None:
+        feas = (ff < 0) | (g.ds[smp][:, None] != 0)
+        best = np.where(feas.any(1), np.where(feas, sc, -1).max(1), -1)
+        ok_score = bool(np.array_equal(kscore, best))
+    return {"oracle_sample": ok_node and ok_score is not False, "oracle_pods": int(len(smp)),
+            "oracle_scores_checked": ok_score is not None}
+
+
 def k2_read(spec, b_ts, now_ns):
     """The bindings K2 reads, as the engine decides (engine option k2_sorted, default on): a
     log in time order is read from the first binding inside the widest window on, node ids
@@ -1012,10 +1037,12 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
     d_keys = [[torch.empty(P, dtype=torch.int64, device=dv) for dv in devs] for _ in range(K)]
     fns = [[grp.step_keys_fn(d_now[t], d_flags, d_keys[s]) for t in range(C)] for s in range(K)]
     seq = [0]  # batches enqueued on the group so far: batch b runs on slot b % K
+    slot_t = [None] * K  # the batch time (cycle position) of each slot's latest batch
 
     def step(i):
         t = i % C
         fns[seq[0] % K][t](nows[t], nows[t])
+        slot_t[seq[0] % K] = t
         seq[0] += 1
 
     def sync_all():
@@ -1051,6 +1078,16 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
     last = d_keys[s_last]
     keys = last[0].cpu().numpy()
     keys_agree = all(torch.equal(last[0].cpu(), k.cpu()) for k in last[1:]) if n_dev > 1 else None
+    # the timed path pinned at full size: the last timed batch and the one before it (another slot,
+    # another `now`: the cutoffs moved between them) against one engine over the whole cluster on a
+    # HIP stream and against the CPU oracle on a pod sample (checker only, after the timed region)
+    pinned = []
+    for s_ in sorted({s_last, (s_last - 1) % K}, key=lambda x: x != s_last):
+        t_ = slot_t[s_]
+        ref_k, _ = keys_one_engine(cd, synth, spec, devs[0], lambda: g_all, d_now[t_][0], d_flags[0], nows[t_])
+        got = d_keys[s_][0].cpu().numpy()
+        pinned.append({"slot": s_, "now_ns": int(nows[t_]), "stream": bool(np.array_equal(ref_k.cpu().numpy(), got)),
+                       **oracle_sample(spec, g_all, grp.metric_names, pods[t_], nows[t_], got)})
     keys_match, keys_match_how = None, "one device: no combine step"
     if n_dev > 1:
         ref_k, _ = keys_one_engine(cd, synth, spec, devs[0], lambda: g_all, d_now[t_last][0], d_flags[0], nows[t_last])
@@ -1081,7 +1118,7 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
     val, ts, _ = c.rows(grp.metric_names)
     m = dict(c=c, N=c.n_nodes, P=P, n_total=n_total, val=val, ts=ts, eng=eng, ms_step=elapsed * 1e3 / args.steps,
              keys=keys, keys_agree=keys_agree, keys_match=keys_match, keys_match_how=keys_match_how, host=host,
-             batch_latency_ms=batch_latency_ms, kt=kt, ar_ms=None, K=K, nows=nows, span=span, stream=st0,
+             pinned=pinned, batch_latency_ms=batch_latency_ms, kt=kt, ar_ms=None, K=K, nows=nows, span=span, stream=st0,
              how=(f"one process, crane_dyn_group over {n_dev} device(s) (C ABI, group.cpp): {K} batch slots, each "
                   "with an engine per device (own copy of its shard) on its own HIP stream, batch i on slot i % K; "
                   "every batch runs the whole shard step on every device" +
@@ -1386,6 +1423,14 @@ def finish(cd, synth, spec, args, m, n_gpus, rank, solo, dev, shash):
             "host": m["host"],
             "keys_match_1gpu": m["keys_match"],
             "keys_match_1gpu_how": m["keys_match_how"],
+            "keys_match_stream": (all(b["stream"] for b in m["pinned"]) if m.get("pinned") else None),
+            "keys_match_oracle_sample": (all(b["oracle_sample"] for b in m["pinned"]) if m.get("pinned") else None),
+            "keys_pinned": m.get("pinned") and {
+                "batches": m["pinned"],
+                "how": ("the last timed batch and the one before it (another slot and `now`), as the timed path left "
+                        "them: all keys == one engine over the whole cluster stepped on a HIP stream "
+                        "(crane_dyn_step_keys_async, same pods and now); a 64-pod sample's chosen node (and score, "
+                        "when the matrix fits) == the CPU oracle with the binding log's hot values at that now")},
             "roofline": roofline,
             "roofline_kernels": roofs,
             "roofline_cold": roofline_cold,

@@ -16,6 +16,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <vector>
 
 #include "../../include/crane_dyn.h"
 
@@ -137,6 +138,8 @@ struct crane_queue {
     uint64_t first = 0, next = 0;   // packets [first, next) written, not yet committed
     std::unordered_map<const void*, KInfo> kinfo;  // per host stub
     std::string err;
+    std::mutex umu;
+    std::vector<crane_dyn*> users;  // engines that put steps here (aql_add_user)
 
     hipError_t fail(hipError_t e, const std::string& m) {
         err = m;
@@ -146,7 +149,41 @@ struct crane_queue {
 
 namespace crane {
 
+// The queue's run-time check of the hand-packed implicit arguments (aql_launch): a kernel that
+// reads the grid and group dimensions HIP derives from them (hidden block counts and group sizes
+// of code object v5) and counts its workgroups.  A runtime whose layout differs fails the queue's
+// creation, and the group keeps HIP launches (its dispatch -1).
+__global__ void k_aql_selfcheck(uint32_t* out) {
+    if (threadIdx.x == 0 && threadIdx.y == 0 && threadIdx.z == 0) {
+        atomicAdd(&out[6], 1u);
+        if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+            out[0] = gridDim.x;
+            out[1] = gridDim.y;
+            out[2] = gridDim.z;
+            out[3] = blockDim.x;
+            out[4] = blockDim.y;
+            out[5] = blockDim.z;
+        }
+    }
+}
+
 const char* aql_error(const crane_queue* q) { return q ? q->err.c_str() : "null queue"; }
+
+void aql_add_user(crane_queue* q, crane_dyn* h) {
+    std::lock_guard<std::mutex> l(q->umu);
+    for (crane_dyn* u : q->users)
+        if (u == h) return;
+    q->users.push_back(h);
+}
+
+void aql_remove_user(crane_queue* q, crane_dyn* h) {
+    std::lock_guard<std::mutex> l(q->umu);
+    for (size_t i = 0; i < q->users.size(); ++i)
+        if (q->users[i] == h) {
+            q->users.erase(q->users.begin() + (long)i);
+            return;
+        }
+}
 
 static const KInfo* lookup(crane_queue* q, const void* fn) {
     auto it = q->kinfo.find(fn);
@@ -190,7 +227,13 @@ hipError_t aql_launch(crane_queue* q, const void* fn, dim3 grid, dim3 block, uin
             hipError_t e = aql_commit(q);  // (let the processor reach what this thread wrote)
             if (e != hipSuccess) return e;
         }
-        while (hsa_queue_load_read_index_scacquire(q->q) + kQueuePackets < i + 2) cpu_relax();
+        // (bounded like aql_wait: a faulted or hung kernel is reported, not waited for forever)
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spins = 0; hsa_queue_load_read_index_scacquire(q->q) + kQueuePackets < i + 2; ++spins) {
+            cpu_relax();
+            if ((spins & 4095) == 4095 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+                return q->fail(hipErrorLaunchTimeOut, "aql: the queue's packet ring did not drain within 60 s");
+        }
     }
     unsigned char* ka = q->ring + (i & (kQueuePackets - 1)) * kSlotBytes;
     // the explicit arguments, then the code-object-v5 implicit ones the kernel may read, at
@@ -284,6 +327,43 @@ hipError_t aql_wait(crane_queue* q) {
 
 using namespace crane;
 
+namespace {
+
+// one launch of k_aql_selfcheck on the new queue over a 3-D grid; its readings must be the
+// launch's own dimensions
+int aql_selfcheck(crane_queue* q) {
+    const dim3 grid(5, 3, 2), block(32, 2, 1);
+    uint32_t* d = nullptr;
+    uint32_t h[8] = {};
+    if (hipMalloc(reinterpret_cast<void**>(&d), sizeof h) != hipSuccess) {
+        q->err = "aql self-check: hipMalloc failed";
+        return CRANE_E_HIP;
+    }
+    hipError_t e = hipMemset(d, 0, sizeof h);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    unsigned char args[8];
+    size_t off = 0;
+    aql_pack(args, off, d);
+    if (e == hipSuccess) e = aql_launch(q, reinterpret_cast<const void*>(&k_aql_selfcheck), grid, block, 0, args, off);
+    if (e == hipSuccess) e = aql_wait(q);
+    if (e == hipSuccess) e = hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) {
+        if (q->err.empty()) q->err = std::string("aql self-check: ") + hipGetErrorString(e);
+        return CRANE_E_HIP;
+    }
+    const uint32_t want[7] = {grid.x, grid.y, grid.z, block.x, block.y, block.z, grid.x * grid.y * grid.z};
+    for (int i = 0; i < 7; ++i)
+        if (h[i] != want[i]) {
+            q->err = "aql self-check: implicit-argument layout differs from this runtime's (field " + std::to_string(i) +
+                     ": " + std::to_string(h[i]) + ", want " + std::to_string(want[i]) + ")";
+            return CRANE_E_HIP;
+        }
+    return CRANE_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int crane_queue_create(int32_t device, int32_t ring_kind, crane_queue** out) {
@@ -357,7 +437,7 @@ int crane_queue_create(int32_t device, int32_t ring_kind, crane_queue** out) {
         return CRANE_E_HIP;
     }
     std::memset(q->ring, 0, bytes);
-    return CRANE_OK;
+    return aql_selfcheck(q);
 }
 
 int crane_queue_wait(crane_queue* q) {
@@ -370,6 +450,13 @@ const char* crane_queue_last_error(const crane_queue* q) { return aql_error(q); 
 int crane_queue_destroy(crane_queue* q) {
     if (!q) return CRANE_OK;
     if (q->q && q->sig.handle) (void)aql_wait(q);
+    // the engines that used the queue forget it (their next state change would wait on it)
+    std::vector<crane_dyn*> us;
+    {
+        std::lock_guard<std::mutex> l(q->umu);
+        us.swap(q->users);
+    }
+    for (crane_dyn* h : us) engine_drop_queue(h, q);
     if (q->q) hsa_queue_destroy(q->q);
     if (q->sig.handle) hsa_signal_destroy(q->sig);
     if (q->ring) {

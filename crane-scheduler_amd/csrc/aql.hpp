@@ -20,6 +20,7 @@
 #include <cstring>
 
 struct crane_queue;
+struct crane_dyn;
 
 namespace crane {
 
@@ -36,6 +37,13 @@ hipError_t aql_commit(crane_queue* q);
 // commit, then wait until every committed packet has completed
 hipError_t aql_wait(crane_queue* q);
 const char* aql_error(const crane_queue* q);
+// Engines that put steps on a queue register with it (crane_dyn_step_keys_queue), so whichever of
+// the two is destroyed first can tell the other: a queue's destroy hands itself back to every
+// registered engine (engine_drop_queue, engine.hip), an engine's destroy waits for the queues it
+// used and unregisters.
+void aql_add_user(crane_queue* q, crane_dyn* h);
+void aql_remove_user(crane_queue* q, crane_dyn* h);
+void engine_drop_queue(crane_dyn* h, crane_queue* q);
 
 template <typename T>
 inline void aql_pack(unsigned char* buf, size_t& off, const T& v) {

@@ -240,6 +240,7 @@ struct crane_dyn {
     // keep running).  A handle is kept only until that wait.
     std::vector<hipStream_t> busy;
     std::vector<crane_queue*> busy_q;  // the same for dispatch queues (crane_dyn_step_keys_queue)
+    std::vector<crane_queue*> seen_q;  // every queue this engine is registered with (aql_add_user)
     DevBuf<unsigned char> upd_dev;   // crane_dyn_update_nodes / _node_steps_subset staging
     HostBuf<unsigned char> upd_host;
     // kernel timing (crane_dyn_set_profiling)
@@ -775,6 +776,13 @@ static int quiesce(crane_dyn* h) {
     return CRANE_OK;
 }
 
+// a queue being destroyed hands itself back (aql.cpp; it has waited for its steps)
+void crane::engine_drop_queue(crane_dyn* h, crane_queue* q) {
+    std::lock_guard<std::mutex> g(h->mu);
+    h->busy_q.erase(std::remove(h->busy_q.begin(), h->busy_q.end(), q), h->busy_q.end());
+    h->seen_q.erase(std::remove(h->seen_q.begin(), h->seen_q.end(), q), h->seen_q.end());
+}
+
 extern "C" {
 
 const char* crane_dyn_version(void) { return "crane_dyn 0.2 gfx950"; }
@@ -822,7 +830,15 @@ int crane_dyn_destroy(crane_dyn* h) {
         (void)hipDeviceSynchronize();
     }
     h->busy.clear();
-    h->busy_q.clear();  // (not waited for: the caller waits for or destroys its queues first)
+    // the queues still registered are alive (a destroyed queue unregisters itself,
+    // engine_drop_queue): wait for the ones with steps of this engine, then unregister
+    {
+        std::lock_guard<std::mutex> g(h->mu);
+        for (crane_queue* q : h->busy_q) (void)aql_wait(q);
+        for (crane_queue* q : h->seen_q) aql_remove_user(q, h);
+        h->busy_q.clear();
+        h->seen_q.clear();
+    }
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->ev.clear();
     h->val.release(); h->hv.release(); h->ts.release(); h->hv_ts.release(); h->rec.release();
@@ -859,6 +875,11 @@ int crane_dyn_forget_stream(crane_dyn* h, void* stream) {
 int crane_dyn_forget_queue(crane_dyn* h, crane_queue* q) {
     if (!h) return CRANE_E_INVALID;
     std::lock_guard<std::mutex> g(h->mu);
+    auto sq = std::find(h->seen_q.begin(), h->seen_q.end(), q);
+    if (sq != h->seen_q.end()) {
+        h->seen_q.erase(sq);
+        aql_remove_user(q, h);
+    }
     auto it = std::find(h->busy_q.begin(), h->busy_q.end(), q);
     if (it == h->busy_q.end()) return CRANE_OK;
     h->busy_q.erase(it);
@@ -1303,6 +1324,10 @@ int crane_dyn_step_keys_queue(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
     // (what was written runs even after an error: the packets before it are whole)
     const hipError_t ce = aql_commit(q);
     if (std::find(h->busy_q.begin(), h->busy_q.end(), q) == h->busy_q.end()) h->busy_q.push_back(q);
+    if (std::find(h->seen_q.begin(), h->seen_q.end(), q) == h->seen_q.end()) {
+        h->seen_q.push_back(q);
+        aql_add_user(q, h);
+    }
     if (rc) return rc;
     if (ce != hipSuccess) return h->fail(CRANE_E_HIP, std::string("queue: ") + aql_error(q));
     return CRANE_OK;

@@ -627,28 +627,37 @@ int crane_dyn_group_schedule(crane_dyn_group* g, int64_t now_ns, int64_t hv_ts_n
         if (e != hipSuccess) return g->hipfail(e, "hipHostMalloc");
         g->h_cap = hk;
     }
+    // a batch like the asynchronous ones (its slot counted in g->batch): every later wait_all —
+    // this call's error path, the next call's start before it may reallocate the pod buffers —
+    // waits for its streams and queues
+    const int slot = (int)(g->batch++ % (uint64_t)g->depth);
     for (int i = 0; i < g->n; ++i) {
-        hipStream_t s = g->st[0][(size_t)i];
+        hipStream_t s = g->st[(size_t)slot][(size_t)i];
         hipError_t e = hipSetDevice(g->dev[(size_t)i]);
         if (e == hipSuccess) e = hipMemcpyAsync(g->b_now[(size_t)i], now_pods, sizeof(int64_t) * P, hipMemcpyHostToDevice, s);
         if (e == hipSuccess)
             e = pod_flags ? hipMemcpyAsync(g->b_flags[(size_t)i], pod_flags, P, hipMemcpyHostToDevice, s)
                           : hipMemsetAsync(g->b_flags[(size_t)i], 0, P, s);
-        if (e == hipSuccess && g->queue(0, i)) e = hipStreamSynchronize(s);  // (a queue orders with nothing)
-        if (e != hipSuccess) return g->hipfail(e, "pod upload");
+        if (e == hipSuccess && g->queue(slot, i)) e = hipStreamSynchronize(s);  // (a queue orders with nothing)
+        if (e != hipSuccess) {
+            (void)wait_all(g);
+            return g->hipfail(e, "pod upload");
+        }
     }
-    Job j{now_ns, hv_ts_ns, n_pods, nullptr, nullptr, nullptr, 0};
+    Job j{now_ns, hv_ts_ns, n_pods, nullptr, nullptr, nullptr, slot};
     std::vector<const int64_t*> pn(g->b_now.begin(), g->b_now.end());
     std::vector<const uint8_t*> pf(g->b_flags.begin(), g->b_flags.end());
     if (int rc = step_here(g, j, pn.data(), pf.data(), g->b_keys.data())) {
+        const std::string m = g->err;
         (void)wait_all(g);
+        g->err = m;
         return rc;
     }
     // the combined keys from device 0; without the collective every shard's, max-combined here
     const int nk = g->use_coll() ? 1 : g->n;
     for (int i = 0; i < nk; ++i) {
-        hipStream_t s = g->st[0][(size_t)i];
-        if (crane_queue* qq = g->queue(0, i))
+        hipStream_t s = g->st[(size_t)slot][(size_t)i];
+        if (crane_queue* qq = g->queue(slot, i))
             if (crane_queue_wait(qq)) return g->fail(CRANE_E_HIP, std::string("queue: ") + crane_queue_last_error(qq));
         hipError_t e = hipSetDevice(g->dev[(size_t)i]);
         if (e == hipSuccess)

@@ -212,14 +212,20 @@ class AddrIndex {
         shift_ = 64 - __builtin_ctzll(cap);
         slots_.assign(cap, {nullptr, -1});
         used_ = 0;
+        base_ = n;
     }
+    // (keeps the table at most half full itself: a caller may put more entries than it sized the
+    // table for — nodes joining in one cycle — and a full table would make put / get spin)
     void put(const void* k, int64_t i) {
+        if (slots_.empty()) reset(0);
+        if (2 * (used_ + 1) > slots_.size()) rehash(2 * slots_.size());
         size_t h = hash(k);
         while (slots_[h].first && slots_[h].first != k) h = (h + 1) & (slots_.size() - 1);
         if (!slots_[h].first) ++used_;
         slots_[h] = {k, i};
     }
     int64_t get(const void* k) const {
+        if (slots_.empty()) return -1;
         size_t h = hash(k);
         for (;;) {
             const auto& s = slots_[h];
@@ -228,13 +234,31 @@ class AddrIndex {
             h = (h + 1) & (slots_.size() - 1);
         }
     }
-    bool crowded() const { return 2 * used_ > slots_.size(); }
+    // stale entries (replaced or departed objects) past the node count the table was built for:
+    // time to rebuild it from the live rows
+    bool crowded() const { return used_ > 2 * base_ + 64; }
+
+    size_t capacity() const { return slots_.size(); }
 
    private:
+    void rehash(size_t cap) {
+        std::vector<std::pair<const void*, int64_t>> old;
+        old.swap(slots_);
+        shift_ = 64 - __builtin_ctzll(cap);
+        slots_.assign(cap, {nullptr, -1});
+        used_ = 0;
+        for (const auto& s : old)
+            if (s.first) {
+                size_t h = hash(s.first);
+                while (slots_[h].first) h = (h + 1) & (cap - 1);
+                slots_[h] = s;
+                ++used_;
+            }
+    }
     size_t hash(const void* k) const { return (size_t)((((uint64_t)(uintptr_t)k >> 4) * 0x9E3779B97F4A7C15ull) >> shift_); }
     std::vector<std::pair<const void*, int64_t>> slots_;
     int shift_ = 64;
-    size_t used_ = 0;
+    size_t used_ = 0, base_ = 0;
 };
 
 // ---------------------------------------------------------------- plugin

@@ -206,3 +206,55 @@ def test_forget_stream_before_destroying_it():
             torch.cuda.synchronize()
             assert hip.hipStreamDestroy(s) == 0
     eng.close()  # (the second stream was destroyed without forget: destroy waits for the device only)
+
+
+@pytest.mark.slow
+def test_group_queues_config3_advancing_batch_times():
+    """The bench's headline path at full size: BASELINE config 3 (100k nodes x 10k pods, a
+    1M-entry binding log) through the group on dispatch queues (depth 4, one device, no
+    collective), six batches whose `now` advances by the pods' span (the hot-value cutoffs move
+    every batch, each slot sees a different time than its previous batch), all in flight before
+    one sync.  Every batch: all keys == one engine stepped on a HIP stream, and a 32-pod sample's
+    chosen node and score == the oracle with the binding log's hot values at that batch's now.
+    Reference: plugins.go:39-98 + selectHost; binding.go:81-97."""
+    import torch
+    spec = cd.default_policy_spec()
+    c = synth.make_cluster(spec, 100_000, 10_000, n_bindings=1_000_000, seed=20250215 + 3000)
+    c.now, c.ds = synth.make_pods(10_000, seed=20250215 + 3)
+    dev = torch.device("cuda", 0)
+    g = cd.Group(cd.Policy(spec), devices=[0], depth=4)
+    g.set_option("collective", 0)
+    g.set_option("dispatch", 1)
+    val, ts, ok = c.rows(g.metric_names)
+    g.upload_nodes(val, ts, c.hv, c.hv_ts)
+    g.upload_bindings(c.b_node, c.b_ts)
+    span = int(c.now[-1] - c.now[0]) + int(c.now[1] - c.now[0])
+    times = [int(c.now[0]) + j * span for j in (0, 1, 2, 3, 4, 5)]
+    pods = [c.now + j * span for j in range(6)]
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    d_now = [torch.from_numpy(p).to(dev) for p in pods]
+    keys = [torch.empty(len(c.now), dtype=torch.int64, device=dev) for _ in range(6)]
+    for b in range(6):  # batch b on slot b % 4; six key buffers, so every batch's keys survive
+        g.step_keys_async(times[b], times[b], [d_now[b]], [d_flags], [keys[b]])
+    g.sync()
+    eng = cd.Engine(cd.Policy(spec), 0)
+    eng.upload_nodes(val, ts, c.hv, c.hv_ts)
+    eng.upload_bindings(c.b_node, c.b_ts)
+    st = torch.cuda.Stream(dev)
+    ref = torch.empty_like(keys[0])
+    smp = np.unique(np.concatenate([np.linspace(0, 9999, 24).astype(int), np.flatnonzero(c.ds)[:8]]))
+    for b in range(6):
+        eng.step_keys_async(times[b], times[b], d_now[b], d_flags, ref, st.cuda_stream)
+        st.synchronize()
+        got = keys[b].cpu().numpy()
+        assert np.array_equal(got, ref.cpu().numpy()), f"batch {b}: queue group keys differ from the stream engine's"
+        _, hv = O.hot_values(spec, c.b_node, c.b_ts, c.n_nodes, times[b] // 10**9)
+        off, osc, och = oracle_soa(spec, c, now=pods[b][smp], ds=c.ds[smp],
+                                   hv_override=(hv.astype(np.float64), np.full(c.n_nodes, times[b], np.int64)))
+        node, score = shard.unpack_keys(got[smp])
+        assert np.array_equal(node, och), f"batch {b}"
+        for i in range(len(smp)):
+            feas = (off[i] < 0) | (c.ds[smp[i]] != 0)
+            assert score[i] == (osc[i][feas].max() if feas.any() else -1), (b, i)
+    eng.close()
+    g.close()

@@ -207,3 +207,82 @@ def test_churn_through_plugin(driver, cluster_small, tmp_path, horizon):
         if t0 is None or not (t0 <= pod["now_ns"] < t1):
             want, t0, t1 = want + 1, pod["now_ns"], pod["now_ns"] + 60 * 10**9
     assert tables == (1 if horizon == "all" else want)
+
+
+@pytest.mark.gpu
+def test_many_joins_after_a_small_first_sync(driver, cluster_small, tmp_path):
+    """A first sync over a handful of nodes sizes the plugin's address indexes for them; then
+    sixty nodes join in one cycle (below the full-resync threshold, so the incremental path takes
+    them).  The indexes grow as the joins go in (a full open-addressing table made the leader spin
+    while holding the plugin's lock), and every Filter / Score equals the oracle's string mode."""
+    import numpy as np
+    from oracle import oracle as O
+    c = cluster_small
+    pol = policy_from_json(c["policy"])
+    nodes = [dict(a) for a in c["nodes"][:4]]
+    names = [f"node-{i}" for i in range(len(nodes))]
+    lines = [f"policy\t{write_policy(tmp_path, pol)}"]
+    for i, a in enumerate(nodes):
+        lines.append(f"node\t{names[i]}")
+        lines += [f"anno\t{k}\t{v}" for k, v in a.items()]
+    pods = c["pods"][:2]
+    lines.append(f"pod\tp0\t{pods[0]['now_ns']}\t0")
+    for j in range(60):
+        a = dict(c["nodes"][j % len(c["nodes"])])
+        nodes.append(a)
+        names.append(f"joined-{j}")
+        lines.append(f"node\t{names[-1]}")
+        lines += [f"anno\t{k}\t{v}" for k, v in a.items()]
+    lines.append(f"pod\tp1\t{pods[1]['now_ns']}\t0")
+    lines.append("counters")
+    out = run(driver, "\n".join(lines) + "\n")
+    F = [o for o in out if o[0] == "F"]
+    S = [o for o in out if o[0] == "S"]
+    off = 0
+    for p, n_nodes in ((0, 4), (1, len(nodes))):
+        ff, sc, _ = O.eval_strings(pol, nodes[:n_nodes], np.array([pods[p]["now_ns"]], np.int64),
+                                   np.array([0], np.uint8))
+        for n in range(n_nodes):
+            f, s = F[off + n], S[off + n]
+            assert f[2] == names[n] and s[2] == names[n]
+            assert f[3] == str(SUCCESS if ff[0][n] < 0 else UNSCHED), (p, n)
+            assert s[3] == str(sc[0][n]), (p, n)
+        off += n_nodes
+    C = [o for o in out if o[0] == "C"][0]
+    full, joined = int(C[2]), int(C[5])
+    assert full == 1 and joined == 60
+
+
+def test_addr_index_grows_past_its_sizing(tmp_path):
+    """AddrIndex (crane_dyn_plugin.hpp) sized for 0 or 10 entries takes thousands of puts: it
+    rehashes itself instead of filling up (the put loop would spin on a full table)."""
+    src = tmp_path / "ai.cpp"
+    src.write_text(r'''
+#include "crane_dyn_plugin.hpp"
+#include <cstdio>
+int main() {
+    using crane::dynamic::AddrIndex;
+    static int objs[5000];
+    for (size_t first : {0, 10}) {
+        AddrIndex ix;
+        ix.reset(first);
+        for (int i = 0; i < 5000; ++i) ix.put(&objs[i], i);
+        for (int i = 0; i < 5000; ++i)
+            if (ix.get(&objs[i]) != i) { std::printf("BAD %d\n", i); return 1; }
+        if (ix.get(&first) != -1 || 2 * 5000 > ix.capacity() || !ix.crowded()) { std::printf("BAD\n"); return 1; }
+    }
+    AddrIndex empty;
+    if (empty.get(objs) != -1) return 1;
+    std::printf("OK\n");
+    return 0;
+}
+''')
+    exe = str(tmp_path / "ai")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-fsyntax-only", "-I", os.path.join(ROOT, "include"),
+                    str(src)], check=True)
+    if not os.path.exists(os.path.join(LIB_DIR, "libcrane_dyn.so")):
+        pytest.skip("libcrane_dyn.so not built")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-pthread", "-I", os.path.join(ROOT, "include"), str(src),
+                    "-L", LIB_DIR, "-lcrane_dyn", "-Wl,-rpath," + LIB_DIR, "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip() == "OK", r.stdout
