@@ -111,25 +111,13 @@ int64_t floor_div(int64_t a, int64_t b) {
 // Engine options: fixed defaults; crane_dyn_set_option changes them per engine
 // (tests and A/B tools only — nothing reads the environment).
 struct Options {
-    int k2_form = 0;          // 0: dedupe (large / binned / hash when it does not fit), 1: binned, 2: hash,
-                              // 3: large (region pass with coarse bins + dense per-bin histograms)
-    int k1_threads = 256;     // K1 workgroup size (the dedupe K2 bins nodes by it): 128 or 256
-    bool k1_keep_rec = false; // the fused keys-only step also writes the node records
-    bool k1_fuse = true;      // K3a (step tables) fused into the node pass
-    bool k3p_in_k2 = true;    // K3p rides as extra workgroups of the K2x launch
+    int k2_form = 0;          // 0: dedupe, the large form past its count/offset cap, the atomics form past that;
+                              // 2: the atomics form (LDS hash + global atomics); 3: the large form (region
+                              // pass with coarse bins + dense per-bin histograms)
     int keys_path = 0;        // 0: step path when it applies, 1: the per-pair kernel (K3m keys)
     int greedy_form = 0;      // 0: merge form when every hotValue count > 0, 1: sequential kernel
-    int matrix_vec = 0;       // K3m nodes per lane: 0 automatic, 1 / 4 / 8 / 16
-    int matrix_chunk = 0;     // K3m pods per workgroup: 0 automatic
-    int step_rows = 1;        // 1: producers write per-tile record ranges for K3s, 0: K3s searches
-    int k3s_blocks = 0;       // K3s producer blocks per workgroup aimed for: 0 automatic
-    int k2x_threads = 512;    // dedupe K2 workgroup size: 256, 512 or 1024
-    int k2l_region = 4096;    // large K2: bindings per region (2048 or 4096)
-    int k2l_co_t = 0;         // large K2: count/offset words [bin][region] (1) or [region][bin] (0)
-    int k2l_threads = 1024;   // large K2: partition workgroup size at 4096-binding regions (512 or 1024;
-                              // cold 4M x 16M: 1024 0.084-0.085 ms vs 512 0.087-0.089, same-box sweeps
-                              // profiles/ab/r03_k2_cold_*.txt)
     int sel_chain = 0;        // selection windows: 0 LDS rank/select walk when it fits, 1 streaming kernel
+    int step_rows = 1;        // 1: producers write per-tile record ranges for K3s (when they fit), 0: K3s searches
     int step_lds_cap = 1 << 30;  // K1: one-step records per kind staged in LDS at most (0: always st.stage)
     int step_pieces = 0;      // middle pieces cut into elementary ones per block (step_pieces): 0 when the
                               // producer blocks take more than 4 rounds of the CUs (there the producers'
@@ -144,9 +132,12 @@ struct Options {
     int k1_tail = 0;          // the streamed pass's tail: 0 on one wave when the grid has >= 4096 blocks
                               // (the other waves leave), 1 always on one wave, 4 on all four
     int k2_sorted = 1;        // a time-ordered log: K2 reads the widest window's suffix, ranks by position
-    int k2_slide = 0;         // 1: ... and keeps dense window counts, moved by the bindings between the last
-                              // refresh's window starts and this one's | 0 recount every refresh
 };
+// Fixed launch shapes (round 6 removed their options; the A/B sweeps that chose them are in
+// profiles/ab/r03_k2_cold_*.txt and profiles/r05/config3_option_sweep_queues.txt)
+constexpr int kK1Block = 256;     // K1 workgroup size (the dedupe K2 bins nodes by it)
+constexpr int kK2xThreads = 512;  // dedupe K2 workgroup size
+constexpr int kK2lThreads = 1024; // large K2 partition workgroup size (4096-binding regions)
 constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
 
 }  // namespace
@@ -192,8 +183,6 @@ struct crane_dyn {
     std::vector<int64_t> hts_copy;      // ... and its timestamps (the windows' suffixes are found here)
     std::vector<int64_t> hts_sample;    // every 64th of them: the suffix search touches one 512-byte run
     bool pos_valid = false;             // pos_s[r]: the suffix start of window rank r for cutoffs pos_cut
-    bool slide_valid = false;           // buckets hold the window-rank counts for suffix starts slide_s
-    int64_t slide_s[kMaxWin] = {};
     int64_t pos_cut[kMaxWin] = {};
     int64_t pos_s[kMaxWin] = {};
     HostBuf<int32_t> hnode;       // pinned mirror of the slots in heap mode
@@ -213,7 +202,7 @@ struct crane_dyn {
     DevBuf<int8_t> score8;
     HostBuf<int8_t> stage8;
     HostBuf<long long> stagek;
-    DevBuf<uint32_t> k2_cnt, k2_tot, k2_sorted;  // K2 scratch
+    DevBuf<uint32_t> k2_sorted;  // K2 scratch
     DevBuf<double> hvc;                           // [N] binding-log hot values of the last consuming K1
     DevBuf<uint32_t> gcnt;  // greedy: per-window counts [W][N]
     DevBuf<int64_t> gbase, gchosen;
@@ -439,57 +428,17 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         bn = h->bnode.p + s0;
         Bk = h->B - s0;
     }
-    // Sliding windows: the last refresh's dense counts moved by the bindings between its window
-    // starts and this one's (a batch 10 s later: tens of thousands of bindings instead of the
-    // suffix's hundreds of thousands); a first refresh, or most of the log in between, recounts
-    // with the large form (dense counts), which the next refreshes then move
-    const bool slide = by_pos && h->opt.k2_slide != 0 && h->opt.k2_form == 0;
-    if (!slide) h->slide_valid = false;
-    if (slide && h->slide_valid) {
-        SlideArgs sa{};
-        sa.bnode = h->bnode.p;
-        sa.N = h->N;
-        sa.W = dp.n_win;
-        sa.buckets = h->buckets.p;
-        std::pair<int64_t, int64_t> iv[kMaxWin];
-        int ni = 0;
-        for (int r = 0; r < dp.n_win; ++r) {
-            sa.s_old[r] = h->slide_s[r];
-            sa.s_new[r] = h->pos_s[r];
-            const int64_t a = std::min(sa.s_old[r], sa.s_new[r]), b = std::max(sa.s_old[r], sa.s_new[r]);
-            if (a < b) iv[ni++] = {a, b};
-        }
-        std::sort(iv, iv + ni);
-        for (int i = 0; i < ni; ++i) {  // the disjoint union
-            if (sa.nr > 0 && iv[i].first <= sa.lo[sa.nr - 1] + sa.len[sa.nr - 1]) {
-                sa.len[sa.nr - 1] = std::max(sa.len[sa.nr - 1], iv[i].second - sa.lo[sa.nr - 1]);
-            } else {
-                sa.lo[sa.nr] = iv[i].first;
-                sa.len[sa.nr] = iv[i].second - iv[i].first;
-                ++sa.nr;
-            }
-        }
-        for (int i = 0; i < sa.nr; ++i) sa.total += sa.len[i];
-        if (sa.total <= Bk / 2) {
-            HIPTRY(h, launch_hot_slide(sa, st, pods));
-            if (pods_done) *pods_done = pods != nullptr && pods->P > 0;
-            std::memcpy(h->slide_s, h->pos_s, sizeof(int64_t) * dp.n_win);
-            h->buckets_zero = false;
-            h->buckets_dense = true;
-            return CRANE_OK;
-        }
-    }
-    HotPart gx = hot_dedupe_geometry(Bk, h->N, dp.n_win, h->opt.k1_threads);
+    HotPart gx = hot_dedupe_geometry(Bk, h->N, dp.n_win, kK1Block);
     gx.trace = gx.nblk <= kTraceWgs ? h->trace_region(0) : nullptr;
-    if (h->opt.k2_form == 0 && gx.ok && !slide) {
+    if (h->opt.k2_form == 0 && gx.ok) {
         // one launch (+ K3p); the node pass counts its own block's entries (no buckets).  The
         // scratch is sized for the whole log, not this refresh's suffix: the suffix moves with
         // `now`, and a reallocation (hipFree waits for the device) inside a pipeline of batches
         // cost 30-55 us per batch when the batch times advanced
-        const HotPart gf = hot_dedupe_geometry(h->B, h->N, dp.n_win, h->opt.k1_threads);
+        const HotPart gf = hot_dedupe_geometry(h->B, h->N, dp.n_win, kK1Block);
         HIPTRY(h, h->k2_sorted.reserve(std::max(hot_dedupe_scratch(gx), gf.ok ? hot_dedupe_scratch(gf) : 0)));
         HIPTRY(h, launch_hot_count_dedupe(bn, h->bts.p, Bk, h->N, by_pos ? pcut : cut, gx, h->k2_sorted.p, st, pods,
-                                          h->opt.k2x_threads));
+                                          kK2xThreads));
         if (pods_done) *pods_done = pods != nullptr && pods->P > 0;
         h->hx_g = gx;
         h->hx_pending = true;
@@ -498,23 +447,20 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     const size_t nb = (size_t)std::max(1, dp.n_win) * (size_t)std::max<int64_t>(h->N, 1);
     if (nb > h->buckets.n) h->buckets_zero = false;
     HIPTRY(h, h->buckets.reserve(nb));
-    HotPart gl = hot_large_geometry(Bk, h->N, dp.n_win, h->opt.k2l_region, h->opt.k2l_co_t);
+    HotPart gl = hot_large_geometry(Bk, h->N, dp.n_win);
     gl.trace = gl.nblk <= kTraceWgs ? h->trace_region(0) : nullptr;  // (stamps per region)
     if ((h->opt.k2_form == 0 || h->opt.k2_form == 3) && gl.ok) {
         // the region pass with coarse bins + the dense per-bin histogram: every bucket row
         // is rewritten, so nothing is zeroed before and K1 leaves them
-        const HotPart gf = hot_large_geometry(h->B, h->N, dp.n_win, h->opt.k2l_region, h->opt.k2l_co_t);
+        const HotPart gf = hot_large_geometry(h->B, h->N, dp.n_win);
         HIPTRY(h, h->k2_sorted.reserve(std::max(hot_dedupe_scratch(gl), gf.ok ? hot_dedupe_scratch(gf) : 0)));
         HIPTRY(h, launch_hot_count_large(bn, h->bts.p, Bk, h->N, by_pos ? pcut : cut, gl, h->k2_sorted.p,
-                                         h->buckets.p, h->n_cu, st, h->opt.k2l_threads));
+                                         h->buckets.p, h->n_cu, st, kK2lThreads));
         h->buckets_zero = false;
         h->buckets_dense = true;
-        h->slide_valid = slide;
-        if (slide) std::memcpy(h->slide_s, h->pos_s, sizeof(int64_t) * dp.n_win);
         return CRANE_OK;
     }
     h->buckets_dense = false;
-    h->slide_valid = false;
     if (!h->buckets_zero && tl_aql) {
         // (on a dispatch queue: a fill is no kernel here — after the queue's packets, on the engine
         // stream, waited for)
@@ -524,23 +470,15 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     } else if (!h->buckets_zero) {
         HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
     }
-    const HotBins g = hot_bins_geometry(h->B, h->N, dp.n_win);
-    if (g.ok && h->opt.k2_form != 2) {
-        HIPTRY(h, h->k2_cnt.reserve((size_t)g.nbins * (size_t)g.nchunks));
-        HIPTRY(h, h->k2_tot.reserve((size_t)g.nbins));
-        HIPTRY(h, h->k2_sorted.reserve((size_t)std::max<int64_t>(h->B, 1)));
-        HIPTRY(h, launch_hot_count_binned(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, g, h->k2_cnt.p,
-                                          h->k2_tot.p, h->k2_sorted.p, st));
-    } else {
-        HIPTRY(h, launch_hot_count(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, st));
-    }
+    // the atomics form (any size; shards past the large form's caps)
+    HIPTRY(h, launch_hot_count(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, st));
     h->buckets_zero = false;
     return CRANE_OK;
 }
 
 // K1's workgroup size: the dedupe-form K2 bins nodes by it
 static int k1_bs(const crane_dyn* h) {
-    return h->hv_from_counts && h->counts_pending && h->hx_pending ? 1 << h->hx_g.bb : h->opt.k1_threads;
+    return h->hv_from_counts && h->counts_pending && h->hx_pending ? 1 << h->hx_g.bb : kK1Block;
 }
 
 // K1 (optionally with the K3 step tables fused in).  Hot values: pending K2
@@ -555,7 +493,7 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
     a.ts = h->ts.p;
     // the fused keys-only step reads its records from LDS; writing them out
     // (160 B/node of the pass's 280) is left to the next pass that reads them
-    const bool keep = !step || h->opt.k1_keep_rec;
+    const bool keep = !step;
     a.out = keep ? h->rec.p : nullptr;
     a.hv_ts_counts = h->hv_ts_counts;
     const bool consume = h->hv_from_counts && h->counts_pending;
@@ -603,10 +541,10 @@ static bool step_path_ok(const crane_dyn* h, int64_t P) {
 }
 
 static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
-    sp.fuse = h->rec_dirty && h->opt.k1_fuse;
+    sp.fuse = h->rec_dirty;
     const int32_t bs = sp.fuse ? k1_bs(h) : kStepSeg;  // producer workgroup size
     const int32_t nblk = (int32_t)((h->N + bs - 1) / bs);
-    sp.g = step_geometry(P, h->N, nblk, h->opt.k3s_blocks);
+    sp.g = step_geometry(P, h->N, nblk, 0);
     const StepGeometry& g = sp.g;
     HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
     HIPTRY(h, h->stile.reserve((size_t)(kTileStat * g.ntiles)));
@@ -707,8 +645,6 @@ static int matrix_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const ui
     a.score = d_score;
     a.score_i64 = score_i64 ? 1 : 0;
     a.keys = d_keys;
-    a.matrix_vec = h->opt.matrix_vec;
-    a.matrix_chunk = h->opt.matrix_chunk;
     std::memcpy(a.pred_orig, h->pred_orig, sizeof a.pred_orig);
     if (d_keys && P > 0) HIPTRY(h, hipMemsetAsync(d_keys, 0xFF, sizeof(long long) * (size_t)P, st));
     HIPTRY(h, launch_matrix(h->shape, a, st));
@@ -845,7 +781,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->buckets.release(); h->bnode.release(); h->bts.release(); h->now.release(); h->flags.release();
     h->keys.release(); h->ff.release(); h->score.release(); h->score8.release();
     h->stage8.release(); h->stagek.release(); h->hnode.release(); h->hts.release();
-    h->k2_cnt.release(); h->k2_tot.release(); h->k2_sorted.release(); h->hvc.release();
+    h->k2_sorted.release(); h->hvc.release();
     h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
     h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
     h->mFs.release(); h->mIs.release(); h->mgi.release();
@@ -900,27 +836,15 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     const std::string n = name;
     Options& o = h->opt;
     auto range = [&](int64_t lo, int64_t hi) { return value >= lo && value <= hi; };
-    if (n == "k2_form" && range(0, 3)) o.k2_form = (int)value;
-    else if (n == "k1_threads" && (value == 128 || value == 256)) o.k1_threads = (int)value;
-    else if (n == "k1_keep_records" && range(0, 1)) o.k1_keep_rec = value != 0;
-    else if (n == "k1_fuse_steps" && range(0, 1)) o.k1_fuse = value != 0;
-    else if (n == "k3p_in_k2" && range(0, 1)) o.k3p_in_k2 = value != 0;
+    if (n == "k2_form" && (value == 0 || value == 2 || value == 3)) o.k2_form = (int)value;
     else if (n == "keys_path" && range(0, 1)) o.keys_path = (int)value;
     else if (n == "greedy_form" && range(0, 1)) o.greedy_form = (int)value;
-    else if (n == "matrix_vec" && (value == 0 || value == 1 || value == 4 || value == 8 || value == 16)) o.matrix_vec = (int)value;
-    else if (n == "matrix_chunk" && range(0, 1024)) o.matrix_chunk = (int)value;
-    else if (n == "step_rows" && range(0, 1)) o.step_rows = (int)value;
-    else if (n == "k3s_blocks" && range(0, 256)) o.k3s_blocks = (int)value;
-    else if (n == "k2x_threads" && (value == 256 || value == 512 || value == 1024)) o.k2x_threads = (int)value;
-    else if (n == "k2l_region" && (value == 2048 || value == 4096)) o.k2l_region = (int)value;
-    else if (n == "k2l_co_t" && range(0, 1)) o.k2l_co_t = (int)value;
-    else if (n == "k2l_threads" && (value == 512 || value == 1024)) o.k2l_threads = (int)value;
     else if (n == "sel_chain" && range(0, 1)) o.sel_chain = (int)value;
+    else if (n == "step_rows" && range(0, 1)) o.step_rows = (int)value;
     else if (n == "step_pieces" && range(0, 2)) o.step_pieces = (int)value;
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
     else if (n == "k2_sorted" && range(0, 1)) o.k2_sorted = (int)value;
     else if (n == "k1_stream" && range(0, 1)) o.k1_stream = (int)value;
-    else if (n == "k2_slide" && range(0, 1)) o.k2_slide = (int)value;
     else if (n == "k1_tail" && (value == 0 || value == 1 || value == 4)) o.k1_tail = (int)value;
     else if (n == "trace" && range(0, 1)) {
         o.trace = value != 0;
@@ -977,7 +901,6 @@ int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const d
     }
     HIPTRY(h, hipStreamSynchronize(h->stream));
     if (n != h->N) h->buckets_zero = false;
-    h->slide_valid = false;
     h->N = n;
     h->node_offset = node_offset;
     h->have_hv = hv != nullptr;
@@ -1004,7 +927,6 @@ int crane_dyn_upload_bindings(crane_dyn* h, int64_t n, const int32_t* node, cons
     // a ring of bindings appended in time order (the synthetic and the controller-shaped logs):
     // kept for the suffix search of every refresh
     h->pos_valid = false;
-    h->slide_valid = false;
     h->log_sorted = n > 0 && std::is_sorted(ts_s, ts_s + n);
     h->hts_sample.clear();
     if (h->log_sorted) {
@@ -1044,7 +966,6 @@ int crane_dyn_binding_records(crane_dyn* h, int64_t size, int64_t gc_time_range_
     h->heap_mode = true;
     h->log_sorted = false;  // heap order
     h->pos_valid = false;
-    h->slide_valid = false;
     h->hts_copy.clear();
     h->hts_sample.clear();
     h->B = size;
@@ -1278,7 +1199,7 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
     if (rc) return rc;
     const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys, h->sbatch.p};
     bool pods_done = false;
-    rc = hot_values_locked(h, now_ns, hv_ts_ns, st, h->opt.k3p_in_k2 ? &pp : nullptr, &pods_done);
+    rc = hot_values_locked(h, now_ns, hv_ts_ns, st, &pp, &pods_done);
     if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, st);
     if (!rc) rc = step_rest(h, sp, P, keys, st);
     return rc ? rc : mark_busy(h, st);
@@ -1317,7 +1238,7 @@ int crane_dyn_step_keys_queue(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
         rc = step_plan(h, P, sp);
         const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys, h->sbatch.p};
         bool pods_done = false;
-        if (!rc) rc = hot_values_locked(h, now_ns, hv_ts_ns, h->stream, h->opt.k3p_in_k2 ? &pp : nullptr, &pods_done);
+        if (!rc) rc = hot_values_locked(h, now_ns, hv_ts_ns, h->stream, &pp, &pods_done);
         if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, h->stream);
         if (!rc) rc = step_rest(h, sp, P, keys, h->stream);
     }
@@ -1663,7 +1584,6 @@ int crane_dyn_resize_nodes(crane_dyn* h, int64_t n) {
     HIPTRY(h, h->rec.reserve((size_t)n * h->rec_bytes));
     h->N = n;
     h->buckets_zero = false;
-    h->slide_valid = false;     // the dense counts' layout is [W][N]
     h->hv_from_counts = false;  // binding-log hot values were per old node index
     h->counts_pending = false;
     h->hx_pending = false;

@@ -10,16 +10,9 @@
 //   per distinct pair, binned by K1 node block, plus a coalesced row of
 //   (count, offset) words; K1 counts its own block's entries in LDS.  No global
 //   atomics, no bucket matrix.
-// Binned form (when the count/offset matrix would pass 2^22 words, e.g. 4M nodes
-//   x 16M bindings): bindings partitioned by node range ("bins" of 2^BB nodes),
-//   each bin counted in a dense LDS histogram and flushed with contiguous
-//   atomics (lane i -> node i) into the bucket matrix K1 reads and zeroes.
-//     A  bin_count : chunk of bindings -> per-(bin, chunk) counts
-//     B  bin_scan  : per bin, exclusive scan over chunks + bin total
-//     C  scatter   : chunk of bindings -> bin-contiguous packed entries
-//                    (local node | bucket << 24)
-//     D  bin_hist  : (bin, split) -> LDS histogram [W][2^BB] -> buckets
-// Order inside a bin is not deterministic; counts are.
+// Large form (past the dedupe form's count/offset cap, e.g. 4M nodes x 16M bindings): the same
+//   region pass with coarse bins, then one workgroup per bin writes its rows of a dense bucket
+//   matrix.  The atomics form (kernels.hip, k2_hot_count) takes any shape past the large form's caps.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -31,138 +24,12 @@
 
 namespace crane {
 
-constexpr int kHT = 256;  // threads per workgroup in all four kernels
-
 __device__ __forceinline__ int window_rank(int64_t ts, const HotCutoffs& cut) {
     int j = 0;
 #pragma unroll
     for (int w = 0; w < kMaxWin; ++w)
         if (w < cut.n_win) j += ts > cut.sorted[w] ? 1 : 0;
     return j;  // 0: in no window
-}
-
-__global__ __launch_bounds__(kHT) void k2a_bin_count(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
-                                                     int64_t B, int64_t N, HotCutoffs cut, HotBins g,
-                                                     uint32_t* __restrict__ chunk_cnt) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // [nbins]
-    for (int i = threadIdx.x; i < g.nbins; i += kHT) hist[i] = 0;
-    __syncthreads();
-    const int64_t b0 = (int64_t)blockIdx.x * g.chunk, b1 = min(B, b0 + g.chunk);
-    for (int64_t b = b0 + threadIdx.x; b < b1; b += kHT) {
-        const int32_t nd = bnode[b];
-        if (nd < 0 || (int64_t)nd >= N || !window_rank(bts[b], cut)) continue;
-        atomicAdd(&hist[nd >> g.bb], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < g.nbins; i += kHT) chunk_cnt[(int64_t)i * g.nchunks + blockIdx.x] = hist[i];
-}
-
-// exclusive scan of up to kHT*16 values in place; returns the total (block-wide)
-__global__ __launch_bounds__(kHT) void k2b_bin_scan(uint32_t* __restrict__ chunk_cnt, HotBins g,
-                                                    uint32_t* __restrict__ bin_tot) {
-    __shared__ uint32_t part[kHT];
-    uint32_t* row = chunk_cnt + (int64_t)blockIdx.x * g.nchunks;
-    const int per = (g.nchunks + kHT - 1) / kHT;
-    const int lo = threadIdx.x * per, hi = min(g.nchunks, lo + per);
-    uint32_t s = 0;
-    for (int i = lo; i < hi; ++i) s += row[i];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int off = 1; off < kHT; off <<= 1) {  // Hillis-Steele inclusive scan of the partials
-        const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    for (int i = lo; i < hi; ++i) {
-        const uint32_t v = row[i];
-        row[i] = run;
-        run += v;
-    }
-    if (threadIdx.x == kHT - 1) bin_tot[blockIdx.x] = part[kHT - 1];
-}
-
-// LDS exclusive scan of bin_tot[0..nbins) into base[] (nbins <= kMaxBins)
-__device__ void scan_bins(const uint32_t* __restrict__ bin_tot, int nbins, uint32_t* base /*LDS*/,
-                          uint32_t* part /*LDS kHT*/) {
-    const int per = (nbins + kHT - 1) / kHT;
-    const int lo = threadIdx.x * per, hi = min(nbins, lo + per);
-    uint32_t s = 0;
-    for (int i = lo; i < hi; ++i) s += bin_tot[i];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int off = 1; off < kHT; off <<= 1) {
-        const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    for (int i = lo; i < hi; ++i) {
-        base[i] = run;
-        run += bin_tot[i];
-    }
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(kHT) void k2c_scatter(const int32_t* __restrict__ bnode, const int64_t* __restrict__ bts,
-                                                   int64_t B, int64_t N, HotCutoffs cut, HotBins g,
-                                                   const uint32_t* __restrict__ chunk_off,
-                                                   const uint32_t* __restrict__ bin_tot, uint32_t* __restrict__ sorted) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t cursor[];  // [nbins]
-    __shared__ uint32_t part[kHT];
-    scan_bins(bin_tot, g.nbins, cursor, part);
-    for (int i = threadIdx.x; i < g.nbins; i += kHT) cursor[i] += chunk_off[(int64_t)i * g.nchunks + blockIdx.x];
-    __syncthreads();
-    const int64_t b0 = (int64_t)blockIdx.x * g.chunk, b1 = min(B, b0 + g.chunk);
-    const uint32_t mask = (1u << g.bb) - 1;
-    for (int64_t b = b0 + threadIdx.x; b < b1; b += kHT) {
-        const int32_t nd = bnode[b];
-        if (nd < 0 || (int64_t)nd >= N) continue;
-        const int j = window_rank(bts[b], cut);
-        if (!j) continue;
-        const uint32_t pos = atomicAdd(&cursor[nd >> g.bb], 1u);
-        sorted[pos] = ((uint32_t)nd & mask) | ((uint32_t)(j - 1) << 24);
-    }
-}
-
-__global__ __launch_bounds__(kHT) void k2d_bin_hist(const uint32_t* __restrict__ sorted,
-                                                    const uint32_t* __restrict__ bin_tot, HotBins g, int32_t W,
-                                                    int64_t N, uint32_t* __restrict__ buckets) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // [W][binw]
-    __shared__ uint32_t part[kHT];
-    __shared__ uint32_t start_s;
-    const int bin = blockIdx.x, split = blockIdx.y;
-    // base of this bin = sum of the totals of the bins before it
-    {
-        uint32_t s = 0;
-        for (int i = threadIdx.x; i < bin; i += kHT) s += bin_tot[i];
-        part[threadIdx.x] = s;
-        __syncthreads();
-        for (int off = kHT / 2; off > 0; off >>= 1) {
-            if (threadIdx.x < off) part[threadIdx.x] += part[threadIdx.x + off];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) start_s = part[0];
-    }
-    const int binw = 1 << g.bb;
-    for (int i = threadIdx.x; i < W * binw; i += kHT) hist[i] = 0;
-    __syncthreads();
-    const uint32_t len = bin_tot[bin], start = start_s;
-    const uint32_t e0 = start + (uint32_t)((uint64_t)len * split / gridDim.y);
-    const uint32_t e1 = start + (uint32_t)((uint64_t)len * (split + 1) / gridDim.y);
-    for (uint32_t e = e0 + threadIdx.x; e < e1; e += kHT) {
-        const uint32_t v = sorted[e];
-        atomicAdd(&hist[(v >> 24) * binw + (v & 0xFFFFFF)], 1u);
-    }
-    __syncthreads();
-    const int64_t n0 = (int64_t)bin << g.bb;
-    for (int w = 0; w < W; ++w)
-        for (int i = threadIdx.x; i < binw; i += kHT) {
-            const uint32_t c = hist[w * binw + i];
-            if (c && n0 + i < N) atomicAdd(&buckets[(int64_t)w * N + n0 + i], c);  // contiguous across lanes
-        }
 }
 
 constexpr int kXChunk = kHxRegion;  // bindings per dedupe-form workgroup (K1 reads the regions with this stride)
@@ -382,11 +249,8 @@ static hipError_t launch_dedupe_p(const int32_t* bnode, const int64_t* bts, int6
 hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                    const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
                                    const PodPrep* pods, int threads) {
-    switch (threads) {
-        case 256: return launch_dedupe_p<256>(bnode, bts, B, N, cut, g, scratch, st, pods);
-        case 512: return launch_dedupe_p<512>(bnode, bts, B, N, cut, g, scratch, st, pods);
-        default: return launch_dedupe_p<1024>(bnode, bts, B, N, cut, g, scratch, st, pods);
-    }
+    if (threads != 512) return hipErrorInvalidValue;  // (512: profiles/r05/config3_option_sweep_queues.txt)
+    return launch_dedupe_p<512>(bnode, bts, B, N, cut, g, scratch, st, pods);
 }
 
 size_t hot_dedupe_scratch(const HotPart& g) { return (size_t)g.cap + (size_t)g.nbins * (size_t)g.nblk; }
@@ -404,8 +268,8 @@ size_t hot_dedupe_scratch(const HotPart& g) { return (size_t)g.cap + (size_t)g.n
 //      region (the count/offset words, then the runs) into an LDS histogram [W][2^bb] and
 //      writes the bin's rows of buckets [W][N] whole — no global atomics, nothing to zero
 //      (K1 reads them and leaves them, K1Args::buckets_keep).
-// Count/offset words: CO [nblk][nbins] (g.co_t = 0: X writes its row coalesced, Y reads a
-// column) or [nbins][nblk] (co_t = 1: Y reads its row coalesced, X writes a column).
+// Count/offset words: CO [nblk][nbins] (X writes its row coalesced, Y reads a column; the
+// transposed layout measured no better, profiles/ab/r03_k2_cold_*.txt).
 // POS: a time-ordered log ranked by position (HotCutoffs::by_pos): no timestamp loads (a
 // template parameter: a load inside a run-time branch makes the compiler wait for every load
 // at the join, which serialised the next region's prefetch)
@@ -470,7 +334,7 @@ void k2l_partition(const int32_t* __restrict__ bnode,
         for (int i = lo; i < hi; ++i) {  // offsets + this region's count/offset words; hist cleared
             const uint32_t c = hist[i];
             off[i] = run;
-            CO[g.co_t ? (int64_t)i * g.nblk + r : r * g.nbins + i] = c | (run << 16);
+            CO[r * g.nbins + i] = c | (run << 16);
             hist[i] = 0;
             run += c;
         }
@@ -525,7 +389,7 @@ __global__ __launch_bounds__(kYThreads) void k2y_bin_hist(const uint32_t* __rest
         for (int u = 0; u < kYPer; ++u) {
             const int i = i0 + u * kYThreads + threadIdx.x;
             const int ic = min(i, g.nblk - 1);
-            const uint32_t co = CO[g.co_t ? bin * g.nblk + ic : (int64_t)ic * g.nbins + bin];
+            const uint32_t co = CO[(int64_t)ic * g.nbins + bin];
             c[u] = i < g.nblk ? co & 0xFFFF : 0u;
             o[u] = co >> 16;
         }
@@ -596,13 +460,12 @@ __global__ __launch_bounds__(kYThreads) void k2y_bin_hist(const uint32_t* __rest
     CRANE_TSTAMP(g.trace, bin, 6);
 }
 
-HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W, int32_t reg, int32_t co_t) {
+HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W) {
     HotPart g{};
     int bb = 16;  // entry format: local node in 16 bits
     while (bb > 8 && (int64_t)std::max(W, 1) * (4LL << bb) > kK2LargeHistBytes) --bb;  // Y's LDS histogram
     g.bb = bb;
-    g.reg = reg == 2048 ? 2048 : 4096;
-    g.co_t = co_t ? 1 : 0;
+    g.reg = kK2lRegion;
     g.nbins = (int32_t)((N + (1LL << bb) - 1) >> bb);
     g.nblk = (int32_t)((B + g.reg - 1) / g.reg);
     g.cap = (int64_t)g.nblk * g.reg;
@@ -654,10 +517,8 @@ static hipError_t launch_y(const uint32_t* scratch, const HotPart& g, int32_t W,
 hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, uint32_t* buckets,
                                   int n_cu, hipStream_t st, int threads) {
-    hipError_t e;
-    if (g.reg == 2048) e = launch_large_x<512, 2048>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
-    else if (threads == 1024) e = launch_large_x<1024, 4096>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
-    else e = launch_large_x<512, 4096>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
+    if (threads != 1024) return hipErrorInvalidValue;  // (1024 threads per 4096-binding region: round 3's sweep)
+    hipError_t e = launch_large_x<1024, kK2lRegion>(bnode, bts, B, N, cut, g, scratch, n_cu, st);
     if (e != hipSuccess) return e;
     // kYPer = the fewest regions per lane that cover the log; kYFirst = the 16-byte blocks of each
     // run loaded in the count/offset words' round (round 4's sweep, profiles/r04/k2y_first.txt:
@@ -666,95 +527,6 @@ hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int6
     if (g.nblk > 4 * kYThreads) return launch_y<8, 2>(scratch, g, cut.n_win, N, buckets, st);
     if (g.nblk > 2 * kYThreads) return launch_y<4, 5>(scratch, g, cut.n_win, N, buckets, st);
     return launch_y<2, 6>(scratch, g, cut.n_win, N, buckets, st);
-}
-
-HotBins hot_bins_geometry(int64_t B, int64_t N, int32_t W) {
-    HotBins g{};
-    int bb = 12;
-    while (((N + (1LL << bb) - 1) >> bb) > kMaxBins) ++bb;
-    g.bb = bb;
-    g.nbins = (int32_t)((N + (1LL << bb) - 1) >> bb);
-    int64_t chunk = (B + 1023) / 1024;
-    chunk = (chunk + kHT - 1) / kHT * kHT;
-    if (chunk < 4096) chunk = 4096;
-    g.chunk = chunk;
-    g.nchunks = (int32_t)((B + chunk - 1) / chunk);
-    g.splits = 8;
-    // usable when the per-bin histogram fits LDS
-    g.ok = N > 0 && B > 0 && bb <= 24 && (size_t)W * ((size_t)1 << bb) * 4 <= 128 * 1024;
-    return g;
-}
-
-hipError_t launch_hot_count_binned(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
-                                   const HotCutoffs& cut, uint32_t* buckets, const HotBins& g, uint32_t* chunk_cnt,
-                                   uint32_t* bin_tot, uint32_t* sorted, hipStream_t st) {
-    if (B <= 0 || cut.n_win <= 0 || N <= 0) return hipSuccess;
-    // dynamic LDS above 64 KiB must be opted into; k2d also has ~1 KiB of static LDS
-    static const hipError_t attr =
-        hipFuncSetAttribute((const void*)k2d_bin_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
-    if (attr != hipSuccess) return attr;
-    const size_t lds_bins = sizeof(uint32_t) * g.nbins;
-    hipError_t e = klaunch("k2a_bin_count", k2a_bin_count, dim3(g.nchunks), dim3(kHT), lds_bins, st, bnode, bts, B, N,
-                           cut, g, chunk_cnt);
-    if (e == hipSuccess)
-        e = klaunch("k2b_bin_scan", k2b_bin_scan, dim3(g.nbins), dim3(kHT), 0, st, chunk_cnt, g, bin_tot);
-    if (e == hipSuccess)
-        e = klaunch("k2c_scatter", k2c_scatter, dim3(g.nchunks), dim3(kHT), lds_bins, st, bnode, bts, B, N, cut, g,
-                    (const uint32_t*)chunk_cnt, (const uint32_t*)bin_tot, sorted);
-    const size_t lds_hist = sizeof(uint32_t) * (size_t)cut.n_win * ((size_t)1 << g.bb);
-    if (e == hipSuccess)
-        e = klaunch("k2d_bin_hist", k2d_bin_hist, dim3(g.nbins, g.splits), dim3(kHT), lds_hist, st,
-                    (const uint32_t*)sorted, (const uint32_t*)bin_tot, g, cut.n_win, N, buckets);
-    return e;
-}
-
-
-// ---------------------------------------------------------------- sliding windows (kernels.hpp)
-constexpr int kSlideThreads = 512;
-__device__ __forceinline__ void slide_body(const SlideArgs& a, int64_t b, int64_t nb) {
-    for (int64_t i = b * kSlideThreads + threadIdx.x; i < a.total; i += nb * kSlideThreads) {
-        int64_t off = i, p = -1;
-        for (int r = 0; r < a.nr; ++r) {  // (nr <= kMaxWin: the range holding flat index i)
-            if (p < 0 && off < a.len[r]) p = a.lo[r] + off;
-            off -= a.len[r];
-        }
-        int ro = 0, rn = 0;
-        for (int r = 0; r < a.W; ++r) {
-            ro += p >= a.s_old[r];
-            rn += p >= a.s_new[r];
-        }
-        if (ro == rn) continue;
-        const int32_t nd = a.bnode[p];
-        if (nd < 0 || (int64_t)nd >= a.N) continue;  // binding.go:85-91 counts known nodes only
-        if (ro > 0) atomicSub(&a.buckets[(int64_t)(ro - 1) * a.N + nd], 1u);
-        if (rn > 0) atomicAdd(&a.buckets[(int64_t)(rn - 1) * a.N + nd], 1u);
-    }
-}
-
-__global__ __launch_bounds__(kSlideThreads) void k2s_slide(SlideArgs a) {
-    slide_body(a, blockIdx.x, gridDim.x);
-}
-
-__global__ __launch_bounds__(kSlideThreads) void k2s_slide_pods(SlideArgs a, PodPrep pp) {
-    if ((int64_t)blockIdx.x < pp.ntiles) {  // the pod tiles first (dispatched first)
-        extern __shared__ __attribute__((aligned(16))) unsigned char k3p_lds[];
-        k3p_tile<kSlideThreads>((int64_t)blockIdx.x, pp, k3p_lds);
-    } else {
-        slide_body(a, (int64_t)blockIdx.x - pp.ntiles, (int64_t)gridDim.x - pp.ntiles);
-    }
-}
-
-hipError_t launch_hot_slide(const SlideArgs& a, hipStream_t st, const PodPrep* pods) {
-    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((a.total + kSlideThreads - 1) / kSlideThreads, 1024));
-    if (pods && pods->P > 0) {
-        static const hipError_t attr = hipFuncSetAttribute((const void*)k2s_slide_pods,
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kK3pLds);
-        if (attr != hipSuccess) return attr;
-        return klaunch("k2s_slide+k3p_pods", k2s_slide_pods, dim3((unsigned)(pods->ntiles + (a.total > 0 ? nb : 0))),
-                       dim3(kSlideThreads), kK3pLds, st, a, *pods);
-    }
-    if (a.total <= 0) return hipSuccess;
-    return klaunch("k2s_slide", k2s_slide, dim3((unsigned)nb), dim3(kSlideThreads), 0, st, a);
 }
 
 }  // namespace crane

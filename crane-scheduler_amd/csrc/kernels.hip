@@ -341,7 +341,7 @@ template <int PD, int PR>
 static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t st, int stream) {
     if (a.N <= 0) return hipSuccess;
     const int T = a.threads;
-    if (T != 128 && T != 256) return hipErrorInvalidValue;
+    if (T != 256) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((a.N + T - 1) / T);
     // + the sorted one-step records past the node records when both are kept (kernel above)
     // records: every node's when written out (+ the sorted one-step records past them); keys-only
@@ -354,11 +354,8 @@ static hipError_t launch_k1_t(const K1Args& a, const K1Step* step, hipStream_t s
     const char* nm = step ? "k1_node_pass+k3a_steps" : "k1_node_pass";
     if (step && stream && !a.out && a.hx_region == nullptr && T == 256)
         return launch_stream_steps(PD, PR, a, sa, st);
-    if (T == 256)
-        return step ? klaunch(nm, k1_node_pass<PD, PR, 256, true>, dim3(grid), dim3(256), lds, st, a, sa)
-                    : klaunch(nm, k1_node_pass<PD, PR, 256, false>, dim3(grid), dim3(256), lds, st, a, sa);
-    return step ? klaunch(nm, k1_node_pass<PD, PR, 128, true>, dim3(grid), dim3(128), lds, st, a, sa)
-                : klaunch(nm, k1_node_pass<PD, PR, 128, false>, dim3(grid), dim3(128), lds, st, a, sa);
+    return step ? klaunch(nm, k1_node_pass<PD, PR, 256, true>, dim3(grid), dim3(256), lds, st, a, sa)
+                : klaunch(nm, k1_node_pass<PD, PR, 256, false>, dim3(grid), dim3(256), lds, st, a, sa);
 }
 
 hipError_t launch_node_pass(int shape, const K1Args& a, hipStream_t st, const K1Step* step, int stream) {

@@ -83,8 +83,6 @@ struct MatrixArgs {
     int32_t score_i64;
     int32_t pad2;
     long long* keys;        // [P] or null: max-combined (atomicMax, keys must be initialised to -1)
-    int32_t matrix_vec;     // 0: automatic geometry; 1 / 4 / 8 nodes per lane (A/B)
-    int32_t matrix_chunk;   // 0: automatic; pods per workgroup (A/B)
     int8_t pred_orig[kMaxPred];  // device predicate -> policy predicate index
 };
 hipError_t launch_matrix(int shape, const MatrixArgs& a, hipStream_t st);
@@ -191,19 +189,6 @@ hipError_t launch_merge_assign(const int64_t* Fs, int64_t nF, const int64_t* Is,
                                hipStream_t st);
 
 // ---------------------------------------------------------------- K2 (hotcount.hip, kernels.hip)
-// Bin-partitioned K2 (four kernels, bucket matrix): the form for large node counts.
-constexpr int kMaxBins = 4096;
-struct HotBins {
-    int32_t bb;       // log2(nodes per bin)
-    int32_t nbins, nchunks, splits;
-    int64_t chunk;    // bindings per chunk workgroup
-    bool ok;          // per-bin histogram fits LDS
-};
-HotBins hot_bins_geometry(int64_t B, int64_t N, int32_t W);
-// scratch: chunk_cnt [nbins * nchunks], bin_tot [nbins], sorted [B]
-hipError_t launch_hot_count_binned(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
-                                   const HotCutoffs& cut, uint32_t* buckets, const HotBins& g, uint32_t* chunk_cnt,
-                                   uint32_t* bin_tot, uint32_t* sorted, hipStream_t st);
 // LDS-hash K2 (one kernel, global atomics into the bucket matrix): the fallback of any shape.
 hipError_t launch_hot_count(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N, const HotCutoffs& cut,
                             uint32_t* buckets, hipStream_t st);
@@ -215,7 +200,6 @@ struct HotPart {
     int64_t cap;        // region entries (nblk * reg)
     int32_t nblk;       // regions
     int32_t reg;        // bindings per region (the dedupe form: kHxRegion)
-    int32_t co_t;       // count/offset words [nbins][nblk] (large form option), else [nblk][nbins]
     bool ok;
     unsigned long long* trace;  // phase trace or null
 };
@@ -238,33 +222,17 @@ HotPart hot_dedupe_geometry(int64_t B, int64_t N, int32_t W, int32_t bs);
 size_t hot_dedupe_scratch(const HotPart& g);  // uint32 entries: regions + count/offset matrix
 hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                    const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
-                                   const PodPrep* pods = nullptr, int threads = 1024);
+                                   const PodPrep* pods = nullptr, int threads = 512);
 // Large form (past the dedupe form's cap): the same region pass with coarse bins of 2^bb
 // nodes (Y's LDS histogram [W][2^bb] <= kK2LargeHistBytes), then k2y_bin_hist writes the
 // dense window-rank buckets [W][N] (every row of every bin: K1 reads them, nothing to zero).
 // scratch: hot_dedupe_scratch(g) words.
 constexpr int64_t kK2LargeHistBytes = 128 * 1024;
-HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W, int32_t reg, int32_t co_t);
+constexpr int32_t kK2lRegion = 4096;  // large form: bindings per region
+HotPart hot_large_geometry(int64_t B, int64_t N, int32_t W);
 hipError_t launch_hot_count_large(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                   const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, uint32_t* buckets,
-                                  int n_cu, hipStream_t st, int threads = 512);
-
-// Sliding windows on a time-ordered log (round 5): the dense window-rank buckets [W][N] of the
-// previous refresh, whose window suffixes started at positions s_old[r], moved to the cutoffs'
-// new starts s_new[r]: only the bindings between an old and a new start change rank — each
-// leaves its old bucket and joins its new one (rank = #{r : p >= s[r]}, bucket rank - 1, rank 0
-// counted nowhere).  ranges: the disjoint union of [min(s_old, s_new), max(s_old, s_new)) per
-// rank (nr <= kMaxWin).  With pods, K3p's tiles ride as the launch's first workgroups.
-struct SlideArgs {
-    const int32_t* bnode;
-    int64_t N;
-    int32_t W, nr;
-    int64_t s_old[kMaxWin], s_new[kMaxWin];
-    int64_t lo[kMaxWin], len[kMaxWin];  // the ranges
-    int64_t total;                      // their summed length
-    uint32_t* buckets;
-};
-hipError_t launch_hot_slide(const SlideArgs& a, hipStream_t st, const PodPrep* pods = nullptr);
+                                  int n_cu, hipStream_t st, int threads = 1024);
 
 // ---------------------------------------------------------------- K3 step path (step.hip)
 constexpr int kStepSeg = 256;                 // nodes per segment (K3a workgroup)
@@ -377,7 +345,7 @@ struct K1Args {
     const uint32_t* hx_region;
     const uint32_t* hx_CO;
     int32_t hx_nblk;
-    int32_t threads;        // workgroup size: 128 or 256
+    int32_t threads;        // workgroup size: 256
     unsigned long long* trace;  // phase trace or null
 };
 // step (optional): also build the K3 step tables of a pod batch (K3a fused).  stream: with step,

@@ -66,7 +66,7 @@ __device__ __forceinline__ void store_bytes(int8_t* p, const uint32_t* w) {
 template <int PD, int PR, int VEC, bool I64, bool OUT, bool KEYS>
 __global__ __launch_bounds__(kMxT) void k3m_matrix(MatrixArgs a, int32_t chunk, int32_t nbx, int32_t per,
                                                    int32_t ncy) {
-    static_assert(VEC == 1 || VEC == 4 || VEC == 8 || VEC == 16, "byte, dword, dwordx2 or dwordx4 stores");
+    static_assert(VEC == 1 || VEC == 4 || VEC == 8, "byte, dword or dwordx2 stores");
     static_assert(!I64 || VEC == 1, "int64 scores: one node per lane");
     constexpr int NW = (VEC + 3) / 4;  // packed words per lane
     __shared__ int32_t best[KEYS ? kMxChunk : 1];
@@ -249,11 +249,9 @@ static MatrixGeometry matrix_geometry(const MatrixArgs& a, bool out) {
             break;
         }
     }
-    if (a.matrix_vec && aligned(a.matrix_vec)) g.vec = a.matrix_vec;  // A/B override (crane_dyn_set_option)
     int64_t chunk = std::max<int64_t>(1, ppw / (64 * g.vec));
     if (g.vec >= 8) chunk *= 4;
     if (chunk >= 64) chunk = std::min<int64_t>(kMxChunk, (chunk + 63) / 64 * 64);
-    if (a.matrix_chunk > 0) chunk = std::min<int64_t>(kMxChunk, a.matrix_chunk);
     g.chunk = std::min(chunk, a.P);
     g.nbx = (a.N + kMxT * g.vec - 1) / (kMxT * g.vec);
     g.ncy = (a.P + g.chunk - 1) / g.chunk;
@@ -289,7 +287,6 @@ static hipError_t launch_matrix_t(const MatrixArgs& a, hipStream_t st) {
     const MatrixGeometry g = matrix_geometry(a, out);
     if (g.nbx > 0x7FFFFFFF / 8 || g.ncy > 0x7FFFFFFF) return hipErrorInvalidValue;
     switch (g.vec) {
-        case 16: return launch_vec<PD, PR, 16>(a, g, out, keys, st);
         case 8: return launch_vec<PD, PR, 8>(a, g, out, keys, st);
         case 4: return launch_vec<PD, PR, 4>(a, g, out, keys, st);
         default: return launch_vec<PD, PR, 1>(a, g, out, keys, st);

@@ -340,19 +340,15 @@ int64_t crane_dyn_key_node(int64_t key, int64_t *score);
 const char *crane_dyn_version(void);
 
 /* Alternative kernel forms of the same results, for tests and A/B tools:
- *   "k2_form" 0 dedupe (default; large past its cap) | 1 binned | 2 hash | 3 large   "k1_threads" 256 | 128
- *   "k1_keep_records" 0 | 1   "k1_fuse_steps" 1 | 0   "k3p_in_k2" 1 | 0
-  *   "k2_sorted" 1 a time-ordered log (checked at upload): K2 reads the widest window's suffix only | 0 never
-  *   "k2_slide" 0 recount every refresh | 1 keep dense window counts and move them by the bindings between
-  *     the last refresh's window starts and this one's (time-ordered log; slower at large shifts)
-  *   "k1_stream" 1 the streamed step pass without dedupe-form K2 entries | 0 the record-holding fused pass
-  *   "k1_tail" 0 its tail on one wave when the grid has >= 4096 blocks | 1 always | 4 on all four waves
-  *   "keys_path" 0 step path | 1 per-pair kernel   "greedy_form" 0 merge | 1 sequential
- *   "matrix_vec" 0 auto | 1 | 4 | 8 | 16 nodes per lane   "matrix_chunk" 0 auto | pods per workgroup (<= 1024)
+ *   "k2_form" 0 dedupe (default; the large form past its count/offset cap, the atomics form past the
+ *     large form's) | 2 atomics (LDS hash + global atomics, any shape) | 3 large
+ *   "k2_sorted" 1 a time-ordered log (checked at upload): K2 reads the widest window's suffix only | 0 never
+ *   "k1_stream" 1 the streamed step pass without dedupe-form K2 entries | 0 the record-holding fused pass
+ *   "k1_tail" 0 its tail on one wave when the grid has >= 4096 blocks | 1 always | 4 on all four waves
+ *   "keys_path" 0 step path | 1 per-pair kernel   "greedy_form" 0 merge | 1 sequential
  *   "step_rows" 1 producers index the records per pod tile | 0 K3s searches them
- *   "k3s_blocks" 0 auto | producer blocks per K3s workgroup aimed for (1..256)
- *   "k2x_threads" 512 | 1024 | 256: dedupe K2 workgroup size
- *   "k2l_region" 4096 | 2048: large K2 bindings per region   "k2l_co_t" 0 | 1: its count/offset layout
+ *   "step_pieces" 0 auto | 1 | 2: middle pieces cut into elementary ones when it pays | always | never
+ *   "step_lds_cap" one-step records per kind staged in K1's LDS at most (0: all through device memory)
  *   "sel_chain" 0 LDS rank/select walk of the selection windows (N <= 131072) | 1 streaming kernel
  *   "trace" 0 | 1: phase stamps of the step kernels (crane_dyn_debug_trace) */
 int crane_dyn_set_option(crane_dyn *h, const char *name, int64_t value);

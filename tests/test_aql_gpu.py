@@ -70,13 +70,10 @@ def test_queue_step_equals_stream_and_oracle():
 
 
 @pytest.mark.parametrize("opts", [
-    (("k2_form", 3),),            # large-form K2 (two kernels, dense buckets)
-    (("k2_form", 1),),            # binned K2: a bucket fill between packets (engine stream, waited for)
+    (("k2_form", 3),),            # large-form K2 (two kernels, dense buckets; K3p its own launch)
+    (("k2_form", 2),),            # atomics K2: a bucket fill between packets (engine stream, waited for)
     (("k1_stream", 0),),          # the record-holding fused node pass
-    (("k3p_in_k2", 0),),          # K3p as its own launch
-    (("k2_slide", 1),),           # sliding windows after the first refresh
     (("keys_path", 1),),          # per-pair kernel: fills and copies, run on the engine stream
-    (("k1_fuse_steps", 0),),      # stand-alone K3a
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o))
 def test_queue_kernel_forms(opts):
     _, c, engs, dev = _setup(5000, 1500, 40000, 20250302, opts)

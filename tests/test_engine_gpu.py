@@ -142,7 +142,7 @@ def test_hot_values_vs_oracle(kats):
     assert sc[0, 0] == 50  # hv = 5 (SURVEY KAT-11)
 
 
-@pytest.mark.parametrize("k2", [0, 1, 2, 3], ids=["dedupe", "binned", "hash", "large"])
+@pytest.mark.parametrize("k2", [0, 2, 3], ids=["dedupe", "atomics", "large"])
 @pytest.mark.parametrize("n_nodes,n_bind,seed", [(1000, 50_000, 1), (20_000, 300_000, 2), (100, 10, 3),
                                                  (70_000, 2_000_000, 4), (40_000, 5_000_000, 5)])
 def test_hot_values_random(n_nodes, n_bind, seed, k2):
@@ -209,14 +209,13 @@ def test_hot_values_time_ordered_log(order, k2):
     eng.close()
 
 
-@pytest.mark.parametrize("threads,k2x,k2", [(128, 512, 0), (256, 512, 0), (256, 1024, 0), (256, 256, 0),
-                                            (256, 4096, 3), (256, 2048, 3), (256, -4096, 3)])
+@pytest.mark.parametrize("k2", [0, 3, 2], ids=["dedupe", "large", "atomics"])
 @pytest.mark.parametrize("case", ["one_hot_node", "eight_windows", "last_node", "odd_counts"])
-def test_hot_values_dedupe_edges(case, threads, k2x, k2):
+def test_hot_values_dedupe_edges(case, k2):
     """Dedupe-form K2 (per-workgroup (node, bucket) aggregation, counts read by the
     node pass) at its packing limits: a region whose 2048 bindings all hit one node
     (count field), eight windows (bucket field), the shard's last node and bindings
-    past the shard; 128- and 256-node bins.  odd_counts: hotValue.count negative
+    past the shard; the large form's and the atomics form's the same.  odd_counts: hotValue.count negative
     and past 32 bits (the node pass divides in u32 only when both operands fit;
     Go's int64 division truncates toward zero otherwise, node.go:117)."""
     m = 60 * 10**9
@@ -235,9 +234,7 @@ def test_hot_values_dedupe_edges(case, threads, k2x, k2):
         bn[::3] = n_nodes - 1
         bn[1::7] = n_nodes  # past the shard: ignored
         bn[2::11] = -3
-    # (k2 = 3: the large form; k2x = its region size, negative = count/offset words [bin][region])
-    opts = {"k2_form": k2, "k1_threads": threads}
-    opts.update({"k2l_region": abs(k2x), "k2l_co_t": int(k2x < 0)} if k2 == 3 else {"k2x_threads": k2x})
+    opts = {"k2_form": k2}
     eng = engine_for(spec, c, opts=opts)
     eng.upload_bindings(bn, c.b_ts)
     now = int(c.now[0])
@@ -256,7 +253,7 @@ def test_hot_values_dedupe_edges(case, threads, k2x, k2):
 def test_hot_values_large_form_16m():
     """The cold-leg size (4M nodes x 16M bindings), where the dedupe form's count/offset
     matrix passes its cap and the large form runs by default: hot values equal the oracle's
-    (binding.go:81-97, node.go:113-121) and the binned form's, before and after a K1 pass
+    (binding.go:81-97, node.go:113-121) and the atomics form's, before and after a K1 pass
     consumed them; a pod sample's Filter/Score/argmax equals the oracle over all 4M nodes."""
     spec = cd.default_policy_spec()
     N, B = 4_000_000, 16_000_000
@@ -283,7 +280,7 @@ def test_hot_values_large_form_16m():
         eng.set_option("k2_sorted", srt)
         eng.refresh_hot_values(now, now)
         assert np.array_equal(eng.hot_values(), ref), srt
-    eng.set_option("k2_form", 1)
+    eng.set_option("k2_form", 2)
     eng.refresh_hot_values(now, now)
     assert np.array_equal(eng.hot_values(), ref)
     eng.set_option("k2_form", 0)

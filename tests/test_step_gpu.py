@@ -183,15 +183,15 @@ def test_hot_values_kept_after_consumption():
     assert np.array_equal(ff, off) and np.array_equal(sc, osc)
 
 
-@pytest.mark.parametrize("ride,pods", [(1, 5000), (0, 5000), (1, 1), (1, 300), (1, 2048)])
-def test_step_keys_async_matches_oracle(ride, pods):
-    """crane_dyn_step_keys_async replayed (K3p riding in K2x's launch or in its own):
+@pytest.mark.parametrize("pods", [5000, 1, 300, 2048])
+def test_step_keys_async_matches_oracle(pods):
+    """crane_dyn_step_keys_async replayed (K3p riding in K2x's launch):
     each step equals the oracle with binding-log hot values; with kernel timing on
     too (dispatch-stamped events name every kernel of the step)."""
     import torch
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 30000, pods, n_bindings=300_000, seed=27, pod_step_ns=2_000_000, ds_frac=0.02)
-    eng = engine_for(spec, c, opts={"k3p_in_k2": ride})
+    eng = engine_for(spec, c)
     eng.upload_bindings(c.b_node, c.b_ts)
     now = int(synth.NOW0_NS)
     dev = torch.device("cuda", 0)
@@ -209,53 +209,14 @@ def test_step_keys_async_matches_oracle(ride, pods):
             assert np.array_equal(ch, och), rep
     times = eng.stage_times()
     names = [n for n, _ in times]
-    if ride:
-        assert names == ["k2x_dedupe+k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
-    else:
-        assert names == ["k2x_dedupe", "k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
+    assert names == ["k2x_dedupe+k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
     assert all(0 < t < 50 for _, t in times), times
 
 
-@pytest.mark.parametrize("W,n_nodes,n_bind", [(2, 20000, 300_000), (3, 5000, 100_000)])
-def test_step_sliding_windows(W, n_nodes, n_bind):
-    """Option k2_slide: the dense window counts moved between refreshes (batches advancing,
-    retreating, jumping past half the log, repeated) equal the oracle's hot values at each
-    `now`, through the whole step; the first refresh and the big jump recount (large form)."""
-    import torch
-    spec = cd.default_policy_spec()
-    if W == 3:
-        spec = dict(spec, hotValue=list(spec["hotValue"]) + [(120_000_000_000, 3)])
-    c = synth.make_cluster(spec, n_nodes, 2000, n_bindings=n_bind, seed=31 + W, pod_step_ns=2_000_000, ds_frac=0.02)
-    eng = engine_for(spec, c, opts={"k2_slide": 1})
-    eng.upload_bindings(c.b_node, c.b_ts)
-    dev = torch.device("cuda", 0)
-    st = torch.cuda.Stream(dev)
-    d_flags = torch.from_numpy(c.ds).to(dev)
-    d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
-    t0 = int(synth.NOW0_NS)
-    names = []
-    with torch.cuda.stream(st):
-        for i, dt_s in enumerate((0, 10, 20, 5, 5, 400, 410, -30, 0)):
-            now = t0 + dt_s * 10**9
-            pods_now = c.now + dt_s * 10**9
-            d_now = torch.from_numpy(pods_now).to(dev)
-            eng.set_profiling(True)
-            eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
-            st.synchronize()
-            names.append([n for n, _ in eng.stage_times()][0])
-            ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
-            c.now, saved = pods_now, c.now  # (the oracle's pods at this batch's times)
-            _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=_oracle_hv(spec, c, now))
-            c.now = saved
-            assert np.array_equal(ch, och), (i, dt_s)
-    assert any(n.startswith("k2s_slide") for n in names), names
-    assert any(n.startswith("k2l_partition") for n in names), names
-
-
-@pytest.mark.parametrize("k2", [0, 1, 2, 3], ids=["dedupe", "binned", "hash", "large"])
+@pytest.mark.parametrize("k2", [0, 2, 3], ids=["dedupe", "atomics", "large"])
 def test_step_keys_async_k2_forms(k2):
     """The combined step with each K2 form (dedupe: counts consumed by the fused node
-    pass from per-block entries; binned / hash / large: buckets) equals the oracle, replayed."""
+    pass from per-block entries; atomics / large: buckets; K3p its own launch) equals the oracle, replayed."""
     import torch
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 20000, 3000, n_bindings=400_000, seed=29, pod_step_ns=2_000_000, ds_frac=0.03)
@@ -280,15 +241,13 @@ def test_step_keys_async_k2_forms(k2):
     assert ("k1_node_pass+k3a_steps" if k2 == 0 else "k1_stream_steps") in names, names
 
 
-@pytest.mark.parametrize("keep", [0, 1])
-def test_records_rebuilt_after_keys_step(keep):
-    """The fused keys-only step does not write the node records (option
-    k1_keep_records does): a matrix eval and a greedy pass after it rebuild them from
+def test_records_rebuilt_after_keys_step():
+    """The fused keys-only step does not write the node records: a matrix eval and a greedy pass after it rebuild them from
     the kept binding-log hot values and still equal the oracle."""
     import torch
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 4000, 700, n_bindings=50_000, seed=28, pod_step_ns=3_000_000, ds_frac=0.05)
-    eng = engine_for(spec, c, opts={"k1_keep_records": keep})
+    eng = engine_for(spec, c)
     eng.upload_bindings(c.b_node, c.b_ts)
     now = int(synth.NOW0_NS)
     dev = torch.device("cuda", 0)
