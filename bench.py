@@ -215,7 +215,8 @@ def parse():
     ap.add_argument("--inflight", type=int, default=4,
                     help="independent pod batches in flight (engines x HIP streams); 1 = one batch at a time")
     ap.add_argument("--ar-group", type=int, default=0,
-                    help="N>1: batches per keys all-reduce (a multiple of --inflight; 0 = 16 x inflight)")
+                    help="with the collective: batches per keys all-reduce (ranks: a multiple of --inflight, 0 = "
+                         "16 x inflight; group: 0 = min(steps, 64))")
     ap.add_argument("--rehearse-collective", action="store_true",
                     help="run the ranks path's N>1 collective on one rank (under torchrun)")
     ap.add_argument("--no-extras", action="store_true", help="headline step only (matrix / drop-in / controller legs off)")
@@ -230,7 +231,8 @@ def parse():
                     help="group engine: -1 auto (a worker per device when n > 1), 0 the caller's thread, 1 workers")
     ap.add_argument("--group-dispatch", type=int, default=-1, choices=(-1, 0, 1),
                     help="group engine: 1 the steps' kernels as AQL packets on dispatch queues (crane_queue), "
-                         "0 HIP launches on the slots' streams, -1 auto (queues unless the collective runs)")
+                         "0 HIP launches on the slots' streams, -1 auto (queues; with the collective the batch form "
+                         "orders one all-reduce per window of batches after them)")
     ap.add_argument("--engine", default="group", choices=("group", "ranks"),
                     help="group: one process drives every GPU through the C ABI group (crane_dyn_group_*, "
                          "in-library RCCL); ranks: one process per GPU under torch.distributed (comparison)")
@@ -1021,7 +1023,7 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
     grp.set_option("collective", args.group_collective)
     grp.set_option("threads", args.group_threads)
     coll_on = args.group_collective == 2 or (args.group_collective == 1 and n_dev > 1)
-    dispatch = args.group_dispatch if args.group_dispatch >= 0 else (0 if coll_on else 1)
+    dispatch = args.group_dispatch if args.group_dispatch >= 0 else 1
     grp.set_option("dispatch", dispatch)
     for o in args.opt:  # engine options (name=value) on every slot's engines
         k, v = o.split("=")
@@ -1035,15 +1037,48 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
     d_now = [[torch.from_numpy(p).to(dv) for dv in devs] for p in pods]
     d_flags = [torch.from_numpy(g_all.ds).to(dv) for dv in devs]
     d_keys = [[torch.empty(P, dtype=torch.int64, device=dv) for dv in devs] for _ in range(K)]
-    fns = [[grp.step_keys_fn(d_now[t], d_flags, d_keys[s]) for t in range(C)] for s in range(K)]
     seq = [0]  # batches enqueued on the group so far: batch b runs on slot b % K
-    slot_t = [None] * K  # the batch time (cycle position) of each slot's latest batch
+    recent = []  # (keys getter, cycle position) of the latest batches, newest last
+    if not coll_on:
+        # one batch per call (crane_dyn_group_step_keys_async), each slot its key buffer
+        fns = [[grp.step_keys_fn(d_now[t], d_flags, d_keys[s]) for t in range(C)] for s in range(K)]
+        G = 1
 
-    def step(i):
-        t = i % C
-        fns[seq[0] % K][t](nows[t], nows[t])
-        slot_t[seq[0] % K] = t
-        seq[0] += 1
+        def step(i):
+            t = i % C
+            s_ = seq[0] % K
+            fns[s_][t](nows[t], nows[t])
+            recent.append((lambda s_=s_: d_keys[s_][0], t))
+            del recent[:-2]
+            seq[0] += 1
+    else:
+        # the collective: windows of G batches per call (crane_dyn_group_step_keys_batch), ONE
+        # all-reduce of a window's keys [G][P] per device, two key buffers alternating
+        G = max(1, args.ar_group or min(args.steps, 64))
+        gdn = {}  # (first cycle position, rows) -> per-device pod times [rows][P]
+        gfl = [torch.from_numpy(np.tile(g_all.ds, (G, 1))).to(dv) for dv in devs]
+        gkeys = [[torch.empty((G, P), dtype=torch.int64, device=dv) for dv in devs] for _ in range(2)]
+        gfns = {}
+        win = [0]
+
+        def window(i0, rows):
+            key = (i0 % C, rows)
+            if key not in gdn:
+                gdn[key] = [torch.from_numpy(np.stack([pods[(i0 + j) % C] for j in range(rows)])).to(dv) for dv in devs]
+            b = win[0] % 2
+            fk = (key, b)
+            if fk not in gfns:
+                gfns[fk] = grp.step_keys_batch_fn(gdn[key], [f[:rows] for f in gfl], [k[:rows] for k in gkeys[b]])
+            ts_ = [nows[(i0 + j) % C] for j in range(rows)]
+            gfns[fk](ts_, ts_)
+            for j in range(max(0, rows - 2), rows):
+                recent.append((lambda b=b, j=j: gkeys[b][0][j], (i0 + j) % C))
+            del recent[:-2]
+            seq[0] += rows
+            win[0] += 1
+
+        def step(i):  # (a one-batch window: warmup and the latency loop)
+            window(i, 1)
 
     def sync_all():
         grp.sync()
@@ -1063,35 +1098,49 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
         step(0)
     for i in range(1, args.warmup):
         step(i)
+    if coll_on:  # (every window shape of the timed region once, untimed: RCCL sets up per size)
+        for rows in sorted({G, args.steps % G or G}):
+            window(0, rows)
+            window(0, rows)
     sync_all()
     cpu0 = task_cpu()
     t0 = time.perf_counter()
     tc0 = time.thread_time()
-    for i in range(args.steps):
-        step(i)
+    if coll_on:
+        for i0 in range(0, args.steps, G):
+            window(i0, min(G, args.steps - i0))
+    else:
+        for i in range(args.steps):
+            step(i)
     t_enq = time.perf_counter() - t0
     tc_enq = time.thread_time() - tc0
     grp.sync()
     elapsed = time.perf_counter() - t0
     host = host_threads(cpu0, task_cpu(), t_enq, tc_enq, elapsed, args.steps)
-    t_last, s_last = (args.steps - 1) % C, (seq[0] - 1) % K
-    last = d_keys[s_last]
-    keys = last[0].cpu().numpy()
-    keys_agree = all(torch.equal(last[0].cpu(), k.cpu()) for k in last[1:]) if n_dev > 1 else None
+    t_last = (args.steps - 1) % C
+    last_get, _ = recent[-1]
+    keys = last_get().cpu().numpy()
+    if n_dev > 1:  # every device holds the all-reduced keys
+        keys_agree = True
+        if coll_on:
+            b_last = (win[0] - 1) % 2
+            row = (args.steps - 1) % G
+            keys_agree = all(torch.equal(gkeys[b_last][0][row].cpu(), gkeys[b_last][d][row].cpu())
+                             for d in range(1, n_dev))
+    else:
+        keys_agree = None
     # the timed path pinned at full size: the last timed batch and the one before it (another slot,
     # another `now`: the cutoffs moved between them) against one engine over the whole cluster on a
     # HIP stream and against the CPU oracle on a pod sample (checker only, after the timed region)
     pinned = []
-    for s_ in sorted({s_last, (s_last - 1) % K}, key=lambda x: x != s_last):
-        t_ = slot_t[s_]
+    for get_, t_ in reversed(recent):
         ref_k, _ = keys_one_engine(cd, synth, spec, devs[0], lambda: g_all, d_now[t_][0], d_flags[0], nows[t_])
-        got = d_keys[s_][0].cpu().numpy()
-        pinned.append({"slot": s_, "now_ns": int(nows[t_]), "stream": bool(np.array_equal(ref_k.cpu().numpy(), got)),
+        got = get_().cpu().numpy()
+        pinned.append({"now_ns": int(nows[t_]), "stream": bool(np.array_equal(ref_k.cpu().numpy(), got)),
                        **oracle_sample(spec, g_all, grp.metric_names, pods[t_], nows[t_], got)})
     keys_match, keys_match_how = None, "one device: no combine step"
     if n_dev > 1:
-        ref_k, _ = keys_one_engine(cd, synth, spec, devs[0], lambda: g_all, d_now[t_last][0], d_flags[0], nows[t_last])
-        keys_match = bool(torch.equal(ref_k.cpu(), last[0].cpu()))
+        keys_match = pinned[0]["stream"] and bool(keys_agree)
         keys_match_how = ("the last batch's all-reduced keys on every device == one engine holding the whole "
                           f"{n_total}-node global cluster and its binding log, same pods")
     elif strong:
@@ -1104,7 +1153,7 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
     nl = max(10, args.steps // 4)
     t1 = time.perf_counter()
     for i in range(nl):
-        step(i)
+        step(i)  # (with the collective: a one-batch window and its all-reduce)
         grp.sync()
     batch_latency_ms = (time.perf_counter() - t1) * 1e3 / nl
     # per-kernel durations: shard 0's engine of slot 0 stepping the same batch on its own stream
@@ -1120,10 +1169,12 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
              keys=keys, keys_agree=keys_agree, keys_match=keys_match, keys_match_how=keys_match_how, host=host,
              pinned=pinned, batch_latency_ms=batch_latency_ms, kt=kt, ar_ms=None, K=K, nows=nows, span=span, stream=st0,
              how=(f"one process, crane_dyn_group over {n_dev} device(s) (C ABI, group.cpp): {K} batch slots, each "
-                  "with an engine per device (own copy of its shard) on its own HIP stream, batch i on slot i % K; "
-                  "every batch runs the whole shard step on every device" +
-                  ("; then an in-place RCCL ncclAllReduce(int64, max) of its keys on each device's stream "
-                   "(ncclCommInitAll communicators)" if coll else "") +
+                  "with an engine per device (the slots of a device share one copy of its shard's nodes and log) "
+                  "on its own stream or dispatch queue, batch i on slot i % K; every batch runs the whole shard "
+                  "step on every device" +
+                  (f"; windows of {G} batches (crane_dyn_group_step_keys_batch), then ONE in-place RCCL "
+                   f"ncclAllReduce(int64, max) of a window's keys [{G}][P] per device on a collective stream "
+                   "ordered after the dispatch queues (ncclCommInitAll communicators)" if coll else "") +
                   ("; enqueued by one worker thread per device" if workers else "; enqueued by the caller's thread") +
                   ("; the step's kernels written as AQL packets to one user-mode queue per slot (crane_queue: "
                    "~0.3 us per kernel instead of a HIP launch's 2.6-3.7 us)" if dispatch else

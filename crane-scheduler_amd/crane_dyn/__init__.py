@@ -116,6 +116,18 @@ def _load():
         "crane_dyn_group_step_keys_async": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp]),
         "crane_dyn_group_sync": (C.c_int, [vp]),
         "crane_dyn_group_schedule": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp, vp]),
+        "crane_dyn_group_step_keys_batch": (C.c_int, [vp, C.c_int32, vp, vp, C.c_int64, vp, vp, vp]),
+        "crane_dyn_group_update_nodes": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp]),
+        "crane_dyn_group_update_node_steps": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, C.c_int64, C.c_int64,
+                                                        vp, vp, vp, vp]),
+        "crane_dyn_group_resize_nodes": (C.c_int, [vp, C.c_int64]),
+        "crane_dyn_group_binding_records": (C.c_int, [vp, C.c_int64, C.c_int64]),
+        "crane_dyn_group_add_bindings": (C.c_int, [vp, C.c_int64, vp, vp]),
+        "crane_dyn_group_gc_bindings": (C.c_int, [vp, C.c_int64]),
+        "crane_dyn_group_binding_count": (C.c_int64, [vp]),
+        "crane_dyn_group_refresh_hot_values": (C.c_int, [vp, C.c_int64, C.c_int64]),
+        "crane_dyn_group_hot_values": (C.c_int, [vp, C.c_int64, vp]),
+        "crane_dyn_group_node_steps": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp, vp]),
         "crane_queue_create": (C.c_int, [C.c_int32, C.c_int32, P(vp)]),
         "crane_queue_wait": (C.c_int, [vp]),
         "crane_queue_last_error": (C.c_char_p, [vp]),
@@ -150,6 +162,10 @@ ABI_SYMBOLS = (
     "crane_dyn_group_last_error", "crane_dyn_group_set_option", "crane_dyn_group_size", "crane_dyn_group_shard",
     "crane_dyn_group_engine", "crane_dyn_group_upload_nodes", "crane_dyn_group_upload_bindings",
     "crane_dyn_group_step_keys_async", "crane_dyn_group_sync", "crane_dyn_group_schedule",
+    "crane_dyn_group_step_keys_batch", "crane_dyn_group_update_nodes", "crane_dyn_group_update_node_steps",
+    "crane_dyn_group_resize_nodes", "crane_dyn_group_binding_records", "crane_dyn_group_add_bindings",
+    "crane_dyn_group_gc_bindings", "crane_dyn_group_binding_count", "crane_dyn_group_refresh_hot_values",
+    "crane_dyn_group_hot_values", "crane_dyn_group_node_steps",
     "crane_queue_create", "crane_queue_wait", "crane_queue_last_error", "crane_queue_destroy",
     "crane_dyn_step_keys_queue", "crane_dyn_forget_queue",
 )
@@ -786,8 +802,104 @@ class Group:
     def step_keys_async(self, now_ns, hv_ts_ns, d_now, d_flags, d_keys):
         self.step_keys_fn(d_now, d_flags, d_keys)(int(now_ns), int(hv_ts_ns))
 
+    def step_keys_batch_fn(self, d_now, d_flags, d_keys):
+        """crane_dyn_group_step_keys_batch bound to per-device torch tensors [G][P] (lists, one per
+        device; d_flags None or [G][P] per device): returns f(now_ns[G], hv_ts_ns[G])."""
+        G, P = d_now[0].shape
+        pn, pk = self._ptrs(d_now), self._ptrs(d_keys)
+        pf = None if d_flags is None else self._ptrs(d_flags)
+        fn, h, check = lib.crane_dyn_group_step_keys_batch, self.h, self._check
+        an, ak = C.cast(pn, C.c_void_p), C.cast(pk, C.c_void_p)
+        af = None if pf is None else C.cast(pf, C.c_void_p)
+        tn, th = (C.c_int64 * G)(), (C.c_int64 * G)()
+        keep = (pn, pk, pf, tn, th)
+
+        def step(now_ns, hv_ts_ns):
+            _ = keep
+            for b in range(G):
+                tn[b], th[b] = int(now_ns[b]), int(hv_ts_ns[b])
+            rc = fn(h, G, C.cast(tn, C.c_void_p), C.cast(th, C.c_void_p), P, an, af, ak)
+            if rc:
+                check(rc)
+
+        return step
+
+    def step_keys_batch(self, now_ns, hv_ts_ns, d_now, d_flags, d_keys):
+        self.step_keys_batch_fn(d_now, d_flags, d_keys)(now_ns, hv_ts_ns)
+
     def sync(self):
         self._check(lib.crane_dyn_group_sync(self.h))
+
+    # -- shard state changes, by global node index (routed to the owning shard)
+    def update_nodes(self, idx, val, ts, hv=None, hv_ts=None):
+        idx = np.ascontiguousarray(idx, np.int64)
+        k, M = len(idx), len(self.metric_names)
+        val = np.ascontiguousarray(val, np.float64).reshape(M, k)
+        ts = np.ascontiguousarray(ts, np.int64).reshape(M, k)
+        if hv is not None:
+            hv = np.ascontiguousarray(hv, np.float64).reshape(k)
+            hv_ts = np.ascontiguousarray(hv_ts, np.int64).reshape(k)
+        self._check(lib.crane_dyn_group_update_nodes(self.h, len(idx), _ptr(idx), _ptr(val), _ptr(ts), _ptr(hv),
+                                                     _ptr(hv_ts)))
+
+    def update_node_steps(self, idx, val, ts, hv, hv_ts, t0_ns, t1_ns):
+        idx = np.ascontiguousarray(idx, np.int64)
+        k, M = len(idx), len(self.metric_names)
+        val = np.ascontiguousarray(val, np.float64).reshape(M, k)
+        ts = np.ascontiguousarray(ts, np.int64).reshape(M, k)
+        if hv is not None:
+            hv = np.ascontiguousarray(hv, np.float64).reshape(k)
+            hv_ts = np.ascontiguousarray(hv_ts, np.int64).reshape(k)
+        S = lib.crane_dyn_step_slots(lib.crane_dyn_group_engine(self.h, 0, 0))
+        ns = np.zeros(k, np.uint8)
+        bp = np.zeros((k, S), np.int64)
+        ff = np.zeros((k, S + 1), np.int8)
+        sc = np.zeros((k, S + 1), np.int8)
+        self._check(lib.crane_dyn_group_update_node_steps(self.h, k, _ptr(idx), _ptr(val), _ptr(ts), _ptr(hv),
+                                                          _ptr(hv_ts), int(t0_ns), int(t1_ns), _ptr(ns), _ptr(bp),
+                                                          _ptr(ff), _ptr(sc)))
+        return ns, bp, ff, sc
+
+    def resize_nodes(self, n):
+        self._check(lib.crane_dyn_group_resize_nodes(self.h, int(n)))
+        self.n_nodes = int(n)
+
+    def binding_records(self, size, gc_time_range_ns):
+        self._check(lib.crane_dyn_group_binding_records(self.h, int(size), int(gc_time_range_ns)))
+
+    def add_bindings(self, node, ts_s):
+        node = np.ascontiguousarray(node, np.int32)
+        ts_s = np.ascontiguousarray(ts_s, np.int64)
+        self._check(lib.crane_dyn_group_add_bindings(self.h, len(node), _ptr(node), _ptr(ts_s)))
+
+    def gc_bindings(self, now_ns):
+        self._check(lib.crane_dyn_group_gc_bindings(self.h, int(now_ns)))
+
+    def binding_count(self):
+        n = lib.crane_dyn_group_binding_count(self.h)
+        if n < 0:
+            self._check(n)
+        return n
+
+    def refresh_hot_values(self, now_ns, hv_ts_ns):
+        self._check(lib.crane_dyn_group_refresh_hot_values(self.h, int(now_ns), int(hv_ts_ns)))
+
+    def hot_values(self):
+        out = np.empty(self.n_nodes, np.float64)
+        self._check(lib.crane_dyn_group_hot_values(self.h, self.n_nodes, _ptr(out)))
+        return out
+
+    def node_steps(self, t0_ns, t1_ns):
+        """Every node's answer rows over [t0, t1): (n_steps [N], bp [N][S], first_fail [N][S+1], score [N][S+1])."""
+        S = lib.crane_dyn_step_slots(lib.crane_dyn_group_engine(self.h, 0, 0))
+        N = self.n_nodes
+        ns = np.zeros(N, np.uint8)
+        bp = np.zeros((N, S), np.int64)
+        ff = np.zeros((N, S + 1), np.int8)
+        sc = np.zeros((N, S + 1), np.int8)
+        self._check(lib.crane_dyn_group_node_steps(self.h, int(t0_ns), int(t1_ns), N, _ptr(ns), _ptr(bp), _ptr(ff),
+                                                   _ptr(sc)))
+        return ns, bp, ff, sc
 
     def schedule(self, now_ns, hv_ts_ns, pods_now, pod_flags=None):
         """One batch from host arrays: (chosen global node [P], chosen score [P])."""

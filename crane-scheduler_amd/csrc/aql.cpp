@@ -167,6 +167,13 @@ __global__ void k_aql_selfcheck(uint32_t* out) {
     }
 }
 
+// A device flag set once the queue's packets before it are done (aql_flag): what a HIP stream
+// waits for (hipStreamWaitValue64) to order work after a queue's steps — the group's collective
+// after its batches.  System scope: the waiting stream's packet processor reads the flag.
+__global__ void k_aql_flag(uint64_t* p, uint64_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 const char* aql_error(const crane_queue* q) { return q ? q->err.c_str() : "null queue"; }
 
 void aql_add_user(crane_queue* q, crane_dyn* h) {
@@ -309,6 +316,15 @@ hipError_t aql_commit(crane_queue* q) {
     hsa_signal_store_screlease(q->q->doorbell_signal, (hsa_signal_value_t)last);
     q->first = q->next;
     return hipSuccess;
+}
+
+hipError_t aql_flag(crane_queue* q, uint64_t* flag, uint64_t value) {
+    unsigned char args[16];
+    size_t off = 0;
+    aql_pack(args, off, flag);
+    aql_pack(args, off, value);
+    hipError_t e = aql_launch(q, reinterpret_cast<const void*>(&k_aql_flag), dim3(1), dim3(64), 0, args, off);
+    return e == hipSuccess ? aql_commit(q) : e;
 }
 
 hipError_t aql_wait(crane_queue* q) {

@@ -36,6 +36,9 @@ hipError_t aql_launch(crane_queue* q, const void* host_fn, dim3 grid, dim3 block
 hipError_t aql_commit(crane_queue* q);
 // commit, then wait until every committed packet has completed
 hipError_t aql_wait(crane_queue* q);
+// a packet after the ones written so far that stores `value` to *flag (signal memory) when they
+// are done, committed: a HIP stream ordered after them waits for it (hipStreamWaitValue64)
+hipError_t aql_flag(crane_queue* q, uint64_t* flag, uint64_t value);
 const char* aql_error(const crane_queue* q);
 // Engines that put steps on a queue register with it (crane_dyn_step_keys_queue), so whichever of
 // the two is destroyed first can tell the other: a queue's destroy hands itself back to every
@@ -44,6 +47,8 @@ const char* aql_error(const crane_queue* q);
 void aql_add_user(crane_queue* q, crane_dyn* h);
 void aql_remove_user(crane_queue* q, crane_dyn* h);
 void engine_drop_queue(crane_dyn* h, crane_queue* q);
+// (group.cpp) engine h shares engine from's shard inputs (engine.hip: ShardData)
+int engine_share_shard(crane_dyn* h, crane_dyn* from);
 
 template <typename T>
 inline void aql_pack(unsigned char* buf, size_t& off, const T& v) {

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -144,6 +145,35 @@ constexpr int64_t kTraceWgs = 65536;  // workgroups traced per kernel
 
 struct crane_dyn;
 
+// A node shard's inputs: the parsed annotation SoA, the binding log (or the binding heap and its
+// slot log) and what describes them.  One per engine, or shared by the engines of a group's batch
+// slots on one device (crane::engine_share_shard): those slots then hold one copy of the shard's
+// nodes and log, and only their own derived state and scratch.  A change through any sharing
+// engine bumps a version; each engine adopts the new description (and drops what it derived from
+// the old) at its next call.  The engines sharing a shard are driven by one caller at a time, which
+// waits for their work in flight before it changes the shard (the group: wait_all).
+struct ShardData {
+    int device = 0;
+    uint64_t node_ver = 1, log_ver = 1;
+    int64_t N = -1, node_offset = 0, B = 0;
+    bool have_hv = false, log_sorted = false, heap_mode = false;
+    DevBuf<double> val, hv;
+    DevBuf<int64_t> ts, hv_ts;
+    DevBuf<int32_t> bnode;
+    DevBuf<int64_t> bts;
+    HostBuf<int32_t> hnode;  // pinned mirror of the slots in heap mode
+    HostBuf<int64_t> hts;
+    BindingHeap heap;        // BindingRecords restatement (crane_dyn_binding_records mode)
+    std::vector<int64_t> hts_copy;    // a time-ordered log's timestamps (the windows' suffixes are found here)
+    std::vector<int64_t> hts_sample;  // every 64th of them: the suffix search touches one 512-byte run
+    explicit ShardData(int dev) : device(dev) {}
+    ~ShardData() {
+        (void)hipSetDevice(device);
+        val.release(); hv.release(); ts.release(); hv_ts.release(); bnode.release(); bts.release();
+        hnode.release(); hts.release();
+    }
+};
+
 struct EngineTimer final : KernelTimer {
     crane_dyn* h = nullptr;
     void next(const char* name, hipEvent_t* start, hipEvent_t* stop) override;
@@ -177,22 +207,16 @@ struct crane_dyn {
     HotPart hx_g{};
     // binding log on the device: B slots (node < 0 = empty slot)
     int64_t B = 0;
-    BindingHeap heap;             // BindingRecords restatement (crane_dyn_binding_records mode)
     bool heap_mode = false;
     bool log_sorted = false;            // uploaded log in non-decreasing time order (upload_bindings)
-    std::vector<int64_t> hts_copy;      // ... and its timestamps (the windows' suffixes are found here)
-    std::vector<int64_t> hts_sample;    // every 64th of them: the suffix search touches one 512-byte run
     bool pos_valid = false;             // pos_s[r]: the suffix start of window rank r for cutoffs pos_cut
     int64_t pos_cut[kMaxWin] = {};
     int64_t pos_s[kMaxWin] = {};
-    HostBuf<int32_t> hnode;       // pinned mirror of the slots in heap mode
-    HostBuf<int64_t> hts;
-    DevBuf<double> val, hv;
-    DevBuf<int64_t> ts, hv_ts;
+    // the shard's inputs (ShardData), shared by the engines of a group's batch slots on one device
+    std::shared_ptr<ShardData> sd;
+    uint64_t sd_node_ver = 0, sd_log_ver = 0;  // the versions this engine's derived state follows
     DevBuf<unsigned char> rec;
     DevBuf<uint32_t> buckets;
-    DevBuf<int32_t> bnode;
-    DevBuf<int64_t> bts;
     // scratch for the host-pointer API
     DevBuf<int64_t> now;
     DevBuf<uint8_t> flags;
@@ -274,12 +298,65 @@ void EngineTimer::next(const char* name, hipEvent_t* start, hipEvent_t* stop) {
 
 namespace {
 
-// Every ABI entry that enqueues work holds the engine mutex and installs the
-// engine's kernel timer on the calling thread while profiling is on.
+// After this engine changed the shard's nodes (upload, update, resize) or its bindings (upload,
+// heap): the new description for the engines sharing it; this engine's own derived state was
+// updated by the change itself
+void publish_nodes(crane_dyn* h) {
+    ShardData& d = *h->sd;
+    d.N = h->N;
+    d.node_offset = h->node_offset;
+    d.have_hv = h->have_hv;
+    h->sd_node_ver = ++d.node_ver;
+}
+void publish_log(crane_dyn* h) {
+    ShardData& d = *h->sd;
+    d.B = h->B;
+    d.log_sorted = h->log_sorted;
+    d.heap_mode = h->heap_mode;
+    h->sd_log_ver = ++d.log_ver;
+}
+
+// Another engine changed the shared shard: take its description and drop what was derived from
+// the old one, as this engine's own upload_nodes / upload_bindings would
+int adopt(crane_dyn* h) {
+    ShardData& d = *h->sd;
+    if (h->sd_node_ver != d.node_ver) {
+        if (d.N >= 0) {
+            hipError_t e = hipSetDevice(h->device);
+            if (e == hipSuccess) e = h->rec.reserve((size_t)d.N * h->rec_bytes);
+            if (e != hipSuccess) return h->hipfail(e, "shared shard: record buffer");
+        }
+        if (d.N != h->N) h->buckets_zero = false;
+        h->N = d.N;
+        h->node_offset = d.node_offset;
+        h->have_hv = d.have_hv;
+        h->hv_from_counts = false;
+        h->counts_pending = false;
+        h->hx_pending = false;
+        h->rec_dirty = true;
+        h->sd_node_ver = d.node_ver;
+    }
+    if (h->sd_log_ver != d.log_ver) {
+        h->B = d.B;
+        h->log_sorted = d.log_sorted;
+        h->heap_mode = d.heap_mode;
+        h->pos_valid = false;
+        h->sd_log_ver = d.log_ver;
+    }
+    return CRANE_OK;
+}
+
+// Every ABI entry that enqueues work holds the engine mutex, takes a shared shard's changes
+// (adopt; rc holds its error) and installs the engine's kernel timer on the calling thread while
+// profiling is on.
 struct Locked {
     std::lock_guard<std::mutex> g;
     KernelTimer* prev;
-    explicit Locked(crane_dyn* h) : g(h->mu), prev(tl_ktimer) { tl_ktimer = h->prof ? &h->timer : nullptr; }
+    int rc = 0;
+    explicit Locked(crane_dyn* h) : g(h->mu), prev(tl_ktimer) {
+        tl_ktimer = h->prof ? &h->timer : nullptr;
+        if (h->sd && (h->sd_node_ver != h->sd->node_ver || h->sd_log_ver != h->sd->log_ver)) rc = adopt(h);
+    }
     ~Locked() { tl_ktimer = prev; }
 };
 
@@ -403,17 +480,17 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
     // then read only the node ids of the widest window's suffix and rank a binding by its
     // position — the same counts as the timestamp test, without the 8-byte stamps and without
     // the bindings older than every window.
-    const int32_t* bn = h->bnode.p;
+    const int32_t* bn = h->sd->bnode.p;
     int64_t Bk = h->B;
     HotCutoffs pcut = cut;
-    const bool by_pos = h->log_sorted && h->opt.k2_sorted && dp.n_win > 0 && (int64_t)h->hts_copy.size() == h->B;
+    const bool by_pos = h->log_sorted && h->opt.k2_sorted && dp.n_win > 0 && (int64_t)h->sd->hts_copy.size() == h->B;
     if (by_pos) {
         // (the cutoffs move once per second: the last search's suffixes are reused until they do)
         if (!h->pos_valid || std::memcmp(h->pos_cut, cut.sorted, sizeof(int64_t) * dp.n_win) != 0) {
             // (a batch whose time advanced moves them: the sampled stamps narrow each search to one
             // 64-stamp run, ~7 + 6 probes, instead of 20 probes across the 8 MB stamp array)
-            const std::vector<int64_t>& smp = h->hts_sample;
-            const int64_t* t0 = h->hts_copy.data();
+            const std::vector<int64_t>& smp = h->sd->hts_sample;
+            const int64_t* t0 = h->sd->hts_copy.data();
             for (int r = 0; r < dp.n_win; ++r) {
                 const int64_t j = std::upper_bound(smp.begin(), smp.end(), cut.sorted[r]) - smp.begin();
                 const int64_t lo = j == 0 ? 0 : 64 * (j - 1), hi = std::min<int64_t>(h->B, 64 * j);
@@ -425,7 +502,7 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         const int64_t s0 = h->pos_s[0];
         for (int r = 0; r < dp.n_win; ++r) pcut.sorted[r] = h->pos_s[r] - s0 - 1;
         pcut.by_pos = 1;
-        bn = h->bnode.p + s0;
+        bn = h->sd->bnode.p + s0;
         Bk = h->B - s0;
     }
     HotPart gx = hot_dedupe_geometry(Bk, h->N, dp.n_win, kK1Block);
@@ -437,7 +514,7 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         // cost 30-55 us per batch when the batch times advanced
         const HotPart gf = hot_dedupe_geometry(h->B, h->N, dp.n_win, kK1Block);
         HIPTRY(h, h->k2_sorted.reserve(std::max(hot_dedupe_scratch(gx), gf.ok ? hot_dedupe_scratch(gf) : 0)));
-        HIPTRY(h, launch_hot_count_dedupe(bn, h->bts.p, Bk, h->N, by_pos ? pcut : cut, gx, h->k2_sorted.p, st, pods,
+        HIPTRY(h, launch_hot_count_dedupe(bn, h->sd->bts.p, Bk, h->N, by_pos ? pcut : cut, gx, h->k2_sorted.p, st, pods,
                                           kK2xThreads));
         if (pods_done) *pods_done = pods != nullptr && pods->P > 0;
         h->hx_g = gx;
@@ -454,7 +531,7 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         // is rewritten, so nothing is zeroed before and K1 leaves them
         const HotPart gf = hot_large_geometry(h->B, h->N, dp.n_win);
         HIPTRY(h, h->k2_sorted.reserve(std::max(hot_dedupe_scratch(gl), gf.ok ? hot_dedupe_scratch(gf) : 0)));
-        HIPTRY(h, launch_hot_count_large(bn, h->bts.p, Bk, h->N, by_pos ? pcut : cut, gl, h->k2_sorted.p,
+        HIPTRY(h, launch_hot_count_large(bn, h->sd->bts.p, Bk, h->N, by_pos ? pcut : cut, gl, h->k2_sorted.p,
                                          h->buckets.p, h->n_cu, st, kK2lThreads));
         h->buckets_zero = false;
         h->buckets_dense = true;
@@ -471,7 +548,7 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         HIPTRY(h, hipMemsetAsync(h->buckets.p, 0, nb * sizeof(uint32_t), st));
     }
     // the atomics form (any size; shards past the large form's caps)
-    HIPTRY(h, launch_hot_count(h->bnode.p, h->bts.p, h->B, h->N, cut, h->buckets.p, st));
+    HIPTRY(h, launch_hot_count(h->sd->bnode.p, h->sd->bts.p, h->B, h->N, cut, h->buckets.p, st));
     h->buckets_zero = false;
     return CRANE_OK;
 }
@@ -489,8 +566,8 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
     K1Args a{};
     a.pol = h->dp;
     a.N = h->N;
-    a.val = h->val.p;
-    a.ts = h->ts.p;
+    a.val = h->sd->val.p;
+    a.ts = h->sd->ts.p;
     // the fused keys-only step reads its records from LDS; writing them out
     // (160 B/node of the pass's 280) is left to the next pass that reads them
     const bool keep = !step;
@@ -514,8 +591,8 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
     } else if (h->hv_from_counts) {
         a.hv = h->hvc.p;  // hv_ts null: stamped hv_ts_counts
     } else if (h->have_hv) {
-        a.hv = h->hv.p;
-        a.hv_ts = h->hv_ts.p;
+        a.hv = h->sd->hv.p;
+        a.hv_ts = h->sd->hv_ts.p;
     }
     a.threads = k1_bs(h);
     a.trace = (h->N + a.threads - 1) / a.threads <= kTraceWgs ? h->trace_region(1) : nullptr;
@@ -667,12 +744,12 @@ static int keys_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint
 // Re-upload the dirty binding-record slots of the heap mode (pinned mirror -> device).
 static int flush_heap_slots(crane_dyn* h) {
     std::vector<std::pair<int64_t, int64_t>> runs;
-    h->heap.take_dirty_runs(&runs);
+    h->sd->heap.take_dirty_runs(&runs);
     for (const auto& r : runs) {
         const size_t n = (size_t)(r.second - r.first);
-        HIPTRY(h, hipMemcpyAsync(h->bnode.p + r.first, h->hnode.p + r.first, n * sizeof(int32_t),
+        HIPTRY(h, hipMemcpyAsync(h->sd->bnode.p + r.first, h->sd->hnode.p + r.first, n * sizeof(int32_t),
                                  hipMemcpyHostToDevice, h->stream));
-        HIPTRY(h, hipMemcpyAsync(h->bts.p + r.first, h->hts.p + r.first, n * sizeof(int64_t), hipMemcpyHostToDevice,
+        HIPTRY(h, hipMemcpyAsync(h->sd->bts.p + r.first, h->sd->hts.p + r.first, n * sizeof(int64_t), hipMemcpyHostToDevice,
                                  h->stream));
     }
     if (!runs.empty()) HIPTRY(h, hipStreamSynchronize(h->stream));  // the mirror may change after we return
@@ -712,6 +789,19 @@ static int quiesce(crane_dyn* h) {
     return CRANE_OK;
 }
 
+// A group's batch slots on one device share the shard of slot 0 (group.cpp): h drops its own
+// (empty) shard inputs and takes from's; its derived state follows at its next call (adopt)
+int crane::engine_share_shard(crane_dyn* h, crane_dyn* from) {
+    if (!h || !from || h == from) return CRANE_E_INVALID;
+    std::scoped_lock l(h->mu, from->mu);
+    if (h->device != from->device || h->shape != from->shape || h->dp.n_slots != from->dp.n_slots)
+        return h->fail(CRANE_E_INVALID, "a shared shard needs the same device and policy");
+    if (int rc = quiesce(h)) return rc;
+    h->sd = from->sd;
+    h->sd_node_ver = h->sd_log_ver = 0;  // (versions start at 1: adopt at the next call)
+    return CRANE_OK;
+}
+
 // a queue being destroyed hands itself back (aql.cpp; it has waited for its steps)
 void crane::engine_drop_queue(crane_dyn* h, crane_queue* q) {
     std::lock_guard<std::mutex> g(h->mu);
@@ -746,6 +836,9 @@ int crane_dyn_create(const crane_policy* pol, int32_t device, crane_dyn** out) {
         return rc;
     }
     h->device = device;
+    h->sd = std::make_shared<ShardData>(device);
+    h->sd_node_ver = h->sd->node_ver;
+    h->sd_log_ver = h->sd->log_ver;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device);
@@ -777,10 +870,11 @@ int crane_dyn_destroy(crane_dyn* h) {
     }
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->ev.clear();
-    h->val.release(); h->hv.release(); h->ts.release(); h->hv_ts.release(); h->rec.release();
-    h->buckets.release(); h->bnode.release(); h->bts.release(); h->now.release(); h->flags.release();
+    h->sd.reset();  // (the shard's inputs go with the last engine holding them)
+    h->rec.release();
+    h->buckets.release(); h->now.release(); h->flags.release();
     h->keys.release(); h->ff.release(); h->score.release(); h->score8.release();
-    h->stage8.release(); h->stagek.release(); h->hnode.release(); h->hts.release();
+    h->stage8.release(); h->stagek.release();
     h->k2_sorted.release(); h->hvc.release();
     h->gcnt.release(); h->gbase.release(); h->gchosen.release(); h->gleaf.release(); h->gflags.release();
     h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
@@ -878,6 +972,7 @@ int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const d
                            const double* hv, const int64_t* hv_ts) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (h->N == -2) return h->fail(CRANE_E_STATE, "engine was not created successfully");
     if (n < 0 || n > 0xFFFFFFFFLL || node_offset < 0 || node_offset + n > 0xFFFFFFFFLL)
         return h->fail(CRANE_E_INVALID, "node count/offset out of range (global indices must fit 32 bits)");
@@ -886,18 +981,18 @@ int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const d
     if ((hv == nullptr) != (hv_ts == nullptr)) return h->fail(CRANE_E_INVALID, "hv and hv_ts must both be set or NULL");
     HIPTRY(h, hipSetDevice(h->device));
     if (int rc = quiesce(h)) return rc;
-    HIPTRY(h, h->val.reserve((size_t)(M * n)));
-    HIPTRY(h, h->ts.reserve((size_t)(M * n)));
-    HIPTRY(h, h->hv.reserve((size_t)n));
-    HIPTRY(h, h->hv_ts.reserve((size_t)n));
+    HIPTRY(h, h->sd->val.reserve((size_t)(M * n)));
+    HIPTRY(h, h->sd->ts.reserve((size_t)(M * n)));
+    HIPTRY(h, h->sd->hv.reserve((size_t)n));
+    HIPTRY(h, h->sd->hv_ts.reserve((size_t)n));
     HIPTRY(h, h->rec.reserve((size_t)n * h->rec_bytes));
     if (M * n > 0) {
-        HIPTRY(h, hipMemcpyAsync(h->val.p, val, sizeof(double) * M * n, hipMemcpyHostToDevice, h->stream));
-        HIPTRY(h, hipMemcpyAsync(h->ts.p, ts, sizeof(int64_t) * M * n, hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipMemcpyAsync(h->sd->val.p, val, sizeof(double) * M * n, hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipMemcpyAsync(h->sd->ts.p, ts, sizeof(int64_t) * M * n, hipMemcpyHostToDevice, h->stream));
     }
     if (hv && n > 0) {
-        HIPTRY(h, hipMemcpyAsync(h->hv.p, hv, sizeof(double) * n, hipMemcpyHostToDevice, h->stream));
-        HIPTRY(h, hipMemcpyAsync(h->hv_ts.p, hv_ts, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipMemcpyAsync(h->sd->hv.p, hv, sizeof(double) * n, hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipMemcpyAsync(h->sd->hv_ts.p, hv_ts, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
     }
     HIPTRY(h, hipStreamSynchronize(h->stream));
     if (n != h->N) h->buckets_zero = false;
@@ -908,100 +1003,112 @@ int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const d
     h->counts_pending = false;
     h->hx_pending = false;
     h->rec_dirty = true;
+    publish_nodes(h);
     return CRANE_OK;
 }
 
 int crane_dyn_upload_bindings(crane_dyn* h, int64_t n, const int32_t* node, const int64_t* ts_s) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (h->N == -2) return h->fail(CRANE_E_STATE, "engine was not created successfully");
     if (n < 0 || (n > 0 && (!node || !ts_s))) return h->fail(CRANE_E_INVALID, "bad binding arrays");
     HIPTRY(h, hipSetDevice(h->device));
     if (int rc = quiesce(h)) return rc;
-    HIPTRY(h, h->bnode.reserve((size_t)n));
-    HIPTRY(h, h->bts.reserve((size_t)n));
+    HIPTRY(h, h->sd->bnode.reserve((size_t)n));
+    HIPTRY(h, h->sd->bts.reserve((size_t)n));
     if (n > 0) {
-        HIPTRY(h, hipMemcpyAsync(h->bnode.p, node, sizeof(int32_t) * n, hipMemcpyHostToDevice, h->stream));
-        HIPTRY(h, hipMemcpyAsync(h->bts.p, ts_s, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipMemcpyAsync(h->sd->bnode.p, node, sizeof(int32_t) * n, hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipMemcpyAsync(h->sd->bts.p, ts_s, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
     }
     // a ring of bindings appended in time order (the synthetic and the controller-shaped logs):
     // kept for the suffix search of every refresh
     h->pos_valid = false;
     h->log_sorted = n > 0 && std::is_sorted(ts_s, ts_s + n);
-    h->hts_sample.clear();
+    h->sd->hts_sample.clear();
     if (h->log_sorted) {
-        h->hts_copy.assign(ts_s, ts_s + n);
-        for (int64_t i = 0; i < n; i += 64) h->hts_sample.push_back(ts_s[i]);
+        h->sd->hts_copy.assign(ts_s, ts_s + n);
+        for (int64_t i = 0; i < n; i += 64) h->sd->hts_sample.push_back(ts_s[i]);
     } else {
-        h->hts_copy.clear();
+        h->sd->hts_copy.clear();
     }
     HIPTRY(h, hipStreamSynchronize(h->stream));
     h->B = n;
     h->heap_mode = false;
-    h->heap.reset(0, 0);
+    h->sd->heap.reset(0, 0);
+    publish_log(h);
     return CRANE_OK;
 }
 
 int crane_dyn_binding_records(crane_dyn* h, int64_t size, int64_t gc_time_range_ns) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (h->N == -2) return h->fail(CRANE_E_STATE, "engine was not created successfully");
     // size 0 would pop an empty heap in AddBinding (binding.go:73-75); size < 0 never evicts
     if (size <= 0 || size > 0x7FFFFFFF) return h->fail(CRANE_E_INVALID, "binding heap size must be in [1, 2^31)");
     HIPTRY(h, hipSetDevice(h->device));
     if (int rc = quiesce(h)) return rc;
-    HIPTRY(h, h->hnode.reserve((size_t)size));
-    HIPTRY(h, h->hts.reserve((size_t)size));
-    HIPTRY(h, h->bnode.reserve((size_t)size));
-    HIPTRY(h, h->bts.reserve((size_t)size));
+    HIPTRY(h, h->sd->hnode.reserve((size_t)size));
+    HIPTRY(h, h->sd->hts.reserve((size_t)size));
+    HIPTRY(h, h->sd->bnode.reserve((size_t)size));
+    HIPTRY(h, h->sd->bts.reserve((size_t)size));
     for (int64_t i = 0; i < size; ++i) {
-        h->hnode.p[i] = -1;
-        h->hts.p[i] = 0;
+        h->sd->hnode.p[i] = -1;
+        h->sd->hts.p[i] = 0;
     }
-    HIPTRY(h, hipMemcpyAsync(h->bnode.p, h->hnode.p, sizeof(int32_t) * size, hipMemcpyHostToDevice, h->stream));
-    HIPTRY(h, hipMemcpyAsync(h->bts.p, h->hts.p, sizeof(int64_t) * size, hipMemcpyHostToDevice, h->stream));
+    HIPTRY(h, hipMemcpyAsync(h->sd->bnode.p, h->sd->hnode.p, sizeof(int32_t) * size, hipMemcpyHostToDevice, h->stream));
+    HIPTRY(h, hipMemcpyAsync(h->sd->bts.p, h->sd->hts.p, sizeof(int64_t) * size, hipMemcpyHostToDevice, h->stream));
     HIPTRY(h, hipStreamSynchronize(h->stream));
-    h->heap.reset(size, gc_time_range_ns);
-    h->heap.bind(h->hnode.p, h->hts.p);
+    h->sd->heap.reset(size, gc_time_range_ns);
+    h->sd->heap.bind(h->sd->hnode.p, h->sd->hts.p);
     h->heap_mode = true;
     h->log_sorted = false;  // heap order
     h->pos_valid = false;
-    h->hts_copy.clear();
-    h->hts_sample.clear();
+    h->sd->hts_copy.clear();
+    h->sd->hts_sample.clear();
     h->B = size;
+    publish_log(h);
     return CRANE_OK;
 }
 
 int crane_dyn_add_bindings(crane_dyn* h, int64_t n, const int32_t* node, const int64_t* ts_s) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (!h->heap_mode) return h->fail(CRANE_E_STATE, "crane_dyn_binding_records first");
     if (n < 0 || (n > 0 && (!node || !ts_s))) return h->fail(CRANE_E_INVALID, "bad binding arrays");
     HIPTRY(h, hipSetDevice(h->device));
     if (int rc = quiesce(h)) return rc;
-    for (int64_t i = 0; i < n; ++i) h->heap.add(node[i], ts_s[i]);
-    return flush_heap_slots(h);
+    for (int64_t i = 0; i < n; ++i) h->sd->heap.add(node[i], ts_s[i]);
+    const int rc = flush_heap_slots(h);
+    publish_log(h);  // (the slots changed: the sharing engines' suffix searches restart)
+    return rc;
 }
 
 int crane_dyn_gc_bindings(crane_dyn* h, int64_t now_ns) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (!h->heap_mode) return h->fail(CRANE_E_STATE, "crane_dyn_binding_records first");
     HIPTRY(h, hipSetDevice(h->device));
     if (int rc = quiesce(h)) return rc;
-    h->heap.gc(floor_div(now_ns, 1000000000LL));
-    return flush_heap_slots(h);
+    h->sd->heap.gc(floor_div(now_ns, 1000000000LL));
+    const int rc = flush_heap_slots(h);
+    publish_log(h);
+    return rc;
 }
 
 int64_t crane_dyn_binding_count(const crane_dyn* h) {
     if (!h) return CRANE_E_INVALID;
     std::lock_guard<std::mutex> g(const_cast<crane_dyn*>(h)->mu);
-    return h->heap_mode ? h->heap.len() : h->B;
+    return h->heap_mode ? h->sd->heap.len() : h->B;
 }
 
 int crane_dyn_refresh_hot_values(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     HIPTRY(h, hipSetDevice(h->device));
     if (int rc = quiesce(h)) return rc;
     int rc = hot_values_locked(h, now_ns, hv_ts_ns, h->stream);
@@ -1013,6 +1120,7 @@ int crane_dyn_refresh_hot_values(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns)
 int crane_dyn_hot_values(crane_dyn* h, int64_t n, double* hv_out) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before reading hot values");
     if (n != h->N || (n > 0 && !hv_out)) return h->fail(CRANE_E_INVALID, "hv_out must hold one value per node");
     if (n == 0) return CRANE_OK;
@@ -1026,7 +1134,7 @@ int crane_dyn_hot_values(crane_dyn* h, int64_t n, double* hv_out) {
         }
         src = h->hvc.p;
     } else if (h->have_hv) {
-        src = h->hv.p;
+        src = h->sd->hv.p;
     }
     if (src) {
         HIPTRY(h, hipMemcpyAsync(hv_out, src, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
@@ -1040,6 +1148,7 @@ int crane_dyn_hot_values(crane_dyn* h, int64_t n, double* hv_out) {
 int crane_dyn_refresh_hot_values_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, void* stream) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     HIPTRY(h, hipSetDevice(h->device));
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     int rc = hot_values_locked(h, now_ns, hv_ts_ns, st);
@@ -1049,6 +1158,7 @@ int crane_dyn_refresh_hot_values_async(crane_dyn* h, int64_t now_ns, int64_t hv_
 int crane_dyn_node_pass_async(crane_dyn* h, void* stream) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     HIPTRY(h, hipSetDevice(h->device));
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     int rc = node_pass_locked(h, st);
@@ -1059,6 +1169,7 @@ int crane_dyn_eval_keys_async(crane_dyn* h, int64_t P, const int64_t* d_now, con
                               int64_t* d_keys, void* stream) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (P < 0 || (P > 0 && (!d_now || !d_keys))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
     HIPTRY(h, hipSetDevice(h->device));
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
@@ -1070,6 +1181,7 @@ int crane_dyn_eval_matrix_async(crane_dyn* h, int64_t P, const int64_t* d_now, c
                                 int8_t* d_first_fail, int8_t* d_score, int64_t ld, int64_t* d_keys, void* stream) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (P < 0 || (P > 0 && !d_now)) return h->fail(CRANE_E_INVALID, "bad pod arrays");
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
     if ((d_first_fail || d_score) && ld < h->N) return h->fail(CRANE_E_INVALID, "ld must be >= the node count");
@@ -1101,6 +1213,7 @@ int crane_dyn_select(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_
                      int64_t* d_wlen, int64_t* next_start, void* stream) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (P < 0 || (P > 0 && (!d_now || !d_chosen))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
     if (dyn_weight < 0 || dyn_weight > (1 << 20)) return h->fail(CRANE_E_INVALID, "dyn_weight must be in [0, 2^20]");
@@ -1178,6 +1291,7 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
                               const uint8_t* d_flags, int64_t* d_keys, void* stream) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (P < 0 || (P > 0 && (!d_now || !d_keys))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
     HIPTRY(h, hipSetDevice(h->device));
@@ -1209,6 +1323,7 @@ int crane_dyn_step_keys_queue(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
                               const uint8_t* d_flags, int64_t* d_keys, crane_queue* q) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (!q) return h->fail(CRANE_E_INVALID, "null queue");
     if (P < 0 || (P > 0 && (!d_now || !d_keys))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before evaluating pods");
@@ -1320,6 +1435,7 @@ int crane_dyn_eval(crane_dyn* h, int64_t P, const int64_t* now_ns, const uint8_t
                    int64_t* score, int64_t* chosen, int64_t* chosen_score) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     return eval_host(h, P, now_ns, pod_flags, first_fail, score, true, chosen, chosen_score);
 }
 
@@ -1327,6 +1443,7 @@ int crane_dyn_eval_compact(crane_dyn* h, int64_t P, const int64_t* now_ns, const
                            int8_t* first_fail, int8_t* score, int64_t* chosen, int64_t* chosen_score) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     return eval_host(h, P, now_ns, pod_flags, first_fail, score, false, chosen, chosen_score);
 }
 
@@ -1336,6 +1453,7 @@ int crane_dyn_node_steps(crane_dyn* h, int64_t t0_ns, int64_t t1_ns, int64_t n, 
                          int8_t* first_fail, int8_t* score) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before building node tables");
     if (n != h->N) return h->fail(CRANE_E_INVALID, "the tables hold one entry per node of the shard");
     if (n > 0 && (!n_steps || !bp || !first_fail || !score)) return h->fail(CRANE_E_INVALID, "NULL output");
@@ -1422,10 +1540,10 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
         h->rec_dirty = true;
     }
     if (hv && !h->have_hv) {  // the first hot-value annotations of the shard: the others have none
-        HIPTRY(h, h->hv.reserve((size_t)h->N));
-        HIPTRY(h, h->hv_ts.reserve((size_t)h->N));
-        HIPTRY(h, hipMemsetAsync(h->hv.p, 0, sizeof(double) * (size_t)h->N, h->stream));
-        HIPTRY(h, launch_fill_i64(h->hv_ts.p, h->N, kTsInvalid, h->stream));
+        HIPTRY(h, h->sd->hv.reserve((size_t)h->N));
+        HIPTRY(h, h->sd->hv_ts.reserve((size_t)h->N));
+        HIPTRY(h, hipMemsetAsync(h->sd->hv.p, 0, sizeof(double) * (size_t)h->N, h->stream));
+        HIPTRY(h, launch_fill_i64(h->sd->hv_ts.p, h->N, kTsInvalid, h->stream));
         h->have_hv = true;
     }
     // staging: in idx [k] | val [M][k] | ts [M][k] | hv [k] | hv_ts [k];  out (rows) bp [k][S] | ns [k] |
@@ -1461,10 +1579,10 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
     a.sts = reinterpret_cast<const int64_t*>(d + o_ts);
     a.shv = hv ? reinterpret_cast<const double*>(d + o_hv) : nullptr;
     a.shv_ts = hv ? reinterpret_cast<const int64_t*>(d + o_hvt) : nullptr;
-    a.val = h->val.p;
-    a.ts = h->ts.p;
-    a.hv = h->have_hv ? h->hv.p : nullptr;
-    a.hv_ts = h->have_hv ? h->hv_ts.p : nullptr;
+    a.val = h->sd->val.p;
+    a.ts = h->sd->ts.p;
+    a.hv = h->have_hv ? h->sd->hv.p : nullptr;
+    a.hv_ts = h->have_hv ? h->sd->hv_ts.p : nullptr;
     a.rec = h->rec_dirty ? nullptr : h->rec.p;  // current records stay current
     if (rows) {
         a.ma.wsum = h->dp.wsum;
@@ -1519,6 +1637,7 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
                      "sync %.1f us (kernel between events %.1f us; %lld queries, the longest %.1f us)\n",
                      (long long)k, us(u0, u1), us(u1, u2), us(u2, u3), us(u3, u4), gpu_ms * 1000.f, nq, qmax_us);
     }
+    publish_nodes(h);  // (the engines sharing the shard rebuild their records from the new columns)
     if (rows) {
         std::memcpy(rows->bp, p + o_out, 8 * K * S);
         std::memcpy(rows->n_steps, p + r_ns, K);
@@ -1535,6 +1654,7 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
 int crane_dyn_resize_nodes(crane_dyn* h, int64_t n) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before resizing the shard");
     if (n < 0 || n > 0xFFFFFFFFLL || h->node_offset + n > 0xFFFFFFFFLL)
         return h->fail(CRANE_E_INVALID, "node count out of range (global indices must fit 32 bits)");
@@ -1555,10 +1675,10 @@ int crane_dyn_resize_nodes(crane_dyn* h, int64_t n) {
     if (e != hipSuccess) return fail(e, "resize: hipMalloc");
     hipStream_t st = h->stream;
     if (M > 0 && keep > 0) {
-        e = hipMemcpy2DAsync(val.p, sizeof(double) * n, h->val.p, sizeof(double) * N0, sizeof(double) * keep, M,
+        e = hipMemcpy2DAsync(val.p, sizeof(double) * n, h->sd->val.p, sizeof(double) * N0, sizeof(double) * keep, M,
                              hipMemcpyDeviceToDevice, st);
         if (e == hipSuccess)
-            e = hipMemcpy2DAsync(ts.p, sizeof(int64_t) * n, h->ts.p, sizeof(int64_t) * N0, sizeof(int64_t) * keep, M,
+            e = hipMemcpy2DAsync(ts.p, sizeof(int64_t) * n, h->sd->ts.p, sizeof(int64_t) * N0, sizeof(int64_t) * keep, M,
                                  hipMemcpyDeviceToDevice, st);
     }
     for (int64_t m = 0; m < M && n > keep && e == hipSuccess; ++m) {
@@ -1566,9 +1686,9 @@ int crane_dyn_resize_nodes(crane_dyn* h, int64_t n) {
         if (e == hipSuccess) e = launch_fill_i64(ts.p + m * n + keep, n - keep, kTsInvalid, st);
     }
     if (h->have_hv && keep > 0 && e == hipSuccess) {
-        e = hipMemcpyAsync(hv.p, h->hv.p, sizeof(double) * (size_t)keep, hipMemcpyDeviceToDevice, st);
+        e = hipMemcpyAsync(hv.p, h->sd->hv.p, sizeof(double) * (size_t)keep, hipMemcpyDeviceToDevice, st);
         if (e == hipSuccess)
-            e = hipMemcpyAsync(hv_ts.p, h->hv_ts.p, sizeof(int64_t) * (size_t)keep, hipMemcpyDeviceToDevice, st);
+            e = hipMemcpyAsync(hv_ts.p, h->sd->hv_ts.p, sizeof(int64_t) * (size_t)keep, hipMemcpyDeviceToDevice, st);
     }
     if (h->have_hv && n > keep && e == hipSuccess) {
         e = hipMemsetAsync(hv.p + keep, 0, sizeof(double) * (size_t)(n - keep), st);
@@ -1576,10 +1696,10 @@ int crane_dyn_resize_nodes(crane_dyn* h, int64_t n) {
     }
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return fail(e, "resize: copy");
-    std::swap(h->val, val);
-    std::swap(h->ts, ts);
-    std::swap(h->hv, hv);
-    std::swap(h->hv_ts, hv_ts);
+    std::swap(h->sd->val, val);
+    std::swap(h->sd->ts, ts);
+    std::swap(h->sd->hv, hv);
+    std::swap(h->sd->hv_ts, hv_ts);
     val.release(); ts.release(); hv.release(); hv_ts.release();
     HIPTRY(h, h->rec.reserve((size_t)n * h->rec_bytes));
     h->N = n;
@@ -1588,6 +1708,7 @@ int crane_dyn_resize_nodes(crane_dyn* h, int64_t n) {
     h->counts_pending = false;
     h->hx_pending = false;
     h->rec_dirty = true;
+    publish_nodes(h);
     return CRANE_OK;
 }
 
@@ -1595,6 +1716,7 @@ int crane_dyn_update_nodes(crane_dyn* h, int64_t k, const int64_t* idx, const do
                            const double* hv, const int64_t* hv_ts) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     return update_locked(h, k, idx, val, ts, hv, hv_ts, nullptr);
 }
 
@@ -1603,6 +1725,7 @@ int crane_dyn_update_node_steps(crane_dyn* h, int64_t k, const int64_t* idx, con
                                 uint8_t* n_steps, int64_t* bp, int8_t* first_fail, int8_t* score) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     const RowOut rows{t0_ns, t1_ns, n_steps, bp, first_fail, score};
     return update_locked(h, k, idx, val, ts, hv, hv_ts, &rows);
 }
@@ -1611,6 +1734,7 @@ int crane_dyn_node_steps_subset(crane_dyn* h, int64_t t0_ns, int64_t t1_ns, int6
                                 uint8_t* n_steps, int64_t* bp, int8_t* first_fail, int8_t* score) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (int rc = check_subset(h, k, idx)) return rc;
     if (k > 0 && (!n_steps || !bp || !first_fail || !score)) return h->fail(CRANE_E_INVALID, "NULL output");
     if (!(t0_ns < t1_ns)) return h->fail(CRANE_E_INVALID, "t0 must be before t1");
@@ -1684,6 +1808,7 @@ int crane_dyn_stage_times(crane_dyn* h, int32_t max, const char** names, double*
 int crane_dyn_greedy(crane_dyn* h, int64_t P, int64_t now_ns, const uint8_t* pod_flags, int64_t* chosen) {
     if (!h) return CRANE_E_INVALID;
     Locked lk(h);
+    if (lk.rc) return lk.rc;
     if (P < 0 || (P > 0 && !chosen)) return h->fail(CRANE_E_INVALID, "bad pod arrays");
     if (h->N < 0) return h->fail(CRANE_E_STATE, "upload nodes before greedy placement");
     if (h->N > kGreedyMaxNodes) return h->fail(CRANE_E_INVALID, "greedy mode supports up to 64^4 nodes");

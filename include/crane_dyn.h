@@ -362,18 +362,20 @@ int64_t crane_dyn_debug_trace(crane_dyn *h, int32_t which, int64_t max, uint64_t
  * scheduler is one Go process with one plugin instance (cmd/scheduler/main.go:18-32,
  * plugins.go:105-120), so the node-shard path is reached through one handle.  A group holds per
  * device `depth` engines (one per batch in flight) over the device's contiguous node range
- * (crane_shard_range of the cluster over n_dev shards), their HIP streams and one RCCL
- * communicator per device (ncclCommInitAll).  A batch = every device's shard step
+ * (crane_shard_range of the cluster over n_dev shards) — sharing ONE copy of the shard's nodes and
+ * binding log, each with its own scratch —, their HIP streams and one RCCL communicator per device
+ * (ncclCommInitAll).  A batch = every device's shard step
  * (crane_dyn_step_keys_async), then an in-place ncclAllReduce(int64, ncclMax) of the packed keys
  * on the same streams: every device then holds the global choice per pod.  With n_dev > 1 each
  * device has a worker thread enqueueing its part (the caller only hands over the batch).
  * Options (crane_dyn_group_set_option): "collective" 0 never (crane_dyn_group_schedule max-combines
  * on the host; the async form leaves per-shard keys) | 1 when n_dev > 1 (default) | 2 always (a
  * one-rank communicator: tests); "threads" -1 auto | 0 the caller's thread (the collective in
- * ncclGroupStart/End) | 1 worker threads; "dispatch" -1 (default) dispatch queues unless the
- * collective runs | 0 the steps' kernels launched through HIP on the slots' streams | 1 on dispatch
- * queues (crane_queue, one per slot and device; no collective); "dispatch_ring" 0 | 1 their
- * ring_kind; any other name goes to every engine.  Either way the batch's d_now / d_flags must be
+ * ncclGroupStart/End) | 1 worker threads; "dispatch" -1 (default) dispatch queues, except for the
+ * per-batch collective (step_keys_async / schedule with the collective on) | 0 the steps' kernels
+ * launched through HIP on the slots' streams | 1 on dispatch queues (crane_queue, one per slot and
+ * device; the batch form crane_dyn_group_step_keys_batch orders its collective after them);
+ * "dispatch_ring" 0 | 1 their ring_kind; any other name goes to every engine.  Either way the batch's d_now / d_flags must be
  * complete on the devices when it is handed over (the group's streams and queues are its own). */
 typedef struct crane_dyn_group crane_dyn_group;
 /* Contiguous balanced node range of shard `shard` of n_shards (the first n % n_shards get one more). */
@@ -406,8 +408,49 @@ int crane_dyn_group_upload_bindings(crane_dyn_group *g, int64_t n, const int32_t
 int crane_dyn_group_step_keys_async(crane_dyn_group *g, int64_t now_ns, int64_t hv_ts_ns, int64_t n_pods,
                                     const int64_t *const *d_now, const uint8_t *const *d_flags,
                                     int64_t *const *d_keys);
+/* G batches at once, asynchronous, with ONE collective: batch b (b < n_batches) at now_ns[b] /
+ * hv_ts_ns[b] over the pods d_now[i] + b * n_pods (device i's [n_batches][n_pods] times; d_flags[i]
+ * likewise or NULL) into d_keys[i] + b * n_pods, on slot (the group's batch count) % depth, its
+ * kernels on the slot's dispatch queue unless "dispatch" is 0; then, with the collective on, one
+ * in-place ncclAllReduce(int64, max) of the whole [n_batches][n_pods] keys per device on a
+ * collective stream of the group, ordered after those batches' queues (a device flag written by
+ * each slot's last packet, hipStreamWaitValue64) — the per-batch all-reduce's latency paid once per
+ * G batches, as a scheduler collecting a window of batches' choices would.  A later batch that
+ * writes keys where that all-reduce still works waits for it (host side): alternate two key
+ * buffers.  Errors of the enqueued work are reported by crane_dyn_group_sync. */
+int crane_dyn_group_step_keys_batch(crane_dyn_group *g, int32_t n_batches, const int64_t *now_ns,
+                                    const int64_t *hv_ts_ns, int64_t n_pods, const int64_t *const *d_now,
+                                    const uint8_t *const *d_flags, int64_t *const *d_keys);
 /* wait for every batch enqueued on the group */
 int crane_dyn_group_sync(crane_dyn_group *g);
+/* The shard state changes of the drop-in plugin and the controller, routed by GLOBAL node index to
+ * the owning shard (each shard's batch slots share one copy of its inputs and follow the change):
+ *   update_nodes / update_node_steps = crane_dyn_update_nodes / _update_node_steps with global
+ *     indices (rows j of the outputs for idx[j]);
+ *   resize_nodes = the cluster's node count becomes n: the last shard grows (joining nodes take
+ *     indices at the end, no annotations until updated), shrinking empties shards from the end;
+ *     bindings uploaded with crane_dyn_group_upload_bindings for nodes past the old end need a
+ *     re-upload (the heap form routes them as they come);
+ *   binding_records / add_bindings / gc_bindings / binding_count = the BindingRecords heap
+ *     (binding.go:50-123) with global node indices: every device runs the same heap (its order
+ *     depends on timestamps only) with the other shards' nodes as "no node";
+ *   refresh_hot_values / hot_values / node_steps = per shard, results at the global rows.
+ * Synchronous; each first waits for the group's batches in flight. */
+int crane_dyn_group_update_nodes(crane_dyn_group *g, int64_t k, const int64_t *idx, const double *val,
+                                 const int64_t *ts, const double *hv, const int64_t *hv_ts);
+int crane_dyn_group_update_node_steps(crane_dyn_group *g, int64_t k, const int64_t *idx, const double *val,
+                                      const int64_t *ts, const double *hv, const int64_t *hv_ts, int64_t t0_ns,
+                                      int64_t t1_ns, uint8_t *n_steps, int64_t *bp, int8_t *first_fail,
+                                      int8_t *score);
+int crane_dyn_group_resize_nodes(crane_dyn_group *g, int64_t n);
+int crane_dyn_group_binding_records(crane_dyn_group *g, int64_t size, int64_t gc_time_range_ns);
+int crane_dyn_group_add_bindings(crane_dyn_group *g, int64_t n, const int32_t *node, const int64_t *ts_s);
+int crane_dyn_group_gc_bindings(crane_dyn_group *g, int64_t now_ns);
+int64_t crane_dyn_group_binding_count(crane_dyn_group *g);
+int crane_dyn_group_refresh_hot_values(crane_dyn_group *g, int64_t now_ns, int64_t hv_ts_ns);
+int crane_dyn_group_hot_values(crane_dyn_group *g, int64_t n, double *hv_out);
+int crane_dyn_group_node_steps(crane_dyn_group *g, int64_t t0_ns, int64_t t1_ns, int64_t n, uint8_t *n_steps,
+                               int64_t *bp, int8_t *first_fail, int8_t *score);
 /* One batch from host arrays, synchronous: chosen[p] = global node index or -1, chosen_score[p]
  * (either may be NULL) — the scheduler's call per pod batch. */
 int crane_dyn_group_schedule(crane_dyn_group *g, int64_t now_ns, int64_t hv_ts_ns, int64_t n_pods,

@@ -173,6 +173,62 @@ class Snapshot {
 struct Handle {
     const Snapshot* snapshot = nullptr;
     int32_t device = 0;
+    // more than one: the plugin's nodes are sharded over these devices (crane_dyn_group_*: each
+    // device holds a contiguous range of the synced rows; the same answers as one engine)
+    std::vector<int32_t> devices;
+};
+
+// The engine the plugin keeps its nodes in: one engine, or a group of node shards over several
+// devices (the same calls routed by node row, crane_dyn_group_*)
+class Backend {
+   public:
+    ~Backend() {
+        if (eng_) crane_dyn_destroy(eng_);
+        if (grp_) crane_dyn_group_destroy(grp_);
+    }
+    int create(const crane_policy* pol, const Handle& h) {
+        if (h.devices.size() > 1) {
+            int rc = crane_dyn_group_create(pol, (int32_t)h.devices.size(), h.devices.data(), 1, &grp_);
+            if (!rc) rc = crane_dyn_group_set_option(grp_, "collective", 0);  // (answer tables only: no batches)
+            return rc;
+        }
+        return crane_dyn_create(pol, h.devices.size() == 1 ? h.devices[0] : h.device, &eng_);
+    }
+    const char* error() const {
+        return grp_ ? crane_dyn_group_last_error(grp_) : eng_ ? crane_dyn_last_error(eng_) : "engine creation failed";
+    }
+    crane_dyn* first() const { return grp_ ? crane_dyn_group_engine(grp_, 0, 0) : eng_; }
+    int32_t num_metrics() const { return crane_dyn_num_metrics(first()); }
+    const char* metric_name(int32_t m) const { return crane_dyn_metric_name(first(), m); }
+    int32_t step_slots() const { return crane_dyn_step_slots(first()); }
+    int set_option(const char* name, int64_t v) {
+        return grp_ ? crane_dyn_group_set_option(grp_, name, v) : crane_dyn_set_option(eng_, name, v);
+    }
+    int upload_nodes(int64_t n, const double* val, const int64_t* ts, const double* hv, const int64_t* hv_ts) {
+        return grp_ ? crane_dyn_group_upload_nodes(grp_, n, val, ts, hv, hv_ts)
+                    : crane_dyn_upload_nodes(eng_, n, 0, val, ts, hv, hv_ts);
+    }
+    int node_steps(int64_t t0, int64_t t1, int64_t n, uint8_t* ns, int64_t* bp, int8_t* ff, int8_t* sc) {
+        return grp_ ? crane_dyn_group_node_steps(grp_, t0, t1, n, ns, bp, ff, sc)
+                    : crane_dyn_node_steps(eng_, t0, t1, n, ns, bp, ff, sc);
+    }
+    int update_nodes(int64_t k, const int64_t* idx, const double* val, const int64_t* ts, const double* hv,
+                     const int64_t* hv_ts) {
+        return grp_ ? crane_dyn_group_update_nodes(grp_, k, idx, val, ts, hv, hv_ts)
+                    : crane_dyn_update_nodes(eng_, k, idx, val, ts, hv, hv_ts);
+    }
+    int update_node_steps(int64_t k, const int64_t* idx, const double* val, const int64_t* ts, const double* hv,
+                          const int64_t* hv_ts, int64_t t0, int64_t t1, uint8_t* ns, int64_t* bp, int8_t* ff,
+                          int8_t* sc) {
+        return grp_ ? crane_dyn_group_update_node_steps(grp_, k, idx, val, ts, hv, hv_ts, t0, t1, ns, bp, ff, sc)
+                    : crane_dyn_update_node_steps(eng_, k, idx, val, ts, hv, hv_ts, t0, t1, ns, bp, ff, sc);
+    }
+    int resize_nodes(int64_t n) { return grp_ ? crane_dyn_group_resize_nodes(grp_, n) : crane_dyn_resize_nodes(eng_, n); }
+    int32_t shards() const { return grp_ ? crane_dyn_group_size(grp_) : 1; }
+
+   private:
+    crane_dyn* eng_ = nullptr;
+    crane_dyn_group* grp_ = nullptr;
 };
 
 // runtime.Object for plugin args
@@ -265,7 +321,6 @@ class AddrIndex {
 class DynamicScheduler {
    public:
     ~DynamicScheduler() {
-        if (eng_) crane_dyn_destroy(eng_);
         if (doc_) crane_policy_free(doc_);
         if (zone_) crane_tz_free(zone_);
     }
@@ -324,7 +379,9 @@ class DynamicScheduler {
     // host threads of the full-snapshot annotation parse (<= 0: all hardware threads)
     void SetParseThreads(int32_t n) { parse_threads_ = n; }
     // an engine option (crane_dyn_set_option: alternative kernel forms, tests and A/B tools)
-    bool SetEngineOption(const char* name, int64_t value) { return crane_dyn_set_option(eng_, name, value) == 0; }
+    bool SetEngineOption(const char* name, int64_t value) { return eng_.set_option(name, value) == 0; }
+    // node shards the plugin's engine spans (Handle::devices)
+    int32_t Shards() const { return eng_.shards(); }
     // time span one answer table covers from the pod that builds it (a later pod gets a new
     // table); by default (and ns <= 0) the whole time axis, which never needs a new table
     void SetHorizon(int64_t ns) { horizon_ns_ = ns > 0 ? ns : kAllTime; }
@@ -448,8 +505,8 @@ class DynamicScheduler {
 
     const std::vector<std::string>& keys() {  // rows: metric slots 0..M-1, node_hot_value
         if (keys_.empty()) {
-            const int32_t M = crane_dyn_num_metrics(eng_);
-            for (int32_t m = 0; m < M; ++m) keys_.emplace_back(crane_dyn_metric_name(eng_, m));
+            const int32_t M = eng_.num_metrics();
+            for (int32_t m = 0; m < M; ++m) keys_.emplace_back(eng_.metric_name(m));
             keys_.emplace_back(NodeHotValue);
         }
         return keys_;
@@ -548,9 +605,9 @@ class DynamicScheduler {
             t0 = now;
             t1 = now > INT64_MAX - horizon_ns_ ? INT64_MAX : now + horizon_ns_;
         }
-        if (crane_dyn_node_steps(eng_, t0, t1, (int64_t)N, v->n_steps.data(), v->bp.data(), v->first_fail.data(),
-                                 v->score.data())) {
-            *err = crane_dyn_last_error(eng_);
+        if (eng_.node_steps(t0, t1, (int64_t)N, v->n_steps.data(), v->bp.data(), v->first_fail.data(),
+                            v->score.data())) {
+            *err = eng_.error();
             return false;
         }
         v->t0 = t0;
@@ -564,7 +621,7 @@ class DynamicScheduler {
     std::shared_ptr<View> full_sync(const std::vector<const NodeInfo*>& L, int64_t now, std::string* err) {
         auto v = std::make_shared<View>();
         const size_t N = L.size();
-        v->S = (size_t)crane_dyn_step_slots(eng_);
+        v->S = (size_t)eng_.step_slots();
         v->grow(N);
         v->by_name.reserve(N);
         for (size_t i = 0; i < N; ++i) {
@@ -582,10 +639,9 @@ class DynamicScheduler {
         std::vector<double> val;
         std::vector<int64_t> ts;
         if (!parse(v->nodes, parse_threads_, &val, &ts, err)) return nullptr;
-        const size_t M = (size_t)crane_dyn_num_metrics(eng_);
-        if (crane_dyn_upload_nodes(eng_, (int64_t)N, 0, val.data(), ts.data(), val.data() + M * N,
-                                   ts.data() + M * N)) {
-            *err = crane_dyn_last_error(eng_);
+        const size_t M = (size_t)eng_.num_metrics();
+        if (eng_.upload_nodes((int64_t)N, val.data(), ts.data(), val.data() + M * N, ts.data() + M * N)) {
+            *err = eng_.error();
             return nullptr;
         }
         ++cnt_.full_syncs;
@@ -601,10 +657,9 @@ class DynamicScheduler {
                 ct[m] = ts[m * N];
             }
             const int64_t r0 = 0;
-            if (crane_dyn_update_node_steps(eng_, 1, &r0, cv.data(), ct.data(), cv.data() + M, ct.data() + M, v->t0,
-                                            v->t1, v->n_steps.data(), v->bp.data(), v->first_fail.data(),
-                                            v->score.data())) {
-                *err = crane_dyn_last_error(eng_);
+            if (eng_.update_node_steps(1, &r0, cv.data(), ct.data(), cv.data() + M, ct.data() + M, v->t0, v->t1,
+                                       v->n_steps.data(), v->bp.data(), v->first_fail.data(), v->score.data())) {
+                *err = eng_.error();
                 return nullptr;
             }
         }
@@ -628,8 +683,8 @@ class DynamicScheduler {
         if (added_.size() > v->free_rows.size()) {
             const size_t rows = v->rows(), need = added_.size() - v->free_rows.size();
             const size_t cap = rows + std::max(need, rows / 8 + 64);
-            if (crane_dyn_resize_nodes(eng_, (int64_t)cap)) {
-                *err = crane_dyn_last_error(eng_);
+            if (eng_.resize_nodes((int64_t)cap)) {
+                *err = eng_.error();
                 return false;
             }
             v->grow(cap);
@@ -682,7 +737,7 @@ class DynamicScheduler {
                                    .count();
             }
         } et{cnt_, te};
-        const size_t M = (size_t)crane_dyn_num_metrics(eng_);
+        const size_t M = (size_t)eng_.num_metrics();
         auto record = [&] {
             for (size_t j = 0; j < k; ++j) {
                 const size_t i = (size_t)changed_[j];
@@ -695,9 +750,9 @@ class DynamicScheduler {
             cnt_.nodes_updated += k;
         };
         if (now < v->t0 || now >= v->t1) {  // the caller rebuilds the whole table: the columns only
-            if (crane_dyn_update_nodes(eng_, (int64_t)k, changed_.data(), val.data(), ts.data(), val.data() + M * k,
-                                       ts.data() + M * k)) {
-                *err = crane_dyn_last_error(eng_);
+            if (eng_.update_nodes((int64_t)k, changed_.data(), val.data(), ts.data(), val.data() + M * k,
+                                  ts.data() + M * k)) {
+                *err = eng_.error();
                 return false;
             }
             record();
@@ -709,10 +764,10 @@ class DynamicScheduler {
         rbp_.resize(k * S);
         rff_.resize(k * (S + 1));
         rsc_.resize(k * (S + 1));
-        if (crane_dyn_update_node_steps(eng_, (int64_t)k, changed_.data(), val.data(), ts.data(), val.data() + M * k,
-                                        ts.data() + M * k, v->t0, v->t1, rns_.data(), rbp_.data(), rff_.data(),
-                                        rsc_.data())) {
-            *err = crane_dyn_last_error(eng_);
+        if (eng_.update_node_steps((int64_t)k, changed_.data(), val.data(), ts.data(), val.data() + M * k,
+                                   ts.data() + M * k, v->t0, v->t1, rns_.data(), rbp_.data(), rff_.data(),
+                                   rsc_.data())) {
+            *err = eng_.error();
             return false;
         }
         for (size_t j = 0; j < k; ++j) {
@@ -887,7 +942,7 @@ class DynamicScheduler {
 
     Handle handle_;
     crane_policy_doc* doc_ = nullptr;
-    crane_dyn* eng_ = nullptr;
+    Backend eng_;
     crane_tz* zone_ = nullptr;  // the IANA zone of $TZ, or null: the fixed offset tz_
     int64_t tz_ = 8 * 3600;
     int32_t parse_threads_ = 16;  // the framework's parallelism (upstream default)
@@ -927,10 +982,8 @@ inline std::pair<std::unique_ptr<DynamicScheduler>, std::string> NewDynamicSched
     const std::string zname = tzenv && *tzenv ? tzenv : "Asia/Shanghai";
     if (crane_tz_load(zname.c_str(), nullptr, &ds->zone_) && crane_tz_offset(zname.c_str(), &ds->tz_))
         return {nullptr, "unknown time zone " + zname};
-    if (crane_dyn_create(crane_policy_view(doc), h.device, &ds->eng_)) {
-        std::string e = ds->eng_ ? crane_dyn_last_error(ds->eng_) : "engine creation failed";
-        return {nullptr, "failed to create the Dynamic engine: " + e};
-    }
+    if (ds->eng_.create(crane_policy_view(doc), h))
+        return {nullptr, std::string("failed to create the Dynamic engine: ") + ds->eng_.error()};
     return {std::move(ds), ""};
 }
 

@@ -18,6 +18,8 @@
 //                            of them on a Clone() of the cycle state (preemption dry runs)
 //   counters                 the plugin's sync counters
 //   horizon <ns>             SetHorizon (a finite table span; default: the whole time axis)
+//   devices <list>           Handle::devices for the next `policy` (comma-separated: the plugin's nodes
+//                            sharded over them through the group, crane_dyn_group_*)
 // The node-shard group through the C ABI (crane_dyn_group_*), over the same snapshot and policy:
 //   group <devices> <depth> <collective> <threads>   crane_dyn_group_create over the comma-separated
 //                            device list, options set, the snapshot's annotations parsed (the plugin's
@@ -112,6 +114,13 @@ int main() {
             }
             ds = std::move(r.first);
             std::cout << "NEW\t" << ds->name() << "\t" << (ds->ScoreExtensions() == nullptr) << "\n";
+        } else if (f[0] == "devices") {
+            h.devices.clear();
+            for (size_t a = 0, b; a <= f[1].size(); a = b + 1) {
+                b = f[1].find(',', a);
+                if (b == std::string::npos) b = f[1].size();
+                h.devices.push_back((int32_t)std::stoi(f[1].substr(a, b - a)));
+            }
         } else if (f[0] == "badargs") {
             auto r = NewDynamicScheduler(Other(), h);
             std::cout << "NEWERR\t" << r.second << "\n";
@@ -207,7 +216,8 @@ int main() {
         } else if (f[0] == "counters") {
             const auto c = ds->counters();
             std::cout << "C\t" << c.tables_built << "\t" << c.full_syncs << "\t" << c.incremental_syncs << "\t"
-                      << c.nodes_updated << "\t" << c.nodes_joined << "\t" << c.nodes_left << "\t" << c.grows << "\n";
+                      << c.nodes_updated << "\t" << c.nodes_joined << "\t" << c.nodes_left << "\t" << c.grows << "\t"
+                      << ds->Shards() << "\n";
         } else if (f[0] == "mt") {
             Pod pod;
             pod.UID = pod.Name = f[1];

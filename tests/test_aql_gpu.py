@@ -124,6 +124,8 @@ def test_group_dispatch_queues(threads):
 
 
 def test_group_dispatch_refuses_collective():
+    """Queues with the PER-BATCH collective are refused (RCCL follows each batch on its HIP stream);
+    the batch form takes both (test_group_state_gpu.py)."""
     import torch
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 500, 64, n_bindings=100, seed=20250306)
@@ -134,7 +136,7 @@ def test_group_dispatch_refuses_collective():
     g.upload_nodes(val, ts, c.hv, c.hv_ts)
     dev = torch.device("cuda", 0)
     k = torch.empty(64, dtype=torch.int64, device=dev)
-    with pytest.raises(cd.CraneError, match="no collective"):
+    with pytest.raises(cd.CraneError, match="per-batch collective"):
         g.step_keys_async(int(synth.NOW0_NS), int(synth.NOW0_NS), [torch.from_numpy(c.now).to(dev)], None, [k])
     g.close()
 

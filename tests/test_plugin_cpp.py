@@ -124,8 +124,8 @@ def _stamp(unix_s):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("horizon", ["all", "finite"])
-def test_churn_through_plugin(driver, cluster_small, tmp_path, horizon):
+@pytest.mark.parametrize("horizon,shards", [("all", 1), ("finite", 1), ("all", 3)])
+def test_churn_through_plugin(driver, cluster_small, tmp_path, horizon, shards):
     """The controller keeps patching annotations between scheduling cycles (node.go:88-96,
     123-146): each patch publishes a new Node object.  The plugin re-parses only the changed
     nodes (crane_dyn_update_node_steps) and must answer every Filter / Score exactly as the
@@ -133,7 +133,9 @@ def test_churn_through_plugin(driver, cluster_small, tmp_path, horizon):
     the patched annotation maps.  Nodes join (a free row, or the shard grows:
     crane_dyn_resize_nodes) and leave (their rows freed; the freed NodeInfo addresses may come
     back for a new node) without a full resync.  Tables over the whole time axis (the default)
-    never need rebuilding; pods are hours apart here."""
+    never need rebuilding; pods are hours apart here. With three shards (Handle::devices, the group's routed
+    calls: crane_dyn_group_upload_nodes / _update_node_steps / _resize_nodes / _node_steps) the
+    answers are the same."""
     import numpy as np
     from oracle import oracle as O
     c = cluster_small
@@ -142,7 +144,7 @@ def test_churn_through_plugin(driver, cluster_small, tmp_path, horizon):
     names = [f"node-{i}" for i in range(len(nodes))]
     keys = [n for n, _ in pol["syncPolicy"]] + ["node_hot_value"]
     rng = np.random.default_rng(5150)
-    lines = [f"policy\t{write_policy(tmp_path, pol)}"]
+    lines = ([f"devices\t{','.join(['0'] * shards)}"] if shards > 1 else []) + [f"policy\t{write_policy(tmp_path, pol)}"]
     for i, a in enumerate(nodes):
         lines.append(f"node\t{names[i]}")
         lines += [f"anno\t{k}\t{v}" for k, v in a.items()]
@@ -182,7 +184,7 @@ def test_churn_through_plugin(driver, cluster_small, tmp_path, horizon):
         expect.append((ff[0].copy(), sc[0].copy(), list(names)))
     lines.append("counters")
     if horizon == "finite":
-        lines.insert(1, "horizon\t60000000000")
+        lines.insert(lines.index(next(x for x in lines if x.startswith("policy"))) + 1, "horizon\t60000000000")
     out = run(driver, "\n".join(lines) + "\n")
     F = [o for o in out if o[0] == "F"]
     S = [o for o in out if o[0] == "S"]
@@ -198,7 +200,8 @@ def test_churn_through_plugin(driver, cluster_small, tmp_path, horizon):
             assert s[3] == str(sc[n]), (p, n)
         off += len(nm)
     C = [o for o in out if o[0] == "C"][0]
-    tables, full, incr, upd, joined, left, grows = (int(x) for x in C[1:8])
+    tables, full, incr, upd, joined, left, grows, nshards = (int(x) for x in C[1:9])
+    assert nshards == shards
     assert full == 1  # the first cycle only: joins and departures are incremental
     assert joined == n_joined and left == n_left and grows >= 1
     assert incr >= len(pods) - 3 and upd >= incr
