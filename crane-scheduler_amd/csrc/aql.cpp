@@ -10,6 +10,8 @@
 
 #include <cxxabi.h>
 
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <map>
@@ -136,6 +138,7 @@ struct crane_queue {
     hsa_signal_t sig{0};  // committed steps still running
     unsigned char* ring = nullptr;  // kernarg slot of packet i: ring + (i % kQueuePackets) * kSlotBytes
     uint64_t first = 0, next = 0;   // packets [first, next) written, not yet committed
+    std::atomic<uint64_t> commits{0};  // commits so far (each adds one to sig, its last packet takes one)
     std::unordered_map<const void*, KInfo> kinfo;  // per host stub
     std::string err;
     std::mutex umu;
@@ -165,13 +168,6 @@ __global__ void k_aql_selfcheck(uint32_t* out) {
             out[5] = blockDim.z;
         }
     }
-}
-
-// A device flag set once the queue's packets before it are done (aql_flag): what a HIP stream
-// waits for (hipStreamWaitValue64) to order work after a queue's steps — the group's collective
-// after its batches.  System scope: the waiting stream's packet processor reads the flag.
-__global__ void k_aql_flag(uint64_t* p, uint64_t v) {
-    if (threadIdx.x == 0) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 const char* aql_error(const crane_queue* q) { return q ? q->err.c_str() : "null queue"; }
@@ -289,6 +285,7 @@ hipError_t aql_commit(crane_queue* q) {
     const uint64_t last = q->next - 1;
     packet(q, last)->completion_signal = q->sig;
     hsa_signal_add_relaxed(q->sig, 1);
+    q->commits.fetch_add(1, std::memory_order_release);
     if (q->ring_kind == 0) {
         // the kernargs went through write-combining BAR stores: fence them and read one back so
         // they are in device memory before the packet processor can fetch them
@@ -318,13 +315,14 @@ hipError_t aql_commit(crane_queue* q) {
     return hipSuccess;
 }
 
-hipError_t aql_flag(crane_queue* q, uint64_t* flag, uint64_t value) {
-    unsigned char args[16];
-    size_t off = 0;
-    aql_pack(args, off, flag);
-    aql_pack(args, off, value);
-    hipError_t e = aql_launch(q, reinterpret_cast<const void*>(&k_aql_flag), dim3(1), dim3(64), 0, args, off);
-    return e == hipSuccess ? aql_commit(q) : e;
+uint64_t aql_commits(const crane_queue* q) { return q->commits.load(std::memory_order_acquire); }
+
+uint64_t aql_completed(const crane_queue* q) {
+    // (the signal counts the commits still running; read after the count so a commit between the
+    // two reads makes the result smaller, never larger)
+    const uint64_t c = q->commits.load(std::memory_order_acquire);
+    const hsa_signal_value_t v = hsa_signal_load_scacquire(q->sig);
+    return v <= 0 ? c : c - std::min<uint64_t>(c, (uint64_t)v);
 }
 
 hipError_t aql_wait(crane_queue* q) {

@@ -36,9 +36,11 @@ hipError_t aql_launch(crane_queue* q, const void* host_fn, dim3 grid, dim3 block
 hipError_t aql_commit(crane_queue* q);
 // commit, then wait until every committed packet has completed
 hipError_t aql_wait(crane_queue* q);
-// a packet after the ones written so far that stores `value` to *flag (signal memory) when they
-// are done, committed: a HIP stream ordered after them waits for it (hipStreamWaitValue64)
-hipError_t aql_flag(crane_queue* q, uint64_t* flag, uint64_t value);
+// commits (steps) made visible on the queue so far, and how many of them have completed (in
+// order: a queue runs its packets one after the other) — what a host thread polls to order work
+// after a step without a device-side wait
+uint64_t aql_commits(const crane_queue* q);
+uint64_t aql_completed(const crane_queue* q);
 const char* aql_error(const crane_queue* q);
 // Engines that put steps on a queue register with it (crane_dyn_step_keys_queue), so whichever of
 // the two is destroyed first can tell the other: a queue's destroy hands itself back to every

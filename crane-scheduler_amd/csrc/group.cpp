@@ -13,8 +13,8 @@
 // K3 Filter/Score/argmax, engine.hip) on every device; the keys are then max-combined by an
 // in-place ncclAllReduce(int64, ncclMax): per batch (crane_dyn_group_step_keys_async, on the
 // slot's stream), or once per group of G batches over their keys [G][P]
-// (crane_dyn_group_step_keys_batch, on a collective stream per device ordered after the batches'
-// dispatch queues by a device flag the last packet of each slot writes).
+// (crane_dyn_group_step_keys_batch, on a collective stream per device, issued by the enqueueing
+// thread once it sees the slots' dispatch queues complete the window's steps).
 //
 // The shard's state changes go to the shard's slot-0 engine (its slots follow, engine.hip
 // adopt), routed by global node index: the controller's patches (update_nodes /
@@ -38,6 +38,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -76,9 +77,19 @@ struct GroupWorker;
 // What the thread that enqueues for a shard (its worker, or the caller) keeps per shard
 struct DevCtx {
     hipStream_t cstream = nullptr;    // the group collective's stream
-    std::vector<uint64_t*> flag;      // [slot] signal memory the slot's queue sets (aql_flag)
-    std::vector<uint64_t> seq;        // [slot] the last value asked of flag[slot]
     std::vector<hipEvent_t> slot_ev;  // [slot] after the slot's last batch (HIP-stream steps)
+    // group collectives after batches on dispatch queues, not issued yet: issued (in order) once
+    // the host sees every slot's queue complete the steps the window committed on it (a queue is
+    // ordered with no HIP stream; a device-side wait on a flag the queue writes,
+    // hipStreamWaitValue64, runs as a polling kernel that holds the GPU meanwhile: measured
+    // 0.0125 -> 0.026 ms per batch at config 3 on one device)
+    struct PendColl {
+        int64_t* keys;
+        int64_t count;
+        std::vector<uint64_t> target;  // [slot] commits of the slot's queue to complete (0: none)
+        std::chrono::steady_clock::time_point t0;
+    };
+    std::deque<PendColl> pcoll;
     struct Pending {                  // a group collective in flight over [p, p + bytes)
         const char* p;
         size_t bytes;
@@ -148,22 +159,47 @@ int engine_err(crane_dyn_group* g, crane_dyn* e, int rc, int i) {
     return rc;
 }
 
-// the collective stream of shard i waits for slot s's work so far (its queue's flag packet, or an
-// event on its stream); called by the thread enqueueing for the shard
-hipError_t order_after_slot(crane_dyn_group* g, int i, int s, bool qmode) {
+// the collective stream of shard i waits for slot s's work so far on its HIP stream (steps
+// launched through HIP); called by the thread enqueueing for the shard
+hipError_t order_after_slot(crane_dyn_group* g, int i, int s) {
     DevCtx& c = g->ctx[(size_t)i];
-    if (crane_queue* qq = qmode ? g->queue(s, i) : nullptr) {
-        const uint64_t v = ++c.seq[(size_t)s];
-        hipError_t e = crane::aql_flag(qq, c.flag[(size_t)s], v);
-        if (e != hipSuccess) return e;
-        return hipStreamWaitValue64(c.cstream, c.flag[(size_t)s], v, hipStreamWaitValueGte, ~0ull);
-    }
     hipError_t e = hipEventRecord(c.slot_ev[(size_t)s], g->st[(size_t)s][(size_t)i]);
     return e == hipSuccess ? hipStreamWaitEvent(c.cstream, c.slot_ev[(size_t)s], 0) : e;
 }
 
+// a group collective after steps on dispatch queues: held until the queues completed them
+void pcoll_push(crane_dyn_group* g, int i, const Job& j) {
+    DevCtx::PendColl pc{j.d_keys, j.count, std::vector<uint64_t>((size_t)g->depth, 0),
+                        std::chrono::steady_clock::now()};
+    for (int sl = 0; sl < g->depth; ++sl)
+        if (j.slots >> sl & 1)
+            if (crane_queue* qq = g->queue(sl, i)) pc.target[(size_t)sl] = crane::aql_commits(qq);
+    g->ctx[(size_t)i].pcoll.push_back(std::move(pc));
+}
+
+// 1: the oldest held collective of shard i may be issued, 0: not yet, <0: its steps did not finish
+// within 60 s (a fault or a hang: reported, not waited for forever)
+int pcoll_ready(crane_dyn_group* g, int i) {
+    const DevCtx::PendColl& pc = g->ctx[(size_t)i].pcoll.front();
+    for (int sl = 0; sl < g->depth; ++sl)
+        if (pc.target[(size_t)sl] && crane::aql_completed(g->queue(sl, i)) < pc.target[(size_t)sl])
+            return std::chrono::steady_clock::now() - pc.t0 > std::chrono::seconds(60) ? -1 : 0;
+    return 1;
+}
+
+// a held (not yet issued) group collective of shard i over keys at [p, p + bytes)
+bool held_overlap(const crane_dyn_group* g, int i, const void* p, size_t bytes) {
+    const char* a = static_cast<const char*>(p);
+    for (const auto& pc : g->ctx[(size_t)i].pcoll) {
+        const char* k = reinterpret_cast<const char*>(pc.keys);
+        if (k < a + bytes && a < k + sizeof(int64_t) * (size_t)pc.count) return true;
+    }
+    return false;
+}
+
 // before a batch writes keys at [p, p + bytes) on shard i: a group collective still reducing
 // (in place) keys there is waited for — callers alternate key buffers, so this rarely blocks
+// (a held one is issued first by the caller of this: held_overlap)
 hipError_t wait_pending(crane_dyn_group* g, int i, const void* p, size_t bytes) {
     DevCtx& c = g->ctx[(size_t)i];
     const char* a = static_cast<const char*>(p);
@@ -190,9 +226,10 @@ int run_job_dev(crane_dyn_group* g, int i, const Job& j, std::string* msg) {
             *msg = who + ": " + hipGetErrorString(r);
             return CRANE_E_HIP;
         }
+        if (j.qmode) return 0;  // (held until the queues completed the window: pcoll_push)
         for (int sl = 0; sl < g->depth; ++sl)
             if (j.slots >> sl & 1)
-                if (hipError_t r = order_after_slot(g, i, sl, j.qmode)) {
+                if (hipError_t r = order_after_slot(g, i, sl)) {
                     *msg = who + ": ordering the collective: " + hipGetErrorString(r);
                     return CRANE_E_HIP;
                 }
@@ -228,6 +265,7 @@ int run_job_dev(crane_dyn_group* g, int i, const Job& j, std::string* msg) {
 // completion, for wait_pending
 hipError_t note_pending(crane_dyn_group* g, int i, const Job& j) {
     DevCtx& c = g->ctx[(size_t)i];
+    if (hipError_t e = hipSetDevice(g->dev[(size_t)i])) return e;
     hipEvent_t ev = nullptr;
     if (!c.free_ev.empty()) {
         ev = c.free_ev.back();
@@ -242,6 +280,24 @@ hipError_t note_pending(crane_dyn_group* g, int i, const Job& j) {
     }
     c.pending.push_back({reinterpret_cast<const char*>(j.d_keys), sizeof(int64_t) * (size_t)j.count, ev});
     return hipSuccess;
+}
+
+// a held group collective issued on shard i's collective stream (ncclAllReduce, in place)
+int issue_held(crane_dyn_group* g, int i, const DevCtx::PendColl& pc, std::string* msg) {
+    ncclResult_t r = ncclAllReduce(pc.keys, pc.keys, (size_t)pc.count, ncclInt64, ncclMax, g->comm[(size_t)i],
+                                   g->ctx[(size_t)i].cstream);
+    if (r != ncclSuccess) {
+        *msg = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
+        return CRANE_E_HIP;
+    }
+    Job j;
+    j.d_keys = pc.keys;
+    j.count = pc.count;
+    if (hipError_t e = note_pending(g, i, j)) {
+        *msg = hipGetErrorString(e);
+        return CRANE_E_HIP;
+    }
+    return 0;
 }
 
 bool has_coll(const Job& j) { return (j.kind == kJobStep && j.per_batch_coll) || j.kind == kJobGroupColl; }
@@ -261,6 +317,7 @@ struct GroupWorker {
     std::atomic<uint64_t> head{0}, tail{0};
     std::atomic<bool> stop{false};
     std::atomic<int> sleeping{0};
+    std::atomic<int> held{0};  // group collectives held for their queues (DevCtx::pcoll)
     std::mutex m;
     std::condition_variable cv;
     std::mutex emu;
@@ -280,13 +337,39 @@ struct GroupWorker {
     // even after a failed step: the other devices' all-reduce kernels wait for this one's)
     void run_job(const Job& j) {
         std::string msg;
+        if (j.kind == kJobStep)  // (keys a held collective will reduce: it goes first)
+            while (held_overlap(g, i, j.d_keys, sizeof(int64_t) * (size_t)j.P)) {
+                progress();
+                cpu_relax();
+            }
         if (int rc = run_job_dev(g, i, j, &msg)) record(rc, msg);
+        if (j.kind == kJobGroupColl && j.qmode) {  // held until the queues completed the window
+            pcoll_push(g, i, j);
+            progress();
+            return;
+        }
         if (!has_coll(j) || coll_count(j) <= 0) return;
         ncclResult_t r = ncclAllReduce(j.d_keys, j.d_keys, (size_t)coll_count(j), ncclInt64, ncclMax,
                                        g->comm[(size_t)i], coll_stream(g, j, i));
         if (r != ncclSuccess) record(CRANE_E_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
         if (j.kind == kJobGroupColl)
             if (hipError_t e = note_pending(g, i, j)) record(CRANE_E_HIP, hipGetErrorString(e));
+    }
+
+    // the held collectives whose queues completed their windows, in order (every device issues
+    // its part of the same sequence); one whose steps did not finish within 60 s is dropped and
+    // reported (wait_all then aborts the communicators)
+    void progress() {
+        auto& pc = g->ctx[(size_t)i].pcoll;
+        while (!pc.empty()) {
+            const int r = pcoll_ready(g, i);
+            if (r == 0) break;
+            std::string msg;
+            if (r < 0) record(CRANE_E_HIP, "the steps before a group collective did not finish within 60 s");
+            else if (int rc = issue_held(g, i, pc.front(), &msg)) record(rc, msg);
+            pc.pop_front();
+        }
+        held.store((int)pc.size(), std::memory_order_release);
     }
 
     void loop() {
@@ -296,6 +379,11 @@ struct GroupWorker {
             uint64_t h = head.load(std::memory_order_acquire);
             for (int spins = 0; h == t; h = head.load(std::memory_order_acquire)) {
                 if (stop.load(std::memory_order_acquire)) return;
+                if (held.load(std::memory_order_relaxed)) {  // (no sleep while collectives are held)
+                    progress();
+                    cpu_relax();
+                    continue;
+                }
                 if (++spins < (1 << 14)) {
                     cpu_relax();
                     continue;
@@ -329,7 +417,9 @@ struct GroupWorker {
     }
 
     void drain() const {
-        while (tail.load(std::memory_order_acquire) != head.load(std::memory_order_acquire)) cpu_relax();
+        while (tail.load(std::memory_order_acquire) != head.load(std::memory_order_acquire) ||
+               held.load(std::memory_order_acquire))
+            cpu_relax();
     }
 };
 
@@ -362,26 +452,68 @@ int ensure_ctx(crane_dyn_group* g) {
         DevCtx& c = g->ctx[(size_t)i];
         if (c.cstream) continue;
         hipError_t e = hipSetDevice(g->dev[(size_t)i]);
-        c.flag.assign((size_t)g->depth, nullptr);
-        c.seq.assign((size_t)g->depth, 0);
         c.slot_ev.assign((size_t)g->depth, nullptr);
-        for (int s = 0; s < g->depth && e == hipSuccess; ++s) {
-            e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c.flag[(size_t)s]), sizeof(uint64_t),
-                                      hipMallocSignalMemory);
-            if (e == hipSuccess) e = hipMemset(c.flag[(size_t)s], 0, sizeof(uint64_t));
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&c.slot_ev[(size_t)s], hipEventDisableTiming);
-        }
-        if (e == hipSuccess) e = hipDeviceSynchronize();  // (the flags' fills before any wait on them)
+        for (int s = 0; s < g->depth && e == hipSuccess; ++s)
+            e = hipEventCreateWithFlags(&c.slot_ev[(size_t)s], hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&c.cstream, hipStreamNonBlocking);
-        if (e != hipSuccess) return g->hipfail(e, "collective stream / flags");
+        if (e != hipSuccess) return g->hipfail(e, "collective stream / events");
     }
     return 0;
+}
+
+// the caller's thread (threads 0): the held collectives whose queues completed, on every device at
+// once (grouped), in order
+int progress_here(crane_dyn_group* g) {
+    int rc = 0;
+    for (;;) {
+        bool all = true, late = false;
+        for (int i = 0; i < g->n && all; ++i) {
+            if (g->ctx[(size_t)i].pcoll.empty()) return rc;
+            const int r = pcoll_ready(g, i);
+            all = r != 0;
+            late = late || r < 0;
+        }
+        if (!all) return rc;
+        if (late) {
+            if (!rc) rc = g->fail(CRANE_E_HIP, "the steps before a group collective did not finish within 60 s");
+        } else {
+            ncclResult_t r = ncclGroupStart();
+            std::string msg;
+            for (int i = 0; i < g->n && r == ncclSuccess; ++i) {
+                const auto& pc = g->ctx[(size_t)i].pcoll.front();
+                r = ncclAllReduce(pc.keys, pc.keys, (size_t)pc.count, ncclInt64, ncclMax, g->comm[(size_t)i],
+                                  g->ctx[(size_t)i].cstream);
+            }
+            const ncclResult_t r2 = ncclGroupEnd();
+            if (r != ncclSuccess && !rc) rc = g->ncclfail(r, "ncclAllReduce");
+            if (r2 != ncclSuccess && !rc) rc = g->ncclfail(r2, "ncclGroupEnd");
+            for (int i = 0; i < g->n; ++i) {
+                Job j;
+                j.d_keys = g->ctx[(size_t)i].pcoll.front().keys;
+                j.count = g->ctx[(size_t)i].pcoll.front().count;
+                if (hipError_t e = note_pending(g, i, j))
+                    if (!rc) rc = g->hipfail(e, "collective event");
+            }
+        }
+        for (int i = 0; i < g->n; ++i) g->ctx[(size_t)i].pcoll.pop_front();
+    }
 }
 
 // wait for every pushed job, the used slots' streams and queues and the collective streams; the
 // first error since the last wait
 int wait_all(crane_dyn_group* g) {
     int rc = 0;
+    if (g->workers.empty()) {  // (caller's thread: its held collectives, issued as their queues finish)
+        for (bool held = true; held;) {
+            if (int r = progress_here(g)) {
+                if (!rc) rc = r;
+                for (auto& c : g->ctx) c.pcoll.clear();
+            }
+            held = false;
+            for (auto& c : g->ctx) held = held || !c.pcoll.empty();
+            if (held) cpu_relax();
+        }
+    }
     for (auto& w : g->workers) {
         w->drain();
         std::lock_guard<std::mutex> l(w->emu);
@@ -459,12 +591,19 @@ int run_here(crane_dyn_group* g, const Job& j, const int64_t* const* d_now, cons
         ji.d_now = d_now ? d_now[i] : nullptr;
         ji.d_flags = d_flags ? d_flags[i] : nullptr;
         ji.d_keys = d_keys[i];
+        if (j.kind == kJobStep)  // (keys a held collective will reduce: it goes first)
+            while (held_overlap(g, i, ji.d_keys, sizeof(int64_t) * (size_t)j.P)) {
+                if (int rc = progress_here(g)) return rc;
+                cpu_relax();
+            }
         std::string msg;
         if (int rc = run_job_dev(g, i, ji, &msg)) {
             g->err = msg;
             return rc;
         }
+        if (j.kind == kJobGroupColl && j.qmode) pcoll_push(g, i, ji);
     }
+    if (j.kind == kJobGroupColl && j.qmode) return progress_here(g);
     if (!has_coll(j) || coll_count(j) <= 0) return 0;
     ncclResult_t r = ncclGroupStart();
     for (int i = 0; i < g->n && r == ncclSuccess; ++i)
@@ -704,8 +843,6 @@ int crane_dyn_group_destroy(crane_dyn_group* g) {
         for (size_t i = 0; i < g->ctx.size(); ++i) {
             DevCtx& c = g->ctx[i];
             (void)hipSetDevice(g->dev[i]);
-            for (uint64_t* f : c.flag)
-                if (f) (void)hipFree(f);
             for (hipEvent_t ev : c.slot_ev)
                 if (ev) (void)hipEventDestroy(ev);
             for (auto& pe : c.pending) (void)hipEventDestroy(pe.ev);

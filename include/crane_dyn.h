@@ -413,9 +413,10 @@ int crane_dyn_group_step_keys_async(crane_dyn_group *g, int64_t now_ns, int64_t 
  * likewise or NULL) into d_keys[i] + b * n_pods, on slot (the group's batch count) % depth, its
  * kernels on the slot's dispatch queue unless "dispatch" is 0; then, with the collective on, one
  * in-place ncclAllReduce(int64, max) of the whole [n_batches][n_pods] keys per device on a
- * collective stream of the group, ordered after those batches' queues (a device flag written by
- * each slot's last packet, hipStreamWaitValue64) — the per-batch all-reduce's latency paid once per
- * G batches, as a scheduler collecting a window of batches' choices would.  A later batch that
+ * collective stream of the group, issued by the thread enqueueing for the device once it sees the
+ * slots' dispatch queues complete the window's steps (with HIP launches: ordered by events) — the
+ * per-batch all-reduce's latency paid once per G batches, as a scheduler collecting a window of
+ * batches' choices would.  A later batch that
  * writes keys where that all-reduce still works waits for it (host side): alternate two key
  * buffers.  Errors of the enqueued work are reported by crane_dyn_group_sync. */
 int crane_dyn_group_step_keys_batch(crane_dyn_group *g, int32_t n_batches, const int64_t *now_ns,
