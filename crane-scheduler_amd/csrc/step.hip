@@ -103,9 +103,11 @@ __global__ __launch_bounds__(kStepSeg) void k3a_steps(const NodeRec<PD, PR>* __r
 // key is the max over its leaf's ancestors, the kind's uniform maximum and
 // what the other workgroups of the tile merge: one 64-bit atomicMax per pod
 // per workgroup.
-constexpr int kK3sWaves = 4;
+// 8 waves (512 lanes, 2 pods per lane) against 4: K3s 10.6 -> 9.6 us at config 3, 65.4 ->
+// 61 us at config 4 on one GPU, same box (profiles/r06/ab/k1_first_entry_rows_dropped_k3s_8waves.txt)
+constexpr int kK3sWaves = 8;
 constexpr int kK3sThreads = kK3sWaves * 64;
-constexpr int kK3sPPL = 4;                          // pods per lane
+constexpr int kK3sPPL = 1024 / kK3sThreads;         // pods per lane
 constexpr int kK3sPods = kK3sThreads * kK3sPPL;     // pods per workgroup (= kPodTile)
 // producer blocks per workgroup aimed for (launches over kMaxWg workgroups are capped first):
 // 64 -> config 3 (391 blocks) and the config-4 shard (489) take 8 workgroups per tile.  Round 3,
@@ -122,6 +124,7 @@ constexpr int kK3sListBlk = 64;
 constexpr int kK3sRecList = 512;
 constexpr int kK3sPieceList = 512;
 static_assert(kK3sMaxBlk <= kK3sThreads, "at least one lane per producer block");
+static_assert(4 * kK3sListBlk <= 256, "list entries index the item map in 8 bits");
 static_assert(kK3sPods == kPodTile, "a workgroup resolves one K3p tile");
 
 // The four counts "records of kind T with bp <= t" (t = the kind's lo, then hi)
@@ -192,6 +195,9 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     __shared__ int32_t wpre[4 * kK3sListBlk + 1];
     __shared__ int32_t wjl[2 * kK3sListBlk];
     __shared__ int32_t wpl[2 * kK3sListBlk];  // the first middle piece per (block, kind)
+    // item -> its entry: the list's records and pieces expanded (one LDS read per item instead of a
+    // binary search of the prefix, 8 dependent reads)
+    __shared__ uint8_t imap[kK3sRecList + kK3sPieceList];
     const int64_t b = blockIdx.x;
     CRANE_TSTAMP(st.trace, b, 0);
     const int32_t r = (int32_t)(b % R);
@@ -330,32 +336,54 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     const bool piece_list = lists && total - nrec <= kK3sPieceList;
     const bool rec_list = lists && nrec <= kK3sRecList;
     bool upd = false;  // this lane wrote the tree
-    for (int32_t it = threadIdx.x + (rec_list ? 0 : nrec); it < (piece_list ? total : nrec); it += kK3sThreads) {
-        // the entry holding item it: the last e with wpre[e] <= it, in its half
-        int32_t lo = it < nrec ? 0 : 2 * m, hi = it < nrec ? 2 * m - 1 : E - 1;
-        while (lo < hi) {
-            const int32_t mid = (lo + hi + 1) >> 1;
-            if (wpre[mid] <= it) lo = mid;
-            else hi = mid - 1;
+    const int32_t i0 = rec_list ? 0 : nrec, i1 = piece_list ? total : nrec;  // (workgroup-uniform)
+    if (i1 > i0) {
+        // the entries' items into the map (an entry's lane writes its run; E <= 256 entries)
+        for (int32_t e = threadIdx.x; e < E; e += kK3sThreads) {
+            const int32_t a = max(wpre[e], i0), z = min(wpre[e + 1], i1);
+            for (int32_t i = a; i < z; ++i) imap[i - i0] = (uint8_t)e;
         }
-        const bool rec = lo < 2 * m;
-        const int32_t ej = rec ? lo : lo - 2 * m, jb = ej >> 1, T = ej & 1, idx = it - wpre[lo];
-        const int64_t obj = xc + (int64_t)stride * (k0 + jb);
-        if (rec) {
-            // a one-step record stepping inside (lo, hi]: split the kind's slots
-            const Step1 r1 = (st.single + s1_at(st, T, obj))[wjl[2 * jb + T] + idx];
-            const int32_t sp = slot_lower(tt, klo[T], khi[T], r1.bp);
-            if (r1.k0 >= 0) tree_max(tree, klo[T], sp, r1.k0);
-            if (r1.k1 >= 0) tree_max(tree, sp, khi[T], r1.k1);
-            upd = true;
-        } else {
-            // a middle piece: covering -> uniform, overlapping partly -> range maximum over
-            // the slots with s <= now < e
-            const Mid pm = st.mid[(int64_t)T * st.mpad + obj * st.mstride + wpl[ej] + idx];
-            if (pm.s <= tlo[T] && pm.e > thi[T]) um[T] = max(um[T], pm.key);
-            else if (pm.s <= thi[T] && pm.e > tlo[T]) {
-                tree_max(tree, slot_lower(tt, klo[T], khi[T], pm.s), slot_lower(tt, klo[T], khi[T], pm.e), pm.key);
+        __syncthreads();
+        // every item of this lane: its entry, then its record / piece loads all in flight, then the
+        // searches and the tree
+        constexpr int kU = (kK3sRecList + kK3sPieceList) / kK3sThreads;
+        Step1 r1[kU];
+        Mid pm[kU];
+        int32_t ee[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int32_t it = i0 + u * kK3sThreads + (int32_t)threadIdx.x;
+            ee[u] = -1;
+            if (it >= i1) continue;
+            const int32_t e = imap[it - i0];
+            ee[u] = e;
+            const bool rec = e < 2 * m;
+            const int32_t ej = rec ? e : e - 2 * m, jb = ej >> 1, T = ej & 1, idx = it - wpre[e];
+            const int64_t obj = xc + (int64_t)stride * (k0 + jb);
+            if (rec) r1[u] = (st.single + s1_at(st, T, obj))[wjl[2 * jb + T] + idx];
+            else pm[u] = st.mid[(int64_t)T * st.mpad + obj * st.mstride + wpl[ej] + idx];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int32_t e = ee[u];
+            if (e < 0) continue;
+            const bool rec = e < 2 * m;
+            const int T = (rec ? e : e - 2 * m) & 1;
+            if (rec) {
+                // a one-step record stepping inside (lo, hi]: split the kind's slots
+                const int32_t sp = slot_lower(tt, klo[T], khi[T], r1[u].bp);
+                if (r1[u].k0 >= 0) tree_max(tree, klo[T], sp, r1[u].k0);
+                if (r1[u].k1 >= 0) tree_max(tree, sp, khi[T], r1[u].k1);
                 upd = true;
+            } else {
+                // a middle piece: covering -> uniform, overlapping partly -> range maximum over
+                // the slots with s <= now < e
+                const Mid& q = pm[u];
+                if (q.s <= tlo[T] && q.e > thi[T]) um[T] = max(um[T], q.key);
+                else if (q.s <= thi[T] && q.e > tlo[T]) {
+                    tree_max(tree, slot_lower(tt, klo[T], khi[T], q.s), slot_lower(tt, klo[T], khi[T], q.e), q.key);
+                    upd = true;
+                }
             }
         }
     }
