@@ -355,6 +355,7 @@ def cold_leg(cd, synth, spec, dev, reps=5, pmc=None, pmc_src=None, opts=()):
     c = synth.make_cluster(spec, N, P, n_bindings=B, seed=7)
     c.now, c.ds = synth.make_pods(P, seed=8)
     eng = cd.Engine(cd.Policy(spec), dev.index)
+    eng.set_option("k2_delta", 0)  # (every refresh here re-counts: the leg prices the whole suffix pass)
     for o in opts:
         k, v = o.split("=")
         eng.set_option(k, int(v))

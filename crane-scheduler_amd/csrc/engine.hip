@@ -133,6 +133,8 @@ struct Options {
     int k1_tail = 0;          // the streamed pass's tail: 0 on one wave when the grid has >= 4096 blocks
                               // (the other waves leave), 1 always on one wave, 4 on all four
     int k2_sorted = 1;        // a time-ordered log: K2 reads the widest window's suffix, ranks by position
+    int k2_delta = 1;         // ... and, once anchored, only the bindings whose window rank changed since
+                              // the anchor refresh (delta form, HotDelta); 0: every refresh re-counts
 };
 // Fixed launch shapes (round 6 removed their options; the A/B sweeps that chose them are in
 // profiles/ab/r03_k2_cold_*.txt and profiles/r05/config3_option_sweep_queues.txt)
@@ -205,6 +207,13 @@ struct crane_dyn {
     bool counts_pending = false;  // buckets hold K2 counts no node pass has consumed yet
     bool hx_pending = false;      // ... in the dedupe form: per-block entries in k2_sorted (hx_g)
     HotPart hx_g{};
+    // delta form (hot_delta_locked): dense anchor counts at suffix starts dl_pos (valid for log
+    // version dl_log_ver, N dl_N), the adjustments of the next node pass (zero unless dl_adj_dirty)
+    bool dl_valid = false, dl_pending = false, dl_adj_dirty = true;
+    uint64_t dl_log_ver = 0;
+    int64_t dl_N = -1, dl_B = -1;
+    int64_t dl_pos[kMaxWin] = {};
+    DevBuf<uint32_t> dl_base, dl_adj;
     // binding log on the device: B slots (node < 0 = empty slot)
     int64_t B = 0;
     bool heap_mode = false;
@@ -333,6 +342,7 @@ int adopt(crane_dyn* h) {
         h->hv_from_counts = false;
         h->counts_pending = false;
         h->hx_pending = false;
+        h->dl_pending = false;
         h->rec_dirty = true;
         h->sd_node_ver = d.node_ver;
     }
@@ -440,6 +450,92 @@ static int flatten_policy(crane_dyn* h, const crane_policy* pol) {
 
 // ------------------------------------------------------------- pipeline pieces
 
+// Zeroes a buffer the next kernels on `st` read: on a dispatch queue (no fill kernel there) after
+// the queue's packets, on the engine stream, waited for
+static int zero_for(crane_dyn* h, uint32_t* p, size_t n, hipStream_t st) {
+    if (tl_aql) {
+        HIPTRY(h, aql_wait(tl_aql));
+        HIPTRY(h, hipMemsetAsync(p, 0, n * sizeof(uint32_t), h->stream));
+        HIPTRY(h, hipStreamSynchronize(h->stream));
+    } else {
+        HIPTRY(h, hipMemsetAsync(p, 0, n * sizeof(uint32_t), st));
+    }
+    return CRANE_OK;
+}
+
+// Delta form of a time-ordered log's refresh (kernels.hpp HotDelta), after the suffix search
+// (h->pos_s): counts = the anchor's dense counts + the changed bindings' adjustments.  The first
+// refresh after the log or the node count changed, or one whose changed bindings pass half the
+// widest window's suffix, re-anchors here: the large form writes its dense counts as the new
+// anchor (adjustments zero).  *done false: the form does not apply (the caller's forms run).
+static int hot_delta_locked(crane_dyn* h, int64_t Bk, const HotCutoffs& pcut, hipStream_t st, const PodPrep* pods,
+                            bool* pods_done, bool* done) {
+    const DevPolicy& dp = h->dp;
+    const int nw = dp.n_win;
+    *done = false;
+    if (h->N <= 0 || h->N >= (1LL << 27) || nw < 1) return CRANE_OK;
+    const size_t nb = (size_t)nw * (size_t)h->N;
+    const bool anchored = h->dl_valid && h->dl_log_ver == h->sd_log_ver && h->dl_N == h->N && h->dl_B == h->B;
+    // the changed positions: per window rank r, between the anchor's and this refresh's suffix
+    // starts; merged
+    HotDelta d{};
+    d.n_win = nw;
+    int64_t L = 0;
+    if (anchored) {
+        std::pair<int64_t, int64_t> rg[kMaxWin];
+        int n = 0;
+        for (int r = 0; r < nw; ++r) {
+            d.a[r] = h->dl_pos[r];
+            d.p[r] = h->pos_s[r];
+            const int64_t lo = std::min(d.a[r], d.p[r]), hi = std::max(d.a[r], d.p[r]);
+            if (hi > lo) rg[n++] = {lo, hi};
+        }
+        std::sort(rg, rg + n);
+        int m = 0;
+        for (int i = 0; i < n; ++i) {
+            if (m > 0 && rg[i].first <= rg[m - 1].second) rg[m - 1].second = std::max(rg[m - 1].second, rg[i].second);
+            else rg[m++] = rg[i];
+        }
+        d.n_rng = m;
+        d.start[0] = 0;
+        for (int k = 0; k < m; ++k) {
+            d.lo[k] = rg[k].first;
+            d.start[k + 1] = d.start[k] + (rg[k].second - rg[k].first);
+        }
+        L = d.start[m];
+    }
+    if (h->dl_adj.n < nb) {
+        HIPTRY(h, h->dl_adj.reserve(nb));
+        h->dl_adj_dirty = true;
+    }
+    if (h->dl_adj_dirty) {  // (an earlier refresh's adjustments no node pass consumed, or a new buffer)
+        if (int rc = zero_for(h, h->dl_adj.p, h->dl_adj.n, st)) return rc;
+        h->dl_adj_dirty = false;
+    }
+    if (!anchored || 2 * L > Bk) {
+        const HotPart gl = hot_large_geometry(Bk, h->N, nw);
+        const HotPart gf = hot_large_geometry(h->B, h->N, nw);
+        if (!gl.ok) return CRANE_OK;
+        HIPTRY(h, h->dl_base.reserve(nb));
+        HIPTRY(h, h->k2_sorted.reserve(std::max(hot_dedupe_scratch(gl), gf.ok ? hot_dedupe_scratch(gf) : 0)));
+        h->dl_valid = false;
+        HIPTRY(h, launch_hot_count_large(h->sd->bnode.p + h->pos_s[0], h->sd->bts.p, Bk, h->N, pcut, gl,
+                                         h->k2_sorted.p, h->dl_base.p, h->n_cu, st, kK2lThreads));
+        std::memcpy(h->dl_pos, h->pos_s, sizeof(int64_t) * nw);
+        h->dl_valid = true;
+        h->dl_log_ver = h->sd_log_ver;
+        h->dl_N = h->N;
+        h->dl_B = h->B;
+    } else {
+        HIPTRY(h, launch_hot_count_delta(h->sd->bnode.p, h->N, d, h->dl_adj.p, st, pods));
+        if (pods_done) *pods_done = pods != nullptr && pods->P > 0;
+    }
+    h->dl_adj_dirty = true;  // (until the node pass reads and zeroes the adjustments)
+    h->dl_pending = true;
+    *done = true;
+    return CRANE_OK;
+}
+
 // pods (optional): the step path's pod preparation, launched together with K2x
 // when the dedupe K2 runs (*pods_done reports whether it did).
 static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hipStream_t st,
@@ -470,6 +566,7 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         if (cw >= 1 && cw <= 0xFFFFFFFFLL) make_div_magic((uint32_t)cw, &dp.win_div_m[r], &dp.win_div_sh[r]);
     }
     h->hx_pending = false;
+    h->dl_pending = false;
     h->counts_pending = true;
     h->hv_from_counts = true;
     h->hv_ts_counts = hv_ts_ns;
@@ -504,6 +601,11 @@ static int hot_values_locked(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, hip
         pcut.by_pos = 1;
         bn = h->sd->bnode.p + s0;
         Bk = h->B - s0;
+    }
+    if (by_pos && h->opt.k2_delta && h->opt.k2_form == 0) {
+        bool done = false;
+        const int rc = hot_delta_locked(h, Bk, pcut, st, pods, pods_done, &done);
+        if (rc || done) return rc;
     }
     HotPart gx = hot_dedupe_geometry(Bk, h->N, dp.n_win, kK1Block);
     gx.trace = gx.nblk <= kTraceWgs ? h->trace_region(0) : nullptr;
@@ -582,6 +684,10 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
             a.hx_region = h->k2_sorted.p;
             a.hx_CO = h->k2_sorted.p + g.cap;
             a.hx_nblk = g.nblk;
+        } else if (h->dl_pending) {
+            a.buckets = h->dl_adj.p;  // read and zeroed
+            a.bucket_base = h->dl_base.p;
+            a.buckets_keep = 0;
         } else {
             a.buckets = h->buckets.p;
             a.buckets_keep = h->buckets_dense ? 1 : 0;
@@ -598,9 +704,11 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
     a.trace = (h->N + a.threads - 1) / a.threads <= kTraceWgs ? h->trace_region(1) : nullptr;
     HIPTRY(h, launch_node_pass(h->shape, a, st, step, h->opt.k1_stream));
     if (consume) {
-        if (!h->hx_pending) h->buckets_zero = !h->buckets_dense;  // K1 zeroed what it read
+        if (h->dl_pending) h->dl_adj_dirty = false;  // K1 zeroed the adjustments
+        else if (!h->hx_pending) h->buckets_zero = !h->buckets_dense;  // K1 zeroed what it read
         h->counts_pending = false;
         h->hx_pending = false;
+        h->dl_pending = false;
     }
     h->rec_dirty = !keep;
     return CRANE_OK;
@@ -938,6 +1046,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "step_pieces" && range(0, 2)) o.step_pieces = (int)value;
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
     else if (n == "k2_sorted" && range(0, 1)) o.k2_sorted = (int)value;
+    else if (n == "k2_delta" && range(0, 1)) o.k2_delta = (int)value;
     else if (n == "k1_stream" && range(0, 1)) o.k1_stream = (int)value;
     else if (n == "k1_tail" && (value == 0 || value == 1 || value == 4)) o.k1_tail = (int)value;
     else if (n == "trace" && range(0, 1)) {
@@ -1002,6 +1111,7 @@ int crane_dyn_upload_nodes(crane_dyn* h, int64_t n, int64_t node_offset, const d
     h->hv_from_counts = false;
     h->counts_pending = false;
     h->hx_pending = false;
+    h->dl_pending = false;
     h->rec_dirty = true;
     publish_nodes(h);
     return CRANE_OK;
@@ -1537,6 +1647,7 @@ static int update_locked(crane_dyn* h, int64_t k, const int64_t* idx, const doub
         h->hv_from_counts = false;
         h->counts_pending = false;
         h->hx_pending = false;
+        h->dl_pending = false;
         h->rec_dirty = true;
     }
     if (hv && !h->have_hv) {  // the first hot-value annotations of the shard: the others have none
@@ -1707,6 +1818,7 @@ int crane_dyn_resize_nodes(crane_dyn* h, int64_t n) {
     h->hv_from_counts = false;  // binding-log hot values were per old node index
     h->counts_pending = false;
     h->hx_pending = false;
+    h->dl_pending = false;
     h->rec_dirty = true;
     publish_nodes(h);
     return CRANE_OK;

@@ -255,6 +255,93 @@ hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int
 
 size_t hot_dedupe_scratch(const HotPart& g) { return (size_t)g.cap + (size_t)g.nbins * (size_t)g.nblk; }
 
+// ---------------------------------------------------------------- delta form
+// (kernels.hpp HotDelta.)  Per workgroup 1024 changed bindings, two keys each: (node * 8 +
+// bucket) * 2 + sign, -1 from the anchor bucket (sign 1) and +1 to the new one (sign 0),
+// aggregated in the LDS hash as the dedupe form does (a Zipf-hot node costs one global atomic per
+// workgroup and bucket), then one atomicAdd per distinct key into adj.  Counts are modulo 2^32:
+// anchor + adj is the exact count.
+constexpr int kDeltaChunk = 1024;
+
+template <int BT>
+__device__ __forceinline__ void k2_delta_body(const int32_t blk, const int32_t* __restrict__ bnode, int64_t N,
+                                              const HotDelta& d, uint32_t* __restrict__ adj) {
+    constexpr int kPer = kDeltaChunk / BT;
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+    __shared__ uint32_t hist[32];  // (hash_add's bin counts: not read)
+    int32_t* hkey = reinterpret_cast<int32_t*>(sh);
+    uint32_t* hcnt = sh + kDSlots;
+    uint16_t* uniq = reinterpret_cast<uint16_t*>(hcnt + kDSlots);
+    const int64_t L = d.start[d.n_rng];
+    int64_t pos[kPer];
+    int32_t nd[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        const int64_t t = (int64_t)blk * kDeltaChunk + u * BT + threadIdx.x;
+        int k = 0;
+        for (int r = 1; r < d.n_rng; ++r) k += t >= d.start[r] ? 1 : 0;
+        pos[u] = d.lo[k] + (t - d.start[k]);
+        nd[u] = bnode[t < L ? pos[u] : d.lo[0]];  // (unconditional load, clamped)
+        if (t >= L) nd[u] = -1;
+    }
+    for (int i = threadIdx.x; i < kDSlots; i += BT) {
+        hkey[i] = -1;
+        hcnt[i] = 0;
+    }
+    if (threadIdx.x < 32) hist[threadIdx.x] = 0;
+    __syncthreads();
+    int32_t key[2 * kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        int ja = 0, jp = 0;
+        for (int r = 0; r < d.n_win; ++r) {
+            ja += pos[u] >= d.a[r] ? 1 : 0;
+            jp += pos[u] >= d.p[r] ? 1 : 0;
+        }
+        const bool ch = nd[u] >= 0 && (int64_t)nd[u] < N && ja != jp;  // binding.go:85-91 at both cutoffs
+        key[2 * u] = ch && ja > 0 ? ((nd[u] * 8 + (ja - 1)) << 1) | 1 : -1;
+        key[2 * u + 1] = ch && jp > 0 ? (nd[u] * 8 + (jp - 1)) << 1 : -1;
+    }
+    uint16_t* useg = uniq + (threadIdx.x >> 6) * (2 * kPer * 64);
+    const uint32_t nw = wave_aggregate<kDSlots, 2 * kPer>(key, hkey, hcnt, hist, 24, useg);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x & 63; i < nw; i += 64) {  // this wave's new keys
+        const int s = useg[i];
+        const int32_t k = hkey[s];
+        const uint32_t c = hcnt[s];
+        atomicAdd(&adj[(int64_t)((k >> 1) & 7) * N + (k >> 4)], (k & 1) ? 0u - c : c);
+    }
+}
+
+template <int BT>
+__global__ __launch_bounds__(BT) void k2_delta_pods(const int32_t* __restrict__ bnode, int64_t N, HotDelta d,
+                                                    uint32_t* __restrict__ adj, PodPrep pp) {
+    if ((int64_t)blockIdx.x >= pp.ntiles) {
+        k2_delta_body<BT>((int32_t)(blockIdx.x - pp.ntiles), bnode, N, d, adj);
+    } else {
+        extern __shared__ __attribute__((aligned(16))) unsigned char k3p_lds[];
+        k3p_tile<BT>((int64_t)blockIdx.x, pp, k3p_lds);
+    }
+}
+
+hipError_t launch_hot_count_delta(const int32_t* bnode, int64_t N, const HotDelta& d, uint32_t* adj, hipStream_t st,
+                                  const PodPrep* pods) {
+    constexpr int BT = 512;
+    if (d.n_rng < 0 || d.n_rng > kMaxWin || d.n_win < 1 || d.n_win > kMaxWin || N >= (1LL << 27))
+        return hipErrorInvalidValue;
+    const int64_t L = d.n_rng > 0 ? d.start[d.n_rng] : 0;
+    const int64_t nb = (L + kDeltaChunk - 1) / kDeltaChunk;
+    PodPrep pp{};
+    if (pods && pods->P > 0) pp = *pods;
+    const int64_t grid = pp.ntiles + nb;
+    if (grid == 0) return hipSuccess;
+    if (grid >= (1LL << 31)) return hipErrorInvalidValue;
+    size_t lds = sizeof(uint32_t) * 2 * (size_t)kDSlots + sizeof(uint16_t) * 2 * kDeltaChunk;
+    if (pp.ntiles > 0) lds = std::max(lds, kK3pLds);
+    return klaunch(pp.ntiles > 0 ? "k2_delta+k3p_pods" : "k2_delta", k2_delta_pods<BT>, dim3((unsigned)grid), dim3(BT),
+                   lds, st, bnode, N, d, adj, pp);
+}
+
 // ---------------------------------------------------------------- large form
 // When the dedupe form's count/offset matrix (K1 blocks x regions) would pass its cap
 // (e.g. 4M nodes x 16M bindings: 15,625 x 7,813 words), the log goes through two kernels:

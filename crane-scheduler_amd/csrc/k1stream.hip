@@ -234,8 +234,18 @@ void k1_stream_steps(K1Args a, K1Step step) {
     double hvl = 0.0;
     int64_t hvt = kTsInvalid;
     if (a.buckets) {
+        // (+ the delta form's anchor counts: kernels.hip)
+        const uint32_t* __restrict__ base = a.bucket_base ? a.bucket_base : a.buckets;
+        uint32_t bz[kMaxWin];
 #pragma unroll
-        for (int b = 0; b < kMaxWin; ++b) bc[b] = b < pol.n_win ? (a.buckets + first)[(int64_t)b * N + lo] : 0u;
+        for (int b = 0; b < kMaxWin; ++b) {
+            bc[b] = b < pol.n_win ? (a.buckets + first)[(int64_t)b * N + lo] : 0u;
+            bz[b] = b < pol.n_win ? (base + first)[(int64_t)b * N + lo] : 0u;
+        }
+        if (a.bucket_base) {
+#pragma unroll
+            for (int b = 0; b < kMaxWin; ++b) bc[b] += bz[b];
+        }
     } else if (a.hv) {
         hvl = a.hv[first + lo];
         hvt = a.hv_ts ? a.hv_ts[first + lo] : a.hv_ts_counts;

@@ -204,9 +204,19 @@ void k1_node_pass(K1Args a, K1Step step) {
         }
     }
     if (buckets) {
+        // the delta form's anchor counts beside the adjustments (without them: the adjustments
+        // again, added as zero)
+        const uint32_t* __restrict__ base = a.bucket_base ? a.bucket_base : buckets;
+        uint32_t bz[kMaxWin];
 #pragma unroll
-        for (int b = 0; b < kMaxWin; ++b)
+        for (int b = 0; b < kMaxWin; ++b) {
             bc[b] = b < pol.n_win ? (buckets + first)[(int64_t)b * N + lo] : 0u;
+            bz[b] = b < pol.n_win ? (base + first)[(int64_t)b * N + lo] : 0u;
+        }
+        if (a.bucket_base) {
+#pragma unroll
+            for (int b = 0; b < kMaxWin; ++b) bc[b] += bz[b];
+        }
     }
     if (!buckets && !hx && hv) {
         hvl = hv[first + lo];

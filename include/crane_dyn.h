@@ -343,6 +343,8 @@ const char *crane_dyn_version(void);
  *   "k2_form" 0 dedupe (default; the large form past its count/offset cap, the atomics form past the
  *     large form's) | 2 atomics (LDS hash + global atomics, any shape) | 3 large
  *   "k2_sorted" 1 a time-ordered log (checked at upload): K2 reads the widest window's suffix only | 0 never
+ *   "k2_delta" 1 ... and with k2_form 0, once anchored, only the bindings whose window rank changed since
+ *     the anchor refresh (the anchor's dense counts + adjustments) | 0 every refresh re-counts the suffix
  *   "k1_stream" 1 the streamed step pass without dedupe-form K2 entries | 0 the record-holding fused pass
  *   "k1_tail" 0 its tail on one wave when the grid has >= 4096 blocks | 1 always | 4 on all four waves
  *   "keys_path" 0 step path | 1 per-pair kernel   "greedy_form" 0 merge | 1 sequential

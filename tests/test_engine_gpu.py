@@ -152,7 +152,7 @@ def test_hot_values_random(n_nodes, n_bind, seed, k2):
     bn = c.b_node.copy()
     bn[::97] = -1
     bn[1::101] = n_nodes + 5
-    eng = engine_for(spec, c, opts={"k2_form": k2})
+    eng = engine_for(spec, c, opts={"k2_form": k2, "k2_delta": 0})
     eng.upload_bindings(bn, c.b_ts)
     now = int(c.now[0])
     eng.refresh_hot_values(now, now)
@@ -162,7 +162,7 @@ def test_hot_values_random(n_nodes, n_bind, seed, k2):
     assert np.array_equal(ff, off) and np.array_equal(sc, osc) and np.array_equal(ch, och)
 
 
-@pytest.mark.parametrize("k2", [0, 3], ids=["dedupe", "large"])
+@pytest.mark.parametrize("k2", [0, 3, "delta"], ids=["dedupe", "large", "delta"])
 @pytest.mark.parametrize("order", ["sorted", "ties", "shuffled", "sorted_off", "all_old", "all_new", "one_out"])
 def test_hot_values_time_ordered_log(order, k2):
     """A time-ordered log (a ring appended as bindings happen): K2 reads only the widest
@@ -188,7 +188,7 @@ def test_hot_values_time_ordered_log(order, k2):
     if order == "one_out":
         bt = np.full(n_bind, nu, np.int64)
         bt[0] = nu - 300  # not > cutoff: outside every window
-    opts = {"k2_form": k2}
+    opts = {} if k2 == "delta" else {"k2_form": k2, "k2_delta": 0}
     if order == "sorted_off":
         opts["k2_sorted"] = 0
     if order == "shuffled":
@@ -206,6 +206,47 @@ def test_hot_values_time_ordered_log(order, k2):
     _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=(cnt_hv.astype(np.float64),
                                                                     np.full(n_nodes, now, np.int64)))
     assert np.array_equal(ch, och)
+    eng.close()
+
+
+def test_hot_values_delta_sequence():
+    """Delta form (engine option k2_delta): after an anchor refresh, a time-ordered log's refresh
+    reads only the bindings whose window rank changed (between the anchor's and this refresh's
+    suffix starts) and adjusts the anchor's counts.  Each refresh of a sequence of times --
+    forward, back past the anchor, within one second, a jump past half the suffix (re-anchor),
+    two refreshes with no read between (the first's adjustments dropped), a new log and a
+    resized node set (anchor dropped) -- equals the oracle (binding.go:85-91)."""
+    spec = cd.default_policy_spec()
+    n_nodes, n_bind = 30_000, 400_000
+    c = synth.make_cluster(spec, n_nodes, 32, n_bindings=n_bind, seed=53, pod_step_ns=3_000_000_000)
+    now = int(c.now[0])
+    nu = now // 10**9
+    bn, bt = c.b_node.copy(), c.b_ts.copy()
+    bn[::89] = -1
+    bn[5::97] = n_nodes + 1
+    eng = engine_for(spec, c)
+    eng.upload_bindings(bn, bt)
+
+    def check(dt, nn=n_nodes, b=(bn, bt), read=True):
+        eng.refresh_hot_values(now + dt * 10**9, now)
+        if read:
+            _, cnt_hv = O.hot_values(spec, b[0], b[1], nn, nu + dt)
+            assert np.array_equal(eng.hot_values(), cnt_hv.astype(np.float64)), dt
+
+    for dt in (0, 7, 13, 13, -25, -24, 0, 40, -290, -200, 30):
+        check(dt)
+    check(-100, read=False)
+    check(-90, read=False)
+    check(5)
+    # a new log: the anchor goes
+    bt2 = np.sort(bt + np.random.default_rng(3).integers(-30, 30, n_bind))
+    eng.upload_bindings(bn, bt2)
+    for dt in (5, 11, -9):
+        check(dt, b=(bn, bt2))
+    # fewer nodes: bindings to the dropped ones fall out
+    eng.resize_nodes(n_nodes - 1000)
+    for dt in (-9, 2):
+        check(dt, nn=n_nodes - 1000, b=(bn, bt2))
     eng.close()
 
 
@@ -234,7 +275,7 @@ def test_hot_values_dedupe_edges(case, k2):
         bn[::3] = n_nodes - 1
         bn[1::7] = n_nodes  # past the shard: ignored
         bn[2::11] = -3
-    opts = {"k2_form": k2}
+    opts = {"k2_form": k2, "k2_delta": 0}
     eng = engine_for(spec, c, opts=opts)
     eng.upload_bindings(bn, c.b_ts)
     now = int(c.now[0])

@@ -183,15 +183,17 @@ def test_hot_values_kept_after_consumption():
     assert np.array_equal(ff, off) and np.array_equal(sc, osc)
 
 
+@pytest.mark.parametrize("delta", [1, 0], ids=["delta", "recount"])
 @pytest.mark.parametrize("pods", [5000, 1, 300, 2048])
-def test_step_keys_async_matches_oracle(pods):
-    """crane_dyn_step_keys_async replayed (K3p riding in K2x's launch):
+def test_step_keys_async_matches_oracle(pods, delta):
+    """crane_dyn_step_keys_async replayed (K3p riding in K2's launch) at hot-value times that
+    move between steps (the delta form adjusts its anchor's counts; recount: the dedupe form):
     each step equals the oracle with binding-log hot values; with kernel timing on
     too (dispatch-stamped events name every kernel of the step)."""
     import torch
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 30000, pods, n_bindings=300_000, seed=27, pod_step_ns=2_000_000, ds_frac=0.02)
-    eng = engine_for(spec, c)
+    eng = engine_for(spec, c, opts={"k2_delta": delta})
     eng.upload_bindings(c.b_node, c.b_ts)
     now = int(synth.NOW0_NS)
     dev = torch.device("cuda", 0)
@@ -199,17 +201,20 @@ def test_step_keys_async_matches_oracle(pods):
     d_now = torch.from_numpy(c.now).to(dev)
     d_flags = torch.from_numpy(c.ds).to(dev)
     d_keys = torch.empty(len(c.now), dtype=torch.int64, device=dev)
-    _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=_oracle_hv(spec, c, now))
     with torch.cuda.stream(st):
-        for rep in range(4):
+        for rep, dt in enumerate((0, 9, -4, 30)):
+            t = now + dt * 10**9
+            _, _, och = oracle_soa(spec, c, want_matrix=False, hv_override=_oracle_hv(spec, c, t))
             eng.set_profiling(rep == 3)
-            eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
+            eng.step_keys_async(t, t, d_now, d_flags, d_keys, st.cuda_stream)
             st.synchronize()
             ch = np.array([cd.key_node(int(k))[0] for k in d_keys.cpu().numpy()])
             assert np.array_equal(ch, och), rep
     times = eng.stage_times()
     names = [n for n, _ in times]
-    assert names == ["k2x_dedupe+k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"], names
+    want = (["k2_delta+k3p_pods", "k1_stream_steps", "k3s_eval"] if delta else
+            ["k2x_dedupe+k3p_pods", "k1_node_pass+k3a_steps", "k3s_eval"])
+    assert names == want, names
     assert all(0 < t < 50 for _, t in times), times
 
 
@@ -220,7 +225,7 @@ def test_step_keys_async_k2_forms(k2):
     import torch
     spec = cd.default_policy_spec()
     c = synth.make_cluster(spec, 20000, 3000, n_bindings=400_000, seed=29, pod_step_ns=2_000_000, ds_frac=0.03)
-    eng = engine_for(spec, c, opts={"k2_form": k2})
+    eng = engine_for(spec, c, opts={"k2_form": k2, "k2_delta": 0})
     eng.upload_bindings(c.b_node, c.b_ts)
     now = int(synth.NOW0_NS)
     dev = torch.device("cuda", 0)
