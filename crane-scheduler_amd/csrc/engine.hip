@@ -246,6 +246,7 @@ struct crane_dyn {
     DevBuf<unsigned long long> trace;  // [3][kTraceWgs][8] phase stamps (option "trace")
     DevBuf<int32_t> sperm, scnt;  // K3 step path scratch (step.hip)
     DevBuf<int64_t> stile, spnow, sbatch;
+    int sbatch_par = 0;  // the range of sbatch the next step folds into (StepPlan::batch)
     DevBuf<int64_t> sel_fth, sel_win, sel_state;  // framework selection (select.hip)
     DevBuf<long long> sel_keys;
     DevBuf<unsigned char> stp_dev;  // node answer tables (crane_dyn_node_steps): bp, ns, ff, score
@@ -527,6 +528,9 @@ static int hot_delta_locked(crane_dyn* h, int64_t Bk, const HotCutoffs& pcut, hi
         h->dl_N = h->N;
         h->dl_B = h->B;
     } else {
+        d.trace = h->trace_region(0);  // (the delta launch stays far below kTraceWgs workgroups at
+                                       // config 3; larger ones are not traced)
+        if ((pods ? pods->ntiles : 0) + (L + 1023) / 1024 > kTraceWgs) d.trace = nullptr;
         HIPTRY(h, launch_hot_count_delta(h->sd->bnode.p, h->N, d, h->dl_adj.p, st, pods));
         if (pods_done) *pods_done = pods != nullptr && pods->P > 0;
     }
@@ -719,6 +723,8 @@ struct StepPlan {
     StepGeometry g;
     StepTables stt;
     bool fuse;  // K3a fused into the node pass (records stale)
+    int64_t* batch;       // this step's time range (K3p folds it, K1 reads it)
+    int64_t* batch_next;  // the other range: reset by K3p for the next step
 };
 
 static bool step_path_ok(const crane_dyn* h, int64_t P) {
@@ -733,14 +739,19 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     const StepGeometry& g = sp.g;
     HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
     HIPTRY(h, h->stile.reserve((size_t)(kTileStat * g.ntiles)));
-    if (!h->sbatch.p) {  // {tmin, tmax, tile counter}: the counter starts at 0, K3p re-arms it
+    if (!h->sbatch.p) {  // two {tmin, tmax} ranges, alternating between steps, start empty
         HIPTRY(h, h->sbatch.reserve(4));
-        // on the engine stream and waited for: a null-stream hipMemset is not ordered with the
+        // on the engine stream and waited for: a null-stream copy is not ordered with the
         // non-blocking streams K3p runs on and may land after it (a batch then saw tmin = tmax
         // = 0: every pod scored as at time 0, seen once in test_greedy_then_eval_consistent)
-        HIPTRY(h, hipMemsetAsync(h->sbatch.p, 0, 4 * sizeof(int64_t), h->stream));
+        static const int64_t empty[4] = {INT64_MAX, INT64_MIN, INT64_MAX, INT64_MIN};
+        HIPTRY(h, hipMemcpyAsync(h->sbatch.p, empty, sizeof(empty), hipMemcpyHostToDevice, h->stream));
         HIPTRY(h, hipStreamSynchronize(h->stream));
+        h->sbatch_par = 0;
     }
+    // (the ranges alternate once K3p was launched: pods_ran)
+    sp.batch = h->sbatch.p + 2 * h->sbatch_par;
+    sp.batch_next = h->sbatch.p + 2 * (h->sbatch_par ^ 1);
     HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
     HIPTRY(h, h->scnt.reserve((size_t)std::max<int32_t>(nblk, 1) * 6));  // cnt [nblk][4] + flat [nblk][2]
     // per kind and producer block: 2 * bs one-step records, bs * (breakpoints - 1) middle pieces
@@ -784,9 +795,16 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     return CRANE_OK;
 }
 
+// K3p was launched for a step: the next step folds into the range this one reset
+static void pods_ran(crane_dyn* h, int64_t P) {
+    if (P > 0) h->sbatch_par ^= 1;
+}
+
 static int step_pods(crane_dyn* h, const StepPlan& sp, int64_t P, const int64_t* d_now, const uint8_t* d_flags,
                      long long* d_keys, hipStream_t st) {
-    HIPTRY(h, launch_step_pods(d_now, d_flags, P, d_keys, h->sbatch.p, sp.g, h->sperm.p, h->spnow.p, h->stile.p, st));
+    HIPTRY(h, launch_step_pods(d_now, d_flags, P, d_keys, sp.batch, sp.batch_next, sp.g, h->sperm.p, h->spnow.p,
+                               h->stile.p, st));
+    pods_ran(h, P);
     return CRANE_OK;
 }
 
@@ -794,7 +812,7 @@ static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_k
     if (P == 0) return CRANE_OK;
     if (sp.fuse) {
         // (the records the fused step leaves stale serve as the streamed pass's scratch)
-        const K1Step ks{h->stile.p, h->sbatch.p, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, h->dp.winv, sp.stt,
+        const K1Step ks{h->stile.p, sp.batch, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, h->dp.winv, sp.stt,
                         h->rec.p, h->opt.k1_tail};
         int rc = node_pass_locked(h, st, nullptr, &ks);
         if (rc) return rc;
@@ -1421,9 +1439,11 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
     StepPlan sp;
     int rc = step_plan(h, P, sp);
     if (rc) return rc;
-    const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys, h->sbatch.p};
+    const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys, sp.batch,
+                         sp.batch_next};
     bool pods_done = false;
     rc = hot_values_locked(h, now_ns, hv_ts_ns, st, &pp, &pods_done);
+    if (pods_done) pods_ran(h, P);
     if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, st);
     if (!rc) rc = step_rest(h, sp, P, keys, st);
     return rc ? rc : mark_busy(h, st);
@@ -1461,9 +1481,11 @@ int crane_dyn_step_keys_queue(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
         h->rec_dirty = true;
         StepPlan sp{};
         rc = step_plan(h, P, sp);
-        const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys, h->sbatch.p};
+        const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys, sp.batch,
+                         sp.batch_next};
         bool pods_done = false;
         if (!rc) rc = hot_values_locked(h, now_ns, hv_ts_ns, h->stream, &pp, &pods_done);
+        if (pods_done) pods_ran(h, P);
         if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, h->stream);
         if (!rc) rc = step_rest(h, sp, P, keys, h->stream);
     }

@@ -316,12 +316,14 @@ __device__ __forceinline__ void k2_delta_body(const int32_t blk, const int32_t* 
 template <int BT>
 __global__ __launch_bounds__(BT) void k2_delta_pods(const int32_t* __restrict__ bnode, int64_t N, HotDelta d,
                                                     uint32_t* __restrict__ adj, PodPrep pp) {
+    CRANE_TSTAMP(d.trace, blockIdx.x, 0);
     if ((int64_t)blockIdx.x >= pp.ntiles) {
         k2_delta_body<BT>((int32_t)(blockIdx.x - pp.ntiles), bnode, N, d, adj);
     } else {
         extern __shared__ __attribute__((aligned(16))) unsigned char k3p_lds[];
         k3p_tile<BT>((int64_t)blockIdx.x, pp, k3p_lds);
     }
+    for (int k = 1; k <= 4; ++k) CRANE_TSTAMP(d.trace, blockIdx.x, k);  // (one phase: start -> end)
 }
 
 hipError_t launch_hot_count_delta(const int32_t* bnode, int64_t N, const HotDelta& d, uint32_t* adj, hipStream_t st,

@@ -213,9 +213,12 @@ struct PodPrep {
     int64_t* pnow;
     int64_t* tile_mm;
     long long* keys;
-    // the batch's time range {tmin, tmax, tile counter (u32)}: the last tile of K3p to finish
-    // folds every tile's stats into it (the counter starts at 0 and is re-armed), or null
+    // the batch's time range {tmin, tmax}: every tile folds its pods' range in with one relaxed
+    // atomic min / max (no tile waits for another), or null.  batch_next: the other of the two
+    // ranges the engine alternates between batches, reset to {INT64_MAX, INT64_MIN} by tile 0 for
+    // the next batch (the kernels that read this batch's range precede the next K3p)
     int64_t* batch;
+    int64_t* batch_next;
 };
 constexpr int kHxRegion = 2048;
 HotPart hot_dedupe_geometry(int64_t B, int64_t N, int32_t W, int32_t bs);
@@ -233,6 +236,7 @@ struct HotDelta {
     int32_t n_win, n_rng;
     int64_t a[kMaxWin], p[kMaxWin];
     int64_t lo[kMaxWin], start[kMaxWin + 1];
+    unsigned long long* trace;  // phase stamps per workgroup (K3p tiles first) or null
 };
 hipError_t launch_hot_count_delta(const int32_t* bnode, int64_t N, const HotDelta& d, uint32_t* adj, hipStream_t st,
                                   const PodPrep* pods);
@@ -312,6 +316,7 @@ int step_breakpoints(int shape);  // in-range expiries per node and kind at most
 StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk, int32_t blk_per_wg = 0);
 // K3p: perm, pnow [ntiles * 1024], tile_mm [kTileStat * ntiles]; initialises keys[0..P) to -1
 hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys, int64_t* batch,
+                            int64_t* batch_next,
                             const StepGeometry& g, int32_t* perm, int64_t* pnow, int64_t* tile_mm, hipStream_t s);
 // K3a: step tables from NodeRecs in HBM (after K3p)
 hipError_t launch_step_nodes(int shape, const void* rec, int64_t N, double wsum, int32_t noprio,

@@ -126,29 +126,26 @@ __device__ __forceinline__ void k3p_tile(const int64_t t, const PodPrep& pp, uns
         // (e0 / e1 from the counts, not a binary search over the sorted classes: 20 dependent LDS
         // reads on the launch's critical path)
         int64_t* ts = pp.tile_mm + kTileStat * t;
-        ts[0] = e0 > 0 ? (int64_t)(ku[0] ^ kSign) : INT64_MAX;
-        ts[1] = e0 > 0 ? (int64_t)(ku[e0 - 1] ^ kSign) : INT64_MIN;
-        ts[2] = e1 > e0 ? (int64_t)(ku[e0] ^ kSign) : INT64_MAX;
-        ts[3] = e1 > e0 ? (int64_t)(ku[e1 - 1] ^ kSign) : INT64_MIN;
+        const int64_t n0 = e0 > 0 ? (int64_t)(ku[0] ^ kSign) : INT64_MAX;
+        const int64_t x0 = e0 > 0 ? (int64_t)(ku[e0 - 1] ^ kSign) : INT64_MIN;
+        const int64_t n1 = e1 > e0 ? (int64_t)(ku[e0] ^ kSign) : INT64_MAX;
+        const int64_t x1 = e1 > e0 ? (int64_t)(ku[e1 - 1] ^ kSign) : INT64_MIN;
+        ts[0] = n0;
+        ts[1] = x0;
+        ts[2] = n1;
+        ts[3] = x1;
         ts[4] = e0;
         ts[5] = e1 - e0;
         if (pp.batch) {
-            // the batch's time range, once for every consumer: the last tile to finish folds
-            // the tiles' stats (its acquire sees every other tile's stores, released by their
-            // increments) and re-arms the counter for the next batch
-            unsigned* ctr = reinterpret_cast<unsigned*>(pp.batch + 2);
-            const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-            if (prev + 1u == (unsigned)pp.ntiles) {
-                int64_t mn = INT64_MAX, mx = INT64_MIN;
-                for (int64_t i = 0; i < pp.ntiles; ++i) {
-                    const int64_t* q = pp.tile_mm + kTileStat * i;
-                    mn = min(mn, min(q[0], q[2]));
-                    mx = max(mx, max(q[1], q[3]));
-                }
-                pp.batch[0] = mn;
-                pp.batch[1] = mx;
-                __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // (round 5 had the last tile to finish fold every tile's stats behind an acquire /
+            // release counter: two whole-L2 cache operations on the launch's critical path)
+            if (t == 0) {
+                pp.batch_next[0] = INT64_MAX;
+                pp.batch_next[1] = INT64_MIN;
             }
+            const int64_t mn = min(n0, n1), mx = max(x0, x1);
+            if (mn != INT64_MAX) __hip_atomic_fetch_min(&pp.batch[0], mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (mx != INT64_MIN) __hip_atomic_fetch_max(&pp.batch[1], mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

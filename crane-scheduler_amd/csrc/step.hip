@@ -505,9 +505,10 @@ static hipError_t launch_steps_t(const void* rec, int64_t N, double wsum, int32_
 }
 
 hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys, int64_t* batch,
-                            const StepGeometry& g, int32_t* perm, int64_t* pnow, int64_t* tile_mm, hipStream_t s) {
+                            int64_t* batch_next, const StepGeometry& g, int32_t* perm, int64_t* pnow,
+                            int64_t* tile_mm, hipStream_t s) {
     if (P <= 0) return hipSuccess;
-    const PodPrep pp{now, flags, P, g.ntiles, perm, pnow, tile_mm, keys, batch};
+    const PodPrep pp{now, flags, P, g.ntiles, perm, pnow, tile_mm, keys, batch, batch_next};
     return klaunch("k3p_pods", k3p_pods, dim3((unsigned)g.ntiles), dim3(kPodTile), kK3pLds, s, pp);
 }
 

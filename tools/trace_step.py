@@ -6,7 +6,12 @@ Every workgroup of K2x (dedupe), K1 (+K3a) and K3s stamps s_memrealtime (100 MHz
 10 ns) at its phase boundaries; per kernel this prints the spread of workgroup
 start times, each phase's duration (median / p90 / max over workgroups) and the
 span first start -> last end, so the critical path of a launch can be read off.
+With --queue the steps go to a dispatch queue (the headline's launch route); "timeline" gives the
+launch-to-launch view of one step: each kernel's first workgroup start and last end relative to the
+first kernel's start, and the gaps between the kernels.  --dt S moves the hot-value time by S
+seconds per traced step (the delta form then adjusts its anchor by the bindings that changed).
 Phases:
+  K2 (delta form + K3p tiles): 0 start | 4 end
   K2x: 0 start | 1 bindings loaded + LDS cleared | 2 (node, bucket) aggregated | 3 counts/offsets written | 4 entries written
   K1 : 0 start | 1 SoA + K2 entries in (LDS counts) | 2 record computed | 3 step tables published | 4 stepped records emitted
   K3s: 0 start | 1 pods + producer counts in | 2 record rounds done | 3 uniform maxima reduced | 4 keys merged
@@ -31,6 +36,8 @@ ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--opt", action="append", default=[], help="engine option name=value (repeatable)")
 ap.add_argument("--nodes", type=int, default=0, help="override the config's node count")
 ap.add_argument("--bindings", type=int, default=-1, help="override the config's binding count")
+ap.add_argument("--queue", action="store_true", help="steps on a dispatch queue (crane_queue)")
+ap.add_argument("--dt", type=int, default=0, help="hot-value time moved by this many seconds per traced step")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 st = torch.cuda.Stream(dev)
@@ -55,21 +62,43 @@ d_now = torch.from_numpy(c.now).to(dev)
 d_flags = torch.from_numpy(c.ds).to(dev)
 d_keys = torch.empty(P, dtype=torch.int64, device=dev)
 now = int(synth.NOW0_NS)
+q = cd.Queue(0) if args.queue else None
+torch.cuda.synchronize()
+
+
+def step(t):
+    if q is not None:
+        eng.step_keys_queue(t, t, d_now, d_flags, d_keys, q)
+        q.wait()
+    else:
+        eng.step_keys_async(t, t, d_now, d_flags, d_keys, st.cuda_stream)
+        st.synchronize()
+
+
 for _ in range(3):
-    eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
+    step(now)
 eng.set_option("trace", 1)
 nwg = {0: -(-B // 2048), 1: -(-N // 256)}
 res = {}
 xcd = {}
 acc = {k: [] for k in ("K2x", "K1", "K3s")}
+import time  # noqa: E402
+tl, host = [], []
 for r in range(args.reps):
-    eng.step_keys_async(now, now, d_now, d_flags, d_keys, st.cuda_stream)
-    st.synchronize()
+    h0 = time.perf_counter()
+    step(now + (r + 1) * args.dt * 10**9)
+    host.append((time.perf_counter() - h0) * 1e6)
+    ends = {}
     for which, name in ((0, "K2x"), (1, "K1"), (2, "K3s")):
         t = eng.debug_trace(which, 65536).astype(np.int64)
         wg = np.nonzero(t[:, 0] > 0)[0]
         t = t[wg]
         acc[name].append(t)
+        if len(t):
+            ends[name] = (int(t[:, 0].min()), int(t[:, 4].max()))
+    if len(ends) == 3:
+        t0 = ends["K2x"][0]
+        tl.append([(ends[k][i] - t0) / 100.0 for k in ("K2x", "K1", "K3s") for i in (0, 1)])
         # workgroup -> XCD placement: the XCD of each label (workgroup id % 8), as observed
         lab = {}
         for w, x in zip(wg % 8, t[:, 7]):
@@ -99,5 +128,11 @@ for name, runs in acc.items():
     if name in subs:
         sub = subs[name]
         out[name]["sub"] = {k: q(cat([(t[:, b] - t[:, a]) / 100.0 for t in runs])) for k, (a, b) in sub.items()}
+if tl:
+    m = np.median(np.array(tl), axis=0)
+    out["timeline"] = {"K2_end": round(m[1], 2), "K1_start": round(m[2], 2), "K1_end": round(m[3], 2),
+                       "K3s_start": round(m[4], 2), "K3s_end": round(m[5], 2),
+                       "gap_K2_K1": round(m[2] - m[1], 2), "gap_K1_K3s": round(m[4] - m[3], 2)}
+out["host_step_us"] = round(float(np.median(host)), 2)  # enqueue -> completion seen, traced
 out["xcd_of_label"] = {k: v[:3] for k, v in xcd.items()}
 print(json.dumps(out))
