@@ -190,6 +190,31 @@ def rec_bytes(spec):
     return -(-(24 + 16 * pr_ + 8 * pd_) // 16) * 16
 
 
+def delta_changed(spec, b_ts, nows):
+    """The delta form's work per batch (engine option k2_delta): bindings whose window rank at the
+    batch's time differs from the anchor refresh's (the first batch time: a slot's anchor), i.e. the
+    merged ranges between the windows' suffix starts, for each of the timed batches' times."""
+    trs = sorted(tr // 10**9 for tr, _ in spec["hotValue"])
+
+    def starts(now_ns):
+        cut = np.sort(np.array([now_ns // 10**9 - t for t in trs], np.int64))
+        return np.searchsorted(b_ts, cut, side="right")
+
+    a = starts(nows[0])
+    ls = []
+    for n in nows:
+        p = starts(n)
+        rg = sorted((min(x, y), max(x, y)) for x, y in zip(a, p) if x != y)
+        tot, end = 0, -1
+        for lo, hi in rg:
+            lo = max(lo, end)
+            if hi > lo:
+                tot += hi - lo
+            end = max(end, hi)
+        ls.append(tot)
+    return {"per_time": [int(x) for x in ls], "mean": float(np.mean(ls)), "anchor_now_ns": int(nows[0])}
+
+
 def kernel_times(eng, fn, reps):
     """Mean dispatch-stamped duration per kernel name over `reps` calls of fn()."""
     acc = {}
@@ -1163,8 +1188,14 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
     eng = grp.engine(0, 0)
     st0 = torch.cuda.Stream(devs[0])
     k0 = torch.empty(P, dtype=torch.int64, device=devs[0])
-    kt = kernel_times(eng, lambda: eng.step_keys_async(nows[0], nows[0], d_now[0][0], d_flags[0], k0,
-                                                       st0.cuda_stream), args.steps)
+    kcyc = [0]
+
+    def kstep():  # the timed batches' times in turn (the delta form's changed bindings vary with them)
+        t = kcyc[0] % len(nows)
+        kcyc[0] += 1
+        eng.step_keys_async(nows[t], nows[t], d_now[t][0], d_flags[0], k0, st0.cuda_stream)
+
+    kt = kernel_times(eng, kstep, max(args.steps, 2 * len(nows)))
     val, ts, _ = c.rows(grp.metric_names)
     m = dict(c=c, N=c.n_nodes, P=P, n_total=n_total, val=val, ts=ts, eng=eng, ms_step=elapsed * 1e3 / args.steps,
              keys=keys, keys_agree=keys_agree, keys_match=keys_match, keys_match_how=keys_match_how, host=host,
@@ -1293,6 +1324,7 @@ def finish(cd, synth, spec, args, m, n_gpus, rank, solo, dev, shash):
     co_b = 4 * (-(-N // 256)) * (-(-kb["read"] // 2048))
     k3p_b = P * (8 + 1 + 4 + 8 + 8)
     k2d_b = kb["bytes"] + E * 4 + co_b
+    dl = delta_changed(spec, c.b_ts, m["nows"])
     alg = {
         "k2x_dedupe": (k2d_b, kb["what"] + " + distinct (region, node, bucket) entries + count/offset written"),
         "k2x_dedupe+k3p_pods": (k2d_b + k3p_b, kb["what"] + " + distinct entries + count/offset written; pod now + "
@@ -1301,6 +1333,10 @@ def finish(cd, synth, spec, args, m, n_gpus, rank, solo, dev, shash):
                                    "SoA (value, ts) read + hot value written + K2 entries and count/offset read"),
         "k1_stream_steps": (N * (16 * M + 8 + 4 * W), "SoA (value, ts) read + hot value written + window counts read"),
         "k3p_pods": (k3p_b, "pod now + flag read, partition + keys written"),
+        "k2_delta+k3p_pods": (12 * dl["mean"] + k3p_b,
+                              "per changed binding (window rank differs from the anchor refresh's): node id read "
+                              "+ its -1 / +1 adjustments written (12 B, mean over the timed batches' times); pod now "
+                              "+ flag read, partition + keys written"),
     }
     pmc, pmc_src = pmc_summary(args.config, shash)
     roofs = {}
@@ -1471,6 +1507,14 @@ def finish(cd, synth, spec, args, m, n_gpus, rank, solo, dev, shash):
                                   "batch_latency_ms": round(m["batch_latency_ms"], 4)},
             "placements_per_s": round(placements, 1),
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
+            "hot_value_refresh": {
+                "form": "delta" if any(k.startswith("k2_delta") for k in kt) else "recount",
+                "changed_bindings_mean": round(dl["mean"], 1), "changed_bindings_per_time": dl["per_time"],
+                "anchor_now_ns": dl["anchor_now_ns"],
+                "how": ("engine option k2_delta (time-ordered log): a slot's first refresh counts the widest window's "
+                        "suffix (large form) as its anchor; each later batch reads only the bindings whose window rank "
+                        "at its now differs from the anchor's and adjusts the anchor counts (kernel_ms, over the timed "
+                        "batches' times in turn); re-anchors when they pass half the suffix or the log changes")},
             "allreduce_ms": None if m["ar_ms"] is None else round(m["ar_ms"], 4),
             "host": m["host"],
             "keys_match_1gpu": m["keys_match"],

@@ -474,7 +474,7 @@ static int hot_delta_locked(crane_dyn* h, int64_t Bk, const HotCutoffs& pcut, hi
     const DevPolicy& dp = h->dp;
     const int nw = dp.n_win;
     *done = false;
-    if (h->N <= 0 || h->N >= (1LL << 27) || nw < 1) return CRANE_OK;
+    if (h->N <= 0 || h->N >= (1LL << 27) || nw < 1 || nw > kDeltaMaxWin) return CRANE_OK;
     const size_t nb = (size_t)nw * (size_t)h->N;
     const bool anchored = h->dl_valid && h->dl_log_ver == h->sd_log_ver && h->dl_N == h->N && h->dl_B == h->B;
     // the changed positions: per window rank r, between the anchor's and this refresh's suffix

@@ -256,17 +256,21 @@ hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int
 size_t hot_dedupe_scratch(const HotPart& g) { return (size_t)g.cap + (size_t)g.nbins * (size_t)g.nblk; }
 
 // ---------------------------------------------------------------- delta form
-// (kernels.hpp HotDelta.)  Per workgroup 1024 changed bindings, two keys each: (node * 8 +
-// bucket) * 2 + sign, -1 from the anchor bucket (sign 1) and +1 to the new one (sign 0),
+// (kernels.hpp HotDelta.)  Per workgroup 1024 changed bindings.  A binding whose position is
+// inside window rank k at one of the two times and outside at the other changes that rank's
+// count by one: key (node * 8 + k) * 2 + sign (sign 1: it left, -1; 0: it entered, +1) — one key
+// per crossed cutoff, at most two with two windows (the form's limit, kDeltaMaxWin).  Keys are
 // aggregated in the LDS hash as the dedupe form does (a Zipf-hot node costs one global atomic per
-// workgroup and bucket), then one atomicAdd per distinct key into adj.  Counts are modulo 2^32:
-// anchor + adj is the exact count.
+// workgroup and rank), then one atomicAdd per distinct key into adj [W][N] — per window rank, not
+// per bucket: K1 turns them into bucket adjustments (adj[b] - adj[b + 1]).  Counts are modulo
+// 2^32: anchor + adjustment is the exact count.
 constexpr int kDeltaChunk = 1024;
 
 template <int BT>
 __device__ __forceinline__ void k2_delta_body(const int32_t blk, const int32_t* __restrict__ bnode, int64_t N,
                                               const HotDelta& d, uint32_t* __restrict__ adj) {
     constexpr int kPer = kDeltaChunk / BT;
+    constexpr int kKeys = kPer * kDeltaMaxWin;  // key slots per thread: (binding, rank)
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     __shared__ uint32_t hist[32];  // (hash_add's bin counts: not read)
     int32_t* hkey = reinterpret_cast<int32_t*>(sh);
@@ -290,20 +294,18 @@ __device__ __forceinline__ void k2_delta_body(const int32_t blk, const int32_t* 
     }
     if (threadIdx.x < 32) hist[threadIdx.x] = 0;
     __syncthreads();
-    int32_t key[2 * kPer];
+    int32_t key[kKeys];
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
-        int ja = 0, jp = 0;
-        for (int r = 0; r < d.n_win; ++r) {
-            ja += pos[u] >= d.a[r] ? 1 : 0;
-            jp += pos[u] >= d.p[r] ? 1 : 0;
+        const bool ok = nd[u] >= 0 && (int64_t)nd[u] < N;  // binding.go:85-91 at both times
+#pragma unroll
+        for (int r = 0; r < kDeltaMaxWin; ++r) {
+            const bool ia = pos[u] >= d.a[r], ip = pos[u] >= d.p[r];
+            key[u * kDeltaMaxWin + r] = ok && r < d.n_win && ia != ip ? ((nd[u] * 8 + r) << 1) | (ia ? 1 : 0) : -1;
         }
-        const bool ch = nd[u] >= 0 && (int64_t)nd[u] < N && ja != jp;  // binding.go:85-91 at both cutoffs
-        key[2 * u] = ch && ja > 0 ? ((nd[u] * 8 + (ja - 1)) << 1) | 1 : -1;
-        key[2 * u + 1] = ch && jp > 0 ? (nd[u] * 8 + (jp - 1)) << 1 : -1;
     }
-    uint16_t* useg = uniq + (threadIdx.x >> 6) * (2 * kPer * 64);
-    const uint32_t nw = wave_aggregate<kDSlots, 2 * kPer>(key, hkey, hcnt, hist, 24, useg);
+    uint16_t* useg = uniq + (threadIdx.x >> 6) * (kKeys * 64);
+    const uint32_t nw = wave_aggregate<kDSlots, kKeys>(key, hkey, hcnt, hist, 24, useg);
     __syncthreads();
     for (uint32_t i = threadIdx.x & 63; i < nw; i += 64) {  // this wave's new keys
         const int s = useg[i];
@@ -329,7 +331,7 @@ __global__ __launch_bounds__(BT) void k2_delta_pods(const int32_t* __restrict__ 
 hipError_t launch_hot_count_delta(const int32_t* bnode, int64_t N, const HotDelta& d, uint32_t* adj, hipStream_t st,
                                   const PodPrep* pods) {
     constexpr int BT = 512;
-    if (d.n_rng < 0 || d.n_rng > kMaxWin || d.n_win < 1 || d.n_win > kMaxWin || N >= (1LL << 27))
+    if (d.n_rng < 0 || d.n_rng > kMaxWin || d.n_win < 1 || d.n_win > kDeltaMaxWin || N >= (1LL << 27))
         return hipErrorInvalidValue;
     const int64_t L = d.n_rng > 0 ? d.start[d.n_rng] : 0;
     const int64_t nb = (L + kDeltaChunk - 1) / kDeltaChunk;
@@ -338,7 +340,7 @@ hipError_t launch_hot_count_delta(const int32_t* bnode, int64_t N, const HotDelt
     const int64_t grid = pp.ntiles + nb;
     if (grid == 0) return hipSuccess;
     if (grid >= (1LL << 31)) return hipErrorInvalidValue;
-    size_t lds = sizeof(uint32_t) * 2 * (size_t)kDSlots + sizeof(uint16_t) * 2 * kDeltaChunk;
+    size_t lds = sizeof(uint32_t) * 2 * (size_t)kDSlots + sizeof(uint16_t) * kDeltaMaxWin * kDeltaChunk;
     if (pp.ntiles > 0) lds = std::max(lds, kK3pLds);
     return klaunch(pp.ntiles > 0 ? "k2_delta+k3p_pods" : "k2_delta", k2_delta_pods<BT>, dim3((unsigned)grid), dim3(BT),
                    lds, st, bnode, N, d, adj, pp);

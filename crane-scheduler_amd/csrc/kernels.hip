@@ -213,9 +213,9 @@ void k1_node_pass(K1Args a, K1Step step) {
             bc[b] = b < pol.n_win ? (buckets + first)[(int64_t)b * N + lo] : 0u;
             bz[b] = b < pol.n_win ? (base + first)[(int64_t)b * N + lo] : 0u;
         }
-        if (a.bucket_base) {
+        if (a.bucket_base) {  // (rows past n_win read as 0)
 #pragma unroll
-            for (int b = 0; b < kMaxWin; ++b) bc[b] += bz[b];
+            for (int b = 0; b < kMaxWin; ++b) bc[b] = bz[b] + bc[b] - (b + 1 < kMaxWin ? bc[b + 1] : 0u);
         }
     }
     if (!buckets && !hx && hv) {

@@ -226,12 +226,15 @@ size_t hot_dedupe_scratch(const HotPart& g);  // uint32 entries: regions + count
 hipError_t launch_hot_count_dedupe(const int32_t* bnode, const int64_t* bts, int64_t B, int64_t N,
                                    const HotCutoffs& cut, const HotPart& g, uint32_t* scratch, hipStream_t st,
                                    const PodPrep* pods = nullptr, int threads = 512);
-// Delta form (a time-ordered log whose window cutoffs moved since an anchor refresh): only the
-// bindings whose window rank differs between the anchor's suffix starts a[] and this refresh's
-// p[] (absolute positions, ascending by rank) are read; each adds -1 to its anchor bucket and +1
-// to its new one in the adjustment matrix adj [W][N] (zero on entry; K1 reads anchor + adj and
-// zeroes adj).  The changed positions are the merged ranges [lo_k, lo_k + len_k), start[] their
-// prefix lengths.  pods: K3p fused (its tiles first), as in the dedupe form.
+// Delta form (a time-ordered log whose window cutoffs moved since an anchor refresh; at most
+// kDeltaMaxWin windows): only the bindings whose window rank differs between the anchor's suffix
+// starts a[] and this refresh's p[] (absolute positions, ascending by rank) are read; each changes
+// the count of every window rank whose cutoff it crossed by -1 (left) or +1 (entered), in the
+// adjustment matrix adj [W][N] per window rank (zero on entry; K1 reads the anchor's buckets +
+// adj[b] - adj[b + 1] and zeroes adj).  The changed positions are the merged ranges
+// [lo_k, lo_k + len_k), start[] their prefix lengths.  pods: K3p fused (its tiles first), as in
+// the dedupe form.
+constexpr int kDeltaMaxWin = 2;
 struct HotDelta {
     int32_t n_win, n_rng;
     int64_t a[kMaxWin], p[kMaxWin];
@@ -352,7 +355,8 @@ struct K1Args {
     const double* hv;       // [N] or null
     const int64_t* hv_ts;   // [N] or null
     uint32_t* buckets;      // [W][N] K2 window-rank buckets or null
-    const uint32_t* bucket_base;  // [W][N] added to them (the delta form's anchor counts) or null
+    const uint32_t* bucket_base;  // [W][N] the delta form's anchor buckets, with buckets its per-rank
+                                  // adjustments (bucket b = base[b] + adj[b] - adj[b + 1]), or null
     int32_t buckets_keep;   // 1: leave them (the large form rewrites every row), 0: zero what was read
     int64_t hv_ts_counts;   // stamp of binding-log hot values
     void* out;              // NodeRec [N], or null (keys-only step: records not kept)
