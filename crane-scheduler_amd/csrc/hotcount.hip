@@ -265,6 +265,7 @@ size_t hot_dedupe_scratch(const HotPart& g) { return (size_t)g.cap + (size_t)g.n
 // per bucket: K1 turns them into bucket adjustments (adj[b] - adj[b + 1]).  Counts are modulo
 // 2^32: anchor + adjustment is the exact count.
 constexpr int kDeltaChunk = 1024;
+constexpr int kDeltaSlots = 4 * kDeltaChunk;  // two per key, at most two keys per binding
 
 template <int BT>
 __device__ __forceinline__ void k2_delta_body(const int32_t blk, const int32_t* __restrict__ bnode, int64_t N,
@@ -274,7 +275,7 @@ __device__ __forceinline__ void k2_delta_body(const int32_t blk, const int32_t* 
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     __shared__ uint32_t hist[32];  // (hash_add's bin counts: not read)
     int32_t* hkey = reinterpret_cast<int32_t*>(sh);
-    uint32_t* hcnt = sh + kDSlots;
+    uint32_t* hcnt = sh + kDeltaSlots;
     uint16_t* uniq = reinterpret_cast<uint16_t*>(hcnt + kDSlots);
     const int64_t L = d.start[d.n_rng];
     int64_t pos[kPer];
@@ -288,7 +289,7 @@ __device__ __forceinline__ void k2_delta_body(const int32_t blk, const int32_t* 
         nd[u] = bnode[t < L ? pos[u] : d.lo[0]];  // (unconditional load, clamped)
         if (t >= L) nd[u] = -1;
     }
-    for (int i = threadIdx.x; i < kDSlots; i += BT) {
+    for (int i = threadIdx.x; i < kDeltaSlots; i += BT) {
         hkey[i] = -1;
         hcnt[i] = 0;
     }
@@ -305,7 +306,7 @@ __device__ __forceinline__ void k2_delta_body(const int32_t blk, const int32_t* 
         }
     }
     uint16_t* useg = uniq + (threadIdx.x >> 6) * (kKeys * 64);
-    const uint32_t nw = wave_aggregate<kDSlots, kKeys>(key, hkey, hcnt, hist, 24, useg);
+    const uint32_t nw = wave_aggregate<kDeltaSlots, kKeys>(key, hkey, hcnt, hist, 24, useg);
     __syncthreads();
     for (uint32_t i = threadIdx.x & 63; i < nw; i += 64) {  // this wave's new keys
         const int s = useg[i];
@@ -340,7 +341,7 @@ hipError_t launch_hot_count_delta(const int32_t* bnode, int64_t N, const HotDelt
     const int64_t grid = pp.ntiles + nb;
     if (grid == 0) return hipSuccess;
     if (grid >= (1LL << 31)) return hipErrorInvalidValue;
-    size_t lds = sizeof(uint32_t) * 2 * (size_t)kDSlots + sizeof(uint16_t) * kDeltaMaxWin * kDeltaChunk;
+    size_t lds = sizeof(uint32_t) * 2 * (size_t)kDeltaSlots + sizeof(uint16_t) * kDeltaMaxWin * kDeltaChunk;
     if (pp.ntiles > 0) lds = std::max(lds, kK3pLds);
     return klaunch(pp.ntiles > 0 ? "k2_delta+k3p_pods" : "k2_delta", k2_delta_pods<BT>, dim3((unsigned)grid), dim3(BT),
                    lds, st, bnode, N, d, adj, pp);
