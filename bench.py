@@ -231,7 +231,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=8,
+                    help="untimed batches first: two per batch slot, so every slot has anchored its hot-value "
+                         "counts (delta form) and sized its scratch before the timed region")
     ap.add_argument("--config", type=int, default=3, choices=(3, 4))
     ap.add_argument("--cpu-pods", type=int, default=1920, help="pods in the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16, help="upstream kube-scheduler parallelism")
