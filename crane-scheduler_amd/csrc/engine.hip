@@ -210,6 +210,7 @@ struct crane_dyn {
     // delta form (hot_delta_locked): dense anchor counts at suffix starts dl_pos (valid for log
     // version dl_log_ver, N dl_N), the adjustments of the next node pass (zero unless dl_adj_dirty)
     bool dl_valid = false, dl_pending = false, dl_adj_dirty = true;
+    bool dl_zero = false;  // this refresh has no binding in any window (K1: adjustments as the anchor)
     uint64_t dl_log_ver = 0;
     int64_t dl_N = -1, dl_B = -1;
     int64_t dl_pos[kMaxWin] = {};
@@ -513,13 +514,18 @@ static int hot_delta_locked(crane_dyn* h, int64_t Bk, const HotCutoffs& pcut, hi
         if (int rc = zero_for(h, h->dl_adj.p, h->dl_adj.n, st)) return rc;
         h->dl_adj_dirty = false;
     }
-    if (!anchored || 2 * L > Bk) {
+    h->dl_zero = false;
+    if (Bk == 0) {
+        // no binding inside any window: every count is zero — K1 reads the (clean) adjustments as
+        // the anchor too; the anchor itself is kept for the next refresh
+        h->dl_zero = true;
+    } else if (!anchored || 2 * L > Bk) {
         const HotPart gl = hot_large_geometry(Bk, h->N, nw);
         const HotPart gf = hot_large_geometry(h->B, h->N, nw);
         if (!gl.ok) return CRANE_OK;
         HIPTRY(h, h->dl_base.reserve(nb));
-        HIPTRY(h, h->k2_sorted.reserve(std::max(hot_dedupe_scratch(gl), gf.ok ? hot_dedupe_scratch(gf) : 0)));
         h->dl_valid = false;
+        HIPTRY(h, h->k2_sorted.reserve(std::max(hot_dedupe_scratch(gl), gf.ok ? hot_dedupe_scratch(gf) : 0)));
         HIPTRY(h, launch_hot_count_large(h->sd->bnode.p + h->pos_s[0], h->sd->bts.p, Bk, h->N, pcut, gl,
                                          h->k2_sorted.p, h->dl_base.p, h->n_cu, st, kK2lThreads));
         std::memcpy(h->dl_pos, h->pos_s, sizeof(int64_t) * nw);
@@ -690,7 +696,7 @@ static int node_pass_locked(crane_dyn* h, hipStream_t st, uint32_t* cnt_out = nu
             a.hx_nblk = g.nblk;
         } else if (h->dl_pending) {
             a.buckets = h->dl_adj.p;  // read and zeroed
-            a.bucket_base = h->dl_base.p;
+            a.bucket_base = h->dl_zero ? h->dl_adj.p : h->dl_base.p;
             a.buckets_keep = 0;
         } else {
             a.buckets = h->buckets.p;

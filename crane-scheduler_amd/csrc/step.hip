@@ -114,7 +114,7 @@ constexpr int kK3sPods = kK3sThreads * kK3sPPL;     // pods per workgroup (= kPo
 // same box (option k3s_blocks, tools/gpu_r03k3.sh / gpu_r03k3b.sh): shard 0.0343 -> 0.0300 ms
 // per batch with 4 in flight (R 16 -> 8), config 3 unchanged (0.0120-0.0126); 32 per tile (16
 // blocks) had measured 0.0128 vs 0.0123 at config 3 in round 2
-constexpr int kK3sBlkPerWg = 64;
+constexpr int kK3sBlkPerWg = 64;  // (round 6, 8-wave K3s: 32 per workgroup within noise, 16 slower: profiles/r06/ab/k3s_blocks_per_wg.txt)
 // Work lists (k3s_eval) for slices of at most kK3sListBlk blocks, holding at most this many
 // straddling records / middle pieces (more: the blocks' teams).  Same-box A/B at configs 3 / 4
 // (one GPU) / 4 shard against the team loops alone: K3s 0.0397 -> 0.0364 ms per batch,
