@@ -849,16 +849,30 @@ class DynamicScheduler {
             job->n = L.size();
             job->chunk = kScanChunk;
             job->nchunks = (job->n + kScanChunk - 1) / kScanChunk;
-            job->changed.resize(job->nchunks);
-            job->added.resize(job->nchunks);
+            // every chunk's lists hold a whole chunk already (kept across cycles): the cycle's
+            // other callers never allocate (a first allocation on a thread maps a malloc arena)
+            job->changed = std::move(scan_changed_);
+            job->added = std::move(scan_added_);
+            if (job->changed.size() < job->nchunks) job->changed.resize(job->nchunks);
+            if (job->added.size() < job->nchunks) job->added.resize(job->nchunks);
+            for (size_t c = 0; c < job->nchunks; ++c) {
+                job->changed[c].clear();
+                job->added[c].clear();
+                job->changed[c].reserve(kScanChunk);
+                job->added[c].reserve(kScanChunk);
+            }
             if (state && job->nchunks > 1) {
                 state->dyn_job_ = job;
                 state->dyn_phase_.store(2, std::memory_order_release);
             }
             job->work();
             while (job->done.load(std::memory_order_acquire) < job->nchunks) relax();
-            for (const auto& c : job->changed) changed_.insert(changed_.end(), c.begin(), c.end());
-            for (const auto& c : job->added) added_.insert(added_.end(), c.begin(), c.end());
+            for (size_t c = 0; c < job->nchunks; ++c) {
+                changed_.insert(changed_.end(), job->changed[c].begin(), job->changed[c].end());
+                added_.insert(added_.end(), job->added[c].begin(), job->added[c].end());
+            }
+            scan_changed_ = std::move(job->changed);  // (every chunk is done: no caller touches them)
+            scan_added_ = std::move(job->added);
         }
         // the live rows no NodeInfo of this snapshot claimed: the nodes that left
         if (L.size() - added_.size() != v->live)
@@ -955,6 +969,7 @@ class DynamicScheduler {
     // scratch of the syncs (under mu_)
     std::vector<std::string> keys_;
     std::vector<int64_t> changed_, added_, removed_;
+    std::vector<std::vector<int64_t>> scan_changed_, scan_added_;  // ScanJob's per-chunk lists, reused
     std::vector<const Node*> cnodes_;
     std::vector<const char*> strs_;
     std::vector<size_t> lens_;

@@ -354,6 +354,7 @@ int main(int argc, char** argv) {
     int threads = 16;
     int node_events = 0;
     bool cpu = false;
+    bool lead_main = false;  // the caller's thread makes each cycle's first Filter call (probe)
     double churn_scale = 0.0;
     std::string churn_log;
     uint64_t seed = 1;
@@ -363,6 +364,7 @@ int main(int argc, char** argv) {
         auto next = [&]() -> std::string { return a + 1 < argc ? argv[++a] : ""; };
         if (k == "--threads") threads = std::atoi(next().c_str());
         else if (k == "--cpu") cpu = true;
+        else if (k == "--lead-main") lead_main = true;
         else if (k == "--churn") churn_scale = std::atof(next().c_str());
         else if (k == "--churn-log") churn_log = next();
         else if (k == "--seed") seed = std::strtoull(next().c_str(), nullptr, 10);
@@ -542,6 +544,7 @@ int main(int argc, char** argv) {
         st.now_ns = p.now;
         // (the cycle's first Filter calls bring the plugin up to date: the first one leads the
         // sync, the pool's other threads take chunks of its snapshot scan)
+        if (lead_main && !cpu && N > 0) (void)ds.Filter(st, p.pod, *snap.list[0]);
         pool.until(N, [&](int64_t i) {  // findNodesThatPassFilters
             Status s;
 #ifdef DROPIN_CPU
