@@ -62,6 +62,8 @@ KERNEL_PMC = {
     "k1_node_pass": ("crane::k1_node_pass", {3: "false"}),
     "k2x_dedupe+k3p_pods": ("crane::k2x_dedupe_pods", {}),
     "k2x_dedupe": ("crane::k2x_dedupe", {}),
+    "k2_delta+k3p_pods": ("crane::k2_delta_pods", {}),
+    "k2_delta": ("crane::k2_delta_pods", {}),
     "k3p_pods": ("crane::k3p_pods", {}),
     "k3s_eval": ("crane::k3s_eval", {}),
     "k3m_matrix+keys": ("crane::k3m_matrix", {-2: "true", -1: "true"}),

@@ -43,7 +43,10 @@ def test_k2_path_traffic_picks_each_paths_kernels():
 
 def test_committed_summaries_resolve_every_leg():
     pmc3 = _summary("3")
-    assert bench.pmc_traffic(pmc3, "k1_node_pass+k3a_steps") is not None
+    # the headline step's node pass: the streamed one beside the delta form's dense rows, the
+    # record-holding one beside dedupe-form entries; the delta form's K2 + K3p launch
+    assert (bench.pmc_traffic(pmc3, "k1_stream_steps") or bench.pmc_traffic(pmc3, "k1_node_pass+k3a_steps")) is not None
+    assert (bench.pmc_traffic(pmc3, "k2_delta+k3p_pods") or bench.pmc_traffic(pmc3, "k2x_dedupe+k3p_pods")) is not None
     cold = _summary("cold")
     # the cold leg's step pass (bench.cold_leg: the streamed pass, else the fused one) and the
     # record-writing pass
