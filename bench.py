@@ -1066,17 +1066,20 @@ def measure_group(cd, synth, spec, args, n_dev, dev):
     devs = [torch.device("cuda", d) for d in range(n_dev)]
     d_now = [[torch.from_numpy(p).to(dv) for dv in devs] for p in pods]
     d_flags = [torch.from_numpy(g_all.ds).to(dv) for dv in devs]
-    d_keys = [[torch.empty(P, dtype=torch.int64, device=dv) for dv in devs] for _ in range(K)]
+    # two key buffers per slot, alternating: a slot's step leaves its last kernel (K3s) to the slot's
+    # next step (engine option step_defer, set by the group on its queues), which must not reset
+    # keys it still writes
+    d_keys = [[torch.empty(P, dtype=torch.int64, device=dv) for dv in devs] for _ in range(2 * K)]
     seq = [0]  # batches enqueued on the group so far: batch b runs on slot b % K
     recent = []  # (keys getter, cycle position) of the latest batches, newest last
     if not coll_on:
-        # one batch per call (crane_dyn_group_step_keys_async), each slot its key buffer
-        fns = [[grp.step_keys_fn(d_now[t], d_flags, d_keys[s]) for t in range(C)] for s in range(K)]
+        # one batch per call (crane_dyn_group_step_keys_async)
+        fns = [[grp.step_keys_fn(d_now[t], d_flags, d_keys[s]) for t in range(C)] for s in range(2 * K)]
         G = 1
 
         def step(i):
             t = i % C
-            s_ = seq[0] % K
+            s_ = seq[0] % (2 * K)
             fns[s_][t](nows[t], nows[t])
             recent.append((lambda s_=s_: d_keys[s_][0], t))
             del recent[:-2]

@@ -134,6 +134,7 @@ def _load():
         "crane_queue_destroy": (C.c_int, [vp]),
         "crane_dyn_step_keys_queue": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp, vp]),
         "crane_dyn_forget_queue": (C.c_int, [vp, vp]),
+        "crane_dyn_step_flush": (C.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -167,7 +168,7 @@ ABI_SYMBOLS = (
     "crane_dyn_group_gc_bindings", "crane_dyn_group_binding_count", "crane_dyn_group_refresh_hot_values",
     "crane_dyn_group_hot_values", "crane_dyn_group_node_steps",
     "crane_queue_create", "crane_queue_wait", "crane_queue_last_error", "crane_queue_destroy",
-    "crane_dyn_step_keys_queue", "crane_dyn_forget_queue",
+    "crane_dyn_step_keys_queue", "crane_dyn_forget_queue", "crane_dyn_step_flush",
 )
 
 
@@ -570,6 +571,10 @@ class Engine:
         self._check(lib.crane_dyn_step_keys_queue(self.h, int(now_ns), int(hv_ts_ns), P, C.c_void_p(d_now.data_ptr()),
                                                   None if d_flags is None else C.c_void_p(d_flags.data_ptr()),
                                                   C.c_void_p(d_keys.data_ptr()), queue.h))
+
+    def step_flush(self):
+        """Option step_defer: run the last queue step's deferred K3s now (crane_dyn_step_flush)."""
+        self._check(lib.crane_dyn_step_flush(self.h))
 
     def step_keys_fn(self, d_now, d_flags, d_keys, stream=None):
         """step_keys_async bound to fixed device buffers and stream: returns f(now_ns, hv_ts_ns).

@@ -135,6 +135,8 @@ struct Options {
     int k2_sorted = 1;        // a time-ordered log: K2 reads the widest window's suffix, ranks by position
     int k2_delta = 1;         // ... and, once anchored, only the bindings whose window rank changed since
                               // the anchor refresh (delta form, HotDelta); 0: every refresh re-counts
+    int step_defer = 0;       // 1: a step on a dispatch queue leaves its K3s to the engine's next step,
+                              // which runs it in its first launch (crane_dyn_step_flush; the group sets it)
 };
 // Fixed launch shapes (round 6 removed their options; the A/B sweeps that chose them are in
 // profiles/ab/r03_k2_cold_*.txt and profiles/r05/config3_option_sweep_queues.txt)
@@ -247,7 +249,21 @@ struct crane_dyn {
     DevBuf<unsigned long long> trace;  // [3][kTraceWgs][8] phase stamps (option "trace")
     DevBuf<int32_t> sperm, scnt;  // K3 step path scratch (step.hip)
     DevBuf<int64_t> stile, spnow, sbatch;
-    int sbatch_par = 0;  // the range of sbatch the next step folds into (StepPlan::batch)
+    DevBuf<int32_t> sperm2;       // ... the second set of K3p's outputs: steps alternate (sbatch_par)
+    DevBuf<int64_t> stile2, spnow2;
+    int sbatch_par = 0;  // the range of sbatch and the K3p output set the next step uses (StepPlan)
+    // option step_defer: the last step's K3s, not launched yet (its queue, tables, pod set, keys)
+    struct PendK3s {
+        bool on = false;
+        crane_queue* q = nullptr;
+        StepTables stt{};
+        StepGeometry g{};
+        const int32_t* perm = nullptr;
+        const int64_t* pnow = nullptr;
+        const int64_t* tiles = nullptr;
+        int64_t P = 0;
+        long long* keys = nullptr;
+    } pend;
     DevBuf<int64_t> sel_fth, sel_win, sel_state;  // framework selection (select.hip)
     DevBuf<long long> sel_keys;
     DevBuf<unsigned char> stp_dev;  // node answer tables (crane_dyn_node_steps): bp, ns, ff, score
@@ -361,13 +377,18 @@ int adopt(crane_dyn* h) {
 // Every ABI entry that enqueues work holds the engine mutex, takes a shared shard's changes
 // (adopt; rc holds its error) and installs the engine's kernel timer on the calling thread while
 // profiling is on.
+int flush_pending(crane_dyn* h);
+
 struct Locked {
     std::lock_guard<std::mutex> g;
     KernelTimer* prev;
     int rc = 0;
-    explicit Locked(crane_dyn* h) : g(h->mu), prev(tl_ktimer) {
+    // keep_pending: the caller is a step on a dispatch queue, which takes a deferred K3s into its
+    // own first launch (option step_defer); every other call runs it first
+    explicit Locked(crane_dyn* h, bool keep_pending = false) : g(h->mu), prev(tl_ktimer) {
         tl_ktimer = h->prof ? &h->timer : nullptr;
-        if (h->sd && (h->sd_node_ver != h->sd->node_ver || h->sd_log_ver != h->sd->log_ver)) rc = adopt(h);
+        if (!keep_pending && h->pend.on) rc = flush_pending(h);
+        if (!rc && h->sd && (h->sd_node_ver != h->sd->node_ver || h->sd_log_ver != h->sd->log_ver)) rc = adopt(h);
     }
     ~Locked() { tl_ktimer = prev; }
 };
@@ -534,10 +555,18 @@ static int hot_delta_locked(crane_dyn* h, int64_t Bk, const HotCutoffs& pcut, hi
         h->dl_N = h->N;
         h->dl_B = h->B;
     } else {
-        d.trace = h->trace_region(0);  // (the delta launch stays far below kTraceWgs workgroups at
-                                       // config 3; larger ones are not traced)
-        if ((pods ? pods->ntiles : 0) + (L + 1023) / 1024 > kTraceWgs) d.trace = nullptr;
-        HIPTRY(h, launch_hot_count_delta(h->sd->bnode.p, h->N, d, h->dl_adj.p, st, pods));
+        crane_dyn::PendK3s& pk = h->pend;
+        if (pk.on && tl_aql && pk.q == tl_aql && pods && pods->P > 0) {
+            // the previous step's K3s in this launch (option step_defer: step.hip k3s_delta_pods)
+            HIPTRY(h, launch_k3s_delta_pods(h->N, h->node_offset, pk.P, pk.keys, pk.stt, pk.g, pk.perm, pk.pnow,
+                                            pk.tiles, h->sd->bnode.p, h->N, d, h->dl_adj.p, *pods, st));
+            pk.on = false;
+        } else {
+            d.trace = h->trace_region(0);  // (the delta launch stays far below kTraceWgs workgroups at
+                                           // config 3; larger ones are not traced)
+            if ((pods ? pods->ntiles : 0) + (L + 1023) / 1024 > kTraceWgs) d.trace = nullptr;
+            HIPTRY(h, launch_hot_count_delta(h->sd->bnode.p, h->N, d, h->dl_adj.p, st, pods));
+        }
         if (pods_done) *pods_done = pods != nullptr && pods->P > 0;
     }
     h->dl_adj_dirty = true;  // (until the node pass reads and zeroes the adjustments)
@@ -731,6 +760,9 @@ struct StepPlan {
     bool fuse;  // K3a fused into the node pass (records stale)
     int64_t* batch;       // this step's time range (K3p folds it, K1 reads it)
     int64_t* batch_next;  // the other range: reset by K3p for the next step
+    int32_t* perm;        // this step's K3p outputs (one of two sets, by sbatch_par)
+    int64_t* pnow;
+    int64_t* tiles;
 };
 
 static bool step_path_ok(const crane_dyn* h, int64_t P) {
@@ -745,6 +777,9 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     const StepGeometry& g = sp.g;
     HIPTRY(h, h->sperm.reserve((size_t)(g.ntiles * 1024)));
     HIPTRY(h, h->stile.reserve((size_t)(kTileStat * g.ntiles)));
+    HIPTRY(h, h->sperm2.reserve((size_t)(g.ntiles * 1024)));
+    HIPTRY(h, h->stile2.reserve((size_t)(kTileStat * g.ntiles)));
+    HIPTRY(h, h->spnow2.reserve((size_t)(g.ntiles * 1024)));
     if (!h->sbatch.p) {  // two {tmin, tmax} ranges, alternating between steps, start empty
         HIPTRY(h, h->sbatch.reserve(4));
         // on the engine stream and waited for: a null-stream copy is not ordered with the
@@ -759,6 +794,9 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     sp.batch = h->sbatch.p + 2 * h->sbatch_par;
     sp.batch_next = h->sbatch.p + 2 * (h->sbatch_par ^ 1);
     HIPTRY(h, h->spnow.reserve((size_t)(g.ntiles * 1024)));
+    sp.perm = h->sbatch_par ? h->sperm2.p : h->sperm.p;
+    sp.pnow = h->sbatch_par ? h->spnow2.p : h->spnow.p;
+    sp.tiles = h->sbatch_par ? h->stile2.p : h->stile.p;
     HIPTRY(h, h->scnt.reserve((size_t)std::max<int32_t>(nblk, 1) * 6));  // cnt [nblk][4] + flat [nblk][2]
     // per kind and producer block: 2 * bs one-step records, bs * (breakpoints - 1) middle pieces
     const int64_t s1pad = 2 * g.npad, mstride = (int64_t)bs * (step_breakpoints(h->shape) - 1);
@@ -787,7 +825,7 @@ static int step_plan(crane_dyn* h, int64_t P, StepPlan& sp) {
     t.nblk = nblk;
     t.mstride = (int32_t)mstride;
     t.ntiles = (int32_t)g.ntiles;
-    t.tiles = h->stile.p;
+    t.tiles = sp.tiles;
     const int64_t nrows = g.ntiles * (int64_t)nblk;
     if (h->opt.step_rows && nrows <= kStepRowsMax) {
         HIPTRY(h, h->srows.reserve((size_t)std::max<int64_t>(nrows, 1)));
@@ -808,17 +846,18 @@ static void pods_ran(crane_dyn* h, int64_t P) {
 
 static int step_pods(crane_dyn* h, const StepPlan& sp, int64_t P, const int64_t* d_now, const uint8_t* d_flags,
                      long long* d_keys, hipStream_t st) {
-    HIPTRY(h, launch_step_pods(d_now, d_flags, P, d_keys, sp.batch, sp.batch_next, sp.g, h->sperm.p, h->spnow.p,
-                               h->stile.p, st));
+    HIPTRY(h, launch_step_pods(d_now, d_flags, P, d_keys, sp.batch, sp.batch_next, sp.g, sp.perm, sp.pnow, sp.tiles,
+                               st));
     pods_ran(h, P);
     return CRANE_OK;
 }
 
-static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_keys, hipStream_t st) {
+static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_keys, hipStream_t st,
+                     bool defer = false) {
     if (P == 0) return CRANE_OK;
     if (sp.fuse) {
         // (the records the fused step leaves stale serve as the streamed pass's scratch)
-        const K1Step ks{h->stile.p, sp.batch, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, h->dp.winv, sp.stt,
+        const K1Step ks{sp.tiles, sp.batch, (int32_t)sp.g.ntiles, h->dp.noprio, h->dp.wsum, h->dp.winv, sp.stt,
                         h->rec.p, h->opt.k1_tail};
         int rc = node_pass_locked(h, st, nullptr, &ks);
         if (rc) return rc;
@@ -827,11 +866,42 @@ static int step_rest(crane_dyn* h, const StepPlan& sp, int64_t P, long long* d_k
             int rc = node_pass_locked(h, st);
             if (rc) return rc;
         }
-        HIPTRY(h, launch_step_nodes(h->shape, h->rec.p, h->N, h->dp.wsum, h->dp.noprio, sp.stt, sp.g, h->stile.p, st));
+        HIPTRY(h, launch_step_nodes(h->shape, h->rec.p, h->N, h->dp.wsum, h->dp.noprio, sp.stt, sp.g, sp.tiles, st));
     }
-    HIPTRY(h, launch_step_pairs(h->shape, h->N, h->node_offset, P, d_keys, sp.stt, sp.g, h->sperm.p, h->spnow.p, h->stile.p, st));
+    if (defer) {  // (the next step's first launch runs it: PendK3s)
+        crane_dyn::PendK3s& pk = h->pend;
+        pk.on = true;
+        pk.q = tl_aql;
+        pk.stt = sp.stt;
+        pk.g = sp.g;
+        pk.perm = sp.perm;
+        pk.pnow = sp.pnow;
+        pk.tiles = sp.tiles;
+        pk.P = P;
+        pk.keys = d_keys;
+        return CRANE_OK;
+    }
+    HIPTRY(h, launch_step_pairs(h->shape, h->N, h->node_offset, P, d_keys, sp.stt, sp.g, sp.perm, sp.pnow, sp.tiles, st));
     return CRANE_OK;
 }
+
+// option step_defer: the last step's K3s launched now on its queue (alone) and committed
+namespace {
+int flush_pending(crane_dyn* h) {
+    crane_dyn::PendK3s& pk = h->pend;
+    if (!pk.on) return CRANE_OK;
+    pk.on = false;
+    crane_queue* const prev = tl_aql;
+    tl_aql = pk.q;
+    const hipError_t e = launch_step_pairs(h->shape, h->N, h->node_offset, pk.P, pk.keys, pk.stt, pk.g, pk.perm,
+                                           pk.pnow, pk.tiles, h->stream);
+    const hipError_t c = aql_commit(pk.q);
+    tl_aql = prev;
+    if (e != hipSuccess) return h->hipfail(e, "deferred k3s_eval");
+    if (c != hipSuccess) return h->fail(CRANE_E_HIP, std::string("queue: ") + aql_error(pk.q));
+    return CRANE_OK;
+}
+}  // namespace
 
 // The per-pair kernel (K3m): first-fail / score matrices [P][ld] and/or keys.
 static int matrix_locked(crane_dyn* h, int64_t P, const int64_t* d_now, const uint8_t* d_flags, long long* d_keys,
@@ -905,6 +975,7 @@ static int mark_busy(crane_dyn* h, hipStream_t st) {
 // engines' batches and collectives in flight are not drained.  State changes are per
 // snapshot sync / controller tick, not per batch.
 static int quiesce(crane_dyn* h) {
+    if (int rc = flush_pending(h)) return rc;
     if (!h->busy_q.empty()) {
         std::vector<crane_queue*> qs;
         qs.swap(h->busy_q);
@@ -937,6 +1008,7 @@ int crane::engine_share_shard(crane_dyn* h, crane_dyn* from) {
 // a queue being destroyed hands itself back (aql.cpp; it has waited for its steps)
 void crane::engine_drop_queue(crane_dyn* h, crane_queue* q) {
     std::lock_guard<std::mutex> g(h->mu);
+    if (h->pend.q == q) h->pend.on = false;  // (a deferred K3s on a queue going away: not run)
     h->busy_q.erase(std::remove(h->busy_q.begin(), h->busy_q.end(), q), h->busy_q.end());
     h->seen_q.erase(std::remove(h->seen_q.begin(), h->seen_q.end(), q), h->seen_q.end());
 }
@@ -995,6 +1067,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     // engine_drop_queue): wait for the ones with steps of this engine, then unregister
     {
         std::lock_guard<std::mutex> g(h->mu);
+        (void)flush_pending(h);
         for (crane_queue* q : h->busy_q) (void)aql_wait(q);
         for (crane_queue* q : h->seen_q) aql_remove_user(q, h);
         h->busy_q.clear();
@@ -1012,6 +1085,7 @@ int crane_dyn_destroy(crane_dyn* h) {
     h->mH.release(); h->mbs.release(); h->mflag.release(); h->mapos.release(); h->mtk.release();
     h->mFs.release(); h->mIs.release(); h->mgi.release();
     h->trace.release();
+    h->sperm2.release(); h->stile2.release(); h->spnow2.release();
     h->sperm.release(); h->scnt.release(); h->stile.release(); h->sbatch.release(); h->spnow.release(); h->smid.release(); h->sstep1.release(); h->sstage.release();
     h->spm1.release(); h->ssm0.release(); h->srows.release(); h->sprow.release();
     h->sel_fth.release(); h->sel_win.release(); h->sel_state.release(); h->sel_keys.release();
@@ -1034,9 +1108,17 @@ int crane_dyn_forget_stream(crane_dyn* h, void* stream) {
     return CRANE_OK;
 }
 
+int crane_dyn_step_flush(crane_dyn* h) {
+    if (!h) return CRANE_E_INVALID;
+    Locked lk(h);  // (runs a deferred K3s)
+    return lk.rc;
+}
+
 int crane_dyn_forget_queue(crane_dyn* h, crane_queue* q) {
     if (!h) return CRANE_E_INVALID;
     std::lock_guard<std::mutex> g(h->mu);
+    if (h->pend.on && h->pend.q == q)
+        if (int rc = flush_pending(h)) return rc;
     auto sq = std::find(h->seen_q.begin(), h->seen_q.end(), q);
     if (sq != h->seen_q.end()) {
         h->seen_q.erase(sq);
@@ -1071,6 +1153,7 @@ int crane_dyn_set_option(crane_dyn* h, const char* name, int64_t value) {
     else if (n == "step_lds_cap" && value >= 0) o.step_lds_cap = (int)std::min<int64_t>(value, 1 << 30);
     else if (n == "k2_sorted" && range(0, 1)) o.k2_sorted = (int)value;
     else if (n == "k2_delta" && range(0, 1)) o.k2_delta = (int)value;
+    else if (n == "step_defer" && range(0, 1)) o.step_defer = (int)value;
     else if (n == "k1_stream" && range(0, 1)) o.k1_stream = (int)value;
     else if (n == "k1_tail" && (value == 0 || value == 1 || value == 4)) o.k1_tail = (int)value;
     else if (n == "trace" && range(0, 1)) {
@@ -1445,8 +1528,7 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
     StepPlan sp;
     int rc = step_plan(h, P, sp);
     if (rc) return rc;
-    const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys, sp.batch,
-                         sp.batch_next};
+    const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, sp.perm, sp.pnow, sp.tiles, keys, sp.batch, sp.batch_next};
     bool pods_done = false;
     rc = hot_values_locked(h, now_ns, hv_ts_ns, st, &pp, &pods_done);
     if (pods_done) pods_ran(h, P);
@@ -1458,7 +1540,7 @@ int crane_dyn_step_keys_async(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
 int crane_dyn_step_keys_queue(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, int64_t P, const int64_t* d_now,
                               const uint8_t* d_flags, int64_t* d_keys, crane_queue* q) {
     if (!h) return CRANE_E_INVALID;
-    Locked lk(h);
+    Locked lk(h, true);  // (a deferred K3s goes into this step's first launch)
     if (lk.rc) return lk.rc;
     if (!q) return h->fail(CRANE_E_INVALID, "null queue");
     if (P < 0 || (P > 0 && (!d_now || !d_keys))) return h->fail(CRANE_E_INVALID, "bad pod arrays");
@@ -1481,19 +1563,24 @@ int crane_dyn_step_keys_queue(crane_dyn* h, int64_t now_ns, int64_t hv_ts_ns, in
         explicit OnQueue(crane_queue* x) { tl_aql = x; }
         ~OnQueue() { tl_aql = nullptr; }
     };
-    int rc;
+    int rc = CRANE_OK;
     {
         OnQueue on(q);
+        const bool defer = h->opt.step_defer != 0;
+        // a deferred K3s of another queue, or one writing the keys this step writes (its K3p resets
+        // them), runs first, alone
+        if (h->pend.on && (h->pend.q != q || h->pend.keys == keys || !defer)) rc = flush_pending(h);
         h->rec_dirty = true;
         StepPlan sp{};
-        rc = step_plan(h, P, sp);
-        const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, h->sperm.p, h->spnow.p, h->stile.p, keys, sp.batch,
-                         sp.batch_next};
+        if (!rc) rc = step_plan(h, P, sp);
+        const PodPrep pp{d_now, d_flags, P, sp.g.ntiles, sp.perm, sp.pnow, sp.tiles, keys, sp.batch, sp.batch_next};
         bool pods_done = false;
         if (!rc) rc = hot_values_locked(h, now_ns, hv_ts_ns, h->stream, &pp, &pods_done);
         if (pods_done) pods_ran(h, P);
+        // (not taken into the first launch: before this step's node pass rewrites its tables)
+        if (!rc && h->pend.on) rc = flush_pending(h);
         if (!rc && !pods_done) rc = step_pods(h, sp, P, d_now, d_flags, keys, h->stream);
-        if (!rc) rc = step_rest(h, sp, P, keys, h->stream);
+        if (!rc) rc = step_rest(h, sp, P, keys, h->stream, defer);
     }
     // (what was written runs even after an error: the packets before it are whole)
     const hipError_t ce = aql_commit(q);

@@ -117,6 +117,7 @@ struct crane_dyn_group {
     // (crane_dyn_group_step_keys_async / _schedule with the collective on: RCCL follows each batch
     // on its stream).  ring_kind of their kernargs
     int dispatch = -1, ring_kind = 0;
+    int defer = 1;  // engine option step_defer on the queues' engines (a step's K3s in the slot's next launch)
     std::vector<std::vector<crane_queue*>> q;  // [slot][shard]
     bool comm_broken = false;
     uint64_t batch = 0;
@@ -226,7 +227,17 @@ int run_job_dev(crane_dyn_group* g, int i, const Job& j, std::string* msg) {
             *msg = who + ": " + hipGetErrorString(r);
             return CRANE_E_HIP;
         }
-        if (j.qmode) return 0;  // (held until the queues completed the window: pcoll_push)
+        if (j.qmode) {
+            // the window's deferred K3s (option step_defer) run now, so the targets pcoll_push reads
+            // count them; then held until the queues completed the window
+            for (int sl = 0; sl < g->depth; ++sl)
+                if (j.slots >> sl & 1)
+                    if (int rc = crane_dyn_step_flush(g->eng[(size_t)sl][(size_t)i])) {
+                        *msg = who + ": " + crane_dyn_last_error(g->eng[(size_t)sl][(size_t)i]);
+                        return rc;
+                    }
+            return 0;
+        }
         for (int sl = 0; sl < g->depth; ++sl)
             if (j.slots >> sl & 1)
                 if (hipError_t r = order_after_slot(g, i, sl)) {
@@ -524,6 +535,11 @@ int wait_all(crane_dyn_group* g) {
         w->ecode = 0;
         w->emsg.clear();
     }
+    // the slots' deferred K3s (option step_defer), from this thread: the workers are idle
+    for (size_t s = 0; s < g->eng.size(); ++s)
+        for (size_t i = 0; i < g->eng[s].size(); ++i)
+            if (g->eng[s][i] && crane_dyn_step_flush(g->eng[s][i]) && !rc)
+                rc = engine_err(g, g->eng[s][i], CRANE_E_HIP, (int)i);
     if (rc && !g->comm.empty() && !g->comm_broken) {
         // a device that failed may have left the others' all-reduce kernels waiting for it:
         // abort the communicators (their kernels see the abort flag and exit) before waiting
@@ -676,6 +692,9 @@ int ensure_queues(crane_dyn_group* g, bool* qmode) {
                 return g->fail(CRANE_E_HIP, m);
             }
             g->q[(size_t)s][(size_t)i] = qq;
+            // the slot's K3s rides in its next step's first launch (flushed at wait_all)
+            if (g->eng[(size_t)s][(size_t)i])
+                (void)crane_dyn_set_option(g->eng[(size_t)s][(size_t)i], "step_defer", g->defer);
         }
     return 0;
 }
@@ -883,6 +902,15 @@ int crane_dyn_group_set_option(crane_dyn_group* g, const char* name, int64_t val
     GLock lk(g);
     if (g->n <= 0) return g->fail(CRANE_E_STATE, "group was not created successfully");
     const std::string nm = name;
+    if (nm == "defer") {
+        if (value < 0 || value > 1) return g->fail(CRANE_E_INVALID, "defer: 0 | 1");
+        if (wait_all(g)) return CRANE_E_STATE;
+        g->defer = (int)value;
+        for (auto& row : g->eng)
+            for (crane_dyn* e : row)
+                if (e) (void)crane_dyn_set_option(e, "step_defer", g->q.empty() ? 0 : value);
+        return 0;
+    }
     if (nm == "dispatch" || nm == "dispatch_ring") {
         if (value < (nm == "dispatch" ? -1 : 0) || value > 1)
             return g->fail(CRANE_E_INVALID, nm + (nm == "dispatch" ? ": -1 | 0 | 1" : ": 0 | 1"));
@@ -1253,6 +1281,8 @@ int crane_dyn_group_schedule(crane_dyn_group* g, int64_t now_ns, int64_t hv_ts_n
     const int nk = g->use_coll() ? 1 : g->n;
     for (int i = 0; i < nk; ++i) {
         hipStream_t s = g->st[(size_t)slot][(size_t)i];
+        // (the step's deferred K3s, option step_defer: run now)
+        if (int rc = crane_dyn_step_flush(g->eng[(size_t)slot][(size_t)i])) return engine_err(g, g->eng[(size_t)slot][(size_t)i], rc, i);
         if (crane_queue* qq = qmode ? g->queue(slot, i) : nullptr)
             if (crane_queue_wait(qq)) return g->fail(CRANE_E_HIP, std::string("queue: ") + crane_queue_last_error(qq));
         hipError_t e = hipSetDevice(g->dev[(size_t)i]);

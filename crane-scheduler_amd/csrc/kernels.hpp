@@ -317,6 +317,12 @@ struct StepGeometry {
 constexpr int kK3sMaxBlk = 256;  // producer blocks per K3s workgroup (one lane each)
 int step_breakpoints(int shape);  // in-range expiries per node and kind at most: PR + 2
 StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk, int32_t blk_per_wg = 0);
+// The previous step's K3s (launch_step_pairs' arguments) with this step's delta form + K3p in one
+// launch (step.hip k3s_delta_pods)
+hipError_t launch_k3s_delta_pods(int64_t N_k3s, int64_t node_offset, int64_t P_k3s, long long* keys_k3s,
+                                 const StepTables& st, const StepGeometry& g, const int32_t* perm, const int64_t* pnow,
+                                 const int64_t* tile_mm, const int32_t* bnode, int64_t N, const HotDelta& d,
+                                 uint32_t* adj, const PodPrep& pods, hipStream_t s);
 // K3p: perm, pnow [ntiles * 1024], tile_mm [kTileStat * ntiles]; initialises keys[0..P) to -1
 hipError_t launch_step_pods(const int64_t* now, const uint8_t* flags, int64_t P, long long* keys, int64_t* batch,
                             int64_t* batch_next,

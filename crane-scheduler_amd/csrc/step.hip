@@ -35,6 +35,7 @@
 #include "dyn_types.hpp"
 #include "kernels.hpp"
 #include "pods.hpp"
+#include "lds_hash.hpp"
 #include "step_node.hpp"
 
 namespace crane {
@@ -180,11 +181,9 @@ __device__ __forceinline__ void tree_max(int32_t* tree, int32_t a, int32_t b, in
     }
 }
 
-__global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int32_t* __restrict__ perm,
-                                                        const int64_t* __restrict__ pnow,
-                                                        const int64_t* __restrict__ tile_mm, int64_t P,
-                                                        int64_t node_offset, int32_t R,
-                                                        long long* __restrict__ keys) {
+__device__ __forceinline__ void k3s_body(const int64_t b, const StepTables& st, const int32_t* __restrict__ perm,
+                                         const int64_t* __restrict__ pnow, const int64_t* __restrict__ tile_mm,
+                                         int64_t P, int64_t node_offset, int32_t R, long long* __restrict__ keys) {
     __shared__ int64_t tt[kK3sPods];         // the tile's pod times (sorted per kind)
     __shared__ int32_t tree[2 * kK3sPods];   // range maxima: node i covers its leaves' slots
     __shared__ int32_t umax[2];
@@ -198,7 +197,6 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
     // item -> its entry: the list's records and pieces expanded (one LDS read per item instead of a
     // binary search of the prefix, 8 dependent reads)
     __shared__ uint8_t imap[kK3sRecList + kK3sPieceList];
-    const int64_t b = blockIdx.x;
     CRANE_TSTAMP(st.trace, b, 0);
     const int32_t r = (int32_t)(b % R);
     const int64_t grp = b / R;
@@ -472,6 +470,45 @@ int step_breakpoints(int shape) {
     }
 }
 
+__global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int32_t* __restrict__ perm,
+                                                        const int64_t* __restrict__ pnow,
+                                                        const int64_t* __restrict__ tile_mm, int64_t P,
+                                                        int64_t node_offset, int32_t R,
+                                                        long long* __restrict__ keys) {
+    k3s_body((int64_t)blockIdx.x, st, perm, pnow, tile_mm, P, node_offset, R, keys);
+}
+
+// The previous step's K3s and this step's first launch (the delta form's K2 + K3p's pod tiles)
+// as one launch on an engine's dispatch queue (engine option step_defer, the group's slots): the
+// two are independent — K3s reads the previous step's tables and pod tiles, K3p writes this
+// step's (the engine alternates two sets), the delta form writes adjustments the previous K1 has
+// consumed — and a queue runs its kernels one after the other, so this takes one launch and
+// one kernel boundary out of each batch's chain.  Workgroups: K3s's first (its XCD placement
+// follows blockIdx), then the pod tiles, then the delta's.
+struct K3sArgs {
+    StepTables st;
+    const int32_t* perm;
+    const int64_t* pnow;
+    const int64_t* tile_mm;
+    int64_t P, node_offset;
+    int32_t R;
+    long long* keys;
+};
+static_assert(kK3sThreads == 512, "the fused launch's workgroups are the delta form's and K3p's 512 lanes");
+
+__global__ __launch_bounds__(kK3sThreads) void k3s_delta_pods(K3sArgs k, int32_t nk3s, const int32_t* __restrict__ bnode,
+                                                              int64_t N, HotDelta d, uint32_t* __restrict__ adj,
+                                                              PodPrep pp) {
+    const int64_t b = blockIdx.x;
+    if (b < nk3s) {
+        k3s_body(b, k.st, k.perm, k.pnow, k.tile_mm, k.P, k.node_offset, k.R, k.keys);
+        return;
+    }
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
+    if (b - nk3s < pp.ntiles) k3p_tile<kK3sThreads>(b - nk3s, pp, dyn_lds);
+    else k2_delta_body<kK3sThreads>((int32_t)(b - nk3s - pp.ntiles), bnode, N, d, adj);
+}
+
 StepGeometry step_geometry(int64_t P, int64_t N, int32_t nblk, int32_t blk_per_wg) {
     StepGeometry g{};
     g.nseg = (N + kStepSeg - 1) / kStepSeg;
@@ -521,6 +558,29 @@ hipError_t launch_step_nodes(int shape, const void* rec, int64_t N, double wsum,
         case kShape8x8: return launch_steps_t<8, 8>(rec, N, wsum, noprio, st, g, tile_mm, s);
         default: return launch_steps_t<16, 16>(rec, N, wsum, noprio, st, g, tile_mm, s);
     }
+}
+
+hipError_t launch_k3s_delta_pods(int64_t N_k3s, int64_t node_offset, int64_t P_k3s, long long* keys_k3s,
+                                 const StepTables& st, const StepGeometry& g, const int32_t* perm, const int64_t* pnow,
+                                 const int64_t* tile_mm, const int32_t* bnode, int64_t N, const HotDelta& d,
+                                 uint32_t* adj, const PodPrep& pods, hipStream_t s) {
+    if (P_k3s <= 0 || N_k3s <= 0 || d.n_win < 1 || d.n_win > kDeltaMaxWin || d.n_rng < 0 || d.n_rng > kMaxWin ||
+        N >= (1LL << 27))
+        return hipErrorInvalidValue;
+    const int64_t nk = g.ngroups * g.R;
+    const int64_t L = d.n_rng > 0 ? d.start[d.n_rng] : 0;
+    const int64_t grid = nk + (pods.P > 0 ? pods.ntiles : 0) + (L + kDeltaChunk - 1) / kDeltaChunk;
+    if (grid >= (1LL << 31) || nk >= (1LL << 31)) return hipErrorInvalidValue;
+    PodPrep pp{};
+    if (pods.P > 0) pp = pods;
+    const size_t lds = std::max(kK3pLds, sizeof(uint32_t) * 2 * (size_t)kDeltaSlots +
+                                             sizeof(uint16_t) * kDeltaMaxWin * kDeltaChunk);
+    static const hipError_t attr = hipFuncSetAttribute((const void*)k3s_delta_pods,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (attr != hipSuccess) return attr;
+    const K3sArgs k{st, perm, pnow, tile_mm, P_k3s, node_offset, g.R, keys_k3s};
+    return klaunch("k3s_eval+k2_delta+k3p_pods", k3s_delta_pods, dim3((unsigned)grid), dim3(kK3sThreads), lds, s, k,
+                   (int32_t)nk, bnode, N, d, adj, pp);
 }
 
 hipError_t launch_step_pairs(int shape, int64_t N, int64_t node_offset, int64_t P, long long* keys,

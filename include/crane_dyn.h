@@ -310,6 +310,8 @@ int crane_queue_destroy(crane_queue *q);
  * next state change, or be handed back first with crane_dyn_forget_queue. */
 int crane_dyn_step_keys_queue(crane_dyn *h, int64_t now_ns, int64_t hv_ts_ns, int64_t n_pods,
                               const int64_t *d_now_ns, const uint8_t *d_pod_flags, int64_t *d_keys, crane_queue *q);
+/* option step_defer: run the last step's deferred K3s now (on its queue; then wait for the queue) */
+int crane_dyn_step_flush(crane_dyn *h);
 /* Hand a queue back (waits for it): the engine no longer waits for it at its state changes. */
 int crane_dyn_forget_queue(crane_dyn *h, crane_queue *q);
 /* Asynchronous pieces of one scheduling step on `stream`:
@@ -345,6 +347,11 @@ const char *crane_dyn_version(void);
  *   "k2_sorted" 1 a time-ordered log (checked at upload): K2 reads the widest window's suffix only | 0 never
  *   "k2_delta" 1 ... and with k2_form 0, once anchored, only the bindings whose window rank changed since
  *     the anchor refresh (the anchor's dense counts + adjustments) | 0 every refresh re-counts the suffix
+ *   "step_defer" 0 | 1: a step on a dispatch queue (crane_dyn_step_keys_queue) leaves its last kernel
+ *     (K3s) to the engine's next step on that queue, which runs it inside its own first launch (one
+ *     launch and one kernel boundary fewer per step); its keys are final once that launch, or
+ *     crane_dyn_step_flush, or any other call on the engine, has run it and the queue completed it.
+ *     The group sets it on its slots' engines and flushes at crane_dyn_group_sync
  *   "k1_stream" 1 the streamed step pass without dedupe-form K2 entries | 0 the record-holding fused pass
  *   "k1_tail" 0 its tail on one wave when the grid has >= 4096 blocks | 1 always | 4 on all four waves
  *   "keys_path" 0 step path | 1 per-pair kernel   "greedy_form" 0 merge | 1 sequential
@@ -377,7 +384,10 @@ int64_t crane_dyn_debug_trace(crane_dyn *h, int32_t which, int64_t max, uint64_t
  * per-batch collective (step_keys_async / schedule with the collective on) | 0 the steps' kernels
  * launched through HIP on the slots' streams | 1 on dispatch queues (crane_queue, one per slot and
  * device; the batch form crane_dyn_group_step_keys_batch orders its collective after them);
- * "dispatch_ring" 0 | 1 their ring_kind; any other name goes to every engine.  Either way the batch's d_now / d_flags must be
+ * "dispatch_ring" 0 | 1 their ring_kind; "defer" 1 (default) | 0: engine option step_defer on the
+ * queues' engines (a slot's K3s runs in its next step's first launch; crane_dyn_group_sync runs the
+ * last ones — the caller alternates key buffers per slot, or the deferred K3s runs alone first);
+ * any other name goes to every engine.  Either way the batch's d_now / d_flags must be
  * complete on the devices when it is handed over (the group's streams and queues are its own). */
 typedef struct crane_dyn_group crane_dyn_group;
 /* Contiguous balanced node range of shard `shard` of n_shards (the first n % n_shards get one more). */

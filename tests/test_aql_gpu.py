@@ -190,3 +190,45 @@ def test_queue_runs_ahead_past_its_ring():
     for e in engs:
         e.close()
     q.close()
+
+
+@pytest.mark.parametrize("opts", [(), (("k2_form", 3),), (("k2_delta", 0),)], ids=["delta", "large", "dedupe"])
+def test_queue_deferred_k3s(opts):
+    """Engine option step_defer: a queue step leaves its K3s to the next step on the queue, which
+    runs it inside its first launch (with the delta form: k3s_delta_pods; any other first launch
+    runs it alone first).  Batches with their own key buffers, one that reuses the previous
+    batch's buffer (the deferred K3s runs alone before the new step's K3p resets the keys: the new
+    batch's keys must come out whole), a state change in between (the upload runs it first), and
+    the last one run by crane_dyn_step_flush: every batch's keys equal the same batch stepped on a
+    HIP stream."""
+    import torch
+    _, c, engs, dev = _setup(5000, 1500, 40000, 20250309, opts)
+    engs[1].set_option("step_defer", 1)
+    t0 = int(synth.NOW0_NS)
+    q = cd.Queue(0)
+    st = torch.cuda.Stream(dev)
+    P = len(c.now)
+    d_flags = torch.from_numpy(c.ds).to(dev)
+    times = [t0 + (k % 4) * 9_000_000_000 for k in range(9)]
+    d_now = [torch.from_numpy(c.now + (t - t0)).to(dev) for t in times]
+    kq = [torch.empty(P, dtype=torch.int64, device=dev) for _ in times]
+    kq[5] = kq[4]  # (batch 5 writes batch 4's buffer: batch 4's result is overwritten, batch 5's checked)
+    ref = []
+    torch.cuda.synchronize()
+    for b, t in enumerate(times):
+        ks = torch.empty(P, dtype=torch.int64, device=dev)
+        engs[0].step_keys_async(t, t, d_now[b], d_flags, ks, st.cuda_stream)
+        st.synchronize()
+        ref.append(ks)
+        if b == 7:  # a state change on the deferring engine between two steps
+            val, ts, _ = c.rows(engs[1].metric_names)
+            engs[1].upload_nodes(val, ts, c.hv, c.hv_ts)
+        engs[1].step_keys_queue(t, t, d_now[b], d_flags, kq[b], q)
+    engs[1].step_flush()
+    q.wait()
+    for b in range(len(times)):
+        if b != 4:
+            assert torch.equal(kq[b], ref[b]), f"batch {b}"
+    for e in engs:
+        e.close()
+    q.close()
