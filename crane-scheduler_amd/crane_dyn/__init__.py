@@ -565,7 +565,8 @@ class Engine:
 
     def step_keys_queue(self, now_ns, hv_ts_ns, d_now, d_flags, d_keys, queue):
         """step_keys_async with the kernels on a dispatch queue (Queue): the inputs must be complete
-        on the device (torch.cuda.synchronize() after writing them); keys after queue.wait()."""
+        on the device (torch.cuda.synchronize() after writing them); keys after queue.wait() (with
+        engine option step_defer: after the next step on the queue or step_flush(), then the wait)."""
         P = d_now.numel()
         assert d_keys.numel() == P and d_now.dtype.itemsize == 8 and d_keys.dtype.itemsize == 8
         self._check(lib.crane_dyn_step_keys_queue(self.h, int(now_ns), int(hv_ts_ns), P, C.c_void_p(d_now.data_ptr()),
