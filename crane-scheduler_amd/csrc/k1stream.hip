@@ -71,6 +71,12 @@ __device__ __forceinline__ int32_t score_at_lds(int64_t t, const NodeRec<PD, PR>
 #ifndef K1S_WAVES  // waves per SIMD the 4x6 form is built for (72 VGPRs: 7; 64: 8)
 #define K1S_WAVES 7
 #endif
+#ifndef K1S_KWARM  // the kernarg lines warmed in the scalar cache while the rows load (A/B: 0 off)
+#define K1S_KWARM 1
+#endif
+#ifndef K1S_FULL  // the instance for a policy of exactly 4 predicates / 6 priorities / 2 windows (A/B: 0 off)
+#define K1S_FULL 1
+#endif
 #ifndef K1S_SREC
 #define K1S_SREC 64
 #endif
@@ -185,11 +191,16 @@ __device__ __forceinline__ void tail(bool g1, Rec* lrec, Step1* s1l, Step1* srt,
     CRANE_TSTAMP(trace, blockIdx.x, 4);
 }
 
-template <int PD, int PR>
+// FULL: the policy has exactly PD predicates, PR priorities and kFullWin hot-value windows (the
+// reference's shipped policy at 4 x 6): every per-term loop is static, so the policy words load
+// together instead of one scalar load and wait per term under its own uniform branch
+constexpr int kFullWin = 2;
+template <int PD, int PR, bool FULL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PD * PR <= 24 ? K1S_WAVES : 1)))
 void k1_stream_steps(K1Args a, K1Step step) {
     using Rec = NodeRec<PD, PR>;
     constexpr int BS = 256;
+    const int npd = FULL ? PD : a.pol.npd, npr = FULL ? PR : a.pol.npr, nwin = FULL ? kFullWin : a.pol.n_win;
     // a staged stepped node's record: e_fail, pen, e_hv, e_prio, t (what the emit reads), and in
     // e_pred's first words its slots per kind (slot < 0: none), multi flags and the score at tmin
     __shared__ __attribute__((aligned(16))) Rec lrec[kSRec];
@@ -203,6 +214,8 @@ void k1_stream_steps(K1Args a, K1Step step) {
     const int64_t blk = xcd_block(blockIdx.x, gridDim.x), first = blk * BS, n = first + threadIdx.x;
     CRANE_TSTAMP(a.trace, blockIdx.x, 0);
     const int lo = (int)min((int64_t)threadIdx.x, N - 1 - first);  // lane offset, clamped
+    // the batch range K3p folded: loaded first, so waiting for it does not wait for the rows
+    const int64_t bt0 = step.batch[0], bt1 = step.batch[1];
     // ---- A: stream the rows (every load unconditional, clamped index: all in flight at once)
     int64_t pt[PD], qt[PR];
     double pv[PD], qv[PR];
@@ -219,13 +232,13 @@ void k1_stream_steps(K1Args a, K1Step step) {
     if (pol.n_slots > 0) {
 #pragma unroll
         for (int k = 0; k < PD; ++k) {
-            const int64_t row = k < pol.npd ? pol.pred_slot[k] : 0;
+            const int64_t row = k < npd ? pol.pred_slot[k] : 0;
             pt[k] = (a.ts + (row * N + first))[lo];
             pv[k] = (a.val + (row * N + first))[lo];
         }
 #pragma unroll
         for (int k = 0; k < PR; ++k) {
-            const int64_t row = k < pol.npr ? pol.prio_slot[k] : 0;
+            const int64_t row = k < npr ? pol.prio_slot[k] : 0;
             qt[k] = (a.ts + (row * N + first))[lo];
             qv[k] = (a.val + (row * N + first))[lo];
         }
@@ -239,8 +252,8 @@ void k1_stream_steps(K1Args a, K1Step step) {
         uint32_t bz[kMaxWin];
 #pragma unroll
         for (int b = 0; b < kMaxWin; ++b) {
-            bc[b] = b < pol.n_win ? (a.buckets + first)[(int64_t)b * N + lo] : 0u;
-            bz[b] = b < pol.n_win ? (base + first)[(int64_t)b * N + lo] : 0u;
+            bc[b] = b < nwin ? (a.buckets + first)[(int64_t)b * N + lo] : 0u;
+            bz[b] = b < nwin ? (base + first)[(int64_t)b * N + lo] : 0u;
         }
         if (a.bucket_base) {  // (rows past n_win read as 0)
 #pragma unroll
@@ -250,20 +263,24 @@ void k1_stream_steps(K1Args a, K1Step step) {
         hvl = a.hv[first + lo];
         hvt = a.hv_ts ? a.hv_ts[first + lo] : a.hv_ts_counts;
     }
+#if K1S_KWARM
+    kernarg_warm<(int)sizeof(K1Args) + (int)sizeof(K1Step)>();
+#endif
     // the batch range K3p folded, uniform: kept in SGPRs
-    const int64_t tmin = readfirstlane64(step.batch[0]), tmax = readfirstlane64(step.batch[1]);
+    const int64_t tmin = readfirstlane64(bt0), tmax = readfirstlane64(bt1);
     if (threadIdx.x < 4) ssh.lc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
     CRANE_TSTAMP(a.trace, blockIdx.x, 1);
     const bool valid = n < N;
     // isOverLoad per predicate (stats.go:94-112): the Filter rejects iff now < e_fail
     int64_t e_fail = kTsInvalid;
+    // (every policy word read unconditionally, the per-term conditions as selects: the scalar
+    // loads then issue together instead of one wait per term under its own branch)
 #pragma unroll
     for (int k = 0; k < PD; ++k) {
-        if (k < pol.npd) {
-            const double u = pv[k], lim = pol.pred_limit[k];
-            const bool over = pt[k] != kTsInvalid && !(u < 0.0) && lim != 0.0 && u > lim;
-            if (over) e_fail = max(e_fail, sat_add(pt[k], pol.pred_dur[k]));
-        }
+        const double u = pv[k], lim = pol.pred_limit[k];
+        const int64_t e = sat_add(pt[k], pol.pred_dur[k]);
+        const bool over = k < npd && pt[k] != kTsInvalid && !(u < 0.0) && lim != 0.0 && u > lim;
+        e_fail = over ? max(e_fail, e) : e_fail;
     }
     // hot value (getNodeHotValue / the binding-log counts) -> penalty and its expiry
     Rec hr;  // (only pen / e_hv are set and read)
@@ -271,9 +288,9 @@ void k1_stream_steps(K1Args a, K1Step step) {
         if (valid && !a.buckets_keep) {
 #pragma unroll
             for (int b = 0; b < kMaxWin; ++b)  // consumed: leaves the buckets zeroed for the next K2
-                if (b < pol.n_win) (a.buckets + first)[(int64_t)b * N + threadIdx.x] = 0;
+                if (b < nwin) (a.buckets + first)[(int64_t)b * N + threadIdx.x] = 0;
         }
-        rec_hot_counts<PD, PR>(pol, bc, N, n, valid ? a.cnt_out : nullptr, valid ? a.hvc_out : nullptr,
+        rec_hot_counts<PD, PR, FULL ? kFullWin : 0>(pol, bc, N, n, valid ? a.cnt_out : nullptr, valid ? a.hvc_out : nullptr,
                                a.hv_ts_counts, hr);
     } else if (a.hv) {
         rec_hot_annotation<PD, PR>(hvl, hvt, hr);
@@ -298,14 +315,13 @@ void k1_stream_steps(K1Args a, K1Step step) {
     double tp[PR];
 #pragma unroll
     for (int k = 0; k < PR; ++k) {
-        ep[k] = kTsInvalid;
-        tp[k] = 0.0;
-        if (k < pol.npr && qt[k] != kTsInvalid && !(qv[k] < 0.0)) {
-            ep[k] = sat_add(qt[k], pol.prio_dur[k]);
-            tp[k] = (1.0 - qv[k]) * pol.prio_w[k];  // getScore (stats.go:89), no FMA
-            tp[k] = tp[k] * 100.0;
-        }
-        if (tmin < ep[k]) s += tp[k];  // stats.go:124-133
+        const bool use = k < npr && qt[k] != kTsInvalid && !(qv[k] < 0.0);
+        double term = (1.0 - qv[k]) * pol.prio_w[k];  // getScore (stats.go:89), no FMA
+        term = term * 100.0;
+        const int64_t e = sat_add(qt[k], pol.prio_dur[k]);
+        ep[k] = use ? e : kTsInvalid;
+        tp[k] = use ? term : 0.0;
+        s = tmin < ep[k] ? s + tp[k] : s;  // stats.go:124-133
         add(ep[k], cnt1, mn1, mx1);
     }
     add(hr.e_hv, cnt1, mn1, mx1);
@@ -437,14 +453,15 @@ void k1_stream_steps(K1Args a, K1Step step) {
     tail<BS>(g1, lrec, s1l, srt, ssh, step, blk, a.trace);
 }
 
-template <int PD, int PR>
+template <int PD, int PR, bool FULL = false>
 static hipError_t launch_t(const K1Args& a, const K1Step& sa, hipStream_t st) {
     const unsigned grid = (unsigned)((a.N + 255) / 256);
-    return klaunch("k1_stream_steps", k1_stream_steps<PD, PR>, dim3(grid), dim3(256), 0, st, a, sa);
+    return klaunch("k1_stream_steps", k1_stream_steps<PD, PR, FULL>, dim3(grid), dim3(256), 0, st, a, sa);
 }
 
 hipError_t launch_stream_steps(int pd, int pr, const K1Args& a, const K1Step& sa, hipStream_t st) {
     if (a.N <= 0) return hipSuccess;
+    if (K1S_FULL && a.pol.npd == 4 && a.pol.npr == 6 && a.pol.n_win == kFullWin) return launch_t<4, 6, true>(a, sa, st);
     if (pd <= 4 && pr <= 6) return launch_t<4, 6>(a, sa, st);
     if (pd <= 8 && pr <= 8) return launch_t<8, 8>(a, sa, st);
     return launch_t<16, 16>(a, sa, st);

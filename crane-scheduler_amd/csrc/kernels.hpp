@@ -53,6 +53,21 @@ inline hipError_t klaunch(const char* name, void (*kernel)(KArgs...), dim3 grid,
         }                                                                                            \
     } while (0)
 
+// One scalar load per 64-byte line of the first BYTES of this launch's kernarg segment, all in
+// flight together and waited for once, so the launch's later argument reads (chains of scalar
+// load -> wait -> branch, the policy words under per-term conditions) hit the scalar cache instead
+// of each waiting for its own L2 round trip.  Called after a kernel's first vector loads are
+// issued, so the wait overlaps theirs.
+template <int BYTES>
+__device__ __forceinline__ void kernarg_warm() {
+    typedef const uint32_t __attribute__((address_space(4)))* kptr;
+    const kptr p = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < BYTES / 4; i += 16) x ^= p[i];
+    asm volatile("" ::"s"(x));
+}
+
 struct HotCutoffs {
     int32_t n_win;
     // 0: sorted[] are the ascending cutoffs now_unix - int64(timeRange.Seconds()) and a

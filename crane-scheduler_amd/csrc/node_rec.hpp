@@ -23,8 +23,8 @@ __device__ __forceinline__ int64_t go_int(double x) {
 
 __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {
     int64_t r;
-    if (__builtin_add_overflow(a, b, &r)) return b > 0 ? INT64_MAX : INT64_MIN;
-    return r;
+    const bool o = __builtin_add_overflow(a, b, &r);
+    return o ? (b > 0 ? INT64_MAX : INT64_MIN) : r;  // (selects: no branch around a caller's loads)
 }
 
 // Predicate and priority parts of the record from the metric rows the policy reads
@@ -76,7 +76,7 @@ __device__ __forceinline__ void rec_hot_annotation(double h, int64_t t, NodeRec<
 // (annotateNodeHotValue, node.go:113-121: value += count / p.Count, Go int division;
 // window w counts the bindings of buckets >= its cutoff rank): one running suffix sum.
 // cnt_out / hvc_out (null: not kept): the per-window counts and the value.
-template <int PD, int PR>
+template <int PD, int PR, int NW = 0>
 __device__ __forceinline__ void rec_hot_counts(const DevPolicy& pol, const uint32_t (&bc)[kMaxWin], int64_t N, int64_t n,
                                                uint32_t* __restrict__ cnt_out, double* __restrict__ hvc_out,
                                                int64_t hv_ts_counts, NodeRec<PD, PR>& r) {
@@ -84,14 +84,18 @@ __device__ __forceinline__ void rec_hot_counts(const DevPolicy& pol, const uint3
     uint64_t suf = 0;
 #pragma unroll
     for (int k = kMaxWin - 1; k >= 0; --k) {
-        if (k >= pol.n_win) continue;
-        suf += bc[k];
+        if (k >= (NW ? NW : pol.n_win)) continue;  // (NW: the policy's window count, static)
+        // (the rank's words read before any branch or store: one wait for the three)
         const int w = pol.win_of_rank[k];
+        const uint32_t dm = pol.win_div_m[k];
+        const int32_t dsh = pol.win_div_sh[k];
+        suf += bc[k];
+        const uint32_t q = div_magic((uint32_t)suf, dm, dsh);
         if (cnt_out) cnt_out[(int64_t)w * N + n] = (uint32_t)suf;
         // Go int division (truncates toward 0): exact multiply-high division when the
         // count fits 32 bits and hotValue.count is in [1, 2^32)
-        if (pol.win_div_m[k] != 0 && suf <= 0xFFFFFFFFull)
-            v += (int64_t)div_magic((uint32_t)suf, pol.win_div_m[k], pol.win_div_sh[k]);
+        if (dm != 0 && suf <= 0xFFFFFFFFull)
+            v += (int64_t)q;
         else
             v += (int64_t)suf / pol.win_count[w];
     }

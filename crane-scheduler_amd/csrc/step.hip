@@ -38,6 +38,10 @@
 #include "lds_hash.hpp"
 #include "step_node.hpp"
 
+#ifndef K3_KWARM  // the launch's kernarg lines warmed in the scalar cache first (A/B: 0 off)
+#define K3_KWARM 1
+#endif
+
 namespace crane {
 
 // ---------------------------------------------------------------- K3p
@@ -475,6 +479,9 @@ __global__ __launch_bounds__(kK3sThreads) void k3s_eval(StepTables st, const int
                                                         const int64_t* __restrict__ tile_mm, int64_t P,
                                                         int64_t node_offset, int32_t R,
                                                         long long* __restrict__ keys) {
+#if K3_KWARM
+    kernarg_warm<(int)sizeof(StepTables) + 64>();
+#endif
     k3s_body((int64_t)blockIdx.x, st, perm, pnow, tile_mm, P, node_offset, R, keys);
 }
 
@@ -499,6 +506,9 @@ static_assert(kK3sThreads == 512, "the fused launch's workgroups are the delta f
 __global__ __launch_bounds__(kK3sThreads) void k3s_delta_pods(K3sArgs k, int32_t nk3s, const int32_t* __restrict__ bnode,
                                                               int64_t N, HotDelta d, uint32_t* __restrict__ adj,
                                                               PodPrep pp) {
+#if K3_KWARM
+    kernarg_warm<(int)(sizeof(K3sArgs) + 32 + sizeof(HotDelta) + 8 + sizeof(PodPrep))>();
+#endif
     const int64_t b = blockIdx.x;
     if (b < nk3s) {
         k3s_body(b, k.st, k.perm, k.pnow, k.tile_mm, k.P, k.node_offset, k.R, k.keys);
