@@ -77,6 +77,9 @@ __device__ __forceinline__ int32_t score_at_lds(int64_t t, const NodeRec<PD, PR>
 #ifndef K1S_FULL  // the instance for a policy of exactly 4 predicates / 6 priorities / 2 windows (A/B: 0 off)
 #define K1S_FULL 1
 #endif
+#ifndef K1S_EMIT_SCORE  // the emit's score from the candidates in registers, terms loaded together (A/B: 0 off)
+#define K1S_EMIT_SCORE 1
+#endif
 #ifndef K1S_SREC
 #define K1S_SREC 64
 #endif
@@ -123,8 +126,19 @@ __device__ __forceinline__ void emit_task(const NodeRec<PD, PR>& r, int64_t n, i
         }
     }
     const int rk1 = rk0 - (fb ? 1 : 0);
-    // one score per instant serves both kinds (the Filter only gates kind 0's key)
+    // one score per instant serves both kinds (the Filter only gates kind 0's key): score_at with
+    // the expiries already in c[] and the terms read side by side (one LDS wait, not one per term)
+#if K1S_EMIT_SCORE
+    double tk[PR];
+#pragma unroll
+    for (int k = 0; k < PR; ++k) tk[k] = r.t[k];
+    double ssum = 0.0;
+#pragma unroll
+    for (int k = 0; k < PR; ++k) ssum = cq < c[k] ? ssum + tk[k] : ssum;  // stats.go:124-133, policy order
+    const int64_t pk = pack_key(score_of_sum(ssum, cq < c[PR] ? r.pen : 0, wsum, noprio, winv), n);
+#else
     const int64_t pk = pack_key(score_at_lds<PD, PR>(cq, r, wsum, noprio, winv), n);
+#endif
     // the score at tmin: phase A's, kept in the record's slot words (dw[5])
     const int64_t pk0 = pack_key(dw[5], n);
 #pragma unroll
@@ -229,7 +243,7 @@ void k1_stream_steps(K1Args a, K1Step step) {
         qt[k] = kTsInvalid;
         qv[k] = 0.0;
     }
-    if (pol.n_slots > 0) {
+    if (FULL || pol.n_slots > 0) {  // (FULL: the policy reads metrics)
 #pragma unroll
         for (int k = 0; k < PD; ++k) {
             const int64_t row = k < npd ? pol.pred_slot[k] : 0;
