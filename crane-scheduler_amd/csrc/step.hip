@@ -205,11 +205,10 @@ __device__ __forceinline__ void k3s_body(const int64_t b, const StepTables& st, 
     const int32_t r = (int32_t)(b % R);
     const int64_t grp = b / R;
     const int lane = threadIdx.x & 63;
-    // the tile's kinds: time range and slot range (K3p)
+    // the tile's kinds: time range and slot range (K3p's tile stats): one vector load, lane k
+    // stat k, issued after this slice's and the pods' loads and broadcast once they are in (as
+    // scalar loads they missed the scalar cache, and any scalar load's wait waits for all of them)
     const int64_t* ts = tile_mm + kTileStat * grp;
-    const int64_t tlo[2] = {ts[0], ts[2]}, thi[2] = {ts[1], ts[3]};
-    const int32_t cn = (int32_t)ts[4], cd = (int32_t)ts[5];
-    const int32_t klo[2] = {0, cn}, khi[2] = {cn, cn + cd};
     // the slice's producer blocks: with R a multiple of 8, workgroup label g = r % 8 (= its
     // XCD group, blockIdx % 8) takes the blocks the node pass ran in the same group — its
     // workgroup w built block xcd_block(w) (step_node.hpp), the contiguous run of XCD w % 8 —
@@ -238,7 +237,6 @@ __device__ __forceinline__ void k3s_body(const int64_t b, const StepTables& st, 
     const int lead = lane - sub;  // the block's leader lane (same wave)
     // the block's team: counts (one broadcast load), the searches; the leader adds the
     // flat maxima and the prefix / suffix maxima to the uniform keys
-    const bool any[2] = {cn > 0, cd > 0};
     // this slice's loads first (counts, the tile rows), then the pods, so they overlap
     int4 c = make_int4(0, 0, 0, 0);  // [records kind 0, pieces 0, records 1, pieces 1]
     int4 row = make_int4(-1, -1, 0, 0);
@@ -250,18 +248,37 @@ __device__ __forceinline__ void k3s_body(const int64_t b, const StepTables& st, 
     }
     bool live[kK3sPPL], ds[kK3sPPL];
     int32_t pod[kK3sPPL];
+    // every pod load issued before the first LDS store waits for one (unconditional, clamped
+    // slot): a conditional load per pod made each store wait for its own round trip
+    int32_t praw[kK3sPPL];
+    int64_t pn[kK3sPPL];
 #pragma unroll
     for (int u = 0; u < kK3sPPL; ++u) {
-        const int32_t i = u * kK3sThreads + threadIdx.x;
-        const int64_t slot = grp * kK3sPods + i;
+        const int64_t slot = grp * kK3sPods + u * kK3sThreads + threadIdx.x;
         live[u] = slot < P;
-        const int32_t praw = live[u] ? perm[slot] : 0;
-        tt[i] = live[u] ? pnow[slot] : INT64_MAX;
-        ds[u] = praw < 0;
-        pod[u] = praw & 0x7FFFFFFF;
+        const int64_t sc = live[u] ? slot : 0;
+        praw[u] = perm[sc];
+        pn[u] = pnow[sc];
     }
+#pragma unroll
+    for (int u = 0; u < kK3sPPL; ++u) {
+        tt[u * kK3sThreads + threadIdx.x] = live[u] ? pn[u] : INT64_MAX;
+        const int32_t pr = live[u] ? praw[u] : 0;
+        ds[u] = pr < 0;
+        pod[u] = pr & 0x7FFFFFFF;
+    }
+    const int64_t tsv = ts[lane < kTileStat ? lane : 0];
     for (int i = threadIdx.x; i < 2 * kK3sPods; i += kK3sThreads) tree[i] = -1;
     if (threadIdx.x < 2) umax[threadIdx.x] = -1;
+    auto stat = [&](int k) {
+        const uint32_t lo32 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)tsv, k);
+        const uint32_t hi32 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)tsv >> 32), k);
+        return (int64_t)(((uint64_t)hi32 << 32) | lo32);
+    };
+    const int64_t tlo[2] = {stat(0), stat(2)}, thi[2] = {stat(1), stat(3)};
+    const int32_t cn = (int32_t)stat(4), cd = (int32_t)stat(5);
+    const int32_t klo[2] = {0, cn}, khi[2] = {cn, cn + cd};
+    const bool any[2] = {cn > 0, cd > 0};
     CRANE_TSTAMP(st.trace, b, 5);  // (pods in: the LDS stores waited for them)
     const int32_t n1[2] = {any[0] ? c.x : 0, any[1] ? c.z : 0};
     // middle pieces [pl, pl + nm) per kind: with piece ranges, those overlapping the tile (the
