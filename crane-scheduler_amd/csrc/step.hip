@@ -38,6 +38,9 @@
 #include "lds_hash.hpp"
 #include "step_node.hpp"
 
+#ifndef K3S_BUCKETS  // slot searches through a per-kind time-bucket table (A/B: 0 plain binary search)
+#define K3S_BUCKETS 1
+#endif
 #ifndef K3_KWARM  // the launch's kernarg lines warmed in the scalar cache first (A/B: 0 off)
 #define K3_KWARM 1
 #endif
@@ -126,6 +129,7 @@ constexpr int kK3sBlkPerWg = 64;  // (round 6, 8-wave K3s: 32 per workgroup with
 // 0.122 -> 0.118 ms, 28.7 -> 24.8 us; every record and piece listed (and 4x the LDS):
 // 0.0362, 0.270 ms, 52 us (tools/gpu_lib_ab.sh)
 constexpr int kK3sListBlk = 64;
+constexpr int kSearchBucketBits = 8, kSearchBuckets = 1 << kSearchBucketBits;  // K3S_BUCKETS: per kind
 constexpr int kK3sRecList = 512;
 constexpr int kK3sPieceList = 512;
 static_assert(kK3sMaxBlk <= kK3sThreads, "at least one lane per producer block");
@@ -201,6 +205,11 @@ __device__ __forceinline__ void k3s_body(const int64_t b, const StepTables& st, 
     // item -> its entry: the list's records and pieces expanded (one LDS read per item instead of a
     // binary search of the prefix, 8 dependent reads)
     __shared__ uint8_t imap[kK3sRecList + kK3sPieceList];
+#if K3S_BUCKETS
+    // per kind, the first slot of each time bucket (bucket k: [lo + k 2^sh, lo + (k + 1) 2^sh)): a
+    // slot search reads its bucket's two bounds and searches the few slots between them
+    __shared__ int32_t sfirst[2][kSearchBuckets + 1];
+#endif
     CRANE_TSTAMP(st.trace, b, 0);
     const int32_t r = (int32_t)(b % R);
     const int64_t grp = b / R;
@@ -279,6 +288,25 @@ __device__ __forceinline__ void k3s_body(const int64_t b, const StepTables& st, 
     const int32_t cn = (int32_t)stat(4), cd = (int32_t)stat(5);
     const int32_t klo[2] = {0, cn}, khi[2] = {cn, cn + cd};
     const bool any[2] = {cn > 0, cd > 0};
+#if K3S_BUCKETS
+    int32_t sbs[2];  // bucket width 2^sbs per kind: the kind's time span in kSearchBuckets buckets
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+        const uint64_t span = klo[T] < khi[T] ? (uint64_t)(thi[T] - tlo[T]) : 0ull;
+        const int bits = span ? 64 - __builtin_clzll(span) : 0;
+        sbs[T] = bits > kSearchBucketBits ? bits - kSearchBucketBits : 0;
+    }
+    // first slot of kind T with tt >= x (slot_lower over [klo, khi)): its bucket's bounds, then
+    // a binary search of the slots between them
+    auto find = [&](int T, int64_t x) -> int32_t {
+        if (klo[T] >= khi[T] || x <= tlo[T]) return klo[T];
+        if (x > thi[T]) return khi[T];
+        const int32_t k = (int32_t)((uint64_t)(x - tlo[T]) >> sbs[T]);
+        return slot_lower(tt, sfirst[T][k], sfirst[T][k + 1], x);
+    };
+#else
+    auto find = [&](int T, int64_t x) -> int32_t { return slot_lower(tt, klo[T], khi[T], x); };
+#endif
     CRANE_TSTAMP(st.trace, b, 5);  // (pods in: the LDS stores waited for them)
     const int32_t n1[2] = {any[0] ? c.x : 0, any[1] ? c.z : 0};
     // middle pieces [pl, pl + nm) per kind: with piece ranges, those overlapping the tile (the
@@ -332,6 +360,18 @@ __device__ __forceinline__ void k3s_body(const int64_t b, const StepTables& st, 
     __syncthreads();  // tt, tree, umax initialised; the counts in
     CRANE_TSTAMP(st.trace, b, 1);
     const int32_t E = 4 * m;
+    // the bucket table (K3S_BUCKETS): lane (T, k) searches bucket k's first slot of kind T, all at
+    // once (one search's time, wave 0 after its prefix), ordered by the next barrier
+    auto bucket_table = [&]() {
+#if K3S_BUCKETS
+        static_assert(kK3sThreads == 2 * kSearchBuckets, "a lane per (kind, bucket)");
+        const int T = threadIdx.x / kSearchBuckets, k = threadIdx.x % kSearchBuckets;
+        if (klo[T] < khi[T]) {
+            sfirst[T][k] = slot_lower(tt, klo[T], khi[T], tlo[T] + ((int64_t)k << sbs[T]));
+            if (k == 0) sfirst[T][kSearchBuckets] = khi[T];
+        }
+#endif
+    };
     int32_t nrec = 0, total = 0;
     if (lists) {
         if (threadIdx.x < 64) {  // wave 0: exclusive prefix over the entries, in place (wpre[E] = total)
@@ -348,9 +388,13 @@ __device__ __forceinline__ void k3s_body(const int64_t b, const StepTables& st, 
             }
             if (lane == 0) wpre[E] = carry;
         }
+        bucket_table();
         __syncthreads();
         nrec = wpre[2 * m];
         total = wpre[E];
+    } else if (K3S_BUCKETS) {
+        bucket_table();
+        __syncthreads();
     }
     const bool piece_list = lists && total - nrec <= kK3sPieceList;
     const bool rec_list = lists && nrec <= kK3sRecList;
@@ -390,7 +434,7 @@ __device__ __forceinline__ void k3s_body(const int64_t b, const StepTables& st, 
             const int T = (rec ? e : e - 2 * m) & 1;
             if (rec) {
                 // a one-step record stepping inside (lo, hi]: split the kind's slots
-                const int32_t sp = slot_lower(tt, klo[T], khi[T], r1[u].bp);
+                const int32_t sp = find(T, r1[u].bp);
                 if (r1[u].k0 >= 0) tree_max(tree, klo[T], sp, r1[u].k0);
                 if (r1[u].k1 >= 0) tree_max(tree, sp, khi[T], r1[u].k1);
                 upd = true;
@@ -400,7 +444,7 @@ __device__ __forceinline__ void k3s_body(const int64_t b, const StepTables& st, 
                 const Mid& q = pm[u];
                 if (q.s <= tlo[T] && q.e > thi[T]) um[T] = max(um[T], q.key);
                 else if (q.s <= thi[T] && q.e > tlo[T]) {
-                    tree_max(tree, slot_lower(tt, klo[T], khi[T], q.s), slot_lower(tt, klo[T], khi[T], q.e), q.key);
+                    tree_max(tree, find(T, q.s), find(T, q.e), q.key);
                     upd = true;
                 }
             }
@@ -412,7 +456,7 @@ __device__ __forceinline__ void k3s_body(const int64_t b, const StepTables& st, 
             // many records: by the block's team (consecutive records, a lane each)
             for (int32_t i = jj[2 * T] + sub; i < jj[2 * T + 1]; i += lpb) {
                 const Step1 q = base[T][i];
-                const int32_t sp = slot_lower(tt, klo[T], khi[T], q.bp);
+                const int32_t sp = find(T, q.bp);
                 if (q.k0 >= 0) tree_max(tree, klo[T], sp, q.k0);
                 if (q.k1 >= 0) tree_max(tree, sp, khi[T], q.k1);
                 upd = true;
@@ -437,8 +481,7 @@ __device__ __forceinline__ void k3s_body(const int64_t b, const StepTables& st, 
                     const Mid& pm = q[v];
                     if (pm.s <= tlo[T] && pm.e > thi[T]) um[T] = max(um[T], pm.key);
                     else if (pm.s <= thi[T] && pm.e > tlo[T]) {
-                        tree_max(tree, slot_lower(tt, klo[T], khi[T], pm.s), slot_lower(tt, klo[T], khi[T], pm.e),
-                                 pm.key);
+                        tree_max(tree, find(T, pm.s), find(T, pm.e), pm.key);
                         upd = true;
                     }
                 }
