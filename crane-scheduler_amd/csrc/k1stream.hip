@@ -80,6 +80,9 @@ __device__ __forceinline__ int32_t score_at_lds(int64_t t, const NodeRec<PD, PR>
 #ifndef K1S_EMIT_SCORE  // the emit's score from the candidates in registers, terms loaded together (A/B: 0 off)
 #define K1S_EMIT_SCORE 1
 #endif
+#ifndef K1S_PUB1  // step_publish folded into the slots' exchange (one barrier; A/B: 0 its own barrier)
+#define K1S_PUB1 1
+#endif
 #ifndef K1S_SREC
 #define K1S_SREC 64
 #endif
@@ -355,6 +358,14 @@ void k1_stream_steps(K1Args a, K1Step step) {
     const uint32_t w1 = (cnt1 ? (multi1 ? 2u : 1u) : 0u) | (multi1 ? (uint32_t)(cnt1 - 1) << 16 : 0u);
     const uint32_t w2 = (cnt0 | cnt1) ? 1u : 0u;
     uint32_t e0 = wave_scan_add(w0), e1 = wave_scan_add(w1), e2 = wave_scan_add(w2);
+#if K1S_PUB1
+    // the flat maxima per wave go out with the totals (step_publish's exchange: one barrier for both)
+    const int32_t fm0 = wave_max(so.flat0), fm1 = wave_max(so.flat1);
+    if (lane == 0) {
+        ssh.fm[0][wv] = fm0;
+        ssh.fm[1][wv] = fm1;
+    }
+#endif
     if (lane == 63) {
         xch[0][wv] = e0;
         xch[1][wv] = e1;
@@ -383,10 +394,23 @@ void k1_stream_steps(K1Args a, K1Step step) {
         ssh.lc[1][0] = (int32_t)(tot[1] & 0xFFFF);
         ssh.lc[1][1] = (int32_t)(tot[1] >> 16);
     }
+#if K1S_PUB1
+    // step_publish's stores from the exchanged values (ssh.lc is read after the next barrier)
+    if (threadIdx.x < 2) {
+        const int T = threadIdx.x;
+        step.st.flat[blk * 2 + T] = max(max(ssh.fm[T][0], ssh.fm[T][1]), max(ssh.fm[T][2], ssh.fm[T][3]));
+    } else if (threadIdx.x < 6) {
+        const int L = threadIdx.x - 2;  // kind L >> 1: one-step records (L & 1 = 0) / middle pieces
+        step.st.cnt[blk * 4 + L] = (int32_t)((L & 1) ? tot[L >> 1] >> 16 : tot[L >> 1] & 0xFFFF);
+    }
+    const bool g1 = (int32_t)max(tot[0] & 0xFFFF, tot[1] & 0xFFFF) > min(kSCap, step.st.lds_cap);
+    CRANE_TSTAMP(a.trace, blockIdx.x, 3);
+#else
     step_publish<BS>(so, ssh, step.st, blk);  // flat maxima, counts (its barrier: ssh.lc final)
     CRANE_TSTAMP(a.trace, blockIdx.x, 3);
     // one-step records staged in LDS, or (more of a kind than it holds) in st.stage
     const bool g1 = max(ssh.lc[0][0], ssh.lc[1][0]) > min(kSCap, step.st.lds_cap);
+#endif
     const S1Out s1o{s1l, step.st.stage + blk * 2 * step.st.bs, g1, (int64_t)kSCap, step.st.s1pad};
     // ---- C: the stepped nodes' records in LDS, chunk by chunk, and their (node, kind) items.
     // The first kSRec stepped nodes write their part (e_fail, pen, e_hv, slots) into the LDS
